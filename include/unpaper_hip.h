@@ -1,0 +1,421 @@
+/*
+ * unpaper_hip.h — C ABI of the MI355X-native (gfx950) page-cleanup backend.
+ *
+ * This header is the drop-in boundary: it is what a `backend_hip.c` inside the
+ * reference tree binds.  Every declaration cites the
+ * reference interface it replaces (paths relative to ErrorTzy/unpaper-gpu).
+ *
+ *  - value types           <- imageprocess/primitives.h:13-108, masks.h:14-101,
+ *                             filters.h:12-70, deskew.h:13-20, interpolate.h:10-15
+ *  - UphipImage            <- imageprocess/image.h:11-15 (Image{AVFrame*,...});
+ *                             the device copy that the reference hangs off
+ *                             AVFrame.opaque_ref (backend_cuda_internal.h:18-27)
+ *                             is the UphipFrame itself here.
+ *  - UphipBackend / ops    <- imageprocess/backend.h:19-57 (ImageBackend vtable)
+ *  - uphip_try_init        <- imageprocess/cuda_runtime.h (unpaper_cuda_try_init)
+ *  - stream pool / TLS     <- imageprocess/cuda_stream_pool.h, cuda_runtime.c:70
+ *  - UphipOptions          <- lib/options.h:32-127 (Options) + SheetProcessConfig
+ *                             (sheet_process.h:22-37)
+ *  - uphip_batch_*         <- sheet_process.c:134 process_sheet driven by
+ *                             lib/batch_worker.c:79 batch_process_job
+ *
+ * No torch or HIP types appear in any signature: plain pointers, sizes, PODs.
+ * All structs are layout-identical to their reference counterparts (checked by
+ * static asserts in INTEGRATION.md's adapter) so the adapter can cast.
+ */
+#ifndef UNPAPER_HIP_H
+#define UNPAPER_HIP_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UPHIP_ABI_VERSION 1
+
+/* constants.h:8-12 */
+#define UPHIP_MAX_MASKS 100
+#define UPHIP_MAX_POINTS 100
+#define UPHIP_MAX_PAGES 2
+
+/* ---------------------------------------------------------------------------
+ * Value types — imageprocess/primitives.h:13-108
+ * ------------------------------------------------------------------------- */
+typedef struct { int32_t x, y; } UphipPoint;                  /* primitives.h:13-16 */
+typedef struct { int32_t horizontal, vertical; } UphipDelta;  /* primitives.h:23-26 */
+typedef struct { bool horizontal, vertical; } UphipDirection; /* primitives.h:40-43 */
+typedef struct { bool left, top, right, bottom; } UphipEdges; /* primitives.h:54-59 */
+typedef struct { uint8_t r, g, b; } UphipPixel;               /* primitives.h:61-65 */
+typedef struct { UphipPoint vertex[2]; } UphipRectangle;      /* primitives.h:72-74, inclusive */
+typedef struct { int32_t width, height; } UphipRectangleSize; /* primitives.h:76-79 */
+
+/* masks.h:84-89 */
+typedef struct { int32_t left, top, right, bottom; } UphipBorder;
+
+/* masks.h:65-70 (MAX_WIPES == MAX_MASKS) */
+typedef struct {
+  size_t count;
+  UphipRectangle areas[UPHIP_MAX_MASKS];
+} UphipWipes;
+
+/* interpolate.h:10-15 */
+typedef enum {
+  UPHIP_INTERP_NN = 0,
+  UPHIP_INTERP_LINEAR = 1,
+  UPHIP_INTERP_CUBIC = 2,
+} UphipInterpolation;
+
+/* blit.h:25-27 */
+typedef int8_t UphipRotationDirection;
+#define UPHIP_ROTATE_CLOCKWISE ((UphipRotationDirection)1)
+#define UPHIP_ROTATE_ANTICLOCKWISE ((UphipRotationDirection)-1)
+
+/* constants.h:18-23 */
+typedef enum {
+  UPHIP_LAYOUT_NONE = 0,
+  UPHIP_LAYOUT_SINGLE = 1,
+  UPHIP_LAYOUT_DOUBLE = 2,
+} UphipLayout;
+
+/* Pixel formats the reference accepts natively (sheet_stages.c:75-92,
+ * cuda_kernels_format.h:27-34). Values are ours, not FFmpeg's. */
+typedef enum {
+  UPHIP_FMT_NONE = -1,
+  UPHIP_FMT_GRAY8 = 0,
+  UPHIP_FMT_Y400A = 1,
+  UPHIP_FMT_RGB24 = 2,
+  UPHIP_FMT_MONOWHITE = 3,
+  UPHIP_FMT_MONOBLACK = 4,
+} UphipPixelFormat;
+
+/* filters.h:12-31 — exclusions are an inline array here (the reference keeps a
+ * caller-owned Rectangle* next to a count). */
+typedef struct {
+  UphipRectangleSize scan_size;
+  UphipDelta scan_step;
+  struct { uint32_t horizontal, vertical; } scan_depth;
+  UphipDirection scan_direction;
+  uint8_t abs_threshold;
+  int32_t intensity;
+  size_t exclusions_count;
+  UphipRectangle exclusions[UPHIP_MAX_MASKS];
+} UphipBlackfilterParameters;
+
+/* filters.h:43-49 */
+typedef struct {
+  UphipRectangleSize scan_size;
+  UphipDelta scan_step;
+  float intensity;
+} UphipBlurfilterParameters;
+
+/* filters.h:59-65 */
+typedef struct {
+  UphipRectangleSize scan_size;
+  UphipDelta scan_step;
+  uint8_t abs_threshold;
+} UphipGrayfilterParameters;
+
+/* masks.h:14-37 */
+typedef struct {
+  UphipRectangleSize scan_size;
+  UphipDelta scan_step;
+  struct { int32_t horizontal, vertical; } scan_depth;
+  UphipDirection scan_direction;
+  struct { float horizontal, vertical; } scan_threshold;
+  int32_t minimum_width;
+  int32_t maximum_width;
+  int32_t minimum_height;
+  int32_t maximum_height;
+} UphipMaskDetectionParameters;
+
+/* masks.h:53-56 */
+typedef struct {
+  UphipEdges alignment;
+  UphipDelta margin;
+} UphipMaskAlignmentParameters;
+
+/* masks.h:90-100 */
+typedef struct {
+  UphipRectangleSize scan_size;
+  UphipDelta scan_step;
+  struct { int32_t horizontal, vertical; } scan_threshold;
+  UphipDirection scan_direction;
+} UphipBorderScanParameters;
+
+/* deskew.h:13-20 (radians) */
+typedef struct {
+  float deskewScanRangeRad;
+  float deskewScanStepRad;
+  float deskewScanDeviationRad;
+  int deskewScanSize;
+  float deskewScanDepth;
+  UphipEdges scan_edges;
+} UphipDeskewParameters;
+
+/* ---------------------------------------------------------------------------
+ * Device frames and images — imageprocess/image.h:11-38
+ * ------------------------------------------------------------------------- */
+typedef struct UphipFrame UphipFrame; /* device-resident AVFrame peer */
+
+typedef struct {
+  UphipFrame *frame;
+  UphipPixel background;
+  uint8_t abs_black_threshold;
+} UphipImage;
+
+/* create_image (image.c:19-44): allocate on the current device; rows are
+ * pitched for coalesced access; `fill` wipes with `background`. */
+UphipImage uphip_create_image(UphipRectangleSize size, UphipPixelFormat format,
+                              bool fill, UphipPixel background,
+                              uint8_t abs_black_threshold);
+/* free_image (image.c:51-54) */
+void uphip_free_image(UphipImage *image);
+/* replace_image (image.c:46-50) */
+void uphip_replace_image(UphipImage *image, UphipImage *new_image);
+/* create_compatible_image (image.c:56-59) */
+UphipImage uphip_create_compatible_image(UphipImage source,
+                                         UphipRectangleSize size, bool fill);
+/* size_of_image (image.c:61-66) */
+UphipRectangleSize uphip_size_of_image(UphipImage image);
+UphipPixelFormat uphip_image_format(UphipImage image);
+/* image_ensure_cuda / image_ensure_cpu (image.h:32-38, image_cuda.c:135-269):
+ * explicit H2D / D2H of the frame contents.  `linesize` is the host row stride
+ * in bytes (>= bytes per row of `format`).  Synchronous w.r.t. the host. */
+int uphip_image_upload(UphipImage image, const void *host, int64_t linesize);
+int uphip_image_download(UphipImage image, void *host, int64_t linesize);
+/* Device pointer + pitch of a frame (image_get_gpu_ptr / _pitch, image.h:52-58). */
+void *uphip_image_device_ptr(UphipImage image);
+int64_t uphip_image_device_pitch(UphipImage image);
+
+/* ---------------------------------------------------------------------------
+ * ImageBackend ops — imageprocess/backend.h:22-56, same argument meaning.
+ * ------------------------------------------------------------------------- */
+void uphip_wipe_rectangle(UphipImage image, UphipRectangle input_area,
+                          UphipPixel color);
+void uphip_copy_rectangle(UphipImage source, UphipImage target,
+                          UphipRectangle source_area, UphipPoint target_coords);
+void uphip_center_image(UphipImage source, UphipImage target,
+                        UphipPoint target_origin, UphipRectangleSize target_size);
+void uphip_stretch_and_replace(UphipImage *pImage, UphipRectangleSize size,
+                               UphipInterpolation interpolate_type);
+void uphip_resize_and_replace(UphipImage *pImage, UphipRectangleSize size,
+                              UphipInterpolation interpolate_type);
+void uphip_flip_rotate_90(UphipImage *pImage, UphipRotationDirection direction);
+void uphip_mirror(UphipImage image, UphipDirection direction);
+void uphip_shift_image(UphipImage *pImage, UphipDelta d);
+void uphip_apply_masks(UphipImage image, const UphipRectangle masks[],
+                       size_t masks_count, UphipPixel color);
+void uphip_apply_wipes(UphipImage image, UphipWipes wipes, UphipPixel color);
+void uphip_apply_border(UphipImage image, const UphipBorder border,
+                        UphipPixel color);
+size_t uphip_detect_masks(UphipImage image, UphipMaskDetectionParameters params,
+                          const UphipPoint points[], size_t points_count,
+                          UphipRectangle masks[]);
+void uphip_align_mask(UphipImage image, const UphipRectangle inside_area,
+                      const UphipRectangle outside,
+                      UphipMaskAlignmentParameters params);
+UphipBorder uphip_detect_border(UphipImage image, UphipBorderScanParameters params,
+                                const UphipRectangle outside_mask);
+void uphip_blackfilter(UphipImage image, UphipBlackfilterParameters params);
+void uphip_blurfilter(UphipImage image, UphipBlurfilterParameters params,
+                      uint8_t abs_white_threshold);
+void uphip_noisefilter(UphipImage image, uint64_t intensity,
+                       uint8_t min_white_level);
+void uphip_grayfilter(UphipImage image, UphipGrayfilterParameters params);
+float uphip_detect_rotation(UphipImage image, UphipRectangle mask,
+                            const UphipDeskewParameters params);
+void uphip_deskew(UphipImage source, UphipRectangle mask, float radians,
+                  UphipInterpolation interpolate_type);
+
+/* The vtable itself, field-for-field ImageBackend (backend.h:19-57). */
+typedef struct {
+  const char *name;
+  void (*wipe_rectangle)(UphipImage, UphipRectangle, UphipPixel);
+  void (*copy_rectangle)(UphipImage, UphipImage, UphipRectangle, UphipPoint);
+  void (*center_image)(UphipImage, UphipImage, UphipPoint, UphipRectangleSize);
+  void (*stretch_and_replace)(UphipImage *, UphipRectangleSize, UphipInterpolation);
+  void (*resize_and_replace)(UphipImage *, UphipRectangleSize, UphipInterpolation);
+  void (*flip_rotate_90)(UphipImage *, UphipRotationDirection);
+  void (*mirror)(UphipImage, UphipDirection);
+  void (*shift_image)(UphipImage *, UphipDelta);
+  void (*apply_masks)(UphipImage, const UphipRectangle[], size_t, UphipPixel);
+  void (*apply_wipes)(UphipImage, UphipWipes, UphipPixel);
+  void (*apply_border)(UphipImage, const UphipBorder, UphipPixel);
+  size_t (*detect_masks)(UphipImage, UphipMaskDetectionParameters,
+                         const UphipPoint[], size_t, UphipRectangle[]);
+  void (*align_mask)(UphipImage, const UphipRectangle, const UphipRectangle,
+                     UphipMaskAlignmentParameters);
+  UphipBorder (*detect_border)(UphipImage, UphipBorderScanParameters,
+                               const UphipRectangle);
+  void (*blackfilter)(UphipImage, UphipBlackfilterParameters);
+  void (*blurfilter)(UphipImage, UphipBlurfilterParameters, uint8_t);
+  void (*noisefilter)(UphipImage, uint64_t, uint8_t);
+  void (*grayfilter)(UphipImage, UphipGrayfilterParameters);
+  float (*detect_rotation)(UphipImage, UphipRectangle, const UphipDeskewParameters);
+  void (*deskew)(UphipImage, UphipRectangle, float, UphipInterpolation);
+} UphipBackend;
+
+/* image_backend_get() for UNPAPER_DEVICE_HIP (backend.c:135-157). */
+const UphipBackend *uphip_backend(void);
+
+/* ---------------------------------------------------------------------------
+ * Runtime — cuda_runtime.h / cuda_stream_pool.h peers.  One process may drive
+ * several GPUs: the current device and current stream are thread-local
+ * (cuda_runtime.c:70 keeps only a TLS stream; we add the device).
+ * ------------------------------------------------------------------------- */
+typedef enum {
+  UPHIP_INIT_OK = 0,
+  UPHIP_INIT_NO_RUNTIME = 1,
+  UPHIP_INIT_NO_DEVICE = 2,
+  UPHIP_INIT_ERROR = 3,
+} UphipInitStatus;
+
+UphipInitStatus uphip_try_init(void);
+const char *uphip_init_status_string(UphipInitStatus st);
+int uphip_device_count(void);
+int uphip_set_device(int device);     /* TLS current device */
+int uphip_get_device(void);
+/* Per-device stream pool (cuda_stream_pool_global_acquire/release). */
+void *uphip_stream_acquire(void);
+void uphip_stream_release(void *stream);
+void uphip_set_current_stream(void *stream); /* TLS; NULL = per-thread default */
+void *uphip_get_current_stream(void);
+int uphip_synchronize(void);           /* current stream */
+/* Error reporting.  The reference's errOutput() exits (lib/logging.h); here a
+ * failing op records the message and returns, and the caller checks.  Set
+ * `fatal` to restore exit-on-error. */
+const char *uphip_last_error(void);    /* NULL when no error since clear */
+void uphip_clear_error(void);
+void uphip_set_fatal_errors(bool fatal);
+const char *uphip_version(void);
+
+/* ---------------------------------------------------------------------------
+ * Per-sheet options — lib/options.h:32-127 (processing subset) plus the
+ * SheetProcessConfig fields (sheet_process.h:22-37).  Per-sheet "--no-xxx"
+ * multi-indexes are resolved by the caller into `disable` bits for the sheet.
+ * ------------------------------------------------------------------------- */
+enum {
+  UPHIP_NO_BLACKFILTER = 1u << 0,
+  UPHIP_NO_NOISEFILTER = 1u << 1,
+  UPHIP_NO_BLURFILTER = 1u << 2,
+  UPHIP_NO_GRAYFILTER = 1u << 3,
+  UPHIP_NO_MASK_SCAN = 1u << 4,
+  UPHIP_NO_MASK_CENTER = 1u << 5,
+  UPHIP_NO_DESKEW = 1u << 6,
+  UPHIP_NO_WIPE = 1u << 7,
+  UPHIP_NO_BORDER = 1u << 8,
+  UPHIP_NO_BORDER_SCAN = 1u << 9,
+  UPHIP_NO_BORDER_ALIGN = 1u << 10,
+};
+
+typedef struct {
+  int32_t layout;               /* UphipLayout */
+  int32_t input_count;          /* --input-pages (1..2) */
+  int32_t output_count;         /* --output-pages (1..2) */
+  int32_t output_pixel_format;  /* UPHIP_FMT_NONE = same as first input */
+  uint32_t disable;             /* UPHIP_NO_* bits for this sheet */
+
+  int16_t pre_rotate, post_rotate; /* 0, 90, -90 */
+  UphipDirection pre_mirror, post_mirror;
+  UphipDelta pre_shift, post_shift;
+  UphipRectangleSize sheet_size, page_size, post_page_size;
+  UphipRectangleSize stretch_size, post_stretch_size;
+  float pre_zoom_factor, post_zoom_factor;
+
+  UphipPixel sheet_background;
+  UphipPixel mask_color;
+  uint8_t abs_black_threshold;
+  uint8_t abs_white_threshold;
+
+  UphipBorder pre_border, border, post_border;
+  UphipWipes pre_wipes, wipes, post_wipes;
+
+  UphipDeskewParameters deskew_parameters;
+  UphipMaskDetectionParameters mask_detection_parameters;
+  UphipMaskAlignmentParameters mask_alignment_parameters;
+  UphipBorderScanParameters border_scan_parameters;
+  int32_t interpolate_type;     /* UphipInterpolation */
+  UphipGrayfilterParameters grayfilter_parameters;
+  UphipBlackfilterParameters blackfilter_parameters; /* exclusions = config */
+  UphipBlurfilterParameters blurfilter_parameters;
+  uint64_t noisefilter_intensity;
+
+  /* SheetProcessConfig */
+  size_t pre_mask_count;
+  UphipRectangle pre_masks[UPHIP_MAX_MASKS];
+  size_t point_count;           /* initial points (0 = layout default) */
+  UphipPoint points[UPHIP_MAX_POINTS];
+  int32_t middle_wipe[2];
+} UphipOptions;
+
+/* options_init + options_init_filter_defaults (lib/options.c:23-173) with the
+ * CLI's derived thresholds (cli_options.c:229-269,1108-1109). */
+void uphip_options_init(UphipOptions *o);
+
+/* ---------------------------------------------------------------------------
+ * Device batch pipeline — the MI355X-native peer of lib/batch_worker.c's
+ * per-job loop over process_sheet (sheet_process.c:134).  A batch holds up to
+ * `capacity` sheets of identical input geometry resident in HBM; one run pushes
+ * every sheet through the full stage table of src/core/sheet_stages.c:660-672
+ * with one kernel launch per stage per batch, no host synchronisation between
+ * stages.  Results are bit-identical to process_sheet on the CPU backend.
+ * ------------------------------------------------------------------------- */
+typedef struct UphipBatch UphipBatch;
+
+typedef struct {
+  int32_t capacity;        /* sheets per batch */
+  int32_t page_width;      /* input page geometry (all pages) */
+  int32_t page_height;
+  int32_t page_format;     /* UphipPixelFormat of the inputs */
+} UphipBatchGeometry;
+
+UphipBatch *uphip_batch_create(const UphipOptions *options,
+                               const UphipBatchGeometry *geometry);
+void uphip_batch_destroy(UphipBatch *batch);
+/* Output geometry every sheet of this batch will have. */
+int uphip_batch_output_info(UphipBatch *batch, int32_t *width, int32_t *height,
+                            int32_t *format, int64_t *bytes_per_sheet);
+/* Device pointer of input slot `i` (page j of the sheet: i*input_count + j),
+ * pitch in bytes.  Caller may write input pages there directly (device-side
+ * decode / pre-staged inputs). */
+void *uphip_batch_input_ptr(UphipBatch *batch, int32_t slot, int64_t *pitch);
+/* Host → device copy of one page (async on the batch stream). */
+int uphip_batch_set_input(UphipBatch *batch, int32_t slot, const void *host,
+                          int64_t linesize);
+/* Copy `count` device-resident pages (contiguous, `pitch` bytes per row,
+ * `page_stride` bytes per page) into input slots [first, first+count). */
+int uphip_batch_set_inputs_device(UphipBatch *batch, int32_t first, int32_t count,
+                                  const void *device_src, int64_t pitch,
+                                  int64_t page_stride);
+/* Run the pipeline on sheets [0, count).  Asynchronous: returns after
+ * enqueueing; uphip_batch_wait() joins. */
+int uphip_batch_run(UphipBatch *batch, int32_t count);
+int uphip_batch_wait(UphipBatch *batch);
+/* Device → host copy of output sheet `i` (output page j for output_count 2 is
+ * returned side by side, exactly as the sheet). */
+int uphip_batch_get_output(UphipBatch *batch, int32_t sheet, void *host,
+                           int64_t linesize);
+void *uphip_batch_output_ptr(UphipBatch *batch, int32_t sheet, int64_t *pitch);
+/* Per-sheet results for inspection / tests: masks, rotation, borders. */
+typedef struct {
+  int32_t mask_count;
+  UphipRectangle masks[UPHIP_MAX_PAGES];
+  float rotation[UPHIP_MAX_PAGES];
+  UphipRectangle border_masks[UPHIP_MAX_PAGES];
+  int32_t width, height;
+  uint32_t flags;
+} UphipSheetReport;
+int uphip_batch_get_report(UphipBatch *batch, int32_t sheet,
+                           UphipSheetReport *report);
+/* Per-kernel timing of the last run (HIP events on the batch stream). */
+int uphip_batch_kernel_times(UphipBatch *batch, const char **names, float *ms,
+                             int max_entries);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* UNPAPER_HIP_H */
