@@ -385,14 +385,15 @@ void *uphip_batch_input_ptr(UphipBatch *batch, int32_t slot, int64_t *pitch);
 /* Host → device copy of one page (async on the batch stream). */
 int uphip_batch_set_input(UphipBatch *batch, int32_t slot, const void *host,
                           int64_t linesize);
-/* Copy `count` device-resident pages (contiguous, `pitch` bytes per row,
- * `page_stride` bytes per page) into input slots [first, first+count). */
-int uphip_batch_set_inputs_device(UphipBatch *batch, int32_t first, int32_t count,
-                                  const void *device_src, int64_t pitch,
-                                  int64_t page_stride);
-/* Run the pipeline on sheets [0, count).  Asynchronous: returns after
- * enqueueing; uphip_batch_wait() joins. */
+/* Run the pipeline on sheets [0, count) whose pages sit in the batch's input
+ * slots.  Asynchronous: returns after enqueueing; uphip_batch_wait() joins
+ * and reports device-side failures. */
 int uphip_batch_run(UphipBatch *batch, int32_t count);
+/* Same, reading the pages in place from device memory: page j of sheet s is
+ * at pages + (s*input_count + j)*page_stride, rows `pitch` bytes apart
+ * (pre-staged / device-decoded inputs, no copy). */
+int uphip_batch_run_device(UphipBatch *batch, int32_t count, const void *pages,
+                           int64_t pitch, int64_t page_stride);
 int uphip_batch_wait(UphipBatch *batch);
 /* Device → host copy of output sheet `i` (output page j for output_count 2 is
  * returned side by side, exactly as the sheet). */
@@ -413,6 +414,21 @@ int uphip_batch_get_report(UphipBatch *batch, int32_t sheet,
 /* Per-kernel timing of the last run (HIP events on the batch stream). */
 int uphip_batch_kernel_times(UphipBatch *batch, const char **names, float *ms,
                              int max_entries);
+
+/* ---------------------------------------------------------------------------
+ * Benchmark / test support (not part of the reference interface): the
+ * deterministic synthetic page generator of BASELINE.md §3 (identical bytes
+ * on host and device) and raw device buffers.
+ * ------------------------------------------------------------------------- */
+int uphip_synth_pages(void *device_dst, int64_t pitch, int64_t page_stride,
+                      int32_t width, int32_t height, uint32_t first_page,
+                      int32_t count);
+void uphip_synth_page_host(uint8_t *host, int64_t linesize, int32_t width,
+                           int32_t height, uint32_t page);
+void *uphip_device_alloc(size_t bytes);
+void uphip_device_free(void *ptr);
+int uphip_memcpy_htod(void *dst, const void *src, size_t bytes);
+int uphip_memcpy_dtoh(void *dst, const void *src, size_t bytes);
 
 #ifdef __cplusplus
 }

@@ -253,10 +253,23 @@ void o_wipe_rectangle(OImage im, UphipRectangle input_area, UphipPixel color) {
 
 void o_copy_rectangle(OImage src, OImage dst, UphipRectangle source_area,
                       UphipPoint tc) {
-  /* copy_rectangle_cpu, blit.c:30-80.  The reference's memcpy fast path and
-   * its per-pixel path produce identical bytes whenever the fast path's
-   * conditions hold, so only the per-pixel semantics is restated. */
+  /* copy_rectangle_cpu, blit.c:30-80.  The memcpy fast path (same byte
+   * format, whole target rectangle inside the target) copies raw bytes, which
+   * differs from the per-pixel path only for Y400A: set_pixel writes alpha
+   * 0xFF, memcpy keeps the source alpha. */
   UphipRectangle a = clip_rect(src, source_area);
+  const int32_t w = a.vertex[1].x - a.vertex[0].x + 1;
+  const int32_t h = a.vertex[1].y - a.vertex[0].y + 1;
+  const int bpp = src.format == UPHIP_FMT_GRAY8 ? 1 : src.format == UPHIP_FMT_Y400A ? 2
+                  : src.format == UPHIP_FMT_RGB24 ? 3 : 0;
+  if (src.format == dst.format && w > 0 && h > 0 && tc.x >= 0 && tc.y >= 0 &&
+      tc.x + w <= dst.width && tc.y + h <= dst.height && bpp > 0) {
+    for (int32_t sy = a.vertex[0].y, ty = tc.y; sy <= a.vertex[1].y; sy++, ty++)
+      memcpy(dst.data + (int64_t)ty * dst.linesize + (int64_t)tc.x * bpp,
+             src.data + (int64_t)sy * src.linesize + (int64_t)a.vertex[0].x * bpp,
+             (size_t)w * bpp);
+    return;
+  }
   for (int32_t sy = a.vertex[0].y, ty = tc.y; sy <= a.vertex[1].y; sy++, ty++)
     for (int32_t sx = a.vertex[0].x, tx = tc.x; sx <= a.vertex[1].x; sx++, tx++)
       o_set_pixel(dst, (UphipPoint){tx, ty}, o_get_pixel(src, (UphipPoint){sx, sy}));
@@ -1084,7 +1097,10 @@ float o_detect_rotation(OImage im, UphipRectangle mask,
   for (int i = 0; i < count; i++) total += rot[i];
   float average = total / count;
   total = 0.0;
-  for (int i = 0; i < count; i++) total += powf(rot[i] - average, 2);
+  /* called through a pointer: the reference's default (-O0) build calls
+   * glibc powf, which gcc -O2 would otherwise fold into x*x */
+  static float (*volatile pw)(float, float) = powf;
+  for (int i = 0; i < count; i++) total += pw(rot[i] - average, 2);
   float deviation = sqrtf(total);
   return deviation <= pr->deskewScanDeviationRad ? average : 0.0f;
 }

@@ -1,0 +1,266 @@
+"""GPU parity of the filters and rotation detection (filters.c / deskew.c
+peers): HIP == oracle bit for bit.  The small hand-made scenes restate the
+reference's own unit tests (tests/cuda_filters_test.c:42-383,
+tests/cuda_deskew_test.c:18-40); the synthetic pages exercise the default
+parameters, order-dependent cases (clustered specks, edge-zone quirks, wipe
+feedback on colour tiles, flood fills) and odd geometries."""
+import math
+
+import numpy as np
+import pytest
+
+from unpaper_hip import ctypes_abi as A
+from unpaper_hip.hostimage import HostImage
+from helpers import BYTE_FORMATS, assert_same, make_image
+
+pytestmark = pytest.mark.gpu
+
+WHITE, BLACK = A.Pixel(255, 255, 255), A.Pixel(0, 0, 0)
+
+
+def blank(w, h, fmt, thr):
+    shape = {A.FMT_RGB24: (h, w, 3), A.FMT_Y400A: (h, w, 2)}.get(fmt, (h, w))
+    return HostImage.from_array(np.full(shape, 255, np.uint8), fmt, abs_black_threshold=thr)
+
+
+def put(oracle, h, x, y, px):
+    oracle.wipe_rectangle(h, A.rect(x, y, x, y), px)
+
+
+def both(hip, oracle, h, op_hip, op_oracle):
+    d = hip.upload(h)
+    op_hip(d)
+    op_oracle(h)
+    assert_same(d.to_host(), h)
+
+
+# ---------------------------------------------------------------- noisefilter
+def scene_noise(oracle, h):          # cuda_filters_test.c:42-54
+    put(oracle, h, 5, 5, BLACK)
+    oracle.wipe_rectangle(h, A.rect(15, 10, 17, 12), BLACK)
+
+
+def scene_noise_diag(oracle, h):     # cuda_filters_test.c:56-75
+    for i in range(4):
+        put(oracle, h, 2 + i, 2 + i, BLACK)
+    for dx, dy in [(0, 0), (1, 0), (-1, 0), (0, 1), (0, -1)]:
+        put(oracle, h, 12 + dx, 12 + dy, BLACK)
+    put(oracle, h, 24, 6, BLACK)
+    put(oracle, h, 25, 6, BLACK)
+
+
+@pytest.mark.parametrize("scene,fmt,size,thr,intensity,white", [
+    (scene_noise, A.FMT_GRAY8, (32, 24), 64, 2, 200),
+    (scene_noise_diag, A.FMT_GRAY8, (32, 24), 64, 4, 200),
+    (scene_noise_diag, A.FMT_GRAY8, (32, 24), 64, 3, 200),
+    (scene_noise, A.FMT_Y400A, (20, 16), 64, 3, 180),
+])
+def test_noisefilter_reference_scenes(hip, oracle, scene, fmt, size, thr, intensity, white):
+    h = blank(*size, fmt, thr)
+    scene(oracle, h)
+    both(hip, oracle, h, lambda d: hip.noisefilter(d, intensity, white),
+         lambda o: oracle.noisefilter(o, intensity, white))
+
+
+def test_noisefilter_rgb_scene(hip, oracle):  # cuda_filters_test.c:77-90
+    h = blank(32, 24, A.FMT_RGB24, 64)
+    put(oracle, h, 4, 4, A.Pixel(30, 0, 0))
+    put(oracle, h, 5, 4, A.Pixel(28, 0, 0))
+    oracle.wipe_rectangle(h, A.rect(14, 10, 16, 12), A.Pixel(20, 40, 60))
+    both(hip, oracle, h, lambda d: hip.noisefilter(d, 2, 200),
+         lambda o: oracle.noisefilter(o, 2, 200))
+
+
+@pytest.mark.parametrize("fmt", BYTE_FORMATS)
+@pytest.mark.parametrize("size,seed,specks", [((300, 200), 1, 400), ((640, 480), 2, 3000),
+                                              ((129, 257), 3, 800), ((1000, 700), 4, 6000)])
+@pytest.mark.parametrize("intensity", [4, 2, 6])
+def test_noisefilter_pages(hip, oracle, fmt, size, seed, specks, intensity):
+    # dense specks -> many clustered (sequentially resolved) components; specks
+    # touch the left/top edge -> the unsigned-loop quirk zone
+    h = make_image(*size, fmt, seed=seed, specks=specks, margin=0)
+    both(hip, oracle, h, lambda d: hip.noisefilter(d, intensity, 229),
+         lambda o: oracle.noisefilter(o, intensity, 229))
+
+
+def test_noisefilter_edge_quirk(hip, oracle):
+    # components hugging x < level / y < level-1, where the reference's ring
+    # loops skip whole rows (int32 vs uint32 comparison)
+    g = np.full((40, 50), 255, np.uint8)
+    for (x, y) in [(0, 0), (1, 0), (0, 5), (1, 6), (2, 10), (0, 20), (3, 1), (10, 0), (11, 1),
+                   (20, 2), (21, 2), (22, 2), (2, 30), (2, 31), (3, 31), (4, 31), (1, 32)]:
+        g[y, x] = 0
+    h = HostImage.from_array(g, A.FMT_GRAY8)
+    both(hip, oracle, h, lambda d: hip.noisefilter(d, 4, 229),
+         lambda o: oracle.noisefilter(o, 4, 229))
+
+
+# ---------------------------------------------------------------- grayfilter
+def test_grayfilter_reference_scene(hip, oracle):  # cuda_filters_test.c:296-331
+    h = blank(8, 8, A.FMT_GRAY8, 50)
+    oracle.wipe_rectangle(h, A.rect(0, 0, 3, 3), A.Pixel(150, 150, 150))
+    oracle.wipe_rectangle(h, A.rect(4, 0, 7, 3), A.Pixel(80, 80, 80))
+    p = A.GrayfilterParameters(A.RectangleSize(4, 4), A.Delta(4, 4), 127)
+    both(hip, oracle, h, lambda d: hip.grayfilter(d, p), lambda o: oracle.grayfilter(o, p))
+
+
+@pytest.mark.parametrize("fmt", BYTE_FORMATS)
+@pytest.mark.parametrize("size", [(300, 200), (1001, 777), (50, 50), (7, 3)])
+@pytest.mark.parametrize("params", [((50, 50), (20, 20), 127), ((30, 20), (15, 8), 127),
+                                    ((50, 50), (20, 20), 200), ((13, 7), (5, 3), 60)])
+def test_grayfilter_pages(hip, oracle, fmt, size, params):
+    h = make_image(*size, fmt, seed=5)
+    p = A.GrayfilterParameters(A.RectangleSize(*params[0]), A.Delta(*params[1]), params[2])
+    both(hip, oracle, h, lambda d: hip.grayfilter(d, p), lambda o: oracle.grayfilter(o, p))
+
+
+@pytest.mark.parametrize("black", [40, 100, 170])
+def test_grayfilter_feedback_rgb(hip, oracle, black):
+    # saturated colour blocks: gray > black threshold but min(rgb) tiny, so a
+    # tile fails on the original image and passes once earlier tiles are wiped
+    rng = np.random.default_rng(7)
+    rgb = np.full((260, 330, 3), 255, np.uint8)
+    for _ in range(60):
+        x, y = int(rng.integers(0, 320)), int(rng.integers(0, 250))
+        rgb[y:y + int(rng.integers(3, 30)), x:x + int(rng.integers(3, 30))] = \
+            [int(rng.integers(200, 256)), int(rng.integers(200, 256)), int(rng.integers(0, 30))]
+    h = HostImage.from_array(rgb, A.FMT_RGB24, abs_black_threshold=black)
+    for thr in (127, 160, 90):
+        p = A.GrayfilterParameters(A.RectangleSize(50, 50), A.Delta(20, 20), thr)
+        hh = h.copy()
+        both(hip, oracle, hh, lambda d: hip.grayfilter(d, p), lambda o: oracle.grayfilter(o, p))
+
+
+# ---------------------------------------------------------------- blurfilter
+def test_blurfilter_reference_scene(hip, oracle):  # cuda_filters_test.c:337-383
+    h = blank(16, 16, A.FMT_GRAY8, 64)
+    for (x, y) in [(1, 5), (2, 5), (1, 6)]:
+        put(oracle, h, x, y, BLACK)
+    oracle.wipe_rectangle(h, A.rect(8, 4, 11, 7), BLACK)
+    p = A.BlurfilterParameters(A.RectangleSize(4, 4), A.Delta(2, 2), 0.1)
+    both(hip, oracle, h, lambda d: hip.blurfilter(d, p, 200),
+         lambda o: oracle.blurfilter(o, p, 200))
+
+
+@pytest.mark.parametrize("fmt", BYTE_FORMATS)
+@pytest.mark.parametrize("size", [(2480 // 4, 3508 // 4), (1001, 777), (99, 300), (100, 100)])
+@pytest.mark.parametrize("params", [((100, 100), (50, 50), 0.01), ((40, 30), (15, 20), 0.05),
+                                    ((64, 64), (64, 13), 0.2)])
+def test_blurfilter_pages(hip, oracle, fmt, size, params):
+    h = make_image(*size, fmt, seed=6, specks=300)
+    p = A.BlurfilterParameters(A.RectangleSize(*params[0]), A.Delta(*params[1]), params[2])
+    both(hip, oracle, h, lambda d: hip.blurfilter(d, p, 229),
+         lambda o: oracle.blurfilter(o, p, 229))
+
+
+# ---------------------------------------------------------------- blackfilter
+def black_params(oracle, size=(20, 20), step=(5, 5), depth=(500, 500), thr=242, intensity=20,
+                 direction=(True, True), exclusions=()):
+    p = oracle.default_options().blackfilter_parameters
+    p.scan_size = A.RectangleSize(*size)
+    p.scan_step = A.Delta(*step)
+    p.scan_depth.horizontal, p.scan_depth.vertical = depth
+    p.abs_threshold = thr
+    p.intensity = intensity
+    p.scan_direction = A.Direction(*direction)
+    p.exclusions_count = len(exclusions)
+    for i, e in enumerate(exclusions):
+        p.exclusions[i] = A.rect(*e)
+    return p
+
+
+def test_blackfilter_reference_scene(hip, oracle):  # cuda_filters_test.c:249-290
+    h = blank(32, 24, A.FMT_GRAY8, 128)
+    oracle.wipe_rectangle(h, A.rect(8, 0, 11, 23), BLACK)
+    p = black_params(oracle, (4, 4), (2, 2), (32, 24), int(255 * np.float32(0.9)), 2)
+    both(hip, oracle, h, lambda d: hip.blackfilter(d, p), lambda o: oracle.blackfilter(o, p))
+
+
+def band_page(w, h, fmt, band, seed, noise=True):
+    rng = np.random.default_rng(seed)
+    g = make_image(w, h, A.FMT_GRAY8, seed=seed).to_gray()
+    x0, x1, y0, y1 = band
+    g[y0:y1, x0:x1] = rng.integers(0, 11, size=(y1 - y0, x1 - x0)) if noise else 0
+    if fmt == A.FMT_GRAY8:
+        return HostImage.from_array(g, fmt)
+    if fmt == A.FMT_RGB24:
+        return HostImage.from_array(np.repeat(g[:, :, None], 3, axis=2), fmt)
+    return HostImage.from_array(np.stack([g, np.full_like(g, 255)], axis=2), fmt)
+
+
+@pytest.mark.parametrize("fmt", BYTE_FORMATS)
+@pytest.mark.parametrize("band", [(0, 40, 0, 700), (0, 600, 0, 25), (560, 600, 100, 300),
+                                  (0, 30, 200, 400)])
+def test_blackfilter_bands(hip, oracle, fmt, band):
+    h = band_page(600, 700, fmt, band, seed=8)
+    p = black_params(oracle, exclusions=[(150, 175, 449, 524)])
+    both(hip, oracle, h, lambda d: hip.blackfilter(d, p), lambda o: oracle.blackfilter(o, p))
+
+
+@pytest.mark.parametrize("intensity", [20, 1, 3])
+@pytest.mark.parametrize("size", [(300, 400), (123, 77)])
+def test_blackfilter_irregular(hip, oracle, intensity, size):
+    # dark blobs with holes, gaps and stray strokes: the fill order matters
+    rng = np.random.default_rng(intensity + size[0])
+    w, hh = size
+    g = np.full((hh, w), 255, np.uint8)
+    g[:, :12] = rng.integers(0, 40, size=(hh, 12))
+    for _ in range(40):
+        y, x = int(rng.integers(0, hh)), int(rng.integers(0, 30))
+        g[y:y + int(rng.integers(1, 5)), x:x + int(rng.integers(1, 25))] = rng.integers(0, 200)
+    g[rng.random((hh, w)) < 0.02] = 0
+    h = HostImage.from_array(g, A.FMT_GRAY8)
+    p = black_params(oracle, intensity=intensity, depth=(100, 100))
+    both(hip, oracle, h, lambda d: hip.blackfilter(d, p), lambda o: oracle.blackfilter(o, p))
+
+
+# ---------------------------------------------------------- rotation detection
+def skewed_edge(w, h, radians, fmt=A.FMT_GRAY8):  # cuda_deskew_test.c:18-33
+    cx = np.float32(w) * np.float32(0.35)
+    cy = np.float32(h) / np.float32(2.0)
+    m = np.float32(math.tan(np.float32(radians)))
+    y, x = np.mgrid[0:h, 0:w].astype(np.float32)
+    black = x >= cx + m * (y - cy)
+    g = np.where(black, 0, 255).astype(np.uint8)
+    return HostImage.from_array(g if fmt == A.FMT_GRAY8 else np.repeat(g[:, :, None], 3, 2),
+                                fmt, abs_black_threshold=128)
+
+
+def deskew_params(oracle, rng=5.0, step=0.1, dev=1.0, size=1500, depth=0.5,
+                  edges=(True, False, True, False)):
+    p = oracle.default_options().deskew_parameters
+    p.deskewScanRangeRad = np.float32(np.float32(rng) * math.pi / 180.0)
+    p.deskewScanStepRad = np.float32(np.float32(step) * math.pi / 180.0)
+    p.deskewScanDeviationRad = np.float32(np.float32(dev) * math.pi / 180.0)
+    p.deskewScanSize = size
+    p.deskewScanDepth = depth
+    p.scan_edges = A.Edges(*edges)
+    return p
+
+
+@pytest.mark.parametrize("edges", [(True, False, False, False), (True, False, True, False),
+                                   (False, True, False, True), (True, True, True, True)])
+def test_detect_rotation_reference_scene(hip, oracle, edges):  # cuda_deskew_test.c:86-108
+    h = skewed_edge(241, 179, 2.0 * math.pi / 180.0)
+    p = deskew_params(oracle, dev=10.0, size=400, edges=edges)
+    mask = A.rect(0, 0, 240, 178)
+    r1 = hip.detect_rotation(hip.upload(h), mask, p)
+    r2 = oracle.detect_rotation(h, mask, p)
+    assert np.float32(r1).tobytes() == np.float32(r2).tobytes()
+    if edges[0] and not edges[2]:
+        assert abs(r2) > 1e-4
+
+
+@pytest.mark.parametrize("fmt", [A.FMT_GRAY8, A.FMT_RGB24])
+@pytest.mark.parametrize("deg", [0.0, 0.6, -1.3, 3.7])
+@pytest.mark.parametrize("mask", [(60, 0, 739, 599), (0, 0, 799, 599), (-20, 30, 820, 560)])
+def test_detect_rotation_pages(hip, oracle, fmt, deg, mask):
+    # a text block rotated by `deg` (rendered via the reference deskew itself)
+    h = make_image(800, 600, fmt, seed=9, margin=90)
+    if deg:
+        oracle.deskew(h, A.rect(0, 0, 799, 599), float(np.float32(deg * math.pi / 180)),
+                      A.INTERP_LINEAR)
+    p = deskew_params(oracle, size=400)
+    r1 = hip.detect_rotation(hip.upload(h), A.rect(*mask), p)
+    r2 = oracle.detect_rotation(h, A.rect(*mask), p)
+    assert np.float32(r1).tobytes() == np.float32(r2).tobytes()

@@ -1,0 +1,110 @@
+// filters.h — geometry records and launchers of the filter kernels
+// (imageprocess/filters.c) and rotation detection (imageprocess/deskew.c).
+#pragma once
+
+#include "scan.h"
+
+namespace uph {
+
+// ---- grayfilter (filters.c:370-402) -------------------------------------
+// Tiles of scan_w x scan_h at origins (i*step_x, j*step_y) decompose exactly
+// into cells of gcd(step_x, scan_w) x gcd(step_y, scan_h) pixels.
+struct GrayGeom {
+  int32_t W, H;
+  int32_t cw, ch;      // cell size (pixels)
+  int32_t ncx, ncy;    // cells covering the image
+  int32_t tw, th;      // tile size in cells
+  int32_t tsx, tsy;    // tile step in cells
+  int32_t ntx, nty;    // tiles per row, tile rows (raster order, x fastest)
+  int32_t scan_w, scan_h, step_x, step_y;
+  uint8_t black_thr, abs_thr;
+};
+bool gray_geometry(int32_t W, int32_t H, const UphipGrayfilterParameters& p, uint8_t black_thr,
+                   GrayGeom* g);
+size_t gray_scratch_bytes(const GrayGeom& g);  // per sheet
+void launch_grayfilter(const PlaneRef& img, const GrayGeom& g, void* scratch,
+                       int64_t scratch_stride, const int32_t* active, int count, hipStream_t st);
+
+// ---- blurfilter (filters.c:149-232) -------------------------------------
+struct BlurGeom {
+  int32_t W, H;
+  int32_t sw, sh, step_y;
+  int32_t bpr;       // blocks per row
+  int32_t T;         // iterations of the top loop
+  int32_t nrect;     // counted rectangles: bpr (row 0) + T*(bpr+1)
+  uint8_t white;
+  float intensity;
+};
+bool blur_geometry(int32_t W, int32_t H, const UphipBlurfilterParameters& p, uint8_t white,
+                   BlurGeom* g);
+size_t blur_scratch_bytes(const BlurGeom& g);
+void launch_blurfilter(const PlaneRef& img, const BlurGeom& g, void* scratch,
+                       int64_t scratch_stride, const int32_t* active, int count, hipStream_t st);
+
+// ---- noisefilter (filters.c:238-338) ------------------------------------
+struct NoiseGeom {
+  int32_t W, H;
+  int32_t intensity;   // clamped: > 4 => everything resolved sequentially
+  uint8_t white;
+  int32_t capacity;    // entries per list per sheet
+  int32_t all_seq;
+};
+bool noise_geometry(int32_t W, int32_t H, uint64_t intensity, uint8_t white, NoiseGeom* g);
+size_t noise_scratch_bytes(const NoiseGeom& g);
+void launch_noisefilter(const PlaneRef& img, const NoiseGeom& g, void* scratch,
+                        int64_t scratch_stride, const int32_t* active, SheetCtl* ctl, int count,
+                        hipStream_t st);
+
+// ---- blackfilter (filters.c:49-127, fill.c) -----------------------------
+struct BlackBar {
+  Rect r;          // the bar as scanned (not clipped)
+  int32_t dir;     // 0: horizontal-scan stripe, 1: vertical-scan stripe
+  int32_t excluded;
+};
+struct BlackGeom {
+  int32_t W, H;
+  int32_t nbars;
+  int32_t nbars_h;     // first nbars_h bars belong to the horizontal scan
+  Rect hregion, vregion;  // clipped sum regions (rows of h-stripe, cols of v-stripe)
+  uint8_t abs_threshold;
+  uint8_t mask_max;       // image.abs_black_threshold
+  uint64_t intensity;
+  int32_t stack_capacity; // DFS frames per sheet
+};
+// Enumerates the bars exactly as blackfilter_scan's loops visit them.
+bool black_geometry(int32_t W, int32_t H, const UphipBlackfilterParameters& p, uint8_t mask_max,
+                    BlackGeom* g, BlackBar* bars, int max_bars);
+size_t black_scratch_bytes(const BlackGeom& g);
+void launch_blackfilter(const PlaneRef& img, const BlackGeom& g, const BlackBar* bars,
+                        void* scratch, int64_t scratch_stride, const int32_t* active,
+                        SheetCtl* ctl, int count, hipStream_t st);
+
+// ---- rotation detection (deskew.c:48-241) -------------------------------
+constexpr int kMaxAngles = 512;
+struct RotTable {
+  int32_t nangles;
+  float angle[kMaxAngles];
+  float slope[kMaxAngles];   // tanf(angle) computed on the host (deskew.c:161)
+};
+struct RotGeom {
+  int32_t W, H;
+  int32_t nedges;           // enabled edges (<= 4)
+  int32_t edge_shift[4][2]; // shift per edge in enable order (left,top,right,bottom)
+  int32_t scan_size;        // params.deskewScanSize
+  float scan_depth;
+  int32_t max_masks;
+};
+// peaks[(sheet*max_masks + mask)*4 + edge][angle]
+void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable* table,
+                           const Rect* masks, const int32_t* mask_active, int mask_index,
+                           int32_t* peaks, int count, hipStream_t st, int nangles, int max_scan);
+// Host: the angle sequence of detect_edge_rotation (deskew.c:153-174).
+int rotation_angles(const UphipDeskewParameters& p, RotTable* t);
+// Host: detect_rotation_cpu's combination of per-edge results (deskew.c:219-240)
+float combine_edge_rotations(const float* rot, int count, float deviation_rad);
+void launch_blackfilter_impl(const PlaneRef& img, const BlackGeom& g, const BlackBar* bars,
+                             void* scratch, int64_t ss, const int32_t* active, SheetCtl* ctl,
+                             int count, hipStream_t st, const AxisArgs* hargs,
+                             const AxisArgs* vargs);
+
+}  // namespace uph

@@ -1,0 +1,82 @@
+// kernels.h — launch interface of the HIP kernels (host side).
+//
+// Every data kernel processes a batch of frames: grid.z (or the per-sheet
+// loop) selects the sheet, per-sheet arguments come from device arrays so the
+// same kernels serve the single-image C-ABI ops (count = 1, host-written
+// arguments) and the batch pipeline (arguments written by control kernels).
+#pragma once
+
+#include "common.h"
+
+namespace uph {
+
+// A plane reference: which of the two ping-pong planes of each sheet to use.
+struct PlaneRef {
+  Planes P;
+  const SheetCtl* ctl;  // may be null: then `which` is the plane index
+  int32_t which;        // with ctl: 0 = current plane, 1 = the other one
+};
+
+__device__ __forceinline__ uint8_t* plane_ptr(const PlaneRef& R, int s) {
+  int k = R.which;
+  if (R.ctl) k = R.which ? 1 - R.ctl[s].cur : R.ctl[s].cur;
+  return R.P.base[k] + (int64_t)s * R.P.stride;
+}
+
+inline PlaneRef cur_ref(const Planes& P, const SheetCtl* ctl) { return PlaneRef{P, ctl, 0}; }
+inline PlaneRef other_ref(const Planes& P, const SheetCtl* ctl) { return PlaneRef{P, ctl, 1}; }
+inline PlaneRef fixed_ref(const Planes& P, int k) { return PlaneRef{P, nullptr, k}; }
+
+// ---- per-sheet argument records -----------------------------------------
+struct FillArgs {
+  Rect r;           // already clipped; empty (x1<x0) = no-op
+  uint8_t color[3];
+  int32_t active;
+};
+
+struct CopyArgs {
+  Rect a;           // clipped source area
+  int32_t tx, ty;   // target coordinates of a's top-left
+  int32_t active;
+};
+
+struct MaskArgs {  // apply_masks: up to UPHIP_MAX_MASKS rectangles (as given)
+  int32_t n;
+  uint8_t color[3];
+  Rect m[UPHIP_MAX_MASKS];
+};
+
+struct MoveArgs {  // center_mask / align_mask as one gather (masks.c:222-300)
+  Rect area;         // source area as given (size_of_rectangle(area) = new size)
+  int32_t tx, ty;    // target top-left
+  uint8_t bg[3];
+  int32_t active;    // 0: identity (no pass; plane not flipped)
+};
+
+struct RotateArgs {  // deskew (deskew.c:248-286)
+  Rect mask;
+  float sinval, cosval;
+  int32_t active;
+};
+
+// ---- launchers (kernels_blit.hip) ---------------------------------------
+void launch_fill(const PlaneRef& dst, const FillArgs* args, int count, int rows_hint,
+                 hipStream_t st);
+void launch_copy(const PlaneRef& src, const PlaneRef& dst, const CopyArgs* args, int count,
+                 int rows_hint, hipStream_t st);
+void launch_apply_masks(const PlaneRef& dst, const MaskArgs* args, int count, hipStream_t st);
+void launch_mirror(const PlaneRef& img, bool horizontal, bool vertical, int count,
+                   hipStream_t st);
+void launch_rotate90(const PlaneRef& src, const PlaneRef& dst, int direction, int count,
+                     hipStream_t st);
+void launch_stretch(const PlaneRef& src, const PlaneRef& dst, int interp, int count,
+                    hipStream_t st);
+void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* args,
+                      int count, hipStream_t st);
+void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
+                        int interp, int count, hipStream_t st);
+// Flip `cur` of every sheet whose args[s].active (int at byte offset) is set.
+void launch_flip_if_active(SheetCtl* ctl, const int32_t* active, int64_t stride_bytes,
+                           int count, hipStream_t st);
+
+}  // namespace uph

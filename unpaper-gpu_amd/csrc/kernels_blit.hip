@@ -1,0 +1,574 @@
+// kernels_blit.hip — fill / copy / mask / geometry kernels (imageprocess/blit.c,
+// masks.c apply/center/align, deskew.c rotate) for gfx950.
+//
+// All kernels are destination-driven: every output byte is produced by exactly
+// one thread, so mono (1 bit per pixel) targets need no atomics (a thread owns
+// a whole byte = 8 pixels).  Rows start 256-byte aligned, so the interior of a
+// row is written with 16-byte stores.
+#include "interp.h"
+#include "kernels.h"
+
+namespace uph {
+
+constexpr int kThreads = 256;
+
+// Write one pixel of any format into `row`; mono formats handled by callers.
+__device__ __forceinline__ void store_px_fmt(uint8_t* row, int fmt, int32_t x, Px p) {
+  if (fmt == F_GRAY8) store_px_row<F_GRAY8>(row, x, p);
+  else if (fmt == F_Y400A) store_px_row<F_Y400A>(row, x, p);
+  else store_px_row<F_RGB24>(row, x, p);
+}
+
+// Raw byte copy of one pixel (keeps Y400A alpha, as memcpy paths do).
+template <int FMT>
+__device__ __forceinline__ void copy_px_raw(uint8_t* drow, int32_t dx, const uint8_t* srow,
+                                            int32_t sx) {
+  constexpr int B = FMT == F_GRAY8 ? 1 : FMT == F_Y400A ? 2 : 3;
+#pragma unroll
+  for (int k = 0; k < B; k++) drow[dx * B + k] = srow[sx * B + k];
+}
+
+// set_pixel semantics for a mono byte: returns the new byte value after
+// writing pixel bit `k` (0 = MSB) with colour p (pixel.c:142-168).
+__device__ __forceinline__ uint8_t mono_set(uint8_t byte, int fmt, int k, Px p,
+                                            uint8_t thr) {
+  bool black = gray_of(p) < thr;
+  if (fmt == F_MONOWHITE) black = !black;
+  const uint8_t bit = (uint8_t)(128 >> k);
+  return black ? (uint8_t)(byte & ~bit) : (uint8_t)(byte | bit);
+}
+
+// Uniform byte fill of [b0, b1) of a 16-byte aligned row.
+__device__ __forceinline__ void fill_bytes(uint8_t* row, int64_t b0, int64_t b1, uint8_t v) {
+  const int64_t c0 = b0 >> 4, c1 = (b1 + 15) >> 4;
+  const uint32_t w = v * 0x01010101u;
+  const uint4 q = make_uint4(w, w, w, w);
+  for (int64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) {
+    const int64_t s = c << 4;
+    if (s >= b0 && s + 16 <= b1) {
+      *reinterpret_cast<uint4*>(row + s) = q;
+    } else {
+      for (int k = 0; k < 16; k++) {
+        const int64_t b = s + k;
+        if (b >= b0 && b < b1) row[b] = v;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// wipe_rectangle_cpu (blit.c:20-24): args[s].r is already clipped.
+// ---------------------------------------------------------------------------
+struct FillLaunch {
+  PlaneRef dst;
+  const FillArgs* args;
+  uint8_t thr;
+};
+
+__global__ void __launch_bounds__(kThreads) k_fill(FillLaunch L) {
+  const int s = blockIdx.z;
+  const FillArgs a = L.args[s];
+  if (!a.active || a.r.x1 < a.r.x0 || a.r.y1 < a.r.y0) return;
+  const Planes& P = L.dst.P;
+  uint8_t* base = plane_ptr(L.dst, s);
+  const Px c{a.color[0], a.color[1], a.color[2]};
+  for (int32_t y = a.r.y0 + blockIdx.x; y <= a.r.y1; y += gridDim.x) {
+    uint8_t* row = base + (int64_t)y * P.pitch;
+    if (P.fmt == F_GRAY8) {
+      fill_bytes(row, a.r.x0, (int64_t)a.r.x1 + 1, gray_of(c));
+    } else if (P.fmt == F_RGB24 && c.r == c.g && c.g == c.b) {
+      fill_bytes(row, 3 * (int64_t)a.r.x0, 3 * ((int64_t)a.r.x1 + 1), c.r);
+    } else if (P.fmt == F_RGB24 || P.fmt == F_Y400A) {
+      for (int32_t x = a.r.x0 + threadIdx.x; x <= a.r.x1; x += blockDim.x)
+        store_px_fmt(row, P.fmt, x, c);
+    } else {  // mono: one thread per byte
+      const int32_t b0 = a.r.x0 >> 3, b1 = a.r.x1 >> 3;
+      for (int32_t b = b0 + threadIdx.x; b <= b1; b += blockDim.x) {
+        uint8_t v = row[b];
+        for (int k = 0; k < 8; k++) {
+          const int32_t x = b * 8 + k;
+          if (x >= a.r.x0 && x <= a.r.x1) v = mono_set(v, P.fmt, k, c, L.thr);
+        }
+        row[b] = v;
+      }
+    }
+  }
+}
+
+void launch_fill(const PlaneRef& dst, const FillArgs* args, int count, int rows_hint,
+                 hipStream_t st) {
+  FillLaunch L{dst, args, 0};
+  int gx = rows_hint < 1 ? 1 : (rows_hint > 1024 ? 1024 : rows_hint);
+  hipLaunchKernelGGL(k_fill, dim3(gx, 1, count), dim3(kThreads), 0, st, L);
+}
+
+// Mono-aware fill (needs the frame's abs_black_threshold).
+void launch_fill_thr(const PlaneRef& dst, const FillArgs* args, int count, int rows_hint,
+                     uint8_t thr, hipStream_t st) {
+  FillLaunch L{dst, args, thr};
+  int gx = rows_hint < 1 ? 1 : (rows_hint > 1024 ? 1024 : rows_hint);
+  hipLaunchKernelGGL(k_fill, dim3(gx, 1, count), dim3(kThreads), 0, st, L);
+}
+
+// ---------------------------------------------------------------------------
+// copy_rectangle_cpu (blit.c:30-80): dst(tx+u, ty+v) = src(a.x0+u, a.y0+v)
+// for (u,v) in the clipped source area; target writes outside are dropped.
+// Format conversion goes through get_pixel/set_pixel semantics.
+// ---------------------------------------------------------------------------
+struct CopyLaunch {
+  PlaneRef src, dst;
+  const CopyArgs* args;
+  uint8_t thr;  // target abs_black_threshold (mono targets)
+};
+
+__global__ void __launch_bounds__(kThreads) k_copy(CopyLaunch L) {
+  const int s = blockIdx.z;
+  const CopyArgs a = L.args[s];
+  if (!a.active || a.a.x1 < a.a.x0 || a.a.y1 < a.a.y0) return;
+  const Planes& S = L.src.P;
+  const Planes& D = L.dst.P;
+  const uint8_t* sbase = plane_ptr(L.src, s);
+  uint8_t* dbase = plane_ptr(L.dst, s);
+  // target columns covered: [tx, tx + w) ∩ [0, D.W)
+  const int32_t w = a.a.x1 - a.a.x0 + 1;
+  const int32_t tx0 = imax(a.tx, 0), tx1 = imin(a.tx + w - 1, D.W - 1);
+  if (tx1 < tx0) return;
+  const int32_t h = a.a.y1 - a.a.y0 + 1;
+  // blit.c:38-69: the memcpy path (raw bytes, Y400A alpha kept) is taken only
+  // when the whole target rectangle lies inside the target frame; otherwise
+  // set_pixel per pixel (Y400A alpha := 0xFF).  Identical for GRAY8/RGB24.
+  const bool fully_inside = a.tx >= 0 && a.ty >= 0 && a.tx + w <= D.W && a.ty + h <= D.H;
+  const bool same_bytes =
+      S.fmt == D.fmt && !is_mono(S.fmt) && (fully_inside || S.fmt != F_Y400A);
+  const int bpp = bytes_per_pixel(D.fmt);
+  for (int32_t sy = a.a.y0 + blockIdx.x; sy <= a.a.y1; sy += gridDim.x) {
+    const int32_t ty = a.ty + (sy - a.a.y0);
+    if (ty < 0 || ty >= D.H) continue;
+    const uint8_t* srow = sbase + (int64_t)sy * S.pitch;
+    uint8_t* drow = dbase + (int64_t)ty * D.pitch;
+    if (same_bytes) {
+      // byte copy: dst bytes [tx0*bpp, (tx1+1)*bpp) from src shifted by delta
+      const int64_t db0 = (int64_t)tx0 * bpp, db1 = ((int64_t)tx1 + 1) * bpp;
+      const int64_t delta = ((int64_t)a.a.x0 - a.tx) * bpp;  // src byte = dst byte + delta
+      if ((delta & 15) == 0) {
+        const int64_t c0 = db0 >> 4, c1 = (db1 + 15) >> 4;
+        for (int64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) {
+          const int64_t b = c << 4;
+          if (b >= db0 && b + 16 <= db1) {
+            *reinterpret_cast<uint4*>(drow + b) =
+                *reinterpret_cast<const uint4*>(srow + b + delta);
+          } else {
+            for (int k = 0; k < 16; k++)
+              if (b + k >= db0 && b + k < db1) drow[b + k] = srow[b + k + delta];
+          }
+        }
+      } else {
+        for (int64_t b = db0 + threadIdx.x; b < db1; b += blockDim.x) drow[b] = srow[b + delta];
+      }
+    } else if (!is_mono(D.fmt)) {
+      for (int32_t tx = tx0 + threadIdx.x; tx <= tx1; tx += blockDim.x) {
+        const int32_t sx = a.a.x0 + (tx - a.tx);
+        store_px_fmt(drow, D.fmt, tx,
+                     load_px_any(sbase, S.pitch, S.fmt, S.W, S.H, sx, sy));
+      }
+    } else {
+      for (int32_t b = (tx0 >> 3) + threadIdx.x; b <= (tx1 >> 3); b += blockDim.x) {
+        uint8_t v = drow[b];
+        for (int k = 0; k < 8; k++) {
+          const int32_t tx = b * 8 + k;
+          if (tx < tx0 || tx > tx1) continue;
+          const int32_t sx = a.a.x0 + (tx - a.tx);
+          v = mono_set(v, D.fmt, k, load_px_any(sbase, S.pitch, S.fmt, S.W, S.H, sx, sy), L.thr);
+        }
+        drow[b] = v;
+      }
+    }
+  }
+}
+
+void launch_copy_thr(const PlaneRef& src, const PlaneRef& dst, const CopyArgs* args, int count,
+                     int rows_hint, uint8_t thr, hipStream_t st) {
+  CopyLaunch L{src, dst, args, thr};
+  int gx = rows_hint < 1 ? 1 : (rows_hint > 1024 ? 1024 : rows_hint);
+  hipLaunchKernelGGL(k_copy, dim3(gx, 1, count), dim3(kThreads), 0, st, L);
+}
+
+void launch_copy(const PlaneRef& src, const PlaneRef& dst, const CopyArgs* args, int count,
+                 int rows_hint, hipStream_t st) {
+  launch_copy_thr(src, dst, args, count, rows_hint, 0, st);
+}
+
+// ---------------------------------------------------------------------------
+// apply_masks_cpu (masks.c:306-322): pixels outside every mask <- colour.
+// No reads of the image: outside pixels are written, inside left untouched.
+// ---------------------------------------------------------------------------
+struct MasksLaunch {
+  PlaneRef dst;
+  const MaskArgs* args;
+  uint8_t thr;
+};
+
+__global__ void __launch_bounds__(kThreads) k_apply_masks(MasksLaunch L) {
+  const int s = blockIdx.z;
+  const MaskArgs* a = L.args + s;
+  const int32_t n = a->n;
+  if (n <= 0) return;
+  __shared__ Rect m[UPHIP_MAX_MASKS];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) m[i] = normalize(a->m[i]);
+  __syncthreads();
+  const Planes& P = L.dst.P;
+  uint8_t* base = plane_ptr(L.dst, s);
+  const Px c{a->color[0], a->color[1], a->color[2]};
+  for (int32_t y = blockIdx.x; y < P.H; y += gridDim.x) {
+    uint8_t* row = base + (int64_t)y * P.pitch;
+    // fast path: a single mask covering this row -> two runs outside it
+    if (!is_mono(P.fmt)) {
+      for (int32_t x = threadIdx.x; x < P.W; x += blockDim.x) {
+        bool inside = false;
+        for (int i = 0; i < n && !inside; i++)
+          inside = x >= m[i].x0 && x <= m[i].x1 && y >= m[i].y0 && y <= m[i].y1;
+        if (!inside) store_px_fmt(row, P.fmt, x, c);
+      }
+    } else {
+      for (int32_t b = threadIdx.x; b < (P.W + 7) / 8; b += blockDim.x) {
+        uint8_t v = row[b];
+        for (int k = 0; k < 8; k++) {
+          const int32_t x = b * 8 + k;
+          if (x >= P.W) break;
+          bool inside = false;
+          for (int i = 0; i < n && !inside; i++)
+            inside = x >= m[i].x0 && x <= m[i].x1 && y >= m[i].y0 && y <= m[i].y1;
+          if (!inside) v = mono_set(v, P.fmt, k, c, L.thr);
+        }
+        row[b] = v;
+      }
+    }
+  }
+}
+
+void launch_apply_masks_thr(const PlaneRef& dst, const MaskArgs* args, int count, uint8_t thr,
+                            hipStream_t st) {
+  MasksLaunch L{dst, args, thr};
+  int gx = dst.P.H < 1 ? 1 : (dst.P.H > 1024 ? 1024 : dst.P.H);
+  hipLaunchKernelGGL(k_apply_masks, dim3(gx, 1, count), dim3(kThreads), 0, st, L);
+}
+void launch_apply_masks(const PlaneRef& dst, const MaskArgs* args, int count, hipStream_t st) {
+  launch_apply_masks_thr(dst, args, count, 0, st);
+}
+
+// ---------------------------------------------------------------------------
+// Generic destination-driven gather: dst(x,y) = src(map(x,y)) or a constant.
+// Used for mirror, rotate90, shift (out of place).
+// ---------------------------------------------------------------------------
+enum GatherKind : int32_t { G_MIRROR = 0, G_ROT90 = 1, G_SHIFT = 2 };
+
+struct GatherLaunch {
+  PlaneRef src, dst;
+  int32_t kind;
+  int32_t p0, p1;   // mirror: h, v; rot90: direction; shift: dx, dy
+  uint8_t bg[3];
+  uint8_t thr;
+};
+
+__device__ __forceinline__ Px gather_px(const GatherLaunch& L, const uint8_t* sbase, int32_t x,
+                                        int32_t y) {
+  const Planes& S = L.src.P;
+  int32_t sx, sy;
+  if (L.kind == G_MIRROR) {
+    sx = L.p0 ? S.W - 1 - x : x;
+    sy = L.p1 ? S.H - 1 - y : y;
+  } else if (L.kind == G_ROT90) {
+    // flip_rotate_90_cpu (blit.c:289-310) inverted: dst(xx,yy) = src(x,y)
+    if (L.p0 > 0) {  // xx = H-1-y, yy = x
+      sx = y;
+      sy = S.H - 1 - x;
+    } else {         // xx = y, yy = W-1-x
+      sx = S.W - 1 - y;
+      sy = x;
+    }
+  } else {  // shift: new frame filled with background, src copied at (dx,dy)
+    sx = x - L.p0;
+    sy = y - L.p1;
+    if (sx < 0 || sy < 0 || sx >= S.W || sy >= S.H) return Px{L.bg[0], L.bg[1], L.bg[2]};
+  }
+  return load_px_any(sbase, S.pitch, S.fmt, S.W, S.H, sx, sy);
+}
+
+__global__ void __launch_bounds__(kThreads) k_gather(GatherLaunch L) {
+  const int s = blockIdx.z;
+  const Planes& D = L.dst.P;
+  const uint8_t* sbase = plane_ptr(L.src, s);
+  uint8_t* dbase = plane_ptr(L.dst, s);
+  for (int32_t y = blockIdx.x; y < D.H; y += gridDim.x) {
+    uint8_t* row = dbase + (int64_t)y * D.pitch;
+    if (!is_mono(D.fmt)) {
+      for (int32_t x = threadIdx.x; x < D.W; x += blockDim.x)
+        store_px_fmt(row, D.fmt, x, gather_px(L, sbase, x, y));
+    } else {
+      for (int32_t b = threadIdx.x; b < (D.W + 7) / 8; b += blockDim.x) {
+        uint8_t v = row[b];
+        for (int k = 0; k < 8; k++) {
+          const int32_t x = b * 8 + k;
+          if (x >= D.W) break;
+          v = mono_set(v, D.fmt, k, gather_px(L, sbase, x, y), L.thr);
+        }
+        row[b] = v;
+      }
+    }
+  }
+}
+
+static void launch_gather(const GatherLaunch& L, int count, hipStream_t st) {
+  int gx = L.dst.P.H < 1 ? 1 : (L.dst.P.H > 1024 ? 1024 : L.dst.P.H);
+  hipLaunchKernelGGL(k_gather, dim3(gx, 1, count), dim3(kThreads), 0, st, L);
+}
+
+void launch_mirror_oop(const PlaneRef& src, const PlaneRef& dst, bool h, bool v, uint8_t thr,
+                       int count, hipStream_t st) {
+  GatherLaunch L{src, dst, G_MIRROR, h ? 1 : 0, v ? 1 : 0, {0, 0, 0}, thr};
+  launch_gather(L, count, st);
+}
+void launch_rotate90_thr(const PlaneRef& src, const PlaneRef& dst, int direction, uint8_t thr,
+                         int count, hipStream_t st) {
+  GatherLaunch L{src, dst, G_ROT90, direction, 0, {0, 0, 0}, thr};
+  launch_gather(L, count, st);
+}
+void launch_rotate90(const PlaneRef& src, const PlaneRef& dst, int direction, int count,
+                     hipStream_t st) {
+  launch_rotate90_thr(src, dst, direction, 0, count, st);
+}
+void launch_shift(const PlaneRef& src, const PlaneRef& dst, int dx, int dy, const uint8_t bg[3],
+                  uint8_t thr, int count, hipStream_t st) {
+  GatherLaunch L{src, dst, G_SHIFT, dx, dy, {bg[0], bg[1], bg[2]}, thr};
+  launch_gather(L, count, st);
+}
+void launch_mirror(const PlaneRef&, bool, bool, int, hipStream_t) {}
+
+// ---------------------------------------------------------------------------
+// stretch_frame (blit.c:209-229): dst(x,y) = interpolate(src, x*hr, y*vr).
+// ---------------------------------------------------------------------------
+struct StretchLaunch {
+  PlaneRef src, dst;
+  int32_t interp;
+  float hr, vr;
+  uint8_t thr;
+};
+
+template <int SF>
+__device__ __forceinline__ Px stretch_px(const StretchLaunch& L, const uint8_t* sbase, int32_t x,
+                                         int32_t y) {
+  Src<SF> s{sbase, L.src.P.pitch, L.src.P.W, L.src.P.H};
+  return interpolate<SF>(s, x * L.hr, y * L.vr, L.interp);
+}
+
+__device__ __forceinline__ Px stretch_any(const StretchLaunch& L, const uint8_t* sbase, int32_t x,
+                                          int32_t y) {
+  switch (L.src.P.fmt) {
+    case F_GRAY8: return stretch_px<F_GRAY8>(L, sbase, x, y);
+    case F_Y400A: return stretch_px<F_Y400A>(L, sbase, x, y);
+    case F_RGB24: return stretch_px<F_RGB24>(L, sbase, x, y);
+    default: {
+      // mono sources: interpolate over the 0/255 expansion
+      const Planes& S = L.src.P;
+      struct MonoSrc {
+        const uint8_t* b;
+        int64_t p;
+        int f;
+        int32_t W, H;
+      } ms{sbase, S.pitch, S.fmt, S.W, S.H};
+      (void)ms;
+      // NN / linear / cubic on a mono source read through load_px_any
+      const float cx = x * L.hr, cy = y * L.vr;
+      auto at = [&](int32_t xx, int32_t yy) {
+        return load_px_any(sbase, S.pitch, S.fmt, S.W, S.H, xx, yy);
+      };
+      if (L.interp == UPHIP_INTERP_NN) return at((int)roundf(cx), (int)roundf(cy));
+      if (L.interp == UPHIP_INTERP_LINEAR) {
+        const int x1 = (int)floorf(cx), y1 = (int)floorf(cy);
+        const int x2 = (int)ceilf(cx), y2 = (int)ceilf(cy);
+        if (!(x2 >= 0 && x2 <= S.W - 1 && y2 >= 0 && y2 <= S.H - 1)) return at(x1, y1);
+        if (x1 == x2 && y1 == y2) return at(x1, y1);
+        if (x1 == x2) return linear_px(cx - x1, at(x1, y1), at(x2, y2));
+        if (y1 == y2) return linear_px(cy - y1, at(x1, y1), at(x2, y2));
+        Px h1 = linear_px(cx - x1, at(x1, y1), at(x2, y1));
+        Px h2 = linear_px(cx - x1, at(x1, y2), at(x2, y2));
+        return linear_px(cy - y1, h1, h2);
+      }
+      const int px = (int)cx, py = (int)cy;
+      Px col[4];
+      for (int i = -1; i < 3; ++i)
+        col[i + 1] = cubic_px(cx - px, at(px - 1, py + i), at(px, py + i), at(px + 1, py + i),
+                              at(px + 2, py + i));
+      return cubic_px(cy - py, col[0], col[1], col[2], col[3]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) k_stretch(StretchLaunch L) {
+  const int s = blockIdx.z;
+  const Planes& D = L.dst.P;
+  const uint8_t* sbase = plane_ptr(L.src, s);
+  uint8_t* dbase = plane_ptr(L.dst, s);
+  for (int32_t y = blockIdx.x; y < D.H; y += gridDim.x) {
+    uint8_t* row = dbase + (int64_t)y * D.pitch;
+    if (!is_mono(D.fmt)) {
+      for (int32_t x = threadIdx.x; x < D.W; x += blockDim.x)
+        store_px_fmt(row, D.fmt, x, stretch_any(L, sbase, x, y));
+    } else {
+      for (int32_t b = threadIdx.x; b < (D.W + 7) / 8; b += blockDim.x) {
+        uint8_t v = row[b];
+        for (int k = 0; k < 8; k++) {
+          const int32_t x = b * 8 + k;
+          if (x >= D.W) break;
+          v = mono_set(v, D.fmt, k, stretch_any(L, sbase, x, y), L.thr);
+        }
+        row[b] = v;
+      }
+    }
+  }
+}
+
+void launch_stretch_thr(const PlaneRef& src, const PlaneRef& dst, int interp, uint8_t thr,
+                        int count, hipStream_t st) {
+  StretchLaunch L{src, dst, interp, (float)src.P.W / (float)dst.P.W,
+                  (float)src.P.H / (float)dst.P.H, thr};
+  int gx = dst.P.H < 1 ? 1 : (dst.P.H > 1024 ? 1024 : dst.P.H);
+  hipLaunchKernelGGL(k_stretch, dim3(gx, 1, count), dim3(kThreads), 0, st, L);
+}
+void launch_stretch(const PlaneRef& src, const PlaneRef& dst, int interp, int count,
+                    hipStream_t st) {
+  launch_stretch_thr(src, dst, interp, 0, count, st);
+}
+
+// ---------------------------------------------------------------------------
+// center_mask / align_mask as a single out-of-place gather (masks.c:222-300):
+//   newimage = bg-filled |area|; copy clip(area) -> newimage at (0,0);
+//   wipe clip(area) with bg; copy newimage -> image at (tx,ty).
+// ---------------------------------------------------------------------------
+template <int FMT>
+__global__ void __launch_bounds__(kThreads) k_move_rect(PlaneRef src, PlaneRef dst,
+                                                        const MoveArgs* args) {
+  const int s = blockIdx.z;
+  const MoveArgs a = args[s];
+  if (!a.active) return;
+  const Planes& P = src.P;
+  const uint8_t* sbase = plane_ptr(src, s);
+  uint8_t* dbase = plane_ptr(dst, s);
+  const Rect A = clip(a.area, P.W, P.H);
+  const int32_t aw = A.x1 - A.x0 + 1, ah = A.y1 - A.y0 + 1;  // copied extent (may be <= 0)
+  const int32_t sw = iabs(a.area.x0 - a.area.x1) + 1, sh = iabs(a.area.y0 - a.area.y1) + 1;
+  const Px bg{a.bg[0], a.bg[1], a.bg[2]};
+  // the paste back (copy_rectangle newimage -> image) is a raw memcpy only when
+  // the whole target rectangle is inside the image (blit.c:38-69); otherwise
+  // set_pixel per pixel, which rewrites Y400A alpha as 0xFF
+  const bool raw_paste = a.tx >= 0 && a.ty >= 0 && a.tx + sw <= P.W && a.ty + sh <= P.H;
+  for (int32_t y = blockIdx.x; y < P.H; y += gridDim.x) {
+    const uint8_t* srow = sbase + (int64_t)y * P.pitch;
+    uint8_t* drow = dbase + (int64_t)y * P.pitch;
+    const int32_t v = y - a.ty;
+    for (int32_t x = threadIdx.x; x < P.W; x += blockDim.x) {
+      const int32_t u = x - a.tx;
+      Px o;
+      if (u >= 0 && u < sw && v >= 0 && v < sh) {
+        if (u < aw && v < ah) {
+          const uint8_t* srow_m = sbase + (int64_t)(A.y0 + v) * P.pitch;
+          if (raw_paste) {
+            copy_px_raw<FMT>(drow, x, srow_m, A.x0 + u);
+            continue;
+          }
+          o = load_px_row<FMT>(srow_m, A.x0 + u);
+        } else {
+          o = bg;
+        }
+      } else if (x >= A.x0 && x <= A.x1 && y >= A.y0 && y <= A.y1) {
+        o = bg;
+      } else {
+        copy_px_raw<FMT>(drow, x, srow, x);
+        continue;
+      }
+      store_px_row<FMT>(drow, x, o);
+    }
+  }
+}
+
+void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* args, int count,
+                      hipStream_t st) {
+  int gx = src.P.H < 1 ? 1 : (src.P.H > 1024 ? 1024 : src.P.H);
+  if (src.P.fmt == F_GRAY8)
+    hipLaunchKernelGGL(k_move_rect<F_GRAY8>, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst,
+                       args);
+  else if (src.P.fmt == F_Y400A)
+    hipLaunchKernelGGL(k_move_rect<F_Y400A>, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst,
+                       args);
+  else
+    hipLaunchKernelGGL(k_move_rect<F_RGB24>, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst,
+                       args);
+}
+
+// ---------------------------------------------------------------------------
+// deskew_cpu + rotate (deskew.c:248-286) fused out of place: inside the mask
+// rectangle (placed at mask.vertex[0], clipped to the image) the rotated
+// pixel, elsewhere the source pixel.
+// ---------------------------------------------------------------------------
+template <int FMT>
+__global__ void __launch_bounds__(kThreads) k_rotate_mask(PlaneRef src, PlaneRef dst,
+                                                          const RotateArgs* args, int interp) {
+  const int s = blockIdx.z;
+  const RotateArgs a = args[s];
+  if (!a.active) return;
+  const Planes& P = src.P;
+  const uint8_t* sbase = plane_ptr(src, s);
+  uint8_t* dbase = plane_ptr(dst, s);
+  const Rect nm = normalize(a.mask);
+  const int32_t sw = nm.x1 - nm.x0 + 1, sh = nm.y1 - nm.y0 + 1;
+  // center_of_rectangle (primitives.c:137-145)
+  const float scx = nm.x0 + sw / 2.0f, scy = nm.y0 + sh / 2.0f;
+  const float tcx = 0 + sw / 2.0f, tcy = 0 + sh / 2.0f;
+  const Src<FMT> S{sbase, P.pitch, P.W, P.H};
+  for (int32_t y = blockIdx.x; y < P.H; y += gridDim.x) {
+    uint8_t* drow = dbase + (int64_t)y * P.pitch;
+    const uint8_t* srow = sbase + (int64_t)y * P.pitch;
+    const int32_t v = y - a.mask.y0;
+    for (int32_t x = threadIdx.x; x < P.W; x += blockDim.x) {
+      const int32_t u = x - a.mask.x0;
+      Px o;
+      if (u >= 0 && u < sw && v >= 0 && v < sh) {
+        const float srcX = scx + (u - tcx) * a.cosval + (v - tcy) * a.sinval;
+        const float srcY = scy + (v - tcy) * a.cosval - (u - tcx) * a.sinval;
+        o = interpolate<FMT>(S, srcX, srcY, interp);
+      } else {
+        copy_px_raw<FMT>(drow, x, srow, x);
+        continue;
+      }
+      store_px_row<FMT>(drow, x, o);
+    }
+  }
+}
+
+void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
+                        int interp, int count, hipStream_t st) {
+  int gx = src.P.H < 1 ? 1 : (src.P.H > 2048 ? 2048 : src.P.H);
+  if (src.P.fmt == F_GRAY8)
+    hipLaunchKernelGGL(k_rotate_mask<F_GRAY8>, dim3(gx, 1, count), dim3(kThreads), 0, st, src,
+                       dst, args, interp);
+  else if (src.P.fmt == F_Y400A)
+    hipLaunchKernelGGL(k_rotate_mask<F_Y400A>, dim3(gx, 1, count), dim3(kThreads), 0, st, src,
+                       dst, args, interp);
+  else
+    hipLaunchKernelGGL(k_rotate_mask<F_RGB24>, dim3(gx, 1, count), dim3(kThreads), 0, st, src,
+                       dst, args, interp);
+}
+
+__global__ void k_flip_if_active(SheetCtl* ctl, const int32_t* active, int64_t stride_ints,
+                                 int count) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < count && active[(int64_t)s * stride_ints]) ctl[s].cur ^= 1;
+}
+
+void launch_flip_if_active(SheetCtl* ctl, const int32_t* active, int64_t stride_bytes, int count,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(k_flip_if_active, dim3((count + 255) / 256), dim3(256), 0, st, ctl, active,
+                     stride_bytes / 4, count);
+}
+
+}  // namespace uph

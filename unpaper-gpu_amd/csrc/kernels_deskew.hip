@@ -1,0 +1,203 @@
+// kernels_deskew.hip — rotation detection (deskew.c:48-241).
+//
+// One workgroup per (sheet, edge, angle).  The reference walks a 1500-point
+// virtual line inward one pixel per step, summing 255-max(rgb) under the line,
+// until the accumulated blackness reaches 255*size*depth; the peak is the
+// largest step-to-step increase.  Here the four waves split the line points
+// and each lane owns one inward step of a 64-step chunk, so a wave reads 64
+// consecutive pixels of one image row per point (one coalesced load) and the
+// stopping rule is evaluated on the chunk with a wave prefix sum.
+#include <climits>
+#include <cmath>
+
+#include "filters.h"
+
+namespace uph {
+
+__device__ __forceinline__ int iwave_prefix_excl(int v, int* total) {
+  const int lane = threadIdx.x & 63;
+  int pre = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    int t = __shfl_up(pre, o, 64);
+    if (lane >= o) pre += t;
+  }
+  *total = __shfl(pre, 63, 64);
+  return pre - v;
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, const RotTable* table,
+                                                   const Rect* masks, const int32_t* mask_active,
+                                                   int mask_index, int32_t* peaks) {
+  const int a = blockIdx.x, e = blockIdx.y, s = blockIdx.z;
+  const int na = table->nangles;
+  int32_t* out = peaks + (((int64_t)s * g.max_masks + mask_index) * 4 + e) * na + a;
+  if (mask_active && !mask_active[s]) {
+    if (threadIdx.x == 0) *out = 0;
+    return;
+  }
+  const Rect mask = masks[s];
+  const int sxh = g.edge_shift[e][0], syv = g.edge_shift[e][1];
+  const float m = table->slope[a];
+  // detect_edge_rotation_peak, deskew.c:48-146
+  const int32_t mw = iabs(mask.x0 - mask.x1) + 1, mh = iabs(mask.y0 - mask.y1) + 1;
+  const int maxAbs = (int)(255 * g.scan_size * g.scan_depth);
+  int scan = g.scan_size, maxDepth, half, outer, mid, side;
+  float X, Y, stepX, stepY;
+  if (syv == 0) {
+    if (scan == -1) scan = mh;
+    scan = imin(imin(scan, 10000), mh);
+    maxDepth = mw / 2;
+    half = scan / 2;
+    outer = (int)(fabsf(m) * half);
+    mid = mh / 2;
+    side = sxh > 0 ? mask.x0 - outer : mask.x1 + outer;
+    X = side + half * m;
+    Y = mask.y0 + mid - half;
+    stepX = -m;
+    stepY = 1.0;
+  } else {
+    if (scan == -1) scan = mw;
+    scan = imin(imin(scan, 10000), mw);
+    maxDepth = mh / 2;
+    half = scan / 2;
+    outer = (int)(fabsf(m) * half);
+    mid = mw / 2;
+    side = syv > 0 ? mask.x0 - outer : mask.x1 + outer;  // x-vertices (deskew.c:96-97)
+    X = mask.x0 + mid - half;
+    Y = side - (half * m);
+    stepX = 1.0;
+    stepY = -m;
+  }
+  extern __shared__ int32_t pts[];  // [scan] x, then [scan] y
+  __shared__ int32_t part[4][64];
+  __shared__ int32_t done_flag, result;
+  if (scan <= 0) {
+    if (threadIdx.x == 0) *out = 0;
+    return;
+  }
+  int32_t* px = pts;
+  int32_t* py = pts + scan;
+  if (threadIdx.x == 0) {
+    // the float recurrence of deskew.c:107-112, in order
+    for (int i = 0; i < scan; i++) {
+      px[i] = (int)X;
+      py[i] = (int)Y;
+      X += stepX;
+      Y += stepY;
+    }
+    done_flag = 0;
+    result = 0;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint8_t* base = plane_ptr(img, s);
+  const Rect nm = normalize(mask);
+  int carry_acc = 0, last = 0, maxDiff = 0;  // wave 0 state
+  for (int d0 = 0; d0 < maxDepth; d0 += 64) {
+    const int dep = d0 + lane;
+    int acc = 0;
+    for (int i = w; i < scan; i += 4) {
+      const int32_t x = px[i] + sxh * dep, y = py[i] + syv * dep;
+      if (x >= nm.x0 && x <= nm.x1 && y >= nm.y0 && y <= nm.y1 && x >= 0 && y >= 0 && x < g.W &&
+          y < g.H)
+        acc += 255 - dark_of(load_px_row<FMT>(base + (int64_t)y * img.P.pitch, x));
+    }
+    part[w][lane] = acc;
+    __syncthreads();
+    if (w == 0) {
+      const int B = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+      int tot;
+      const int before = carry_acc + iwave_prefix_excl(B, &tot);
+      const bool exec = before < maxAbs && dep < maxDepth;
+      const unsigned long long X_ = __ballot(!exec);
+      const int stop = X_ ? __ffsll((long long)X_) - 1 : 64;
+      // the permute runs on the whole wave: a lane reading an inactive lane's
+      // register gets no defined value
+      const int up = __shfl_up(B, 1, 64);
+      const int prevB = lane == 0 ? last : up;
+      const int diff = B - prevB;
+      int md = lane < stop ? diff : INT_MIN;
+      for (int o = 32; o > 0; o >>= 1) md = max(md, __shfl_xor(md, o, 64));
+      if (md > maxDiff) maxDiff = md;  // `if (diff >= maxDiff) maxDiff = diff`
+      if (stop < 64) {
+        if (lane == 0) {
+          result = (d0 + stop) < maxDepth ? maxDiff : 0;
+          done_flag = 1;
+        }
+      } else {
+        carry_acc += tot;
+        last = __shfl(B, 63, 64);
+      }
+    }
+    __syncthreads();
+    if (done_flag) break;
+  }
+  if (threadIdx.x == 0) *out = done_flag ? result : 0;
+}
+
+void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable* table,
+                           const Rect* masks, const int32_t* mask_active, int mask_index,
+                           int32_t* peaks, int count, hipStream_t st, int nangles,
+                           int max_scan) {
+  if (g.nedges <= 0 || nangles <= 0) return;
+  dim3 grid(nangles, g.nedges, count);
+  const size_t lds = sizeof(int32_t) * 2 * (size_t)(max_scan > 0 ? max_scan : 1);
+  if (lds > 64 * 1024) {
+    hipFuncSetAttribute((const void*)k_rot_peaks<F_GRAY8>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void*)k_rot_peaks<F_Y400A>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void*)k_rot_peaks<F_RGB24>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  }
+  switch (img.P.fmt) {
+    case F_GRAY8:
+      hipLaunchKernelGGL(k_rot_peaks<F_GRAY8>, grid, dim3(256), lds, st, img, g, table, masks,
+                         mask_active, mask_index, peaks);
+      break;
+    case F_Y400A:
+      hipLaunchKernelGGL(k_rot_peaks<F_Y400A>, grid, dim3(256), lds, st, img, g, table, masks,
+                         mask_active, mask_index, peaks);
+      break;
+    default:
+      hipLaunchKernelGGL(k_rot_peaks<F_RGB24>, grid, dim3(256), lds, st, img, g, table, masks,
+                         mask_active, mask_index, peaks);
+      break;
+  }
+}
+
+}  // namespace uph
+
+namespace uph {
+
+int rotation_angles(const UphipDeskewParameters& p, RotTable* t) {
+  // for (rotation = 0.0; rotation <= range; rotation = (rotation >= 0.0) ?
+  //      -(rotation + step) : -rotation)   (deskew.c:158-160), m = tanf (:161)
+  int n = 0;
+  for (float r = 0.0; r <= p.deskewScanRangeRad;
+       r = (r >= 0.0) ? -(r + p.deskewScanStepRad) : -r) {
+    if (n >= kMaxAngles) return -1;
+    t->angle[n] = r;
+    t->slope[n] = tanf(r);
+    n++;
+  }
+  t->nangles = n;
+  return n;
+}
+
+float combine_edge_rotations(const float* rotation, int count, float deviation_rad) {
+  // detect_rotation_cpu, deskew.c:219-240
+  float total = 0.0;
+  for (int i = 0; i < count; i++) total += rotation[i];
+  float average = total / count;
+  total = 0.0;
+  // glibc powf through a pointer, as the reference's default -O0 build calls
+  // it (an optimising compiler would fold powf(x, 2) into x*x)
+  static float (*volatile pw)(float, float) = powf;
+  for (int i = 0; i < count; i++) total += pw(rotation[i] - average, 2);
+  float deviation = sqrtf(total);
+  return deviation <= deviation_rad ? average : 0.0f;
+}
+
+}  // namespace uph

@@ -1,0 +1,846 @@
+// kernels_filters.hip — grayfilter, blurfilter and noisefilter for gfx950.
+//
+// All three are raster-order scans in the reference whose later decisions can
+// depend on earlier writes.  Each is split into (1) one streaming pass that
+// computes every decision input in parallel on the unmodified image and (2) an
+// exact resolution of the order dependence on small per-sheet data, proven
+// equivalent to the sequential scan (DESIGN.md §Order-dependent scans).
+#include <climits>
+
+#include "filters.h"
+
+namespace uph {
+
+__host__ __device__ static inline int32_t gcd_i(int32_t a, int32_t b) {
+  a = a < 0 ? -a : a;
+  b = b < 0 ? -b : b;
+  while (b) {
+    int32_t t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+template <int FMT>
+__device__ __forceinline__ void white_px(uint8_t* row, int32_t x) {
+  store_px_row<FMT>(row, x, Px{255, 255, 255});
+}
+
+// =========================================================================
+// GRAYFILTER (filters.c:370-402)
+//   tile T at (i*sx, j*sy), visited x-fastest for x = 0.. first x >= W and
+//   y = 0.. <= H.  T is wiped iff it holds no pixel with gray <= black_thr and
+//   255 - lightness_sum/count(clip T) < abs_thr, evaluated on the image as
+//   left by the wipes of EARLIER tiles.  A wipe never changes a dark count
+//   (wiped tiles had none) and only raises lightness, so T's predicate is
+//   monotone in the set of earlier wipes.  The exact result is the unique
+//   fixed point of "wiped(T) = pred(T, {earlier wiped})", reached by Jacobi
+//   iteration from the tiles that pass on the original image.
+// =========================================================================
+bool gray_geometry(int32_t W, int32_t H, const UphipGrayfilterParameters& p, uint8_t black_thr,
+                   GrayGeom* g) {
+  if (p.scan_size.width <= 0 || p.scan_size.height <= 0 || p.scan_step.horizontal <= 0 ||
+      p.scan_step.vertical <= 0)
+    return false;
+  g->W = W;
+  g->H = H;
+  g->scan_w = p.scan_size.width;
+  g->scan_h = p.scan_size.height;
+  g->step_x = p.scan_step.horizontal;
+  g->step_y = p.scan_step.vertical;
+  g->cw = gcd_i(g->step_x, g->scan_w);
+  g->ch = gcd_i(g->step_y, g->scan_h);
+  g->ncx = (W + g->cw - 1) / g->cw;
+  g->ncy = (H + g->ch - 1) / g->ch;
+  g->tw = g->scan_w / g->cw;
+  g->th = g->scan_h / g->ch;
+  g->tsx = g->step_x / g->cw;
+  g->tsy = g->step_y / g->ch;
+  // x = 0, sx, ... up to and including the first value >= W (filters.c:392-399)
+  g->ntx = (W + g->step_x - 1) / g->step_x + 1;
+  g->nty = H / g->step_y + 1;  // y = 0.. <= H
+  g->black_thr = black_thr;
+  g->abs_thr = p.abs_threshold;
+  return true;
+}
+
+size_t gray_scratch_bytes(const GrayGeom& g) {
+  const size_t cells = (size_t)g.ncx * g.ncy;
+  const size_t tiles = (size_t)g.ntx * g.nty;
+  size_t b = cells * 8 + tiles + cells;  // dark+light (2 x u32), tile state, cell wipe
+  return (b + 255) & ~(size_t)255;
+}
+
+struct GrayPtrs {
+  uint32_t* dark;
+  uint32_t* light;
+  uint8_t* tile;
+  uint8_t* cellw;
+};
+__device__ __forceinline__ GrayPtrs gray_ptrs(const GrayGeom& g, uint8_t* base) {
+  const size_t cells = (size_t)g.ncx * g.ncy;
+  const size_t tiles = (size_t)g.ntx * g.nty;
+  GrayPtrs p;
+  p.dark = (uint32_t*)base;
+  p.light = p.dark + cells;
+  p.tile = (uint8_t*)(p.light + cells);
+  p.cellw = p.tile + tiles;
+  return p;
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(256) k_gray_cells(PlaneRef img, GrayGeom g, uint8_t* scratch,
+                                                    int64_t sstride, const int32_t* active) {
+  const int s = blockIdx.z;
+  if (active && !active[s]) return;
+  const int32_t cx = blockIdx.x * 256 + threadIdx.x, cy = blockIdx.y;
+  if (cx >= g.ncx) return;
+  GrayPtrs P = gray_ptrs(g, scratch + s * sstride);
+  const uint8_t* base = plane_ptr(img, s);
+  const int32_t x0 = cx * g.cw, x1 = imin(x0 + g.cw, g.W);
+  const int32_t y0 = cy * g.ch, y1 = imin(y0 + g.ch, g.H);
+  uint32_t dark = 0, light = 0;
+  for (int32_t y = y0; y < y1; y++) {
+    const uint8_t* row = base + (int64_t)y * img.P.pitch;
+    for (int32_t x = x0; x < x1; x++) {
+      Px p = load_px_row<FMT>(row, x);
+      dark += gray_of(p) <= g.black_thr ? 1u : 0u;
+      light += light_of(p);
+    }
+  }
+  const size_t c = (size_t)cy * g.ncx + cx;
+  P.dark[c] = dark;
+  P.light[c] = light;
+}
+
+__device__ __forceinline__ uint32_t cell_pixels(const GrayGeom& g, int32_t cx, int32_t cy) {
+  const int32_t w = imin((cx + 1) * g.cw, g.W) - cx * g.cw;
+  const int32_t h = imin((cy + 1) * g.ch, g.H) - cy * g.ch;
+  return (w > 0 && h > 0) ? (uint32_t)(w * h) : 0u;
+}
+
+// inverse_lightness_rect of tile (tx,ty) with wiped cells reading 255.
+// mode 0: original image; mode 1: cells covered by an EARLIER wiped tile are white.
+__device__ uint8_t gray_tile_inv(const GrayGeom& g, const GrayPtrs& P, int32_t tx, int32_t ty,
+                                 int mode) {
+  const Rect r = clip(rect_from_size(tx * g.step_x, ty * g.step_y, g.scan_w, g.scan_h), g.W, g.H);
+  const uint64_t count = count_pixels(r);
+  uint64_t sum = 0;
+  const int32_t cx0 = tx * g.tsx, cy0 = ty * g.tsy;
+  for (int32_t j = 0; j < g.th; j++) {
+    const int32_t cy = cy0 + j;
+    if (cy >= g.ncy) break;
+    for (int32_t i = 0; i < g.tw; i++) {
+      const int32_t cx = cx0 + i;
+      if (cx >= g.ncx) break;
+      const size_t c = (size_t)cy * g.ncx + cx;
+      bool white = false;
+      if (mode) {
+        // tiles covering cell (cx,cy) that precede (tx,ty) and are wiped
+        for (int32_t oy = cy - g.th + 1; oy <= cy && !white; oy++) {
+          if (oy < 0 || oy % g.tsy) continue;
+          const int32_t uy = oy / g.tsy;
+          if (uy >= g.nty || uy > ty) continue;
+          for (int32_t ox = cx - g.tw + 1; ox <= cx; ox++) {
+            if (ox < 0 || ox % g.tsx) continue;
+            const int32_t ux = ox / g.tsx;
+            if (ux >= g.ntx) continue;
+            if (uy == ty && ux >= tx) continue;
+            if (P.tile[(size_t)uy * g.ntx + ux] == 2) {
+              white = true;
+              break;
+            }
+          }
+        }
+      }
+      sum += white ? 255u * cell_pixels(g, cx, cy) : P.light[c];
+    }
+  }
+  if (r.x1 < r.x0 || r.y1 < r.y0) sum = 0;  // loop body never runs
+  return (uint8_t)(0xFFull - sum / count);
+}
+
+__global__ void __launch_bounds__(1024) k_gray_decide(GrayGeom g, uint8_t* scratch, int64_t sstride,
+                                                      const int32_t* active) {
+  const int s = blockIdx.x;
+  if (active && !active[s]) return;
+  GrayPtrs P = gray_ptrs(g, scratch + s * sstride);
+  const int32_t ntiles = g.ntx * g.nty;
+  __shared__ int32_t undecided, changed;
+  if (threadIdx.x == 0) undecided = 0;
+  __syncthreads();
+  // 0 = never, 1 = undecided, 2 = wiped, 3 = newly wiped (this pass)
+  for (int32_t t = threadIdx.x; t < ntiles; t += blockDim.x) {
+    const int32_t tx = t % g.ntx, ty = t / g.ntx;
+    uint32_t dark = 0;
+    for (int32_t j = 0; j < g.th; j++) {
+      const int32_t cy = ty * g.tsy + j;
+      if (cy >= g.ncy) break;
+      for (int32_t i = 0; i < g.tw; i++) {
+        const int32_t cx = tx * g.tsx + i;
+        if (cx >= g.ncx) break;
+        dark += P.dark[(size_t)cy * g.ncx + cx];
+      }
+    }
+    uint8_t st = 0;
+    if (dark == 0) {
+      st = gray_tile_inv(g, P, tx, ty, 0) < g.abs_thr ? 2 : 1;
+      if (st == 1) atomicAdd(&undecided, 1);
+    }
+    P.tile[t] = st;
+  }
+  __syncthreads();
+  if (undecided) {
+    for (int iter = 0; iter < ntiles + 1; iter++) {
+      if (threadIdx.x == 0) changed = 0;
+      __syncthreads();
+      for (int32_t t = threadIdx.x; t < ntiles; t += blockDim.x) {
+        if (P.tile[t] != 1) continue;
+        const int32_t tx = t % g.ntx, ty = t / g.ntx;
+        if (gray_tile_inv(g, P, tx, ty, 1) < g.abs_thr) {
+          P.tile[t] = 3;
+          changed = 1;
+        }
+      }
+      __threadfence_block();
+      __syncthreads();
+      if (!changed) break;
+      for (int32_t t = threadIdx.x; t < ntiles; t += blockDim.x)
+        if (P.tile[t] == 3) P.tile[t] = 2;
+      __threadfence_block();
+      __syncthreads();
+    }
+  }
+  // cell wipe flags: any covering tile wiped
+  const int32_t ncells = g.ncx * g.ncy;
+  for (int32_t c = threadIdx.x; c < ncells; c += blockDim.x) {
+    const int32_t cx = c % g.ncx, cy = c / g.ncx;
+    uint8_t w = 0;
+    for (int32_t oy = cy - g.th + 1; oy <= cy && !w; oy++) {
+      if (oy < 0 || oy % g.tsy) continue;
+      const int32_t uy = oy / g.tsy;
+      if (uy >= g.nty) continue;
+      for (int32_t ox = cx - g.tw + 1; ox <= cx; ox++) {
+        if (ox < 0 || ox % g.tsx) continue;
+        const int32_t ux = ox / g.tsx;
+        if (ux >= g.ntx) continue;
+        if (P.tile[(size_t)uy * g.ntx + ux] == 2) {
+          w = 1;
+          break;
+        }
+      }
+    }
+    P.cellw[c] = w;
+  }
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(256) k_gray_wipe(PlaneRef img, GrayGeom g, uint8_t* scratch,
+                                                   int64_t sstride, const int32_t* active) {
+  const int s = blockIdx.z;
+  if (active && !active[s]) return;
+  const int32_t cx = blockIdx.x * 256 + threadIdx.x, cy = blockIdx.y;
+  if (cx >= g.ncx) return;
+  GrayPtrs P = gray_ptrs(g, scratch + s * sstride);
+  if (!P.cellw[(size_t)cy * g.ncx + cx]) return;
+  uint8_t* base = plane_ptr(img, s);
+  const int32_t x0 = cx * g.cw, x1 = imin(x0 + g.cw, g.W);
+  const int32_t y0 = cy * g.ch, y1 = imin(y0 + g.ch, g.H);
+  for (int32_t y = y0; y < y1; y++) {
+    uint8_t* row = base + (int64_t)y * img.P.pitch;
+    for (int32_t x = x0; x < x1; x++) white_px<FMT>(row, x);
+  }
+}
+
+template <int FMT>
+static void launch_gray_t(const PlaneRef& img, const GrayGeom& g, uint8_t* scr, int64_t ss,
+                          const int32_t* active, int count, hipStream_t st) {
+  dim3 grid((g.ncx + 255) / 256, g.ncy, count);
+  hipLaunchKernelGGL(k_gray_cells<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active);
+  hipLaunchKernelGGL(k_gray_decide, dim3(count), dim3(1024), 0, st, g, scr, ss, active);
+  hipLaunchKernelGGL(k_gray_wipe<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active);
+}
+
+void launch_grayfilter(const PlaneRef& img, const GrayGeom& g, void* scratch,
+                       int64_t scratch_stride, const int32_t* active, int count, hipStream_t st) {
+  uint8_t* scr = (uint8_t*)scratch;
+  switch (img.P.fmt) {
+    case F_GRAY8: launch_gray_t<F_GRAY8>(img, g, scr, scratch_stride, active, count, st); break;
+    case F_Y400A: launch_gray_t<F_Y400A>(img, g, scr, scratch_stride, active, count, st); break;
+    default: launch_gray_t<F_RGB24>(img, g, scr, scratch_stride, active, count, st); break;
+  }
+}
+
+// =========================================================================
+// BLURFILTER (filters.c:149-232)
+//   Every count the reference takes is of the unmodified image (no wipe ever
+//   overlaps a rectangle counted later), so all counts are computed in
+//   parallel; the reference's three count rows are pointers into ONE row of
+//   its VLA at offsets 0/1/2 that rotate every row, so the wipe decisions are
+//   the literal pointer recurrence replayed by one lane over those counts.
+//   The slot read before it is written (prev[0] on the first row, an
+//   uninitialised stack value in the reference) is 0 here.
+// =========================================================================
+bool blur_geometry(int32_t W, int32_t H, const UphipBlurfilterParameters& p, uint8_t white,
+                   BlurGeom* g) {
+  if (p.scan_size.width <= 0 || p.scan_size.height <= 0) return false;
+  g->W = W;
+  g->H = H;
+  g->sw = p.scan_size.width;
+  g->sh = p.scan_size.height;
+  g->step_y = p.scan_step.vertical;
+  g->bpr = (int32_t)((uint32_t)(W / g->sw));
+  g->T = H >= g->sh ? (H - g->sh) / g->sh + 1 : 0;
+  g->nrect = g->bpr + g->T * (g->bpr + 1);
+  g->white = white;
+  g->intensity = p.intensity;
+  return true;
+}
+
+size_t blur_scratch_bytes(const BlurGeom& g) {
+  size_t b = (size_t)g.nrect * 4 + (size_t)g.T * (g.bpr > 0 ? g.bpr : 1);
+  return (b + 255) & ~(size_t)255;
+}
+
+__device__ __forceinline__ void blur_rect_origin(const BlurGeom& g, int32_t r, int32_t* x,
+                                                 int32_t* y) {
+  if (r < g.bpr) {
+    *x = r * g.sw;
+    *y = 0;
+  } else {
+    const int32_t q = r - g.bpr, t = q / (g.bpr + 1), j = q % (g.bpr + 1);
+    *x = j * g.sw;
+    *y = t * g.sh + g.step_y;
+  }
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(256) k_blur_counts(PlaneRef img, BlurGeom g, uint8_t* scratch,
+                                                     int64_t sstride, const int32_t* active) {
+  const int s = blockIdx.y;
+  if (active && !active[s]) return;
+  const int32_t r = blockIdx.x;
+  int32_t rx, ry;
+  blur_rect_origin(g, r, &rx, &ry);
+  const uint8_t* base = plane_ptr(img, s);
+  // count_pixels_within_brightness(0, white): unclipped, outside = white
+  const int32_t x0 = imax(rx, 0), x1 = imin(rx + g.sw - 1, g.W - 1);
+  const int32_t y0 = imax(ry, 0), y1 = imin(ry + g.sh - 1, g.H - 1);
+  uint32_t acc = 0;
+  if (x0 <= x1 && y0 <= y1) {
+    const int32_t w = x1 - x0 + 1;
+    const int32_t n = w * (y1 - y0 + 1);
+    for (int32_t i = threadIdx.x; i < n; i += 256) {
+      const int32_t yy = y0 + i / w, xx = x0 + i % w;
+      acc += gray_of(load_px_row<FMT>(base + (int64_t)yy * img.P.pitch, xx)) <= g.white ? 1u : 0u;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+  __shared__ uint32_t red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t* counts = (uint32_t*)(scratch + s * sstride);
+    counts[r] = red[0] + red[1] + red[2] + red[3];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_blur_resolve(BlurGeom g, uint8_t* scratch, int64_t sstride,
+                                                      const int32_t* active) {
+  const int s = blockIdx.x;
+  if (active && !active[s]) return;
+  const uint32_t* counts = (const uint32_t*)(scratch + s * sstride);
+  uint8_t* wipe = scratch + s * sstride + (size_t)g.nrect * 4;
+  extern __shared__ uint64_t sh[];  // [nrect] counts + [3*(bpr+2)] buffers
+  uint64_t* cnt = sh;
+  uint64_t* buf = sh + g.nrect;
+  const int32_t nbuf = 3 * (g.bpr + 2);
+  for (int32_t i = threadIdx.x; i < g.nrect; i += blockDim.x) cnt[i] = counts[i];
+  for (int32_t i = threadIdx.x; i < nbuf; i += blockDim.x) buf[i] = 0;
+  for (int32_t i = threadIdx.x; i < g.T * g.bpr; i += blockDim.x) wipe[i] = 0;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const uint64_t total = (uint64_t)(g.sw * g.sh);
+  const int32_t bpr = g.bpr;
+  int32_t op = 0, oc = 1, on = 2;  // prev / cur / next offsets into buf
+  buf[oc + 0] = total;
+  buf[oc + bpr] = total;
+  buf[on + 0] = total;
+  buf[on + bpr] = total;
+  for (int32_t b = 0; b < bpr; b++) buf[oc + 1 + b] = cnt[b];
+  for (int32_t t = 0; t < g.T; t++) {
+    const int32_t base = bpr + t * (bpr + 1);
+    buf[on + 0] = cnt[base + 0];
+    for (int32_t block = 1; block <= bpr; block++) {
+      buf[on + block + 1] = cnt[base + block];
+      const uint64_t a = buf[op + block - 1], b = buf[op + block + 1], c = buf[oc + block];
+      const uint64_t m1 = a > b ? (a > c ? a : c) : (b > c ? b : c);
+      const uint64_t d = buf[on + block - 1], e = buf[on + block + 1];
+      const uint64_t mx = d > e ? (d > m1 ? d : m1) : (e > m1 ? e : m1);
+      if ((((float)mx) / total) <= g.intensity) {
+        wipe[t * bpr + block - 1] = 1;
+        buf[oc + block] = total;
+      }
+    }
+    const int32_t tmp = op;
+    op = oc;
+    oc = on;
+    on = tmp;
+  }
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(256) k_blur_wipe(PlaneRef img, BlurGeom g, uint8_t* scratch,
+                                                   int64_t sstride, const int32_t* active) {
+  const int s = blockIdx.y;
+  if (active && !active[s]) return;
+  const int32_t b = blockIdx.x;  // t*bpr + j
+  const uint8_t* wipe = scratch + s * sstride + (size_t)g.nrect * 4;
+  if (!wipe[b]) return;
+  const int32_t t = b / g.bpr, j = b % g.bpr;
+  const Rect r = clip(rect_from_size(j * g.sw, t * g.sh, g.sw, g.sh), g.W, g.H);
+  uint8_t* base = plane_ptr(img, s);
+  const int32_t w = r.x1 - r.x0 + 1;
+  if (w <= 0 || r.y1 < r.y0) return;
+  const int32_t n = w * (r.y1 - r.y0 + 1);
+  for (int32_t i = threadIdx.x; i < n; i += 256) {
+    const int32_t yy = r.y0 + i / w, xx = r.x0 + i % w;
+    white_px<FMT>(base + (int64_t)yy * img.P.pitch, xx);
+  }
+}
+
+template <int FMT>
+static void launch_blur_t(const PlaneRef& img, const BlurGeom& g, uint8_t* scr, int64_t ss,
+                          const int32_t* active, int count, hipStream_t st) {
+  if (g.nrect > 0)
+    hipLaunchKernelGGL(k_blur_counts<FMT>, dim3(g.nrect, count), dim3(256), 0, st, img, g, scr, ss,
+                       active);
+  const size_t lds = sizeof(uint64_t) * ((size_t)g.nrect + 3 * (size_t)(g.bpr + 2));
+  hipLaunchKernelGGL(k_blur_resolve, dim3(count), dim3(256), lds, st, g, scr, ss, active);
+  if (g.T * g.bpr > 0)
+    hipLaunchKernelGGL(k_blur_wipe<FMT>, dim3(g.T * g.bpr, count), dim3(256), 0, st, img, g, scr,
+                       ss, active);
+}
+
+void launch_blurfilter(const PlaneRef& img, const BlurGeom& g, void* scratch,
+                       int64_t scratch_stride, const int32_t* active, int count, hipStream_t st) {
+  uint8_t* scr = (uint8_t*)scratch;
+  switch (img.P.fmt) {
+    case F_GRAY8: launch_blur_t<F_GRAY8>(img, g, scr, scratch_stride, active, count, st); break;
+    case F_Y400A: launch_blur_t<F_Y400A>(img, g, scr, scratch_stride, active, count, st); break;
+    default: launch_blur_t<F_RGB24>(img, g, scr, scratch_stride, active, count, st); break;
+  }
+}
+
+// =========================================================================
+// NOISEFILTER (filters.c:238-338)
+//   Raster scan; a pixel p with max(rgb) < white ("trigger") counts the
+//   pixels with min(rgb) < white ("dark") in square rings of level 1..N
+//   (N = intensity) until a ring is empty; if 1 + rings <= N the centre and
+//   the counted rings are cleared.  Away from the left/top edge (where the
+//   ring loops' unsigned comparisons drop whole rows, see oracle.c) an empty
+//   ring separates its inside from everything else, so a clear removes whole
+//   8-connected dark components of <= N pixels ("small").  Hence:
+//     * triggers of large components outside the edge zone never clear;
+//     * a small component C farther than 2N-1 from any other small pixel and
+//       from the edge zone is cleared iff one of its triggers passes the test
+//       on the ORIGINAL image (nothing that test reads ever changes);
+//     * everything else (edge zone, clustered small components) is replayed
+//       literally, in raster order, by one wave per sheet.
+//   The parallel path is used for N <= 4 (radius constants below).
+// =========================================================================
+constexpr int kNT = 64;                    // tile edge
+constexpr int kHalo = 14;                  // 4 (ring) + 7 (cluster) + 3 (component)
+constexpr int kRW = kNT + 2 * kHalo;       // 92
+constexpr int kZone = 32;                  // sequential edge zone (x or y < 32)
+constexpr int kEligible = kZone + 8;       // parallel only for components at >= 40
+
+bool noise_geometry(int32_t W, int32_t H, uint64_t intensity, uint8_t white, NoiseGeom* g) {
+  g->W = W;
+  g->H = H;
+  g->intensity = intensity > 64 ? 64 : (int32_t)intensity;
+  g->white = white;
+  // the parallel path only queues edge-zone and clustered triggers; the
+  // all-sequential path (intensity > 4) may queue every pixel
+  g->all_seq = intensity > 4 ? 1 : 0;
+  int64_t cap = g->all_seq ? (int64_t)W * H + 64 : ((int64_t)W * H) / 4 + 1024;
+  if (cap > (1 << 27)) cap = 1 << 27;
+  g->capacity = (int32_t)cap;
+  return true;
+}
+
+static size_t noise_list_bytes(const NoiseGeom& g) {
+  // counters (2 x u32 padded to 256 B) + clear list + seq list
+  size_t b = 256 + (size_t)g.capacity * 4 * 2;
+  return (b + 255) & ~(size_t)255;
+}
+
+static size_t pow2_at_least(size_t n) {
+  size_t p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+size_t noise_scratch_bytes(const NoiseGeom& g) {
+  // lists + a global sort buffer for the rare > 8192-trigger sequential case
+  return noise_list_bytes(g) + 4 * pow2_at_least((size_t)g.capacity);
+}
+
+struct NoisePtrs {
+  uint32_t* nclear;
+  uint32_t* nseq;
+  uint32_t* clear;
+  uint32_t* seq;
+};
+__device__ __forceinline__ NoisePtrs noise_ptrs(const NoiseGeom& g, uint8_t* base) {
+  NoisePtrs p;
+  p.nclear = (uint32_t*)base;
+  p.nseq = p.nclear + 1;
+  p.clear = (uint32_t*)(base + 256);
+  p.seq = p.clear + g.capacity;
+  return p;
+}
+
+// 9 bits of a region row bitmask starting at column c (bit i = column c+i)
+__device__ __forceinline__ uint32_t row9(const uint32_t* w, int c) {
+  const int word = c >> 5, off = c & 31;
+  uint64_t v = ((uint64_t)w[word + 1] << 32) | w[word];
+  return (uint32_t)(v >> off) & 0x1FFu;
+}
+
+// Dark component of (cx,cy) restricted to its 9x9 box; returns popcount
+// (capped growth after 4 dilations) and the mask rows.
+__device__ __forceinline__ int flood9(const uint32_t (*drow)[4], int cx, int cy, uint32_t* comp) {
+  uint32_t D[9], cur[9];
+#pragma unroll
+  for (int r = 0; r < 9; r++) {
+    D[r] = row9(drow[cy - 4 + r], cx - 4);
+    cur[r] = 0;
+  }
+  cur[4] = 1u << 4;
+  for (int it = 0; it < 4; it++) {
+    uint32_t nx[9];
+    bool same = true;
+#pragma unroll
+    for (int r = 0; r < 9; r++) {
+      uint32_t u = cur[r] | (r > 0 ? cur[r - 1] : 0) | (r < 8 ? cur[r + 1] : 0);
+      u = (u | (u << 1) | (u >> 1)) & D[r] & 0x1FFu;
+      nx[r] = u;
+      same &= (u == cur[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 9; r++) cur[r] = nx[r];
+    if (same) break;
+  }
+  int n = 0;
+#pragma unroll
+  for (int r = 0; r < 9; r++) {
+    comp[r] = cur[r];
+    n += __popc(cur[r]);
+  }
+  return n;
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom g, uint8_t* scratch,
+                                                        int64_t sstride, const int32_t* active,
+                                                        SheetCtl* ctl) {
+  const int s = blockIdx.z;
+  if (active && !active[s]) return;
+  const int32_t tx0 = blockIdx.x * kNT, ty0 = blockIdx.y * kNT;
+  const int32_t ox = tx0 - kHalo, oy = ty0 - kHalo;  // region origin
+  const uint8_t* base = plane_ptr(img, s);
+  NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
+  // bit0 dark (light < white), bit1 trigger (max < white), bit2 small
+  __shared__ uint8_t px[kRW * kRW];
+  __shared__ uint32_t drow[kRW][4];
+  __shared__ int32_t any_dark;
+  if (threadIdx.x == 0) any_dark = 0;
+  for (int i = threadIdx.x; i < kRW * 4; i += 256) drow[i >> 2][i & 3] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < kRW * kRW; i += 256) {
+    const int ry = i / kRW, rx = i % kRW;
+    const int32_t gx = ox + rx, gy = oy + ry;
+    uint8_t f = 0;
+    if (gx >= 0 && gy >= 0 && gx < g.W && gy < g.H) {
+      Px p = load_px_row<FMT>(base + (int64_t)gy * img.P.pitch, gx);
+      if (light_of(p) < g.white) f |= 1;
+      if (dark_of(p) < g.white) f |= 2;
+    }
+    px[i] = f;
+    if (f & 1) {
+      atomicOr(&drow[ry][rx >> 5], 1u << (rx & 31));
+      if (rx >= kHalo && rx < kHalo + kNT && ry >= kHalo && ry < kHalo + kNT) any_dark = 1;
+    }
+  }
+  __syncthreads();
+  if (!any_dark) return;
+  // small flags within radius 10 of the tile: region [4, 88)
+  for (int i = threadIdx.x; i < 84 * 84; i += 256) {
+    const int ry = 4 + i / 84, rx = 4 + i % 84;
+    if (!(px[ry * kRW + rx] & 1)) continue;
+    uint32_t comp[9];
+    if (flood9(drow, rx, ry, comp) <= 4) px[ry * kRW + rx] |= 4;
+  }
+  __syncthreads();
+  const int N = g.intensity;
+  for (int i = threadIdx.x; i < kNT * kNT; i += 256) {
+    const int ry = kHalo + i / kNT, rx = kHalo + i % kNT;
+    const int32_t gx = ox + rx, gy = oy + ry;
+    const uint8_t f = px[ry * kRW + rx];
+    if (!(f & 1)) continue;
+    if (g.all_seq || gx < kZone || gy < kZone) {
+      if (f & 2) {
+        uint32_t k = atomicAdd(NP.nseq, 1u);
+        if (k < (uint32_t)g.capacity) NP.seq[k] = ((uint32_t)gy << 16) | (uint32_t)gx;
+      }
+      continue;
+    }
+    if (!(f & 4)) continue;  // large component: never cleared
+    uint32_t comp[9];
+    flood9(drow, rx, ry, comp);
+    // component pixels (<= 4), relative to (rx, ry)
+    int cxs[4], cys[4], nc = 0;
+    bool eligible = true;
+    for (int r = 0; r < 9; r++)
+      for (int b = 0; b < 9; b++)
+        if (comp[r] >> b & 1) {
+          if (nc < 4) {
+            cxs[nc] = b - 4;
+            cys[nc] = r - 4;
+          }
+          nc++;
+          if (gx + b - 4 < kEligible || gy + r - 4 < kEligible) eligible = false;
+        }
+    if (nc > 4) eligible = false;  // cannot happen (small)
+    // no foreign small pixel within Chebyshev 7 of the component
+    for (int dy = -10; dy <= 10 && eligible; dy++)
+      for (int dx = -10; dx <= 10; dx++) {
+        const uint8_t q = px[(ry + dy) * kRW + rx + dx];
+        if (!(q & 4)) continue;
+        bool mine = false, near = false;
+        for (int k = 0; k < nc; k++) {
+          if (cxs[k] == dx && cys[k] == dy) mine = true;
+          if (iabs(cxs[k] - dx) <= 7 && iabs(cys[k] - dy) <= 7) near = true;
+        }
+        if (!mine && near) {
+          eligible = false;
+          break;
+        }
+      }
+    if (!eligible) {
+      if (f & 2) {
+        uint32_t k = atomicAdd(NP.nseq, 1u);
+        if (k < (uint32_t)g.capacity) NP.seq[k] = ((uint32_t)gy << 16) | (uint32_t)gx;
+      }
+      continue;
+    }
+    // cleared iff some trigger of the component passes the ring test
+    bool clear = false;
+    for (int k = 0; k < nc && !clear; k++) {
+      const int cx = rx + cxs[k], cy = ry + cys[k];
+      if (!(px[cy * kRW + cx] & 2)) continue;
+      int count = 1, lc;
+      int level = 1;
+      do {
+        lc = 0;
+        for (int d = -level; d <= level; d++) {
+          lc += px[(cy - level) * kRW + cx + d] & 1;
+          lc += px[(cy + level) * kRW + cx + d] & 1;
+        }
+        for (int d = -(level - 1); d <= level - 1; d++) {
+          lc += px[(cy + d) * kRW + cx - level] & 1;
+          lc += px[(cy + d) * kRW + cx + level] & 1;
+        }
+        count += lc;
+        level++;
+      } while (lc != 0 && level <= N);
+      clear = count <= N;
+    }
+    if (clear) {
+      uint32_t k = atomicAdd(NP.nclear, 1u);
+      if (k < (uint32_t)g.capacity) NP.clear[k] = ((uint32_t)gy << 16) | (uint32_t)gx;
+    }
+  }
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(256) k_noise_apply(PlaneRef img, NoiseGeom g, uint8_t* scratch,
+                                                     int64_t sstride, const int32_t* active,
+                                                     SheetCtl* ctl) {
+  const int s = blockIdx.y;
+  if (active && !active[s]) return;
+  NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
+  const uint32_t n = *NP.nclear;
+  if (n > (uint32_t)g.capacity) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && ctl) atomicOr(&ctl[s].status, STATUS_NOISE_OVERFLOW);
+    return;
+  }
+  uint8_t* base = plane_ptr(img, s);
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const uint32_t k = NP.clear[i];
+    white_px<FMT>(base + (int64_t)(k >> 16) * img.P.pitch, (int32_t)(k & 0xFFFF));
+  }
+}
+
+// In-LDS / in-global bitonic sort of n uint32 keys by one 256-thread block.
+__device__ void block_sort(uint32_t* a, int n_pow2) {
+  for (int k = 2; k <= n_pow2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n_pow2; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const uint32_t x = a[i], y = a[l];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) {
+            a[i] = y;
+            a[l] = x;
+          }
+        }
+      }
+      __threadfence_block();
+      __syncthreads();
+    }
+  }
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(256) k_noise_resolve(PlaneRef img, NoiseGeom g, uint8_t* scratch,
+                                                       int64_t sstride, const int32_t* active,
+                                                       SheetCtl* ctl, uint32_t* sortbuf,
+                                                       int64_t sort_stride) {
+  const int s = blockIdx.x;
+  if (active && !active[s]) return;
+  NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
+  uint32_t n = *NP.nseq;
+  if (n == 0) return;
+  if (n > (uint32_t)g.capacity) {
+    if (threadIdx.x == 0 && ctl) atomicOr(&ctl[s].status, STATUS_NOISE_OVERFLOW);
+    return;
+  }
+  int p2 = 1;
+  while (p2 < (int)n) p2 <<= 1;
+  __shared__ uint32_t lk[8192];
+  uint32_t* keys;
+  if (p2 <= 8192) {
+    keys = lk;
+  } else {
+    keys = sortbuf + s * sort_stride;  // global fallback (rare: dark edge zones)
+  }
+  for (int i = threadIdx.x; i < p2; i += blockDim.x) keys[i] = i < (int)n ? NP.seq[i] : 0xFFFFFFFFu;
+  __threadfence_block();
+  __syncthreads();
+  block_sort(keys, p2);
+  if (threadIdx.x >= 64) return;
+  // one wave replays the raster scan over the sorted triggers
+  const int lane = threadIdx.x;
+  const int N = g.intensity;
+  const int R = N;                       // box radius
+  const int side = 2 * R + 1, area = side * side;
+  uint8_t* base = plane_ptr(img, s);
+  const int64_t pitch = img.P.pitch;
+  for (uint32_t idx = 0; idx < n; idx++) {
+    const uint32_t key = keys[idx];
+    const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
+    __threadfence_block();
+    const Px cp = load_px_row<FMT>(base + (int64_t)y * pitch, x);
+    if (!(dark_of(cp) < g.white)) continue;  // cleared meanwhile
+    // ring counts with the reference loops' unsigned-comparison semantics:
+    // rows +-L counted iff x >= L, columns +-L (|dy| < L) counted iff y >= L-1
+    int cnt[65];
+    for (int L = 0; L <= R; L++) cnt[L] = 0;
+    for (int b = 0; b < area; b += 64) {
+      const int pos = b + lane;
+      int L = 0;
+      bool dark = false;
+      if (pos < area) {
+        const int dx = pos % side - R, dy = pos / side - R;
+        const int adx = iabs(dx), ady = iabs(dy);
+        L = imax(adx, ady);
+        bool member = L > 0 && ((ady == L && x >= L) || (ady < L && adx == L && y >= L - 1));
+        if (member) {
+          const int32_t qx = x + dx, qy = y + dy;
+          if (qx >= 0 && qy >= 0 && qx < g.W && qy < g.H)
+            dark = light_of(load_px_row<FMT>(base + (int64_t)qy * pitch, qx)) < g.white;
+        }
+      }
+      for (int l = 1; l <= R; l++) cnt[l] += __popcll(__ballot(dark && L == l));
+    }
+    int count = 1, k = 0, level = 1;
+    int lc;
+    do {
+      lc = cnt[level];
+      count += lc;
+      level++;
+    } while (lc != 0 && level <= N);
+    if (count > N) continue;
+    // rings 1..k-1 (the loop stopped at the first empty ring k) + centre
+    k = level - 1;  // the empty ring
+    if (lane == 0) white_px<FMT>(base + (int64_t)y * pitch, x);
+    for (int b = 0; b < area; b += 64) {
+      const int pos = b + lane;
+      if (pos >= area) continue;
+      const int dx = pos % side - R, dy = pos / side - R;
+      const int adx = iabs(dx), ady = iabs(dy);
+      const int L = imax(adx, ady);
+      if (L == 0 || L >= k) continue;
+      bool member = (ady == L && x >= L) || (ady < L && adx == L && y >= L - 1);
+      if (!member) continue;
+      const int32_t qx = x + dx, qy = y + dy;
+      if (qx < 0 || qy < 0 || qx >= g.W || qy >= g.H) continue;
+      uint8_t* row = base + (int64_t)qy * pitch;
+      if (light_of(load_px_row<FMT>(row, qx)) < g.white) white_px<FMT>(row, qx);
+    }
+    __threadfence_block();
+  }
+}
+
+__global__ void k_noise_zero(uint8_t* scr, int64_t stride, int count) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < count) {
+    uint32_t* c = (uint32_t*)(scr + s * stride);
+    c[0] = 0;
+    c[1] = 0;
+  }
+}
+
+template <int FMT>
+static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr, int64_t ss,
+                           const int32_t* active, SheetCtl* ctl, int count, hipStream_t st,
+                           uint32_t* sortbuf, int64_t sort_stride) {
+  dim3 grid((g.W + kNT - 1) / kNT, (g.H + kNT - 1) / kNT, count);
+  hipLaunchKernelGGL(k_noise_classify<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active, ctl);
+  hipLaunchKernelGGL(k_noise_apply<FMT>, dim3(64, count), dim3(256), 0, st, img, g, scr, ss,
+                     active, ctl);
+  hipLaunchKernelGGL(k_noise_resolve<FMT>, dim3(count), dim3(256), 0, st, img, g, scr, ss, active,
+                     ctl, sortbuf, sort_stride);
+}
+
+void launch_noisefilter(const PlaneRef& img, const NoiseGeom& g, void* scratch,
+                        int64_t scratch_stride, const int32_t* active, SheetCtl* ctl, int count,
+                        hipStream_t st) {
+  // layout of `scratch` per sheet: [noise lists][sort buffer (capacity pow2)]
+  uint8_t* scr = (uint8_t*)scratch;
+  const size_t lists = noise_list_bytes(g);
+  uint32_t* sortbuf = (uint32_t*)(scr + lists);
+  const int64_t sort_stride = scratch_stride / 4;
+  hipLaunchKernelGGL(k_noise_zero, dim3((count + 255) / 256), dim3(256), 0, st, scr,
+                     scratch_stride, count);
+  switch (img.P.fmt) {
+    case F_GRAY8:
+      launch_noise_t<F_GRAY8>(img, g, scr, scratch_stride, active, ctl, count, st, sortbuf,
+                              sort_stride);
+      break;
+    case F_Y400A:
+      launch_noise_t<F_Y400A>(img, g, scr, scratch_stride, active, ctl, count, st, sortbuf,
+                              sort_stride);
+      break;
+    default:
+      launch_noise_t<F_RGB24>(img, g, scr, scratch_stride, active, ctl, count, st, sortbuf,
+                              sort_stride);
+      break;
+  }
+}
+
+}  // namespace uph

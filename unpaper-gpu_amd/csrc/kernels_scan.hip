@@ -1,0 +1,267 @@
+// kernels_scan.hip — axis reductions and the sequential scans that consume
+// them: detect_edge / detect_mask (masks.c:54-209), detect_border_edge /
+// detect_border (masks.c:410-488).
+//
+// The reference evaluates every scan bar independently by re-reading its
+// 50 x H pixels (29 % of CPU time).  Here one streaming pass produces the
+// per-column (or per-row) sums over the bar's fixed extent; every bar sum is
+// then a sum of <= size entries from LDS, and the sequential stopping rule
+// becomes a block-wide prefix scan + first-failure search (bit-exact: integer
+// sums, the same float expression for the threshold test).
+#include <climits>
+
+#include "scan.h"
+
+namespace uph {
+
+constexpr int kRedThreads = 256;
+
+template <int FMT, int MEAS>
+__device__ __forceinline__ uint32_t measure(const uint8_t* row, int32_t x, uint8_t thr) {
+  Px p = load_px_row<FMT>(row, x);
+  if (MEAS == M_GRAY_SUM) return gray_of(p);
+  if (MEAS == M_DARK_COUNT) return gray_of(p) <= thr ? 1u : 0u;
+  if (MEAS == M_DARKINV_SUM) return dark_of(p);
+  return light_of(p);  // M_LIGHT_SUM
+}
+
+// axis 0 (column sums): threads own columns, blocks own (column tile, row
+// chunk); one atomic per column per block.
+template <int FMT, int MEAS>
+__global__ void __launch_bounds__(kRedThreads) k_colsum(PlaneRef ref, const AxisArgs* args,
+                                                        uint32_t* out, int64_t out_stride,
+                                                        int rows_per_block) {
+  const int s = blockIdx.z;
+  const AxisArgs a = args[s];
+  if (!a.active) return;
+  const Rect r = a.region;
+  const int32_t x = r.x0 + (int32_t)blockIdx.x * kRedThreads + (int32_t)threadIdx.x;
+  const int32_t y0 = r.y0 + (int32_t)blockIdx.y * rows_per_block;
+  if (r.x1 < r.x0 || x > r.x1 || y0 > r.y1) return;
+  const int32_t y1 = imin(r.y1, y0 + rows_per_block - 1);
+  const uint8_t* base = plane_ptr(ref, s);
+  const int64_t pitch = ref.P.pitch;
+  uint32_t acc = 0;
+  for (int32_t y = y0; y <= y1; y++)
+    acc += measure<FMT, MEAS>(base + (int64_t)y * pitch, x, a.thr);
+  if (acc) atomicAdd(out + (int64_t)s * out_stride + x, acc);
+}
+
+// axis 1 (row sums): a block per row (grid-strided), block reduction.
+template <int FMT, int MEAS>
+__global__ void __launch_bounds__(kRedThreads) k_rowsum(PlaneRef ref, const AxisArgs* args,
+                                                        uint32_t* out, int64_t out_stride) {
+  const int s = blockIdx.z;
+  const AxisArgs a = args[s];
+  if (!a.active) return;
+  const Rect r = a.region;
+  if (r.x1 < r.x0) return;
+  const uint8_t* base = plane_ptr(ref, s);
+  __shared__ uint32_t red[kRedThreads / 64];
+  for (int32_t y = r.y0 + (int32_t)blockIdx.x; y <= r.y1; y += gridDim.x) {
+    const uint8_t* row = base + (int64_t)y * ref.P.pitch;
+    uint32_t acc = 0;
+    for (int32_t x = r.x0 + (int32_t)threadIdx.x; x <= r.x1; x += kRedThreads)
+      acc += measure<FMT, MEAS>(row, x, a.thr);
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (int w = 0; w < kRedThreads / 64; w++) t += red[w];
+      out[(int64_t)s * out_stride + y] = t;
+    }
+    __syncthreads();
+  }
+}
+
+template <int FMT, int MEAS>
+static void launch_axis_t(const PlaneRef& ref, const AxisArgs* args, int axis, int32_t span_x,
+                          int32_t span_y, uint32_t* out, int64_t out_stride, int count,
+                          hipStream_t st) {
+  if (span_x <= 0 || span_y <= 0) return;
+  if (axis == 0) {
+    const int rpb = 64;
+    dim3 grid((span_x + kRedThreads - 1) / kRedThreads, (span_y + rpb - 1) / rpb, count);
+    hipLaunchKernelGGL((k_colsum<FMT, MEAS>), grid, dim3(kRedThreads), 0, st, ref, args, out,
+                       out_stride, rpb);
+  } else {
+    int gx = span_y > 2048 ? 2048 : span_y;
+    hipLaunchKernelGGL((k_rowsum<FMT, MEAS>), dim3(gx, 1, count), dim3(kRedThreads), 0, st, ref,
+                       args, out, out_stride);
+  }
+}
+
+template <int FMT>
+static void launch_axis_f(const PlaneRef& ref, const AxisArgs* args, int axis, int meas,
+                          int32_t sx, int32_t sy, uint32_t* out, int64_t os, int count,
+                          hipStream_t st) {
+  switch (meas) {
+    case M_GRAY_SUM:
+      launch_axis_t<FMT, M_GRAY_SUM>(ref, args, axis, sx, sy, out, os, count, st);
+      break;
+    case M_DARK_COUNT:
+      launch_axis_t<FMT, M_DARK_COUNT>(ref, args, axis, sx, sy, out, os, count, st);
+      break;
+    case M_DARKINV_SUM:
+      launch_axis_t<FMT, M_DARKINV_SUM>(ref, args, axis, sx, sy, out, os, count, st);
+      break;
+    default:
+      launch_axis_t<FMT, M_LIGHT_SUM>(ref, args, axis, sx, sy, out, os, count, st);
+      break;
+  }
+}
+
+void launch_axis_reduce(const PlaneRef& ref, const AxisArgs* args, int axis, int meas,
+                        int32_t span_x, int32_t span_y, uint32_t* out, int64_t out_stride,
+                        int count, hipStream_t st) {
+  // axis 0 accumulates with atomics: the caller zeroes `out` first.
+  switch (ref.P.fmt) {
+    case F_GRAY8:
+      launch_axis_f<F_GRAY8>(ref, args, axis, meas, span_x, span_y, out, out_stride, count, st);
+      break;
+    case F_Y400A:
+      launch_axis_f<F_Y400A>(ref, args, axis, meas, span_x, span_y, out, out_stride, count, st);
+      break;
+    default:
+      launch_axis_f<F_RGB24>(ref, args, axis, meas, span_x, span_y, out, out_stride, count, st);
+      break;
+  }
+}
+
+// Block-wide inclusive prefix sum of `v` (256 threads = 4 waves) plus a carry.
+__device__ __forceinline__ uint32_t block_prefix(uint32_t v, uint32_t carry, uint32_t* wsum) {
+  uint32_t pre = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t t = __shfl_up(pre, o, 64);
+    if ((threadIdx.x & 63) >= (unsigned)o) pre += t;
+  }
+  if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = pre;
+  __syncthreads();
+  uint32_t add = carry;
+  for (int w = 0; w < (int)(threadIdx.x >> 6); w++) add += wsum[w];
+  return pre + add;
+}
+
+// ---------------------------------------------------------------------------
+// detect_edge (masks.c:54-100) from precomputed sums S[] along the scan axis.
+//   bar k spans [b0 + k*step, b0 + k*step + size - 1] along the scan axis and
+//   [c0, c1] across it; blackness_k = 255 - sum_k / count_pixels(clip(bar_k))
+//   (count_pixels is |dx|+1 * |dy|+1 of the clipped, possibly inverted,
+//   rectangle; the sum is 0 when that rectangle is empty).  The reference loop
+//   runs k = 0,1,.. and continues while b_k >= (thr*total_k)/(k+1) && b_k != 0.
+//   Guard: a bar entirely outside the image stops the scan when thr <= 1 (the
+//   reference would loop forever there; DESIGN.md documents this).
+// ---------------------------------------------------------------------------
+constexpr int kMaxAxis = 16384;
+
+__global__ void __launch_bounds__(256) k_edge_scan(const EdgeArgs* args, const uint32_t* sums,
+                                                   int64_t sums_stride, int32_t* results) {
+  const int s = blockIdx.y;
+  const int job = blockIdx.x;
+  const int64_t slot = (int64_t)s * gridDim.x + job;
+  const EdgeArgs a = args[slot];
+  if (!a.active) return;
+  const uint32_t* S = sums + (int64_t)s * sums_stride + a.sums_offset;
+  __shared__ uint32_t lds[kMaxAxis];
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t carry;
+  __shared__ int32_t stop_k;
+  const int32_t n = a.extent;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) lds[i] = S[i];
+  if (threadIdx.x == 0) {
+    carry = 0;
+    stop_k = INT_MAX;
+  }
+  __syncthreads();
+  // cross extent, clipped (the loop body runs iff cc0 <= cc1)
+  const int32_t clo = imin(a.c0, a.c1), chi = imax(a.c0, a.c1);
+  const int32_t cc0 = imax(clo, 0), cc1 = imin(chi, a.cross_extent - 1);
+  const int32_t ccount = iabs(cc1 - cc0) + 1;
+  const bool cross_out = chi < 0 || clo >= a.cross_extent;
+  for (int32_t kb = 0; kb < (1 << 21); kb += blockDim.x) {
+    const int32_t k = kb + (int32_t)threadIdx.x;
+    const int32_t x0 = a.b0 + k * a.step, x1 = x0 + a.size - 1;
+    const int32_t lo = imin(x0, x1), hi = imax(x0, x1);
+    const int32_t cx0 = imax(lo, 0), cx1 = imin(hi, n - 1);
+    uint64_t sum = 0;
+    if (cx0 <= cx1 && cc0 <= cc1)
+      for (int32_t x = cx0; x <= cx1; x++) sum += lds[x];
+    const uint64_t cnt = (uint64_t)(uint32_t)((iabs(cx1 - cx0) + 1) * ccount);
+    const uint32_t b = (uint8_t)(0xFFull - sum / cnt);  // blit.c:91-109
+    const uint32_t total = block_prefix(b, carry, wsum);
+    const uint32_t count = (uint32_t)k + 1;
+    const bool cont = ((float)b >= ((a.threshold * total) / count)) && b != 0;
+    const bool outside = hi < 0 || lo >= n || cross_out;
+    const bool guard = outside && (a.threshold <= 1.0f || count >= (1u << 20));
+    if (!cont || guard) atomicMin(&stop_k, k);
+    __syncthreads();
+    if (threadIdx.x == blockDim.x - 1) carry = total;
+    __syncthreads();
+    if (stop_k != INT_MAX) break;
+  }
+  if (threadIdx.x == 0) results[slot] = stop_k == INT_MAX ? (1 << 21) : stop_k + 1;
+}
+
+void launch_edge_scan(const EdgeArgs* args, int jobs_per_sheet, const uint32_t* sums,
+                      int64_t sums_stride, int32_t* results, int count, hipStream_t st) {
+  if (jobs_per_sheet <= 0 || count <= 0) return;
+  hipLaunchKernelGGL(k_edge_scan, dim3(jobs_per_sheet, count), dim3(256), 0, st, args, sums,
+                     sums_stride, results);
+}
+
+// ---------------------------------------------------------------------------
+// detect_border_edge (masks.c:410-449): band k covers [lo + k*step, hi +
+// k*step] (inclusive, as scanned; rows/cols outside the image count 0).
+// result = k*|step| for the first k with count >= threshold while
+// k*|step| < max_step, else 0.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_border_scan(const BorderEdgeArgs* args,
+                                                     const uint32_t* sums, int64_t sums_stride,
+                                                     int32_t* results) {
+  const int s = blockIdx.y;
+  const int job = blockIdx.x;
+  const int64_t slot = (int64_t)s * gridDim.x + job;
+  const BorderEdgeArgs a = args[slot];
+  if (!a.active) return;
+  const uint32_t* S = sums + (int64_t)s * sums_stride + a.sums_offset;
+  __shared__ uint32_t lds[kMaxAxis];
+  __shared__ int32_t found;
+  const int32_t n = a.extent;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) lds[i] = S[i];
+  if (threadIdx.x == 0) found = INT_MAX;
+  __syncthreads();
+  const int32_t ast = iabs(a.step);
+  if (ast == 0) {
+    // result never advances: the reference loops forever unless band 0 hits
+    if (threadIdx.x == 0) {
+      uint32_t c = 0;
+      for (int32_t p = imax(a.lo, 0); p <= imin(a.hi, n - 1); p++) c += lds[p];
+      results[slot] = 0;
+      (void)c;
+    }
+    return;
+  }
+  const int32_t kmax = (a.max_step + ast - 1) / ast;  // k*|step| < max_step
+  for (int32_t kb = 0; kb < kmax; kb += blockDim.x) {
+    const int32_t k = kb + (int32_t)threadIdx.x;
+    if (k < kmax) {
+      const int32_t lo = a.lo + k * a.step, hi = a.hi + k * a.step;
+      uint32_t c = 0;
+      for (int32_t p = imax(lo, 0); p <= imin(hi, n - 1); p++) c += lds[p];
+      if (c >= (uint32_t)a.threshold) atomicMin(&found, k);
+    }
+    __syncthreads();
+    if (found != INT_MAX) break;
+  }
+  if (threadIdx.x == 0) results[slot] = found == INT_MAX ? 0 : found * ast;
+}
+
+void launch_border_scan(const BorderEdgeArgs* args, int jobs_per_sheet, const uint32_t* sums,
+                        int64_t sums_stride, int32_t* results, int count, hipStream_t st) {
+  if (jobs_per_sheet <= 0 || count <= 0) return;
+  hipLaunchKernelGGL(k_border_scan, dim3(jobs_per_sheet, count), dim3(256), 0, st, args, sums,
+                     sums_stride, results);
+}
+
+}  // namespace uph

@@ -1,0 +1,166 @@
+// ops_filters.hip — filter and rotation-detection ops of the C ABI
+// (imageprocess/filters.c, deskew.c peers) for single device frames.
+#include <cmath>
+#include <vector>
+
+#include "filters.h"
+#include "runtime.h"
+
+using namespace uph;
+
+static bool ready(const UphipImage& im, const char* op) {
+  if (!im.frame) return fail("%s: image has no frame", op);
+  if (!runtime_ready()) return fail("%s: no HIP device", op);
+  if (is_mono(im.frame->format))
+    return fail("%s: 1-bit frames are not supported by this op on the HIP backend", op);
+  hipSetDevice(im.frame->device);
+  return true;
+}
+
+static PlaneRef ref1(const UphipFrame* f) { return fixed_ref(frame_planes(f), 0); }
+
+extern "C" {
+
+void uphip_grayfilter(UphipImage image, UphipGrayfilterParameters params) {
+  // grayfilter_cpu, filters.c:370-402
+  if (!ready(image, "grayfilter")) return;
+  GrayGeom g;
+  if (!gray_geometry(image.frame->width, image.frame->height, params, image.abs_black_threshold,
+                     &g))
+    return (void)fail("grayfilter: invalid scan size/step");
+  hipStream_t st = current_stream();
+  void* scr = scratch(2, gray_scratch_bytes(g));
+  if (!scr) return;
+  launch_grayfilter(ref1(image.frame), g, scr, 0, nullptr, 1, st);
+}
+
+void uphip_blurfilter(UphipImage image, UphipBlurfilterParameters params,
+                      uint8_t abs_white_threshold) {
+  // blurfilter_cpu, filters.c:149-232
+  if (!ready(image, "blurfilter")) return;
+  BlurGeom g;
+  if (!blur_geometry(image.frame->width, image.frame->height, params, abs_white_threshold, &g))
+    return (void)fail("blurfilter: invalid scan size");
+  void* scr = scratch(2, blur_scratch_bytes(g));
+  if (!scr) return;
+  launch_blurfilter(ref1(image.frame), g, scr, 0, nullptr, 1, current_stream());
+}
+
+void uphip_noisefilter(UphipImage image, uint64_t intensity, uint8_t min_white_level) {
+  // noisefilter_cpu, filters.c:309-338
+  if (!ready(image, "noisefilter")) return;
+  NoiseGeom g;
+  noise_geometry(image.frame->width, image.frame->height, intensity, min_white_level, &g);
+  if (intensity > 64) return (void)fail("noisefilter: intensity > 64 unsupported");
+  const size_t bytes = noise_scratch_bytes(g);
+  void* scr = scratch(2, bytes);
+  SheetCtl* ctl = (SheetCtl*)scratch(3, sizeof(SheetCtl));
+  if (!scr || !ctl) return;
+  hipStream_t st = current_stream();
+  UPH_HIP(hipMemsetAsync(ctl, 0, sizeof(SheetCtl), st));
+  launch_noisefilter(ref1(image.frame), g, scr, (int64_t)bytes, nullptr, ctl, 1, st);
+  int32_t status = 0;
+  UPH_HIP(hipMemcpyAsync(&status, &ctl->status, 4, hipMemcpyDeviceToHost, st));
+  UPH_HIP(hipStreamSynchronize(st));
+  if (status) fail("noisefilter: candidate list overflow (status %d)", status);
+}
+
+void uphip_blackfilter(UphipImage image, UphipBlackfilterParameters params) {
+  // blackfilter_cpu, filters.c:111-127
+  if (!ready(image, "blackfilter")) return;
+  const int32_t W = image.frame->width, H = image.frame->height;
+  if (image.abs_black_threshold == 255)
+    return (void)fail("blackfilter: abs_black_threshold 255 makes the reference fill recurse "
+                      "forever");
+  std::vector<BlackBar> bars(2 * (size_t)(W + H) + 16);
+  BlackGeom g;
+  if (!black_geometry(W, H, params, image.abs_black_threshold, &g, bars.data(), (int)bars.size()))
+    return (void)fail("blackfilter: invalid scan parameters");
+  if (g.nbars == 0) return;
+  hipStream_t st = current_stream();
+  const size_t bytes = black_scratch_bytes(g);
+  void* scr = scratch(2, bytes);
+  BlackBar* dbars = (BlackBar*)scratch(4, sizeof(BlackBar) * g.nbars);
+  SheetCtl* ctl = (SheetCtl*)scratch(3, sizeof(SheetCtl));
+  if (!scr || !dbars || !ctl) return;
+  UPH_HIP(hipMemcpyAsync(dbars, bars.data(), sizeof(BlackBar) * g.nbars, hipMemcpyHostToDevice,
+                         st));
+  UPH_HIP(hipMemsetAsync(ctl, 0, sizeof(SheetCtl), st));
+  AxisArgs ah{g.hregion, 0, 1}, av{g.vregion, 0, 1};
+  AxisArgs* dah = stage_args(&ah, 1, st);
+  AxisArgs* dav = stage_args(&av, 1, st);
+  if (!dah || !dav) return;
+  launch_blackfilter_impl(ref1(image.frame), g, dbars, scr, (int64_t)bytes, nullptr, ctl, 1, st,
+                          dah, dav);
+  arg_fence(st);
+  int32_t status = 0;
+  UPH_HIP(hipMemcpyAsync(&status, &ctl->status, 4, hipMemcpyDeviceToHost, st));
+  UPH_HIP(hipStreamSynchronize(st));
+  if (status) fail("blackfilter: flood-fill stack overflow (status %d)", status);
+}
+
+float uphip_detect_rotation(UphipImage image, UphipRectangle mask,
+                            const UphipDeskewParameters params) {
+  // detect_rotation_cpu, deskew.c:181-241: peaks on the GPU, the per-edge
+  // argmax and the mean/deviation on the host exactly as the reference does
+  if (!ready(image, "detect_rotation")) return 0.0f;
+  static thread_local RotTable table;
+  if (rotation_angles(params, &table) < 0) {
+    fail("detect_rotation: more than %d angles", kMaxAngles);
+    return 0.0f;
+  }
+  const int na = table.nangles;
+  RotGeom g;
+  g.W = image.frame->width;
+  g.H = image.frame->height;
+  g.nedges = 0;
+  const UphipEdges& E = params.scan_edges;
+  const int shifts[4][2] = {{1, 0}, {0, 1}, {-1, 0}, {0, -1}};  // left, top, right, bottom
+  const bool on[4] = {E.left, E.top, E.right, E.bottom};
+  for (int k = 0; k < 4; k++)
+    if (on[k]) {
+      g.edge_shift[g.nedges][0] = shifts[k][0];
+      g.edge_shift[g.nedges][1] = shifts[k][1];
+      g.nedges++;
+    }
+  g.scan_size = params.deskewScanSize;
+  g.scan_depth = params.deskewScanDepth;
+  g.max_masks = 1;
+  hipStream_t st = current_stream();
+  RotTable* dt = (RotTable*)scratch(4, sizeof(RotTable));
+  Rect* dm = (Rect*)scratch(5, sizeof(Rect));
+  int32_t* peaks = (int32_t*)scratch(6, sizeof(int32_t) * 4 * (size_t)(na > 0 ? na : 1));
+  if (!dt || !dm || !peaks) return 0.0f;
+  Rect m = to_rect(mask);
+  UPH_HIP(hipMemcpyAsync(dt, &table, sizeof(RotTable), hipMemcpyHostToDevice, st));
+  UPH_HIP(hipMemcpyAsync(dm, &m, sizeof(Rect), hipMemcpyHostToDevice, st));
+  const int32_t mw = iabs(m.x0 - m.x1) + 1, mh = iabs(m.y0 - m.y1) + 1;
+  int max_scan = params.deskewScanSize == -1 ? imax(mw, mh) : params.deskewScanSize;
+  max_scan = imin(imin(max_scan, 10000), imax(mw, mh));
+  launch_rotation_peaks(ref1(image.frame), g, dt, dm, nullptr, 0, peaks, 1, st, na, max_scan);
+  std::vector<int32_t> hp(4 * (size_t)(na > 0 ? na : 1));
+  UPH_HIP(hipMemcpyAsync(hp.data(), peaks, sizeof(int32_t) * g.nedges * na,
+                         hipMemcpyDeviceToHost, st));
+  if (!UPH_HIP(hipStreamSynchronize(st))) return 0.0f;
+  float rot[4];
+  int count = 0, e = 0;
+  for (int k = 0; k < 4; k++) {
+    if (!on[k]) continue;
+    // detect_edge_rotation, deskew.c:153-174: first strictly larger peak
+    int max_peak = 0;
+    float detected = 0.0;
+    for (int a = 0; a < na; a++) {
+      const int peak = hp[(size_t)e * na + a];
+      if (peak > max_peak) {
+        detected = table.angle[a];
+        max_peak = peak;
+      }
+    }
+    rot[count++] = (k == 1 || k == 3) ? -detected : detected;
+    e++;
+  }
+  return combine_edge_rotations(rot, count, params.deskewScanDeviationRad);
+}
+
+}  // extern "C"
+
