@@ -411,7 +411,10 @@ typedef struct {
 } UphipSheetReport;
 int uphip_batch_get_report(UphipBatch *batch, int32_t sheet,
                            UphipSheetReport *report);
-/* Per-kernel timing of the last run (HIP events on the batch stream). */
+/* Per-stage device time summed over every run since the previous call (HIP
+ * events recorded between stages on the batch stream, cf. the reference's
+ * --perf stage timers, lib/perf.c).  Synchronises the batch stream, returns
+ * the number of stages written and clears the record. */
 int uphip_batch_kernel_times(UphipBatch *batch, const char **names, float *ms,
                              int max_entries);
 

@@ -300,7 +300,9 @@ struct UphipBatch {
   uint8_t* rot_page = nullptr;   // pre_rotate temp pages
   // device argument arrays (uniform per batch or written by control kernels)
   std::vector<void*> allocs;
-  std::vector<std::pair<std::string, hipEvent_t>> marks;
+  // stage boundary events of every run since the last kernel_times() query
+  std::vector<std::vector<std::pair<const char*, hipEvent_t>>> runs;
+  std::vector<std::string> time_names;
   bool timing = true;
   // geometry records
   BlackGeom bgeo{};
@@ -387,10 +389,11 @@ Planes planes_of(UphipBatch* b, int32_t w, int32_t h) {
 
 void mark(UphipBatch* b, const char* name) {
   if (!b->timing) return;
+  if (b->runs.empty()) return;
   hipEvent_t e;
   hipEventCreate(&e);
   hipEventRecord(e, b->st);
-  b->marks.push_back({name, e});
+  b->runs.back().push_back({name, e});
 }
 
 void flip_all(UphipBatch* b, int count) {
@@ -895,8 +898,7 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
                       int64_t sstride) {
   const UphipOptions& o = b->o;
   const uint32_t dis = o.disable;
-  for (auto& m : b->marks) hipEventDestroy(m.second);
-  b->marks.clear();
+  if (b->timing) b->runs.emplace_back();
   b->cache_pos = 0;
   mark(b, "start");
   const UphipPoint p0 = b->points.size() > 0 ? b->points[0] : UphipPoint{0, 0};
@@ -1164,7 +1166,8 @@ void uphip_batch_destroy(UphipBatch* b) {
   if (!b) return;
   hipSetDevice(b->device);
   if (b->st) hipStreamSynchronize(b->st);
-  for (auto& m : b->marks) hipEventDestroy(m.second);
+  for (auto& r : b->runs)
+    for (auto& m : r) hipEventDestroy(m.second);
   for (void* p : b->allocs) hipFree(p);
   if (b->st) hipStreamDestroy(b->st);
   delete b;
@@ -1272,13 +1275,33 @@ int uphip_batch_get_report(UphipBatch* b, int32_t sheet, UphipSheetReport* r) {
 }
 
 int uphip_batch_kernel_times(UphipBatch* b, const char** names, float* ms, int max_entries) {
+  // per-stage totals over every run since the previous query (the events
+  // bracket each stage on the batch stream); the record is then cleared
   if (!b) return -1;
+  hipSetDevice(b->device);
+  if (!UPH_HIP(hipStreamSynchronize(b->st))) return -1;
+  std::vector<std::string> order;
+  std::vector<double> tot;
+  for (auto& r : b->runs) {
+    for (size_t i = 1; i < r.size(); i++) {
+      float t = 0.0f;
+      hipEventElapsedTime(&t, r[i - 1].second, r[i].second);
+      size_t k = 0;
+      while (k < order.size() && order[k] != r[i].first) k++;
+      if (k == order.size()) {
+        order.push_back(r[i].first);
+        tot.push_back(0.0);
+      }
+      tot[k] += t;
+    }
+    for (auto& m : r) hipEventDestroy(m.second);
+  }
+  b->runs.clear();
+  b->time_names = order;
   int k = 0;
-  for (size_t i = 1; i < b->marks.size() && k < max_entries; i++, k++) {
-    float t = 0.0f;
-    hipEventElapsedTime(&t, b->marks[i - 1].second, b->marks[i].second);
-    if (names) names[k] = b->marks[i].first.c_str();
-    if (ms) ms[k] = t;
+  for (; k < (int)order.size() && k < max_entries; k++) {
+    if (names) names[k] = b->time_names[k].c_str();
+    if (ms) ms[k] = (float)tot[k];
   }
   return k;
 }

@@ -52,7 +52,10 @@ SYNTH_FN uint8_t synth_pixel(uint32_t page, int32_t W, int32_t H, int32_t x, int
     const int64_t line = lv / 48, r = lv % 48;
     const uint64_t lh = synth_h(page, 2, (uint64_t)line, 0);
     const int32_t gh = 20 + (int32_t)(lh % 9);
-    const int64_t len = (W - 2 * mx) - (int64_t)((lh >> 8) % (uint64_t)((W - 2 * mx) / 3 + 1));
+    /* justified lines; one in six ends a paragraph short */
+    const int64_t full = W - 2 * mx;
+    const int64_t len = (lh >> 8) % 6 == 0 ? full - (int64_t)((lh >> 11) % (uint64_t)(full / 2 + 1))
+                                          : full;
     if (r < gh && (u - mx) < len && (lh >> 40) % 23 != 0) {
       const int64_t word = (u - mx) / 40, wu = (u - mx) % 40;
       const uint64_t wh = synth_h(page, 3, (uint64_t)line, (uint64_t)word);
