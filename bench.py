@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC HBM bytes per stage launch from a rocprofv3 --pmc pass")
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
+    ap.add_argument("--sweep", default="",
+                    help="tuning only: comma list of BATCHxSTREAMS, each timed over one step "
+                         "and printed to stderr before the main run")
     return ap.parse_args()
 
 
@@ -148,6 +151,25 @@ def cpu_baseline(first_page, npages, threads):
     return npages / (time.perf_counter() - t0)
 
 
+def time_config(opts, pages, pitch, stride, npages, bsz, nstreams):
+    """Seconds for one pass over the pages with a given batch/stream shape
+    (after one warm-up pass)."""
+    bs = [Batch(opts, bsz, W, H, A.FMT_GRAY8) for _ in range(nstreams)]
+    chunks = [(s, min(bsz, npages - s)) for s in range(0, npages, bsz)]
+    try:
+        for rep in range(2):
+            t0 = time.perf_counter()
+            for i, (s, n) in enumerate(chunks):
+                bs[i % nstreams].run_device(n, pages.ptr + s * stride, pitch, stride)
+            for b in bs:
+                b.wait()
+            t = time.perf_counter() - t0
+        return t
+    finally:
+        for b in bs:
+            b.close()
+
+
 def main():
     args = parse()
     d = Dist()
@@ -167,6 +189,11 @@ def main():
 
     opts = A.Options()
     L.uphip_options_init(C.byref(opts))     # the reference's defaults (lib/options.c)
+    for cfg in filter(None, args.sweep.split(",")):
+        sb, ss = (int(v) for v in cfg.split("x"))
+        t = time_config(opts, pages, pitch, stride, npages, sb, ss)
+        print("sweep batch %d streams %d: %.1f pages/s" % (sb, ss, npages / t), file=sys.stderr,
+              flush=True)
     bsz = max(1, min(args.batch, npages))
     batches = [Batch(opts, bsz, W, H, A.FMT_GRAY8) for _ in range(max(1, args.streams))]
     chunks = [(s, min(bsz, npages - s)) for s in range(0, npages, bsz)]

@@ -510,7 +510,10 @@ __device__ __forceinline__ uint32_t row9(const uint32_t* w, int c) {
 }
 
 // Dark component of (cx,cy) restricted to its 9x9 box; returns popcount
-// (capped growth after 4 dilations) and the mask rows.
+// (capped growth after 4 dilations) and the mask rows.  Every dilation step
+// only adds pixels connected to the centre, so the search stops as soon as
+// more than 4 are reached (the component is large; text strokes exit after
+// the first step, whose 3x3 neighbourhood is all 8-adjacent to the centre).
 __device__ __forceinline__ int flood9(const uint32_t (*drow)[4], int cx, int cy, uint32_t* comp) {
   uint32_t D[9], cur[9];
 #pragma unroll
@@ -522,15 +525,22 @@ __device__ __forceinline__ int flood9(const uint32_t (*drow)[4], int cx, int cy,
   for (int it = 0; it < 4; it++) {
     uint32_t nx[9];
     bool same = true;
+    int n = 0;
 #pragma unroll
     for (int r = 0; r < 9; r++) {
       uint32_t u = cur[r] | (r > 0 ? cur[r - 1] : 0) | (r < 8 ? cur[r + 1] : 0);
       u = (u | (u << 1) | (u >> 1)) & D[r] & 0x1FFu;
       nx[r] = u;
       same &= (u == cur[r]);
+      n += __popc(u);
     }
 #pragma unroll
     for (int r = 0; r < 9; r++) cur[r] = nx[r];
+    if (n > 4) {
+#pragma unroll
+      for (int r = 0; r < 9; r++) comp[r] = cur[r];
+      return n;
+    }
     if (same) break;
   }
   int n = 0;
@@ -556,23 +566,68 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
   __shared__ uint8_t px[kRW * kRW];
   __shared__ uint32_t drow[kRW][4];
   __shared__ int32_t any_dark;
-  if (threadIdx.x == 0) any_dark = 0;
-  for (int i = threadIdx.x; i < kRW * 4; i += 256) drow[i >> 2][i & 3] = 0;
+  // Stage the region rows into LDS with 16-byte loads, all issued before any
+  // is consumed (the region is ~2 KB-18 KB; one byte per lane per load would
+  // leave the kernel latency bound).  Rows start 256-byte aligned, so every
+  // vector lies inside its row's pitch; out-of-image pixels are masked below.
+  constexpr int B = FMT == F_GRAY8 ? 1 : FMT == F_Y400A ? 2 : 3;
+  constexpr int NV = (kRW * B + 30) / 16;             // vectors per region row
+  constexpr int NLOAD = (kRW * NV + 255) / 256;       // loads per thread
+  __shared__ uint4 stage[kRW][NV];
+  const int64_t sb = (int64_t)ox * B;                 // first region byte in the row
+  const int64_t a0 = sb >= 0 ? (sb & ~(int64_t)15) : -((-sb + 15) & ~(int64_t)15);
+  const int lead = (int)(sb - a0);                    // region byte 0 within the staged row
+  const int64_t pitch = img.P.pitch;
+  uint4 v[NLOAD];
+#pragma unroll
+  for (int k = 0; k < NLOAD; k++) {
+    const int i = threadIdx.x + k * 256;
+    const int ry = i / NV, vi = i % NV;
+    const int32_t gy = oy + ry;
+    const int64_t off = a0 + 16 * vi;
+    v[k] = make_uint4(0, 0, 0, 0);
+    if (i < kRW * NV && gy >= 0 && gy < g.H && off >= 0 && off < pitch)
+      v[k] = *reinterpret_cast<const uint4*>(base + (int64_t)gy * pitch + off);
+  }
+#pragma unroll
+  for (int k = 0; k < NLOAD; k++) {
+    const int i = threadIdx.x + k * 256;
+    if (i < kRW * NV) stage[i / NV][i % NV] = v[k];
+  }
   __syncthreads();
-  for (int i = threadIdx.x; i < kRW * kRW; i += 256) {
-    const int ry = i / kRW, rx = i % kRW;
-    const int32_t gx = ox + rx, gy = oy + ry;
-    uint8_t f = 0;
-    if (gx >= 0 && gy >= 0 && gx < g.W && gy < g.H) {
-      Px p = load_px_row<FMT>(base + (int64_t)gy * img.P.pitch, gx);
-      if (light_of(p) < g.white) f |= 1;
-      if (dark_of(p) < g.white) f |= 2;
+  // flags + dark bit rows: wave w takes rows w, w+4, ...; lanes own columns
+  // lane and 64+lane, so each row mask is two ballots (no LDS atomics)
+  {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    bool tile_dark = false;
+    for (int ry = w; ry < kRW; ry += 4) {
+      const int32_t gy = oy + ry;
+      const uint8_t* srow = reinterpret_cast<const uint8_t*>(stage[ry]) + lead;
+      unsigned long long m[2];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int rx = h * 64 + lane;
+        const int32_t gx = ox + rx;
+        uint8_t f = 0;
+        if (rx < kRW && gx >= 0 && gx < g.W && gy >= 0 && gy < g.H) {
+          const Px p = load_px_row<FMT>(srow, rx);
+          if (light_of(p) < g.white) f |= 1;
+          if (dark_of(p) < g.white) f |= 2;
+        }
+        if (rx < kRW) px[ry * kRW + rx] = f;
+        if ((f & 1) && rx >= kHalo && rx < kHalo + kNT && ry >= kHalo && ry < kHalo + kNT)
+          tile_dark = true;
+        m[h] = __ballot(f & 1);
+      }
+      if (lane < 4) {
+        const unsigned long long q = m[lane >> 1];
+        drow[ry][lane] = (uint32_t)(lane & 1 ? q >> 32 : q);
+      }
     }
-    px[i] = f;
-    if (f & 1) {
-      atomicOr(&drow[ry][rx >> 5], 1u << (rx & 31));
-      if (rx >= kHalo && rx < kHalo + kNT && ry >= kHalo && ry < kHalo + kNT) any_dark = 1;
-    }
+    const unsigned long long any = __ballot(tile_dark);
+    if (threadIdx.x == 0) any_dark = 0;
+    __syncthreads();
+    if (lane == 0 && any) any_dark = 1;
   }
   __syncthreads();
   if (!any_dark) return;
@@ -705,6 +760,33 @@ __device__ void block_sort(uint32_t* a, int n_pow2) {
   }
 }
 
+// Pixel k of the Chebyshev ring L (8L pixels): the two rows dy = -L, +L
+// (2L+1 each), then the two columns dx = -L, +L without the corners.
+__device__ __forceinline__ bool ring_pos(int L, int k, int* dx, int* dy) {
+  const int row = 2 * L + 1, col = 2 * L - 1;
+  if (k < row) {
+    *dx = k - L;
+    *dy = -L;
+  } else if (k < 2 * row) {
+    *dx = k - row - L;
+    *dy = L;
+  } else if (k < 2 * row + col) {
+    *dx = -L;
+    *dy = k - 2 * row - (L - 1);
+  } else if (k < 2 * row + 2 * col) {
+    *dx = L;
+    *dy = k - 2 * row - col - (L - 1);
+  } else {
+    return false;
+  }
+  return true;
+}
+
+// Whether the reference ring loops visit (x+dx, y+dy) at level L.
+__device__ __forceinline__ bool ring_member(int L, int dx, int dy, int32_t x, int32_t y) {
+  return iabs(dy) == L ? x >= L : y >= L - 1;
+}
+
 template <int FMT>
 __global__ void __launch_bounds__(256) k_noise_resolve(PlaneRef img, NoiseGeom g, uint8_t* scratch,
                                                        int64_t sstride, const int32_t* active,
@@ -736,8 +818,6 @@ __global__ void __launch_bounds__(256) k_noise_resolve(PlaneRef img, NoiseGeom g
   // one wave replays the raster scan over the sorted triggers
   const int lane = threadIdx.x;
   const int N = g.intensity;
-  const int R = N;                       // box radius
-  const int side = 2 * R + 1, area = side * side;
   uint8_t* base = plane_ptr(img, s);
   const int64_t pitch = img.P.pitch;
   for (uint32_t idx = 0; idx < n; idx++) {
@@ -748,49 +828,37 @@ __global__ void __launch_bounds__(256) k_noise_resolve(PlaneRef img, NoiseGeom g
     if (!(dark_of(cp) < g.white)) continue;  // cleared meanwhile
     // ring counts with the reference loops' unsigned-comparison semantics:
     // rows +-L counted iff x >= L, columns +-L (|dy| < L) counted iff y >= L-1
-    int cnt[65];
-    for (int L = 0; L <= R; L++) cnt[L] = 0;
-    for (int b = 0; b < area; b += 64) {
-      const int pos = b + lane;
-      int L = 0;
-      bool dark = false;
-      if (pos < area) {
-        const int dx = pos % side - R, dy = pos / side - R;
-        const int adx = iabs(dx), ady = iabs(dy);
-        L = imax(adx, ady);
-        bool member = L > 0 && ((ady == L && x >= L) || (ady < L && adx == L && y >= L - 1));
-        if (member) {
+    // (filters.c:243-302); ring L is walked as its 8L pixels, one per lane
+    int count = 1, level = 1, lc;
+    do {
+      lc = 0;
+      for (int b = 0; b < 8 * level; b += 64) {
+        int dx, dy;
+        const bool in = ring_pos(level, b + lane, &dx, &dy);
+        bool dark = false;
+        if (in && ring_member(level, dx, dy, x, y)) {
           const int32_t qx = x + dx, qy = y + dy;
           if (qx >= 0 && qy >= 0 && qx < g.W && qy < g.H)
             dark = light_of(load_px_row<FMT>(base + (int64_t)qy * pitch, qx)) < g.white;
         }
+        lc += __popcll(__ballot(dark));
       }
-      for (int l = 1; l <= R; l++) cnt[l] += __popcll(__ballot(dark && L == l));
-    }
-    int count = 1, k = 0, level = 1;
-    int lc;
-    do {
-      lc = cnt[level];
       count += lc;
       level++;
     } while (lc != 0 && level <= N);
     if (count > N) continue;
-    // rings 1..k-1 (the loop stopped at the first empty ring k) + centre
-    k = level - 1;  // the empty ring
+    // centre + rings 1..k-1 (the loop stopped at the first empty ring k)
+    const int k = level - 1;
     if (lane == 0) white_px<FMT>(base + (int64_t)y * pitch, x);
-    for (int b = 0; b < area; b += 64) {
-      const int pos = b + lane;
-      if (pos >= area) continue;
-      const int dx = pos % side - R, dy = pos / side - R;
-      const int adx = iabs(dx), ady = iabs(dy);
-      const int L = imax(adx, ady);
-      if (L == 0 || L >= k) continue;
-      bool member = (ady == L && x >= L) || (ady < L && adx == L && y >= L - 1);
-      if (!member) continue;
-      const int32_t qx = x + dx, qy = y + dy;
-      if (qx < 0 || qy < 0 || qx >= g.W || qy >= g.H) continue;
-      uint8_t* row = base + (int64_t)qy * pitch;
-      if (light_of(load_px_row<FMT>(row, qx)) < g.white) white_px<FMT>(row, qx);
+    for (int L = 1; L < k; L++) {
+      for (int b = 0; b < 8 * L; b += 64) {
+        int dx, dy;
+        if (!ring_pos(L, b + lane, &dx, &dy) || !ring_member(L, dx, dy, x, y)) continue;
+        const int32_t qx = x + dx, qy = y + dy;
+        if (qx < 0 || qy < 0 || qx >= g.W || qy >= g.H) continue;
+        uint8_t* row = base + (int64_t)qy * pitch;
+        if (light_of(load_px_row<FMT>(row, qx)) < g.white) white_px<FMT>(row, qx);
+      }
     }
     __threadfence_block();
   }
