@@ -631,12 +631,29 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
   }
   __syncthreads();
   if (!any_dark) return;
-  // small flags within radius 10 of the tile: region [4, 88)
-  for (int i = threadIdx.x; i < 84 * 84; i += 256) {
-    const int ry = 4 + i / 84, rx = 4 + i % 84;
-    if (!(px[ry * kRW + rx] & 1)) continue;
-    uint32_t comp[9];
-    if (flood9(drow, rx, ry, comp) <= 4) px[ry * kRW + rx] |= 4;
+  // small flags within radius 10 of the tile (region rows/cols [4, 88)), as
+  // LDS bytes (bit 2) and as bit rows built from ballots
+  __shared__ uint32_t srow[kRW][4];
+  {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int ry = w; ry < kRW; ry += 4) {
+      unsigned long long m[2];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int rx = h * 64 + lane;
+        bool small = false;
+        if (ry >= 4 && ry < 88 && rx >= 4 && rx < 88 && (px[ry * kRW + rx] & 1)) {
+          uint32_t comp[9];
+          small = flood9(drow, rx, ry, comp) <= 4;
+          if (small) px[ry * kRW + rx] |= 4;
+        }
+        m[h] = __ballot(small);
+      }
+      if (lane < 4) {
+        const unsigned long long q = m[lane >> 1];
+        srow[ry][lane] = (uint32_t)(lane & 1 ? q >> 32 : q);
+      }
+    }
   }
   __syncthreads();
   const int N = g.intensity;
@@ -655,35 +672,43 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
     if (!(f & 4)) continue;  // large component: never cleared
     uint32_t comp[9];
     flood9(drow, rx, ry, comp);
-    // component pixels (<= 4), relative to (rx, ry)
+    // component pixels (<= 4) relative to (rx, ry), and their bounding box
     int cxs[4], cys[4], nc = 0;
-    bool eligible = true;
-    for (int r = 0; r < 9; r++)
-      for (int b = 0; b < 9; b++)
-        if (comp[r] >> b & 1) {
-          if (nc < 4) {
-            cxs[nc] = b - 4;
-            cys[nc] = r - 4;
-          }
-          nc++;
-          if (gx + b - 4 < kEligible || gy + r - 4 < kEligible) eligible = false;
-        }
-    if (nc > 4) eligible = false;  // cannot happen (small)
-    // no foreign small pixel within Chebyshev 7 of the component
-    for (int dy = -10; dy <= 10 && eligible; dy++)
-      for (int dx = -10; dx <= 10; dx++) {
-        const uint8_t q = px[(ry + dy) * kRW + rx + dx];
-        if (!(q & 4)) continue;
-        bool mine = false, near = false;
-        for (int k = 0; k < nc; k++) {
-          if (cxs[k] == dx && cys[k] == dy) mine = true;
-          if (iabs(cxs[k] - dx) <= 7 && iabs(cys[k] - dy) <= 7) near = true;
-        }
-        if (!mine && near) {
-          eligible = false;
-          break;
-        }
+    int bx0 = 9, bx1 = -1, by0 = 9, by1 = -1;
+#pragma unroll
+    for (int r = 0; r < 9; r++) {
+      uint32_t m = comp[r];
+      if (m) {
+        by0 = imin(by0, r);
+        by1 = r;
+        bx0 = imin(bx0, __ffs(m) - 1);
+        bx1 = imax(bx1, 31 - __clz(m));
       }
+      while (m) {
+        const int b = __ffs(m) - 1;
+        m &= m - 1;
+        if (nc < 4) {
+          cxs[nc] = b - 4;
+          cys[nc] = r - 4;
+        }
+        nc++;
+      }
+    }
+    bool eligible = nc <= 4 && gx - 4 + bx0 >= kEligible && gy - 4 + by0 >= kEligible;
+    // no foreign small pixel within Chebyshev 7 of the component: checked on
+    // the bounding box dilated by 7 (a superset of that neighbourhood, so a
+    // component rejected here merely takes the exact sequential path)
+    if (eligible) {
+      const int X0 = rx - 4 + bx0 - 7, n = bx1 - bx0 + 15;
+      const uint32_t keep = (1u << n) - 1u;
+      int cnt = 0;
+      for (int r = ry - 4 + by0 - 7; r <= ry - 4 + by1 + 7; r++) {
+        const int word = X0 >> 5, off = X0 & 31;
+        const uint64_t v = ((uint64_t)srow[r][word + 1] << 32) | srow[r][word];
+        cnt += __popc((uint32_t)(v >> off) & keep);
+      }
+      eligible = cnt == nc;
+    }
     if (!eligible) {
       if (f & 2) {
         uint32_t k = atomicAdd(NP.nseq, 1u);
@@ -820,6 +845,55 @@ __global__ void __launch_bounds__(256) k_noise_resolve(PlaneRef img, NoiseGeom g
   const int N = g.intensity;
   uint8_t* base = plane_ptr(img, s);
   const int64_t pitch = img.P.pitch;
+  if (N <= 4) {
+    // small intensity: the whole (2N+1)^2 box of a trigger is read in one
+    // round trip (two pixels per lane) and the rings are counted from
+    // registers; clears are written straight back
+    const int side = 2 * N + 1, area = side * side;
+    for (uint32_t idx = 0; idx < n; idx++) {
+      const uint32_t key = keys[idx];
+      const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
+      __threadfence_block();
+      int Lv[2];
+      bool dk[2], ctr = false;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int pos = h * 64 + lane;
+        Lv[h] = -1;
+        dk[h] = false;
+        if (pos < area) {
+          const int dx = pos % side - N, dy = pos / side - N;
+          const int L = imax(iabs(dx), iabs(dy));
+          const int32_t qx = x + dx, qy = y + dy;
+          Lv[h] = L;
+          const bool member = L == 0 || ring_member(L, dx, dy, x, y);
+          if (member && qx >= 0 && qy >= 0 && qx < g.W && qy < g.H) {
+            const Px p = load_px_row<FMT>(base + (int64_t)qy * pitch, qx);
+            dk[h] = L > 0 && light_of(p) < g.white;
+            if (L == 0) ctr = dark_of(p) < g.white;
+          }
+        }
+      }
+      if (!__ballot(ctr)) continue;  // cleared meanwhile
+      int count = 1, level = 1, lc;
+      do {
+        lc = __popcll(__ballot(dk[0] && Lv[0] == level)) +
+             __popcll(__ballot(dk[1] && Lv[1] == level));
+        count += lc;
+        level++;
+      } while (lc != 0 && level <= N);
+      if (count > N) continue;
+      const int k = level - 1;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int pos = h * 64 + lane;
+        if (pos >= area || Lv[h] >= k || (Lv[h] > 0 && !dk[h])) continue;
+        const int32_t qx = x + pos % side - N, qy = y + pos / side - N;
+        white_px<FMT>(base + (int64_t)qy * pitch, qx);
+      }
+    }
+    return;
+  }
   for (uint32_t idx = 0; idx < n; idx++) {
     const uint32_t key = keys[idx];
     const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
