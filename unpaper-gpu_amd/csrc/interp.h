@@ -41,13 +41,15 @@ __device__ __forceinline__ Px linear_px(float f, Px a, Px b) {
   return Px{linear_scale(f, a.r, b.r), linear_scale(f, a.g, b.g), linear_scale(f, a.b, b.b)};
 }
 
-template <int FMT>
-__device__ __forceinline__ Px interp_nn(const Src<FMT>& s, float cx, float cy) {
+// The interpolators are generic over the pixel source S (S::at(x, y) with
+// get_pixel semantics): the global frame (Src) or an LDS-staged window.
+template <class S>
+__device__ __forceinline__ Px interp_nn(const S& s, float cx, float cy) {
   return s.at((int)roundf(cx), (int)roundf(cy));  // interpolate.c:13-18
 }
 
-template <int FMT>
-__device__ __forceinline__ Px interp_bicubic(const Src<FMT>& s, float cx, float cy) {
+template <class S>
+__device__ __forceinline__ Px interp_bicubic(const S& s, float cx, float cy) {
   // interp_bicubic, interpolate.c:43-60: (int) truncates toward zero
   const int px = (int)cx, py = (int)cy;
   const float fx = cx - px;
@@ -60,13 +62,13 @@ __device__ __forceinline__ Px interp_bicubic(const Src<FMT>& s, float cx, float 
   return cubic_px(cy - py, col[0], col[1], col[2], col[3]);
 }
 
-template <int FMT>
-__device__ __forceinline__ Px interp_bilinear(const Src<FMT>& s, float cx, float cy) {
+template <class S>
+__device__ __forceinline__ Px interp_bilinear(const S& s, float cx, float cy) {
   // interp_bilinear, interpolate.c:77-118 (integral-coordinate quirk kept:
   // the one-axis cases use the OTHER axis' fraction, i.e. 0)
   const int x1 = (int)floorf(cx), y1 = (int)floorf(cy);
   const int x2 = (int)ceilf(cx), y2 = (int)ceilf(cy);
-  if (!(x2 >= 0 && x2 <= s.W - 1 && y2 >= 0 && y2 <= s.H - 1)) return s.at(x1, y1);
+  if (!(x2 >= 0 && x2 <= s.W - 1 && y2 >= 0 && y2 <= s.H - 1)) return s.at(x1, y1);  // image size
   if (x1 == x2 && y1 == y2) return s.at(x1, y1);
   if (x1 == x2) return linear_px(cx - x1, s.at(x1, y1), s.at(x2, y2));
   if (y1 == y2) return linear_px(cy - y1, s.at(x1, y1), s.at(x2, y2));
@@ -75,11 +77,11 @@ __device__ __forceinline__ Px interp_bilinear(const Src<FMT>& s, float cx, float
   return linear_px(cy - y1, h1, h2);
 }
 
-template <int FMT>
-__device__ __forceinline__ Px interpolate(const Src<FMT>& s, float cx, float cy, int fn) {
-  if (fn == UPHIP_INTERP_NN) return interp_nn<FMT>(s, cx, cy);
-  if (fn == UPHIP_INTERP_LINEAR) return interp_bilinear<FMT>(s, cx, cy);
-  return interp_bicubic<FMT>(s, cx, cy);
+template <int FMT, class S = Src<FMT>>
+__device__ __forceinline__ Px interpolate(const S& s, float cx, float cy, int fn) {
+  if (fn == UPHIP_INTERP_NN) return interp_nn(s, cx, cy);
+  if (fn == UPHIP_INTERP_LINEAR) return interp_bilinear(s, cx, cy);
+  return interp_bicubic(s, cx, cy);
 }
 
 }  // namespace uph

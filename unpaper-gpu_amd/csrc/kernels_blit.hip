@@ -509,10 +509,43 @@ void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* 
 // deskew_cpu + rotate (deskew.c:248-286) fused out of place: inside the mask
 // rectangle (placed at mask.vertex[0], clipped to the image) the rotated
 // pixel, elsewhere the source pixel.
+//
+// One workgroup per 64x16 output tile.  The source footprint of the tile's
+// in-mask part (a rotated rectangle, plus the interpolation taps) is staged
+// in LDS once -- white outside the image, which is what get_pixel returns --
+// and every tap is then an LDS read.  The float expressions are untouched,
+// so the result is identical to the direct gather, which remains the path
+// for tiles whose footprint does not fit (rotations far beyond the default
+// 5 degree range).
 // ---------------------------------------------------------------------------
+constexpr int kRotTW = 64, kRotTH = 16;
+constexpr int kRotCap = 4096;  // staged pixels per tile
+
+// LDS-staged window [x0, x0+w) x [y0, y0+h) of the source (channels: 1 for
+// GRAY8/Y400A gray, 3 for RGB24); W/H are the image's, for the interpolators.
+template <int FMT>
+struct LdsSrc {
+  const uint8_t* lds;
+  int32_t x0, y0, w, h;
+  int32_t W, H;
+  Src<FMT> g;
+  __device__ __forceinline__ Px at(int32_t x, int32_t y) const {
+    const int32_t u = x - x0, v = y - y0;
+    if (u < 0 || v < 0 || u >= w || v >= h) return g.at(x, y);  // never for in-bound tiles
+    if (FMT == F_RGB24) {
+      const uint8_t* q = lds + 3 * (v * w + u);
+      return Px{q[0], q[1], q[2]};
+    }
+    const uint8_t q = lds[v * w + u];
+    return Px{q, q, q};
+  }
+};
+
 template <int FMT>
 __global__ void __launch_bounds__(kThreads) k_rotate_mask(PlaneRef src, PlaneRef dst,
                                                           const RotateArgs* args, int interp) {
+  constexpr int CH = FMT == F_RGB24 ? 3 : 1;
+  __shared__ uint8_t stage[kRotCap * CH];
   const int s = blockIdx.z;
   const RotateArgs a = args[s];
   if (!a.active) return;
@@ -525,38 +558,101 @@ __global__ void __launch_bounds__(kThreads) k_rotate_mask(PlaneRef src, PlaneRef
   const float scx = nm.x0 + sw / 2.0f, scy = nm.y0 + sh / 2.0f;
   const float tcx = 0 + sw / 2.0f, tcy = 0 + sh / 2.0f;
   const Src<FMT> S{sbase, P.pitch, P.W, P.H};
-  for (int32_t y = blockIdx.x; y < P.H; y += gridDim.x) {
-    uint8_t* drow = dbase + (int64_t)y * P.pitch;
-    const uint8_t* srow = sbase + (int64_t)y * P.pitch;
-    const int32_t v = y - a.mask.y0;
-    for (int32_t x = threadIdx.x; x < P.W; x += blockDim.x) {
-      const int32_t u = x - a.mask.x0;
-      Px o;
-      if (u >= 0 && u < sw && v >= 0 && v < sh) {
-        const float srcX = scx + (u - tcx) * a.cosval + (v - tcy) * a.sinval;
-        const float srcY = scy + (v - tcy) * a.cosval - (u - tcx) * a.sinval;
-        o = interpolate<FMT>(S, srcX, srcY, interp);
-      } else {
-        copy_px_raw<FMT>(drow, x, srow, x);
-        continue;
+  const int32_t tx0 = blockIdx.x * kRotTW, ty0 = blockIdx.y * kRotTH;
+  // in-mask part of the tile, in mask coordinates (u, v)
+  const int32_t u0 = imax(tx0, 0) - a.mask.x0, u1 = imin(tx0 + kRotTW, P.W) - 1 - a.mask.x0;
+  const int32_t v0 = imax(ty0, 0) - a.mask.y0, v1 = imin(ty0 + kRotTH, P.H) - 1 - a.mask.y0;
+  const int32_t cu0 = imax(u0, 0), cu1 = imin(u1, sw - 1);
+  const int32_t cv0 = imax(v0, 0), cv1 = imin(v1, sh - 1);
+  const bool any_in = cu0 <= cu1 && cv0 <= cv1;
+  // source bounding box of the in-mask part (linear map: extremes at corners)
+  int32_t bx0 = 0, by0 = 0, bw = 0, bh = 0;
+  bool staged = false;
+  if (any_in) {
+    float mnx = 3.0e38f, mxx = -3.0e38f, mny = 3.0e38f, mxy = -3.0e38f;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int32_t u = c & 1 ? cu1 : cu0, v = c & 2 ? cv1 : cv0;
+      const float X = scx + (u - tcx) * a.cosval + (v - tcy) * a.sinval;
+      const float Y = scy + (v - tcy) * a.cosval - (u - tcx) * a.sinval;
+      mnx = fminf(mnx, X);
+      mxx = fmaxf(mxx, X);
+      mny = fminf(mny, Y);
+      mxy = fmaxf(mxy, Y);
+    }
+    // taps: cubic (int)c-1 .. (int)c+2 (trunc), bilinear floor..ceil, NN round
+    bx0 = (int32_t)floorf(mnx) - 2;
+    by0 = (int32_t)floorf(mny) - 2;
+    bw = (int32_t)floorf(mxx) + 3 - bx0 + 1;
+    bh = (int32_t)floorf(mxy) + 3 - by0 + 1;
+    staged = bw > 0 && bh > 0 && (int64_t)bw * bh <= kRotCap;
+  }
+  if (staged) {
+    // all loads of a round are issued before the LDS stores
+    const int n = bw * bh;
+    for (int base = 0; base < n; base += 8 * kThreads) {
+      uint8_t v[8][CH];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = base + k * kThreads + threadIdx.x;
+        const int32_t x = bx0 + i % bw, y = by0 + i / bw;
+#pragma unroll
+        for (int c = 0; c < CH; c++) v[k][c] = 255;
+        if (i < n && x >= 0 && y >= 0 && x < P.W && y < P.H) {
+          const Px p = load_px_row<FMT>(sbase + (int64_t)y * P.pitch, x);
+          v[k][0] = p.r;
+          if (CH == 3) {
+            v[k][1] = p.g;
+            v[k][2] = p.b;
+          }
+        }
       }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = base + k * kThreads + threadIdx.x;
+        if (i < n) {
+#pragma unroll
+          for (int c = 0; c < CH; c++) stage[i * CH + c] = v[k][c];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const LdsSrc<FMT> L{stage, bx0, by0, bw, bh, P.W, P.H, S};
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int32_t x = tx0 + lane;
+  if (x >= P.W) return;
+  const int32_t u = x - a.mask.x0;
+#pragma unroll
+  for (int k = 0; k < kRotTH / 4; k++) {
+    const int32_t y = ty0 + w + 4 * k;
+    if (y >= P.H) break;
+    uint8_t* drow = dbase + (int64_t)y * P.pitch;
+    const int32_t v = y - a.mask.y0;
+    if (u >= 0 && u < sw && v >= 0 && v < sh) {
+      const float srcX = scx + (u - tcx) * a.cosval + (v - tcy) * a.sinval;
+      const float srcY = scy + (v - tcy) * a.cosval - (u - tcx) * a.sinval;
+      const Px o = staged ? interpolate<FMT>(L, srcX, srcY, interp)
+                          : interpolate<FMT>(S, srcX, srcY, interp);
       store_px_row<FMT>(drow, x, o);
+    } else {
+      copy_px_raw<FMT>(drow, x, sbase + (int64_t)y * P.pitch, x);
     }
   }
 }
 
 void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
                         int interp, int count, hipStream_t st) {
-  int gx = src.P.H < 1 ? 1 : (src.P.H > 2048 ? 2048 : src.P.H);
+  const dim3 grid((src.P.W + kRotTW - 1) / kRotTW, (src.P.H + kRotTH - 1) / kRotTH, count);
   if (src.P.fmt == F_GRAY8)
-    hipLaunchKernelGGL(k_rotate_mask<F_GRAY8>, dim3(gx, 1, count), dim3(kThreads), 0, st, src,
-                       dst, args, interp);
+    hipLaunchKernelGGL(k_rotate_mask<F_GRAY8>, grid, dim3(kThreads), 0, st, src, dst, args,
+                       interp);
   else if (src.P.fmt == F_Y400A)
-    hipLaunchKernelGGL(k_rotate_mask<F_Y400A>, dim3(gx, 1, count), dim3(kThreads), 0, st, src,
-                       dst, args, interp);
+    hipLaunchKernelGGL(k_rotate_mask<F_Y400A>, grid, dim3(kThreads), 0, st, src, dst, args,
+                       interp);
   else
-    hipLaunchKernelGGL(k_rotate_mask<F_RGB24>, dim3(gx, 1, count), dim3(kThreads), 0, st, src,
-                       dst, args, interp);
+    hipLaunchKernelGGL(k_rotate_mask<F_RGB24>, grid, dim3(kThreads), 0, st, src, dst, args,
+                       interp);
 }
 
 __global__ void k_flip_if_active(SheetCtl* ctl, const int32_t* active, int64_t stride_ints,

@@ -97,11 +97,16 @@ __global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, cons
   for (int d0 = 0; d0 < maxDepth; d0 += 64) {
     const int dep = d0 + lane;
     int acc = 0;
+    // branch-free gather (out-of-mask/out-of-image points read pixel (0,0) and
+    // contribute 0, i.e. get_pixel's white), unrolled so several loads per
+    // lane are in flight
+#pragma unroll 8
     for (int i = w; i < scan; i += 4) {
       const int32_t x = px[i] + sxh * dep, y = py[i] + syv * dep;
-      if (x >= nm.x0 && x <= nm.x1 && y >= nm.y0 && y <= nm.y1 && x >= 0 && y >= 0 && x < g.W &&
-          y < g.H)
-        acc += 255 - dark_of(load_px_row<FMT>(base + (int64_t)y * img.P.pitch, x));
+      const bool ok = x >= nm.x0 && x <= nm.x1 && y >= nm.y0 && y <= nm.y1 && x >= 0 && y >= 0 &&
+                      x < g.W && y < g.H;
+      const Px p = load_px_row<FMT>(base + (int64_t)(ok ? y : 0) * img.P.pitch, ok ? x : 0);
+      acc += ok ? 255 - dark_of(p) : 0;
     }
     part[w][lane] = acc;
     __syncthreads();
