@@ -580,11 +580,13 @@ __global__ void __launch_bounds__(kThreads) k_rotate_mask(PlaneRef src, PlaneRef
       mny = fminf(mny, Y);
       mxy = fmaxf(mxy, Y);
     }
-    // taps: cubic (int)c-1 .. (int)c+2 (trunc), bilinear floor..ceil, NN round
-    bx0 = (int32_t)floorf(mnx) - 2;
-    by0 = (int32_t)floorf(mny) - 2;
-    bw = (int32_t)floorf(mxx) + 3 - bx0 + 1;
-    bh = (int32_t)floorf(mxy) + 3 - by0 + 1;
+    // taps: cubic (int)c-1 .. (int)c+2 (trunc, so up to floor+3 for negative
+    // c), bilinear floor..ceil, NN round; one more pixel each side absorbs
+    // the rounding of per-pixel coordinates against the corner values
+    bx0 = (int32_t)floorf(mnx) - 3;
+    by0 = (int32_t)floorf(mny) - 3;
+    bw = (int32_t)floorf(mxx) + 4 - bx0 + 1;
+    bh = (int32_t)floorf(mxy) + 4 - by0 + 1;
     staged = bw > 0 && bh > 0 && (int64_t)bw * bh <= kRotCap;
   }
   if (staged) {
@@ -632,6 +634,19 @@ __global__ void __launch_bounds__(kThreads) k_rotate_mask(PlaneRef src, PlaneRef
     if (u >= 0 && u < sw && v >= 0 && v < sh) {
       const float srcX = scx + (u - tcx) * a.cosval + (v - tcy) * a.sinval;
       const float srcY = scy + (v - tcy) * a.cosval - (u - tcx) * a.sinval;
+      if (FMT != F_RGB24 && staged && interp == UPHIP_INTERP_CUBIC) {
+        // gray bicubic straight from the window: the 4x4 taps of (int)srcX,
+        // (int)srcY lie inside it by construction of the bounding box
+        const int ix = (int)srcX, iy = (int)srcY;
+        const uint8_t* t = stage + (iy - 1 - by0) * bw + (ix - 1 - bx0);
+        const float fx = srcX - ix;
+        uint8_t col[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++, t += bw) col[r] = cubic_scale(fx, t[0], t[1], t[2], t[3]);
+        const uint8_t o = cubic_scale(srcY - iy, col[0], col[1], col[2], col[3]);
+        store_px_row<FMT>(drow, x, Px{o, o, o});
+        continue;
+      }
       const Px o = staged ? interpolate<FMT>(L, srcX, srcY, interp)
                           : interpolate<FMT>(S, srcX, srcY, interp);
       store_px_row<FMT>(drow, x, o);
