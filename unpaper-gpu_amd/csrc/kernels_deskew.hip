@@ -97,16 +97,35 @@ __global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, cons
   for (int d0 = 0; d0 < maxDepth; d0 += 64) {
     const int dep = d0 + lane;
     int acc = 0;
-    // branch-free gather (out-of-mask/out-of-image points read pixel (0,0) and
-    // contribute 0, i.e. get_pixel's white), unrolled so several loads per
-    // lane are in flight
+    if (syv == 0) {
+      // left/right edges: a point's row is the same for every lane (lanes are
+      // depths), so rows outside the mask/image are skipped uniformly and a
+      // lane only range-checks its column
+      const int32_t xlo = imax(nm.x0, 0), xhi = imin(nm.x1, g.W - 1);
+      const int32_t ylo = imax(nm.y0, 0), yhi = imin(nm.y1, g.H - 1);
+      const int32_t dx = sxh * dep;
+      const int iend = xlo <= xhi ? scan : 0;  // mask entirely off the image: all white
+#pragma unroll 4
+      for (int i = w; i < iend; i += 4) {
+        const int32_t y = __builtin_amdgcn_readfirstlane(py[i]);
+        if (y < ylo || y > yhi) continue;
+        const int32_t x = __builtin_amdgcn_readfirstlane(px[i]) + dx;
+        const bool ok = (uint32_t)(x - xlo) <= (uint32_t)(xhi - xlo);
+        const Px p = load_px_row<FMT>(base + (int64_t)y * img.P.pitch, ok ? x : xlo);
+        acc += ok ? 255 - dark_of(p) : 0;
+      }
+    } else {
+      // branch-free gather (out-of-mask/out-of-image points read pixel (0,0)
+      // and contribute 0, i.e. get_pixel's white), unrolled so several loads
+      // per lane are in flight
 #pragma unroll 8
-    for (int i = w; i < scan; i += 4) {
-      const int32_t x = px[i] + sxh * dep, y = py[i] + syv * dep;
-      const bool ok = x >= nm.x0 && x <= nm.x1 && y >= nm.y0 && y <= nm.y1 && x >= 0 && y >= 0 &&
-                      x < g.W && y < g.H;
-      const Px p = load_px_row<FMT>(base + (int64_t)(ok ? y : 0) * img.P.pitch, ok ? x : 0);
-      acc += ok ? 255 - dark_of(p) : 0;
+      for (int i = w; i < scan; i += 4) {
+        const int32_t x = px[i] + sxh * dep, y = py[i] + syv * dep;
+        const bool ok = x >= nm.x0 && x <= nm.x1 && y >= nm.y0 && y <= nm.y1 && x >= 0 &&
+                        y >= 0 && x < g.W && y < g.H;
+        const Px p = load_px_row<FMT>(base + (int64_t)(ok ? y : 0) * img.P.pitch, ok ? x : 0);
+        acc += ok ? 255 - dark_of(p) : 0;
+      }
     }
     part[w][lane] = acc;
     __syncthreads();
