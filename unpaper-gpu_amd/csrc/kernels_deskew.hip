@@ -94,38 +94,107 @@ __global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, cons
   const uint8_t* base = plane_ptr(img, s);
   const Rect nm = normalize(mask);
   int carry_acc = 0, last = 0, maxDiff = 0;  // wave 0 state
-  for (int d0 = 0; d0 < maxDepth; d0 += 64) {
-    const int dep = d0 + lane;
-    int acc = 0;
-    if (syv == 0) {
-      // left/right edges: a point's row is the same for every lane (lanes are
-      // depths), so rows outside the mask/image are skipped uniformly and a
-      // lane only range-checks its column
-      const int32_t xlo = imax(nm.x0, 0), xhi = imin(nm.x1, g.W - 1);
-      const int32_t ylo = imax(nm.y0, 0), yhi = imin(nm.y1, g.H - 1);
-      const int32_t dx = sxh * dep;
-      const int iend = xlo <= xhi ? scan : 0;  // mask entirely off the image: all white
+  if (syv == 0 && FMT == F_GRAY8) {
+    // left/right edges of a gray plane: lane owns 4 consecutive depths of a
+    // 256-depth chunk and reads them with two aligned dword loads per point
+    // (a point's row is uniform across the wave, so rows outside the mask or
+    // image are skipped with a scalar branch)
+    const int32_t xlo = imax(nm.x0, 0), xhi = imin(nm.x1, g.W - 1);
+    const int32_t ylo = imax(nm.y0, 0), yhi = imin(nm.y1, g.H - 1);
+    const int iend = xlo <= xhi ? scan : 0;   // mask entirely off the image: all white
+    const int64_t pitch = img.P.pitch;
+    __shared__ int32_t part4[4][256];
+    for (int d0 = 0; d0 < maxDepth; d0 += 256) {
+      int acc[4] = {0, 0, 0, 0};
+      const int32_t dl = d0 + 4 * lane;        // first depth of this lane
 #pragma unroll 4
       for (int i = w; i < iend; i += 4) {
         const int32_t y = __builtin_amdgcn_readfirstlane(py[i]);
         if (y < ylo || y > yhi) continue;
-        const int32_t x = __builtin_amdgcn_readfirstlane(px[i]) + dx;
-        const bool ok = (uint32_t)(x - xlo) <= (uint32_t)(xhi - xlo);
-        const Px p = load_px_row<FMT>(base + (int64_t)y * img.P.pitch, ok ? x : xlo);
-        acc += ok ? 255 - dark_of(p) : 0;
+        const int32_t xi = __builtin_amdgcn_readfirstlane(px[i]);
+        // depth k of this lane is at column xi + sxh*(dl + k)
+        const int32_t xs = sxh > 0 ? xi + dl : xi - dl - 3;   // lowest column of the 4
+        const uint8_t* row = base + (int64_t)y * pitch;
+        uint32_t v = 0;  // byte j = column xs + j (columns off the row read as 0)
+        if (xs >= 0 && xs + 8 <= pitch) {
+          const int32_t xa = xs & ~3;
+          const uint32_t* q = reinterpret_cast<const uint32_t*>(row + xa);
+          v = (uint32_t)((((uint64_t)q[1] << 32) | q[0]) >> (8 * (xs - xa)));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (xs + j >= 0 && xs + j < g.W) v |= (uint32_t)row[xs + j] << (8 * j);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int32_t x = sxh > 0 ? xs + k : xs + 3 - k;
+          const int bytei = sxh > 0 ? k : 3 - k;
+          const bool ok = (uint32_t)(x - xlo) <= (uint32_t)(xhi - xlo);
+          acc[k] += ok ? 255 - (int)((v >> (8 * bytei)) & 0xFF) : 0;
+        }
       }
-    } else {
-      // branch-free gather (out-of-mask/out-of-image points read pixel (0,0)
-      // and contribute 0, i.e. get_pixel's white), unrolled so several loads
-      // per lane are in flight
+#pragma unroll
+      for (int k = 0; k < 4; k++) part4[w][4 * lane + k] = acc[k];
+      __syncthreads();
+      if (w == 0) {
+        int B[4], pre[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          B[k] = part4[0][4 * lane + k] + part4[1][4 * lane + k] + part4[2][4 * lane + k] +
+                 part4[3][4 * lane + k];
+          pre[k] = (k ? pre[k - 1] : 0) + B[k];
+        }
+        int tot;
+        const int ex = carry_acc + iwave_prefix_excl(pre[3], &tot);
+        // first depth (in order) that does not execute: before >= maxAbs or dep >= maxDepth
+        int kfail = 4;
+#pragma unroll
+        for (int k = 3; k >= 0; k--) {
+          const int before = ex + (k ? pre[k - 1] : 0);
+          if (!(before < maxAbs && dl + k < maxDepth)) kfail = k;
+        }
+        const unsigned long long F = __ballot(kfail < 4);
+        const int fl = F ? __ffsll((long long)F) - 1 : 64;
+        const int stop = fl < 64 ? 4 * fl + __shfl(kfail, fl, 64) : 256;
+        const int up = __shfl_up(B[3], 1, 64);
+        int prev = lane == 0 ? last : up;
+        int md = INT_MIN;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          if (4 * lane + k < stop) md = max(md, B[k] - prev);
+          prev = B[k];
+        }
+        for (int o = 32; o > 0; o >>= 1) md = max(md, __shfl_xor(md, o, 64));
+        if (md > maxDiff) maxDiff = md;  // `if (diff >= maxDiff) maxDiff = diff`
+        if (stop < 256) {
+          if (lane == 0) {
+            result = (d0 + stop) < maxDepth ? maxDiff : 0;
+            done_flag = 1;
+          }
+        } else {
+          carry_acc += tot;
+          last = __shfl(B[3], 63, 64);
+        }
+      }
+      __syncthreads();
+      if (done_flag) break;
+    }
+    if (threadIdx.x == 0) *out = done_flag ? result : 0;
+    return;
+  }
+  for (int d0 = 0; d0 < maxDepth; d0 += 64) {
+    const int dep = d0 + lane;
+    int acc = 0;
+    // branch-free gather (out-of-mask/out-of-image points read pixel (0,0)
+    // and contribute 0, i.e. get_pixel's white), unrolled so several loads
+    // per lane are in flight
 #pragma unroll 8
-      for (int i = w; i < scan; i += 4) {
-        const int32_t x = px[i] + sxh * dep, y = py[i] + syv * dep;
-        const bool ok = x >= nm.x0 && x <= nm.x1 && y >= nm.y0 && y <= nm.y1 && x >= 0 &&
-                        y >= 0 && x < g.W && y < g.H;
-        const Px p = load_px_row<FMT>(base + (int64_t)(ok ? y : 0) * img.P.pitch, ok ? x : 0);
-        acc += ok ? 255 - dark_of(p) : 0;
-      }
+    for (int i = w; i < scan; i += 4) {
+      const int32_t x = px[i] + sxh * dep, y = py[i] + syv * dep;
+      const bool ok = x >= nm.x0 && x <= nm.x1 && y >= nm.y0 && y <= nm.y1 && x >= 0 && y >= 0 &&
+                      x < g.W && y < g.H;
+      const Px p = load_px_row<FMT>(base + (int64_t)(ok ? y : 0) * img.P.pitch, ok ? x : 0);
+      acc += ok ? 255 - dark_of(p) : 0;
     }
     part[w][lane] = acc;
     __syncthreads();
