@@ -26,7 +26,7 @@ __device__ __forceinline__ int iwave_prefix_excl(int v, int* total) {
 }
 
 template <int FMT>
-__global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, const RotTable* table,
+__global__ void __launch_bounds__(1024) k_rot_peaks(PlaneRef img, RotGeom g, const RotTable* table,
                                                    const Rect* masks, const int32_t* mask_active,
                                                    int mask_index, int32_t* peaks) {
   const int a = blockIdx.x, e = blockIdx.y, s = blockIdx.z;
@@ -70,7 +70,8 @@ __global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, cons
     stepY = -m;
   }
   extern __shared__ int32_t pts[];  // [scan] x, then [scan] y
-  __shared__ int32_t part[4][64];
+  constexpr int kMaxWaves = 16;
+  __shared__ int32_t part[kMaxWaves][64];
   __shared__ int32_t done_flag, result;
   if (scan <= 0) {
     if (threadIdx.x == 0) *out = 0;
@@ -90,7 +91,7 @@ __global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, cons
     result = 0;
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const uint8_t* base = plane_ptr(img, s);
   const Rect nm = normalize(mask);
   int carry_acc = 0, last = 0, maxDiff = 0;  // wave 0 state
@@ -103,14 +104,17 @@ __global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, cons
     const int32_t ylo = imax(nm.y0, 0), yhi = imin(nm.y1, g.H - 1);
     const int iend = xlo <= xhi ? scan : 0;   // mask entirely off the image: all white
     const int64_t pitch = img.P.pitch;
-    __shared__ int32_t part4[4][256];
+    __shared__ int32_t part4[kMaxWaves][256];
     for (int d0 = 0; d0 < maxDepth; d0 += 256) {
       int acc[4] = {0, 0, 0, 0};
       const int32_t dl = d0 + 4 * lane;        // first depth of this lane
-#pragma unroll 4
-      for (int i = w; i < iend; i += 4) {
-        const int32_t y = __builtin_amdgcn_readfirstlane(py[i]);
-        if (y < ylo || y > yhi) continue;
+      // branch-free: a row outside the mask/image is read at a valid row and
+      // masked, so the unrolled loads can all be in flight together
+#pragma unroll 8
+      for (int i = w; i < iend; i += nw) {
+        const int32_t yr = __builtin_amdgcn_readfirstlane(py[i]);
+        const bool rowok = yr >= ylo && yr <= yhi;
+        const int32_t y = rowok ? yr : ylo;
         const int32_t xi = __builtin_amdgcn_readfirstlane(px[i]);
         // depth k of this lane is at column xi + sxh*(dl + k)
         const int32_t xs = sxh > 0 ? xi + dl : xi - dl - 3;   // lowest column of the 4
@@ -129,7 +133,7 @@ __global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, cons
         for (int k = 0; k < 4; k++) {
           const int32_t x = sxh > 0 ? xs + k : xs + 3 - k;
           const int bytei = sxh > 0 ? k : 3 - k;
-          const bool ok = (uint32_t)(x - xlo) <= (uint32_t)(xhi - xlo);
+          const bool ok = rowok && (uint32_t)(x - xlo) <= (uint32_t)(xhi - xlo);
           acc[k] += ok ? 255 - (int)((v >> (8 * bytei)) & 0xFF) : 0;
         }
       }
@@ -140,8 +144,8 @@ __global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, cons
         int B[4], pre[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-          B[k] = part4[0][4 * lane + k] + part4[1][4 * lane + k] + part4[2][4 * lane + k] +
-                 part4[3][4 * lane + k];
+          B[k] = 0;
+          for (int q = 0; q < nw; q++) B[k] += part4[q][4 * lane + k];
           pre[k] = (k ? pre[k - 1] : 0) + B[k];
         }
         int tot;
@@ -189,7 +193,7 @@ __global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, cons
     // and contribute 0, i.e. get_pixel's white), unrolled so several loads
     // per lane are in flight
 #pragma unroll 8
-    for (int i = w; i < scan; i += 4) {
+    for (int i = w; i < scan; i += nw) {
       const int32_t x = px[i] + sxh * dep, y = py[i] + syv * dep;
       const bool ok = x >= nm.x0 && x <= nm.x1 && y >= nm.y0 && y <= nm.y1 && x >= 0 && y >= 0 &&
                       x < g.W && y < g.H;
@@ -199,7 +203,8 @@ __global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, cons
     part[w][lane] = acc;
     __syncthreads();
     if (w == 0) {
-      const int B = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+      int B = 0;
+      for (int q = 0; q < nw; q++) B += part[q][lane];
       int tot;
       const int before = carry_acc + iwave_prefix_excl(B, &tot);
       const bool exec = before < maxAbs && dep < maxDepth;
@@ -246,7 +251,7 @@ void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable
   }
   switch (img.P.fmt) {
     case F_GRAY8:
-      hipLaunchKernelGGL(k_rot_peaks<F_GRAY8>, grid, dim3(256), lds, st, img, g, table, masks,
+      hipLaunchKernelGGL(k_rot_peaks<F_GRAY8>, grid, dim3(1024), lds, st, img, g, table, masks,
                          mask_active, mask_index, peaks);
       break;
     case F_Y400A:
