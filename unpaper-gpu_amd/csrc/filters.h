@@ -97,7 +97,10 @@ struct RotGeom {
 // peaks[(sheet*max_masks + mask)*4 + edge][angle]
 void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable* table,
                            const Rect* masks, const int32_t* mask_active, int mask_index,
-                           int32_t* peaks, int count, hipStream_t st, int nangles, int max_scan);
+                           int32_t* peaks, int count, hipStream_t st, int nangles, int max_scan,
+                           int32_t* lines);
+// Scratch for the scan-line point lists of one launch_rotation_peaks call.
+size_t rotation_lines_bytes(int count, int nedges, int nangles, int max_scan);
 // Host: the angle sequence of detect_edge_rotation (deskew.c:153-174).
 int rotation_angles(const UphipDeskewParameters& p, RotTable* t);
 // Host: detect_rotation_cpu's combination of per-edge results (deskew.c:219-240)

@@ -25,10 +25,76 @@ __device__ __forceinline__ int iwave_prefix_excl(int v, int* total) {
   return pre - v;
 }
 
-template <int FMT>
-__global__ void __launch_bounds__(1024) k_rot_peaks(PlaneRef img, RotGeom g, const RotTable* table,
+// Geometry of one virtual scan line (detect_edge_rotation_peak,
+// deskew.c:48-112): point count, depth limit and the float recurrence start.
+struct LineSetup {
+  int scan, maxDepth;
+  float X, Y, stepX, stepY;
+};
+
+__device__ __forceinline__ LineSetup line_setup(const Rect& mask, const RotGeom& g, int sxh,
+                                                int syv, float m) {
+  LineSetup L;
+  const int32_t mw = iabs(mask.x0 - mask.x1) + 1, mh = iabs(mask.y0 - mask.y1) + 1;
+  int scan = g.scan_size, half, outer, mid, side;
+  if (syv == 0) {
+    if (scan == -1) scan = mh;
+    scan = imin(imin(scan, 10000), mh);
+    L.maxDepth = mw / 2;
+    half = scan / 2;
+    outer = (int)(fabsf(m) * half);
+    mid = mh / 2;
+    side = sxh > 0 ? mask.x0 - outer : mask.x1 + outer;
+    L.X = side + half * m;
+    L.Y = mask.y0 + mid - half;
+    L.stepX = -m;
+    L.stepY = 1.0;
+  } else {
+    if (scan == -1) scan = mw;
+    scan = imin(imin(scan, 10000), mw);
+    L.maxDepth = mh / 2;
+    half = scan / 2;
+    outer = (int)(fabsf(m) * half);
+    mid = mw / 2;
+    side = syv > 0 ? mask.x0 - outer : mask.x1 + outer;  // x-vertices (deskew.c:96-97)
+    L.X = mask.x0 + mid - half;
+    L.Y = side - (half * m);
+    L.stepX = 1.0;
+    L.stepY = -m;
+  }
+  L.scan = scan;
+  return L;
+}
+
+// The point lists of every (sheet, edge, angle) line: one lane per line runs
+// the float recurrence of deskew.c:107-112 in order.  Point i of line t is
+// stored at pts[(2i + c) * nlines + t] (c = 0: x, 1: y) so a wave's stores
+// are contiguous.
+__global__ void __launch_bounds__(64) k_rot_points(RotGeom g, const RotTable* table,
                                                    const Rect* masks, const int32_t* mask_active,
-                                                   int mask_index, int32_t* peaks) {
+                                                   int count, int32_t* pts) {
+  const int na = table->nangles;
+  const int nlines = count * g.nedges * na;
+  const int t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= nlines) return;
+  const int a = t % na, e = (t / na) % g.nedges, s = t / (na * g.nedges);
+  if (mask_active && !mask_active[s]) return;
+  const LineSetup L = line_setup(masks[s], g, g.edge_shift[e][0], g.edge_shift[e][1],
+                                 table->slope[a]);
+  float X = L.X, Y = L.Y;
+  for (int i = 0; i < L.scan; i++) {
+    pts[(int64_t)(2 * i) * nlines + t] = (int)X;
+    pts[(int64_t)(2 * i + 1) * nlines + t] = (int)Y;
+    X += L.stepX;
+    Y += L.stepY;
+  }
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, const RotTable* table,
+                                                  const Rect* masks, const int32_t* mask_active,
+                                                  int mask_index, int32_t* peaks,
+                                                  const int32_t* lines, int count) {
   const int a = blockIdx.x, e = blockIdx.y, s = blockIdx.z;
   const int na = table->nangles;
   int32_t* out = peaks + (((int64_t)s * g.max_masks + mask_index) * 4 + e) * na + a;
@@ -39,38 +105,11 @@ __global__ void __launch_bounds__(1024) k_rot_peaks(PlaneRef img, RotGeom g, con
   const Rect mask = masks[s];
   const int sxh = g.edge_shift[e][0], syv = g.edge_shift[e][1];
   const float m = table->slope[a];
-  // detect_edge_rotation_peak, deskew.c:48-146
-  const int32_t mw = iabs(mask.x0 - mask.x1) + 1, mh = iabs(mask.y0 - mask.y1) + 1;
   const int maxAbs = (int)(255 * g.scan_size * g.scan_depth);
-  int scan = g.scan_size, maxDepth, half, outer, mid, side;
-  float X, Y, stepX, stepY;
-  if (syv == 0) {
-    if (scan == -1) scan = mh;
-    scan = imin(imin(scan, 10000), mh);
-    maxDepth = mw / 2;
-    half = scan / 2;
-    outer = (int)(fabsf(m) * half);
-    mid = mh / 2;
-    side = sxh > 0 ? mask.x0 - outer : mask.x1 + outer;
-    X = side + half * m;
-    Y = mask.y0 + mid - half;
-    stepX = -m;
-    stepY = 1.0;
-  } else {
-    if (scan == -1) scan = mw;
-    scan = imin(imin(scan, 10000), mw);
-    maxDepth = mh / 2;
-    half = scan / 2;
-    outer = (int)(fabsf(m) * half);
-    mid = mw / 2;
-    side = syv > 0 ? mask.x0 - outer : mask.x1 + outer;  // x-vertices (deskew.c:96-97)
-    X = mask.x0 + mid - half;
-    Y = side - (half * m);
-    stepX = 1.0;
-    stepY = -m;
-  }
+  const LineSetup LS = line_setup(mask, g, sxh, syv, m);
+  const int scan = LS.scan, maxDepth = LS.maxDepth;
   extern __shared__ int32_t pts[];  // [scan] x, then [scan] y
-  constexpr int kMaxWaves = 16;
+  constexpr int kMaxWaves = 4;
   __shared__ int32_t part[kMaxWaves][64];
   __shared__ int32_t done_flag, result;
   if (scan <= 0) {
@@ -79,14 +118,15 @@ __global__ void __launch_bounds__(1024) k_rot_peaks(PlaneRef img, RotGeom g, con
   }
   int32_t* px = pts;
   int32_t* py = pts + scan;
-  if (threadIdx.x == 0) {
-    // the float recurrence of deskew.c:107-112, in order
-    for (int i = 0; i < scan; i++) {
-      px[i] = (int)X;
-      py[i] = (int)Y;
-      X += stepX;
-      Y += stepY;
+  {
+    const int nlines = count * g.nedges * na;
+    const int t = (s * g.nedges + e) * na + a;
+    for (int i = threadIdx.x; i < scan; i += blockDim.x) {
+      px[i] = lines[(int64_t)(2 * i) * nlines + t];
+      py[i] = lines[(int64_t)(2 * i + 1) * nlines + t];
     }
+  }
+  if (threadIdx.x == 0) {
     done_flag = 0;
     result = 0;
   }
@@ -234,11 +274,18 @@ __global__ void __launch_bounds__(1024) k_rot_peaks(PlaneRef img, RotGeom g, con
   if (threadIdx.x == 0) *out = done_flag ? result : 0;
 }
 
+size_t rotation_lines_bytes(int count, int nedges, int nangles, int max_scan) {
+  return sizeof(int32_t) * 2 * (size_t)(max_scan > 0 ? max_scan : 1) * count * nedges * nangles;
+}
+
 void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable* table,
                            const Rect* masks, const int32_t* mask_active, int mask_index,
                            int32_t* peaks, int count, hipStream_t st, int nangles,
-                           int max_scan) {
+                           int max_scan, int32_t* lines) {
   if (g.nedges <= 0 || nangles <= 0) return;
+  const int nlines = count * g.nedges * nangles;
+  hipLaunchKernelGGL(k_rot_points, dim3((nlines + 63) / 64), dim3(64), 0, st, g, table, masks,
+                     mask_active, count, lines);
   dim3 grid(nangles, g.nedges, count);
   const size_t lds = sizeof(int32_t) * 2 * (size_t)(max_scan > 0 ? max_scan : 1);
   if (lds > 64 * 1024) {
@@ -251,16 +298,16 @@ void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable
   }
   switch (img.P.fmt) {
     case F_GRAY8:
-      hipLaunchKernelGGL(k_rot_peaks<F_GRAY8>, grid, dim3(1024), lds, st, img, g, table, masks,
-                         mask_active, mask_index, peaks);
+      hipLaunchKernelGGL(k_rot_peaks<F_GRAY8>, grid, dim3(256), lds, st, img, g, table, masks,
+                         mask_active, mask_index, peaks, lines, count);
       break;
     case F_Y400A:
       hipLaunchKernelGGL(k_rot_peaks<F_Y400A>, grid, dim3(256), lds, st, img, g, table, masks,
-                         mask_active, mask_index, peaks);
+                         mask_active, mask_index, peaks, lines, count);
       break;
     default:
       hipLaunchKernelGGL(k_rot_peaks<F_RGB24>, grid, dim3(256), lds, st, img, g, table, masks,
-                         mask_active, mask_index, peaks);
+                         mask_active, mask_index, peaks, lines, count);
       break;
   }
 }

@@ -137,7 +137,10 @@ float uphip_detect_rotation(UphipImage image, UphipRectangle mask,
   const int32_t mw = iabs(m.x0 - m.x1) + 1, mh = iabs(m.y0 - m.y1) + 1;
   int max_scan = params.deskewScanSize == -1 ? imax(mw, mh) : params.deskewScanSize;
   max_scan = imin(imin(max_scan, 10000), imax(mw, mh));
-  launch_rotation_peaks(ref1(image.frame), g, dt, dm, nullptr, 0, peaks, 1, st, na, max_scan);
+  int32_t* lines = (int32_t*)scratch(7, rotation_lines_bytes(1, g.nedges, na, max_scan));
+  if (!lines) return 0.0f;
+  launch_rotation_peaks(ref1(image.frame), g, dt, dm, nullptr, 0, peaks, 1, st, na, max_scan,
+                        lines);
   std::vector<int32_t> hp(4 * (size_t)(na > 0 ? na : 1));
   UPH_HIP(hipMemcpyAsync(hp.data(), peaks, sizeof(int32_t) * g.nedges * na,
                          hipMemcpyDeviceToHost, st));

@@ -316,6 +316,7 @@ struct UphipBatch {
   RotCombo* dcombo = nullptr;
   int max_scan = 0;
   int32_t* peaks = nullptr;
+  int32_t* rot_lines = nullptr;  // scan-line point lists (k_rot_points)
   Rect* pick_mask = nullptr;
   int32_t* pick_active = nullptr;
   RotateArgs* rot_args = nullptr;
@@ -666,6 +667,8 @@ static bool allocate(UphipBatch* b) {
     int ms = o.deskew_parameters.deskewScanSize;
     if (ms == -1 || ms > 10000) ms = 10000;
     b->max_scan = imin(ms, imax(W, H));
+    b->rot_lines = (int32_t*)dalloc<uint8_t>(b, rotation_lines_bytes(cap, nedges, na, b->max_scan));
+    if (!b->rot_lines) return false;
   }
   return true;
 }
@@ -1042,7 +1045,8 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
       hipLaunchKernelGGL(k_mask_pick, dim3((count + 255) / 256), dim3(256), 0, b->st, b->ctl,
                          (int)i, b->pick_mask, b->pick_active, count);
       launch_rotation_peaks(cur_ref(P, b->ctl), rg, b->dtable, b->pick_mask, b->pick_active,
-                            (int)i, b->peaks, count, b->st, b->table.nangles, b->max_scan);
+                            (int)i, b->peaks, count, b->st, b->table.nangles, b->max_scan,
+                            b->rot_lines);
       ra.mask_index = (int)i;
       hipLaunchKernelGGL(k_rot_select, dim3((count + 255) / 256), dim3(256), 0, b->st, b->ctl,
                          b->peaks, b->dtable, b->dcombo, ra, b->rot_args, count);
