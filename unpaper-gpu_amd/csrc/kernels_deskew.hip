@@ -158,23 +158,18 @@ __global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, cons
         const int32_t xi = __builtin_amdgcn_readfirstlane(px[i]);
         // depth k of this lane is at column xi + sxh*(dl + k)
         const int32_t xs = sxh > 0 ? xi + dl : xi - dl - 3;   // lowest column of the 4
-        const uint8_t* row = base + (int64_t)y * pitch;
-        uint32_t v = 0;  // byte j = column xs + j (columns off the row read as 0)
-        if (xs >= 0 && xs + 8 <= pitch) {
-          const int32_t xa = xs & ~3;
-          const uint32_t* q = reinterpret_cast<const uint32_t*>(row + xa);
-          v = (uint32_t)((((uint64_t)q[1] << 32) | q[0]) >> (8 * (xs - xa)));
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; j++)
-            if (xs + j >= 0 && xs + j < g.W) v |= (uint32_t)row[xs + j] << (8 * j);
-        }
+        // one unconditional aligned 8-byte window per lane (no divergent
+        // branch around the loads, so the unrolled points' loads overlap);
+        // every in-range column of the lane lies inside it
+        const int32_t xa = imin(imax(xs, 0), (int32_t)pitch - 8) & ~3;
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(base + (int64_t)y * pitch + xa);
+        const uint64_t V = ((uint64_t)q[1] << 32) | q[0];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           const int32_t x = sxh > 0 ? xs + k : xs + 3 - k;
-          const int bytei = sxh > 0 ? k : 3 - k;
           const bool ok = rowok && (uint32_t)(x - xlo) <= (uint32_t)(xhi - xlo);
-          acc[k] += ok ? 255 - (int)((v >> (8 * bytei)) & 0xFF) : 0;
+          const int b = (int)((V >> ((8 * (x - xa)) & 63)) & 0xFF);
+          acc[k] += (255 - b) & -(int)ok;  // arithmetic mask: the load is never sunk into a branch
         }
       }
 #pragma unroll
@@ -235,10 +230,10 @@ __global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, cons
 #pragma unroll 8
     for (int i = w; i < scan; i += nw) {
       const int32_t x = px[i] + sxh * dep, y = py[i] + syv * dep;
-      const bool ok = x >= nm.x0 && x <= nm.x1 && y >= nm.y0 && y <= nm.y1 && x >= 0 && y >= 0 &&
-                      x < g.W && y < g.H;
+      const bool ok = (x >= nm.x0) & (x <= nm.x1) & (y >= nm.y0) & (y <= nm.y1) & (x >= 0) &
+                      (y >= 0) & (x < g.W) & (y < g.H);
       const Px p = load_px_row<FMT>(base + (int64_t)(ok ? y : 0) * img.P.pitch, ok ? x : 0);
-      acc += ok ? 255 - dark_of(p) : 0;
+      acc += (255 - (int)dark_of(p)) & -(int)ok;
     }
     part[w][lane] = acc;
     __syncthreads();
