@@ -264,3 +264,24 @@ def test_detect_rotation_pages(hip, oracle, fmt, deg, mask):
     r1 = hip.detect_rotation(hip.upload(h), A.rect(*mask), p)
     r2 = oracle.detect_rotation(h, A.rect(*mask), p)
     assert np.float32(r1).tobytes() == np.float32(r2).tobytes()
+
+
+@pytest.mark.parametrize("fmt", [A.FMT_GRAY8, A.FMT_RGB24])
+@pytest.mark.parametrize("case", ["wide_margin", "wide_range", "scan_all"])
+def test_detect_rotation_fallbacks(hip, oracle, fmt, case):
+    """Lines the band path cannot finish: content > 128 steps from the mask
+    edge, a 40 degree range whose band does not fit LDS, and scan size -1."""
+    margin = 330 if case == "wide_margin" else 90
+    h = make_image(1200, 900, fmt, seed=21, margin=margin)
+    oracle.deskew(h, A.rect(0, 0, 1199, 899), float(np.float32(1.7 * math.pi / 180)),
+                  A.INTERP_LINEAR)
+    if case == "wide_range":
+        p = deskew_params(oracle, rng=40.0, step=2.0, dev=90.0, size=1500)
+    elif case == "scan_all":
+        p = deskew_params(oracle, size=-1, dev=10.0)
+    else:
+        p = deskew_params(oracle, size=1500, dev=10.0)
+    mask = A.rect(0, 0, 1199, 899)
+    r1 = hip.detect_rotation(hip.upload(h), mask, p)
+    r2 = oracle.detect_rotation(h, mask, p)
+    assert np.float32(r1).tobytes() == np.float32(r2).tobytes()

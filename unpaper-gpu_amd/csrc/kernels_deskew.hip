@@ -1,18 +1,34 @@
 // kernels_deskew.hip — rotation detection (deskew.c:48-241).
 //
-// One workgroup per (sheet, edge, angle).  The reference walks a 1500-point
-// virtual line inward one pixel per step, summing 255-max(rgb) under the line,
-// until the accumulated blackness reaches 255*size*depth; the peak is the
-// largest step-to-step increase.  Here the four waves split the line points
-// and each lane owns one inward step of a 64-step chunk, so a wave reads 64
-// consecutive pixels of one image row per point (one coalesced load) and the
-// stopping rule is evaluated on the chunk with a wave prefix sum.
+// The reference walks, for every angle and enabled edge, a virtual line of up
+// to 1500 points inward one pixel per step, summing 255-max(rgb) under the
+// line, until the accumulated blackness reaches 255*size*depth; the peak is
+// the largest step-to-step increase (detect_edge_rotation_peak).
+//
+// For the left/right edges (the default) the line's rows do not depend on
+// the angle: point i sits on row Ystart+i for every angle, only its column
+// (int)X_i differs.  So all angles and the first kDepth steps read one band
+// of columns beside the mask edge.  The fast path is
+//   k_rot_points  the float recurrence X += -m of every line, in order
+//                 (deskew.c:107-112), one lane per line -> column lists;
+//   k_rot_band    one workgroup per 128-row slice of a (sheet, edge): the
+//                 slice's band is staged in LDS as per-pixel blackness, then
+//                 every angle x kDepth steps is summed from LDS -> partials;
+//   k_rot_final   one wave per line: slice partials -> blackness per step,
+//                 then the reference's stopping rule and peak, exactly.
+// Lines that do not stop within kDepth steps, top/bottom edges (rows move
+// with the step) and bands too wide for LDS (very large angle ranges) are
+// flagged and walked by k_rot_line, a direct per-line restatement.
 #include <climits>
 #include <cmath>
 
 #include "filters.h"
 
 namespace uph {
+
+constexpr int kDepth = 128;        // steps covered by the band path (2 per lane)
+constexpr int kSliceRows = 128;    // rows per band slice
+constexpr int kBandBytes = 48 * 1024;
 
 __device__ __forceinline__ int iwave_prefix_excl(int v, int* total) {
   const int lane = threadIdx.x & 63;
@@ -66,51 +82,250 @@ __device__ __forceinline__ LineSetup line_setup(const Rect& mask, const RotGeom&
   return L;
 }
 
-// The point lists of every (sheet, edge, angle) line: one lane per line runs
-// the float recurrence of deskew.c:107-112 in order.  Point i of line t is
-// stored at pts[(2i + c) * nlines + t] (c = 0: x, 1: y) so a wave's stores
-// are contiguous.
+// Scratch layout of one launch (all int32):
+//   cols   [nlines][max_scan]   column of point i of each left/right line
+//   ends   [nlines][2]          first and last column of the line
+//   part   [nlines][nslices][kDepth]  band slice sums
+//   flag   [nlines]             1 = walk the line directly (k_rot_line)
+struct RotScratch {
+  int32_t *cols, *ends, *part, *flag;
+};
+
+__host__ __device__ static inline int rot_slices(int max_scan) { return (max_scan + kSliceRows - 1) / kSliceRows; }
+
+__host__ __device__ static inline RotScratch rot_scratch(int32_t* base, int nlines, int max_scan) {
+  RotScratch r;
+  const int64_t ms = max_scan > 0 ? max_scan : 1;
+  const int64_t ns = (ms + kSliceRows - 1) / kSliceRows;
+  r.cols = base;
+  r.ends = r.cols + (int64_t)nlines * ms;
+  r.part = r.ends + 2 * (int64_t)nlines;
+  r.flag = r.part + (int64_t)nlines * ns * kDepth;
+  return r;
+}
+
+size_t rotation_lines_bytes(int count, int nedges, int nangles, int max_scan) {
+  const int64_t nlines = (int64_t)count * nedges * nangles;
+  const int64_t ms = max_scan > 0 ? max_scan : 1;
+  const int64_t ns = (ms + kSliceRows - 1) / kSliceRows;
+  return sizeof(int32_t) * (size_t)(nlines * ms + 2 * nlines + nlines * ns * kDepth + nlines);
+}
+
+// ---- k_rot_points: one lane per left/right line, the recurrence in order --
 __global__ void __launch_bounds__(64) k_rot_points(RotGeom g, const RotTable* table,
                                                    const Rect* masks, const int32_t* mask_active,
-                                                   int count, int32_t* pts) {
+                                                   int count, int max_scan, RotScratch R) {
   const int na = table->nangles;
   const int nlines = count * g.nedges * na;
-  const int t = blockIdx.x * 64 + threadIdx.x;
-  if (t >= nlines) return;
-  const int a = t % na, e = (t / na) % g.nedges, s = t / (na * g.nedges);
-  if (mask_active && !mask_active[s]) return;
-  const LineSetup L = line_setup(masks[s], g, g.edge_shift[e][0], g.edge_shift[e][1],
-                                 table->slope[a]);
-  float X = L.X, Y = L.Y;
-  for (int i = 0; i < L.scan; i++) {
-    pts[(int64_t)(2 * i) * nlines + t] = (int)X;
-    pts[(int64_t)(2 * i + 1) * nlines + t] = (int)Y;
-    X += L.stepX;
-    Y += L.stepY;
+  const int t0 = blockIdx.x * 64, t = t0 + threadIdx.x;
+  __shared__ int32_t tile[64][65];
+  bool live = t < nlines;
+  int a = 0, e = 0, s = 0;
+  if (live) {
+    a = t % na;
+    e = (t / na) % g.nedges;
+    s = t / (na * g.nedges);
+    live = !(mask_active && !mask_active[s]) && g.edge_shift[e][1] == 0;
+  }
+  LineSetup L{0, 0, 0.0f, 0.0f, 0.0f, 0.0f};
+  if (live) L = line_setup(masks[s], g, g.edge_shift[e][0], 0, table->slope[a]);
+  const int scan = live ? L.scan : 0;
+  float X = L.X;
+  int first = 0, last = 0;
+  // 64 points per round go through the LDS tile so that each line's points
+  // are written as one contiguous run
+  int maxscan_blk = scan;
+  for (int o = 32; o > 0; o >>= 1) maxscan_blk = max(maxscan_blk, __shfl_xor(maxscan_blk, o, 64));
+  for (int c0 = 0; c0 < maxscan_blk; c0 += 64) {
+    for (int j = 0; j < 64; j++) {
+      const int i = c0 + j;
+      if (i < scan) {
+        const int x = (int)X;
+        tile[threadIdx.x][j] = x;
+        if (i == 0) first = x;
+        last = x;
+        X += L.stepX;
+      }
+    }
+    __syncthreads();
+    for (int l = 0; l < 64; l++) {
+      const int tl = t0 + l;
+      if (tl >= nlines) break;
+      const int i = c0 + threadIdx.x;
+      if (i < max_scan) R.cols[(int64_t)tl * max_scan + i] = tile[l][threadIdx.x];
+    }
+    __syncthreads();
+  }
+  if (t < nlines) {
+    R.ends[2 * t] = first;
+    R.ends[2 * t + 1] = last;
+    R.flag[t] = live ? 0 : 1;
   }
 }
 
+// Band of one (sheet, edge): columns [bx0, bx0 + bw) cover every point of
+// every angle for steps 0..kDepth-1.  Returns false when it does not fit.
+__device__ __forceinline__ bool band_range(const RotScratch& R, int tbase, int na, int sxh,
+                                           int32_t* bx0, int32_t* bw) {
+  int32_t lo = INT_MAX, hi = INT_MIN;
+  for (int a = 0; a < na; a++) {
+    const int32_t f = R.ends[2 * (tbase + a)], l = R.ends[2 * (tbase + a) + 1];
+    lo = imin(lo, imin(f, l));
+    hi = imax(hi, imax(f, l));
+  }
+  if (sxh > 0) hi += kDepth - 1;
+  else lo -= kDepth - 1;
+  *bx0 = lo;
+  *bw = hi - lo + 1;
+  return (int64_t)*bw * kSliceRows <= kBandBytes;
+}
+
+// ---- k_rot_band: slice sums of every angle x kDepth steps -----------------
 template <int FMT>
-__global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, const RotTable* table,
+__global__ void __launch_bounds__(256) k_rot_band(PlaneRef img, RotGeom g, const RotTable* table,
                                                   const Rect* masks, const int32_t* mask_active,
-                                                  int mask_index, int32_t* peaks,
-                                                  const int32_t* lines, int count) {
-  const int a = blockIdx.x, e = blockIdx.y, s = blockIdx.z;
+                                                  int count, int max_scan, RotScratch R) {
+  const int sl = blockIdx.x, e = blockIdx.y, s = blockIdx.z;
   const int na = table->nangles;
+  const int sxh = g.edge_shift[e][0];
+  if (g.edge_shift[e][1] != 0 || (mask_active && !mask_active[s])) return;
+  const Rect mask = masks[s];
+  const LineSetup LS = line_setup(mask, g, sxh, 0, 0.0f);  // scan, Ystart: angle independent
+  const int i0 = sl * kSliceRows, i1 = imin(LS.scan, i0 + kSliceRows);
+  if (i0 >= i1) return;
+  const int tbase = (s * g.nedges + e) * na;
+  int32_t bx0, bw;
+  if (!band_range(R, tbase, na, sxh, &bx0, &bw)) return;  // k_rot_final flags the lines
+  __shared__ uint8_t band[kBandBytes];
+  const Rect nm = normalize(mask);
+  const int32_t xlo = imax(nm.x0, 0), xhi = imin(nm.x1, g.W - 1);
+  const int32_t ylo = imax(nm.y0, 0), yhi = imin(nm.y1, g.H - 1);
+  const int32_t ystart = (int32_t)LS.Y;  // exact: integer start, +1.0 per point
+  const uint8_t* base = plane_ptr(img, s);
+  const int rows = i1 - i0, n = rows * bw;
+  // stage blackness 255-max(rgb) of in-mask, in-image pixels (0 elsewhere,
+  // get_pixel's white); unconditional clamped loads, masked arithmetically
+  for (int b0 = 0; b0 < n; b0 += 8 * 256) {
+    uint8_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int q = b0 + k * 256 + threadIdx.x;
+      const int r = q / bw, c = q - r * bw;
+      const int32_t y = ystart + i0 + r, x = bx0 + c;
+      const bool ok = (q < n) & (y >= ylo) & (y <= yhi) & (x >= xlo) & (x <= xhi);
+      const Px p = load_px_row<FMT>(base + (int64_t)(ok ? y : ylo) * img.P.pitch, ok ? x : xlo);
+      v[k] = (uint8_t)((255 - dark_of(p)) & -(int)ok);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int q = b0 + k * 256 + threadIdx.x;
+      if (q < n) band[q] = v[k];
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int d0 = lane, d1 = lane + 64;
+  const int32_t o0 = sxh * d0 - bx0, o1 = sxh * d1 - bx0;
+  const int ns = rot_slices(max_scan);
+  for (int a = w; a < na; a += 4) {
+    const int t = tbase + a;
+    const int32_t* cols = R.cols + (int64_t)t * max_scan;
+    int acc0 = 0, acc1 = 0;
+    const uint8_t* row = band;
+#pragma unroll 8
+    for (int i = i0; i < i1; i++, row += bw) {
+      const int32_t x = cols[i];  // uniform
+      acc0 += row[x + o0];
+      acc1 += row[x + o1];
+    }
+    int32_t* P = R.part + ((int64_t)t * ns + sl) * kDepth;
+    P[d0] = acc0;
+    P[d1] = acc1;
+  }
+}
+
+// ---- k_rot_final: the stopping rule on the summed steps, one wave per line --
+__global__ void __launch_bounds__(256) k_rot_final(RotGeom g, const RotTable* table,
+                                                   const Rect* masks, const int32_t* mask_active,
+                                                   int mask_index, int32_t* peaks, int count,
+                                                   int max_scan, RotScratch R) {
+  const int na = table->nangles;
+  const int nlines = count * g.nedges * na;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (t >= nlines) return;
+  const int a = t % na, e = (t / na) % g.nedges, s = t / (na * g.nedges);
   int32_t* out = peaks + (((int64_t)s * g.max_masks + mask_index) * 4 + e) * na + a;
   if (mask_active && !mask_active[s]) {
-    if (threadIdx.x == 0) *out = 0;
+    if (lane == 0) *out = 0;
     return;
   }
+  if (R.flag[t]) return;  // top/bottom edge: k_rot_line
+  const int sxh = g.edge_shift[e][0];
+  const LineSetup LS = line_setup(masks[s], g, sxh, 0, table->slope[a]);
+  int32_t bx0, bw;
+  if (LS.scan <= 0) {
+    if (lane == 0) *out = 0;
+    return;
+  }
+  if (!band_range(R, (s * g.nedges + e) * na, na, sxh, &bx0, &bw)) {
+    if (lane == 0) R.flag[t] = 1;
+    return;
+  }
+  const int ns = rot_slices(max_scan), nsl = (LS.scan + kSliceRows - 1) / kSliceRows;
+  int B[2] = {0, 0};
+  for (int q = 0; q < nsl; q++) {
+    const int32_t* P = R.part + ((int64_t)t * ns + q) * kDepth;
+    B[0] += P[2 * lane];
+    B[1] += P[2 * lane + 1];
+  }
+  // steps 2*lane, 2*lane+1 (deskew.c:114-146)
+  const int maxAbs = (int)(255 * g.scan_size * g.scan_depth);
+  const int pre1 = B[0] + B[1];
+  int tot;
+  const int ex = iwave_prefix_excl(pre1, &tot);
+  int kfail = 2;
+  for (int k = 1; k >= 0; k--) {
+    const int before = ex + (k ? B[0] : 0);
+    if (!(before < maxAbs && 2 * lane + k < LS.maxDepth)) kfail = k;
+  }
+  const unsigned long long F = __ballot(kfail < 2);
+  if (!F) {  // still accumulating after kDepth steps: walk the line directly
+    if (lane == 0) R.flag[t] = 1;
+    return;
+  }
+  const int fl = __ffsll((long long)F) - 1;
+  const int stop = 2 * fl + __shfl(kfail, fl, 64);
+  const int up = __shfl_up(B[1], 1, 64);
+  int prev = lane == 0 ? 0 : up;  // `last` starts at 0
+  int md = INT_MIN;
+  for (int k = 0; k < 2; k++) {
+    if (2 * lane + k < stop) md = max(md, B[k] - prev);
+    prev = B[k];
+  }
+  for (int o = 32; o > 0; o >>= 1) md = max(md, __shfl_xor(md, o, 64));
+  const int maxDiff = md > 0 ? md : 0;  // maxDiff starts at 0, `diff >= maxDiff`
+  if (lane == 0) *out = stop < LS.maxDepth ? maxDiff : 0;
+}
+
+// ---- k_rot_line: direct walk of one flagged line (any edge) ---------------
+template <int FMT>
+__global__ void __launch_bounds__(256) k_rot_line(PlaneRef img, RotGeom g, const RotTable* table,
+                                                  const Rect* masks, const int32_t* mask_active,
+                                                  int mask_index, int32_t* peaks, int count,
+                                                  int max_scan, RotScratch R) {
+  const int a = blockIdx.x, e = blockIdx.y, s = blockIdx.z;
+  const int na = table->nangles;
+  const int t = (s * g.nedges + e) * na + a;
+  if (!R.flag[t] || (mask_active && !mask_active[s])) return;
+  int32_t* out = peaks + (((int64_t)s * g.max_masks + mask_index) * 4 + e) * na + a;
   const Rect mask = masks[s];
   const int sxh = g.edge_shift[e][0], syv = g.edge_shift[e][1];
-  const float m = table->slope[a];
-  const int maxAbs = (int)(255 * g.scan_size * g.scan_depth);
-  const LineSetup LS = line_setup(mask, g, sxh, syv, m);
+  const LineSetup LS = line_setup(mask, g, sxh, syv, table->slope[a]);
   const int scan = LS.scan, maxDepth = LS.maxDepth;
+  const int maxAbs = (int)(255 * g.scan_size * g.scan_depth);
   extern __shared__ int32_t pts[];  // [scan] x, then [scan] y
-  constexpr int kMaxWaves = 4;
-  __shared__ int32_t part[kMaxWaves][64];
+  __shared__ int32_t part[4][64];
   __shared__ int32_t done_flag, result;
   if (scan <= 0) {
     if (threadIdx.x == 0) *out = 0;
@@ -118,117 +333,30 @@ __global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, cons
   }
   int32_t* px = pts;
   int32_t* py = pts + scan;
-  {
-    const int nlines = count * g.nedges * na;
-    const int t = (s * g.nedges + e) * na + a;
-    for (int i = threadIdx.x; i < scan; i += blockDim.x) {
-      px[i] = lines[(int64_t)(2 * i) * nlines + t];
-      py[i] = lines[(int64_t)(2 * i + 1) * nlines + t];
-    }
-  }
   if (threadIdx.x == 0) {
+    // the float recurrence of deskew.c:107-112, in order
+    float X = LS.X, Y = LS.Y;
+    for (int i = 0; i < scan; i++) {
+      px[i] = (int)X;
+      py[i] = (int)Y;
+      X += LS.stepX;
+      Y += LS.stepY;
+    }
     done_flag = 0;
     result = 0;
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint8_t* base = plane_ptr(img, s);
   const Rect nm = normalize(mask);
   int carry_acc = 0, last = 0, maxDiff = 0;  // wave 0 state
-  if (syv == 0 && FMT == F_GRAY8) {
-    // left/right edges of a gray plane: lane owns 4 consecutive depths of a
-    // 256-depth chunk and reads them with two aligned dword loads per point
-    // (a point's row is uniform across the wave, so rows outside the mask or
-    // image are skipped with a scalar branch)
-    const int32_t xlo = imax(nm.x0, 0), xhi = imin(nm.x1, g.W - 1);
-    const int32_t ylo = imax(nm.y0, 0), yhi = imin(nm.y1, g.H - 1);
-    const int iend = xlo <= xhi ? scan : 0;   // mask entirely off the image: all white
-    const int64_t pitch = img.P.pitch;
-    __shared__ int32_t part4[kMaxWaves][256];
-    for (int d0 = 0; d0 < maxDepth; d0 += 256) {
-      int acc[4] = {0, 0, 0, 0};
-      const int32_t dl = d0 + 4 * lane;        // first depth of this lane
-      // branch-free: a row outside the mask/image is read at a valid row and
-      // masked, so the unrolled loads can all be in flight together
-#pragma unroll 8
-      for (int i = w; i < iend; i += nw) {
-        const int32_t yr = __builtin_amdgcn_readfirstlane(py[i]);
-        const bool rowok = yr >= ylo && yr <= yhi;
-        const int32_t y = rowok ? yr : ylo;
-        const int32_t xi = __builtin_amdgcn_readfirstlane(px[i]);
-        // depth k of this lane is at column xi + sxh*(dl + k)
-        const int32_t xs = sxh > 0 ? xi + dl : xi - dl - 3;   // lowest column of the 4
-        // one unconditional aligned 8-byte window per lane (no divergent
-        // branch around the loads, so the unrolled points' loads overlap);
-        // every in-range column of the lane lies inside it
-        const int32_t xa = imin(imax(xs, 0), (int32_t)pitch - 8) & ~3;
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(base + (int64_t)y * pitch + xa);
-        const uint64_t V = ((uint64_t)q[1] << 32) | q[0];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const int32_t x = sxh > 0 ? xs + k : xs + 3 - k;
-          const bool ok = rowok && (uint32_t)(x - xlo) <= (uint32_t)(xhi - xlo);
-          const int b = (int)((V >> ((8 * (x - xa)) & 63)) & 0xFF);
-          acc[k] += (255 - b) & -(int)ok;  // arithmetic mask: the load is never sunk into a branch
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 4; k++) part4[w][4 * lane + k] = acc[k];
-      __syncthreads();
-      if (w == 0) {
-        int B[4], pre[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          B[k] = 0;
-          for (int q = 0; q < nw; q++) B[k] += part4[q][4 * lane + k];
-          pre[k] = (k ? pre[k - 1] : 0) + B[k];
-        }
-        int tot;
-        const int ex = carry_acc + iwave_prefix_excl(pre[3], &tot);
-        // first depth (in order) that does not execute: before >= maxAbs or dep >= maxDepth
-        int kfail = 4;
-#pragma unroll
-        for (int k = 3; k >= 0; k--) {
-          const int before = ex + (k ? pre[k - 1] : 0);
-          if (!(before < maxAbs && dl + k < maxDepth)) kfail = k;
-        }
-        const unsigned long long F = __ballot(kfail < 4);
-        const int fl = F ? __ffsll((long long)F) - 1 : 64;
-        const int stop = fl < 64 ? 4 * fl + __shfl(kfail, fl, 64) : 256;
-        const int up = __shfl_up(B[3], 1, 64);
-        int prev = lane == 0 ? last : up;
-        int md = INT_MIN;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          if (4 * lane + k < stop) md = max(md, B[k] - prev);
-          prev = B[k];
-        }
-        for (int o = 32; o > 0; o >>= 1) md = max(md, __shfl_xor(md, o, 64));
-        if (md > maxDiff) maxDiff = md;  // `if (diff >= maxDiff) maxDiff = diff`
-        if (stop < 256) {
-          if (lane == 0) {
-            result = (d0 + stop) < maxDepth ? maxDiff : 0;
-            done_flag = 1;
-          }
-        } else {
-          carry_acc += tot;
-          last = __shfl(B[3], 63, 64);
-        }
-      }
-      __syncthreads();
-      if (done_flag) break;
-    }
-    if (threadIdx.x == 0) *out = done_flag ? result : 0;
-    return;
-  }
   for (int d0 = 0; d0 < maxDepth; d0 += 64) {
     const int dep = d0 + lane;
     int acc = 0;
-    // branch-free gather (out-of-mask/out-of-image points read pixel (0,0)
-    // and contribute 0, i.e. get_pixel's white), unrolled so several loads
-    // per lane are in flight
+    // unconditional clamped loads, masked arithmetically (get_pixel's white
+    // off the mask/image), so the unrolled loads overlap
 #pragma unroll 8
-    for (int i = w; i < scan; i += nw) {
+    for (int i = w; i < scan; i += 4) {
       const int32_t x = px[i] + sxh * dep, y = py[i] + syv * dep;
       const bool ok = (x >= nm.x0) & (x <= nm.x1) & (y >= nm.y0) & (y <= nm.y1) & (x >= 0) &
                       (y >= 0) & (x < g.W) & (y < g.H);
@@ -238,8 +366,7 @@ __global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, cons
     part[w][lane] = acc;
     __syncthreads();
     if (w == 0) {
-      int B = 0;
-      for (int q = 0; q < nw; q++) B += part[q][lane];
+      const int B = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
       int tot;
       const int before = carry_acc + iwave_prefix_excl(B, &tot);
       const bool exec = before < maxAbs && dep < maxDepth;
@@ -269,8 +396,22 @@ __global__ void __launch_bounds__(256) k_rot_peaks(PlaneRef img, RotGeom g, cons
   if (threadIdx.x == 0) *out = done_flag ? result : 0;
 }
 
-size_t rotation_lines_bytes(int count, int nedges, int nangles, int max_scan) {
-  return sizeof(int32_t) * 2 * (size_t)(max_scan > 0 ? max_scan : 1) * count * nedges * nangles;
+template <int FMT>
+static void launch_rot_t(const PlaneRef& img, const RotGeom& g, const RotTable* table,
+                         const Rect* masks, const int32_t* mask_active, int mask_index,
+                         int32_t* peaks, int count, hipStream_t st, int nangles, int max_scan,
+                         const RotScratch& R) {
+  hipLaunchKernelGGL(k_rot_band<FMT>, dim3(rot_slices(max_scan), g.nedges, count), dim3(256), 0,
+                     st, img, g, table, masks, mask_active, count, max_scan, R);
+  const int nlines = count * g.nedges * nangles;
+  hipLaunchKernelGGL(k_rot_final, dim3((nlines + 3) / 4), dim3(256), 0, st, g, table, masks,
+                     mask_active, mask_index, peaks, count, max_scan, R);
+  const size_t lds = sizeof(int32_t) * 2 * (size_t)(max_scan > 0 ? max_scan : 1);
+  if (lds > 64 * 1024)
+    hipFuncSetAttribute((const void*)k_rot_line<FMT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)lds);
+  hipLaunchKernelGGL(k_rot_line<FMT>, dim3(nangles, g.nedges, count), dim3(256), lds, st, img, g,
+                     table, masks, mask_active, mask_index, peaks, count, max_scan, R);
 }
 
 void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable* table,
@@ -279,30 +420,21 @@ void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable
                            int max_scan, int32_t* lines) {
   if (g.nedges <= 0 || nangles <= 0) return;
   const int nlines = count * g.nedges * nangles;
+  const RotScratch R = rot_scratch(lines, nlines, max_scan);
   hipLaunchKernelGGL(k_rot_points, dim3((nlines + 63) / 64), dim3(64), 0, st, g, table, masks,
-                     mask_active, count, lines);
-  dim3 grid(nangles, g.nedges, count);
-  const size_t lds = sizeof(int32_t) * 2 * (size_t)(max_scan > 0 ? max_scan : 1);
-  if (lds > 64 * 1024) {
-    hipFuncSetAttribute((const void*)k_rot_peaks<F_GRAY8>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipFuncSetAttribute((const void*)k_rot_peaks<F_Y400A>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipFuncSetAttribute((const void*)k_rot_peaks<F_RGB24>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  }
+                     mask_active, count, max_scan, R);
   switch (img.P.fmt) {
     case F_GRAY8:
-      hipLaunchKernelGGL(k_rot_peaks<F_GRAY8>, grid, dim3(256), lds, st, img, g, table, masks,
-                         mask_active, mask_index, peaks, lines, count);
+      launch_rot_t<F_GRAY8>(img, g, table, masks, mask_active, mask_index, peaks, count, st,
+                            nangles, max_scan, R);
       break;
     case F_Y400A:
-      hipLaunchKernelGGL(k_rot_peaks<F_Y400A>, grid, dim3(256), lds, st, img, g, table, masks,
-                         mask_active, mask_index, peaks, lines, count);
+      launch_rot_t<F_Y400A>(img, g, table, masks, mask_active, mask_index, peaks, count, st,
+                            nangles, max_scan, R);
       break;
     default:
-      hipLaunchKernelGGL(k_rot_peaks<F_RGB24>, grid, dim3(256), lds, st, img, g, table, masks,
-                         mask_active, mask_index, peaks, lines, count);
+      launch_rot_t<F_RGB24>(img, g, table, masks, mask_active, mask_index, peaks, count, st,
+                            nangles, max_scan, R);
       break;
   }
 }
