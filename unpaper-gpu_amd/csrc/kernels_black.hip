@@ -106,6 +106,13 @@ struct Canvas {
     return gray_of(load_px_row<FMT>(base + (int64_t)y * pitch, x));
   }
   __device__ __forceinline__ bool match(int32_t x, int32_t y) const { return gray(x, y) <= mmax; }
+  // match() as an unconditional load at a clamped position (no divergent
+  // branch around the load, so a batch of them is in flight together)
+  __device__ __forceinline__ bool match_nb(int32_t x, int32_t y) const {
+    const bool in = (x >= 0) & (y >= 0) & (x < W) & (y < H);
+    const int32_t cx = imin(imax(x, 0), W - 1), cy = imin(imax(y, 0), H - 1);
+    return in & (gray_of(load_px_row<FMT>(base + (int64_t)cy * pitch, cx)) <= mmax);
+  }
   __device__ __forceinline__ void paint(int32_t x, int32_t y) const {
     if (inside(x, y)) store_px_row<FMT>(base + (int64_t)y * pitch, x, Px{255, 255, 255});
   }
@@ -116,7 +123,12 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// fill_line (fill.c:16-52) for one wave: returns the distance painted.
+constexpr int kSlices = 8;  // 64-pixel slices evaluated per memory round trip
+
+// fill_line (fill.c:16-52) for one wave: returns the distance painted.  The
+// 512 positions of a round are loaded together; they are consumed slice by
+// slice in order (a line never revisits its pixels, so painting a slice does
+// not change the matches of the next).
 template <int FMT>
 __device__ int32_t fill_line(const Canvas<FMT>& C, int32_t px, int32_t py, int dir,
                              uint64_t intensity) {
@@ -124,34 +136,45 @@ __device__ int32_t fill_line(const Canvas<FMT>& C, int32_t px, int32_t py, int d
   const int dx = kDX[dir], dy = kDY[dir];
   bool has_last = false;
   int64_t last = 0;  // position of the last matching pixel so far
-  for (int64_t pos = 1;; pos += 64) {
-    const int64_t j = pos + lane;
-    const int32_t qx = px + (int32_t)(j * dx), qy = py + (int32_t)(j * dy);
-    const bool in = C.inside(qx, qy);
-    const bool m = C.match(qx, qy);
-    const unsigned long long M = __ballot(m);
-    // last match at or before this lane within the chunk
-    const unsigned long long upto = M & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-    bool hl = has_last;
-    int64_t lm = last;
-    if (upto) {
-      hl = true;
-      lm = pos + (63 - __clzll((long long)upto));
+  for (int64_t pos0 = 1;; pos0 += 64 * kSlices) {
+    bool mk[kSlices];
+#pragma unroll
+    for (int k = 0; k < kSlices; k++) {
+      const int64_t j = pos0 + 64 * k + lane;
+      mk[k] = C.match_nb(px + (int32_t)(j * dx), py + (int32_t)(j * dy));
     }
-    // counter starts at 1, resets to `intensity` on a match, decrements
-    // otherwise; the line stops (unpainted) where it reaches 0 or leaves
-    bool stop = !in;
-    if (hl) stop |= (uint64_t)(j - lm) >= intensity;
-    else stop |= j >= 1;
-    const unsigned long long S = __ballot(stop);
-    const int first = S ? __ffsll((long long)S) - 1 : 64;
-    if (lane < first) C.paint(qx, qy);
+#pragma unroll
+    for (int k = 0; k < kSlices; k++) {
+      const int64_t pos = pos0 + 64 * k, j = pos + lane;
+      const int32_t qx = px + (int32_t)(j * dx), qy = py + (int32_t)(j * dy);
+      const bool in = C.inside(qx, qy);
+      const unsigned long long M = __ballot(mk[k]);
+      // last match at or before this lane within the slice
+      const unsigned long long upto = M & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+      bool hl = has_last;
+      int64_t lm = last;
+      if (upto) {
+        hl = true;
+        lm = pos + (63 - __clzll((long long)upto));
+      }
+      // counter starts at 1, resets to `intensity` on a match, decrements
+      // otherwise; the line stops (unpainted) where it reaches 0 or leaves
+      bool stop = !in;
+      if (hl) stop |= (uint64_t)(j - lm) >= intensity;
+      else stop |= j >= 1;
+      const unsigned long long S = __ballot(stop);
+      const int first = S ? __ffsll((long long)S) - 1 : 64;
+      if (lane < first) C.paint(qx, qy);
+      if (S) {
+        wave_sync();
+        return (int32_t)(pos + first - 1);
+      }
+      if (M) {
+        has_last = true;
+        last = pos + (63 - __clzll((long long)M));
+      }
+    }
     wave_sync();
-    if (S) return (int32_t)(pos + first - 1);
-    if (M) {
-      has_last = true;
-      last = pos + (63 - __clzll((long long)M));
-    }
   }
 }
 
@@ -191,25 +214,43 @@ __device__ bool flood_fill(const Canvas<FMT>& C, int32_t sx, int32_t sy, uint64_
     }
     const int dx = kDX[top.dir], dy = kDY[top.dir];
     const int32_t n = 2 * top.dist[top.dir];
-    const int32_t c = top.idx + lane;
-    bool m = false;
-    int32_t qx = 0, qy = 0;
-    if (c < n) {
+    // the next 512 neighbour checks of the line in one round trip; the first
+    // match (in order) starts the child frame, later ones are re-read after it
+    bool mk[kSlices];
+#pragma unroll
+    for (int k = 0; k < kSlices; k++) {
+      const int32_t c = top.idx + 64 * k + lane;
       const int32_t d = c >> 1, sub = c & 1;
-      qx = top.x + (d + 1) * dx;
-      qy = top.y + (d + 1) * dy;
+      int32_t qx = top.x + (d + 1) * dx, qy = top.y + (d + 1) * dy;
       if (dx != 0) qy += sub == 0 ? 1 : -1;  // below, then above
       else qx += sub == 0 ? 1 : -1;           // right, then left
-      m = C.match(qx, qy);
+      mk[k] = (c < n) & C.match_nb(qx, qy);
     }
-    const unsigned long long M = __ballot(m);
-    if (!M) {
-      top.idx += 64;
+    int kf = -1;
+    unsigned long long M = 0;
+#pragma unroll
+    for (int k = kSlices - 1; k >= 0; k--) {
+      const unsigned long long b = __ballot(mk[k]);
+      if (b) {
+        kf = k;
+        M = b;
+      }
+    }
+    if (kf < 0) {
+      top.idx += 64 * kSlices;
       continue;
     }
     const int first = __ffsll((long long)M) - 1;
-    const int32_t cx = __shfl(qx, first, 64), cy = __shfl(qy, first, 64);
-    top.idx += first + 1;
+    const int32_t cidx = top.idx + 64 * kf + first;
+    int32_t cx, cy;
+    {
+      const int32_t d = cidx >> 1, sub = cidx & 1;
+      cx = top.x + (d + 1) * dx;
+      cy = top.y + (d + 1) * dy;
+      if (dx != 0) cy += sub == 0 ? 1 : -1;
+      else cx += sub == 0 ? 1 : -1;
+    }
+    top.idx = cidx + 1;
     if (sp >= capacity) return false;  // stack overflow: flagged by the caller
     Frame child;
     if (frame_start<FMT>(C, cx, cy, intensity, &child)) {
