@@ -812,6 +812,142 @@ __device__ __forceinline__ bool ring_member(int L, int dx, int dy, int32_t x, in
   return iabs(dy) == L ? x >= L : y >= L - 1;
 }
 
+// 81-bit position masks of the 9x9 window (bit p = (dy+4)*9 + dx+4): for
+// ring L, its two rows (|dy| = L) and its two columns without the corners.
+struct Mask81 {
+  uint64_t lo;
+  uint32_t hi;
+};
+__device__ __forceinline__ Mask81 ring_part(int L, bool rows) {
+  Mask81 m{0, 0};
+#pragma unroll
+  for (int p = 0; p < 81; p++) {
+    const int dx = p % 9 - 4, dy = p / 9 - 4;
+    const int adx = iabs(dx), ady = iabs(dy);
+    const bool on = rows ? (ady == L && adx <= L) : (adx == L && ady < L);
+    if (on) {
+      if (p < 64) m.lo |= 1ull << p;
+      else m.hi |= 1u << (p - 64);
+    }
+  }
+  return m;
+}
+
+// The sequential replay for intensity N <= 4, scheduled by dependence:
+// trigger T reads pixels within Chebyshev N of itself and clears within N-1,
+// so it depends only on earlier triggers closer than 2N.  level(T) = 1 + the
+// highest level of those (0 if none); triggers of one level are pairwise >= 2N
+// apart and are replayed together, one lane each, level after level.  The
+// result equals the raster-order replay (filters.c:243-348).
+template <int FMT>
+__device__ void noise_resolve_levels(const uint32_t* keys, int n, int N, const NoiseGeom& g,
+                                     uint8_t* base, int64_t pitch) {
+  __shared__ uint16_t lev[8192];
+  __shared__ int32_t max_level;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int R = 2 * N - 1;  // dependence radius
+  if (w == 0) {
+    int top = 0;
+    for (int i = 0; i < n; i++) {
+      const uint32_t key = keys[i];
+      const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
+      int mx = -1;
+      for (int b = i - 1; b >= 0; b -= 64) {
+        const int j = b - lane;
+        const uint32_t kj = j >= 0 ? keys[j] : 0u;
+        const int32_t xj = (int32_t)(kj & 0xFFFF), yj = (int32_t)(kj >> 16);
+        const bool rows = j >= 0 && yj >= y - R;
+        if (rows && iabs(xj - x) <= R) mx = imax(mx, (int)lev[j]);
+        // sorted by (y, x): once a lane falls below the row window, all
+        // earlier keys do too
+        if (__ballot(!rows && j >= 0) || b < 64) break;
+      }
+      for (int o = 32; o > 0; o >>= 1) mx = imax(mx, __shfl_xor(mx, o, 64));
+      if (lane == 0) lev[i] = (uint16_t)(mx + 1);
+      top = imax(top, mx + 1);
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) max_level = top;
+  }
+  __syncthreads();
+  Mask81 rowp[5], colp[5];
+#pragma unroll
+  for (int L = 1; L <= 4; L++) {
+    rowp[L] = ring_part(L, true);
+    colp[L] = ring_part(L, false);
+  }
+  const int levels = max_level;
+  for (int L0 = 0; L0 <= levels; L0++) {
+    for (int c = w * 64; c < n; c += nw * 64) {
+      const int i = c + lane;
+      if (i >= n || lev[i] != L0) continue;
+      const uint32_t key = keys[i];
+      const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
+      // the 9x9 window: unconditional clamped loads, dark = lightness < white
+      uint64_t dlo = 0;
+      uint32_t dhi = 0;
+      bool ctr = false;
+#pragma unroll
+      for (int p = 0; p < 81; p++) {
+        const int32_t qx = x + p % 9 - 4, qy = y + p / 9 - 4;
+        const bool in = (qx >= 0) & (qy >= 0) & (qx < g.W) & (qy < g.H);
+        const Px q = load_px_row<FMT>(base + (int64_t)imin(imax(qy, 0), g.H - 1) * pitch,
+                                      imin(imax(qx, 0), g.W - 1));
+        const bool dk = in & (light_of(q) < g.white);
+        if (p < 64) dlo |= (uint64_t)dk << p;
+        else dhi |= (uint32_t)dk << (p - 64);
+        if (p == 40) ctr = dark_of(q) < g.white;
+      }
+      if (!ctr) continue;  // cleared meanwhile
+      // rings with the reference loops' unsigned comparisons: rows of ring L
+      // counted iff x >= L, its columns iff y >= L-1 (all indices static)
+      Mask81 mem[5];
+      int lc[5];
+#pragma unroll
+      for (int L = 1; L <= 4; L++) {
+        mem[L].lo = (x >= L ? rowp[L].lo : 0ull) | (y >= L - 1 ? colp[L].lo : 0ull);
+        mem[L].hi = (x >= L ? rowp[L].hi : 0u) | (y >= L - 1 ? colp[L].hi : 0u);
+        lc[L] = __popcll(dlo & mem[L].lo) + __popc(dhi & mem[L].hi);
+      }
+      // do { lc = ring(level); count += lc; level++ } while (lc && level <= N)
+      int count = 1, k = N + 1;  // k: first empty ring (N+1: none within N)
+      bool open = true;
+#pragma unroll
+      for (int L = 1; L <= 4; L++) {
+        if (open && L <= N) {
+          count += lc[L];
+          if (lc[L] == 0) {
+            k = L;
+            open = false;
+          }
+        }
+      }
+      if (count > N) continue;
+      // the centre and rings 1..k-1 are cleared
+      white_px<FMT>(base + (int64_t)y * pitch, x);
+#pragma unroll
+      for (int Lc = 1; Lc <= 3; Lc++) {
+        if (Lc >= k) continue;
+        uint64_t clo = dlo & mem[Lc].lo;
+        uint32_t chi = dhi & mem[Lc].hi;
+        while (clo) {
+          const int p = __ffsll((long long)clo) - 1;
+          clo &= clo - 1;
+          white_px<FMT>(base + (int64_t)(y + p / 9 - 4) * pitch, x + p % 9 - 4);
+        }
+        while (chi) {
+          const int p = 64 + __ffs(chi) - 1;
+          chi &= chi - 1;
+          white_px<FMT>(base + (int64_t)(y + p / 9 - 4) * pitch, x + p % 9 - 4);
+        }
+      }
+    }
+    // this level's clears are read by the next level's triggers
+    __threadfence_block();
+    __syncthreads();
+  }
+}
+
 template <int FMT>
 __global__ void __launch_bounds__(256) k_noise_resolve(PlaneRef img, NoiseGeom g, uint8_t* scratch,
                                                        int64_t sstride, const int32_t* active,
@@ -839,12 +975,16 @@ __global__ void __launch_bounds__(256) k_noise_resolve(PlaneRef img, NoiseGeom g
   __threadfence_block();
   __syncthreads();
   block_sort(keys, p2);
-  if (threadIdx.x >= 64) return;
-  // one wave replays the raster scan over the sorted triggers
-  const int lane = threadIdx.x;
   const int N = g.intensity;
   uint8_t* base = plane_ptr(img, s);
   const int64_t pitch = img.P.pitch;
+  if (N <= 4 && p2 <= 8192) {
+    noise_resolve_levels<FMT>(keys, (int)n, N, g, base, pitch);
+    return;
+  }
+  if (threadIdx.x >= 64) return;
+  // one wave replays the raster scan over the sorted triggers
+  const int lane = threadIdx.x;
   if (N <= 4) {
     // small intensity: the whole (2N+1)^2 box of a trigger is read in one
     // round trip (two pixels per lane) and the rings are counted from
