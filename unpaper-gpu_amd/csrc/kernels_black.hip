@@ -123,10 +123,10 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-constexpr int kSlices = 32;  // 64-pixel slices evaluated per memory round trip
+constexpr int kSlices = 8;  // 64-pixel slices evaluated per memory round trip
 
 // fill_line (fill.c:16-52) for one wave: returns the distance painted.  The
-// 2048 positions of a round are loaded together; they are consumed slice by
+// 512 positions of a round are loaded together; they are consumed slice by
 // slice in order (a line never revisits its pixels, so painting a slice does
 // not change the matches of the next).
 template <int FMT>
@@ -214,7 +214,7 @@ __device__ bool flood_fill(const Canvas<FMT>& C, int32_t sx, int32_t sy, uint64_
     }
     const int dx = kDX[top.dir], dy = kDY[top.dir];
     const int32_t n = 2 * top.dist[top.dir];
-    // the next 2048 neighbour checks of the line in one round trip; the first
+    // the next 512 neighbour checks of the line in one round trip; the first
     // match (in order) starts the child frame, later ones are re-read after it
     bool mk[kSlices];
 #pragma unroll

@@ -846,30 +846,43 @@ __device__ void noise_resolve_levels(const uint32_t* keys, int n, int N, const N
   __shared__ int32_t max_level;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int R = 2 * N - 1;  // dependence radius
-  if (w == 0) {
-    int top = 0;
-    for (int i = 0; i < n; i++) {
+  // levels by parallel relaxation: lev(T) = 1 + max lev(dependent earlier T');
+  // values only grow and stay <= the true level, so the sweep repeats until
+  // nothing changes (longest chain + 1 sweeps).  Predecessors of T are found
+  // per row of the window [y-R, y] by binary search in the sorted keys.
+  __shared__ int32_t changed;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) lev[i] = 0;
+  if (threadIdx.x == 0) max_level = 0;
+  __syncthreads();
+  for (;;) {
+    if (threadIdx.x == 0) changed = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
       const uint32_t key = keys[i];
       const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
       int mx = -1;
-      for (int b = i - 1; b >= 0; b -= 64) {
-        const int j = b - lane;
-        const uint32_t kj = j >= 0 ? keys[j] : 0u;
-        const int32_t xj = (int32_t)(kj & 0xFFFF), yj = (int32_t)(kj >> 16);
-        const bool rows = j >= 0 && yj >= y - R;
-        if (rows && iabs(xj - x) <= R) mx = imax(mx, (int)lev[j]);
-        // sorted by (y, x): once a lane falls below the row window, all
-        // earlier keys do too
-        if (__ballot(!rows && j >= 0) || b < 64) break;
+      for (int yy = imax(y - R, 0); yy <= y; yy++) {
+        const uint32_t lo = ((uint32_t)yy << 16) | (uint32_t)imax(x - R, 0);
+        const uint32_t hi = ((uint32_t)yy << 16) | (uint32_t)(x + R);
+        int a = 0, b = i;  // first index in [0, i) with keys >= lo
+        while (a < b) {
+          const int mid = (a + b) >> 1;
+          if (keys[mid] < lo) a = mid + 1;
+          else b = mid;
+        }
+        for (int j = a; j < i && keys[j] <= hi; j++) mx = imax(mx, (int)lev[j]);
       }
-      for (int o = 32; o > 0; o >>= 1) mx = imax(mx, __shfl_xor(mx, o, 64));
-      if (lane == 0) lev[i] = (uint16_t)(mx + 1);
-      top = imax(top, mx + 1);
-      __builtin_amdgcn_wave_barrier();
+      if (mx + 1 > (int)lev[i]) {
+        lev[i] = (uint16_t)(mx + 1);
+        changed = 1;
+        atomicMax(&max_level, mx + 1);
+      }
     }
-    if (lane == 0) max_level = top;
+    __syncthreads();
+    const bool again = changed != 0;
+    __syncthreads();  // every thread has read the flag before it is reset
+    if (!again) break;
   }
-  __syncthreads();
   Mask81 rowp[5], colp[5];
 #pragma unroll
   for (int L = 1; L <= 4; L++) {
