@@ -656,9 +656,130 @@ __global__ void __launch_bounds__(kThreads) k_rotate_mask(PlaneRef src, PlaneRef
   }
 }
 
+// cubic_scale (interpolate.c:24-31) on integer taps.  Its integer-valued
+// subexpressions -- 2a-5b+4c-d, 3(b-c)+d-a and c-a -- are exact in float
+// (|x| < 2^24), so they are formed in int and converted; the six rounding
+// operations remain, in the reference's order:
+//   b + (0.5f*f) * ((c-a) + f * ((2a-5b+4c-d) + f * (3(b-c)+d-a)))
+__device__ __forceinline__ uint8_t cubic_int(float f, float h, int a, int b, int c, int d) {
+  const float s2 = (float)(3 * (b - c) + d - a);
+  const float s1 = (float)(2 * a - 5 * b + 4 * c - d);
+  const float u = s1 + f * s2;
+  const float v = (float)(c - a) + f * u;
+  const int r = (int)((float)b + h * v);
+  return (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));  // av_clip_uint8
+}
+
+// deskew rotate for a gray plane with bicubic interpolation (the default):
+// k_rotate_mask's tiling and staging, with the taps read straight from the
+// window and no other interpolation code in the kernel.
+template <int FMT>
+__global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, PlaneRef dst,
+                                                                const RotateArgs* args) {
+  __shared__ uint8_t stage[kRotCap];
+  const int s = blockIdx.z;
+  const RotateArgs a = args[s];
+  if (!a.active) return;
+  const Planes& P = src.P;
+  const uint8_t* sbase = plane_ptr(src, s);
+  uint8_t* dbase = plane_ptr(dst, s);
+  const Rect nm = normalize(a.mask);
+  const int32_t sw = nm.x1 - nm.x0 + 1, sh = nm.y1 - nm.y0 + 1;
+  const float scx = nm.x0 + sw / 2.0f, scy = nm.y0 + sh / 2.0f;  // primitives.c:137-145
+  const float tcx = 0 + sw / 2.0f, tcy = 0 + sh / 2.0f;
+  const int32_t tx0 = blockIdx.x * kRotTW, ty0 = blockIdx.y * kRotTH;
+  const int32_t u0 = imax(tx0, 0) - a.mask.x0, u1 = imin(tx0 + kRotTW, P.W) - 1 - a.mask.x0;
+  const int32_t v0 = imax(ty0, 0) - a.mask.y0, v1 = imin(ty0 + kRotTH, P.H) - 1 - a.mask.y0;
+  const int32_t cu0 = imax(u0, 0), cu1 = imin(u1, sw - 1);
+  const int32_t cv0 = imax(v0, 0), cv1 = imin(v1, sh - 1);
+  int32_t bx0 = 0, by0 = 0, bw = 0, bh = 0;
+  bool staged = false;
+  if (cu0 <= cu1 && cv0 <= cv1) {
+    float mnx = 3.0e38f, mxx = -3.0e38f, mny = 3.0e38f, mxy = -3.0e38f;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int32_t u = c & 1 ? cu1 : cu0, v = c & 2 ? cv1 : cv0;
+      const float X = scx + (u - tcx) * a.cosval + (v - tcy) * a.sinval;
+      const float Y = scy + (v - tcy) * a.cosval - (u - tcx) * a.sinval;
+      mnx = fminf(mnx, X);
+      mxx = fmaxf(mxx, X);
+      mny = fminf(mny, Y);
+      mxy = fmaxf(mxy, Y);
+    }
+    bx0 = (int32_t)floorf(mnx) - 3;
+    by0 = (int32_t)floorf(mny) - 3;
+    bw = (int32_t)floorf(mxx) + 4 - bx0 + 1;
+    bh = (int32_t)floorf(mxy) + 4 - by0 + 1;
+    staged = bw > 0 && bh > 0 && (int64_t)bw * bh <= kRotCap;
+  }
+  if (staged) {
+    // unconditional clamped loads (white off the image), all of a round in flight
+    const int n = bw * bh;
+    for (int b0 = 0; b0 < n; b0 += 8 * kThreads) {
+      uint8_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = b0 + k * kThreads + threadIdx.x;
+        const int r = i / bw;
+        const int32_t x = bx0 + (i - r * bw), y = by0 + r;
+        const bool ok = (x >= 0) & (y >= 0) & (x < P.W) & (y < P.H);
+        const uint8_t q = load_px_row<FMT>(sbase + (int64_t)imin(imax(y, 0), P.H - 1) * P.pitch,
+                                           imin(imax(x, 0), P.W - 1)).r;
+        v[k] = ok ? q : (uint8_t)255;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = b0 + k * kThreads + threadIdx.x;
+        if (i < n) stage[i] = v[k];
+      }
+    }
+  }
+  __syncthreads();
+  const Src<FMT> S{sbase, P.pitch, P.W, P.H};
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int32_t x = tx0 + lane;
+  if (x >= P.W) return;
+  const int32_t u = x - a.mask.x0;
+#pragma unroll
+  for (int k = 0; k < kRotTH / 4; k++) {
+    const int32_t y = ty0 + w + 4 * k;
+    if (y >= P.H) break;
+    uint8_t* drow = dbase + (int64_t)y * P.pitch;
+    const int32_t v = y - a.mask.y0;
+    if (u >= 0 && u < sw && v >= 0 && v < sh) {
+      const float srcX = scx + (u - tcx) * a.cosval + (v - tcy) * a.sinval;
+      const float srcY = scy + (v - tcy) * a.cosval - (u - tcx) * a.sinval;
+      uint8_t o;
+      if (staged) {
+        const int ix = (int)srcX, iy = (int)srcY;  // interp_bicubic truncates
+        const float fx = srcX - ix, fy = srcY - iy;
+        const float hx = 0.5f * fx, hy = 0.5f * fy;
+        const uint8_t* t = stage + (iy - 1 - by0) * bw + (ix - 1 - bx0);
+        int col[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++, t += bw) col[r] = cubic_int(fx, hx, t[0], t[1], t[2], t[3]);
+        o = cubic_int(fy, hy, col[0], col[1], col[2], col[3]);
+      } else {
+        o = interp_bicubic(S, srcX, srcY).r;
+      }
+      store_px_row<FMT>(drow, x, Px{o, o, o});
+    } else {
+      copy_px_raw<FMT>(drow, x, sbase + (int64_t)y * P.pitch, x);
+    }
+  }
+}
+
 void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
                         int interp, int count, hipStream_t st) {
   const dim3 grid((src.P.W + kRotTW - 1) / kRotTW, (src.P.H + kRotTH - 1) / kRotTH, count);
+  if (interp == UPHIP_INTERP_CUBIC && src.P.fmt == F_GRAY8) {
+    hipLaunchKernelGGL(k_rotate_cubic_gray<F_GRAY8>, grid, dim3(kThreads), 0, st, src, dst, args);
+    return;
+  }
+  if (interp == UPHIP_INTERP_CUBIC && src.P.fmt == F_Y400A) {
+    hipLaunchKernelGGL(k_rotate_cubic_gray<F_Y400A>, grid, dim3(kThreads), 0, st, src, dst, args);
+    return;
+  }
   if (src.P.fmt == F_GRAY8)
     hipLaunchKernelGGL(k_rotate_mask<F_GRAY8>, grid, dim3(kThreads), 0, st, src, dst, args,
                        interp);
