@@ -631,18 +631,75 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
   }
   __syncthreads();
   if (!any_dark) return;
+  // Pixels provably in a component of >= 5 pixels, by bit rows: L3 = dark
+  // pixels with >= 5 dark pixels in their 3x3 block (all of them 8-adjacent
+  // to the centre, so one component), large = dark & (L3 | 8-dilation of L3)
+  // (8-adjacent to an L3 pixel = same component).  Only the remaining dark
+  // pixels need the restricted 9x9 flood.  Rows outside the region read as
+  // empty, which can only leave pixels undecided, never mislabel them.
+  __shared__ uint64_t l3[kRW][2];
+  for (int ry = threadIdx.x; ry < kRW; ry += 256) {
+    uint64_t s0[2], s1[2], c0[2], c1[2], c2[2], c3[2];
+    // horizontal 3-sums (2 bits) of rows ry-1, ry, ry+1, accumulated into a 4-bit count
+#pragma unroll
+    for (int h = 0; h < 2; h++) c0[h] = c1[h] = c2[h] = c3[h] = 0;
+#pragma unroll
+    for (int d = -1; d <= 1; d++) {
+      const int r = ry + d;
+      uint64_t v[2] = {0, 0};
+      if (r >= 0 && r < kRW) {
+        v[0] = ((uint64_t)drow[r][1] << 32) | drow[r][0];
+        v[1] = ((uint64_t)drow[r][3] << 32) | drow[r][2];
+      }
+      // left neighbour of column x is bit x-1 (shift up), right is x+1 (down)
+      const uint64_t L0 = v[0] << 1, L1 = (v[1] << 1) | (v[0] >> 63);
+      const uint64_t R0 = (v[0] >> 1) | (v[1] << 63), R1 = v[1] >> 1;
+      const uint64_t Lw[2] = {L0, L1}, Rw[2] = {R0, R1};
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        s0[h] = v[h] ^ Lw[h] ^ Rw[h];                                   // bit 0
+        s1[h] = (v[h] & Lw[h]) | (v[h] & Rw[h]) | (Lw[h] & Rw[h]);      // bit 1
+        // c += s (c: 4 bits, s: 2 bits)
+        const uint64_t k0 = c0[h] & s0[h];
+        c0[h] ^= s0[h];
+        const uint64_t t1 = c1[h] ^ s1[h];
+        const uint64_t k1 = (c1[h] & s1[h]) | (t1 & k0);
+        c1[h] = t1 ^ k0;
+        const uint64_t k2 = c2[h] & k1;
+        c2[h] ^= k1;
+        c3[h] |= k2;
+      }
+    }
+    uint64_t me[2] = {((uint64_t)drow[ry][1] << 32) | drow[ry][0],
+                      ((uint64_t)drow[ry][3] << 32) | drow[ry][2]};
+#pragma unroll
+    for (int h = 0; h < 2; h++)  // count >= 5: 8 | (4 & (2 | 1))
+      l3[ry][h] = me[h] & (c3[h] | (c2[h] & (c1[h] | c0[h])));
+  }
+  __syncthreads();
   // small flags within radius 10 of the tile (region rows/cols [4, 88)), as
   // LDS bytes (bit 2) and as bit rows built from ballots
   __shared__ uint32_t srow[kRW][4];
   {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int ry = w; ry < kRW; ry += 4) {
+      // large = dark & (L3 | dilate8(L3)) for this row
+      uint64_t dil[2] = {0, 0};
+#pragma unroll
+      for (int d = -1; d <= 1; d++) {
+        const int r = ry + d;
+        if (r < 0 || r >= kRW) continue;
+        const uint64_t a0 = l3[r][0], a1 = l3[r][1];
+        dil[0] |= a0 | (a0 << 1) | (a0 >> 1) | (a1 << 63);
+        dil[1] |= a1 | (a1 << 1) | (a0 >> 63) | (a1 >> 1);
+      }
       unsigned long long m[2];
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const int rx = h * 64 + lane;
         bool small = false;
-        if (ry >= 4 && ry < 88 && rx >= 4 && rx < 88 && (px[ry * kRW + rx] & 1)) {
+        const bool undecided = ((dil[h] >> lane) & 1) == 0;
+        if (undecided && ry >= 4 && ry < 88 && rx >= 4 && rx < 88 && (px[ry * kRW + rx] & 1)) {
           uint32_t comp[9];
           small = flood9(drow, rx, ry, comp) <= 4;
           if (small) px[ry * kRW + rx] |= 4;
