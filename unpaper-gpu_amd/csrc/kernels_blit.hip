@@ -673,10 +673,27 @@ __device__ __forceinline__ uint8_t cubic_int(float f, float h, int a, int b, int
 // deskew rotate for a gray plane with bicubic interpolation (the default):
 // k_rotate_mask's tiling and staging, with the taps read straight from the
 // window and no other interpolation code in the kernel.
+// cubic_scale with its integer-valued terms precomputed (exact, see above):
+// q = {2a-5b+4c-d, 3(b-c)+d-a, c-a, b} as floats.
+__device__ __forceinline__ int cubic_q(float f, float h, float4 q) {
+  const float u = q.x + f * q.y;
+  const float v = q.z + f * u;
+  const int r = (int)(q.w + h * v);
+  return r < 0 ? 0 : (r > 255 ? 255 : r);  // av_clip_uint8
+}
+
+constexpr int kQuadCap = 2560;  // staged quads per tile (40 KB of float4)
+
+// deskew rotate for a gray plane with bicubic interpolation (the default).
+// Tiles as k_rotate_mask.  The staged window is turned into per-position tap
+// quads (the integer terms of cubic_scale for columns c..c+3 of each row,
+// shared by every output pixel whose taps start there), so a row cubic is
+// one 16-byte LDS read and six float operations.
 template <int FMT>
 __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, PlaneRef dst,
                                                                 const RotateArgs* args) {
   __shared__ uint8_t stage[kRotCap];
+  __shared__ float4 quad[kQuadCap];
   const int s = blockIdx.z;
   const RotateArgs a = args[s];
   if (!a.active) return;
@@ -710,7 +727,7 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
     by0 = (int32_t)floorf(mny) - 3;
     bw = (int32_t)floorf(mxx) + 4 - bx0 + 1;
     bh = (int32_t)floorf(mxy) + 4 - by0 + 1;
-    staged = bw > 0 && bh > 0 && (int64_t)bw * bh <= kRotCap;
+    staged = bw > 3 && bh > 0 && (int64_t)bw * bh <= kRotCap && (int64_t)bw * bh <= kQuadCap;
   }
   if (staged) {
     // unconditional clamped loads (white off the image), all of a round in flight
@@ -733,6 +750,16 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
         if (i < n) stage[i] = v[k];
       }
     }
+    __syncthreads();
+    // tap quads: position (r, c) holds the terms of columns c..c+3
+    for (int i = threadIdx.x; i < n; i += kThreads) {
+      const int r = i / bw, c = i - r * bw;
+      if (c + 3 >= bw) continue;  // never the start of a tap quad
+      const uint8_t* t = stage + i;
+      const int A = t[0], B = t[1], Cc = t[2], D = t[3];
+      quad[i] = make_float4((float)(2 * A - 5 * B + 4 * Cc - D), (float)(3 * (B - Cc) + D - A),
+                            (float)(Cc - A), (float)B);
+    }
   }
   __syncthreads();
   const Src<FMT> S{sbase, P.pitch, P.W, P.H};
@@ -754,11 +781,15 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
         const int ix = (int)srcX, iy = (int)srcY;  // interp_bicubic truncates
         const float fx = srcX - ix, fy = srcY - iy;
         const float hx = 0.5f * fx, hy = 0.5f * fy;
-        const uint8_t* t = stage + (iy - 1 - by0) * bw + (ix - 1 - bx0);
-        int col[4];
-#pragma unroll
-        for (int r = 0; r < 4; r++, t += bw) col[r] = cubic_int(fx, hx, t[0], t[1], t[2], t[3]);
-        o = cubic_int(fy, hy, col[0], col[1], col[2], col[3]);
+        const float4* q = quad + (iy - 1 - by0) * bw + (ix - 1 - bx0);
+        const int c0 = cubic_q(fx, hx, q[0]);
+        const int c1 = cubic_q(fx, hx, q[bw]);
+        const int c2 = cubic_q(fx, hx, q[2 * bw]);
+        const int c3 = cubic_q(fx, hx, q[3 * bw]);
+        o = (uint8_t)cubic_q(fy, hy,
+                             make_float4((float)(2 * c0 - 5 * c1 + 4 * c2 - c3),
+                                         (float)(3 * (c1 - c2) + c3 - c0), (float)(c2 - c0),
+                                         (float)c1));
       } else {
         o = interp_bicubic(S, srcX, srcY).r;
       }
