@@ -673,27 +673,16 @@ __device__ __forceinline__ uint8_t cubic_int(float f, float h, int a, int b, int
 // deskew rotate for a gray plane with bicubic interpolation (the default):
 // k_rotate_mask's tiling and staging, with the taps read straight from the
 // window and no other interpolation code in the kernel.
-// cubic_scale with its integer-valued terms precomputed (exact, see above):
-// q = {2a-5b+4c-d, 3(b-c)+d-a, c-a, b} as floats.
-__device__ __forceinline__ int cubic_q(float f, float h, float4 q) {
-  const float u = q.x + f * q.y;
-  const float v = q.z + f * u;
-  const int r = (int)(q.w + h * v);
-  return r < 0 ? 0 : (r > 255 ? 255 : r);  // av_clip_uint8
-}
+// deskew rotate for a gray plane with bicubic interpolation (the default):
+// k_rotate_mask's tiling and staging, with the taps read straight from the
+// window and no other interpolation code in the kernel.
+constexpr int kRotGH = 32;     // output rows per tile of the gray bicubic kernel
+constexpr int kRotGCap = 6144; // its staged pixels per tile
 
-constexpr int kQuadCap = 2560;  // staged quads per tile (40 KB of float4)
-
-// deskew rotate for a gray plane with bicubic interpolation (the default).
-// Tiles as k_rotate_mask.  The staged window is turned into per-position tap
-// quads (the integer terms of cubic_scale for columns c..c+3 of each row,
-// shared by every output pixel whose taps start there), so a row cubic is
-// one 16-byte LDS read and six float operations.
 template <int FMT>
 __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, PlaneRef dst,
                                                                 const RotateArgs* args) {
-  __shared__ uint8_t stage[kRotCap];
-  __shared__ float4 quad[kQuadCap];
+  __shared__ uint8_t stage[kRotGCap];
   const int s = blockIdx.z;
   const RotateArgs a = args[s];
   if (!a.active) return;
@@ -704,9 +693,9 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
   const int32_t sw = nm.x1 - nm.x0 + 1, sh = nm.y1 - nm.y0 + 1;
   const float scx = nm.x0 + sw / 2.0f, scy = nm.y0 + sh / 2.0f;  // primitives.c:137-145
   const float tcx = 0 + sw / 2.0f, tcy = 0 + sh / 2.0f;
-  const int32_t tx0 = blockIdx.x * kRotTW, ty0 = blockIdx.y * kRotTH;
+  const int32_t tx0 = blockIdx.x * kRotTW, ty0 = blockIdx.y * kRotGH;
   const int32_t u0 = imax(tx0, 0) - a.mask.x0, u1 = imin(tx0 + kRotTW, P.W) - 1 - a.mask.x0;
-  const int32_t v0 = imax(ty0, 0) - a.mask.y0, v1 = imin(ty0 + kRotTH, P.H) - 1 - a.mask.y0;
+  const int32_t v0 = imax(ty0, 0) - a.mask.y0, v1 = imin(ty0 + kRotGH, P.H) - 1 - a.mask.y0;
   const int32_t cu0 = imax(u0, 0), cu1 = imin(u1, sw - 1);
   const int32_t cv0 = imax(v0, 0), cv1 = imin(v1, sh - 1);
   int32_t bx0 = 0, by0 = 0, bw = 0, bh = 0;
@@ -727,7 +716,7 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
     by0 = (int32_t)floorf(mny) - 3;
     bw = (int32_t)floorf(mxx) + 4 - bx0 + 1;
     bh = (int32_t)floorf(mxy) + 4 - by0 + 1;
-    staged = bw > 3 && bh > 0 && (int64_t)bw * bh <= kRotCap && (int64_t)bw * bh <= kQuadCap;
+    staged = bw > 0 && bh > 0 && (int64_t)bw * bh <= kRotGCap;
   }
   if (staged) {
     // unconditional clamped loads (white off the image), all of a round in flight
@@ -750,16 +739,6 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
         if (i < n) stage[i] = v[k];
       }
     }
-    __syncthreads();
-    // tap quads: position (r, c) holds the terms of columns c..c+3
-    for (int i = threadIdx.x; i < n; i += kThreads) {
-      const int r = i / bw, c = i - r * bw;
-      if (c + 3 >= bw) continue;  // never the start of a tap quad
-      const uint8_t* t = stage + i;
-      const int A = t[0], B = t[1], Cc = t[2], D = t[3];
-      quad[i] = make_float4((float)(2 * A - 5 * B + 4 * Cc - D), (float)(3 * (B - Cc) + D - A),
-                            (float)(Cc - A), (float)B);
-    }
   }
   __syncthreads();
   const Src<FMT> S{sbase, P.pitch, P.W, P.H};
@@ -768,7 +747,7 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
   if (x >= P.W) return;
   const int32_t u = x - a.mask.x0;
 #pragma unroll
-  for (int k = 0; k < kRotTH / 4; k++) {
+  for (int k = 0; k < kRotGH / 4; k++) {
     const int32_t y = ty0 + w + 4 * k;
     if (y >= P.H) break;
     uint8_t* drow = dbase + (int64_t)y * P.pitch;
@@ -781,15 +760,11 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
         const int ix = (int)srcX, iy = (int)srcY;  // interp_bicubic truncates
         const float fx = srcX - ix, fy = srcY - iy;
         const float hx = 0.5f * fx, hy = 0.5f * fy;
-        const float4* q = quad + (iy - 1 - by0) * bw + (ix - 1 - bx0);
-        const int c0 = cubic_q(fx, hx, q[0]);
-        const int c1 = cubic_q(fx, hx, q[bw]);
-        const int c2 = cubic_q(fx, hx, q[2 * bw]);
-        const int c3 = cubic_q(fx, hx, q[3 * bw]);
-        o = (uint8_t)cubic_q(fy, hy,
-                             make_float4((float)(2 * c0 - 5 * c1 + 4 * c2 - c3),
-                                         (float)(3 * (c1 - c2) + c3 - c0), (float)(c2 - c0),
-                                         (float)c1));
+        const uint8_t* t = stage + (iy - 1 - by0) * bw + (ix - 1 - bx0);
+        int col[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++, t += bw) col[r] = cubic_int(fx, hx, t[0], t[1], t[2], t[3]);
+        o = cubic_int(fy, hy, col[0], col[1], col[2], col[3]);
       } else {
         o = interp_bicubic(S, srcX, srcY).r;
       }
@@ -803,12 +778,13 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
 void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
                         int interp, int count, hipStream_t st) {
   const dim3 grid((src.P.W + kRotTW - 1) / kRotTW, (src.P.H + kRotTH - 1) / kRotTH, count);
+  const dim3 ggrid((src.P.W + kRotTW - 1) / kRotTW, (src.P.H + kRotGH - 1) / kRotGH, count);
   if (interp == UPHIP_INTERP_CUBIC && src.P.fmt == F_GRAY8) {
-    hipLaunchKernelGGL(k_rotate_cubic_gray<F_GRAY8>, grid, dim3(kThreads), 0, st, src, dst, args);
+    hipLaunchKernelGGL(k_rotate_cubic_gray<F_GRAY8>, ggrid, dim3(kThreads), 0, st, src, dst, args);
     return;
   }
   if (interp == UPHIP_INTERP_CUBIC && src.P.fmt == F_Y400A) {
-    hipLaunchKernelGGL(k_rotate_cubic_gray<F_Y400A>, grid, dim3(kThreads), 0, st, src, dst, args);
+    hipLaunchKernelGGL(k_rotate_cubic_gray<F_Y400A>, ggrid, dim3(kThreads), 0, st, src, dst, args);
     return;
   }
   if (src.P.fmt == F_GRAY8)
