@@ -552,6 +552,30 @@ __device__ __forceinline__ int flood9(const uint32_t (*drow)[4], int cx, int cy,
   return n;
 }
 
+// bits [c, c+n) of a 128-bit region row (n <= 32, c + n <= 128)
+__device__ __forceinline__ uint32_t row_bits(const uint32_t* w, int c, int n) {
+  const int word = c >> 5, off = c & 31;
+  const uint64_t v = ((uint64_t)(word < 3 ? w[word + 1] : 0u) << 32) | w[word];
+  return (uint32_t)(v >> off) & (n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u));
+}
+
+// Append the (gx, gy) keys of the lanes with `want` to a list: one atomic per
+// wave, ballot-compacted.
+__device__ __forceinline__ void wave_append(bool want, int32_t gx, int32_t gy, uint32_t* counter,
+                                            uint32_t* list, int32_t capacity) {
+  const unsigned long long M = __ballot(want);
+  if (!M) return;
+  const int lane = threadIdx.x & 63;
+  uint32_t base = 0;
+  const int leader = __ffsll((long long)M) - 1;
+  if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(M));
+  base = __shfl(base, leader, 64);
+  if (want) {
+    const uint32_t k = base + (uint32_t)__popcll(M & ((1ull << lane) - 1ull));
+    if (k < (uint32_t)capacity) list[k] = ((uint32_t)gy << 16) | (uint32_t)gx;
+  }
+}
+
 template <int FMT>
 __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom g, uint8_t* scratch,
                                                         int64_t sstride, const int32_t* active,
@@ -562,87 +586,87 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
   const int32_t ox = tx0 - kHalo, oy = ty0 - kHalo;  // region origin
   const uint8_t* base = plane_ptr(img, s);
   NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
-  // bit0 dark (light < white), bit1 trigger (max < white), bit2 small
-  __shared__ uint8_t px[kRW * kRW];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // Everything is kept as 128-bit region rows (bit = region column):
+  //   drow dark (lightness < white), trow trigger (max < white; the same
+  //   bits for gray planes), srow small (component <= 4 pixels)
+  constexpr bool kSplit = FMT == F_RGB24;
   __shared__ uint32_t drow[kRW][4];
+  __shared__ uint32_t trow_s[kSplit ? kRW : 1][4];
+  __shared__ uint32_t srow[kRW][4];
+  __shared__ uint64_t l3[kRW][2];
   __shared__ int32_t any_dark;
+  uint32_t (*trow)[4] = kSplit ? trow_s : drow;
   // Stage the region rows into LDS with 16-byte loads, all issued before any
-  // is consumed (the region is ~2 KB-18 KB; one byte per lane per load would
-  // leave the kernel latency bound).  Rows start 256-byte aligned, so every
-  // vector lies inside its row's pitch; out-of-image pixels are masked below.
+  // is consumed.  Rows start 256-byte aligned, so every vector lies inside
+  // its row's pitch; out-of-image pixels are masked below.
   constexpr int B = FMT == F_GRAY8 ? 1 : FMT == F_Y400A ? 2 : 3;
   constexpr int NV = (kRW * B + 30) / 16;             // vectors per region row
   constexpr int NLOAD = (kRW * NV + 255) / 256;       // loads per thread
   __shared__ uint4 stage[kRW][NV];
-  const int64_t sb = (int64_t)ox * B;                 // first region byte in the row
-  const int64_t a0 = sb >= 0 ? (sb & ~(int64_t)15) : -((-sb + 15) & ~(int64_t)15);
-  const int lead = (int)(sb - a0);                    // region byte 0 within the staged row
-  const int64_t pitch = img.P.pitch;
-  uint4 v[NLOAD];
-#pragma unroll
-  for (int k = 0; k < NLOAD; k++) {
-    const int i = threadIdx.x + k * 256;
-    const int ry = i / NV, vi = i % NV;
-    const int32_t gy = oy + ry;
-    const int64_t off = a0 + 16 * vi;
-    v[k] = make_uint4(0, 0, 0, 0);
-    if (i < kRW * NV && gy >= 0 && gy < g.H && off >= 0 && off < pitch)
-      v[k] = *reinterpret_cast<const uint4*>(base + (int64_t)gy * pitch + off);
-  }
-#pragma unroll
-  for (int k = 0; k < NLOAD; k++) {
-    const int i = threadIdx.x + k * 256;
-    if (i < kRW * NV) stage[i / NV][i % NV] = v[k];
-  }
-  __syncthreads();
-  // flags + dark bit rows: wave w takes rows w, w+4, ...; lanes own columns
-  // lane and 64+lane, so each row mask is two ballots (no LDS atomics)
   {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t sb = (int64_t)ox * B;
+    const int64_t a0 = sb >= 0 ? (sb & ~(int64_t)15) : -((-sb + 15) & ~(int64_t)15);
+    const int64_t pitch = img.P.pitch;
+    uint4 v[NLOAD];
+#pragma unroll
+    for (int k = 0; k < NLOAD; k++) {
+      const int i = threadIdx.x + k * 256;
+      const int ry = i / NV, vi = i % NV;
+      const int32_t gy = oy + ry;
+      const int64_t off = a0 + 16 * vi;
+      v[k] = make_uint4(0, 0, 0, 0);
+      if (i < kRW * NV && gy >= 0 && gy < g.H && off >= 0 && off < pitch)
+        v[k] = *reinterpret_cast<const uint4*>(base + (int64_t)gy * pitch + off);
+    }
+#pragma unroll
+    for (int k = 0; k < NLOAD; k++) {
+      const int i = threadIdx.x + k * 256;
+      if (i < kRW * NV) stage[i / NV][i % NV] = v[k];
+    }
+    if (threadIdx.x == 0) any_dark = 0;
+    __syncthreads();
+    // dark / trigger bit rows: wave w takes rows w, w+4, ...; lanes own
+    // columns lane and 64+lane, each row mask is two ballots
+    const int lead = (int)(sb - a0);
     bool tile_dark = false;
     for (int ry = w; ry < kRW; ry += 4) {
       const int32_t gy = oy + ry;
-      const uint8_t* srow = reinterpret_cast<const uint8_t*>(stage[ry]) + lead;
-      unsigned long long m[2];
+      const uint8_t* srow_b = reinterpret_cast<const uint8_t*>(stage[ry]) + lead;
+      unsigned long long md[2], mt[2];
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const int rx = h * 64 + lane;
         const int32_t gx = ox + rx;
-        uint8_t f = 0;
-        if (rx < kRW && gx >= 0 && gx < g.W && gy >= 0 && gy < g.H) {
-          const Px p = load_px_row<FMT>(srow, rx);
-          if (light_of(p) < g.white) f |= 1;
-          if (dark_of(p) < g.white) f |= 2;
-        }
-        if (rx < kRW) px[ry * kRW + rx] = f;
-        if ((f & 1) && rx >= kHalo && rx < kHalo + kNT && ry >= kHalo && ry < kHalo + kNT)
-          tile_dark = true;
-        m[h] = __ballot(f & 1);
+        const bool in = (rx < kRW) & (gx >= 0) & (gx < g.W) & (gy >= 0) & (gy < g.H);
+        const Px p = load_px_row<FMT>(srow_b, rx < kRW ? rx : 0);
+        md[h] = __ballot(in & (light_of(p) < g.white));
+        mt[h] = kSplit ? __ballot(in & (dark_of(p) < g.white)) : md[h];
       }
       if (lane < 4) {
-        const unsigned long long q = m[lane >> 1];
+        const unsigned long long q = md[lane >> 1];
         drow[ry][lane] = (uint32_t)(lane & 1 ? q >> 32 : q);
+        if (kSplit) {
+          const unsigned long long t = mt[lane >> 1];
+          trow[ry][lane] = (uint32_t)(lane & 1 ? t >> 32 : t);
+        }
       }
+      // interior columns [kHalo, kHalo + kNT) = bits 14..63 | 64..77
+      if (ry >= kHalo && ry < kHalo + kNT && ((md[0] >> kHalo) | (md[1] & 0x3FFFull)))
+        tile_dark = true;
     }
-    const unsigned long long any = __ballot(tile_dark);
-    if (threadIdx.x == 0) any_dark = 0;
-    __syncthreads();
-    if (lane == 0 && any) any_dark = 1;
+    if (lane == 0 && tile_dark) any_dark = 1;
   }
   __syncthreads();
   if (!any_dark) return;
-  // Pixels provably in a component of >= 5 pixels, by bit rows: L3 = dark
-  // pixels with >= 5 dark pixels in their 3x3 block (all of them 8-adjacent
-  // to the centre, so one component), large = dark & (L3 | 8-dilation of L3)
-  // (8-adjacent to an L3 pixel = same component).  Only the remaining dark
-  // pixels need the restricted 9x9 flood.  Rows outside the region read as
-  // empty, which can only leave pixels undecided, never mislabel them.
-  __shared__ uint64_t l3[kRW][2];
+  // Pixels provably in a component of >= 5 pixels: L3 = dark pixels with >= 5
+  // dark pixels in their 3x3 block (all 8-adjacent to the centre, so one
+  // component); large = dark & (L3 | 8-dilation of L3) (8-adjacent to an L3
+  // pixel = same component).  Only the remaining dark pixels need the
+  // restricted 9x9 flood.  Rows outside the region read as empty, which can
+  // only leave pixels undecided, never mislabel them.
   for (int ry = threadIdx.x; ry < kRW; ry += 256) {
-    uint64_t s0[2], s1[2], c0[2], c1[2], c2[2], c3[2];
-    // horizontal 3-sums (2 bits) of rows ry-1, ry, ry+1, accumulated into a 4-bit count
-#pragma unroll
-    for (int h = 0; h < 2; h++) c0[h] = c1[h] = c2[h] = c3[h] = 0;
+    uint64_t c0[2] = {0, 0}, c1[2] = {0, 0}, c2[2] = {0, 0}, c3[2] = {0, 0};
 #pragma unroll
     for (int d = -1; d <= 1; d++) {
       const int r = ry + d;
@@ -652,153 +676,139 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
         v[1] = ((uint64_t)drow[r][3] << 32) | drow[r][2];
       }
       // left neighbour of column x is bit x-1 (shift up), right is x+1 (down)
-      const uint64_t L0 = v[0] << 1, L1 = (v[1] << 1) | (v[0] >> 63);
-      const uint64_t R0 = (v[0] >> 1) | (v[1] << 63), R1 = v[1] >> 1;
-      const uint64_t Lw[2] = {L0, L1}, Rw[2] = {R0, R1};
+      const uint64_t Lw[2] = {v[0] << 1, (v[1] << 1) | (v[0] >> 63)};
+      const uint64_t Rw[2] = {(v[0] >> 1) | (v[1] << 63), v[1] >> 1};
 #pragma unroll
       for (int h = 0; h < 2; h++) {
-        s0[h] = v[h] ^ Lw[h] ^ Rw[h];                                   // bit 0
-        s1[h] = (v[h] & Lw[h]) | (v[h] & Rw[h]) | (Lw[h] & Rw[h]);      // bit 1
-        // c += s (c: 4 bits, s: 2 bits)
-        const uint64_t k0 = c0[h] & s0[h];
-        c0[h] ^= s0[h];
-        const uint64_t t1 = c1[h] ^ s1[h];
-        const uint64_t k1 = (c1[h] & s1[h]) | (t1 & k0);
+        const uint64_t s0 = v[h] ^ Lw[h] ^ Rw[h];                               // bit 0
+        const uint64_t s1 = (v[h] & Lw[h]) | (v[h] & Rw[h]) | (Lw[h] & Rw[h]);  // bit 1
+        // c += s (c: 4 bits, <= 9; s: 2 bits)
+        const uint64_t k0 = c0[h] & s0;
+        c0[h] ^= s0;
+        const uint64_t t1 = c1[h] ^ s1;
+        const uint64_t k1 = (c1[h] & s1) | (t1 & k0);
         c1[h] = t1 ^ k0;
         const uint64_t k2 = c2[h] & k1;
         c2[h] ^= k1;
         c3[h] |= k2;
       }
     }
-    uint64_t me[2] = {((uint64_t)drow[ry][1] << 32) | drow[ry][0],
-                      ((uint64_t)drow[ry][3] << 32) | drow[ry][2]};
+    const uint64_t me[2] = {((uint64_t)drow[ry][1] << 32) | drow[ry][0],
+                            ((uint64_t)drow[ry][3] << 32) | drow[ry][2]};
 #pragma unroll
     for (int h = 0; h < 2; h++)  // count >= 5: 8 | (4 & (2 | 1))
       l3[ry][h] = me[h] & (c3[h] | (c2[h] & (c1[h] | c0[h])));
   }
   __syncthreads();
-  // small flags within radius 10 of the tile (region rows/cols [4, 88)), as
-  // LDS bytes (bit 2) and as bit rows built from ballots
-  __shared__ uint32_t srow[kRW][4];
-  {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int ry = w; ry < kRW; ry += 4) {
-      // large = dark & (L3 | dilate8(L3)) for this row
+  // small bit rows within radius 10 of the tile (region rows/cols [4, 88)):
+  // the restricted flood only for dark pixels not proven large
+  for (int ry = w; ry < kRW; ry += 4) {
+    unsigned long long m[2] = {0, 0};
+    if (ry >= 4 && ry < 88) {
       uint64_t dil[2] = {0, 0};
 #pragma unroll
       for (int d = -1; d <= 1; d++) {
         const int r = ry + d;
-        if (r < 0 || r >= kRW) continue;
         const uint64_t a0 = l3[r][0], a1 = l3[r][1];
         dil[0] |= a0 | (a0 << 1) | (a0 >> 1) | (a1 << 63);
         dil[1] |= a1 | (a1 << 1) | (a0 >> 63) | (a1 >> 1);
       }
-      unsigned long long m[2];
+      const uint64_t dk[2] = {((uint64_t)drow[ry][1] << 32) | drow[ry][0],
+                              ((uint64_t)drow[ry][3] << 32) | drow[ry][2]};
+      // candidate columns [4, 88): bits 4..63 of word 0, 64..87 of word 1
+      const uint64_t cand[2] = {dk[0] & ~dil[0] & ~0xFull, dk[1] & ~dil[1] & 0xFFFFFFull};
 #pragma unroll
       for (int h = 0; h < 2; h++) {
-        const int rx = h * 64 + lane;
+        if (!cand[h]) continue;  // uniform
         bool small = false;
-        const bool undecided = ((dil[h] >> lane) & 1) == 0;
-        if (undecided && ry >= 4 && ry < 88 && rx >= 4 && rx < 88 && (px[ry * kRW + rx] & 1)) {
+        if ((cand[h] >> lane) & 1) {
           uint32_t comp[9];
-          small = flood9(drow, rx, ry, comp) <= 4;
-          if (small) px[ry * kRW + rx] |= 4;
+          small = flood9(drow, h * 64 + lane, ry, comp) <= 4;
         }
         m[h] = __ballot(small);
       }
-      if (lane < 4) {
-        const unsigned long long q = m[lane >> 1];
-        srow[ry][lane] = (uint32_t)(lane & 1 ? q >> 32 : q);
-      }
+    }
+    if (lane < 4) {
+      const unsigned long long q = m[lane >> 1];
+      srow[ry][lane] = (uint32_t)(lane & 1 ? q >> 32 : q);
     }
   }
   __syncthreads();
   const int N = g.intensity;
-  for (int i = threadIdx.x; i < kNT * kNT; i += 256) {
-    const int ry = kHalo + i / kNT, rx = kHalo + i % kNT;
-    const int32_t gx = ox + rx, gy = oy + ry;
-    const uint8_t f = px[ry * kRW + rx];
-    if (!(f & 1)) continue;
-    if (g.all_seq || gx < kZone || gy < kZone) {
-      if (f & 2) {
-        uint32_t k = atomicAdd(NP.nseq, 1u);
-        if (k < (uint32_t)g.capacity) NP.seq[k] = ((uint32_t)gy << 16) | (uint32_t)gx;
-      }
-      continue;
-    }
-    if (!(f & 4)) continue;  // large component: never cleared
-    uint32_t comp[9];
-    flood9(drow, rx, ry, comp);
-    // component pixels (<= 4) relative to (rx, ry), and their bounding box
-    int cxs[4], cys[4], nc = 0;
-    int bx0 = 9, bx1 = -1, by0 = 9, by1 = -1;
+  // the tile's rows, one wave per row, lanes on the tile's 64 columns
+  for (int t = w; t < kNT; t += 4) {
+    const int ry = kHalo + t, rx = kHalo + lane;
+    const int32_t gy = oy + ry, gx = ox + rx;
+    const bool dark = (drow[ry][rx >> 5] >> (rx & 31)) & 1;
+    const bool trig = (trow[ry][rx >> 5] >> (rx & 31)) & 1;
+    const bool zone = g.all_seq || gx < kZone || gy < kZone;
+    // edge zone (and intensity > 4): every trigger is replayed in order
+    wave_append(dark & zone & trig, gx, gy, NP.nseq, NP.seq, g.capacity);
+    const bool small = !zone && ((srow[ry][rx >> 5] >> (rx & 31)) & 1);
+    bool seq = false, clear = false;
+    if (small) {
+      uint32_t comp[9];
+      flood9(drow, rx, ry, comp);
+      // component pixels (<= 4) relative to (rx, ry), and their bounding box
+      int cxs[4], cys[4], nc = 0;
+      int bx0 = 9, bx1 = -1, by0 = 9, by1 = -1;
 #pragma unroll
-    for (int r = 0; r < 9; r++) {
-      uint32_t m = comp[r];
-      if (m) {
-        by0 = imin(by0, r);
-        by1 = r;
-        bx0 = imin(bx0, __ffs(m) - 1);
-        bx1 = imax(bx1, 31 - __clz(m));
-      }
-      while (m) {
-        const int b = __ffs(m) - 1;
-        m &= m - 1;
-        if (nc < 4) {
-          cxs[nc] = b - 4;
-          cys[nc] = r - 4;
+      for (int r = 0; r < 9; r++) {
+        uint32_t mm = comp[r];
+        if (mm) {
+          by0 = imin(by0, r);
+          by1 = r;
+          bx0 = imin(bx0, __ffs(mm) - 1);
+          bx1 = imax(bx1, 31 - __clz(mm));
         }
-        nc++;
-      }
-    }
-    bool eligible = nc <= 4 && gx - 4 + bx0 >= kEligible && gy - 4 + by0 >= kEligible;
-    // no foreign small pixel within Chebyshev 7 of the component: checked on
-    // the bounding box dilated by 7 (a superset of that neighbourhood, so a
-    // component rejected here merely takes the exact sequential path)
-    if (eligible) {
-      const int X0 = rx - 4 + bx0 - 7, n = bx1 - bx0 + 15;
-      const uint32_t keep = (1u << n) - 1u;
-      int cnt = 0;
-      for (int r = ry - 4 + by0 - 7; r <= ry - 4 + by1 + 7; r++) {
-        const int word = X0 >> 5, off = X0 & 31;
-        const uint64_t v = ((uint64_t)srow[r][word + 1] << 32) | srow[r][word];
-        cnt += __popc((uint32_t)(v >> off) & keep);
-      }
-      eligible = cnt == nc;
-    }
-    if (!eligible) {
-      if (f & 2) {
-        uint32_t k = atomicAdd(NP.nseq, 1u);
-        if (k < (uint32_t)g.capacity) NP.seq[k] = ((uint32_t)gy << 16) | (uint32_t)gx;
-      }
-      continue;
-    }
-    // cleared iff some trigger of the component passes the ring test
-    bool clear = false;
-    for (int k = 0; k < nc && !clear; k++) {
-      const int cx = rx + cxs[k], cy = ry + cys[k];
-      if (!(px[cy * kRW + cx] & 2)) continue;
-      int count = 1, lc;
-      int level = 1;
-      do {
-        lc = 0;
-        for (int d = -level; d <= level; d++) {
-          lc += px[(cy - level) * kRW + cx + d] & 1;
-          lc += px[(cy + level) * kRW + cx + d] & 1;
+        while (mm) {
+          const int b = __ffs(mm) - 1;
+          mm &= mm - 1;
+          if (nc < 4) {
+            cxs[nc] = b - 4;
+            cys[nc] = r - 4;
+          }
+          nc++;
         }
-        for (int d = -(level - 1); d <= level - 1; d++) {
-          lc += px[(cy + d) * kRW + cx - level] & 1;
-          lc += px[(cy + d) * kRW + cx + level] & 1;
+      }
+      bool eligible = nc <= 4 && gx - 4 + bx0 >= kEligible && gy - 4 + by0 >= kEligible;
+      // no foreign small pixel within Chebyshev 7 of the component: checked on
+      // the bounding box dilated by 7 (a superset, so a component rejected
+      // here merely takes the exact sequential path)
+      if (eligible) {
+        const int X0 = rx - 4 + bx0 - 7, n = bx1 - bx0 + 15;
+        int cnt = 0;
+        for (int r = ry - 4 + by0 - 7; r <= ry - 4 + by1 + 7; r++)
+          cnt += __popc(row_bits(srow[r], X0, n));
+        eligible = cnt == nc;
+      }
+      if (!eligible) {
+        seq = trig;
+      } else {
+        // cleared iff some trigger of the component passes the ring test on
+        // the original image (eligible pixels are >= 40 from the edges, so the
+        // reference's unsigned ring-loop skips never apply)
+        for (int k = 0; k < nc && k < 4 && !clear; k++) {
+          const int cx = rx + cxs[k], cy = ry + cys[k];
+          if (!((trow[cy][cx >> 5] >> (cx & 31)) & 1)) continue;
+          int count = 1, lc;
+          int level = 1;
+          do {
+            lc = __popc(row_bits(drow[cy - level], cx - level, 2 * level + 1)) +
+                 __popc(row_bits(drow[cy + level], cx - level, 2 * level + 1));
+            for (int d = -(level - 1); d <= level - 1; d++) {
+              lc += (drow[cy + d][(cx - level) >> 5] >> ((cx - level) & 31)) & 1;
+              lc += (drow[cy + d][(cx + level) >> 5] >> ((cx + level) & 31)) & 1;
+            }
+            count += lc;
+            level++;
+          } while (lc != 0 && level <= N);
+          clear = count <= N;
         }
-        count += lc;
-        level++;
-      } while (lc != 0 && level <= N);
-      clear = count <= N;
+      }
     }
-    if (clear) {
-      uint32_t k = atomicAdd(NP.nclear, 1u);
-      if (k < (uint32_t)g.capacity) NP.clear[k] = ((uint32_t)gy << 16) | (uint32_t)gx;
-    }
+    wave_append(seq, gx, gy, NP.nseq, NP.seq, g.capacity);
+    wave_append(clear, gx, gy, NP.nclear, NP.clear, g.capacity);
   }
 }
 

@@ -75,11 +75,110 @@ __global__ void __launch_bounds__(kRedThreads) k_rowsum(PlaneRef ref, const Axis
   }
 }
 
+// Gray planes: the measure of one byte (gray = lightness = darkness-inverse).
+template <int MEAS>
+__device__ __forceinline__ uint32_t measure_g(uint32_t v, uint8_t thr) {
+  return MEAS == M_DARK_COUNT ? (v <= thr ? 1u : 0u) : v;
+}
+
+// axis 0 on a gray plane: a thread owns 16 consecutive columns (one aligned
+// 16-byte vector per row; rows start 256-byte aligned, so the vector lies in
+// the row's pitch) and 8 rows are loaded before they are summed.
+template <int MEAS>
+__global__ void __launch_bounds__(64) k_colsum_g(PlaneRef ref, const AxisArgs* args, uint32_t* out,
+                                                 int64_t out_stride, int rows_per_block) {
+  const int s = blockIdx.z;
+  const AxisArgs a = args[s];
+  if (!a.active) return;
+  const Rect r = a.region;
+  const int32_t vx0 = (r.x0 & ~15) + ((int32_t)blockIdx.x * 64 + (int32_t)threadIdx.x) * 16;
+  const int32_t y0 = r.y0 + (int32_t)blockIdx.y * rows_per_block;
+  if (r.x1 < r.x0 || vx0 > r.x1 || y0 > r.y1) return;
+  const int32_t y1 = imin(r.y1, y0 + rows_per_block - 1);
+  const uint8_t* base = plane_ptr(ref, s) + vx0;
+  const int64_t pitch = ref.P.pitch;
+  uint32_t acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) acc[j] = 0;
+  for (int32_t y = y0; y <= y1; y += 8) {
+    uint4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++)  // rows past y1 re-read row y1 and are not summed
+      v[k] = *reinterpret_cast<const uint4*>(base + (int64_t)imin(y + k, y1) * pitch);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if (y + k > y1) break;
+      const uint32_t wd[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+      for (int j = 0; j < 16; j++) acc[j] += measure_g<MEAS>((wd[j >> 2] >> (8 * (j & 3))) & 0xFF, a.thr);
+    }
+  }
+  uint32_t* o = out + (int64_t)s * out_stride;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const int32_t x = vx0 + j;
+    if (x >= r.x0 && x <= r.x1 && acc[j]) atomicAdd(o + x, acc[j]);
+  }
+}
+
+// axis 1 on a gray plane: one wave per row, each lane sums up to 4 aligned
+// 16-byte vectors (issued together), then a wave reduction.
+template <int MEAS>
+__global__ void __launch_bounds__(256) k_rowsum_g(PlaneRef ref, const AxisArgs* args, uint32_t* out,
+                                                  int64_t out_stride) {
+  const int s = blockIdx.z;
+  const AxisArgs a = args[s];
+  if (!a.active) return;
+  const Rect r = a.region;
+  if (r.x1 < r.x0) return;
+  const int lane = threadIdx.x & 63;
+  const int32_t y = r.y0 + (int32_t)blockIdx.x * 4 + (int32_t)(threadIdx.x >> 6);
+  if (y > r.y1) return;
+  const uint8_t* row = plane_ptr(ref, s) + (int64_t)y * ref.P.pitch;
+  const int32_t a0 = r.x0 & ~15;
+  uint32_t acc = 0;
+  for (int32_t c0 = a0; c0 <= r.x1; c0 += 64 * 16 * 4) {
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int32_t c = c0 + (k * 64 + lane) * 16;
+      const bool in = c <= r.x1;
+      v[k] = *reinterpret_cast<const uint4*>(row + (in ? c : a0));  // past x1: a valid address
+      if (!in) v[k] = make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int32_t c = c0 + (k * 64 + lane) * 16;
+      const uint32_t wd[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int32_t x = c + j;
+        const uint32_t m = measure_g<MEAS>((wd[j >> 2] >> (8 * (j & 3))) & 0xFF, a.thr);
+        acc += (x >= r.x0 && x <= r.x1) ? m : 0u;
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+  if (lane == 0) out[(int64_t)s * out_stride + y] = acc;
+}
+
 template <int FMT, int MEAS>
 static void launch_axis_t(const PlaneRef& ref, const AxisArgs* args, int axis, int32_t span_x,
                           int32_t span_y, uint32_t* out, int64_t out_stride, int count,
                           hipStream_t st) {
   if (span_x <= 0 || span_y <= 0) return;
+  if (FMT == F_GRAY8) {
+    if (axis == 0) {
+      const int rpb = 64;
+      dim3 grid((span_x + 15 + 64 * 16 - 1) / (64 * 16), (span_y + rpb - 1) / rpb, count);
+      hipLaunchKernelGGL((k_colsum_g<MEAS>), grid, dim3(64), 0, st, ref, args, out, out_stride,
+                         rpb);
+    } else {
+      dim3 grid((span_y + 3) / 4, 1, count);
+      hipLaunchKernelGGL((k_rowsum_g<MEAS>), grid, dim3(256), 0, st, ref, args, out, out_stride);
+    }
+    return;
+  }
   if (axis == 0) {
     const int rpb = 64;
     dim3 grid((span_x + kRedThreads - 1) / kRedThreads, (span_y + rpb - 1) / rpb, count);
