@@ -219,9 +219,24 @@ __global__ void __launch_bounds__(kThreads) k_apply_masks(MasksLaunch L) {
   const Planes& P = L.dst.P;
   uint8_t* base = plane_ptr(L.dst, s);
   const Px c{a->color[0], a->color[1], a->color[2]};
+  if (n == 1 && P.fmt == F_GRAY8) {
+    // one mask on a gray plane: every row is at most two runs outside it,
+    // written with 16-byte stores
+    const Rect m0 = m[0];
+    const uint8_t v = gray_of(c);
+    for (int32_t y = blockIdx.x; y < P.H; y += gridDim.x) {
+      uint8_t* row = base + (int64_t)y * P.pitch;
+      if (y < m0.y0 || y > m0.y1 || m0.x1 < 0 || m0.x0 >= P.W) {
+        fill_bytes(row, 0, P.W, v);
+      } else {
+        if (m0.x0 > 0) fill_bytes(row, 0, imin(m0.x0, P.W), v);
+        if (m0.x1 < P.W - 1) fill_bytes(row, imax(m0.x1 + 1, 0), P.W, v);
+      }
+    }
+    return;
+  }
   for (int32_t y = blockIdx.x; y < P.H; y += gridDim.x) {
     uint8_t* row = base + (int64_t)y * P.pitch;
-    // fast path: a single mask covering this row -> two runs outside it
     if (!is_mono(P.fmt)) {
       for (int32_t x = threadIdx.x; x < P.W; x += blockDim.x) {
         bool inside = false;

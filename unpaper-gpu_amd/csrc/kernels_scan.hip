@@ -81,44 +81,48 @@ __device__ __forceinline__ uint32_t measure_g(uint32_t v, uint8_t thr) {
   return MEAS == M_DARK_COUNT ? (v <= thr ? 1u : 0u) : v;
 }
 
-// axis 0 on a gray plane: a thread owns 16 consecutive columns (one aligned
-// 16-byte vector per row; rows start 256-byte aligned, so the vector lies in
-// the row's pitch) and 8 rows are loaded before they are summed.
+// axis 0 on a gray plane: a lane owns 4 consecutive columns (one aligned
+// dword per row; rows start 256-byte aligned, so it lies in the row's pitch),
+// the 4 waves of a block take quarters of the block's rows (8 loads in flight
+// per lane) and their sums meet in LDS: one atomic per column per block.
 template <int MEAS>
-__global__ void __launch_bounds__(64) k_colsum_g(PlaneRef ref, const AxisArgs* args, uint32_t* out,
-                                                 int64_t out_stride, int rows_per_block) {
+__global__ void __launch_bounds__(256) k_colsum_g(PlaneRef ref, const AxisArgs* args, uint32_t* out,
+                                                  int64_t out_stride, int rows_per_block) {
   const int s = blockIdx.z;
   const AxisArgs a = args[s];
   if (!a.active) return;
   const Rect r = a.region;
-  const int32_t vx0 = (r.x0 & ~15) + ((int32_t)blockIdx.x * 64 + (int32_t)threadIdx.x) * 16;
-  const int32_t y0 = r.y0 + (int32_t)blockIdx.y * rows_per_block;
-  if (r.x1 < r.x0 || vx0 > r.x1 || y0 > r.y1) return;
-  const int32_t y1 = imin(r.y1, y0 + rows_per_block - 1);
-  const uint8_t* base = plane_ptr(ref, s) + vx0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int32_t vx0 = (r.x0 & ~3) + ((int32_t)blockIdx.x * 64 + lane) * 4;
+  const int32_t yb = r.y0 + (int32_t)blockIdx.y * rows_per_block;
+  if (r.x1 < r.x0 || yb > r.y1) return;
+  const int32_t ye = imin(r.y1, yb + rows_per_block - 1);
+  const int32_t q = (rows_per_block + 3) / 4;
+  const int32_t y0 = yb + w * q, y1 = imin(ye, y0 + q - 1);
+  const bool col_ok = vx0 <= r.x1;
+  const uint8_t* base = plane_ptr(ref, s) + (col_ok ? vx0 : (r.x0 & ~3));
   const int64_t pitch = ref.P.pitch;
-  uint32_t acc[16];
-#pragma unroll
-  for (int j = 0; j < 16; j++) acc[j] = 0;
+  uint32_t acc[4] = {0, 0, 0, 0};
   for (int32_t y = y0; y <= y1; y += 8) {
-    uint4 v[8];
+    uint32_t v[8];
 #pragma unroll
     for (int k = 0; k < 8; k++)  // rows past y1 re-read row y1 and are not summed
-      v[k] = *reinterpret_cast<const uint4*>(base + (int64_t)imin(y + k, y1) * pitch);
+      v[k] = *reinterpret_cast<const uint32_t*>(base + (int64_t)imin(y + k, y1) * pitch);
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-      if (y + k > y1) break;
-      const uint32_t wd[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+      const uint32_t keep = (y + k <= y1) ? 1u : 0u;
 #pragma unroll
-      for (int j = 0; j < 16; j++) acc[j] += measure_g<MEAS>((wd[j >> 2] >> (8 * (j & 3))) & 0xFF, a.thr);
+      for (int j = 0; j < 4; j++) acc[j] += keep * measure_g<MEAS>((v[k] >> (8 * j)) & 0xFF, a.thr);
     }
   }
-  uint32_t* o = out + (int64_t)s * out_stride;
+  __shared__ uint32_t red[4][64 * 4];
 #pragma unroll
-  for (int j = 0; j < 16; j++) {
-    const int32_t x = vx0 + j;
-    if (x >= r.x0 && x <= r.x1 && acc[j]) atomicAdd(o + x, acc[j]);
-  }
+  for (int j = 0; j < 4; j++) red[w][lane * 4 + j] = acc[j];
+  __syncthreads();
+  const int c = threadIdx.x;  // 256 columns of the block
+  const int32_t x = (r.x0 & ~3) + (int32_t)blockIdx.x * 256 + c;
+  const uint32_t t = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  if (x >= r.x0 && x <= r.x1 && t) atomicAdd(out + (int64_t)s * out_stride + x, t);
 }
 
 // axis 1 on a gray plane: one wave per row, each lane sums up to 4 aligned
@@ -169,9 +173,9 @@ static void launch_axis_t(const PlaneRef& ref, const AxisArgs* args, int axis, i
   if (span_x <= 0 || span_y <= 0) return;
   if (FMT == F_GRAY8) {
     if (axis == 0) {
-      const int rpb = 64;
-      dim3 grid((span_x + 15 + 64 * 16 - 1) / (64 * 16), (span_y + rpb - 1) / rpb, count);
-      hipLaunchKernelGGL((k_colsum_g<MEAS>), grid, dim3(64), 0, st, ref, args, out, out_stride,
+      const int rpb = 256;
+      dim3 grid((span_x + 3 + 255) / 256, (span_y + rpb - 1) / rpb, count);
+      hipLaunchKernelGGL((k_colsum_g<MEAS>), grid, dim3(256), 0, st, ref, args, out, out_stride,
                          rpb);
     } else {
       dim3 grid((span_y + 3) / 4, 1, count);
