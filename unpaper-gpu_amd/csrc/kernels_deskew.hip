@@ -310,14 +310,30 @@ __global__ void __launch_bounds__(256) k_rot_final(RotGeom g, const RotTable* ta
 
 // ---- k_rot_line: direct walk of one flagged line (any edge) ---------------
 template <int FMT>
+__device__ void walk_line(PlaneRef img, const RotGeom& g, const RotTable* table, const Rect* masks,
+                          int mask_index, int32_t* peaks, int a, int e, int s);
+
+template <int FMT>
 __global__ void __launch_bounds__(256) k_rot_line(PlaneRef img, RotGeom g, const RotTable* table,
                                                   const Rect* masks, const int32_t* mask_active,
                                                   int mask_index, int32_t* peaks, int count,
                                                   int max_scan, RotScratch R) {
-  const int a = blockIdx.x, e = blockIdx.y, s = blockIdx.z;
   const int na = table->nangles;
-  const int t = (s * g.nedges + e) * na + a;
-  if (!R.flag[t] || (mask_active && !mask_active[s])) return;
+  const int nlines = count * g.nedges * na;
+  // grid-strided over the lines: only flagged ones are walked, so an empty
+  // fallback costs one flag read per line
+  for (int t = blockIdx.x; t < nlines; t += gridDim.x) {
+    const int a = t % na, e = (t / na) % g.nedges, s = t / (na * g.nedges);
+    if (!R.flag[t] || (mask_active && !mask_active[s])) continue;
+    walk_line<FMT>(img, g, table, masks, mask_index, peaks, a, e, s);
+    __syncthreads();  // the block's LDS is reused by its next line
+  }
+}
+
+template <int FMT>
+__device__ void walk_line(PlaneRef img, const RotGeom& g, const RotTable* table, const Rect* masks,
+                          int mask_index, int32_t* peaks, int a, int e, int s) {
+  const int na = table->nangles;
   int32_t* out = peaks + (((int64_t)s * g.max_masks + mask_index) * 4 + e) * na + a;
   const Rect mask = masks[s];
   const int sxh = g.edge_shift[e][0], syv = g.edge_shift[e][1];
@@ -410,8 +426,8 @@ static void launch_rot_t(const PlaneRef& img, const RotGeom& g, const RotTable* 
   if (lds > 64 * 1024)
     hipFuncSetAttribute((const void*)k_rot_line<FMT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)lds);
-  hipLaunchKernelGGL(k_rot_line<FMT>, dim3(nangles, g.nedges, count), dim3(256), lds, st, img, g,
-                     table, masks, mask_active, mask_index, peaks, count, max_scan, R);
+  hipLaunchKernelGGL(k_rot_line<FMT>, dim3(imin(nlines, 1024)), dim3(256), lds, st, img, g, table,
+                     masks, mask_active, mask_index, peaks, count, max_scan, R);
 }
 
 void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable* table,
