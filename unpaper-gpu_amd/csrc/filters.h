@@ -101,6 +101,8 @@ void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable
                            int32_t* lines);
 // Scratch for the scan-line point lists of one launch_rotation_peaks call.
 size_t rotation_lines_bytes(int count, int nedges, int nangles, int max_scan);
+// Per-line fallback flags inside that scratch (diagnostics).
+const int32_t* rotation_line_flags(const int32_t* lines, int nlines, int max_scan);
 // Host: the angle sequence of detect_edge_rotation (deskew.c:153-174).
 int rotation_angles(const UphipDeskewParameters& p, RotTable* t);
 // Host: detect_rotation_cpu's combination of per-edge results (deskew.c:219-240)

@@ -506,12 +506,77 @@ __global__ void __launch_bounds__(kThreads) k_move_rect(PlaneRef src, PlaneRef d
   }
 }
 
+// k_move_rect for gray planes (raw copies and the background are the same
+// bytes as set_pixel writes): one aligned dword of the destination per lane.
+// A dword wholly outside the move, wholly background or wholly inside the
+// pasted rectangle is one aligned load, a constant, or two aligned loads and
+// a funnel shift; only dwords on span edges go byte by byte.
+__global__ void __launch_bounds__(kThreads) k_move_rect_g(PlaneRef src, PlaneRef dst,
+                                                          const MoveArgs* args) {
+  const int s = blockIdx.z;
+  const MoveArgs a = args[s];
+  if (!a.active) return;
+  const Planes& P = src.P;
+  const uint8_t* sbase = plane_ptr(src, s);
+  uint8_t* dbase = plane_ptr(dst, s);
+  const Rect A = clip(a.area, P.W, P.H);
+  const int32_t aw = A.x1 - A.x0 + 1, ah = A.y1 - A.y0 + 1;
+  const int32_t sw = iabs(a.area.x0 - a.area.x1) + 1, sh = iabs(a.area.y0 - a.area.y1) + 1;
+  const uint8_t bg = gray_of(Px{a.bg[0], a.bg[1], a.bg[2]});
+  const uint32_t bg4 = bg * 0x01010101u;
+  const int32_t nd = (P.W + 3) >> 2;
+  for (int32_t y = blockIdx.x; y < P.H; y += gridDim.x) {
+    const uint8_t* srow = sbase + (int64_t)y * P.pitch;
+    uint32_t* drow = reinterpret_cast<uint32_t*>(dbase + (int64_t)y * P.pitch);
+    const int32_t v = y - a.ty;
+    const bool trow = v >= 0 && v < sh;              // row crosses the pasted rectangle
+    const bool mrow = trow && v < ah;                // ... and its copied extent
+    const bool arow = y >= A.y0 && y <= A.y1;        // row crosses the wiped area
+    const uint8_t* mrow_p = sbase + (int64_t)(A.y0 + (mrow ? v : 0)) * P.pitch;
+    for (int32_t d = threadIdx.x; d < nd; d += blockDim.x) {
+      const int32_t x0 = d * 4;
+      // class of columns x0..x0+3: 0 unchanged, 1 background, 2 moved
+      int cls[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int32_t x = x0 + j, u = x - a.tx;
+        if (trow && u >= 0 && u < sw) cls[j] = (mrow && u < aw) ? 2 : 1;
+        else cls[j] = (arow && x >= A.x0 && x <= A.x1) ? 1 : 0;
+      }
+      const bool uni = cls[0] == cls[1] && cls[1] == cls[2] && cls[2] == cls[3];
+      uint32_t out;
+      if (uni && cls[0] == 0) {
+        out = *reinterpret_cast<const uint32_t*>(srow + x0);
+      } else if (uni && cls[0] == 1) {
+        out = bg4;
+      } else if (uni && (((A.x0 + (x0 - a.tx)) & ~3) + 8 <= P.pitch)) {
+        const int32_t sx = A.x0 + (x0 - a.tx);       // inside the clipped area
+        const int32_t sa = sx & ~3;                  // sa + 7 within the row's pitch
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(mrow_p + sa);
+        const uint64_t w2 = ((uint64_t)q[1] << 32) | q[0];
+        out = (uint32_t)(w2 >> (8 * (sx - sa)));
+      } else {
+        out = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int32_t x = x0 + j;
+          uint8_t b;
+          if (cls[j] == 0) b = x < P.W ? srow[x] : 0;
+          else if (cls[j] == 1) b = bg;
+          else b = mrow_p[A.x0 + (x - a.tx)];
+          out |= (uint32_t)b << (8 * j);
+        }
+      }
+      drow[d] = out;
+    }
+  }
+}
+
 void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* args, int count,
                       hipStream_t st) {
   int gx = src.P.H < 1 ? 1 : (src.P.H > 1024 ? 1024 : src.P.H);
   if (src.P.fmt == F_GRAY8)
-    hipLaunchKernelGGL(k_move_rect<F_GRAY8>, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst,
-                       args);
+    hipLaunchKernelGGL(k_move_rect_g, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst, args);
   else if (src.P.fmt == F_Y400A)
     hipLaunchKernelGGL(k_move_rect<F_Y400A>, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst,
                        args);

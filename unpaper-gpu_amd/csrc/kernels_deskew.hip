@@ -87,8 +87,10 @@ __device__ __forceinline__ LineSetup line_setup(const Rect& mask, const RotGeom&
 //   ends   [nlines][2]          first and last column of the line
 //   part   [nlines][nslices][kDepth]  band slice sums
 //   flag   [nlines]             1 = walk the line directly (k_rot_line)
+//   state  [nlines][4]          band result after kDepth steps: accumulated,
+//                               last step's blackness, peak, valid
 struct RotScratch {
-  int32_t *cols, *ends, *part, *flag;
+  int32_t *cols, *ends, *part, *flag, *state;
 };
 
 __host__ __device__ static inline int rot_slices(int max_scan) { return (max_scan + kSliceRows - 1) / kSliceRows; }
@@ -101,14 +103,20 @@ __host__ __device__ static inline RotScratch rot_scratch(int32_t* base, int nlin
   r.ends = r.cols + (int64_t)nlines * ms;
   r.part = r.ends + 2 * (int64_t)nlines;
   r.flag = r.part + (int64_t)nlines * ns * kDepth;
+  r.state = r.flag + nlines;
   return r;
+}
+
+const int32_t* rotation_line_flags(const int32_t* lines, int nlines, int max_scan) {
+  return rot_scratch(const_cast<int32_t*>(lines), nlines, max_scan).flag;
 }
 
 size_t rotation_lines_bytes(int count, int nedges, int nangles, int max_scan) {
   const int64_t nlines = (int64_t)count * nedges * nangles;
   const int64_t ms = max_scan > 0 ? max_scan : 1;
   const int64_t ns = (ms + kSliceRows - 1) / kSliceRows;
-  return sizeof(int32_t) * (size_t)(nlines * ms + 2 * nlines + nlines * ns * kDepth + nlines);
+  return sizeof(int32_t) * (size_t)(nlines * ms + 2 * nlines + nlines * ns * kDepth + nlines +
+                                    4 * nlines);
 }
 
 // ---- k_rot_points: one lane per left/right line, the recurrence in order --
@@ -160,6 +168,7 @@ __global__ void __launch_bounds__(64) k_rot_points(RotGeom g, const RotTable* ta
     R.ends[2 * t] = first;
     R.ends[2 * t + 1] = last;
     R.flag[t] = live ? 0 : 1;
+    R.state[4 * t + 3] = 0;
   }
 }
 
@@ -290,8 +299,21 @@ __global__ void __launch_bounds__(256) k_rot_final(RotGeom g, const RotTable* ta
     if (!(before < maxAbs && 2 * lane + k < LS.maxDepth)) kfail = k;
   }
   const unsigned long long F = __ballot(kfail < 2);
-  if (!F) {  // still accumulating after kDepth steps: walk the line directly
-    if (lane == 0) R.flag[t] = 1;
+  if (!F) {
+    // still accumulating after kDepth steps: k_rot_line continues the walk
+    // from step kDepth with the loop state reached here
+    const int up1 = __shfl_up(B[1], 1, 64);
+    const int prev0 = lane == 0 ? 0 : up1;
+    int md = max(B[0] - prev0, B[1] - B[0]);
+    for (int o = 32; o > 0; o >>= 1) md = max(md, __shfl_xor(md, o, 64));
+    const int last = __shfl(B[1], 63, 64);
+    if (lane == 0) {
+      R.state[4 * t] = tot;
+      R.state[4 * t + 1] = last;
+      R.state[4 * t + 2] = md > 0 ? md : 0;
+      R.state[4 * t + 3] = 1;
+      R.flag[t] = 1;
+    }
     return;
   }
   const int fl = __ffsll((long long)F) - 1;
@@ -311,7 +333,8 @@ __global__ void __launch_bounds__(256) k_rot_final(RotGeom g, const RotTable* ta
 // ---- k_rot_line: direct walk of one flagged line (any edge) ---------------
 template <int FMT>
 __device__ void walk_line(PlaneRef img, const RotGeom& g, const RotTable* table, const Rect* masks,
-                          int mask_index, int32_t* peaks, int a, int e, int s);
+                          int mask_index, int32_t* peaks, int a, int e, int s, int t,
+                          int max_scan, const RotScratch& R);
 
 template <int FMT>
 __global__ void __launch_bounds__(256) k_rot_line(PlaneRef img, RotGeom g, const RotTable* table,
@@ -325,14 +348,15 @@ __global__ void __launch_bounds__(256) k_rot_line(PlaneRef img, RotGeom g, const
   for (int t = blockIdx.x; t < nlines; t += gridDim.x) {
     const int a = t % na, e = (t / na) % g.nedges, s = t / (na * g.nedges);
     if (!R.flag[t] || (mask_active && !mask_active[s])) continue;
-    walk_line<FMT>(img, g, table, masks, mask_index, peaks, a, e, s);
+    walk_line<FMT>(img, g, table, masks, mask_index, peaks, a, e, s, t, max_scan, R);
     __syncthreads();  // the block's LDS is reused by its next line
   }
 }
 
 template <int FMT>
 __device__ void walk_line(PlaneRef img, const RotGeom& g, const RotTable* table, const Rect* masks,
-                          int mask_index, int32_t* peaks, int a, int e, int s) {
+                          int mask_index, int32_t* peaks, int a, int e, int s, int t,
+                          int max_scan, const RotScratch& R) {
   const int na = table->nangles;
   int32_t* out = peaks + (((int64_t)s * g.max_masks + mask_index) * 4 + e) * na + a;
   const Rect mask = masks[s];
@@ -349,7 +373,16 @@ __device__ void walk_line(PlaneRef img, const RotGeom& g, const RotTable* table,
   }
   int32_t* px = pts;
   int32_t* py = pts + scan;
-  if (threadIdx.x == 0) {
+  // a left/right line continues from the band's state after kDepth steps,
+  // with the point lists k_rot_points built; others start from scratch
+  const bool resume = R.state[4 * t + 3] != 0;
+  if (syv == 0) {
+    const int32_t ystart = (int32_t)LS.Y;  // rows: Ystart + i exactly
+    for (int i = threadIdx.x; i < scan; i += blockDim.x) {
+      px[i] = R.cols[(int64_t)t * max_scan + i];
+      py[i] = ystart + i;
+    }
+  } else if (threadIdx.x == 0) {
     // the float recurrence of deskew.c:107-112, in order
     float X = LS.X, Y = LS.Y;
     for (int i = 0; i < scan; i++) {
@@ -358,6 +391,8 @@ __device__ void walk_line(PlaneRef img, const RotGeom& g, const RotTable* table,
       X += LS.stepX;
       Y += LS.stepY;
     }
+  }
+  if (threadIdx.x == 0) {
     done_flag = 0;
     result = 0;
   }
@@ -366,7 +401,14 @@ __device__ void walk_line(PlaneRef img, const RotGeom& g, const RotTable* table,
   const uint8_t* base = plane_ptr(img, s);
   const Rect nm = normalize(mask);
   int carry_acc = 0, last = 0, maxDiff = 0;  // wave 0 state
-  for (int d0 = 0; d0 < maxDepth; d0 += 64) {
+  int dstart = 0;
+  if (resume) {
+    carry_acc = R.state[4 * t];
+    last = R.state[4 * t + 1];
+    maxDiff = R.state[4 * t + 2];
+    dstart = kDepth;
+  }
+  for (int d0 = dstart; d0 < maxDepth; d0 += 64) {
     const int dep = d0 + lane;
     int acc = 0;
     // unconditional clamped loads, masked arithmetically (get_pixel's white

@@ -1,6 +1,8 @@
 // ops_filters.hip — filter and rotation-detection ops of the C ABI
 // (imageprocess/filters.c, deskew.c peers) for single device frames.
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "filters.h"
@@ -144,6 +146,15 @@ float uphip_detect_rotation(UphipImage image, UphipRectangle mask,
   std::vector<int32_t> hp(4 * (size_t)(na > 0 ? na : 1));
   UPH_HIP(hipMemcpyAsync(hp.data(), peaks, sizeof(int32_t) * g.nedges * na,
                          hipMemcpyDeviceToHost, st));
+  if (getenv("UPHIP_DEBUG_ROTATION")) {  // diagnostics: lines left to the direct walk
+    std::vector<int32_t> fl((size_t)g.nedges * na);
+    UPH_HIP(hipMemcpyAsync(fl.data(), rotation_line_flags(lines, g.nedges * na, max_scan),
+                           sizeof(int32_t) * fl.size(), hipMemcpyDeviceToHost, st));
+    UPH_HIP(hipStreamSynchronize(st));
+    int nf = 0;
+    for (int32_t f : fl) nf += f != 0;
+    fprintf(stderr, "uphip: detect_rotation %d of %d lines walked directly\n", nf, (int)fl.size());
+  }
   if (!UPH_HIP(hipStreamSynchronize(st))) return 0.0f;
   float rot[4];
   int count = 0, e = 0;

@@ -9,6 +9,8 @@
 // in HBM: small per-sheet control kernels turn detection results into the
 // arguments of the next data kernel, so a batch runs start to finish without
 // a host round trip.  One launch per stage covers every sheet (grid.z).
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -1047,6 +1049,23 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
       launch_rotation_peaks(cur_ref(P, b->ctl), rg, b->dtable, b->pick_mask, b->pick_active,
                             (int)i, b->peaks, count, b->st, b->table.nangles, b->max_scan,
                             b->rot_lines);
+      if (getenv("UPHIP_DEBUG_ROTATION")) {  // diagnostics: lines left to the direct walk
+        const int nl = count * rg.nedges * b->table.nangles;
+        std::vector<int32_t> fl((size_t)nl);
+        UPH_HIP(hipMemcpyAsync(fl.data(), rotation_line_flags(b->rot_lines, nl, b->max_scan),
+                               sizeof(int32_t) * nl, hipMemcpyDeviceToHost, b->st));
+        UPH_HIP(hipStreamSynchronize(b->st));
+        int nf = 0;
+        for (int t = 0; t < nl; t++)
+          if (fl[t]) {
+            if (nf < 8)
+              fprintf(stderr, "uphip: line sheet %d edge %d angle %d walked directly\n",
+                      t / (rg.nedges * b->table.nangles), (t / b->table.nangles) % rg.nedges,
+                      t % b->table.nangles);
+            nf++;
+          }
+        fprintf(stderr, "uphip: batch rotation %d of %d lines walked directly\n", nf, nl);
+      }
       ra.mask_index = (int)i;
       hipLaunchKernelGGL(k_rot_select, dim3((count + 255) / 256), dim3(256), 0, b->st, b->ctl,
                          b->peaks, b->dtable, b->dcombo, ra, b->rot_args, count);
