@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--pages", type=int, default=1000, help="pages per GPU")
     ap.add_argument("--batch", type=int, default=32, help="sheets per batch launch sequence")
-    ap.add_argument("--streams", type=int, default=4, help="batches (HIP streams) in flight")
+    ap.add_argument("--streams", type=int, default=16, help="batches (HIP streams) in flight")
     ap.add_argument("--cpu-pages", type=int, default=0,
                     help="CPU baseline sample (0 = 2 pages per host thread)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, host cores)")

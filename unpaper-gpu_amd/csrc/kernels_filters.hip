@@ -114,6 +114,62 @@ __global__ void __launch_bounds__(256) k_gray_cells(PlaneRef img, GrayGeom g, ui
   P.light[c] = light;
 }
 
+// k_gray_cells for a gray plane: one workgroup per strip of cell rows.  Each
+// lane sums aligned dwords of the strip's rows (all of a round's loads in
+// flight) into per-column 16-bit totals in LDS (ch <= 257 keeps 255*ch in
+// 16 bits), then one lane per cell adds its cw columns.
+constexpr int kGrayStripMaxW = 16384;
+__global__ void __launch_bounds__(256) k_gray_cells_g(PlaneRef img, GrayGeom g, uint8_t* scratch,
+                                                      int64_t sstride, const int32_t* active) {
+  const int s = blockIdx.z;
+  if (active && !active[s]) return;
+  const int32_t cy = blockIdx.x;
+  GrayPtrs P = gray_ptrs(g, scratch + s * sstride);
+  const uint8_t* base = plane_ptr(img, s);
+  const int32_t y0 = cy * g.ch, y1 = imin(y0 + g.ch, g.H);
+  extern __shared__ uint16_t cols16[];  // [W] dark counts, then [W] lightness sums
+  uint16_t* cdark = cols16;
+  uint16_t* clight = cols16 + ((g.W + 3) & ~3);
+  const int32_t nd = (g.W + 3) >> 2;
+  for (int32_t d = threadIdx.x; d < nd; d += 256) {
+    uint32_t dk[4] = {0, 0, 0, 0}, lt[4] = {0, 0, 0, 0};
+    for (int32_t y = y0; y < y1; y += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        v[k] = *reinterpret_cast<const uint32_t*>(base + (int64_t)imin(y + k, y1 - 1) * img.P.pitch +
+                                                  4 * d);
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t keep = y + k < y1 ? 1u : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t px = (v[k] >> (8 * j)) & 0xFF;
+          dk[j] += keep & (px <= g.black_thr ? 1u : 0u);
+          lt[j] += keep * px;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      cdark[4 * d + j] = (uint16_t)dk[j];
+      clight[4 * d + j] = (uint16_t)lt[j];
+    }
+  }
+  __syncthreads();
+  for (int32_t cx = threadIdx.x; cx < g.ncx; cx += 256) {
+    const int32_t x0 = cx * g.cw, x1 = imin(x0 + g.cw, g.W);
+    uint32_t dark = 0, light = 0;
+    for (int32_t x = x0; x < x1; x++) {
+      dark += cdark[x];
+      light += clight[x];
+    }
+    const size_t c = (size_t)cy * g.ncx + cx;
+    P.dark[c] = dark;
+    P.light[c] = light;
+  }
+}
+
 __device__ __forceinline__ uint32_t cell_pixels(const GrayGeom& g, int32_t cx, int32_t cy) {
   const int32_t w = imin((cx + 1) * g.cw, g.W) - cx * g.cw;
   const int32_t h = imin((cy + 1) * g.ch, g.H) - cy * g.ch;
@@ -257,7 +313,11 @@ template <int FMT>
 static void launch_gray_t(const PlaneRef& img, const GrayGeom& g, uint8_t* scr, int64_t ss,
                           const int32_t* active, int count, hipStream_t st) {
   dim3 grid((g.ncx + 255) / 256, g.ncy, count);
-  hipLaunchKernelGGL(k_gray_cells<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active);
+  if (FMT == F_GRAY8 && g.W <= kGrayStripMaxW && g.ch <= 257)
+    hipLaunchKernelGGL(k_gray_cells_g, dim3(g.ncy, 1, count), dim3(256),
+                       4 * (size_t)((g.W + 3) & ~3), st, img, g, scr, ss, active);
+  else
+    hipLaunchKernelGGL(k_gray_cells<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active);
   hipLaunchKernelGGL(k_gray_decide, dim3(count), dim3(1024), 0, st, g, scr, ss, active);
   hipLaunchKernelGGL(k_gray_wipe<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active);
 }
