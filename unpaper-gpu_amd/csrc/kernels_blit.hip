@@ -750,21 +750,6 @@ __device__ __forceinline__ uint8_t cubic_int(float f, float h, int a, int b, int
   return (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));  // av_clip_uint8
 }
 
-// cubic_scale on four taps packed as bytes of `w` (tap k in byte k), each
-// biased by -128 (w ^ 0x80808080 read as int8).  2a-5b+4c-d, 3(b-c)+d-a and
-// c-a have weights summing to zero, so the bias cancels and each is one
-// signed 4-way byte dot product; the float part is cubic_int's, in order.
-__device__ __forceinline__ int cubic_dot(float f, float h, uint32_t wb) {
-  const int s1 = __builtin_amdgcn_sdot4((int)wb, (int)0xFF04FB02u, 0, false);  // 2,-5,4,-1
-  const int s2 = __builtin_amdgcn_sdot4((int)wb, (int)0x01FD03FFu, 0, false);  // -1,3,-3,1
-  const int dd = __builtin_amdgcn_sdot4((int)wb, (int)0x000100FFu, 0, false);  // -1,0,1,0
-  const int b = (int)((wb >> 8) & 0xFFu) ^ 0x80;
-  const float u = (float)s1 + f * (float)s2;
-  const float v = (float)dd + f * u;
-  const int r = (int)((float)b + h * v);
-  return r < 0 ? 0 : (r > 255 ? 255 : r);  // av_clip_uint8
-}
-
 // deskew rotate for a gray plane with bicubic interpolation (the default):
 // k_rotate_mask's tiling and staging, with the taps read straight from the
 // window and no other interpolation code in the kernel.
@@ -778,7 +763,6 @@ template <int FMT>
 __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, PlaneRef dst,
                                                                 const RotateArgs* args) {
   __shared__ uint8_t stage[kRotGCap];
-  __shared__ uint32_t quad[kRotGCap];  // biased taps of columns c..c+3 per position
   const int s = blockIdx.z;
   const RotateArgs a = args[s];
   if (!a.active) return;
@@ -835,14 +819,6 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
         if (i < n) stage[i] = v[k];
       }
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += kThreads) {
-      const int c = i - (i / bw) * bw;
-      if (c + 3 >= bw) continue;  // never the first tap of a row
-      const uint32_t wv = (uint32_t)stage[i] | ((uint32_t)stage[i + 1] << 8) |
-                          ((uint32_t)stage[i + 2] << 16) | ((uint32_t)stage[i + 3] << 24);
-      quad[i] = wv ^ 0x80808080u;
-    }
   }
   __syncthreads();
   const Src<FMT> S{sbase, P.pitch, P.W, P.H};
@@ -864,11 +840,11 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
         const int ix = (int)srcX, iy = (int)srcY;  // interp_bicubic truncates
         const float fx = srcX - ix, fy = srcY - iy;
         const float hx = 0.5f * fx, hy = 0.5f * fy;
-        const uint32_t* q = quad + (iy - 1 - by0) * bw + (ix - 1 - bx0);
-        uint32_t cw = 0;
+        const uint8_t* t = stage + (iy - 1 - by0) * bw + (ix - 1 - bx0);
+        int col[4];
 #pragma unroll
-        for (int r = 0; r < 4; r++) cw |= (uint32_t)cubic_dot(fx, hx, q[r * bw]) << (8 * r);
-        o = (uint8_t)cubic_dot(fy, hy, cw ^ 0x80808080u);
+        for (int r = 0; r < 4; r++, t += bw) col[r] = cubic_int(fx, hx, t[0], t[1], t[2], t[3]);
+        o = cubic_int(fy, hy, col[0], col[1], col[2], col[3]);
       } else {
         o = interp_bicubic(S, srcX, srcY).r;
       }

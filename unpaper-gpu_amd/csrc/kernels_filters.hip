@@ -375,6 +375,50 @@ __device__ __forceinline__ void blur_rect_origin(const BlurGeom& g, int32_t r, i
   }
 }
 
+// k_blur_counts for a gray plane: one workgroup per row of rectangles (the
+// first row at y = 0, row t at step_y + t*sh).  Lanes count dark pixels
+// (gray <= white) of aligned dwords over the strip's rows into per-column
+// 16-bit totals in LDS, then one lane per rectangle adds its sw columns.
+__global__ void __launch_bounds__(256) k_blur_counts_g(PlaneRef img, BlurGeom g, uint8_t* scratch,
+                                                       int64_t sstride, const int32_t* active) {
+  const int s = blockIdx.y;
+  if (active && !active[s]) return;
+  const int32_t row = blockIdx.x;  // 0: the top row of rectangles, 1 + t: row t
+  const int32_t ry = row == 0 ? 0 : (row - 1) * g.sh + g.step_y;
+  const int32_t y0 = imax(ry, 0), y1 = imin(ry + g.sh, g.H);  // [y0, y1)
+  const uint8_t* base = plane_ptr(img, s);
+  extern __shared__ uint16_t ccount[];
+  const int32_t nd = (g.W + 3) >> 2;
+  for (int32_t d = threadIdx.x; d < nd; d += 256) {
+    uint32_t c[4] = {0, 0, 0, 0};
+    for (int32_t y = y0; y < y1; y += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        v[k] = *reinterpret_cast<const uint32_t*>(base + (int64_t)imin(y + k, y1 - 1) * img.P.pitch +
+                                                  4 * d);
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t keep = y + k < y1 ? 1u : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; j++) c[j] += keep & (((v[k] >> (8 * j)) & 0xFF) <= g.white ? 1u : 0u);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) ccount[4 * d + j] = (uint16_t)c[j];
+  }
+  __syncthreads();
+  const int32_t nr = row == 0 ? g.bpr : g.bpr + 1;
+  uint32_t* counts = (uint32_t*)(scratch + s * sstride);
+  for (int32_t j = threadIdx.x; j < nr; j += 256) {
+    const int32_t x0 = imax(j * g.sw, 0), x1 = imin(j * g.sw + g.sw, g.W);
+    uint32_t n = 0;
+    if (y0 < y1)
+      for (int32_t x = x0; x < x1; x++) n += ccount[x];
+    counts[row == 0 ? j : g.bpr + (row - 1) * (g.bpr + 1) + j] = n;
+  }
+}
+
 template <int FMT>
 __global__ void __launch_bounds__(256) k_blur_counts(PlaneRef img, BlurGeom g, uint8_t* scratch,
                                                      int64_t sstride, const int32_t* active) {
@@ -473,7 +517,10 @@ __global__ void __launch_bounds__(256) k_blur_wipe(PlaneRef img, BlurGeom g, uin
 template <int FMT>
 static void launch_blur_t(const PlaneRef& img, const BlurGeom& g, uint8_t* scr, int64_t ss,
                           const int32_t* active, int count, hipStream_t st) {
-  if (g.nrect > 0)
+  if (g.nrect > 0 && FMT == F_GRAY8 && g.sh <= 65535 && g.W <= (1 << 16))
+    hipLaunchKernelGGL(k_blur_counts_g, dim3(1 + g.T, count), dim3(256),
+                       2 * (size_t)((g.W + 3) & ~3), st, img, g, scr, ss, active);
+  else if (g.nrect > 0)
     hipLaunchKernelGGL(k_blur_counts<FMT>, dim3(g.nrect, count), dim3(256), 0, st, img, g, scr, ss,
                        active);
   const size_t lds = sizeof(uint64_t) * ((size_t)g.nrect + 3 * (size_t)(g.bpr + 2));
