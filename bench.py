@@ -56,6 +56,10 @@ STAGE_PLANES = {
 }
 
 
+ROOFLINE_STAGE = "deskew_rotate"
+ROOFLINE_KERNEL = "k_rotate_cubic_gray"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -236,8 +240,10 @@ def main():
 
     roofline = None
     if totals:
-        dom = max((k for k in totals if k in STAGE_PLANES), key=lambda k: totals[k],
-                  default=max(totals, key=totals.get))
+        # the dominant full-chip kernel: the bicubic rotation (its stage events
+        # bracket exactly that launch); the one-wave/one-block sequential
+        # replays are latency bound and overlap other streams' work
+        dom = ROOFLINE_STAGE if ROOFLINE_STAGE in totals else max(totals, key=totals.get)
         avg_ms = totals[dom] / max(nlaunch, 1)
         alg = STAGE_PLANES.get(dom, 1.0) * W * H * (npages * args.steps / max(nlaunch, 1))
         achieved = alg / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
@@ -251,7 +257,8 @@ def main():
         roofline = {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": dom, "alg_bytes_per_launch": int(alg), "avg_launch_ms": round(avg_ms, 3),
+            "kernel": ROOFLINE_KERNEL if dom == ROOFLINE_STAGE else dom,
+            "alg_bytes_per_launch": int(alg), "avg_launch_ms": round(avg_ms, 3),
             "pipeline_frac": round(pages_per_s / max(d.world, 1) * ALG_BYTES_PER_PAGE /
                                    (HBM_PEAK_GBS * 1e9), 5),
         }

@@ -762,7 +762,8 @@ constexpr int kRotGCap = 6144; // its staged pixels per tile
 template <int FMT>
 __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, PlaneRef dst,
                                                                 const RotateArgs* args) {
-  __shared__ uint8_t stage[kRotGCap];
+  __shared__ uint32_t stage32[kRotGCap / 4];
+  uint8_t* stage = reinterpret_cast<uint8_t*>(stage32);
   const int s = blockIdx.z;
   const RotateArgs a = args[s];
   if (!a.active) return;
@@ -796,9 +797,52 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
     by0 = (int32_t)floorf(mny) - 3;
     bw = (int32_t)floorf(mxx) + 4 - bx0 + 1;
     bh = (int32_t)floorf(mxy) + 4 - by0 + 1;
-    staged = bw > 0 && bh > 0 && (int64_t)bw * bh <= kRotGCap;
+    staged = bw > 0 && bh > 0;
   }
-  if (staged) {
+  // gray planes stage whole aligned dwords: row r of the window starts at
+  // byte `lead` of a `sstride`-byte LDS row
+  const int32_t xa = bx0 >= 0 ? (bx0 & ~3) : -((-bx0 + 3) & ~3);
+  const int lead = FMT == F_GRAY8 ? bx0 - xa : 0;
+  const int nd = (lead + bw + 3) >> 2;
+  const int sstride = FMT == F_GRAY8 ? 4 * nd : bw;
+  staged = staged && (int64_t)sstride * bh <= kRotGCap;
+  if (staged && FMT == F_GRAY8) {
+    const int n = nd * bh;
+    for (int b0 = 0; b0 < n; b0 += 8 * kThreads) {
+      uint32_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = b0 + k * kThreads + threadIdx.x;
+        const int r = i / nd;
+        const int32_t xd = xa + 4 * (i - r * nd), y = by0 + r;
+        const bool row_ok = (y >= 0) & (y < P.H);
+        const uint8_t* row = sbase + (int64_t)imin(imax(y, 0), P.H - 1) * P.pitch;
+        // interior dwords: one aligned load (xd is a multiple of 4)
+        v[k] = *reinterpret_cast<const uint32_t*>(row + imin(imax(xd, 0), (int32_t)P.pitch - 4));
+        if (!row_ok) v[k] = 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = b0 + k * kThreads + threadIdx.x;
+        if (i >= n) continue;
+        const int r = i / nd;
+        const int32_t xd = xa + 4 * (i - r * nd), y = by0 + r;
+        uint32_t w4 = v[k];
+        if ((y >= 0) & (y < P.H) & ((xd < 0) | (xd + 3 >= P.W))) {
+          // a dword across the image edge: white outside, bytes inside
+          const uint8_t* row = sbase + (int64_t)y * P.pitch;
+          w4 = 0;
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int32_t x = xd + j;
+            const uint32_t b = (x >= 0 && x < P.W) ? row[x] : 255u;
+            w4 |= b << (8 * j);
+          }
+        }
+        stage32[i] = w4;
+      }
+    }
+  } else if (staged) {
     // unconditional clamped loads (white off the image), all of a round in flight
     const int n = bw * bh;
     for (int b0 = 0; b0 < n; b0 += 8 * kThreads) {
@@ -840,10 +884,11 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
         const int ix = (int)srcX, iy = (int)srcY;  // interp_bicubic truncates
         const float fx = srcX - ix, fy = srcY - iy;
         const float hx = 0.5f * fx, hy = 0.5f * fy;
-        const uint8_t* t = stage + (iy - 1 - by0) * bw + (ix - 1 - bx0);
+        const uint8_t* t = stage + (iy - 1 - by0) * sstride + lead + (ix - 1 - bx0);
         int col[4];
 #pragma unroll
-        for (int r = 0; r < 4; r++, t += bw) col[r] = cubic_int(fx, hx, t[0], t[1], t[2], t[3]);
+        for (int r = 0; r < 4; r++, t += sstride)
+          col[r] = cubic_int(fx, hx, t[0], t[1], t[2], t[3]);
         o = cubic_int(fy, hy, col[0], col[1], col[2], col[3]);
       } else {
         o = interp_bicubic(S, srcX, srcY).r;

@@ -1072,8 +1072,8 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
       mark(b, "deskew_detect");
       launch_rotate_mask(cur_ref(P, b->ctl), other_ref(P, b->ctl), b->rot_args,
                          o.interpolate_type, count, b->st);
+      mark(b, "deskew_rotate");  // brackets exactly the rotation kernel
       launch_flip_if_active(b->ctl, &b->rot_args->active, sizeof(RotateArgs), count, b->st);
-      mark(b, "deskew_rotate");
     }
   }
   // ---- post (sheet_stages.c:415-534) -------------------------------------
