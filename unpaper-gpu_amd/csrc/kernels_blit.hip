@@ -764,7 +764,18 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
                                                                 const RotateArgs* args) {
   __shared__ uint32_t stage32[kRotGCap / 4];
   uint8_t* stage = reinterpret_cast<uint8_t*>(stage32);
-  const int s = blockIdx.z;
+  // XCD-aware tile order: workgroups are dispatched round-robin over the 8
+  // XCDs, so consecutive block ids sit on different L2s.  Give each XCD one
+  // contiguous run of tiles (a bijection of the linear block id) so the rows
+  // shared by neighbouring tiles' windows are fetched into one L2.
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int nblk = gx * gy * gridDim.z;
+  const int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int q = nblk >> 3, rr = nblk & 7, xcd = lin & 7;
+  const int tlin = xcd * q + imin(xcd, rr) + (lin >> 3);
+  const int s = tlin / (gx * gy);
+  const int trem = tlin - s * gx * gy;
+  const int tyi = trem / gx, txi = trem - tyi * gx;
   const RotateArgs a = args[s];
   if (!a.active) return;
   const Planes& P = src.P;
@@ -774,7 +785,7 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
   const int32_t sw = nm.x1 - nm.x0 + 1, sh = nm.y1 - nm.y0 + 1;
   const float scx = nm.x0 + sw / 2.0f, scy = nm.y0 + sh / 2.0f;  // primitives.c:137-145
   const float tcx = 0 + sw / 2.0f, tcy = 0 + sh / 2.0f;
-  const int32_t tx0 = blockIdx.x * kRotTW, ty0 = blockIdx.y * kRotGH;
+  const int32_t tx0 = txi * kRotTW, ty0 = tyi * kRotGH;
   const int32_t u0 = imax(tx0, 0) - a.mask.x0, u1 = imin(tx0 + kRotTW, P.W) - 1 - a.mask.x0;
   const int32_t v0 = imax(ty0, 0) - a.mask.y0, v1 = imin(ty0 + kRotGH, P.H) - 1 - a.mask.y0;
   const int32_t cu0 = imax(u0, 0), cu1 = imin(u1, sw - 1);
