@@ -248,10 +248,11 @@ def main():
         alg = STAGE_PLANES.get(dom, 1.0) * W * H * (npages * args.steps / max(nlaunch, 1))
         achieved = alg / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         traffic = None
-        try:
+        try:  # HBM bytes per page from the committed rocprofv3 --pmc passes
             with open(args.traffic) as f:
-                tr = json.load(f)
-            traffic = tr.get("bytes_per_launch", {}).get(dom)
+                per_page = json.load(f).get("bytes_per_page", {}).get(dom)
+            if per_page:
+                traffic = int(per_page * npages * args.steps / max(nlaunch, 1))
         except (OSError, ValueError):
             pass
         roofline = {

@@ -142,6 +142,22 @@ __device__ __forceinline__ Px load_px_any(const uint8_t* base, int64_t pitch, in
   }
 }
 
+// XCD-aware block order: workgroups are dispatched round-robin over the 8
+// XCDs (each with its own L2), so consecutive block ids sit on different L2s.
+// This bijection of the linear block id gives each XCD one contiguous run of
+// (x, y, z) tiles, so data shared by neighbouring tiles is fetched into one L2.
+__device__ __forceinline__ void xcd_block(int* bx, int* by, int* bz) {
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int nblk = gx * gy * gridDim.z;
+  const int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int q = nblk >> 3, rr = nblk & 7, xcd = lin & 7;
+  const int t = xcd * q + (xcd < rr ? xcd : rr) + (lin >> 3);
+  *bz = t / (gx * gy);
+  const int rem = t - *bz * gx * gy;
+  *by = rem / gx;
+  *bx = rem - *by * gx;
+}
+
 // ---------------------------------------------------------------------------
 // A batch of frames of identical geometry and format.  Frame s of plane k is
 // base[k] + s*stride.  For single-image ops stride = 0 and count = 1.

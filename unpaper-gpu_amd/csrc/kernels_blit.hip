@@ -764,18 +764,9 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
                                                                 const RotateArgs* args) {
   __shared__ uint32_t stage32[kRotGCap / 4];
   uint8_t* stage = reinterpret_cast<uint8_t*>(stage32);
-  // XCD-aware tile order: workgroups are dispatched round-robin over the 8
-  // XCDs, so consecutive block ids sit on different L2s.  Give each XCD one
-  // contiguous run of tiles (a bijection of the linear block id) so the rows
-  // shared by neighbouring tiles' windows are fetched into one L2.
-  const int gx = gridDim.x, gy = gridDim.y;
-  const int nblk = gx * gy * gridDim.z;
-  const int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-  const int q = nblk >> 3, rr = nblk & 7, xcd = lin & 7;
-  const int tlin = xcd * q + imin(xcd, rr) + (lin >> 3);
-  const int s = tlin / (gx * gy);
-  const int trem = tlin - s * gx * gy;
-  const int tyi = trem / gx, txi = trem - tyi * gx;
+  // XCD-aware tile order: neighbouring windows share rows, fetched into one L2
+  int txi, tyi, s;
+  xcd_block(&txi, &tyi, &s);
   const RotateArgs a = args[s];
   if (!a.active) return;
   const Planes& P = src.P;

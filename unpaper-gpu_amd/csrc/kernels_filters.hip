@@ -687,9 +687,11 @@ template <int FMT>
 __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom g, uint8_t* scratch,
                                                         int64_t sstride, const int32_t* active,
                                                         SheetCtl* ctl) {
-  const int s = blockIdx.z;
+  // XCD-aware tile order: neighbouring tiles' halos are fetched into one L2
+  int bxi, byi, s;
+  xcd_block(&bxi, &byi, &s);
   if (active && !active[s]) return;
-  const int32_t tx0 = blockIdx.x * kNT, ty0 = blockIdx.y * kNT;
+  const int32_t tx0 = bxi * kNT, ty0 = byi * kNT;
   const int32_t ox = tx0 - kHalo, oy = ty0 - kHalo;  // region origin
   const uint8_t* base = plane_ptr(img, s);
   NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
