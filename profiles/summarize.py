@@ -13,8 +13,17 @@ import sys
 
 
 def load(path):
+    """Rows {Name, Calls, TotalDurationNs} from a stats CSV or a rocpd database."""
     if os.path.isdir(path):
-        path = glob.glob(os.path.join(path, "*kernel_stats.csv"))[0]
+        found = glob.glob(os.path.join(path, "*kernel_stats.csv"))
+        path = found[0] if found else glob.glob(os.path.join(path, "*.db"))[0]
+    if path.endswith(".db"):
+        import sqlite3
+        con = sqlite3.connect(path)
+        q = ("select name, count(*), sum(duration) from kernels group by name "
+             "order by sum(duration) desc")
+        return [{"Name": n, "Calls": str(c), "TotalDurationNs": str(t), "AverageNs": str(t / c)}
+                for n, c, t in con.execute(q)]
     with open(path) as f:
         return list(csv.DictReader(f))
 

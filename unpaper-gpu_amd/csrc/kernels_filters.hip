@@ -703,7 +703,6 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
   __shared__ uint32_t drow[kRW][4];
   __shared__ uint32_t trow_s[kSplit ? kRW : 1][4];
   __shared__ uint32_t srow[kRW][4];
-  __shared__ uint64_t l3[kRW][2];
   __shared__ int32_t any_dark;
   uint32_t (*trow)[4] = kSplit ? trow_s : drow;
   // Stage the region rows into LDS with 16-byte loads, all issued before any
@@ -738,17 +737,24 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
     // dark / trigger bit rows: wave w takes rows w, w+4, ...; lanes own
     // columns lane and 64+lane, each row mask is two ballots
     const int lead = (int)(sb - a0);
+    bool colok[2];
+    int rxc[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int rx = h * 64 + lane;
+      colok[h] = (rx < kRW) & (ox + rx >= 0) & (ox + rx < g.W);
+      rxc[h] = rx < kRW ? rx : 0;
+    }
     bool tile_dark = false;
     for (int ry = w; ry < kRW; ry += 4) {
       const int32_t gy = oy + ry;
+      const bool rowok = (gy >= 0) & (gy < g.H);
       const uint8_t* srow_b = reinterpret_cast<const uint8_t*>(stage[ry]) + lead;
       unsigned long long md[2], mt[2];
 #pragma unroll
       for (int h = 0; h < 2; h++) {
-        const int rx = h * 64 + lane;
-        const int32_t gx = ox + rx;
-        const bool in = (rx < kRW) & (gx >= 0) & (gx < g.W) & (gy >= 0) & (gy < g.H);
-        const Px p = load_px_row<FMT>(srow_b, rx < kRW ? rx : 0);
+        const bool in = colok[h] & rowok;
+        const Px p = load_px_row<FMT>(srow_b, rxc[h]);
         md[h] = __ballot(in & (light_of(p) < g.white));
         mt[h] = kSplit ? __ballot(in & (dark_of(p) < g.white)) : md[h];
       }
@@ -771,71 +777,76 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
   // Pixels provably in a component of >= 5 pixels: L3 = dark pixels with >= 5
   // dark pixels in their 3x3 block (all 8-adjacent to the centre, so one
   // component); large = dark & (L3 | 8-dilation of L3) (8-adjacent to an L3
-  // pixel = same component).  Only the remaining dark pixels need the
-  // restricted 9x9 flood.  Rows outside the region read as empty, which can
-  // only leave pixels undecided, never mislabel them.
-  for (int ry = threadIdx.x; ry < kRW; ry += 256) {
-    uint64_t c0[2] = {0, 0}, c1[2] = {0, 0}, c2[2] = {0, 0}, c3[2] = {0, 0};
+  // pixel = same component).  Only the remaining dark pixels ("candidates")
+  // need the restricted 9x9 flood.  Rows outside the region read as empty,
+  // which can only leave pixels undecided, never mislabel them.  One thread
+  // per (row, 64-bit half); the staging buffer is dead by now and holds the
+  // l3 and candidate rows.
+  uint64_t (*l3)[2] = reinterpret_cast<uint64_t(*)[2]>(&stage[0][0]);
+  uint64_t (*cand)[2] = l3 + kRW;
+  static_assert(sizeof(stage) >= 2 * kRW * 2 * sizeof(uint64_t), "stage too small");
+  const int hr = threadIdx.x >> 1, hh = threadIdx.x & 1;
+  auto dark64 = [&](int r, int h) -> uint64_t {
+    return ((uint64_t)drow[r][2 * h + 1] << 32) | drow[r][2 * h];
+  };
+  if (threadIdx.x < 2 * kRW) {
+    uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
 #pragma unroll
     for (int d = -1; d <= 1; d++) {
-      const int r = ry + d;
-      uint64_t v[2] = {0, 0};
+      const int r = hr + d;
+      uint64_t v0 = 0, v1 = 0;
       if (r >= 0 && r < kRW) {
-        v[0] = ((uint64_t)drow[r][1] << 32) | drow[r][0];
-        v[1] = ((uint64_t)drow[r][3] << 32) | drow[r][2];
+        v0 = dark64(r, 0);
+        v1 = dark64(r, 1);
       }
       // left neighbour of column x is bit x-1 (shift up), right is x+1 (down)
-      const uint64_t Lw[2] = {v[0] << 1, (v[1] << 1) | (v[0] >> 63)};
-      const uint64_t Rw[2] = {(v[0] >> 1) | (v[1] << 63), v[1] >> 1};
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const uint64_t s0 = v[h] ^ Lw[h] ^ Rw[h];                               // bit 0
-        const uint64_t s1 = (v[h] & Lw[h]) | (v[h] & Rw[h]) | (Lw[h] & Rw[h]);  // bit 1
-        // c += s (c: 4 bits, <= 9; s: 2 bits)
-        const uint64_t k0 = c0[h] & s0;
-        c0[h] ^= s0;
-        const uint64_t t1 = c1[h] ^ s1;
-        const uint64_t k1 = (c1[h] & s1) | (t1 & k0);
-        c1[h] = t1 ^ k0;
-        const uint64_t k2 = c2[h] & k1;
-        c2[h] ^= k1;
-        c3[h] |= k2;
-      }
+      const uint64_t v = hh ? v1 : v0;
+      const uint64_t Lw = hh ? (v1 << 1) | (v0 >> 63) : v0 << 1;
+      const uint64_t Rw = hh ? v1 >> 1 : (v0 >> 1) | (v1 << 63);
+      const uint64_t s0 = v ^ Lw ^ Rw;                          // bit 0
+      const uint64_t s1 = (v & Lw) | (v & Rw) | (Lw & Rw);      // bit 1
+      // c += s (c: 4 bits, <= 9; s: 2 bits)
+      const uint64_t k0 = c0 & s0;
+      c0 ^= s0;
+      const uint64_t t1 = c1 ^ s1;
+      const uint64_t k1 = (c1 & s1) | (t1 & k0);
+      c1 = t1 ^ k0;
+      const uint64_t k2 = c2 & k1;
+      c2 ^= k1;
+      c3 |= k2;
     }
-    const uint64_t me[2] = {((uint64_t)drow[ry][1] << 32) | drow[ry][0],
-                            ((uint64_t)drow[ry][3] << 32) | drow[ry][2]};
-#pragma unroll
-    for (int h = 0; h < 2; h++)  // count >= 5: 8 | (4 & (2 | 1))
-      l3[ry][h] = me[h] & (c3[h] | (c2[h] & (c1[h] | c0[h])));
+    l3[hr][hh] = dark64(hr, hh) & (c3 | (c2 & (c1 | c0)));  // count >= 5: 8 | (4 & (2 | 1))
   }
   __syncthreads();
-  // small bit rows within radius 10 of the tile (region rows/cols [4, 88)):
-  // the restricted flood only for dark pixels not proven large
-  for (int ry = w; ry < kRW; ry += 4) {
-    unsigned long long m[2] = {0, 0};
-    if (ry >= 4 && ry < 88) {
-      uint64_t dil[2] = {0, 0};
+  // candidates within radius 10 of the tile (region rows/cols [4, 88))
+  if (threadIdx.x < 2 * kRW) {
+    uint64_t c = 0;
+    if (hr >= 4 && hr < 88) {
+      uint64_t dil = 0;
 #pragma unroll
       for (int d = -1; d <= 1; d++) {
-        const int r = ry + d;
-        const uint64_t a0 = l3[r][0], a1 = l3[r][1];
-        dil[0] |= a0 | (a0 << 1) | (a0 >> 1) | (a1 << 63);
-        dil[1] |= a1 | (a1 << 1) | (a0 >> 63) | (a1 >> 1);
+        const uint64_t a0 = l3[hr + d][0], a1 = l3[hr + d][1];
+        dil |= hh ? a1 | (a1 << 1) | (a0 >> 63) | (a1 >> 1) : a0 | (a0 << 1) | (a0 >> 1) | (a1 << 63);
       }
-      const uint64_t dk[2] = {((uint64_t)drow[ry][1] << 32) | drow[ry][0],
-                              ((uint64_t)drow[ry][3] << 32) | drow[ry][2]};
-      // candidate columns [4, 88): bits 4..63 of word 0, 64..87 of word 1
-      const uint64_t cand[2] = {dk[0] & ~dil[0] & ~0xFull, dk[1] & ~dil[1] & 0xFFFFFFull};
+      // bits 4..63 of word 0, 64..87 of word 1
+      c = dark64(hr, hh) & ~dil & (hh ? 0xFFFFFFull : ~0xFull);
+    }
+    cand[hr][hh] = c;
+  }
+  __syncthreads();
+  // small bit rows: the restricted flood, only where there are candidates
+  for (int ry = w; ry < kRW; ry += 4) {
+    unsigned long long m[2] = {0, 0};
 #pragma unroll
-      for (int h = 0; h < 2; h++) {
-        if (!cand[h]) continue;  // uniform
-        bool small = false;
-        if ((cand[h] >> lane) & 1) {
-          uint32_t comp[9];
-          small = flood9(drow, h * 64 + lane, ry, comp) <= 4;
-        }
-        m[h] = __ballot(small);
+    for (int h = 0; h < 2; h++) {
+      const uint64_t c = cand[ry][h];
+      if (!c) continue;  // uniform
+      bool small = false;
+      if ((c >> lane) & 1) {
+        uint32_t comp[9];
+        small = flood9(drow, h * 64 + lane, ry, comp) <= 4;
       }
+      m[h] = __ballot(small);
     }
     if (lane < 4) {
       const unsigned long long q = m[lane >> 1];
@@ -845,14 +856,18 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
   __syncthreads();
   const int N = g.intensity;
   // the tile's rows, one wave per row, lanes on the tile's 64 columns
+  const bool zone_tile = g.all_seq || tx0 < kZone || ty0 < kZone;  // uniform
   for (int t = w; t < kNT; t += 4) {
     const int ry = kHalo + t, rx = kHalo + lane;
     const int32_t gy = oy + ry, gx = ox + rx;
-    const bool dark = (drow[ry][rx >> 5] >> (rx & 31)) & 1;
     const bool trig = (trow[ry][rx >> 5] >> (rx & 31)) & 1;
     const bool zone = g.all_seq || gx < kZone || gy < kZone;
-    // edge zone (and intensity > 4): every trigger is replayed in order
-    wave_append(dark & zone & trig, gx, gy, NP.nseq, NP.seq, g.capacity);
+    if (zone_tile) {
+      // edge zone (and intensity > 4): every trigger is replayed in order
+      const bool dark = (drow[ry][rx >> 5] >> (rx & 31)) & 1;
+      wave_append(dark & zone & trig, gx, gy, NP.nseq, NP.seq, g.capacity);
+    }
+    if (!(row_bits(srow[ry], kHalo, 32) | row_bits(srow[ry], kHalo + 32, 32))) continue;  // uniform
     const bool small = !zone && ((srow[ry][rx >> 5] >> (rx & 31)) & 1);
     bool seq = false, clear = false;
     if (small) {
