@@ -225,3 +225,17 @@ def test_deskew(hip, oracle, fmt, interp, deg, mask):
     hip.deskew(d, A.rect(*mask), float(rad), interp)
     oracle.deskew(h, A.rect(*mask), float(rad), interp)
     assert_same(d.to_host(), h)
+
+
+@pytest.mark.parametrize("fmt", BYTE_FORMATS)
+@pytest.mark.parametrize("deg", [1.3, -12.0, 25.0, -44.0])
+@pytest.mark.parametrize("mask", [(0, 0, 1029, 299), (37, 21, 990, 280)])
+def test_deskew_cubic_wide(hip, oracle, fmt, deg, mask):
+    # several 256-column tiles, a width that is not a multiple of 4, and angles
+    # whose source windows exceed the staged height (taps read from the frame)
+    h = make_image(1030, 300, fmt, seed=18)
+    rad = np.float32(deg * math.pi / 180.0)
+    d = hip.upload(h)
+    hip.deskew(d, A.rect(*mask), float(rad), A.INTERP_CUBIC)
+    oracle.deskew(h, A.rect(*mask), float(rad), A.INTERP_CUBIC)
+    assert_same(d.to_host(), h)

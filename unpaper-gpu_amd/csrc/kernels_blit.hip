@@ -750,10 +750,7 @@ __device__ __forceinline__ uint8_t cubic_int(float f, float h, int a, int b, int
   return (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));  // av_clip_uint8
 }
 
-// deskew rotate for a gray plane with bicubic interpolation (the default):
-// k_rotate_mask's tiling and staging, with the taps read straight from the
-// window and no other interpolation code in the kernel.
-// deskew rotate for a gray plane with bicubic interpolation (the default):
+// deskew rotate for a gray plane with bicubic interpolation (Y400A):
 // k_rotate_mask's tiling and staging, with the taps read straight from the
 // window and no other interpolation code in the kernel.
 constexpr int kRotGH = 32;     // output rows per tile of the gray bicubic kernel
@@ -902,12 +899,231 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_gray(PlaneRef src, Pl
   }
 }
 
+// ---------------------------------------------------------------------------
+// deskew rotate, GRAY8 + bicubic (the default pipeline): 256 x 32 output tiles,
+// four horizontally adjacent pixels per lane and row, so one dword store per
+// lane and the float work in pairs of pixels on packed FP32 (v_pk_mul/add/fma).
+//   * the window is staged with a fixed 288-byte row stride, so the four tap
+//     rows of a pixel are one ds_read2_b32 each at immediate offsets, and
+//     v_alignbyte extracts its four taps;
+//   * the integer-valued terms of cubic_scale (2a-5b+4c-d, 3(b-c)+d-a, c-a)
+//     are formed by exact packed FMAs on float-valued bytes (every
+//     intermediate is an integer below 2^24); the six rounding operations stay
+//     separate multiplies and adds in the reference's order
+//     (interpolate.c:24-31), so results are bit-identical.
+// ---------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+constexpr int kRQW = 256;              // output columns per tile (4 per lane)
+constexpr int kRQH = 32;               // output rows per tile
+constexpr int kRQStride = 72;          // staged row stride in dwords (>= window 269 B)
+constexpr int kRQRows = 84;            // staged rows
+constexpr int kRQWords = kRQStride * kRQRows + 2;
+
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 splat2(float v) { return f2{v, v}; }
+
+// cubic_scale on float-valued taps, truncated and clipped like av_clip_uint8
+// (the result is an integer-valued float).  The integer-valued terms are
+// formed from the differences ba = b-a, ca = c-a, da = d-a:
+//   2a-5b+4c-d = -5ba + 4ca - da,   3(b-c)+d-a = 3(ba-ca) + da
+__device__ __forceinline__ f2 cubic2(f2 f, f2 h, f2 a, f2 b, f2 c, f2 d) {
+  const f2 ba = b - a, ca = c - a, da = d - a;                                   // exact
+  const f2 s1 = fma2(splat2(-5.0f), ba, fma2(splat2(4.0f), ca, -da));            // exact
+  const f2 s2 = fma2(splat2(3.0f), ba - ca, da);                                 // exact
+  const f2 u = s1 + f * s2;
+  const f2 v = ca + f * u;
+  const f2 r = b + h * v;
+  return f2{__builtin_amdgcn_fmed3f(__builtin_truncf(r.x), 0.0f, 255.0f),
+            __builtin_amdgcn_fmed3f(__builtin_truncf(r.y), 0.0f, 255.0f)};
+}
+
+// byte K of w as a float.  Inline asm keeps the value opaque: otherwise the
+// compiler turns differences of converted bytes back into integer subtracts
+// plus conversions, which defeats the packed arithmetic.
+template <int K>
+__device__ __forceinline__ float ubyte_f(uint32_t w) {
+  float r;
+  if constexpr (K == 0) asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(r) : "v"(w));
+  else if constexpr (K == 1) asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(r) : "v"(w));
+  else if constexpr (K == 2) asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(r) : "v"(w));
+  else asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(r) : "v"(w));
+  return r;
+}
+template <int K>
+__device__ __forceinline__ f2 tap2(uint32_t p, uint32_t q) {
+  return f2{ubyte_f<K>(p), ubyte_f<K>(q)};
+}
+
+__global__ void __launch_bounds__(kThreads) k_rotate_cubic_g8(PlaneRef src, PlaneRef dst,
+                                                              const RotateArgs* args) {
+  __shared__ uint32_t win[kRQWords];
+  int txi, tyi, s;
+  xcd_block(&txi, &tyi, &s);  // neighbouring windows share rows, fetched into one L2
+  const RotateArgs a = args[s];
+  if (!a.active) return;
+  const Planes& P = src.P;
+  const uint8_t* sbase = plane_ptr(src, s);
+  uint8_t* dbase = plane_ptr(dst, s);
+  const Rect nm = normalize(a.mask);
+  const int32_t sw = nm.x1 - nm.x0 + 1, sh = nm.y1 - nm.y0 + 1;
+  const float scx = nm.x0 + sw / 2.0f, scy = nm.y0 + sh / 2.0f;  // primitives.c:137-145
+  const float tcx = 0 + sw / 2.0f, tcy = 0 + sh / 2.0f;
+  const int32_t tx0 = txi * kRQW, ty0 = tyi * kRQH;
+  const int32_t u0 = imax(tx0, 0) - a.mask.x0, u1 = imin(tx0 + kRQW, P.W) - 1 - a.mask.x0;
+  const int32_t v0 = imax(ty0, 0) - a.mask.y0, v1 = imin(ty0 + kRQH, P.H) - 1 - a.mask.y0;
+  const int32_t cu0 = imax(u0, 0), cu1 = imin(u1, sw - 1);
+  const int32_t cv0 = imax(v0, 0), cv1 = imin(v1, sh - 1);
+  // source window of the tile's in-mask pixels (their 4x4 taps included)
+  int32_t bx0 = 0, by0 = 0, bw = 0, bh = 0;
+  if (cu0 <= cu1 && cv0 <= cv1) {
+    float mnx = 3.0e38f, mxx = -3.0e38f, mny = 3.0e38f, mxy = -3.0e38f;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int32_t u = c & 1 ? cu1 : cu0, v = c & 2 ? cv1 : cv0;
+      const float X = scx + (u - tcx) * a.cosval + (v - tcy) * a.sinval;
+      const float Y = scy + (v - tcy) * a.cosval - (u - tcx) * a.sinval;
+      mnx = fminf(mnx, X);
+      mxx = fmaxf(mxx, X);
+      mny = fminf(mny, Y);
+      mxy = fmaxf(mxy, Y);
+    }
+    bx0 = (int32_t)floorf(mnx) - 3;
+    by0 = (int32_t)floorf(mny) - 3;
+    bw = (int32_t)floorf(mxx) + 4 - bx0 + 1;
+    bh = (int32_t)floorf(mxy) + 4 - by0 + 1;
+  }
+  const int32_t xa = bx0 >= 0 ? (bx0 & ~3) : -((-bx0 + 3) & ~3);  // window start, dword aligned
+  const int lead = bx0 - xa;
+  const int nd = (lead + bw + 3) >> 2;                               // dwords per window row
+  const bool staged = bw > 0 && bh > 0 && nd < kRQStride && bh <= kRQRows;
+  if (staged) {
+    // row of flat dword index i: i / nd as a multiply-high (exact for
+    // i * (m*nd - 2^32) < 2^32, far beyond these sizes)
+    const uint32_t m = nd > 1 ? (uint32_t)((0xFFFFFFFFull / (uint32_t)nd) + 1) : 0u;
+    const int n = nd * bh;
+    for (int b0 = 0; b0 < n; b0 += 8 * kThreads) {
+      uint32_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = b0 + k * kThreads + threadIdx.x;
+        const int r = nd > 1 ? (int)__umulhi((uint32_t)i, m) : i;
+        const int32_t xd = xa + 4 * (i - r * nd), y = by0 + r;
+        const uint8_t* row = sbase + (int64_t)imin(imax(y, 0), P.H - 1) * P.pitch;
+        v[k] = *reinterpret_cast<const uint32_t*>(row + imin(imax(xd, 0), (int32_t)P.pitch - 4));
+        if ((y < 0) | (y >= P.H)) v[k] = 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = b0 + k * kThreads + threadIdx.x;
+        if (i >= n) continue;
+        const int r = nd > 1 ? (int)__umulhi((uint32_t)i, m) : i;
+        const int j = i - r * nd;
+        const int32_t xd = xa + 4 * j, y = by0 + r;
+        uint32_t w4 = v[k];
+        if ((y >= 0) & (y < P.H) & ((xd < 0) | (xd + 3 >= P.W))) {
+          // a dword across the image edge: white outside, bytes inside
+          const uint8_t* row = sbase + (int64_t)y * P.pitch;
+          w4 = 0;
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const int32_t x = xd + q;
+            const uint32_t b = (x >= 0 && x < P.W) ? row[x] : 255u;
+            w4 |= b << (8 * q);
+          }
+        }
+        win[r * kRQStride + j] = w4;
+      }
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int32_t xl = tx0 + 4 * lane;
+  if (xl >= P.W) return;
+  // per-lane terms of the source coordinates (constant down the column):
+  //   srcX = (scx + (u - tcx) cos) + (v - tcy) sin
+  //   srcY = (scy + (v - tcy) cos) - (u - tcx) sin
+  float ax[4], bs[4];
+  bool colin[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int32_t u = xl + j - a.mask.x0;
+    const float cu = u - tcx;
+    ax[j] = scx + cu * a.cosval;
+    bs[j] = cu * a.sinval;
+    colin[j] = (u >= 0) & (u < sw) & (xl + j < P.W);
+  }
+  const f2 AX0{ax[0], ax[1]}, AX1{ax[2], ax[3]}, BS0{bs[0], bs[1]}, BS1{bs[2], bs[3]};
+  const int base_off = (-1 - by0) * (4 * kRQStride) + lead - 1 - bx0;  // tap (ix-1, iy-1)
+  const Src<F_GRAY8> S{sbase, P.pitch, P.W, P.H};
+#pragma unroll 2
+  for (int k = 0; k < kRQH / 4; k++) {
+    const int32_t y = ty0 + w + 4 * k;
+    if (y >= P.H) break;
+    const int32_t v = y - a.mask.y0;
+    const bool rowin = (v >= 0) & (v < sh);
+    const float cv = v - tcy;
+    const f2 VS = splat2(cv * a.sinval), VC = splat2(scy + cv * a.cosval);
+    const f2 SX[2] = {AX0 + VS, AX1 + VS};
+    const f2 SY[2] = {VC - BS0, VC - BS1};
+    const uint8_t* srow = sbase + (int64_t)y * P.pitch;
+    uint32_t out = 0;
+    if (staged) {
+#pragma unroll
+      for (int pr = 0; pr < 2; pr++) {
+        const int ix0 = (int)SX[pr].x, ix1 = (int)SX[pr].y;  // interp_bicubic truncates
+        const int iy0 = (int)SY[pr].x, iy1 = (int)SY[pr].y;
+        const f2 fx = SX[pr] - f2{(float)ix0, (float)ix1};
+        const f2 fy = SY[pr] - f2{(float)iy0, (float)iy1};
+        const f2 hx = 0.5f * fx, hy = 0.5f * fy;
+        const bool in0 = rowin & colin[2 * pr], in1 = rowin & colin[2 * pr + 1];
+        const int o0 = in0 ? base_off + iy0 * (4 * kRQStride) + ix0 : 0;
+        const int o1 = in1 ? base_off + iy1 * (4 * kRQStride) + ix1 : 0;
+        const uint32_t* w0 = win + (o0 >> 2);
+        const uint32_t* w1 = win + (o1 >> 2);
+        f2 col[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const uint32_t p = __builtin_amdgcn_alignbyte(w0[r * kRQStride + 1], w0[r * kRQStride], o0);
+          const uint32_t q = __builtin_amdgcn_alignbyte(w1[r * kRQStride + 1], w1[r * kRQStride], o1);
+          col[r] = cubic2(fx, hx, tap2<0>(p, q), tap2<1>(p, q), tap2<2>(p, q), tap2<3>(p, q));
+        }
+        const f2 o = cubic2(fy, hy, col[0], col[1], col[2], col[3]);
+        // integer-valued in [0, 255]: the conversion is exact whatever its rounding
+        out = __builtin_amdgcn_cvt_pk_u8_f32(o.x, 2 * pr, out);
+        out = __builtin_amdgcn_cvt_pk_u8_f32(o.y, 2 * pr + 1, out);
+      }
+    } else {
+      // window too tall for LDS (large angles): taps from the frame
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const f2 sx = SX[j >> 1], sy = SY[j >> 1];
+        const float fx = (j & 1) ? sx.y : sx.x, fy = (j & 1) ? sy.y : sy.x;
+        if (rowin & colin[j]) out |= (uint32_t)interp_bicubic(S, fx, fy).r << (8 * j);
+      }
+    }
+    // outside the mask the pixel is copied unchanged (deskew.c:268-286)
+    uint32_t inmask = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) inmask |= (rowin & colin[j]) ? 0xFFu << (8 * j) : 0u;
+    uint8_t* drow = dbase + (int64_t)y * P.pitch;
+    if (xl + 3 < P.W) {
+      if (inmask != 0xFFFFFFFFu)
+        out = (out & inmask) | (*reinterpret_cast<const uint32_t*>(srow + xl) & ~inmask);
+      *reinterpret_cast<uint32_t*>(drow + xl) = out;
+    } else {
+      for (int j = 0; xl + j < P.W; j++)
+        drow[xl + j] = (inmask >> (8 * j)) & 1 ? (uint8_t)(out >> (8 * j)) : srow[xl + j];
+    }
+  }
+}
+
 void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
                         int interp, int count, hipStream_t st) {
   const dim3 grid((src.P.W + kRotTW - 1) / kRotTW, (src.P.H + kRotTH - 1) / kRotTH, count);
   const dim3 ggrid((src.P.W + kRotTW - 1) / kRotTW, (src.P.H + kRotGH - 1) / kRotGH, count);
   if (interp == UPHIP_INTERP_CUBIC && src.P.fmt == F_GRAY8) {
-    hipLaunchKernelGGL(k_rotate_cubic_gray<F_GRAY8>, ggrid, dim3(kThreads), 0, st, src, dst, args);
+    const dim3 qgrid((src.P.W + kRQW - 1) / kRQW, (src.P.H + kRQH - 1) / kRQH, count);
+    hipLaunchKernelGGL(k_rotate_cubic_g8, qgrid, dim3(kThreads), 0, st, src, dst, args);
     return;
   }
   if (interp == UPHIP_INTERP_CUBIC && src.P.fmt == F_Y400A) {

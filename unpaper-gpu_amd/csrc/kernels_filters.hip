@@ -754,9 +754,14 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const bool in = colok[h] & rowok;
-        const Px p = load_px_row<FMT>(srow_b, rxc[h]);
-        md[h] = __ballot(in & (light_of(p) < g.white));
-        mt[h] = kSplit ? __ballot(in & (dark_of(p) < g.white)) : md[h];
+        if constexpr (kSplit) {
+          const Px p = load_px_row<FMT>(srow_b, rxc[h]);
+          md[h] = __ballot(in & (light_of(p) < g.white));
+          mt[h] = __ballot(in & (dark_of(p) < g.white));
+        } else {  // one channel: lightness = darkness = the gray byte
+          const uint32_t v = srow_b[rxc[h] * B];
+          md[h] = mt[h] = __ballot(in & (v < (uint32_t)g.white));
+        }
       }
       if (lane < 4) {
         const unsigned long long q = md[lane >> 1];
