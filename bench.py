@@ -57,7 +57,7 @@ STAGE_PLANES = {
 
 
 ROOFLINE_STAGE = "deskew_rotate"
-ROOFLINE_KERNEL = "k_rotate_cubic_gray"
+ROOFLINE_KERNEL = "k_rotate_cubic_g8"
 
 
 def parse():

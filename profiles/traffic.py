@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Build profiles/traffic.json (HBM bytes per launch / per page) from two
+rocprofv3 --pmc passes of the same command: one with FETCH_SIZE, one with
+WRITE_SIZE (they do not fit in one pass on gfx950).
+
+usage: traffic.py <fetch-pass dir> <write-pass dir> <kernel-substring> <stage> \
+                  <alg-bytes-per-launch> <pages-per-launch> [out.json]
+
+Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are
+in KiB; FETCH_SIZE tallies half of the bytes of coalesced streaming reads on
+gfx950, so it is doubled; WRITE_SIZE is exact.  The doubling was re-checked
+on this pipeline's k_copy (16 B/lane) and k_colsum_g (4 B/lane) reads; the
+same pass also carries those kernels, so the check is printed each time.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_launch(path, counter):
+    if os.path.isdir(path):
+        path = glob.glob(os.path.join(path, "*counter_collection.csv"))[0]
+    acc = collections.defaultdict(list)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] == counter:
+                acc[r["Kernel_Name"]].append(float(r["Counter_Value"]) * 1024.0)
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def pick(d, sub):
+    ks = [k for k in d if sub in k]
+    if not ks:
+        raise SystemExit("no kernel matching %r" % sub)
+    return max(d[k] for k in ks)  # the full-plane variant
+
+
+def main():
+    fdir, wdir, kern, stage, alg, pages = sys.argv[1:7]
+    out = sys.argv[7] if len(sys.argv) > 7 else os.path.join(os.path.dirname(__file__), "traffic.json")
+    alg, pages = int(alg), int(pages)
+    fetch, write = per_launch(fdir, "FETCH_SIZE"), per_launch(wdir, "WRITE_SIZE")
+    for ref in ("k_copy", "k_colsum_g"):
+        try:
+            print("calibration %-10s FETCH raw %.1f MB/launch, doubled %.1f MB" %
+                  (ref, pick(fetch, ref) / 1e6, 2 * pick(fetch, ref) / 1e6))
+        except SystemExit:
+            pass
+    fr, wr = pick(fetch, kern), pick(write, kern)
+    hbm = 2 * fr + wr
+    name = kern.split("(")[0].split("::")[-1]
+    doc = {
+        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) --kernel-trace "
+                  "-- python3 bench.py --pages 128 --steps 1 --warmup 1 --streams 1 --no-cpu; "
+                  "1 MI355X; %d sheets per launch" % pages,
+        "correction": "FETCH_SIZE x2 (gfx950 tallies half of coalesced streaming reads); "
+                      "counter values are KiB",
+        "kernels": {name: {"fetch_raw_bytes_per_launch": int(fr),
+                           "write_bytes_per_launch": int(wr),
+                           "hbm_bytes_per_launch": int(hbm),
+                           "alg_bytes_per_launch": alg}},
+        "bytes_per_page": {stage: int(hbm / pages)},
+    }
+    with open(out, "w") as f:
+        json.dump(doc, f, indent=1)
+    print("%s: fetch %.1f MB (x2 %.1f) + write %.1f MB = %.1f MB/launch vs alg %.1f MB (%.3fx)" %
+          (name, fr / 1e6, 2 * fr / 1e6, wr / 1e6, hbm / 1e6, alg / 1e6, hbm / alg))
+
+
+if __name__ == "__main__":
+    main()
