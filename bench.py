@@ -66,8 +66,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--pages", type=int, default=1000, help="pages per GPU")
-    ap.add_argument("--batch", type=int, default=32, help="sheets per batch launch sequence")
-    ap.add_argument("--streams", type=int, default=16, help="batches (HIP streams) in flight")
+    ap.add_argument("--batch", type=int, default=64, help="sheets per batch launch sequence")
+    ap.add_argument("--streams", type=int, default=12, help="batches (HIP streams) in flight")
+    ap.add_argument("--hw-queues", type=int, default=16,
+                    help="GPU_MAX_HW_QUEUES for this process (HIP default 4, at most 32)")
     ap.add_argument("--cpu-pages", type=int, default=0,
                     help="CPU baseline sample (0 = 2 pages per host thread)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, host cores)")
@@ -176,6 +178,11 @@ def time_config(opts, pages, pitch, stride, npages, bsz, nstreams):
 
 def main():
     args = parse()
+    # Batches run on separate HIP streams so that one batch's latency-bound
+    # sequential replays (one wave per sheet) overlap other batches' full-chip
+    # kernels.  HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues
+    # (default 4), read once at HIP init, i.e. in uphip_try_init below.
+    os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, min(32, args.hw_queues)))
     d = Dist()
     L = load_library()
     st = L.uphip_try_init()
@@ -290,7 +297,9 @@ def main():
             "config": {"workload": "%d synthetic GRAY8 A4@300dpi pages (2480x3508) per GPU, "
                                    "default pipeline, batch_run_device" % args.pages,
                        "pages_per_gpu": args.pages, "sheets_per_batch": bsz,
-                       "streams": len(batches), "parallelism": "pages sharded, no collective"},
+                       "streams": len(batches),
+                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                       "parallelism": "pages sharded, no collective"},
             "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -83,6 +83,22 @@ def test_noisefilter_pages(hip, oracle, fmt, size, seed, specks, intensity):
          lambda o: oracle.noisefilter(o, intensity, 229))
 
 
+@pytest.mark.parametrize("fmt", [A.FMT_GRAY8, A.FMT_RGB24])
+@pytest.mark.parametrize("density,intensity", [(0.12, 4), (0.3, 4), (0.3, 2), (0.55, 3)])
+def test_noisefilter_dense_salt(hip, oracle, fmt, density, intensity):
+    # so many small components per 64x64 tile that the classify kernel's LDS
+    # work lists overflow and it takes its row-loop path
+    rng = np.random.default_rng(int(density * 100) + intensity)
+    g = np.where(rng.random((230, 301)) < density, rng.integers(0, 200, (230, 301)), 255)
+    g = g.astype(np.uint8)
+    if fmt == A.FMT_RGB24:
+        h = HostImage.from_array(np.repeat(g[:, :, None], 3, axis=2), fmt)
+    else:
+        h = HostImage.from_array(g, fmt)
+    both(hip, oracle, h, lambda d: hip.noisefilter(d, intensity, 229),
+         lambda o: oracle.noisefilter(o, intensity, 229))
+
+
 def test_noisefilter_edge_quirk(hip, oracle):
     # components hugging x < level / y < level-1, where the reference's ring
     # loops skip whole rows (int32 vs uint32 comparison)

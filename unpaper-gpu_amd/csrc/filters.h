@@ -48,6 +48,7 @@ struct NoiseGeom {
   uint8_t white;
   int32_t capacity;    // entries per list per sheet
   int32_t all_seq;
+  int32_t diag;        // TEMP timing diagnostics
 };
 bool noise_geometry(int32_t W, int32_t H, uint64_t intensity, uint8_t white, NoiseGeom* g);
 size_t noise_scratch_bytes(const NoiseGeom& g);

@@ -506,13 +506,22 @@ __global__ void __launch_bounds__(kThreads) k_move_rect(PlaneRef src, PlaneRef d
   }
 }
 
-// k_move_rect for gray planes (raw copies and the background are the same
-// bytes as set_pixel writes): one aligned dword of the destination per lane.
-// A dword wholly outside the move, wholly background or wholly inside the
-// pasted rectangle is one aligned load, a constant, or two aligned loads and
-// a funnel shift; only dwords on span edges go byte by byte.
-__global__ void __launch_bounds__(kThreads) k_move_rect_g(PlaneRef src, PlaneRef dst,
-                                                          const MoveArgs* args) {
+// k_move_rect for gray planes, 16 bytes of the destination per lane.  The
+// class of a column (unchanged / background / moved) only changes at five
+// breakpoints, so a vector not straddling one is one aligned 16-byte load, a
+// constant, or two aligned loads realigned by the source shift, which is the
+// same for every vector of the sheet ((A.x0 - tx) mod 16).  Vectors across a
+// breakpoint or the right image edge go byte by byte.
+template <int Q>
+__device__ __forceinline__ uint4 shift_bytes16(const uint32_t* w, int r) {
+  return make_uint4(__builtin_amdgcn_alignbyte(w[Q + 1], w[Q], r),
+                    __builtin_amdgcn_alignbyte(w[Q + 2], w[Q + 1], r),
+                    __builtin_amdgcn_alignbyte(w[Q + 3], w[Q + 2], r),
+                    __builtin_amdgcn_alignbyte(w[Q + 4], w[Q + 3], r));
+}
+
+__global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneRef dst,
+                                                            const MoveArgs* args) {
   const int s = blockIdx.z;
   const MoveArgs a = args[s];
   if (!a.active) return;
@@ -524,65 +533,77 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g(PlaneRef src, PlaneRef
   const int32_t sw = iabs(a.area.x0 - a.area.x1) + 1, sh = iabs(a.area.y0 - a.area.y1) + 1;
   const uint8_t bg = gray_of(Px{a.bg[0], a.bg[1], a.bg[2]});
   const uint32_t bg4 = bg * 0x01010101u;
-  const int32_t nd = (P.W + 3) >> 2;
-  for (int32_t y = blockIdx.x; y < P.H; y += gridDim.x) {
+  const int32_t nv = (P.W + 15) >> 4;                  // vectors per row (inside the pitch)
+  const uint32_t total = (uint32_t)nv * (uint32_t)P.H;
+  const uint32_t m = nv > 1 ? (uint32_t)((0xFFFFFFFFull / (uint32_t)nv) + 1) : 0u;
+  const int32_t delta = A.x0 - a.tx;                   // source column - destination column
+  const int r16 = delta & 15, q = r16 >> 2, r = r16 & 3;
+  const int32_t bp[5] = {a.tx, a.tx + aw, a.tx + sw, A.x0, A.x1 + 1};
+  for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < total; i += gridDim.x * kThreads) {
+    const int32_t y = nv > 1 ? (int32_t)__umulhi(i, m) : (int32_t)i;
+    const int32_t x0 = 16 * (int32_t)(i - (uint32_t)y * nv);
     const uint8_t* srow = sbase + (int64_t)y * P.pitch;
-    uint32_t* drow = reinterpret_cast<uint32_t*>(dbase + (int64_t)y * P.pitch);
     const int32_t v = y - a.ty;
     const bool trow = v >= 0 && v < sh;              // row crosses the pasted rectangle
     const bool mrow = trow && v < ah;                // ... and its copied extent
     const bool arow = y >= A.y0 && y <= A.y1;        // row crosses the wiped area
     const uint8_t* mrow_p = sbase + (int64_t)(A.y0 + (mrow ? v : 0)) * P.pitch;
-    for (int32_t d = threadIdx.x; d < nd; d += blockDim.x) {
-      const int32_t x0 = d * 4;
-      // class of columns x0..x0+3: 0 unchanged, 1 background, 2 moved
-      int cls[4];
+    auto cls_of = [&](int32_t x) -> int {
+      const int32_t u = x - a.tx;
+      if (trow && u >= 0 && u < sw) return (mrow && u < aw) ? 2 : 1;
+      return (arow && x >= A.x0 && x <= A.x1) ? 1 : 0;
+    };
+    bool uni = x0 + 16 <= P.W;
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int32_t x = x0 + j, u = x - a.tx;
-        if (trow && u >= 0 && u < sw) cls[j] = (mrow && u < aw) ? 2 : 1;
-        else cls[j] = (arow && x >= A.x0 && x <= A.x1) ? 1 : 0;
+    for (int k = 0; k < 5; k++) uni &= !(bp[k] > x0 && bp[k] < x0 + 16);
+    const int c0 = cls_of(x0);
+    uint4 out;
+    if (uni && c0 == 0) {
+      out = *reinterpret_cast<const uint4*>(srow + x0);
+    } else if (uni && c0 == 1) {
+      out = make_uint4(bg4, bg4, bg4, bg4);
+    } else if (uni && ((x0 + delta) & ~15) + (r16 ? 32 : 16) <= P.pitch) {
+      const uint4* qp = reinterpret_cast<const uint4*>(mrow_p + ((x0 + delta) & ~15));
+      const uint4 lo = qp[0], hi = r16 ? qp[1] : make_uint4(0, 0, 0, 0);
+      const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      switch (q) {  // uniform over the sheet
+        case 0: out = shift_bytes16<0>(w, r); break;
+        case 1: out = shift_bytes16<1>(w, r); break;
+        case 2: out = shift_bytes16<2>(w, r); break;
+        default: out = shift_bytes16<3>(w, r); break;
       }
-      const bool uni = cls[0] == cls[1] && cls[1] == cls[2] && cls[2] == cls[3];
-      uint32_t out;
-      if (uni && cls[0] == 0) {
-        out = *reinterpret_cast<const uint32_t*>(srow + x0);
-      } else if (uni && cls[0] == 1) {
-        out = bg4;
-      } else if (uni && (((A.x0 + (x0 - a.tx)) & ~3) + 8 <= P.pitch)) {
-        const int32_t sx = A.x0 + (x0 - a.tx);       // inside the clipped area
-        const int32_t sa = sx & ~3;                  // sa + 7 within the row's pitch
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(mrow_p + sa);
-        const uint64_t w2 = ((uint64_t)q[1] << 32) | q[0];
-        out = (uint32_t)(w2 >> (8 * (sx - sa)));
-      } else {
-        out = 0;
+    } else {
+      uint32_t o[4] = {0, 0, 0, 0};
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int32_t x = x0 + j;
-          uint8_t b;
-          if (cls[j] == 0) b = x < P.W ? srow[x] : 0;
-          else if (cls[j] == 1) b = bg;
-          else b = mrow_p[A.x0 + (x - a.tx)];
-          out |= (uint32_t)b << (8 * j);
-        }
+      for (int j = 0; j < 16; j++) {
+        const int32_t x = x0 + j;
+        if (x >= P.W) break;
+        const int c = cls_of(x);
+        const uint8_t b = c == 0 ? srow[x] : c == 1 ? bg : mrow_p[x + delta];
+        o[j >> 2] |= (uint32_t)b << (8 * (j & 3));
       }
-      drow[d] = out;
+      out = make_uint4(o[0], o[1], o[2], o[3]);
     }
+    *reinterpret_cast<uint4*>(dbase + (int64_t)y * P.pitch + x0) = out;
   }
 }
 
 void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* args, int count,
                       hipStream_t st) {
   int gx = src.P.H < 1 ? 1 : (src.P.H > 1024 ? 1024 : src.P.H);
-  if (src.P.fmt == F_GRAY8)
-    hipLaunchKernelGGL(k_move_rect_g, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst, args);
-  else if (src.P.fmt == F_Y400A)
+  if (src.P.fmt == F_GRAY8) {
+    // about four 16-byte vectors per lane
+    const int64_t vecs = (int64_t)((src.P.W + 15) >> 4) * src.P.H;
+    const int64_t g16 = (vecs + 4 * kThreads - 1) / (4 * kThreads);
+    hipLaunchKernelGGL(k_move_rect_g16, dim3((unsigned)(g16 < 1 ? 1 : g16), 1, count),
+                       dim3(kThreads), 0, st, src, dst, args);
+  } else if (src.P.fmt == F_Y400A) {
     hipLaunchKernelGGL(k_move_rect<F_Y400A>, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst,
                        args);
-  else
+  } else {
     hipLaunchKernelGGL(k_move_rect<F_RGB24>, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst,
                        args);
+  }
 }
 
 // ---------------------------------------------------------------------------

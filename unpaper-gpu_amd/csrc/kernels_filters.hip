@@ -683,6 +683,89 @@ __device__ __forceinline__ void wave_append(bool want, int32_t gx, int32_t gy, u
   }
 }
 
+// Dark bits of 4 gray bytes (byte < t) as a nibble: 16-bit SWAR lanes hold
+// b + 256 - t, whose bit 8 is (b >= t); no lane carries into the next.
+__device__ __forceinline__ uint32_t lt_nibble(uint32_t x, uint32_t k) {
+  const uint32_t lo = ((x & 0x00FF00FFu) + k) & 0x01000100u;
+  const uint32_t hi = (((x >> 8) & 0x00FF00FFu) + k) & 0x01000100u;
+  const uint32_t ge = (lo >> 8) | (hi >> 7);  // bits 0,1 (bytes 0,1), 16,17 (bytes 2,3)
+  return ~(ge | (ge >> 14)) & 0xFu;
+}
+
+// Whether the classification of a small dark pixel (tile coordinates rx, ry)
+// must go to the sequential replay, or clears it in parallel (see above).
+struct SmallVerdict {
+  bool seq, clear;
+};
+__device__ __forceinline__ SmallVerdict small_verdict(const uint32_t (*drow)[4],
+                                                      const uint32_t (*trow)[4],
+                                                      const uint32_t (*srow)[4], int rx, int ry,
+                                                      int32_t gx, int32_t gy, bool trig, int N) {
+  SmallVerdict v{false, false};
+  uint32_t comp[9];
+  flood9(drow, rx, ry, comp);
+  // component pixels (<= 4) relative to (rx, ry), and their bounding box
+  int cxs[4], cys[4], nc = 0;
+  int bx0 = 9, bx1 = -1, by0 = 9, by1 = -1;
+#pragma unroll
+  for (int r = 0; r < 9; r++) {
+    uint32_t mm = comp[r];
+    if (mm) {
+      by0 = imin(by0, r);
+      by1 = r;
+      bx0 = imin(bx0, __ffs(mm) - 1);
+      bx1 = imax(bx1, 31 - __clz(mm));
+    }
+    while (mm) {
+      const int b = __ffs(mm) - 1;
+      mm &= mm - 1;
+      if (nc < 4) {
+        cxs[nc] = b - 4;
+        cys[nc] = r - 4;
+      }
+      nc++;
+    }
+  }
+  bool eligible = nc <= 4 && gx - 4 + bx0 >= kEligible && gy - 4 + by0 >= kEligible;
+  // no foreign small pixel within Chebyshev 7 of the component: checked on
+  // the bounding box dilated by 7 (a superset, so a component rejected here
+  // merely takes the exact sequential path)
+  if (eligible) {
+    const int X0 = rx - 4 + bx0 - 7, n = bx1 - bx0 + 15;
+    int cnt = 0;
+    for (int r = ry - 4 + by0 - 7; r <= ry - 4 + by1 + 7; r++)
+      cnt += __popc(row_bits(srow[r], X0, n));
+    eligible = cnt == nc;
+  }
+  if (!eligible) {
+    v.seq = trig;
+    return v;
+  }
+  // cleared iff some trigger of the component passes the ring test on the
+  // original image (eligible pixels are >= 40 from the edges, so the
+  // reference's unsigned ring-loop skips never apply)
+  for (int k = 0; k < nc && k < 4 && !v.clear; k++) {
+    const int cx = rx + cxs[k], cy = ry + cys[k];
+    if (!((trow[cy][cx >> 5] >> (cx & 31)) & 1)) continue;
+    int count = 1, lc;
+    int level = 1;
+    do {
+      lc = __popc(row_bits(drow[cy - level], cx - level, 2 * level + 1)) +
+           __popc(row_bits(drow[cy + level], cx - level, 2 * level + 1));
+      for (int d = -(level - 1); d <= level - 1; d++) {
+        lc += (drow[cy + d][(cx - level) >> 5] >> ((cx - level) & 31)) & 1;
+        lc += (drow[cy + d][(cx + level) >> 5] >> ((cx + level) & 31)) & 1;
+      }
+      count += lc;
+      level++;
+    } while (lc != 0 && level <= N);
+    v.clear = count <= N;
+  }
+  return v;
+}
+
+constexpr int kListCap = 1024;  // LDS work list of one tile (else: row loops)
+
 template <int FMT>
 __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom g, uint8_t* scratch,
                                                         int64_t sstride, const int32_t* active,
@@ -699,23 +782,94 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
   // Everything is kept as 128-bit region rows (bit = region column):
   //   drow dark (lightness < white), trow trigger (max < white; the same
   //   bits for gray planes), srow small (component <= 4 pixels)
+  constexpr bool kGray = FMT == F_GRAY8;
   constexpr bool kSplit = FMT == F_RGB24;
   __shared__ uint32_t drow[kRW][4];
   __shared__ uint32_t trow_s[kSplit ? kRW : 1][4];
   __shared__ uint32_t srow[kRW][4];
-  __shared__ int32_t any_dark;
+  __shared__ uint64_t l3[kRW][2], cand[kRW][2];
+  __shared__ uint16_t wl[kListCap];
+  __shared__ int32_t any_dark, nwl;
   uint32_t (*trow)[4] = kSplit ? trow_s : drow;
-  // Stage the region rows into LDS with 16-byte loads, all issued before any
-  // is consumed.  Rows start 256-byte aligned, so every vector lies inside
-  // its row's pitch; out-of-image pixels are masked below.
   constexpr int B = FMT == F_GRAY8 ? 1 : FMT == F_Y400A ? 2 : 3;
-  constexpr int NV = (kRW * B + 30) / 16;             // vectors per region row
-  constexpr int NLOAD = (kRW * NV + 255) / 256;       // loads per thread
-  __shared__ uint4 stage[kRW][NV];
-  {
+  const int64_t pitch = img.P.pitch;
+  if (threadIdx.x == 0) {
+    any_dark = 0;
+    nwl = 0;
+  }
+  for (int i = threadIdx.x; i < kRW * 4; i += 256) (&srow[0][0])[i] = 0;
+  if constexpr (kGray) {
+    // Bit rows straight from 16-byte loads: each vector becomes 16 dark bits
+    // (SWAR compare), kept as 16-bit slots of the region row; a row is then
+    // realigned by the region's lead (ox mod 16) into drow.
+    constexpr int kLead = (16 - kHalo % 16) % 16;   // ox = 64*bx - kHalo = kLead (mod 16)
+    constexpr int kVec = (kLead + kRW + 15) / 16;   // 16-byte vectors per region row
+    static_assert(kVec <= 7, "region row exceeds 7 vectors");
+    constexpr int kItems = kRW * kVec;
+    __shared__ uint16_t m16[kRW][8];  // slots [kVec, 8) unused
+    const int64_t a0 = (int64_t)ox - kLead;
+    const uint32_t kadd = (256u - g.white) * 0x00010001u;
+    uint4 v[(kItems + 255) / 256];
+    bool ok[(kItems + 255) / 256];
+#pragma unroll
+    for (int k = 0; k < (kItems + 255) / 256; k++) {
+      const int i = threadIdx.x + k * 256;
+      const int ry = i / kVec, vi = i - ry * kVec;
+      const int32_t gy = oy + ry;
+      const int64_t off = a0 + 16 * vi;
+      ok[k] = i < kItems && gy >= 0 && gy < g.H && off >= 0 && off < g.W;
+      v[k] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+      if (ok[k]) v[k] = *reinterpret_cast<const uint4*>(base + (int64_t)gy * pitch + off);
+    }
+#pragma unroll
+    for (int k = 0; k < (kItems + 255) / 256; k++) {
+      const int i = threadIdx.x + k * 256;
+      const int ry = i / kVec, vi = i - ry * kVec;
+      if (i < kItems) {
+        uint32_t m = 0;
+        if (ok[k]) {
+          const int64_t off = a0 + 16 * vi;
+          m = lt_nibble(v[k].x, kadd) | (lt_nibble(v[k].y, kadd) << 4) |
+              (lt_nibble(v[k].z, kadd) << 8) | (lt_nibble(v[k].w, kadd) << 12);
+          if (off + 16 > g.W) m &= (1u << (g.W - off)) - 1u;  // columns >= W
+        }
+        m16[ry][vi] = (uint16_t)m;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < kRW) {
+      const int ry = threadIdx.x;
+      const uint32_t* q = reinterpret_cast<const uint32_t*>(m16[ry]);
+      uint32_t d[4];
+      uint32_t qw[5];
+#pragma unroll
+      for (int j = 0; j < 5; j++) {  // slots >= kVec are never written: zero
+        qw[j] = 2 * j < kVec ? q[j] : 0u;
+        if (2 * j + 1 >= kVec) qw[j] &= 0xFFFFu;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        d[j] = kLead ? __builtin_amdgcn_alignbit(qw[j + 1], qw[j], kLead) : qw[j];
+      // region columns >= kRW (the lead pulls up to kLead of them in)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int lo = 32 * j;
+        if (lo + 32 > kRW) d[j] &= lo >= kRW ? 0u : ((1u << (kRW - lo)) - 1u);
+        drow[ry][j] = d[j];
+      }
+      // interior columns [kHalo, kHalo + kNT) = bits 14..63 | 64..77
+      const uint64_t lo64 = ((uint64_t)d[1] << 32) | d[0], hi64 = ((uint64_t)d[3] << 32) | d[2];
+      if (ry >= kHalo && ry < kHalo + kNT && ((lo64 >> kHalo) | (hi64 & 0x3FFFull))) any_dark = 1;
+    }
+  } else {
+    // Stage the region rows into LDS with 16-byte loads, all issued before
+    // any is consumed.  Rows start 256-byte aligned, so every vector lies
+    // inside its row's pitch; out-of-image pixels are masked below.
+    constexpr int NV = (kRW * B + 30) / 16;             // vectors per region row
+    constexpr int NLOAD = (kRW * NV + 255) / 256;       // loads per thread
+    __shared__ uint4 stage[kRW][NV];
     const int64_t sb = (int64_t)ox * B;
     const int64_t a0 = sb >= 0 ? (sb & ~(int64_t)15) : -((-sb + 15) & ~(int64_t)15);
-    const int64_t pitch = img.P.pitch;
     uint4 v[NLOAD];
 #pragma unroll
     for (int k = 0; k < NLOAD; k++) {
@@ -732,7 +886,6 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
       const int i = threadIdx.x + k * 256;
       if (i < kRW * NV) stage[i / NV][i % NV] = v[k];
     }
-    if (threadIdx.x == 0) any_dark = 0;
     __syncthreads();
     // dark / trigger bit rows: wave w takes rows w, w+4, ...; lanes own
     // columns lane and 64+lane, each row mask is two ballots
@@ -779,17 +932,14 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
   }
   __syncthreads();
   if (!any_dark) return;
+  if (g.diag == 1) return;
   // Pixels provably in a component of >= 5 pixels: L3 = dark pixels with >= 5
   // dark pixels in their 3x3 block (all 8-adjacent to the centre, so one
   // component); large = dark & (L3 | 8-dilation of L3) (8-adjacent to an L3
   // pixel = same component).  Only the remaining dark pixels ("candidates")
   // need the restricted 9x9 flood.  Rows outside the region read as empty,
   // which can only leave pixels undecided, never mislabel them.  One thread
-  // per (row, 64-bit half); the staging buffer is dead by now and holds the
-  // l3 and candidate rows.
-  uint64_t (*l3)[2] = reinterpret_cast<uint64_t(*)[2]>(&stage[0][0]);
-  uint64_t (*cand)[2] = l3 + kRW;
-  static_assert(sizeof(stage) >= 2 * kRW * 2 * sizeof(uint64_t), "stage too small");
+  // per (row, 64-bit half).
   const int hr = threadIdx.x >> 1, hh = threadIdx.x & 1;
   auto dark64 = [&](int r, int h) -> uint64_t {
     return ((uint64_t)drow[r][2 * h + 1] << 32) | drow[r][2 * h];
@@ -823,7 +973,8 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
     l3[hr][hh] = dark64(hr, hh) & (c3 | (c2 & (c1 | c0)));  // count >= 5: 8 | (4 & (2 | 1))
   }
   __syncthreads();
-  // candidates within radius 10 of the tile (region rows/cols [4, 88))
+  // candidates within radius 10 of the tile (region rows/cols [4, 88)),
+  // appended to the tile's work list as (row << 8 | column)
   if (threadIdx.x < 2 * kRW) {
     uint64_t c = 0;
     if (hr >= 4 && hr < 88) {
@@ -837,107 +988,114 @@ __global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom 
       c = dark64(hr, hh) & ~dil & (hh ? 0xFFFFFFull : ~0xFull);
     }
     cand[hr][hh] = c;
-  }
-  __syncthreads();
-  // small bit rows: the restricted flood, only where there are candidates
-  for (int ry = w; ry < kRW; ry += 4) {
-    unsigned long long m[2] = {0, 0};
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const uint64_t c = cand[ry][h];
-      if (!c) continue;  // uniform
-      bool small = false;
-      if ((c >> lane) & 1) {
-        uint32_t comp[9];
-        small = flood9(drow, h * 64 + lane, ry, comp) <= 4;
+    if (c) {
+      int k = atomicAdd(&nwl, __popcll(c));
+      while (c) {
+        const int b = __ffsll((long long)c) - 1;
+        c &= c - 1;
+        if (k < kListCap) wl[k] = (uint16_t)((hr << 8) | (hh * 64 + b));
+        k++;
       }
-      m[h] = __ballot(small);
-    }
-    if (lane < 4) {
-      const unsigned long long q = m[lane >> 1];
-      srow[ry][lane] = (uint32_t)(lane & 1 ? q >> 32 : q);
     }
   }
   __syncthreads();
+  if (g.diag == 2) return;
+  // small bit rows: the restricted flood of every candidate
+  const int ncand = nwl;
+  if (ncand <= kListCap) {
+    for (int i = threadIdx.x; i < ncand; i += 256) {
+      const int e = wl[i], ry = e >> 8, rx = e & 0xFF;
+      uint32_t comp[9];
+      if (flood9(drow, rx, ry, comp) <= 4) atomicOr(&srow[ry][rx >> 5], 1u << (rx & 31));
+    }
+  } else {
+    for (int ry = w; ry < kRW; ry += 4) {
+      unsigned long long m[2] = {0, 0};
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const uint64_t c = cand[ry][h];
+        if (!c) continue;  // uniform
+        bool small = false;
+        if ((c >> lane) & 1) {
+          uint32_t comp[9];
+          small = flood9(drow, h * 64 + lane, ry, comp) <= 4;
+        }
+        m[h] = __ballot(small);
+      }
+      if (lane < 4) {
+        const unsigned long long q = m[lane >> 1];
+        srow[ry][lane] = (uint32_t)(lane & 1 ? q >> 32 : q);
+      }
+    }
+  }
+  __syncthreads();
+  if (g.diag == 3) return;
   const int N = g.intensity;
-  // the tile's rows, one wave per row, lanes on the tile's 64 columns
   const bool zone_tile = g.all_seq || tx0 < kZone || ty0 < kZone;  // uniform
-  for (int t = w; t < kNT; t += 4) {
-    const int ry = kHalo + t, rx = kHalo + lane;
-    const int32_t gy = oy + ry, gx = ox + rx;
-    const bool trig = (trow[ry][rx >> 5] >> (rx & 31)) & 1;
-    const bool zone = g.all_seq || gx < kZone || gy < kZone;
-    if (zone_tile) {
-      // edge zone (and intensity > 4): every trigger is replayed in order
+  if (zone_tile) {
+    // edge zone (and intensity > 4): every trigger there is replayed in
+    // order; the tile's rows, one wave per row, lanes on the tile's columns
+    for (int t = w; t < kNT; t += 4) {
+      const int ry = kHalo + t, rx = kHalo + lane;
+      const int32_t gy = oy + ry, gx = ox + rx;
+      const bool trig = (trow[ry][rx >> 5] >> (rx & 31)) & 1;
+      const bool zone = g.all_seq || gx < kZone || gy < kZone;
       const bool dark = (drow[ry][rx >> 5] >> (rx & 31)) & 1;
       wave_append(dark & zone & trig, gx, gy, NP.nseq, NP.seq, g.capacity);
     }
-    if (!(row_bits(srow[ry], kHalo, 32) | row_bits(srow[ry], kHalo + 32, 32))) continue;  // uniform
-    const bool small = !zone && ((srow[ry][rx >> 5] >> (rx & 31)) & 1);
-    bool seq = false, clear = false;
-    if (small) {
-      uint32_t comp[9];
-      flood9(drow, rx, ry, comp);
-      // component pixels (<= 4) relative to (rx, ry), and their bounding box
-      int cxs[4], cys[4], nc = 0;
-      int bx0 = 9, bx1 = -1, by0 = 9, by1 = -1;
-#pragma unroll
-      for (int r = 0; r < 9; r++) {
-        uint32_t mm = comp[r];
-        if (mm) {
-          by0 = imin(by0, r);
-          by1 = r;
-          bx0 = imin(bx0, __ffs(mm) - 1);
-          bx1 = imax(bx1, 31 - __clz(mm));
-        }
-        while (mm) {
-          const int b = __ffs(mm) - 1;
-          mm &= mm - 1;
-          if (nc < 4) {
-            cxs[nc] = b - 4;
-            cys[nc] = r - 4;
-          }
-          nc++;
-        }
-      }
-      bool eligible = nc <= 4 && gx - 4 + bx0 >= kEligible && gy - 4 + by0 >= kEligible;
-      // no foreign small pixel within Chebyshev 7 of the component: checked on
-      // the bounding box dilated by 7 (a superset, so a component rejected
-      // here merely takes the exact sequential path)
-      if (eligible) {
-        const int X0 = rx - 4 + bx0 - 7, n = bx1 - bx0 + 15;
-        int cnt = 0;
-        for (int r = ry - 4 + by0 - 7; r <= ry - 4 + by1 + 7; r++)
-          cnt += __popc(row_bits(srow[r], X0, n));
-        eligible = cnt == nc;
-      }
-      if (!eligible) {
-        seq = trig;
-      } else {
-        // cleared iff some trigger of the component passes the ring test on
-        // the original image (eligible pixels are >= 40 from the edges, so the
-        // reference's unsigned ring-loop skips never apply)
-        for (int k = 0; k < nc && k < 4 && !clear; k++) {
-          const int cx = rx + cxs[k], cy = ry + cys[k];
-          if (!((trow[cy][cx >> 5] >> (cx & 31)) & 1)) continue;
-          int count = 1, lc;
-          int level = 1;
-          do {
-            lc = __popc(row_bits(drow[cy - level], cx - level, 2 * level + 1)) +
-                 __popc(row_bits(drow[cy + level], cx - level, 2 * level + 1));
-            for (int d = -(level - 1); d <= level - 1; d++) {
-              lc += (drow[cy + d][(cx - level) >> 5] >> ((cx - level) & 31)) & 1;
-              lc += (drow[cy + d][(cx + level) >> 5] >> ((cx + level) & 31)) & 1;
-            }
-            count += lc;
-            level++;
-          } while (lc != 0 && level <= N);
-          clear = count <= N;
+  }
+  // small pixels of the tile outside the zone: one lane each
+  if (threadIdx.x == 0) nwl = 0;
+  __syncthreads();
+  if (threadIdx.x < 2 * kNT) {
+    const int ry = kHalo + (threadIdx.x >> 1), h = threadIdx.x & 1;
+    uint32_t m = row_bits(srow[ry], kHalo + 32 * h, 32);
+    if (m && !g.all_seq && oy + ry >= kZone) {
+      const int32_t gx0 = ox + kHalo + 32 * h;  // column of bit 0
+      if (gx0 < kZone) m &= kZone - gx0 >= 32 ? 0u : ~((1u << (kZone - gx0)) - 1u);
+      if (m) {
+        int k = atomicAdd(&nwl, __popc(m));
+        while (m) {
+          const int b = __ffs(m) - 1;
+          m &= m - 1;
+          if (k < kListCap) wl[k] = (uint16_t)((ry << 8) | (kHalo + 32 * h + b));
+          k++;
         }
       }
     }
-    wave_append(seq, gx, gy, NP.nseq, NP.seq, g.capacity);
-    wave_append(clear, gx, gy, NP.nclear, NP.clear, g.capacity);
+  }
+  __syncthreads();
+  const int nsmall = nwl;
+  if (nsmall <= kListCap) {
+    for (int b0 = 0; b0 < nsmall; b0 += 256) {  // uniform trip count
+      const int i = b0 + threadIdx.x;
+      SmallVerdict v{false, false};
+      int32_t gx = 0, gy = 0;
+      if (i < nsmall) {
+        const int e = wl[i], ry = e >> 8, rx = e & 0xFF;
+        gx = ox + rx;
+        gy = oy + ry;
+        const bool trig = (trow[ry][rx >> 5] >> (rx & 31)) & 1;
+        v = small_verdict(drow, trow, srow, rx, ry, gx, gy, trig, N);
+      }
+      wave_append(v.seq, gx, gy, NP.nseq, NP.seq, g.capacity);
+      wave_append(v.clear, gx, gy, NP.nclear, NP.clear, g.capacity);
+    }
+  } else {
+    for (int t = w; t < kNT; t += 4) {
+      const int ry = kHalo + t, rx = kHalo + lane;
+      const int32_t gy = oy + ry, gx = ox + rx;
+      if (!(row_bits(srow[ry], kHalo, 32) | row_bits(srow[ry], kHalo + 32, 32))) continue;  // uniform
+      const bool zone = g.all_seq || gx < kZone || gy < kZone;
+      const bool small = !zone && ((srow[ry][rx >> 5] >> (rx & 31)) & 1);
+      SmallVerdict v{false, false};
+      if (small) {
+        const bool trig = (trow[ry][rx >> 5] >> (rx & 31)) & 1;
+        v = small_verdict(drow, trow, srow, rx, ry, gx, gy, trig, N);
+      }
+      wave_append(v.seq, gx, gy, NP.nseq, NP.seq, g.capacity);
+      wave_append(v.clear, gx, gy, NP.nclear, NP.clear, g.capacity);
+    }
   }
 }
 
@@ -1301,7 +1459,10 @@ static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr
                            const int32_t* active, SheetCtl* ctl, int count, hipStream_t st,
                            uint32_t* sortbuf, int64_t sort_stride) {
   dim3 grid((g.W + kNT - 1) / kNT, (g.H + kNT - 1) / kNT, count);
-  hipLaunchKernelGGL(k_noise_classify<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active, ctl);
+  static const int diag = getenv("UPHIP_DIAG_NOISE") ? atoi(getenv("UPHIP_DIAG_NOISE")) : 0;
+  NoiseGeom gd = g;
+  gd.diag = diag;
+  hipLaunchKernelGGL(k_noise_classify<FMT>, grid, dim3(256), 0, st, img, gd, scr, ss, active, ctl);
   hipLaunchKernelGGL(k_noise_apply<FMT>, dim3(64, count), dim3(256), 0, st, img, g, scr, ss,
                      active, ctl);
   hipLaunchKernelGGL(k_noise_resolve<FMT>, dim3(count), dim3(256), 0, st, img, g, scr, ss, active,
