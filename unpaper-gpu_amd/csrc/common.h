@@ -11,6 +11,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "unpaper_hip.h"
 
@@ -198,6 +199,13 @@ enum : int32_t {
 
 __device__ __forceinline__ uint8_t* sheet_plane(const Planes& P, int s, int k) {
   return P.base[k] + (int64_t)s * P.stride;
+}
+
+// TEMP timing diagnostics: UPHIP_DIAG_SKIP bit mask of sequential kernels
+// not launched (1 black, 2 noise resolve, 4 gray decide, 8 blur resolve).
+inline int diag_skip() {
+  static const int v = getenv("UPHIP_DIAG_SKIP") ? atoi(getenv("UPHIP_DIAG_SKIP")) : 0;
+  return v;
 }
 
 }  // namespace uph

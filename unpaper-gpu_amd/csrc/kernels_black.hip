@@ -351,9 +351,9 @@ static void launch_black_t(const PlaneRef& img, const BlackGeom& g, const BlackB
   if (g.hregion.x1 >= g.hregion.x0 && g.hregion.y1 >= g.hregion.y0)
     launch_axis_reduce(img, hargs, 0, M_DARKINV_SUM, g.W, g.H, (uint32_t*)scr, ss / 4, count, st);
   if (g.vregion.x1 >= g.vregion.x0 && g.vregion.y1 >= g.vregion.y0)
-    launch_axis_reduce(img, vargs, 1, M_DARKINV_SUM, g.W, g.H, (uint32_t*)scr + g.W, ss / 4,
-                       count, st);
-  hipLaunchKernelGGL(k_black_resolve<FMT>, dim3(count), dim3(64), 0, st, img, g, bars, scr, ss,
+    launch_axis_reduce(img, vargs, 1, M_DARKINV_SUM, g.vregion.x1 - g.vregion.x0 + 1, g.H,
+                       (uint32_t*)scr + g.W, ss / 4, count, st);
+  if (!(diag_skip() & 1)) hipLaunchKernelGGL(k_black_resolve<FMT>, dim3(count), dim3(64), 0, st, img, g, bars, scr, ss,
                      active, ctl);
 }
 

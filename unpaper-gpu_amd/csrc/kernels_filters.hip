@@ -68,15 +68,17 @@ bool gray_geometry(int32_t W, int32_t H, const UphipGrayfilterParameters& p, uin
 size_t gray_scratch_bytes(const GrayGeom& g) {
   const size_t cells = (size_t)g.ncx * g.ncy;
   const size_t tiles = (size_t)g.ntx * g.nty;
-  size_t b = cells * 8 + tiles + cells;  // dark+light (2 x u32), tile state, cell wipe
+  size_t b = cells * 8 + tiles;  // dark+light (2 x u32), tile state
+  b = (b + 3) & ~(size_t)3;
+  b += 4;                        // undecided-tile counter
   return (b + 255) & ~(size_t)255;
 }
 
 struct GrayPtrs {
   uint32_t* dark;
   uint32_t* light;
-  uint8_t* tile;
-  uint8_t* cellw;
+  uint8_t* tile;     // 0 = never, 1 = undecided, 2 = wiped (3 = newly wiped, transient)
+  uint32_t* nund;    // undecided tiles
 };
 __device__ __forceinline__ GrayPtrs gray_ptrs(const GrayGeom& g, uint8_t* base) {
   const size_t cells = (size_t)g.ncx * g.ncy;
@@ -85,7 +87,7 @@ __device__ __forceinline__ GrayPtrs gray_ptrs(const GrayGeom& g, uint8_t* base) 
   p.dark = (uint32_t*)base;
   p.light = p.dark + cells;
   p.tile = (uint8_t*)(p.light + cells);
-  p.cellw = p.tile + tiles;
+  p.nund = (uint32_t*)(base + ((cells * 8 + tiles + 3) & ~(size_t)3));
   return p;
 }
 
@@ -95,8 +97,9 @@ __global__ void __launch_bounds__(256) k_gray_cells(PlaneRef img, GrayGeom g, ui
   const int s = blockIdx.z;
   if (active && !active[s]) return;
   const int32_t cx = blockIdx.x * 256 + threadIdx.x, cy = blockIdx.y;
-  if (cx >= g.ncx) return;
   GrayPtrs P = gray_ptrs(g, scratch + s * sstride);
+  if (cx == 0 && cy == 0) *P.nund = 0;
+  if (cx >= g.ncx) return;
   const uint8_t* base = plane_ptr(img, s);
   const int32_t x0 = cx * g.cw, x1 = imin(x0 + g.cw, g.W);
   const int32_t y0 = cy * g.ch, y1 = imin(y0 + g.ch, g.H);
@@ -125,6 +128,7 @@ __global__ void __launch_bounds__(256) k_gray_cells_g(PlaneRef img, GrayGeom g, 
   if (active && !active[s]) return;
   const int32_t cy = blockIdx.x;
   GrayPtrs P = gray_ptrs(g, scratch + s * sstride);
+  if (cy == 0 && threadIdx.x == 0) *P.nund = 0;
   const uint8_t* base = plane_ptr(img, s);
   const int32_t y0 = cy * g.ch, y1 = imin(y0 + g.ch, g.H);
   extern __shared__ uint16_t cols16[];  // [W] dark counts, then [W] lightness sums
@@ -217,17 +221,30 @@ __device__ uint8_t gray_tile_inv(const GrayGeom& g, const GrayPtrs& P, int32_t t
   return (uint8_t)(0xFFull - sum / count);
 }
 
-__global__ void __launch_bounds__(1024) k_gray_decide(GrayGeom g, uint8_t* scratch, int64_t sstride,
-                                                      const int32_t* active) {
-  const int s = blockIdx.x;
+// Whether cell (cx, cy) lies in a wiped tile (2): the tiles covering it are
+// ux in [ceil((cx - tw + 1) / tsx), cx / tsx], likewise uy.
+__device__ __forceinline__ bool gray_cell_wiped(const GrayGeom& g, const uint8_t* tile, int32_t cx,
+                                                int32_t cy) {
+  const int32_t uy0 = imax(0, (cy - g.th + g.tsy) / g.tsy), uy1 = imin(cy / g.tsy, g.nty - 1);
+  const int32_t ux0 = imax(0, (cx - g.tw + g.tsx) / g.tsx), ux1 = imin(cx / g.tsx, g.ntx - 1);
+  for (int32_t uy = uy0; uy <= uy1; uy++)
+    for (int32_t ux = ux0; ux <= ux1; ux++)
+      if (tile[(size_t)uy * g.ntx + ux] == 2) return true;
+  return false;
+}
+
+// Every tile decided on the original image, one thread per tile: tiles with
+// a dark pixel never wipe; tiles light enough on the original always wipe
+// (wipes only brighten); the rest are undecided and counted.
+__global__ void __launch_bounds__(256) k_gray_tiles(GrayGeom g, uint8_t* scratch, int64_t sstride,
+                                                    const int32_t* active) {
+  const int s = blockIdx.y;
   if (active && !active[s]) return;
   GrayPtrs P = gray_ptrs(g, scratch + s * sstride);
+  const int32_t t = blockIdx.x * 256 + threadIdx.x;
   const int32_t ntiles = g.ntx * g.nty;
-  __shared__ int32_t undecided, changed;
-  if (threadIdx.x == 0) undecided = 0;
-  __syncthreads();
-  // 0 = never, 1 = undecided, 2 = wiped, 3 = newly wiped (this pass)
-  for (int32_t t = threadIdx.x; t < ntiles; t += blockDim.x) {
+  bool und = false;
+  if (t < ntiles) {
     const int32_t tx = t % g.ntx, ty = t / g.ntx;
     uint32_t dark = 0;
     for (int32_t j = 0; j < g.th; j++) {
@@ -242,52 +259,42 @@ __global__ void __launch_bounds__(1024) k_gray_decide(GrayGeom g, uint8_t* scrat
     uint8_t st = 0;
     if (dark == 0) {
       st = gray_tile_inv(g, P, tx, ty, 0) < g.abs_thr ? 2 : 1;
-      if (st == 1) atomicAdd(&undecided, 1);
+      und = st == 1;
     }
     P.tile[t] = st;
   }
-  __syncthreads();
-  if (undecided) {
-    for (int iter = 0; iter < ntiles + 1; iter++) {
-      if (threadIdx.x == 0) changed = 0;
-      __syncthreads();
-      for (int32_t t = threadIdx.x; t < ntiles; t += blockDim.x) {
-        if (P.tile[t] != 1) continue;
-        const int32_t tx = t % g.ntx, ty = t / g.ntx;
-        if (gray_tile_inv(g, P, tx, ty, 1) < g.abs_thr) {
-          P.tile[t] = 3;
-          changed = 1;
-        }
-      }
-      __threadfence_block();
-      __syncthreads();
-      if (!changed) break;
-      for (int32_t t = threadIdx.x; t < ntiles; t += blockDim.x)
-        if (P.tile[t] == 3) P.tile[t] = 2;
-      __threadfence_block();
-      __syncthreads();
-    }
-  }
-  // cell wipe flags: any covering tile wiped
-  const int32_t ncells = g.ncx * g.ncy;
-  for (int32_t c = threadIdx.x; c < ncells; c += blockDim.x) {
-    const int32_t cx = c % g.ncx, cy = c / g.ncx;
-    uint8_t w = 0;
-    for (int32_t oy = cy - g.th + 1; oy <= cy && !w; oy++) {
-      if (oy < 0 || oy % g.tsy) continue;
-      const int32_t uy = oy / g.tsy;
-      if (uy >= g.nty) continue;
-      for (int32_t ox = cx - g.tw + 1; ox <= cx; ox++) {
-        if (ox < 0 || ox % g.tsx) continue;
-        const int32_t ux = ox / g.tsx;
-        if (ux >= g.ntx) continue;
-        if (P.tile[(size_t)uy * g.ntx + ux] == 2) {
-          w = 1;
-          break;
-        }
+  const unsigned long long M = __ballot(und);
+  if (M && (threadIdx.x & 63) == __ffsll((long long)M) - 1) atomicAdd(P.nund, (uint32_t)__popcll(M));
+}
+
+// The wipe feedback: Jacobi sweeps over the undecided tiles until nothing
+// changes (one block per sheet; returns at once when none is undecided).
+__global__ void __launch_bounds__(1024) k_gray_decide(GrayGeom g, uint8_t* scratch, int64_t sstride,
+                                                      const int32_t* active) {
+  const int s = blockIdx.x;
+  if (active && !active[s]) return;
+  GrayPtrs P = gray_ptrs(g, scratch + s * sstride);
+  if (*P.nund == 0) return;
+  const int32_t ntiles = g.ntx * g.nty;
+  __shared__ int32_t changed;
+  for (int iter = 0; iter < ntiles + 1; iter++) {
+    if (threadIdx.x == 0) changed = 0;
+    __syncthreads();
+    for (int32_t t = threadIdx.x; t < ntiles; t += blockDim.x) {
+      if (P.tile[t] != 1) continue;
+      const int32_t tx = t % g.ntx, ty = t / g.ntx;
+      if (gray_tile_inv(g, P, tx, ty, 1) < g.abs_thr) {
+        P.tile[t] = 3;
+        changed = 1;
       }
     }
-    P.cellw[c] = w;
+    __threadfence_block();
+    __syncthreads();
+    if (!changed) break;
+    for (int32_t t = threadIdx.x; t < ntiles; t += blockDim.x)
+      if (P.tile[t] == 3) P.tile[t] = 2;
+    __threadfence_block();
+    __syncthreads();
   }
 }
 
@@ -299,7 +306,10 @@ __global__ void __launch_bounds__(256) k_gray_wipe(PlaneRef img, GrayGeom g, uin
   const int32_t cx = blockIdx.x * 256 + threadIdx.x, cy = blockIdx.y;
   if (cx >= g.ncx) return;
   GrayPtrs P = gray_ptrs(g, scratch + s * sstride);
-  if (!P.cellw[(size_t)cy * g.ncx + cx]) return;
+  if (!gray_cell_wiped(g, P.tile, cx, cy)) return;
+  // a cell whose lightness sum is all white is white already (Y400A wipes
+  // also set alpha, so its cells are always written)
+  if (FMT != F_Y400A && P.light[(size_t)cy * g.ncx + cx] == 255u * cell_pixels(g, cx, cy)) return;
   uint8_t* base = plane_ptr(img, s);
   const int32_t x0 = cx * g.cw, x1 = imin(x0 + g.cw, g.W);
   const int32_t y0 = cy * g.ch, y1 = imin(y0 + g.ch, g.H);
@@ -318,7 +328,10 @@ static void launch_gray_t(const PlaneRef& img, const GrayGeom& g, uint8_t* scr, 
                        4 * (size_t)((g.W + 3) & ~3), st, img, g, scr, ss, active);
   else
     hipLaunchKernelGGL(k_gray_cells<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active);
-  hipLaunchKernelGGL(k_gray_decide, dim3(count), dim3(1024), 0, st, g, scr, ss, active);
+  const int32_t ntiles = g.ntx * g.nty;
+  hipLaunchKernelGGL(k_gray_tiles, dim3((ntiles + 255) / 256, count), dim3(256), 0, st, g, scr, ss,
+                     active);
+  if (!(diag_skip() & 4)) hipLaunchKernelGGL(k_gray_decide, dim3(count), dim3(1024), 0, st, g, scr, ss, active);
   hipLaunchKernelGGL(k_gray_wipe<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active);
 }
 
@@ -524,7 +537,7 @@ static void launch_blur_t(const PlaneRef& img, const BlurGeom& g, uint8_t* scr, 
     hipLaunchKernelGGL(k_blur_counts<FMT>, dim3(g.nrect, count), dim3(256), 0, st, img, g, scr, ss,
                        active);
   const size_t lds = sizeof(uint64_t) * ((size_t)g.nrect + 3 * (size_t)(g.bpr + 2));
-  hipLaunchKernelGGL(k_blur_resolve, dim3(count), dim3(256), lds, st, g, scr, ss, active);
+  if (!(diag_skip() & 8)) hipLaunchKernelGGL(k_blur_resolve, dim3(count), dim3(256), lds, st, g, scr, ss, active);
   if (g.T * g.bpr > 0)
     hipLaunchKernelGGL(k_blur_wipe<FMT>, dim3(g.T * g.bpr, count), dim3(256), 0, st, img, g, scr,
                        ss, active);
@@ -1465,7 +1478,7 @@ static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr
   hipLaunchKernelGGL(k_noise_classify<FMT>, grid, dim3(256), 0, st, img, gd, scr, ss, active, ctl);
   hipLaunchKernelGGL(k_noise_apply<FMT>, dim3(64, count), dim3(256), 0, st, img, g, scr, ss,
                      active, ctl);
-  hipLaunchKernelGGL(k_noise_resolve<FMT>, dim3(count), dim3(256), 0, st, img, g, scr, ss, active,
+  if (!(diag_skip() & 2)) hipLaunchKernelGGL(k_noise_resolve<FMT>, dim3(count), dim3(256), 0, st, img, g, scr, ss, active,
                      ctl, sortbuf, sort_stride);
 }
 

@@ -125,45 +125,70 @@ __global__ void __launch_bounds__(256) k_colsum_g(PlaneRef ref, const AxisArgs* 
   if (x >= r.x0 && x <= r.x1 && t) atomicAdd(out + (int64_t)s * out_stride + x, t);
 }
 
-// axis 1 on a gray plane: one wave per row, each lane sums up to 4 aligned
-// 16-byte vectors (issued together), then a wave reduction.
+// axis 1 on a gray plane: a row is a segment of L lanes (L = the power of
+// two covering its 16-byte vectors, at most 64), so narrow regions (the
+// blackfilter's vertical stripe) put several rows in one wave.  Every vector
+// is measured four bytes at a time: v_sad_u8 sums four bytes, the dark count
+// is the popcount of a SWAR compare; only the two edge vectors of a row are
+// masked byte by byte.
+template <int MEAS>
+__device__ __forceinline__ uint32_t measure_g4(uint32_t x, uint32_t keep, uint32_t kadd,
+                                               uint32_t acc) {
+  if (MEAS == M_DARK_COUNT) {
+    const uint32_t lo = ((x & 0x00FF00FFu) + kadd) & 0x01000100u;
+    const uint32_t hi = (((x >> 8) & 0x00FF00FFu) + kadd) & 0x01000100u;
+    const uint32_t ge = (lo >> 8) | (hi >> 7);                 // byte >= thr+1, bits 0,1,16,17
+    const uint32_t lt = ~(ge | (ge >> 14)) & 0xFu;             // bytes <= thr
+    const uint32_t kp = (keep & 1u) | ((keep >> 7) & 2u) | ((keep >> 14) & 4u) | ((keep >> 21) & 8u);
+    return acc + __popc(lt & kp);
+  }
+  return __builtin_amdgcn_sad_u8(x & keep, 0u, acc);
+}
+
 template <int MEAS>
 __global__ void __launch_bounds__(256) k_rowsum_g(PlaneRef ref, const AxisArgs* args, uint32_t* out,
-                                                  int64_t out_stride) {
+                                                  int64_t out_stride, int seg_log2) {
   const int s = blockIdx.z;
   const AxisArgs a = args[s];
   if (!a.active) return;
   const Rect r = a.region;
   if (r.x1 < r.x0) return;
-  const int lane = threadIdx.x & 63;
-  const int32_t y = r.y0 + (int32_t)blockIdx.x * 4 + (int32_t)(threadIdx.x >> 6);
-  if (y > r.y1) return;
-  const uint8_t* row = plane_ptr(ref, s) + (int64_t)y * ref.P.pitch;
-  const int32_t a0 = r.x0 & ~15;
+  const int L = 1 << seg_log2, sl = threadIdx.x & (L - 1);
+  const int32_t y = r.y0 + (int32_t)((blockIdx.x * 256 + threadIdx.x) >> seg_log2);
+  const bool live = y <= r.y1;
+  const uint8_t* row = plane_ptr(ref, s) + (int64_t)(live ? y : r.y0) * ref.P.pitch;
+  const int32_t a0 = r.x0 & ~15, nv = ((r.x1 | 15) - a0 + 1) >> 4;
+  const uint32_t kadd = (256u - ((uint32_t)a.thr + 1u)) * 0x00010001u;
   uint32_t acc = 0;
-  for (int32_t c0 = a0; c0 <= r.x1; c0 += 64 * 16 * 4) {
+  for (int32_t v0 = 0; v0 < nv; v0 += 4 * L) {
     uint4 v[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const int32_t c = c0 + (k * 64 + lane) * 16;
-      const bool in = c <= r.x1;
-      v[k] = *reinterpret_cast<const uint4*>(row + (in ? c : a0));  // past x1: a valid address
-      if (!in) v[k] = make_uint4(0, 0, 0, 0);
+      const int32_t vi = v0 + k * L + sl;
+      v[k] = *reinterpret_cast<const uint4*>(row + a0 + 16 * (vi < nv ? vi : 0));
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const int32_t c = c0 + (k * 64 + lane) * 16;
+      const int32_t vi = v0 + k * L + sl;
+      if (vi >= nv || !live) continue;
+      const int32_t c = a0 + 16 * vi;
       const uint32_t wd[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
 #pragma unroll
-      for (int j = 0; j < 16; j++) {
-        const int32_t x = c + j;
-        const uint32_t m = measure_g<MEAS>((wd[j >> 2] >> (8 * (j & 3))) & 0xFF, a.thr);
-        acc += (x >= r.x0 && x <= r.x1) ? m : 0u;
+      for (int j = 0; j < 4; j++) {
+        const int32_t x = c + 4 * j;
+        uint32_t keep = 0xFFFFFFFFu;
+        if (x < r.x0 || x + 3 > r.x1) {
+          keep = 0;
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            if (x + q >= r.x0 && x + q <= r.x1) keep |= 0xFFu << (8 * q);
+        }
+        acc = measure_g4<MEAS>(wd[j], keep, kadd, acc);
       }
     }
   }
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
-  if (lane == 0) out[(int64_t)s * out_stride + y] = acc;
+  for (int o = L >> 1; o > 0; o >>= 1) acc += __shfl_down(acc, o, L);
+  if (sl == 0 && live) out[(int64_t)s * out_stride + y] = acc;
 }
 
 template <int FMT, int MEAS>
@@ -178,8 +203,15 @@ static void launch_axis_t(const PlaneRef& ref, const AxisArgs* args, int axis, i
       hipLaunchKernelGGL((k_colsum_g<MEAS>), grid, dim3(256), 0, st, ref, args, out, out_stride,
                          rpb);
     } else {
-      dim3 grid((span_y + 3) / 4, 1, count);
-      hipLaunchKernelGGL((k_rowsum_g<MEAS>), grid, dim3(256), 0, st, ref, args, out, out_stride);
+      // lanes per row: the power of two covering a full-width row's vectors
+      // (the regions of one launch differ per sheet only in position)
+      const int nv = (span_x + 30) / 16;
+      int lg = 0;
+      while ((1 << lg) < nv && lg < 6) lg++;
+      const int64_t rows_per_block = 256 >> lg;
+      dim3 grid((unsigned)((span_y + rows_per_block - 1) / rows_per_block), 1, count);
+      hipLaunchKernelGGL((k_rowsum_g<MEAS>), grid, dim3(256), 0, st, ref, args, out, out_stride,
+                         lg);
     }
     return;
   }
