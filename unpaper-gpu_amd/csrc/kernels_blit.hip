@@ -534,15 +534,16 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
   const uint8_t bg = gray_of(Px{a.bg[0], a.bg[1], a.bg[2]});
   const uint32_t bg4 = bg * 0x01010101u;
   const int32_t nv = (P.W + 15) >> 4;                  // vectors per row (inside the pitch)
-  const uint32_t total = (uint32_t)nv * (uint32_t)P.H;
-  const uint32_t m = nv > 1 ? (uint32_t)((0xFFFFFFFFull / (uint32_t)nv) + 1) : 0u;
   const int32_t delta = A.x0 - a.tx;                   // source column - destination column
   const int r16 = delta & 15, q = r16 >> 2, r = r16 & 3;
   const int32_t bp[5] = {a.tx, a.tx + aw, a.tx + sw, A.x0, A.x1 + 1};
-  for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < total; i += gridDim.x * kThreads) {
-    const int32_t y = nv > 1 ? (int32_t)__umulhi(i, m) : (int32_t)i;
-    const int32_t x0 = 16 * (int32_t)(i - (uint32_t)y * nv);
+  const int lane = threadIdx.x & 63;
+  // one wave per destination row, kMoveVec vectors per lane, loads issued first
+  constexpr int kMoveVec = 4;
+  for (int32_t y = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); y < P.H;
+       y += gridDim.x * (kThreads / 64)) {
     const uint8_t* srow = sbase + (int64_t)y * P.pitch;
+    uint8_t* drow = dbase + (int64_t)y * P.pitch;
     const int32_t v = y - a.ty;
     const bool trow = v >= 0 && v < sh;              // row crosses the pasted rectangle
     const bool mrow = trow && v < ah;                // ... and its copied extent
@@ -553,38 +554,58 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
       if (trow && u >= 0 && u < sw) return (mrow && u < aw) ? 2 : 1;
       return (arow && x >= A.x0 && x <= A.x1) ? 1 : 0;
     };
-    bool uni = x0 + 16 <= P.W;
+    for (int32_t vb = 0; vb < nv; vb += 64 * kMoveVec) {
+      int cls[kMoveVec];
+      uint4 lo[kMoveVec], hi[kMoveVec];
 #pragma unroll
-    for (int k = 0; k < 5; k++) uni &= !(bp[k] > x0 && bp[k] < x0 + 16);
-    const int c0 = cls_of(x0);
-    uint4 out;
-    if (uni && c0 == 0) {
-      out = *reinterpret_cast<const uint4*>(srow + x0);
-    } else if (uni && c0 == 1) {
-      out = make_uint4(bg4, bg4, bg4, bg4);
-    } else if (uni && ((x0 + delta) & ~15) + (r16 ? 32 : 16) <= P.pitch) {
-      const uint4* qp = reinterpret_cast<const uint4*>(mrow_p + ((x0 + delta) & ~15));
-      const uint4 lo = qp[0], hi = r16 ? qp[1] : make_uint4(0, 0, 0, 0);
-      const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      switch (q) {  // uniform over the sheet
-        case 0: out = shift_bytes16<0>(w, r); break;
-        case 1: out = shift_bytes16<1>(w, r); break;
-        case 2: out = shift_bytes16<2>(w, r); break;
-        default: out = shift_bytes16<3>(w, r); break;
-      }
-    } else {
-      uint32_t o[4] = {0, 0, 0, 0};
+      for (int k = 0; k < kMoveVec; k++) {
+        const int32_t vi = vb + k * 64 + lane;
+        const int32_t x0 = 16 * vi;
+        bool uni = vi < nv && x0 + 16 <= P.W;
 #pragma unroll
-      for (int j = 0; j < 16; j++) {
-        const int32_t x = x0 + j;
-        if (x >= P.W) break;
-        const int c = cls_of(x);
-        const uint8_t b = c == 0 ? srow[x] : c == 1 ? bg : mrow_p[x + delta];
-        o[j >> 2] |= (uint32_t)b << (8 * (j & 3));
+        for (int j = 0; j < 5; j++) uni &= !(bp[j] > x0 && bp[j] < x0 + 16);
+        int c = vi < nv ? cls_of(x0) : -1;
+        if (c == 2 && !(uni && ((x0 + delta) & ~15) + (r16 ? 32 : 16) <= P.pitch)) uni = false;
+        cls[k] = vi >= nv ? -1 : uni ? c : 3;  // 3: byte by byte
+        lo[k] = make_uint4(bg4, bg4, bg4, bg4);
+        hi[k] = make_uint4(0, 0, 0, 0);
+        if (cls[k] == 0) {
+          lo[k] = *reinterpret_cast<const uint4*>(srow + x0);
+        } else if (cls[k] == 2) {
+          const uint4* qp = reinterpret_cast<const uint4*>(mrow_p + ((x0 + delta) & ~15));
+          lo[k] = qp[0];
+          if (r16) hi[k] = qp[1];
+        }
       }
-      out = make_uint4(o[0], o[1], o[2], o[3]);
+#pragma unroll
+      for (int k = 0; k < kMoveVec; k++) {
+        const int32_t vi = vb + k * 64 + lane;
+        const int32_t x0 = 16 * vi;
+        if (cls[k] < 0) continue;
+        uint4 out = lo[k];
+        if (cls[k] == 2 && r16) {
+          const uint32_t w[8] = {lo[k].x, lo[k].y, lo[k].z, lo[k].w,
+                                 hi[k].x, hi[k].y, hi[k].z, hi[k].w};
+          switch (q) {  // uniform over the sheet
+            case 0: out = shift_bytes16<0>(w, r); break;
+            case 1: out = shift_bytes16<1>(w, r); break;
+            case 2: out = shift_bytes16<2>(w, r); break;
+            default: out = shift_bytes16<3>(w, r); break;
+          }
+        } else if (cls[k] == 3) {
+          uint32_t o[4] = {0, 0, 0, 0};
+          for (int j = 0; j < 16; j++) {
+            const int32_t x = x0 + j;
+            if (x >= P.W) break;
+            const int c = cls_of(x);
+            const uint8_t bb = c == 0 ? srow[x] : c == 1 ? bg : mrow_p[x + delta];
+            o[j >> 2] |= (uint32_t)bb << (8 * (j & 3));
+          }
+          out = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        *reinterpret_cast<uint4*>(drow + x0) = out;
+      }
     }
-    *reinterpret_cast<uint4*>(dbase + (int64_t)y * P.pitch + x0) = out;
   }
 }
 
@@ -592,10 +613,9 @@ void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* 
                       hipStream_t st) {
   int gx = src.P.H < 1 ? 1 : (src.P.H > 1024 ? 1024 : src.P.H);
   if (src.P.fmt == F_GRAY8) {
-    // about four 16-byte vectors per lane
-    const int64_t vecs = (int64_t)((src.P.W + 15) >> 4) * src.P.H;
-    const int64_t g16 = (vecs + 4 * kThreads - 1) / (4 * kThreads);
-    hipLaunchKernelGGL(k_move_rect_g16, dim3((unsigned)(g16 < 1 ? 1 : g16), 1, count),
+    // one wave per row, about two rows per wave
+    const int64_t blocks = (src.P.H + 2 * (kThreads / 64) - 1) / (2 * (kThreads / 64));
+    hipLaunchKernelGGL(k_move_rect_g16, dim3((unsigned)(blocks < 1 ? 1 : blocks), 1, count),
                        dim3(kThreads), 0, st, src, dst, args);
   } else if (src.P.fmt == F_Y400A) {
     hipLaunchKernelGGL(k_move_rect<F_Y400A>, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst,

@@ -119,55 +119,138 @@ size_t rotation_lines_bytes(int count, int nedges, int nangles, int max_scan) {
                                     4 * nlines);
 }
 
-// ---- k_rot_points: one lane per left/right line, the recurrence in order --
-__global__ void __launch_bounds__(64) k_rot_points(RotGeom g, const RotTable* table,
-                                                   const Rect* masks, const int32_t* mask_active,
-                                                   int count, int max_scan, RotScratch R) {
+// ---- k_rot_points: the points of every left/right line --------------------
+// The reference builds a line by the float recurrence X_{i+1} = fl(X_i + s)
+// (deskew.c:107-112).  While X stays inside one binade [2^(E-1), 2^E) the
+// rounding of X_i + s to the binade's ulp u is X_i + round_u(s) -- the same
+// increment d every step, unless s/u is a half-integer (a tie, decided by
+// parity) -- so X_i = T + k*d exactly for a whole run of steps, whose length
+// follows from integer arithmetic in units of u.  Lane 0 of a wave splits its
+// line into such segments (an explicit float step at each binade change);
+// all 64 lanes then write the points in parallel.  A tie, |X| < 1 or too many
+// segments make lane 0 replay the recurrence itself.
+constexpr int kMaxSegs = 16;
+struct PointSeg {
+  int32_t i0, n;     // points i0 .. i0 + n
+  double T, du;      // |X_i0| and the increment d (exact doubles)
+  float sign;
+};
+
+__global__ void __launch_bounds__(256) k_rot_points(RotGeom g, const RotTable* table,
+                                                    const Rect* masks, const int32_t* mask_active,
+                                                    int count, int max_scan, RotScratch R) {
   const int na = table->nangles;
   const int nlines = count * g.nedges * na;
-  const int t0 = blockIdx.x * 64, t = t0 + threadIdx.x;
-  __shared__ int32_t tile[64][65];
-  bool live = t < nlines;
-  int a = 0, e = 0, s = 0;
-  if (live) {
-    a = t % na;
-    e = (t / na) % g.nedges;
-    s = t / (na * g.nedges);
-    live = !(mask_active && !mask_active[s]) && g.edge_shift[e][1] == 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int t = blockIdx.x * 4 + w;
+  if (t >= nlines) return;
+  __shared__ PointSeg segs[4][kMaxSegs];
+  __shared__ int32_t nseg_s[4];
+  const int a = t % na, e = (t / na) % g.nedges, s = t / (na * g.nedges);
+  const bool live = !(mask_active && !mask_active[s]) && g.edge_shift[e][1] == 0;
+  if (!live) {
+    if (lane == 0) {
+      R.ends[2 * t] = 0;
+      R.ends[2 * t + 1] = 0;
+      R.flag[t] = 1;
+      R.state[4 * t + 3] = 0;
+    }
+    return;
   }
-  LineSetup L{0, 0, 0.0f, 0.0f, 0.0f, 0.0f};
-  if (live) L = line_setup(masks[s], g, g.edge_shift[e][0], 0, table->slope[a]);
-  const int scan = live ? L.scan : 0;
-  float X = L.X;
-  int first = 0, last = 0;
-  // 64 points per round go through the LDS tile so that each line's points
-  // are written as one contiguous run
-  int maxscan_blk = scan;
-  for (int o = 32; o > 0; o >>= 1) maxscan_blk = max(maxscan_blk, __shfl_xor(maxscan_blk, o, 64));
-  for (int c0 = 0; c0 < maxscan_blk; c0 += 64) {
-    for (int j = 0; j < 64; j++) {
-      const int i = c0 + j;
-      if (i < scan) {
-        const int x = (int)X;
-        tile[threadIdx.x][j] = x;
-        if (i == 0) first = x;
-        last = x;
-        X += L.stepX;
+  const LineSetup L = line_setup(masks[s], g, g.edge_shift[e][0], 0, table->slope[a]);
+  const int scan = L.scan;
+  int32_t* cols = R.cols + (int64_t)t * max_scan;
+  if (lane == 0) {
+    int ns = 0;
+    bool ok = scan > 0;
+    float X = L.X;
+    const float st = L.stepX;
+    int i = 0;
+    while (ok) {
+      if (!(fabsf(X) >= 1.0f) || ns >= kMaxSegs) {
+        ok = false;
+        break;
+      }
+      const float sign = X > 0.0f ? 1.0f : -1.0f;
+      const double T = (double)fabsf(X), sig = (double)st * (double)sign;
+      int E;
+      frexpf(fabsf(X), &E);  // |X| = m * 2^E, m in [0.5, 1)
+      const double lo = ldexp(1.0, E - 1), hi = ldexp(1.0, E), u = ldexp(1.0, E - 24);
+      const double q = sig / u;  // exact: u is a power of two
+      const double fqd = floor(q);
+      if (q - fqd == 0.5) {      // a tie: the increment alternates
+        ok = false;
+        break;
+      }
+      const int64_t fq = (int64_t)fqd, dq = (int64_t)floor(q + 0.5);
+      const int64_t H = (int64_t)((hi - T) / u), G = (int64_t)((T - lo) / u);
+      const int64_t rem = scan - 1 - i;  // steps still to take
+      // steps k = 1.. whose exact sum X_{k-1} + s stays in [lo, hi)
+      int64_t nn;
+      if (dq > 0) {
+        const int64_t c = H - fq - 1;
+        nn = c >= 0 ? c / dq + 1 : 0;
+      } else if (dq < 0) {
+        const int64_t c = G + fq;
+        nn = c >= 0 ? c / (-dq) + 1 : 0;
+      } else {
+        nn = (q >= 0.0 || G >= 1) ? rem : 0;
+      }
+      if (nn > rem) nn = rem;
+      segs[w][ns] = PointSeg{i, (int32_t)nn, T, (double)dq * u, sign};
+      ns++;
+      i += (int)nn;
+      if (i >= scan - 1) break;
+      // one explicit step across the binade change
+      X = sign * (float)(T + (double)nn * ((double)dq * u)) + st;
+      i++;
+      if (i == scan - 1) {  // the last point alone
+        if (!(fabsf(X) >= 1.0f) || ns >= kMaxSegs) {
+          ok = false;
+          break;
+        }
+        segs[w][ns++] = PointSeg{i, 0, (double)fabsf(X), 0.0, X > 0.0f ? 1.0f : -1.0f};
+        break;
       }
     }
-    __syncthreads();
-    for (int l = 0; l < 64; l++) {
-      const int tl = t0 + l;
-      if (tl >= nlines) break;
-      const int i = c0 + threadIdx.x;
-      if (i < max_scan) R.cols[(int64_t)tl * max_scan + i] = tile[l][threadIdx.x];
+    if (!ok) {
+      // the literal recurrence
+      float Xr = L.X;
+      for (int k = 0; k < scan; k++) {
+        cols[k] = (int)Xr;
+        Xr += st;
+      }
+      ns = -1;
     }
-    __syncthreads();
+    nseg_s[w] = ns;
   }
-  if (t < nlines) {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  const int ns = nseg_s[w];
+  if (ns > 0) {
+    for (int q = 0; q < ns; q++) {
+      const PointSeg sg = segs[w][q];
+      for (int k = lane; k <= sg.n; k += 64)
+        cols[sg.i0 + k] = (int)((double)sg.sign * (sg.T + (double)k * sg.du));
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) {
+    int first = 0, last = 0;
+    if (scan > 0) {
+      if (ns > 0) {
+        const PointSeg s0 = segs[w][0], s1 = segs[w][ns - 1];
+        first = (int)((double)s0.sign * s0.T);
+        last = (int)((double)s1.sign * (s1.T + (double)s1.n * s1.du));
+      } else {
+        first = cols[0];
+        last = cols[scan - 1];
+      }
+    }
     R.ends[2 * t] = first;
     R.ends[2 * t + 1] = last;
-    R.flag[t] = live ? 0 : 1;
+    R.flag[t] = 0;
     R.state[4 * t + 3] = 0;
   }
 }
@@ -479,7 +562,7 @@ void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable
   if (g.nedges <= 0 || nangles <= 0) return;
   const int nlines = count * g.nedges * nangles;
   const RotScratch R = rot_scratch(lines, nlines, max_scan);
-  hipLaunchKernelGGL(k_rot_points, dim3((nlines + 63) / 64), dim3(64), 0, st, g, table, masks,
+  hipLaunchKernelGGL(k_rot_points, dim3((nlines + 3) / 4), dim3(256), 0, st, g, table, masks,
                      mask_active, count, max_scan, R);
   switch (img.P.fmt) {
     case F_GRAY8:
