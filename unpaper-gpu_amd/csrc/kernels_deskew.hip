@@ -122,14 +122,15 @@ size_t rotation_lines_bytes(int count, int nedges, int nangles, int max_scan) {
 // ---- k_rot_points: the points of every left/right line --------------------
 // The reference builds a line by the float recurrence X_{i+1} = fl(X_i + s)
 // (deskew.c:107-112).  While X stays inside one binade [2^(E-1), 2^E) the
-// rounding of X_i + s to the binade's ulp u is X_i + round_u(s) -- the same
-// increment d every step, unless s/u is a half-integer (a tie, decided by
-// parity) -- so X_i = T + k*d exactly for a whole run of steps, whose length
-// follows from integer arithmetic in units of u.  Lane 0 of a wave splits its
-// line into such segments (an explicit float step at each binade change);
-// all 64 lanes then write the points in parallel.  A tie, |X| < 1 or too many
-// segments make lane 0 replay the recurrence itself.
-constexpr int kMaxSegs = 16;
+// rounding of X_i + s to the binade's ulp u is X_i + round_u(s): the same
+// increment d every step (for a tie, s/u a half-integer, the even multiple
+// wins, constant from an even X_i/u on), so X_i = T + k*d exactly for a whole
+// run of steps, whose length follows from integer arithmetic in units of u.
+// Lane 0 of a wave splits its line into such segments, with one explicit
+// float step at each binade change, odd-tie start or X = 0; all 64 lanes then
+// write the points in parallel.  Beyond kMaxSegs segments lane 0 replays the
+// rest of the recurrence itself.
+constexpr int kMaxSegs = 64;
 struct PointSeg {
   int32_t i0, n;     // points i0 .. i0 + n
   double T, du;      // |X_i0| and the increment d (exact doubles)
@@ -145,7 +146,7 @@ __global__ void __launch_bounds__(256) k_rot_points(RotGeom g, const RotTable* t
   const int t = blockIdx.x * 4 + w;
   if (t >= nlines) return;
   __shared__ PointSeg segs[4][kMaxSegs];
-  __shared__ int32_t nseg_s[4];
+  __shared__ int32_t nseg_s[4], last_s[4];
   const int a = t % na, e = (t / na) % g.nedges, s = t / (na * g.nedges);
   const bool live = !(mask_active && !mask_active[s]) && g.edge_shift[e][1] == 0;
   if (!live) {
@@ -161,68 +162,64 @@ __global__ void __launch_bounds__(256) k_rot_points(RotGeom g, const RotTable* t
   const int scan = L.scan;
   int32_t* cols = R.cols + (int64_t)t * max_scan;
   if (lane == 0) {
-    int ns = 0;
-    bool ok = scan > 0;
+    int ns = 0, last = 0;
     float X = L.X;
     const float st = L.stepX;
     int i = 0;
-    while (ok) {
-      if (!(fabsf(X) >= 1.0f) || ns >= kMaxSegs) {
-        ok = false;
+    while (scan > 0) {
+      if (ns >= kMaxSegs) {
+        // the literal recurrence for the remaining points
+        for (int k = i; k < scan; k++) {
+          cols[k] = last = (int)X;
+          X += st;
+        }
         break;
       }
       const float sign = X > 0.0f ? 1.0f : -1.0f;
       const double T = (double)fabsf(X), sig = (double)st * (double)sign;
-      int E;
-      frexpf(fabsf(X), &E);  // |X| = m * 2^E, m in [0.5, 1)
-      const double lo = ldexp(1.0, E - 1), hi = ldexp(1.0, E), u = ldexp(1.0, E - 24);
-      const double q = sig / u;  // exact: u is a power of two
-      const double fqd = floor(q);
-      if (q - fqd == 0.5) {      // a tie: the increment alternates
-        ok = false;
-        break;
-      }
-      const int64_t fq = (int64_t)fqd, dq = (int64_t)floor(q + 0.5);
-      const int64_t H = (int64_t)((hi - T) / u), G = (int64_t)((T - lo) / u);
-      const int64_t rem = scan - 1 - i;  // steps still to take
-      // steps k = 1.. whose exact sum X_{k-1} + s stays in [lo, hi)
-      int64_t nn;
-      if (dq > 0) {
-        const int64_t c = H - fq - 1;
-        nn = c >= 0 ? c / dq + 1 : 0;
-      } else if (dq < 0) {
-        const int64_t c = G + fq;
-        nn = c >= 0 ? c / (-dq) + 1 : 0;
-      } else {
-        nn = (q >= 0.0 || G >= 1) ? rem : 0;
-      }
-      if (nn > rem) nn = rem;
-      segs[w][ns] = PointSeg{i, (int32_t)nn, T, (double)dq * u, sign};
-      ns++;
-      i += (int)nn;
-      if (i >= scan - 1) break;
-      // one explicit step across the binade change
-      X = sign * (float)(T + (double)nn * ((double)dq * u)) + st;
-      i++;
-      if (i == scan - 1) {  // the last point alone
-        if (!(fabsf(X) >= 1.0f) || ns >= kMaxSegs) {
-          ok = false;
-          break;
+      int64_t nn = 0;
+      double du = 0.0;
+      if (X != 0.0f) {
+        int E;
+        frexpf(fabsf(X), &E);  // |X| = m * 2^E, m in [0.5, 1)
+        const double lo = ldexp(1.0, E - 1), hi = ldexp(1.0, E), u = ldexp(1.0, E - 24);
+        const double q = sig / u;  // exact: u is a power of two
+        const double fqd = floor(q);
+        const int64_t fq = (int64_t)fqd;
+        // A tie (q = fq + 1/2) rounds to the even multiple of u: from an even
+        // |X|/u the increment is then always the even one of fq, fq + 1; from
+        // an odd one, one explicit step first.
+        const bool tie = q - fqd == 0.5;
+        if (!tie || !(((int64_t)(T / u)) & 1)) {
+          const int64_t dq = tie ? (fq & 1 ? fq + 1 : fq) : (int64_t)floor(q + 0.5);
+          const int64_t H = (int64_t)((hi - T) / u), G = (int64_t)((T - lo) / u);
+          const int64_t rem = scan - 1 - i;  // steps still to take
+          // steps k = 1.. whose exact sum X_{k-1} + s stays in [lo, hi)
+          if (dq > 0) {
+            const int64_t c = H - fq - 1;
+            nn = c >= 0 ? c / dq + 1 : 0;
+          } else if (dq < 0) {
+            const int64_t c = G + fq;
+            nn = c >= 0 ? c / (-dq) + 1 : 0;
+          } else {
+            nn = (q >= 0.0 || G >= 1) ? rem : 0;
+          }
+          if (nn > rem) nn = rem;
+          du = (double)dq * u;
         }
-        segs[w][ns++] = PointSeg{i, 0, (double)fabsf(X), 0.0, X > 0.0f ? 1.0f : -1.0f};
+      }
+      segs[w][ns++] = PointSeg{i, (int32_t)nn, T, du, sign};
+      i += (int)nn;
+      if (i >= scan - 1) {
+        last = (int)((double)sign * (T + (double)nn * du));
         break;
       }
-    }
-    if (!ok) {
-      // the literal recurrence
-      float Xr = L.X;
-      for (int k = 0; k < scan; k++) {
-        cols[k] = (int)Xr;
-        Xr += st;
-      }
-      ns = -1;
+      // one explicit step (binade change, tie or zero)
+      X = sign * (float)(T + (double)nn * du) + st;
+      i++;
     }
     nseg_s[w] = ns;
+    last_s[w] = last;
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   __builtin_amdgcn_wave_barrier();
@@ -239,14 +236,8 @@ __global__ void __launch_bounds__(256) k_rot_points(RotGeom g, const RotTable* t
   if (lane == 0) {
     int first = 0, last = 0;
     if (scan > 0) {
-      if (ns > 0) {
-        const PointSeg s0 = segs[w][0], s1 = segs[w][ns - 1];
-        first = (int)((double)s0.sign * s0.T);
-        last = (int)((double)s1.sign * (s1.T + (double)s1.n * s1.du));
-      } else {
-        first = cols[0];
-        last = cols[scan - 1];
-      }
+      first = (int)L.X;  // point 0 is the start value itself
+      last = last_s[w];
     }
     R.ends[2 * t] = first;
     R.ends[2 * t + 1] = last;
