@@ -9,11 +9,12 @@
 // the angle: point i sits on row Ystart+i for every angle, only its column
 // (int)X_i differs.  So all angles and the first kDepth steps read one band
 // of columns beside the mask edge.  The fast path is
-//   k_rot_points  the float recurrence X += -m of every line, in order
-//                 (deskew.c:107-112), one lane per line -> column lists;
-//   k_rot_band    one workgroup per 128-row slice of a (sheet, edge): the
-//                 slice's band is staged in LDS as per-pixel blackness, then
-//                 every angle x kDepth steps is summed from LDS -> partials;
+//   k_rot_points  the float recurrence X += -m of every line (deskew.c:
+//                 107-112) in closed form per binade -> column lists;
+//   k_rot_band_g  one workgroup per 128-row slice of a (sheet, edge): the
+//                 slice's band is staged in LDS as per-column prefix sums of
+//                 the blackness, then every angle x kDepth steps is summed
+//                 run by run (two prefix entries per run) -> partials;
 //   k_rot_final   one wave per line: slice partials -> blackness per step,
 //                 then the reference's stopping rule and peak, exactly.
 // Lines that do not stop within kDepth steps, top/bottom edges (rows move
@@ -264,10 +265,14 @@ __device__ __forceinline__ bool band_range(const RotScratch& R, int tbase, int n
 }
 
 // ---- k_rot_band: slice sums of every angle x kDepth steps -----------------
-template <int FMT>
-__global__ void __launch_bounds__(256) k_rot_band(PlaneRef img, RotGeom g, const RotTable* table,
-                                                  const Rect* masks, const int32_t* mask_active,
-                                                  int count, int max_scan, RotScratch R) {
+// Along a slice a line's column changes only where (int)X steps, so it is a
+// few vertical runs (1 + 128*|m| at most).  The slice's band is staged as
+// per-column prefix sums over its rows (16-bit: 128 * 255 fits), and every
+// (angle, depth) sum is a difference of two prefix entries per run.
+constexpr int kBandThreads = 512;
+__global__ void __launch_bounds__(kBandThreads)
+    k_rot_band_g(PlaneRef img, RotGeom g, const RotTable* table, const Rect* masks,
+                 const int32_t* mask_active, int count, int max_scan, RotScratch R, int fmt) {
   const int sl = blockIdx.x, e = blockIdx.y, s = blockIdx.z;
   const int na = table->nangles;
   const int sxh = g.edge_shift[e][0];
@@ -279,51 +284,118 @@ __global__ void __launch_bounds__(256) k_rot_band(PlaneRef img, RotGeom g, const
   const int tbase = (s * g.nedges + e) * na;
   int32_t bx0, bw;
   if (!band_range(R, tbase, na, sxh, &bx0, &bw)) return;  // k_rot_final flags the lines
-  __shared__ uint8_t band[kBandBytes];
+  // pre[r * bw + c]: blackness of rows 0..r of column c; the raw bytes are
+  // staged first in the upper half
+  __shared__ uint16_t pre[kSliceRows * (kBandBytes / kSliceRows)];
+  uint8_t* raw = reinterpret_cast<uint8_t*>(pre) + kSliceRows * bw;
   const Rect nm = normalize(mask);
   const int32_t xlo = imax(nm.x0, 0), xhi = imin(nm.x1, g.W - 1);
   const int32_t ylo = imax(nm.y0, 0), yhi = imin(nm.y1, g.H - 1);
   const int32_t ystart = (int32_t)LS.Y;  // exact: integer start, +1.0 per point
   const uint8_t* base = plane_ptr(img, s);
   const int rows = i1 - i0, n = rows * bw;
-  // stage blackness 255-max(rgb) of in-mask, in-image pixels (0 elsewhere,
+  // blackness 255-max(rgb) of in-mask, in-image pixels (0 elsewhere,
   // get_pixel's white); unconditional clamped loads, masked arithmetically
-  for (int b0 = 0; b0 < n; b0 += 8 * 256) {
+  for (int b0 = 0; b0 < n; b0 += 8 * kBandThreads) {
     uint8_t v[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-      const int q = b0 + k * 256 + threadIdx.x;
+      const int q = b0 + k * kBandThreads + threadIdx.x;
       const int r = q / bw, c = q - r * bw;
       const int32_t y = ystart + i0 + r, x = bx0 + c;
       const bool ok = (q < n) & (y >= ylo) & (y <= yhi) & (x >= xlo) & (x <= xhi);
-      const Px p = load_px_row<FMT>(base + (int64_t)(ok ? y : ylo) * img.P.pitch, ok ? x : xlo);
-      v[k] = (uint8_t)((255 - dark_of(p)) & -(int)ok);
+      const int64_t ro = (int64_t)(ok ? y : ylo) * img.P.pitch;
+      const int32_t xo = ok ? x : xlo;
+      uint32_t d;
+      if (fmt == F_GRAY8) d = base[ro + xo];
+      else if (fmt == F_Y400A) d = base[ro + 2 * xo];
+      else d = dark_of(load_px_row<F_RGB24>(base + ro, xo));
+      v[k] = (uint8_t)((255 - d) & -(int)ok);
     }
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-      const int q = b0 + k * 256 + threadIdx.x;
-      if (q < n) band[q] = v[k];
+      const int q = b0 + k * kBandThreads + threadIdx.x;
+      if (q < n) raw[q] = v[k];
+    }
+  }
+  __syncthreads();
+  // column prefix sums: one thread per column, the column read out first
+  uint32_t colv[kSliceRows / 4];
+  const int c = threadIdx.x;
+  if (c < bw) {
+#pragma unroll
+    for (int k = 0; k < kSliceRows / 4; k++) {
+      uint32_t wv = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int r = 4 * k + j;
+        wv |= (r < rows ? (uint32_t)raw[r * bw + c] : 0u) << (8 * j);
+      }
+      colv[k] = wv;
+    }
+  }
+  __syncthreads();
+  if (c < bw) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < kSliceRows / 4; k++) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        acc += (colv[k] >> (8 * j)) & 0xFFu;
+        if (4 * k + j < rows) pre[(4 * k + j) * bw + c] = (uint16_t)acc;
+      }
     }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int d0 = lane, d1 = lane + 64;
-  const int32_t o0 = sxh * d0 - bx0, o1 = sxh * d1 - bx0;
+  constexpr int nw = kBandThreads / 64;
+  const int32_t o0 = sxh * lane - bx0, o1 = sxh * (lane + 64) - bx0;
   const int ns = rot_slices(max_scan);
-  for (int a = w; a < na; a += 4) {
+  for (int a = w; a < na; a += nw) {
     const int t = tbase + a;
-    const int32_t* cols = R.cols + (int64_t)t * max_scan;
+    const int32_t* cols = R.cols + (int64_t)t * max_scan + i0;
+    // the slice's columns, two rows per lane; run starts by ballot
+    const int32_t cA = lane < rows ? cols[lane] : 0;
+    const int32_t cB = lane + 64 < rows ? cols[lane + 64] : 0;
+    const int32_t upA = __shfl_up(cA, 1, 64), upB = __shfl_up(cB, 1, 64);
+    const int32_t lastA = __builtin_amdgcn_readlane(cA, 63);
+    const bool stA = lane < rows && (lane == 0 || upA != cA);
+    const bool stB = lane + 64 < rows && (lane == 0 ? lastA != cB : upB != cB);
+    unsigned long long MA = __ballot(stA), MB = __ballot(stB);
     int acc0 = 0, acc1 = 0;
-    const uint8_t* row = band;
-#pragma unroll 8
-    for (int i = i0; i < i1; i++, row += bw) {
-      const int32_t x = cols[i];  // uniform
-      acc0 += row[x + o0];
-      acc1 += row[x + o1];
+    int rs = 0;
+    int32_t x = __builtin_amdgcn_readlane(cA, 0);
+    MA &= MA - 1;  // row 0 starts the first run
+    for (;;) {
+      int re;  // end (exclusive) of the run starting at rs
+      int32_t nx = 0;
+      if (MA) {
+        re = __ffsll((long long)MA) - 1;
+        nx = __builtin_amdgcn_readlane(cA, re);
+        MA &= MA - 1;
+      } else if (MB) {
+        const int b = __ffsll((long long)MB) - 1;
+        re = 64 + b;
+        nx = __builtin_amdgcn_readlane(cB, b);
+        MB &= MB - 1;
+      } else {
+        re = rows;
+      }
+      const uint16_t* pe = pre + (re - 1) * bw + x;
+      acc0 += pe[o0];
+      acc1 += pe[o1];
+      if (rs > 0) {
+        const uint16_t* ps = pre + (rs - 1) * bw + x;
+        acc0 -= ps[o0];
+        acc1 -= ps[o1];
+      }
+      if (re >= rows) break;
+      rs = re;
+      x = nx;
     }
     int32_t* P = R.part + ((int64_t)t * ns + sl) * kDepth;
-    P[d0] = acc0;
-    P[d1] = acc1;
+    P[lane] = acc0;
+    P[lane + 64] = acc1;
   }
 }
 
@@ -533,8 +605,9 @@ static void launch_rot_t(const PlaneRef& img, const RotGeom& g, const RotTable* 
                          const Rect* masks, const int32_t* mask_active, int mask_index,
                          int32_t* peaks, int count, hipStream_t st, int nangles, int max_scan,
                          const RotScratch& R) {
-  hipLaunchKernelGGL(k_rot_band<FMT>, dim3(rot_slices(max_scan), g.nedges, count), dim3(256), 0,
-                     st, img, g, table, masks, mask_active, count, max_scan, R);
+  hipLaunchKernelGGL(k_rot_band_g, dim3(rot_slices(max_scan), g.nedges, count),
+                     dim3(kBandThreads), 0, st, img, g, table, masks, mask_active, count, max_scan,
+                     R, (int)FMT);
   const int nlines = count * g.nedges * nangles;
   hipLaunchKernelGGL(k_rot_final, dim3((nlines + 3) / 4), dim3(256), 0, st, g, table, masks,
                      mask_active, mask_index, peaks, count, max_scan, R);
