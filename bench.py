@@ -57,7 +57,7 @@ STAGE_PLANES = {
 
 
 ROOFLINE_STAGE = "deskew_rotate"
-ROOFLINE_KERNEL = "k_rotate_cubic_g8"
+ROOFLINE_KERNEL = "k_rotate_cubic_g8f"
 
 
 def parse():
@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC HBM bytes per stage launch from a rocprofv3 --pmc pass")
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
+    ap.add_argument("--probe", type=int, default=3,
+                    help="isolated single-stream launches after the timed region that time "
+                         "the roofline kernel (0 = use the concurrent timed-region spans)")
     ap.add_argument("--sweep", default="",
                     help="tuning only: comma list of BATCHxSTREAMS, each timed over one step "
                          "and printed to stderr before the main run")
@@ -251,15 +254,28 @@ def main():
         # bracket exactly that launch); the one-wave/one-block sequential
         # replays are latency bound and overlap other streams' work
         dom = ROOFLINE_STAGE if ROOFLINE_STAGE in totals else max(totals, key=totals.get)
-        avg_ms = totals[dom] / max(nlaunch, 1)
-        alg = STAGE_PLANES.get(dom, 1.0) * W * H * (npages * args.steps / max(nlaunch, 1))
+        # In the timed region `streams` batches share the GPU, so one launch's
+        # event span is stretched by the kernels of the other streams.  The
+        # kernel's own duration comes from probe launches right after the
+        # timed region: the same batch shape on one stream with the GPU
+        # otherwise idle (HIP events on that stream).
+        conc_ms = totals[dom] / max(nlaunch, 1)
+        n0 = chunks[0][1]
+        probe = []
+        for _ in range(args.probe):
+            batches[0].run_device(n0, pages.ptr, pitch, stride)
+            batches[0].wait()
+            probe.append(sum(ms for name, ms in batches[0].stage_times() if name == dom))
+        avg_ms = sum(probe) / len(probe) if probe else conc_ms
+        units = n0 if probe else npages * args.steps / max(nlaunch, 1)
+        alg = STAGE_PLANES.get(dom, 1.0) * W * H * units
         achieved = alg / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         traffic = None
         try:  # HBM bytes per page from the committed rocprofv3 --pmc passes
             with open(args.traffic) as f:
                 per_page = json.load(f).get("bytes_per_page", {}).get(dom)
             if per_page:
-                traffic = int(per_page * npages * args.steps / max(nlaunch, 1))
+                traffic = int(per_page * units)
         except (OSError, ValueError):
             pass
         roofline = {
@@ -267,6 +283,9 @@ def main():
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": ROOFLINE_KERNEL if dom == ROOFLINE_STAGE else dom,
             "alg_bytes_per_launch": int(alg), "avg_launch_ms": round(avg_ms, 3),
+            "launch_ms_from": ("%d isolated probe launches of %d sheets" % (len(probe), n0)
+                               if probe else "timed region"),
+            "concurrent_avg_launch_ms": round(conc_ms, 3),
             "pipeline_frac": round(pages_per_s / max(d.world, 1) * ALG_BYTES_PER_PAGE /
                                    (HBM_PEAK_GBS * 1e9), 5),
         }

@@ -2,9 +2,14 @@
 """Summarise a rocprofv3 --kernel-trace --stats CSV directory.
 
 usage: summarize.py <rocprofv3 output dir or *_kernel_stats.csv> [launches]
+                    [--last KERNEL K]
 
 Prints kernels by total time; with `launches` (batch launches in the traced
 run) also the per-launch average of each kernel and of the whole pipeline.
+With --last, also the average duration of the last K dispatches of KERNEL
+from the per-dispatch trace (*kernel_trace.csv): bench.py's isolated probe
+launches of the roofline kernel run after everything else, so this is the
+rocprof figure to set next to bench.py's `roofline.avg_launch_ms`.
 """
 import csv
 import glob
@@ -15,8 +20,9 @@ import sys
 def load(path):
     """Rows {Name, Calls, TotalDurationNs} from a stats CSV or a rocpd database."""
     if os.path.isdir(path):
-        found = glob.glob(os.path.join(path, "*kernel_stats.csv"))
-        path = found[0] if found else glob.glob(os.path.join(path, "*.db"))[0]
+        found = glob.glob(os.path.join(path, "**", "*kernel_stats.csv"), recursive=True)
+        path = found[0] if found else glob.glob(os.path.join(path, "**", "*.db"),
+                                                recursive=True)[0]
     if path.endswith(".db"):
         import sqlite3
         con = sqlite3.connect(path)
@@ -28,9 +34,26 @@ def load(path):
         return list(csv.DictReader(f))
 
 
+def last_dispatches(path, kernel, k):
+    """Durations (us) of the last k dispatches of `kernel` in start order."""
+    found = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)
+    if not found:
+        return []
+    with open(found[0]) as f:
+        rows = [r for r in csv.DictReader(f) if kernel in r.get("Kernel_Name", "")]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    return [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows[-k:]]
+
+
 def main():
-    rows = load(sys.argv[1])
-    launches = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    argv = sys.argv[1:]
+    last = None
+    if "--last" in argv:
+        i = argv.index("--last")
+        last = (argv[i + 1], int(argv[i + 2]))
+        del argv[i:i + 3]
+    rows = load(argv[0])
+    launches = int(argv[1]) if len(argv) > 1 else 0
     total = sum(float(r["TotalDurationNs"]) for r in rows if "k_synth" not in r["Name"])
     print("%-64s %6s %12s %10s %7s" % ("kernel", "calls", "total_us", "avg_us", "share"))
     for r in rows:
@@ -41,6 +64,11 @@ def main():
     if launches:
         print("pipeline kernels per batch launch: %.3f ms (input generation excluded)"
               % (total / 1e6 / launches))
+    if last and os.path.isdir(argv[0]):
+        d = last_dispatches(argv[0], *last)
+        if d:
+            print("last %d dispatches of %s: %s us, average %.1f us"
+                  % (len(d), last[0], " ".join("%.1f" % v for v in d), sum(d) / len(d)))
 
 
 if __name__ == "__main__":

@@ -208,4 +208,19 @@ inline int diag_skip() {
   return v;
 }
 
+// Timing diagnostics: UPHIP_DIAG_DOUBLE bit mask of idempotent full-chip
+// kernels launched twice, so that the throughput drop under the multi-stream
+// load measures each kernel's marginal cost (1 rotation band, 2 rotate,
+// 4 mask move, 8 decode copy, 16 rotation points, 32 gray cells,
+// 64 blur counts, 128 rotation final + line walk).
+inline int diag_double() {
+  static const int v = getenv("UPHIP_DIAG_DOUBLE") ? atoi(getenv("UPHIP_DIAG_DOUBLE")) : 0;
+  return v;
+}
+#define UPH_LAUNCH_DIAG(bit, ...)                              \
+  do {                                                         \
+    hipLaunchKernelGGL(__VA_ARGS__);                           \
+    if (::uph::diag_double() & (bit)) hipLaunchKernelGGL(__VA_ARGS__); \
+  } while (0)
+
 }  // namespace uph

@@ -73,8 +73,10 @@ void launch_stretch(const PlaneRef& src, const PlaneRef& dst, int interp, int co
                     hipStream_t st);
 void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* args,
                       int count, hipStream_t st);
+// max_abs_angle bounds |rotation| of every active sheet (sizes the staged
+// source window; tiles whose window does not fit take a slower exact path).
 void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
-                        int interp, int count, hipStream_t st);
+                        int interp, int count, hipStream_t st, float max_abs_angle);
 // Flip `cur` of every sheet whose args[s].active (int at byte offset) is set.
 void launch_flip_if_active(SheetCtl* ctl, const int32_t* active, int64_t stride_bytes,
                            int count, hipStream_t st);

@@ -190,7 +190,7 @@ void launch_copy_thr(const PlaneRef& src, const PlaneRef& dst, const CopyArgs* a
                      int rows_hint, uint8_t thr, hipStream_t st) {
   CopyLaunch L{src, dst, args, thr};
   int gx = rows_hint < 1 ? 1 : (rows_hint > 1024 ? 1024 : rows_hint);
-  hipLaunchKernelGGL(k_copy, dim3(gx, 1, count), dim3(kThreads), 0, st, L);
+  UPH_LAUNCH_DIAG(8, k_copy, dim3(gx, 1, count), dim3(kThreads), 0, st, L);
 }
 
 void launch_copy(const PlaneRef& src, const PlaneRef& dst, const CopyArgs* args, int count,
@@ -615,8 +615,8 @@ void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* 
   if (src.P.fmt == F_GRAY8) {
     // one wave per row, about two rows per wave
     const int64_t blocks = (src.P.H + 2 * (kThreads / 64) - 1) / (2 * (kThreads / 64));
-    hipLaunchKernelGGL(k_move_rect_g16, dim3((unsigned)(blocks < 1 ? 1 : blocks), 1, count),
-                       dim3(kThreads), 0, st, src, dst, args);
+    UPH_LAUNCH_DIAG(4, k_move_rect_g16, dim3((unsigned)(blocks < 1 ? 1 : blocks), 1, count),
+                    dim3(kThreads), 0, st, src, dst, args);
   } else if (src.P.fmt == F_Y400A) {
     hipLaunchKernelGGL(k_move_rect<F_Y400A>, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst,
                        args);
@@ -1158,13 +1158,349 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_g8(PlaneRef src, Plan
   }
 }
 
+// ---------------------------------------------------------------------------
+// deskew rotate, GRAY8 + bicubic, float window (the default pipeline's
+// dominant kernel).  128 x 48 output tiles; the tile's source window is
+// staged once as fp32 (one conversion per staged byte instead of one per
+// tap), so the taps of a pixel come straight out of LDS in the pairs the
+// packed FP32 ops consume:
+//   * a lane owns output columns tx0+lane and tx0+64+lane (A, B); the row
+//     cubics of one pixel run two tap rows at a time, each tap pair (row r,
+//     row r+1) one ds_read2_b32 at offsets (k, kRFS+k);
+//   * the vertical cubic runs A and B as one packed pair;
+//   * lanes read consecutive columns (a wave whose pixels straddle a row
+//     boundary meets at most two-way bank conflicts);
+//   * all-white stretches of a tile row (the page background) are detected
+//     from per-row non-white masks built while staging and skip the math;
+//   * each wave buffers its six output rows in LDS and stores them 8 bytes
+//     per lane at the end (no global load after a store).
+// Every rounding operation of cubic_scale (interpolate.c:24-31) stays a
+// separate multiply or add in the reference's order, as in cubic2.
+// ---------------------------------------------------------------------------
+constexpr int kRFW = 128;   // output columns per tile (2 per lane)
+constexpr int kRFH = 48;    // output rows per tile (6 per wave)
+constexpr int kRFS = 144;   // staged row stride in floats (>= 141-float window rows at 5 deg)
+constexpr int kRFT = 512;   // threads per tile: 8 waves, kRFH / 8 consecutive rows each
+constexpr int kRFWaves = kRFT / 64;
+
+// The 16 taps of pixels A and B as row pairs: t[p][j] = {tap row 2q, tap row
+// 2q+1} of column j for p = 2*pixel + q.  a[p] is the LDS byte address of
+// (column 0, row 2q).  One ds_read2_b32 per pair (offsets k and kRFS + k,
+// which the compiler would instead merge as k, k+1 and then shuffle), all 16
+// in flight before the one wait.
+#define UPH_TAP_PAIR(o, b, k) \
+  "ds_read2_b32 %" #o ", %" #b " offset0:" #k " offset1:" UPH_STR(UPH_ROWOFF_##k) "\n\t"
+#define UPH_STR2(x) #x
+#define UPH_STR(x) UPH_STR2(x)
+#define UPH_ROWOFF_0 144
+#define UPH_ROWOFF_1 145
+#define UPH_ROWOFF_2 146
+#define UPH_ROWOFF_3 147
+static_assert(kRFS == 144, "tap pair offsets are spelled out for a 144-float row stride");
+__device__ __forceinline__ void lds_taps16(const uint32_t (&a)[4], f2 (&t)[4][4]) {
+  asm volatile(UPH_TAP_PAIR(0, 16, 0) UPH_TAP_PAIR(1, 16, 1) UPH_TAP_PAIR(2, 16, 2)
+               UPH_TAP_PAIR(3, 16, 3) UPH_TAP_PAIR(4, 17, 0) UPH_TAP_PAIR(5, 17, 1)
+               UPH_TAP_PAIR(6, 17, 2) UPH_TAP_PAIR(7, 17, 3) UPH_TAP_PAIR(8, 18, 0)
+               UPH_TAP_PAIR(9, 18, 1) UPH_TAP_PAIR(10, 18, 2) UPH_TAP_PAIR(11, 18, 3)
+               UPH_TAP_PAIR(12, 19, 0) UPH_TAP_PAIR(13, 19, 1) UPH_TAP_PAIR(14, 19, 2)
+               UPH_TAP_PAIR(15, 19, 3) "s_waitcnt lgkmcnt(0)"
+               : "=&v"(t[0][0]), "=&v"(t[0][1]), "=&v"(t[0][2]), "=&v"(t[0][3]),
+                 "=&v"(t[1][0]), "=&v"(t[1][1]), "=&v"(t[1][2]), "=&v"(t[1][3]),
+                 "=&v"(t[2][0]), "=&v"(t[2][1]), "=&v"(t[2][2]), "=&v"(t[2][3]),
+                 "=&v"(t[3][0]), "=&v"(t[3][1]), "=&v"(t[3][2]), "=&v"(t[3][3])
+               : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3])
+               : "memory");
+}
+
+// cubic2 on four independent pairs, step by step, so the dependent packed
+// operations of one chain interleave with the others' (no wait states).
+__device__ __forceinline__ void cubic2x4(const f2 (&f)[4], const f2 (&h)[4],
+                                         const f2 (&t)[4][4], f2 (&out)[4]) {
+  f2 ba[4], ca[4], da[4], s1[4], s2[4], u[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    ba[i] = t[i][1] - t[i][0];
+    ca[i] = t[i][2] - t[i][0];
+    da[i] = t[i][3] - t[i][0];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) s1[i] = fma2(splat2(4.0f), ca[i], -da[i]);                // exact
+#pragma unroll
+  for (int i = 0; i < 4; i++) s2[i] = ba[i] - ca[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) s1[i] = fma2(splat2(-5.0f), ba[i], s1[i]);                // exact
+#pragma unroll
+  for (int i = 0; i < 4; i++) s2[i] = fma2(splat2(3.0f), s2[i], da[i]);                 // exact
+#pragma unroll
+  for (int i = 0; i < 4; i++) u[i] = f[i] * s2[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) u[i] = s1[i] + u[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) u[i] = f[i] * u[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) u[i] = ca[i] + u[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) u[i] = h[i] * u[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) u[i] = t[i][1] + u[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    out[i] = f2{__builtin_amdgcn_fmed3f(__builtin_truncf(u[i].x), 0.0f, 255.0f),
+                __builtin_amdgcn_fmed3f(__builtin_truncf(u[i].y), 0.0f, 255.0f)};
+}
+
+__global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRef dst,
+                                                               const RotateArgs* args,
+                                                               int max_rows, int diag) {
+  // dynamic LDS: window [max_rows][kRFS] floats, nw[max_rows] u64, then one
+  // (kRFH / 8) x kRFW byte output buffer per wave
+  extern __shared__ float winf[];
+  int txi, tyi, s;
+  xcd_block(&txi, &tyi, &s);
+  const RotateArgs a = args[s];
+  if (!a.active) return;
+  const Planes& P = src.P;
+  const uint8_t* sbase = plane_ptr(src, s);
+  uint8_t* dbase = plane_ptr(dst, s);
+  const Rect nm = normalize(a.mask);
+  const int32_t sw = nm.x1 - nm.x0 + 1, sh = nm.y1 - nm.y0 + 1;
+  const float scx = nm.x0 + sw / 2.0f, scy = nm.y0 + sh / 2.0f;  // primitives.c:137-145
+  const float tcx = 0 + sw / 2.0f, tcy = 0 + sh / 2.0f;
+  const int32_t tx0 = txi * kRFW, ty0 = tyi * kRFH;
+  const int32_t u0 = imax(tx0, 0) - a.mask.x0, u1 = imin(tx0 + kRFW, P.W) - 1 - a.mask.x0;
+  const int32_t v0 = imax(ty0, 0) - a.mask.y0, v1 = imin(ty0 + kRFH, P.H) - 1 - a.mask.y0;
+  const int32_t cu0 = imax(u0, 0), cu1 = imin(u1, sw - 1);
+  const int32_t cv0 = imax(v0, 0), cv1 = imin(v1, sh - 1);
+  if (!(cu0 <= cu1 && cv0 <= cv1)) {
+    // no pixel of the tile inside the mask: copied unchanged (deskew.c:268-286)
+    const int cb = 8 * (threadIdx.x & 15);
+    const int32_t x = tx0 + cb;
+    for (int r = threadIdx.x >> 4; r < kRFH; r += kRFT / 16) {
+      const int32_t y = ty0 + r;
+      if (y >= P.H || x >= P.W) continue;
+      const uint8_t* sp = sbase + (int64_t)y * P.pitch + x;
+      uint8_t* dp = dbase + (int64_t)y * P.pitch + x;
+      if (x + 8 <= P.W) *reinterpret_cast<uint64_t*>(dp) = *reinterpret_cast<const uint64_t*>(sp);
+      else for (int j = 0; x + j < P.W; j++) dp[j] = sp[j];
+    }
+    return;
+  }
+  // source window of the tile's in-mask pixels (their 4x4 taps included)
+  int32_t bx0 = 0, by0 = 0, bw = 0, bh = 0;
+  {
+    float mnx = 3.0e38f, mxx = -3.0e38f, mny = 3.0e38f, mxy = -3.0e38f;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int32_t u = c & 1 ? cu1 : cu0, v = c & 2 ? cv1 : cv0;
+      const float X = scx + (u - tcx) * a.cosval + (v - tcy) * a.sinval;
+      const float Y = scy + (v - tcy) * a.cosval - (u - tcx) * a.sinval;
+      mnx = fminf(mnx, X);
+      mxx = fmaxf(mxx, X);
+      mny = fminf(mny, Y);
+      mxy = fmaxf(mxy, Y);
+    }
+    // every pixel's coordinate lies between the corners' (the same float
+    // expression, monotone in u and v); its taps span (int)c - 1 .. (int)c + 2,
+    // and (int)c <= floor(c) + 1 (truncation of negatives)
+    bx0 = (int32_t)floorf(mnx) - 1;
+    by0 = (int32_t)floorf(mny) - 1;
+    bw = (int32_t)floorf(mxx) + 3 - bx0 + 1;
+    bh = (int32_t)floorf(mxy) + 3 - by0 + 1;
+  }
+  const int32_t xa = bx0 >= 0 ? (bx0 & ~3) : -((-bx0 + 3) & ~3);  // window start, dword aligned
+  const int nd = (bx0 - xa + bw + 3) >> 2;                         // source dwords per row
+  const bool staged = bw > 0 && bh > 0 && 4 * nd <= kRFS && bh <= max_rows;
+  uint64_t* nw = reinterpret_cast<uint64_t*>(winf + kRFS * max_rows);
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* obuf = reinterpret_cast<uint8_t*>(nw + max_rows) + wu * (kRFH / kRFWaves * kRFW);
+  if (staged && !(diag & 1024)) {
+    // a wave stages whole rows (lane = source dword), four in flight; nw[r]
+    // bit j: dword j of window row r holds a non-white pixel
+    const int32_t xd = xa + 4 * lane;
+    const bool colv = lane < nd;
+    const bool edge = (xd < 0) | (xd + 3 >= P.W);
+    const int32_t xc = imin(imax(xd, 0), (int32_t)P.pitch - 4);
+    for (int r0 = 4 * wu; r0 < bh; r0 += 4 * kRFWaves) {
+      uint32_t v[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int32_t y = by0 + r0 + q;
+        const uint8_t* row = sbase + (int64_t)imin(imax(y, 0), P.H - 1) * P.pitch;
+        v[q] = colv ? *reinterpret_cast<const uint32_t*>(row + xc) : 0xFFFFFFFFu;
+        if ((y < 0) | (y >= P.H)) v[q] = 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int r = r0 + q;
+        if (r >= bh) break;  // uniform
+        const int32_t y = by0 + r;
+        uint32_t w4 = v[q];
+        if (colv & edge & (y >= 0) & (y < P.H)) {
+          // a dword across the image edge: white outside, bytes inside
+          const uint8_t* row = sbase + (int64_t)y * P.pitch;
+          w4 = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const int32_t x = xd + k;
+            const uint32_t b = (x >= 0 && x < P.W) ? row[x] : 255u;
+            w4 |= b << (8 * k);
+          }
+        }
+        const unsigned long long m = __ballot(w4 != 0xFFFFFFFFu);
+        if (lane == 0) nw[r] = m;
+        if (colv)
+          *reinterpret_cast<float4*>(winf + r * kRFS + 4 * lane) =
+              make_float4(ubyte_f<0>(w4), ubyte_f<1>(w4), ubyte_f<2>(w4), ubyte_f<3>(w4));
+      }
+    }
+  }
+  __syncthreads();
+  const int32_t xA = tx0 + lane, xB = xA + 64;
+  const bool hasA = xA < P.W, hasB = xB < P.W;
+  // per-lane terms of the source coordinates (constant down the column):
+  //   srcX = (scx + (u - tcx) cos) + (v - tcy) sin
+  //   srcY = (scy + (v - tcy) cos) - (u - tcx) sin
+  const int32_t uA = xA - a.mask.x0, uB = xB - a.mask.x0;
+  const float cuA = uA - tcx, cuB = uB - tcx;
+  const float axA = scx + cuA * a.cosval, bsA = cuA * a.sinval;
+  const float axB = scx + cuB * a.cosval, bsB = cuB * a.sinval;
+  const bool colA = hasA & (uA >= 0) & (uA < sw), colB = hasB & (uB >= 0) & (uB < sw);
+  const int base_off = (-1 - by0) * kRFS - 1 - xa;  // tap (ix-1, iy-1) = winf[base_off + iy*S + ix]
+  typedef __attribute__((address_space(3))) float lds_f32;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_f32*)winf;  // LDS byte address of winf
+  const Src<F_GRAY8> S{sbase, P.pitch, P.W, P.H};
+  // Source coordinates are monotone along a row, so the taps of all 128
+  // columns of a tile row lie between those of its end columns (computed
+  // with the same expressions, wave-uniform).  When every tap there is white
+  // (255) the bicubic result is exactly 255: all differences are zero, so
+  // each cubic_scale returns b + (+-0) = b.
+  const float cuL = (tx0 - a.mask.x0) - tcx, cuR = (tx0 + kRFW - 1 - a.mask.x0) - tcx;
+  const float axL = scx + cuL * a.cosval, bsL = cuL * a.sinval;
+  const float axR = scx + cuR * a.cosval, bsR = cuR * a.sinval;
+  constexpr int kRows = kRFH / kRFWaves;            // rows per wave
+  const int32_t yw = ty0 + wu * kRows;              // the wave's rows: yw .. yw + kRows-1
+  // Outside the mask a pixel is copied unchanged (deskew.c:268-286).  Those
+  // source bytes are read into the wave's output buffer first: on gfx9 a
+  // wait for a load also waits for every earlier store, so no global load
+  // may follow the first store.  Tiles wholly inside the mask skip this.
+  // The wave's output rows move through obuf with one mapping for loads and
+  // stores: lane -> row k0 + lane/16, bytes 8*(lane%16), k0 = 0, 4.
+  const int cb = 8 * (lane & 15);
+  const int32_t xo = tx0 + cb;
+  const bool partial = !(cu0 == u0 && cu1 == u1 && cv0 == v0 && cv1 == v1);
+  if (partial) {
+    uint64_t q[2] = {0, 0};
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int rr = 4 * h + (lane >> 4);
+      const int32_t y = imin(yw + rr, P.H - 1);
+      const int32_t x = imin(xo, (int32_t)P.pitch - 8);  // rows are 256-byte pitched
+      if (rr < kRows) q[h] = *reinterpret_cast<const uint64_t*>(sbase + (int64_t)y * P.pitch + x);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int rr = 4 * h + (lane >> 4);
+      if (rr < kRows) *reinterpret_cast<uint64_t*>(obuf + rr * kRFW + cb) = q[h];
+    }
+  }
+#pragma unroll 2
+  for (int k = 0; k < kRows; k++) {
+    const int32_t y = yw + k;
+    const int32_t v = y - a.mask.y0;
+    const bool rowin = (v >= 0) & (v < sh) & (y < P.H);
+    const float cv = v - tcy;
+    const float VS = cv * a.sinval, VC = scy + cv * a.cosval;
+    const bool inA = rowin & colA, inB = rowin & colB;
+    uint32_t oA = 255, oB = 255;
+    bool white = true;
+    if (staged) {
+      const int32_t xl = (int)(axL + VS), xr = (int)(axR + VS);
+      const int32_t yl = (int)(VC - bsL), yr = (int)(VC - bsR);
+      const int32_t c0 = imax((imin(xl, xr) - 1 - xa) >> 2, 0);
+      const int32_t c1 = imin((imax(xl, xr) + 2 - xa) >> 2, nd - 1);
+      const int32_t r0 = imax(imin(yl, yr) - 1 - by0, 0);
+      const int32_t r1 = imin(imax(yl, yr) + 2 - by0, bh - 1);
+      // one window row per lane, then one ballot (instead of a scalar loop
+      // over the rows with an LDS round trip each)
+      const uint64_t cm = c1 >= c0 ? ((2ull << c1) - 1ull) & ~((1ull << c0) - 1ull) : 0ull;
+      bool any = false;
+      for (int rb = r0; rb <= r1; rb += 64) {  // one pass unless |angle| is large
+        const int r = rb + lane;
+        any |= __ballot(r <= r1 && (nw[imin(r, r1)] & cm) != 0) != 0;
+      }
+      white = (!any && !(diag & 2048)) || (diag & 512);
+    }
+    if (!white && staged) {
+      const float sxA = axA + VS, syA = VC - bsA, sxB = axB + VS, syB = VC - bsB;
+      const int ixA = (int)sxA, iyA = (int)syA, ixB = (int)sxB, iyB = (int)syB;  // truncation
+      const float fxA = sxA - ixA, fyA = syA - iyA, fxB = sxB - ixB, fyB = syB - iyB;
+      const uint32_t pA = 4u * (uint32_t)(inA ? base_off + iyA * kRFS + ixA : 0);
+      const uint32_t pB = 4u * (uint32_t)(inB ? base_off + iyB * kRFS + ixB : 0);
+      const uint32_t ta[4] = {lds0 + pA, lds0 + pA + 8 * kRFS, lds0 + pB, lds0 + pB + 8 * kRFS};
+      f2 t[4][4];
+      lds_taps16(ta, t);
+      // rows (0,1) and (2,3) of A, then of B: four packed row cubics
+      const f2 FA = splat2(fxA), HA = splat2(0.5f * fxA);
+      const f2 FB = splat2(fxB), HB = splat2(0.5f * fxB);
+      const f2 F[4] = {FA, FA, FB, FB}, Hh[4] = {HA, HA, HB, HB};
+      f2 c[4];
+      cubic2x4(F, Hh, t, c);
+      // the column cubic of A and B as one pair
+      const f2 o = cubic2(f2{fyA, fyB}, f2{0.5f * fyA, 0.5f * fyB}, f2{c[0].x, c[2].x},
+                          f2{c[0].y, c[2].y}, f2{c[1].x, c[3].x}, f2{c[1].y, c[3].y});
+      oA = (uint32_t)o.x;  // integer-valued in [0, 255]
+      oB = (uint32_t)o.y;
+    } else if (!staged) {
+      // window too large for LDS (large angles): taps from the frame
+      if (inA) oA = interp_bicubic(S, axA + VS, VC - bsA).r;
+      if (inB) oB = interp_bicubic(S, axB + VS, VC - bsB).r;
+    }
+    if (inA) obuf[k * kRFW + lane] = (uint8_t)oA;
+    if (inB) obuf[k * kRFW + 64 + lane] = (uint8_t)oB;
+  }
+  // the wave's rows as 8-byte stores: lane -> row k0 + lane/16, bytes
+  // 8*(lane%16).  One wave's LDS operations complete in order, so its reads
+  // see its writes without a fence.
+  __builtin_amdgcn_wave_barrier();
+  for (int k0 = 0; k0 < kRows; k0 += 4) {
+    const int rr = k0 + (lane >> 4);
+    const int32_t y = yw + rr, x = xo;
+    if (rr < kRows && y < P.H && x < P.W) {
+      const uint64_t q = *reinterpret_cast<const uint64_t*>(obuf + rr * kRFW + cb);
+      uint8_t* d = dbase + (int64_t)y * P.pitch + x;
+      if (x + 8 <= P.W) {
+        *reinterpret_cast<uint64_t*>(d) = q;
+      } else {
+        for (int j = 0; x + j < P.W; j++) d[j] = (uint8_t)(q >> (8 * j));
+      }
+    }
+  }
+}
+
+// Rows of source window a kRFW x kRFH tile needs at rotations up to |angle|.
+static int rotate_window_rows(float max_abs_angle) {
+  const float a = fminf(fabsf(max_abs_angle), 1.5707964f);
+  // (kRFH-1) cos + (kRFW-1) sin rows of pixel centres, + 3 tap rows, + 2 for
+  // the floor/truncation slack of the window bounds
+  return kRFH + (int)ceilf((kRFW - 1) * sinf(a)) + 5;
+}
+
 void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
-                        int interp, int count, hipStream_t st) {
+                        int interp, int count, hipStream_t st, float max_abs_angle) {
   const dim3 grid((src.P.W + kRotTW - 1) / kRotTW, (src.P.H + kRotTH - 1) / kRotTH, count);
   const dim3 ggrid((src.P.W + kRotTW - 1) / kRotTW, (src.P.H + kRotGH - 1) / kRotGH, count);
   if (interp == UPHIP_INTERP_CUBIC && src.P.fmt == F_GRAY8) {
+    const int rows = rotate_window_rows(max_abs_angle);
+    const size_t lds = (sizeof(float) * kRFS + sizeof(uint64_t)) * (size_t)rows + kRFH * kRFW;
+    if (lds <= 56 * 1024 && !(diag_double() & 256)) {
+      const dim3 fgrid((src.P.W + kRFW - 1) / kRFW, (src.P.H + kRFH - 1) / kRFH, count);
+      UPH_LAUNCH_DIAG(2, k_rotate_cubic_g8f, fgrid, dim3(kRFT), lds, st, src, dst, args, rows,
+                      diag_double() & (512 | 1024 | 2048));
+      return;
+    }
     const dim3 qgrid((src.P.W + kRQW - 1) / kRQW, (src.P.H + kRQH - 1) / kRQH, count);
-    hipLaunchKernelGGL(k_rotate_cubic_g8, qgrid, dim3(kThreads), 0, st, src, dst, args);
+    UPH_LAUNCH_DIAG(2, k_rotate_cubic_g8, qgrid, dim3(kThreads), 0, st, src, dst, args);
     return;
   }
   if (interp == UPHIP_INTERP_CUBIC && src.P.fmt == F_Y400A) {

@@ -605,18 +605,18 @@ static void launch_rot_t(const PlaneRef& img, const RotGeom& g, const RotTable* 
                          const Rect* masks, const int32_t* mask_active, int mask_index,
                          int32_t* peaks, int count, hipStream_t st, int nangles, int max_scan,
                          const RotScratch& R) {
-  hipLaunchKernelGGL(k_rot_band_g, dim3(rot_slices(max_scan), g.nedges, count),
-                     dim3(kBandThreads), 0, st, img, g, table, masks, mask_active, count, max_scan,
-                     R, (int)FMT);
+  UPH_LAUNCH_DIAG(1, k_rot_band_g, dim3(rot_slices(max_scan), g.nedges, count),
+                  dim3(kBandThreads), 0, st, img, g, table, masks, mask_active, count, max_scan, R,
+                  (int)FMT);
   const int nlines = count * g.nedges * nangles;
-  hipLaunchKernelGGL(k_rot_final, dim3((nlines + 3) / 4), dim3(256), 0, st, g, table, masks,
-                     mask_active, mask_index, peaks, count, max_scan, R);
+  UPH_LAUNCH_DIAG(128, k_rot_final, dim3((nlines + 3) / 4), dim3(256), 0, st, g, table, masks,
+                  mask_active, mask_index, peaks, count, max_scan, R);
   const size_t lds = sizeof(int32_t) * 2 * (size_t)(max_scan > 0 ? max_scan : 1);
   if (lds > 64 * 1024)
     hipFuncSetAttribute((const void*)k_rot_line<FMT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)lds);
-  hipLaunchKernelGGL(k_rot_line<FMT>, dim3(imin(nlines, 1024)), dim3(256), lds, st, img, g, table,
-                     masks, mask_active, mask_index, peaks, count, max_scan, R);
+  UPH_LAUNCH_DIAG(128, k_rot_line<FMT>, dim3(imin(nlines, 1024)), dim3(256), lds, st, img, g,
+                  table, masks, mask_active, mask_index, peaks, count, max_scan, R);
 }
 
 void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable* table,
@@ -626,8 +626,8 @@ void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable
   if (g.nedges <= 0 || nangles <= 0) return;
   const int nlines = count * g.nedges * nangles;
   const RotScratch R = rot_scratch(lines, nlines, max_scan);
-  hipLaunchKernelGGL(k_rot_points, dim3((nlines + 3) / 4), dim3(256), 0, st, g, table, masks,
-                     mask_active, count, max_scan, R);
+  UPH_LAUNCH_DIAG(16, k_rot_points, dim3((nlines + 3) / 4), dim3(256), 0, st, g, table, masks,
+                  mask_active, count, max_scan, R);
   switch (img.P.fmt) {
     case F_GRAY8:
       launch_rot_t<F_GRAY8>(img, g, table, masks, mask_active, mask_index, peaks, count, st,

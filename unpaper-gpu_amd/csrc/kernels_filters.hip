@@ -324,8 +324,8 @@ static void launch_gray_t(const PlaneRef& img, const GrayGeom& g, uint8_t* scr, 
                           const int32_t* active, int count, hipStream_t st) {
   dim3 grid((g.ncx + 255) / 256, g.ncy, count);
   if (FMT == F_GRAY8 && g.W <= kGrayStripMaxW && g.ch <= 257)
-    hipLaunchKernelGGL(k_gray_cells_g, dim3(g.ncy, 1, count), dim3(256),
-                       4 * (size_t)((g.W + 3) & ~3), st, img, g, scr, ss, active);
+    UPH_LAUNCH_DIAG(32, k_gray_cells_g, dim3(g.ncy, 1, count), dim3(256),
+                    4 * (size_t)((g.W + 3) & ~3), st, img, g, scr, ss, active);
   else
     hipLaunchKernelGGL(k_gray_cells<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active);
   const int32_t ntiles = g.ntx * g.nty;
@@ -531,8 +531,8 @@ template <int FMT>
 static void launch_blur_t(const PlaneRef& img, const BlurGeom& g, uint8_t* scr, int64_t ss,
                           const int32_t* active, int count, hipStream_t st) {
   if (g.nrect > 0 && FMT == F_GRAY8 && g.sh <= 65535 && g.W <= (1 << 16))
-    hipLaunchKernelGGL(k_blur_counts_g, dim3(1 + g.T, count), dim3(256),
-                       2 * (size_t)((g.W + 3) & ~3), st, img, g, scr, ss, active);
+    UPH_LAUNCH_DIAG(64, k_blur_counts_g, dim3(1 + g.T, count), dim3(256),
+                    2 * (size_t)((g.W + 3) & ~3), st, img, g, scr, ss, active);
   else if (g.nrect > 0)
     hipLaunchKernelGGL(k_blur_counts<FMT>, dim3(g.nrect, count), dim3(256), 0, st, img, g, scr, ss,
                        active);

@@ -546,7 +546,7 @@ void uphip_deskew(UphipImage source, UphipRectangle mask, float radians,
   if (!n) return;
   RotateArgs* d = stage_args(&a, 1, st);
   if (!d) return;
-  launch_rotate_mask(ref_of(f), ref_of(n), d, interp, 1, st);
+  launch_rotate_mask(ref_of(f), ref_of(n), d, interp, 1, st, radians);
   arg_fence(st);
   adopt_storage(f, n);
 }

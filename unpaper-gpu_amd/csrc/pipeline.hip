@@ -317,6 +317,7 @@ struct UphipBatch {
   RotTable* dtable = nullptr;
   RotCombo* dcombo = nullptr;
   int max_scan = 0;
+  float max_angle = 0.0f;  // largest |angle| of the scan table (rotation bound)
   int32_t* peaks = nullptr;
   int32_t* rot_lines = nullptr;  // scan-line point lists (k_rot_points)
   Rect* pick_mask = nullptr;
@@ -638,6 +639,7 @@ static bool allocate(UphipBatch* b) {
     if (rotation_angles(o.deskew_parameters, &b->table) < 0)
       return fail("batch: too many deskew angles");
     const int na = b->table.nangles;
+    for (int i = 0; i < na; i++) b->max_angle = fmaxf(b->max_angle, fabsf(b->table.angle[i]));
     b->dtable = dalloc<RotTable>(b, 1);
     UPH_HIP(hipMemcpy(b->dtable, &b->table, sizeof(RotTable), hipMemcpyHostToDevice));
     int nedges = 0;
@@ -1070,8 +1072,9 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
       hipLaunchKernelGGL(k_rot_select, dim3((count + 255) / 256), dim3(256), 0, b->st, b->ctl,
                          b->peaks, b->dtable, b->dcombo, ra, b->rot_args, count);
       mark(b, "deskew_detect");
+      // rotations are angles of the scan table, |angle| <= scan range
       launch_rotate_mask(cur_ref(P, b->ctl), other_ref(P, b->ctl), b->rot_args,
-                         o.interpolate_type, count, b->st);
+                         o.interpolate_type, count, b->st, b->max_angle);
       mark(b, "deskew_rotate");  // brackets exactly the rotation kernel
       launch_flip_if_active(b->ctl, &b->rot_args->active, sizeof(RotateArgs), count, b->st);
     }
