@@ -1254,7 +1254,7 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
                                                                int max_rows, int diag) {
   // dynamic LDS: window [max_rows][kRFS] floats, nw[max_rows] u64, then one
   // (kRFH / 8) x kRFW byte output buffer per wave
-  extern __shared__ float winf[];
+  extern __shared__ __attribute__((aligned(16))) float winf[];
   int txi, tyi, s;
   xcd_block(&txi, &tyi, &s);
   const RotateArgs a = args[s];
@@ -1317,36 +1317,34 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
   if (staged && !(diag & 1024)) {
     // a wave stages whole rows (lane = source dword), four in flight; nw[r]
     // bit j: dword j of window row r holds a non-white pixel
+    // Branch-free: every lane loads the dword at its address clamped into the
+    // row; a dword across an image edge is then realigned by a shift and its
+    // bytes outside [0, W) made white.
     const int32_t xd = xa + 4 * lane;
     const bool colv = lane < nd;
-    const bool edge = (xd < 0) | (xd + 3 >= P.W);
     const int32_t xc = imin(imax(xd, 0), (int32_t)P.pitch - 4);
+    // realignment as one 64-bit shift: (v << 24) >> (24 + 8 (xd - xc)); with
+    // |xd - xc| >= 4 every byte is outside anyway
+    const int fsh = imin(imax(24 + 8 * (xd - xc), 0), 56);
+    uint32_t outside = colv ? 0u : 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (xd + k < 0 || xd + k >= P.W) outside |= 0xFFu << (8 * k);
     for (int r0 = 4 * wu; r0 < bh; r0 += 4 * kRFWaves) {
       uint32_t v[4];
 #pragma unroll
       for (int q = 0; q < 4; q++) {
-        const int32_t y = by0 + r0 + q;
-        const uint8_t* row = sbase + (int64_t)imin(imax(y, 0), P.H - 1) * P.pitch;
-        v[q] = colv ? *reinterpret_cast<const uint32_t*>(row + xc) : 0xFFFFFFFFu;
-        if ((y < 0) | (y >= P.H)) v[q] = 0xFFFFFFFFu;
+        const int32_t y = imin(imax(by0 + r0 + q, 0), P.H - 1);
+        v[q] = *reinterpret_cast<const uint32_t*>(sbase + (int64_t)y * P.pitch + xc);
       }
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int r = r0 + q;
         if (r >= bh) break;  // uniform
         const int32_t y = by0 + r;
-        uint32_t w4 = v[q];
-        if (colv & edge & (y >= 0) & (y < P.H)) {
-          // a dword across the image edge: white outside, bytes inside
-          const uint8_t* row = sbase + (int64_t)y * P.pitch;
-          w4 = 0;
-#pragma unroll
-          for (int k = 0; k < 4; k++) {
-            const int32_t x = xd + k;
-            const uint32_t b = (x >= 0 && x < P.W) ? row[x] : 255u;
-            w4 |= b << (8 * k);
-          }
-        }
+        uint32_t w4 = (uint32_t)(((uint64_t)v[q] << 24) >> fsh);
+        w4 |= outside;
+        if ((y < 0) | (y >= P.H)) w4 = 0xFFFFFFFFu;
         const unsigned long long m = __ballot(w4 != 0xFFFFFFFFu);
         if (lane == 0) nw[r] = m;
         if (colv)
@@ -1424,11 +1422,10 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
       // one window row per lane, then one ballot (instead of a scalar loop
       // over the rows with an LDS round trip each)
       const uint64_t cm = c1 >= c0 ? ((2ull << c1) - 1ull) & ~((1ull << c0) - 1ull) : 0ull;
-      bool any = false;
-      for (int rb = r0; rb <= r1; rb += 64) {  // one pass unless |angle| is large
-        const int r = rb + lane;
-        any |= __ballot(r <= r1 && (nw[imin(r, r1)] & cm) != 0) != 0;
-      }
+      // (lanes past r1 re-read r1, which leaves the OR unchanged)
+      bool any = r0 <= r1 && __ballot((nw[imax(imin(r0 + lane, r1), 0)] & cm) != 0) != 0;
+      for (int rb = r0 + 64; rb <= r1; rb += 64)  // only when |angle| is large
+        any |= __ballot((nw[imin(rb + lane, r1)] & cm) != 0) != 0;
       white = (!any && !(diag & 2048)) || (diag & 512);
     }
     if (!white && staged) {
