@@ -159,6 +159,25 @@ __device__ __forceinline__ void xcd_block(int* bx, int* by, int* bz) {
   *bx = rem - *by * gx;
 }
 
+// xcd_block with its two divisions by host-computed reciprocals
+// m = floor((2^32 - 1) / d) + 1 (exact for n * d < 2^32; m = 0 marks d = 1).
+inline uint32_t div_magic(uint32_t d) { return d > 1 ? (uint32_t)(0xFFFFFFFFull / d + 1) : 0u; }
+__device__ __forceinline__ int div_by_magic(int n, uint32_t m) {
+  return m ? (int)__umulhi((uint32_t)n, m) : n;
+}
+__device__ __forceinline__ void xcd_block_m(uint32_t m_gxy, uint32_t m_gx, int* bx, int* by,
+                                            int* bz) {
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int nblk = gx * gy * gridDim.z;
+  const int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int q = nblk >> 3, rr = nblk & 7, xcd = lin & 7;
+  const int t = xcd * q + (xcd < rr ? xcd : rr) + (lin >> 3);
+  *bz = div_by_magic(t, m_gxy);
+  const int rem = t - *bz * gx * gy;
+  *by = div_by_magic(rem, m_gx);
+  *bx = rem - *by * gx;
+}
+
 // ---------------------------------------------------------------------------
 // A batch of frames of identical geometry and format.  Frame s of plane k is
 // base[k] + s*stride.  For single-image ops stride = 0 and count = 1.

@@ -1251,12 +1251,13 @@ __device__ __forceinline__ void cubic2x4(const f2 (&f)[4], const f2 (&h)[4],
 
 __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRef dst,
                                                                const RotateArgs* args,
-                                                               int max_rows, int diag) {
+                                                               int max_rows, int diag,
+                                                               uint32_t m_gxy, uint32_t m_gx) {
   // dynamic LDS: window [max_rows][kRFS] floats, nw[max_rows] u64, then one
   // (kRFH / 8) x kRFW byte output buffer per wave
   extern __shared__ __attribute__((aligned(16))) float winf[];
   int txi, tyi, s;
-  xcd_block(&txi, &tyi, &s);
+  xcd_block_m(m_gxy, m_gx, &txi, &tyi, &s);
   const RotateArgs a = args[s];
   if (!a.active) return;
   const Planes& P = src.P;
@@ -1364,7 +1365,6 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
   const float axA = scx + cuA * a.cosval, bsA = cuA * a.sinval;
   const float axB = scx + cuB * a.cosval, bsB = cuB * a.sinval;
   const bool colA = hasA & (uA >= 0) & (uA < sw), colB = hasB & (uB >= 0) & (uB < sw);
-  const int base_off = (-1 - by0) * kRFS - 1 - xa;  // tap (ix-1, iy-1) = winf[base_off + iy*S + ix]
   typedef __attribute__((address_space(3))) float lds_f32;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_f32*)winf;  // LDS byte address of winf
   const Src<F_GRAY8> S{sbase, P.pitch, P.W, P.H};
@@ -1432,8 +1432,9 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
       const float sxA = axA + VS, syA = VC - bsA, sxB = axB + VS, syB = VC - bsB;
       const int ixA = (int)sxA, iyA = (int)syA, ixB = (int)sxB, iyB = (int)syB;  // truncation
       const float fxA = sxA - ixA, fyA = syA - iyA, fxB = sxB - ixB, fyB = syB - iyB;
-      const uint32_t pA = 4u * (uint32_t)(inA ? base_off + iyA * kRFS + ixA : 0);
-      const uint32_t pB = 4u * (uint32_t)(inB ? base_off + iyB * kRFS + ixB : 0);
+      // window row index times the stride as a full-rate 24-bit multiply
+      const uint32_t pA = 4u * (uint32_t)(inA ? __mul24(iyA - 1 - by0, kRFS) + ixA - 1 - xa : 0);
+      const uint32_t pB = 4u * (uint32_t)(inB ? __mul24(iyB - 1 - by0, kRFS) + ixB - 1 - xa : 0);
       const uint32_t ta[4] = {lds0 + pA, lds0 + pA + 8 * kRFS, lds0 + pB, lds0 + pB + 8 * kRFS};
       f2 t[4][4];
       lds_taps16(ta, t);
@@ -1493,7 +1494,8 @@ void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateAr
     if (lds <= 56 * 1024 && !(diag_double() & 256)) {
       const dim3 fgrid((src.P.W + kRFW - 1) / kRFW, (src.P.H + kRFH - 1) / kRFH, count);
       UPH_LAUNCH_DIAG(2, k_rotate_cubic_g8f, fgrid, dim3(kRFT), lds, st, src, dst, args, rows,
-                      diag_double() & (512 | 1024 | 2048));
+                      diag_double() & (512 | 1024 | 2048), div_magic(fgrid.x * fgrid.y),
+                      div_magic(fgrid.x));
       return;
     }
     const dim3 qgrid((src.P.W + kRQW - 1) / kRQW, (src.P.H + kRQH - 1) / kRQH, count);
