@@ -38,7 +38,14 @@ def last_dispatches(path, kernel, k):
     """Durations (us) of the last k dispatches of `kernel` in start order."""
     found = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)
     if not found:
-        return []
+        dbs = glob.glob(os.path.join(path, "**", "*.db"), recursive=True)
+        if not dbs:
+            return []
+        import sqlite3
+        con = sqlite3.connect(dbs[0])
+        rows = con.execute("select start, end from kernels where name like ? order by start",
+                           ("%" + kernel + "%",)).fetchall()
+        return [(e - s) / 1e3 for s, e in rows[-k:]]
     with open(found[0]) as f:
         rows = [r for r in csv.DictReader(f) if kernel in r.get("Kernel_Name", "")]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
