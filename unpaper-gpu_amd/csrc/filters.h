@@ -99,7 +99,7 @@ struct RotGeom {
 void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable* table,
                            const Rect* masks, const int32_t* mask_active, int mask_index,
                            int32_t* peaks, int count, hipStream_t st, int nangles, int max_scan,
-                           int32_t* lines);
+                           int32_t* lines, float max_abs_angle);
 // Scratch for the scan-line point lists of one launch_rotation_peaks call.
 size_t rotation_lines_bytes(int count, int nedges, int nangles, int max_scan);
 // Per-line fallback flags inside that scratch (diagnostics).

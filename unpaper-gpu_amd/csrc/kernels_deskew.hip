@@ -29,7 +29,7 @@ namespace uph {
 
 constexpr int kDepth = 128;        // steps covered by the band path (2 per lane)
 constexpr int kSliceRows = 128;    // rows per band slice
-constexpr int kBandBytes = 48 * 1024;
+constexpr int kBandCapMax = 384;   // band columns at most (LDS: 256 bytes per column)
 
 __device__ __forceinline__ int iwave_prefix_excl(int v, int* total) {
   const int lane = threadIdx.x & 63;
@@ -250,7 +250,7 @@ __global__ void __launch_bounds__(256) k_rot_points(RotGeom g, const RotTable* t
 // Band of one (sheet, edge): columns [bx0, bx0 + bw) cover every point of
 // every angle for steps 0..kDepth-1.  Returns false when it does not fit.
 __device__ __forceinline__ bool band_range(const RotScratch& R, int tbase, int na, int sxh,
-                                           int32_t* bx0, int32_t* bw) {
+                                           int band_cap, int32_t* bx0, int32_t* bw) {
   int32_t lo = INT_MAX, hi = INT_MIN;
   for (int a = 0; a < na; a++) {
     const int32_t f = R.ends[2 * (tbase + a)], l = R.ends[2 * (tbase + a) + 1];
@@ -261,7 +261,7 @@ __device__ __forceinline__ bool band_range(const RotScratch& R, int tbase, int n
   else lo -= kDepth - 1;
   *bx0 = lo;
   *bw = hi - lo + 1;
-  return (int64_t)*bw * kSliceRows <= kBandBytes;
+  return *bw <= band_cap;
 }
 
 // ---- k_rot_band: slice sums of every angle x kDepth steps -----------------
@@ -270,9 +270,10 @@ __device__ __forceinline__ bool band_range(const RotScratch& R, int tbase, int n
 // per-column prefix sums over its rows (16-bit: 128 * 255 fits), and every
 // (angle, depth) sum is a difference of two prefix entries per run.
 constexpr int kBandThreads = 512;
-__global__ void __launch_bounds__(kBandThreads)
+__global__ void __launch_bounds__(kBandThreads, 4)
     k_rot_band_g(PlaneRef img, RotGeom g, const RotTable* table, const Rect* masks,
-                 const int32_t* mask_active, int count, int max_scan, RotScratch R, int fmt) {
+                 const int32_t* mask_active, int count, int max_scan, RotScratch R, int fmt,
+                 int band_cap) {
   const int sl = blockIdx.x, e = blockIdx.y, s = blockIdx.z;
   const int na = table->nangles;
   const int sxh = g.edge_shift[e][0];
@@ -283,10 +284,12 @@ __global__ void __launch_bounds__(kBandThreads)
   if (i0 >= i1) return;
   const int tbase = (s * g.nedges + e) * na;
   int32_t bx0, bw;
-  if (!band_range(R, tbase, na, sxh, &bx0, &bw)) return;  // k_rot_final flags the lines
+  if (!band_range(R, tbase, na, sxh, band_cap, &bx0, &bw)) return;  // k_rot_final flags the lines
   // pre[r * bw + c]: blackness of rows 0..r of column c; the raw bytes are
   // staged first in the upper half
-  __shared__ uint16_t pre[kSliceRows * (kBandBytes / kSliceRows)];
+  // dynamic LDS: kSliceRows * band_cap entries (the launch sizes band_cap
+  // from the angle range, so two slices fit a CU at the default range)
+  extern __shared__ __attribute__((aligned(16))) uint16_t pre[];
   uint8_t* raw = reinterpret_cast<uint8_t*>(pre) + kSliceRows * bw;
   const Rect nm = normalize(mask);
   const int32_t xlo = imax(nm.x0, 0), xhi = imin(nm.x1, g.W - 1);
@@ -319,30 +322,36 @@ __global__ void __launch_bounds__(kBandThreads)
     }
   }
   __syncthreads();
-  // column prefix sums: one thread per column, the column read out first
-  uint32_t colv[kSliceRows / 4];
+  // column prefix sums: one thread per column, 32 rows at a time.  Prefix
+  // row r (bytes [2 r bw, 2 r bw + 2 bw)) overwrites raw rows 2r-128 and
+  // 2r-127 only, which every thread has read by then: each chunk is read
+  // out before the barrier and written after it.
   const int c = threadIdx.x;
-  if (c < bw) {
+  uint32_t acc = 0;
+  for (int k0 = 0; k0 < kSliceRows; k0 += 32) {
+    uint32_t colv[8];
+    if (c < bw) {
 #pragma unroll
-    for (int k = 0; k < kSliceRows / 4; k++) {
-      uint32_t wv = 0;
+      for (int k = 0; k < 8; k++) {
+        uint32_t wv = 0;
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int r = 4 * k + j;
-        wv |= (r < rows ? (uint32_t)raw[r * bw + c] : 0u) << (8 * j);
+        for (int j = 0; j < 4; j++) {
+          const int r = k0 + 4 * k + j;
+          wv |= (r < rows ? (uint32_t)raw[r * bw + c] : 0u) << (8 * j);
+        }
+        colv[k] = wv;
       }
-      colv[k] = wv;
     }
-  }
-  __syncthreads();
-  if (c < bw) {
-    uint32_t acc = 0;
+    __syncthreads();
+    if (c < bw) {
 #pragma unroll
-    for (int k = 0; k < kSliceRows / 4; k++) {
+      for (int k = 0; k < 8; k++) {
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        acc += (colv[k] >> (8 * j)) & 0xFFu;
-        if (4 * k + j < rows) pre[(4 * k + j) * bw + c] = (uint16_t)acc;
+        for (int j = 0; j < 4; j++) {
+          const int r = k0 + 4 * k + j;
+          acc += (colv[k] >> (8 * j)) & 0xFFu;
+          if (r < rows) pre[r * bw + c] = (uint16_t)acc;
+        }
       }
     }
   }
@@ -403,7 +412,7 @@ __global__ void __launch_bounds__(kBandThreads)
 __global__ void __launch_bounds__(256) k_rot_final(RotGeom g, const RotTable* table,
                                                    const Rect* masks, const int32_t* mask_active,
                                                    int mask_index, int32_t* peaks, int count,
-                                                   int max_scan, RotScratch R) {
+                                                   int max_scan, RotScratch R, int band_cap) {
   const int na = table->nangles;
   const int nlines = count * g.nedges * na;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -423,7 +432,7 @@ __global__ void __launch_bounds__(256) k_rot_final(RotGeom g, const RotTable* ta
     if (lane == 0) *out = 0;
     return;
   }
-  if (!band_range(R, (s * g.nedges + e) * na, na, sxh, &bx0, &bw)) {
+  if (!band_range(R, (s * g.nedges + e) * na, na, sxh, band_cap, &bx0, &bw)) {
     if (lane == 0) R.flag[t] = 1;
     return;
   }
@@ -604,13 +613,23 @@ template <int FMT>
 static void launch_rot_t(const PlaneRef& img, const RotGeom& g, const RotTable* table,
                          const Rect* masks, const int32_t* mask_active, int mask_index,
                          int32_t* peaks, int count, hipStream_t st, int nangles, int max_scan,
-                         const RotScratch& R) {
+                         const RotScratch& R, float max_abs_angle) {
+  // Band columns: every left/right line lies within scan*tan(max |angle|)
+  // columns of the mask edge (line_setup), plus the kDepth steps and the
+  // truncation slack.  A wider band (k_rot_final re-checks) takes k_rot_line.
+  const float tn = tanf(fminf(fabsf(max_abs_angle), 1.5f));
+  const int band_cap =
+      imin(kBandCapMax, (int)ceilf((float)imax(max_scan, 1) * tn) + kDepth + 4);
+  const size_t band_lds = sizeof(uint16_t) * kSliceRows * (size_t)band_cap;
+  if (band_lds > 64 * 1024)
+    hipFuncSetAttribute((const void*)k_rot_band_g, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)band_lds);
   UPH_LAUNCH_DIAG(1, k_rot_band_g, dim3(rot_slices(max_scan), g.nedges, count),
-                  dim3(kBandThreads), 0, st, img, g, table, masks, mask_active, count, max_scan, R,
-                  (int)FMT);
+                  dim3(kBandThreads), band_lds, st, img, g, table, masks, mask_active, count,
+                  max_scan, R, (int)FMT, band_cap);
   const int nlines = count * g.nedges * nangles;
   UPH_LAUNCH_DIAG(128, k_rot_final, dim3((nlines + 3) / 4), dim3(256), 0, st, g, table, masks,
-                  mask_active, mask_index, peaks, count, max_scan, R);
+                  mask_active, mask_index, peaks, count, max_scan, R, band_cap);
   const size_t lds = sizeof(int32_t) * 2 * (size_t)(max_scan > 0 ? max_scan : 1);
   if (lds > 64 * 1024)
     hipFuncSetAttribute((const void*)k_rot_line<FMT>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -622,7 +641,7 @@ static void launch_rot_t(const PlaneRef& img, const RotGeom& g, const RotTable* 
 void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable* table,
                            const Rect* masks, const int32_t* mask_active, int mask_index,
                            int32_t* peaks, int count, hipStream_t st, int nangles,
-                           int max_scan, int32_t* lines) {
+                           int max_scan, int32_t* lines, float max_abs_angle) {
   if (g.nedges <= 0 || nangles <= 0) return;
   const int nlines = count * g.nedges * nangles;
   const RotScratch R = rot_scratch(lines, nlines, max_scan);
@@ -631,15 +650,15 @@ void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable
   switch (img.P.fmt) {
     case F_GRAY8:
       launch_rot_t<F_GRAY8>(img, g, table, masks, mask_active, mask_index, peaks, count, st,
-                            nangles, max_scan, R);
+                            nangles, max_scan, R, max_abs_angle);
       break;
     case F_Y400A:
       launch_rot_t<F_Y400A>(img, g, table, masks, mask_active, mask_index, peaks, count, st,
-                            nangles, max_scan, R);
+                            nangles, max_scan, R, max_abs_angle);
       break;
     default:
       launch_rot_t<F_RGB24>(img, g, table, masks, mask_active, mask_index, peaks, count, st,
-                            nangles, max_scan, R);
+                            nangles, max_scan, R, max_abs_angle);
       break;
   }
 }

@@ -780,7 +780,7 @@ __device__ __forceinline__ SmallVerdict small_verdict(const uint32_t (*drow)[4],
 constexpr int kListCap = 1024;  // LDS work list of one tile (else: row loops)
 
 template <int FMT>
-__global__ void __launch_bounds__(256) k_noise_classify(PlaneRef img, NoiseGeom g, uint8_t* scratch,
+__global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGeom g, uint8_t* scratch,
                                                         int64_t sstride, const int32_t* active,
                                                         SheetCtl* ctl) {
   // XCD-aware tile order: neighbouring tiles' halos are fetched into one L2

@@ -141,8 +141,10 @@ float uphip_detect_rotation(UphipImage image, UphipRectangle mask,
   max_scan = imin(imin(max_scan, 10000), imax(mw, mh));
   int32_t* lines = (int32_t*)scratch(7, rotation_lines_bytes(1, g.nedges, na, max_scan));
   if (!lines) return 0.0f;
+  float max_angle = 0.0f;
+  for (int i = 0; i < na; i++) max_angle = fmaxf(max_angle, fabsf(table.angle[i]));
   launch_rotation_peaks(ref1(image.frame), g, dt, dm, nullptr, 0, peaks, 1, st, na, max_scan,
-                        lines);
+                        lines, max_angle);
   std::vector<int32_t> hp(4 * (size_t)(na > 0 ? na : 1));
   UPH_HIP(hipMemcpyAsync(hp.data(), peaks, sizeof(int32_t) * g.nedges * na,
                          hipMemcpyDeviceToHost, st));

@@ -1050,7 +1050,7 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
                          (int)i, b->pick_mask, b->pick_active, count);
       launch_rotation_peaks(cur_ref(P, b->ctl), rg, b->dtable, b->pick_mask, b->pick_active,
                             (int)i, b->peaks, count, b->st, b->table.nangles, b->max_scan,
-                            b->rot_lines);
+                            b->rot_lines, b->max_angle);
       if (getenv("UPHIP_DEBUG_ROTATION")) {  // diagnostics: lines left to the direct walk
         const int nl = count * rg.nedges * b->table.nangles;
         std::vector<int32_t> fl((size_t)nl);
