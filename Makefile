@@ -27,7 +27,8 @@ CPP_OBJS   := $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.cpp.o,$(CPP_SRCS))
 C_OBJS     := $(patsubst $(CSRC)/%.c,$(OBJDIR)/%.c.o,$(C_SRCS))
 
 HIPFLAGS   := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
-              -fno-gpu-rdc -Iinclude -I$(CSRC) -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result
+              -fno-gpu-rdc -Iinclude -I$(CSRC) -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result \
+              -Wno-pass-failed  # occupancy hints tuned for GRAY8 miss on RGB instantiations
 CFLAGS_O   := -O2 -std=gnu11 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result
 
 .PHONY: all lib oracle clean

@@ -288,7 +288,6 @@ __device__ __forceinline__ uint32_t block_prefix(uint32_t v, uint32_t carry, uin
 //   Guard: a bar entirely outside the image stops the scan when thr <= 1 (the
 //   reference would loop forever there; DESIGN.md documents this).
 // ---------------------------------------------------------------------------
-constexpr int kMaxAxis = 16384;
 
 __global__ void __launch_bounds__(256) k_edge_scan(const EdgeArgs* args, const uint32_t* sums,
                                                    int64_t sums_stride, int32_t* results) {
@@ -298,7 +297,7 @@ __global__ void __launch_bounds__(256) k_edge_scan(const EdgeArgs* args, const u
   const EdgeArgs a = args[slot];
   if (!a.active) return;
   const uint32_t* S = sums + (int64_t)s * sums_stride + a.sums_offset;
-  __shared__ uint32_t lds[kMaxAxis];
+  extern __shared__ uint32_t lds[];  // a.extent entries (launch: the largest extent)
   __shared__ uint32_t wsum[4];
   __shared__ uint32_t carry;
   __shared__ int32_t stop_k;
@@ -338,11 +337,21 @@ __global__ void __launch_bounds__(256) k_edge_scan(const EdgeArgs* args, const u
   if (threadIdx.x == 0) results[slot] = stop_k == INT_MAX ? (1 << 21) : stop_k + 1;
 }
 
+// The sums along the scan axis are staged in dynamic LDS sized to the largest
+// extent (a static 64 KB array held a CU's LDS for the whole scan).
+static size_t axis_lds(int32_t max_extent, const void* kernel) {
+  const size_t b = sizeof(uint32_t) * (size_t)imax(max_extent, 1);
+  if (b > 64 * 1024) hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b);
+  return b;
+}
+
 void launch_edge_scan(const EdgeArgs* args, int jobs_per_sheet, const uint32_t* sums,
-                      int64_t sums_stride, int32_t* results, int count, hipStream_t st) {
+                      int64_t sums_stride, int32_t* results, int count, hipStream_t st,
+                      int32_t max_extent) {
   if (jobs_per_sheet <= 0 || count <= 0) return;
-  hipLaunchKernelGGL(k_edge_scan, dim3(jobs_per_sheet, count), dim3(256), 0, st, args, sums,
-                     sums_stride, results);
+  hipLaunchKernelGGL(k_edge_scan, dim3(jobs_per_sheet, count), dim3(256),
+                     axis_lds(max_extent, (const void*)k_edge_scan), st, args, sums, sums_stride,
+                     results);
 }
 
 // ---------------------------------------------------------------------------
@@ -360,7 +369,7 @@ __global__ void __launch_bounds__(256) k_border_scan(const BorderEdgeArgs* args,
   const BorderEdgeArgs a = args[slot];
   if (!a.active) return;
   const uint32_t* S = sums + (int64_t)s * sums_stride + a.sums_offset;
-  __shared__ uint32_t lds[kMaxAxis];
+  extern __shared__ uint32_t lds[];  // a.extent entries (launch: the largest extent)
   __shared__ int32_t found;
   const int32_t n = a.extent;
   for (int i = threadIdx.x; i < n; i += blockDim.x) lds[i] = S[i];
@@ -393,10 +402,12 @@ __global__ void __launch_bounds__(256) k_border_scan(const BorderEdgeArgs* args,
 }
 
 void launch_border_scan(const BorderEdgeArgs* args, int jobs_per_sheet, const uint32_t* sums,
-                        int64_t sums_stride, int32_t* results, int count, hipStream_t st) {
+                        int64_t sums_stride, int32_t* results, int count, hipStream_t st,
+                        int32_t max_extent) {
   if (jobs_per_sheet <= 0 || count <= 0) return;
-  hipLaunchKernelGGL(k_border_scan, dim3(jobs_per_sheet, count), dim3(256), 0, st, args, sums,
-                     sums_stride, results);
+  hipLaunchKernelGGL(k_border_scan, dim3(jobs_per_sheet, count), dim3(256),
+                     axis_lds(max_extent, (const void*)k_border_scan), st, args, sums, sums_stride,
+                     results);
 }
 
 }  // namespace uph

@@ -405,7 +405,7 @@ size_t uphip_detect_masks(UphipImage image, UphipMaskDetectionParameters params,
   }
   EdgeArgs* de = stage_args(edges.data(), edges.size(), st);
   if (!de) return 0;
-  launch_edge_scan(de, (int)edges.size(), sums, 0, res, 1, st);
+  launch_edge_scan(de, (int)edges.size(), sums, 0, res, 1, st, imax(W, H));
   arg_fence(st);
   std::vector<int32_t> counts(4 * n);
   UPH_HIP(hipMemcpyAsync(counts.data(), res, sizeof(int32_t) * 4 * n, hipMemcpyDeviceToHost, st));
@@ -515,7 +515,7 @@ UphipBorder uphip_detect_border(UphipImage image, UphipBorderScanParameters para
   BorderEdgeArgs* de = stage_args(e, 4, st);
   if (!de) return b;
   UPH_HIP(hipMemsetAsync(res, 0, sizeof(int32_t) * 4, st));
-  launch_border_scan(de, 4, sums, 0, res, 1, st);
+  launch_border_scan(de, 4, sums, 0, res, 1, st, imax(W, H));
   arg_fence(st);
   int32_t r[4];
   UPH_HIP(hipMemcpyAsync(r, res, sizeof(r), hipMemcpyDeviceToHost, st));

@@ -822,7 +822,7 @@ static void detect_masks_all(UphipBatch* b, int assign, int count) {
   for (int s = 0; s < b->cap; s++)
     for (int j = 0; j < np * 4; j++) all[(size_t)s * np * 4 + j] = ea[j];
   EdgeArgs* de = (EdgeArgs*)upload_cached(b, all.data(), sizeof(EdgeArgs) * all.size());
-  launch_edge_scan(de, np * 4, b->sums, b->sums_stride, b->edge_res, count, b->st);
+  launch_edge_scan(de, np * 4, b->sums, b->sums_stride, b->edge_res, count, b->st, imax(W, H));
   MaskAssembleArgs ma{p, W, H, np, assign};
   hipLaunchKernelGGL(k_mask_assemble, dim3((count + 255) / 256), dim3(256), 0, b->st, b->ctl,
                      b->edge_res, ma, count);
@@ -868,7 +868,8 @@ static void border_all(UphipBatch* b, int count) {
   BorderEdgeArgs* de =
       (BorderEdgeArgs*)upload_cached(b, all.data(), sizeof(BorderEdgeArgs) * all.size());
   UPH_HIP(hipMemsetAsync(b->border_res, 0, sizeof(int32_t) * count * nout * 4, b->st));
-  launch_border_scan(de, nout * 4, b->sums, b->sums_stride, b->border_res, count, b->st);
+  launch_border_scan(de, nout * 4, b->sums, b->sums_stride, b->border_res, count, b->st,
+                     imax(W, H));
   BorderAssembleArgs ba;
   memset(&ba, 0, sizeof(ba));
   ba.W = W;

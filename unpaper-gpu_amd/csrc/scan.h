@@ -46,9 +46,12 @@ void launch_axis_reduce(const PlaneRef& ref, const AxisArgs* args, int axis, int
                         int32_t span_x, int32_t span_y, uint32_t* out, int64_t out_stride,
                         int count, hipStream_t st);
 // grid: jobs_per_sheet x count; results[s*jobs + j] = detect_edge count
+// max_extent: the largest EdgeArgs/BorderEdgeArgs extent of the launch
 void launch_edge_scan(const EdgeArgs* args, int jobs_per_sheet, const uint32_t* sums,
-                      int64_t sums_stride, int32_t* results, int count, hipStream_t st);
+                      int64_t sums_stride, int32_t* results, int count, hipStream_t st,
+                      int32_t max_extent);
 void launch_border_scan(const BorderEdgeArgs* args, int jobs_per_sheet, const uint32_t* sums,
-                        int64_t sums_stride, int32_t* results, int count, hipStream_t st);
+                        int64_t sums_stride, int32_t* results, int count, hipStream_t st,
+                        int32_t max_extent);
 
 }  // namespace uph
