@@ -403,3 +403,31 @@ def test_reference_sources_batch(hip, oracle, ref_path):
         groups.setdefault((s.width, s.height, s.format), []).append([s])
     for sheets in groups.values():
         check(oracle, opts, sheets, "sources")
+
+
+def centered_page(w, h):
+    """A text-like block exactly in the middle of the sheet (the center
+    stage's move is then the identity, MoveArgs.active = 0), plus a dark
+    speckle row near the top for the border scan."""
+    g = np.full((h, w), 255, np.uint8)
+    bw, bh = w // 2, h // 2
+    x0, y0 = (w - bw) // 2, (h - bh) // 2
+    rng = np.random.default_rng(11)
+    blk = rng.integers(0, 256, size=(bh, bw))
+    g[y0:y0 + bh, x0:x0 + bw] = np.where(blk < 90, 20, 255).astype(np.uint8)
+    g[y0 - 30:y0 - 26, x0:x0 + bw // 3] = 30
+    return HostImage.from_array(g, A.FMT_GRAY8, abs_black_threshold=170)
+
+
+def test_center_move_border_counts(hip, oracle):
+    """The border scan's row counts come out of the last center move
+    (k_move_rect_g16 RowCounts); sheets whose move is the identity count the
+    plane in place.  Both kinds in one batch, against the oracle; with a wipe
+    configured the counts take the separate reduction again."""
+    opts = oracle.default_options()
+    sheets = [[centered_page(*SMALL)], [synth(*SMALL, 0)], [centered_page(*SMALL)],
+              [synth(*SMALL, 3)]]
+    check(oracle, opts, sheets, "center + border")
+    opts.wipes.count = 1
+    opts.wipes.areas[0] = A.rect(5, 5, 40, 60)
+    check(oracle, opts, sheets, "center + wipe + border")
