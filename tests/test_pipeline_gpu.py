@@ -420,10 +420,9 @@ def centered_page(w, h):
 
 
 def test_center_move_border_counts(hip, oracle):
-    """The border scan's row counts come out of the last center move
-    (k_move_rect_g16 RowCounts); sheets whose move is the identity count the
-    plane in place.  Both kinds in one batch, against the oracle; with a wipe
-    configured the counts take the separate reduction again."""
+    """Center moves that are the identity (MoveArgs.active = 0, the plane is
+    not flipped) next to real moves in one batch, followed by the border
+    scan, with and without a wipe in between, against the oracle."""
     opts = oracle.default_options()
     sheets = [[centered_page(*SMALL)], [synth(*SMALL, 0)], [centered_page(*SMALL)],
               [synth(*SMALL, 3)]]
