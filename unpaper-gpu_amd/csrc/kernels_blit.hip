@@ -1402,7 +1402,37 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
       if (rr < kRows) *reinterpret_cast<uint64_t*>(obuf + rr * kRFW + cb) = q[h];
     }
   }
-#pragma unroll 2
+  // White flags of the wave's rows, computed lane-parallel up front: lane
+  // 16 q + j tests window row r0 + j (+16, ...) of output row 4 h + q against
+  // the row's dword columns; one ballot per four rows (instead of scalar
+  // bounds and a ballot per row).
+  uint32_t white_rows = 0;  // bit k: every tap of output row k is white
+  if (staged) {
+#pragma unroll
+    for (int h = 0; h < (kRows + 3) / 4; h++) {
+      const int k = 4 * h + (lane >> 4), j = lane & 15;
+      bool hit = false;
+      if (k < kRows) {
+        const float cv = (yw + k - a.mask.y0) - tcy;
+        const float VS = cv * a.sinval, VC = scy + cv * a.cosval;
+        const int32_t xl = (int)(axL + VS), xr = (int)(axR + VS);
+        const int32_t yl = (int)(VC - bsL), yr = (int)(VC - bsR);
+        const int32_t c0 = imax((imin(xl, xr) - 1 - xa) >> 2, 0);
+        const int32_t c1 = imin((imax(xl, xr) + 2 - xa) >> 2, nd - 1);
+        const int32_t r0 = imax(imin(yl, yr) - 1 - by0, 0);
+        const int32_t r1 = imin(imax(yl, yr) + 2 - by0, bh - 1);
+        const uint64_t cm = c1 >= c0 ? ((2ull << c1) - 1ull) & ~((1ull << c0) - 1ull) : 0ull;
+        for (int r = r0 + j; r <= r1; r += 16) hit |= (nw[r] & cm) != 0;  // one pass at 5 deg
+      }
+      const uint64_t m = __ballot(hit);
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (4 * h + q < kRows && ((m >> (16 * q)) & 0xFFFFull) == 0) white_rows |= 1u << (4 * h + q);
+    }
+    if (diag & 2048) white_rows = 0;
+    if (diag & 512) white_rows = ~0u;
+  }
+#pragma unroll
   for (int k = 0; k < kRows; k++) {
     const int32_t y = yw + k;
     const int32_t v = y - a.mask.y0;
@@ -1411,23 +1441,7 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
     const float VS = cv * a.sinval, VC = scy + cv * a.cosval;
     const bool inA = rowin & colA, inB = rowin & colB;
     uint32_t oA = 255, oB = 255;
-    bool white = true;
-    if (staged) {
-      const int32_t xl = (int)(axL + VS), xr = (int)(axR + VS);
-      const int32_t yl = (int)(VC - bsL), yr = (int)(VC - bsR);
-      const int32_t c0 = imax((imin(xl, xr) - 1 - xa) >> 2, 0);
-      const int32_t c1 = imin((imax(xl, xr) + 2 - xa) >> 2, nd - 1);
-      const int32_t r0 = imax(imin(yl, yr) - 1 - by0, 0);
-      const int32_t r1 = imin(imax(yl, yr) + 2 - by0, bh - 1);
-      // one window row per lane, then one ballot (instead of a scalar loop
-      // over the rows with an LDS round trip each)
-      const uint64_t cm = c1 >= c0 ? ((2ull << c1) - 1ull) & ~((1ull << c0) - 1ull) : 0ull;
-      // (lanes past r1 re-read r1, which leaves the OR unchanged)
-      bool any = r0 <= r1 && __ballot((nw[imax(imin(r0 + lane, r1), 0)] & cm) != 0) != 0;
-      for (int rb = r0 + 64; rb <= r1; rb += 64)  // only when |angle| is large
-        any |= __ballot((nw[imin(rb + lane, r1)] & cm) != 0) != 0;
-      white = (!any && !(diag & 2048)) || (diag & 512);
-    }
+    const bool white = staged && ((white_rows >> k) & 1u);
     if (!white && staged) {
       const float sxA = axA + VS, syA = VC - bsA, sxB = axB + VS, syB = VC - bsB;
       const int ixA = (int)sxA, iyA = (int)syA, ixB = (int)sxB, iyB = (int)syB;  // truncation
