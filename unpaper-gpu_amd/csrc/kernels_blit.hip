@@ -1463,13 +1463,24 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
                           f2{c[0].y, c[2].y}, f2{c[1].x, c[3].x}, f2{c[1].y, c[3].y});
       oA = (uint32_t)o.x;  // integer-valued in [0, 255]
       oB = (uint32_t)o.y;
-    } else if (!staged) {
-      // window too large for LDS (large angles): taps from the frame
-      if (inA) oA = interp_bicubic(S, axA + VS, VC - bsA).r;
-      if (inB) oB = interp_bicubic(S, axB + VS, VC - bsB).r;
     }
+    if (!staged) break;  // uniform: the rows go through the loop below
     if (inA) obuf[k * kRFW + lane] = (uint8_t)oA;
     if (inB) obuf[k * kRFW + 64 + lane] = (uint8_t)oB;
+  }
+  if (!staged) {
+    // window too large for LDS (large angles): taps from the frame (kept out
+    // of the unrolled loop above)
+#pragma unroll 1
+    for (int k = 0; k < kRows; k++) {
+      const int32_t y = yw + k;
+      const int32_t v = y - a.mask.y0;
+      const bool rowin = (v >= 0) & (v < sh) & (y < P.H);
+      const float cv = v - tcy;
+      const float VS = cv * a.sinval, VC = scy + cv * a.cosval;
+      if (rowin & colA) obuf[k * kRFW + lane] = interp_bicubic(S, axA + VS, VC - bsA).r;
+      if (rowin & colB) obuf[k * kRFW + 64 + lane] = interp_bicubic(S, axB + VS, VC - bsB).r;
+    }
   }
   // the wave's rows as 8-byte stores: lane -> row k0 + lane/16, bytes
   // 8*(lane%16).  One wave's LDS operations complete in order, so its reads
