@@ -1249,6 +1249,13 @@ __device__ __forceinline__ void cubic2x4(const f2 (&f)[4], const f2 (&h)[4],
                 __builtin_amdgcn_fmed3f(__builtin_truncf(u[i].y), 0.0f, 255.0f)};
 }
 
+// Byte offset of row y (0 <= y < H) as a 32-bit product: the launcher only
+// picks k_rotate_cubic_g8f when pitch * H < 2^31 (one scalar multiply per row
+// instead of a 64-bit product).
+__device__ __forceinline__ uint32_t row_off(int32_t y, int64_t pitch) {
+  return (uint32_t)y * (uint32_t)pitch;
+}
+
 __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRef dst,
                                                                const RotateArgs* args,
                                                                int max_rows, int diag,
@@ -1258,11 +1265,12 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
   extern __shared__ __attribute__((aligned(16))) float winf[];
   int txi, tyi, s;
   xcd_block_m(m_gxy, m_gx, &txi, &tyi, &s);
+  // the plane selectors and the arguments are loaded together (one round trip)
+  const uint8_t* sbase = plane_ptr(src, s);
+  uint8_t* dbase = plane_ptr(dst, s);
   const RotateArgs a = args[s];
   if (!a.active) return;
   const Planes& P = src.P;
-  const uint8_t* sbase = plane_ptr(src, s);
-  uint8_t* dbase = plane_ptr(dst, s);
   const Rect nm = normalize(a.mask);
   const int32_t sw = nm.x1 - nm.x0 + 1, sh = nm.y1 - nm.y0 + 1;
   const float scx = nm.x0 + sw / 2.0f, scy = nm.y0 + sh / 2.0f;  // primitives.c:137-145
@@ -1279,8 +1287,8 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
     for (int r = threadIdx.x >> 4; r < kRFH; r += kRFT / 16) {
       const int32_t y = ty0 + r;
       if (y >= P.H || x >= P.W) continue;
-      const uint8_t* sp = sbase + (int64_t)y * P.pitch + x;
-      uint8_t* dp = dbase + (int64_t)y * P.pitch + x;
+      const uint8_t* sp = sbase + row_off(y, P.pitch) + x;
+      uint8_t* dp = dbase + row_off(y, P.pitch) + x;
       if (x + 8 <= P.W) *reinterpret_cast<uint64_t*>(dp) = *reinterpret_cast<const uint64_t*>(sp);
       else for (int j = 0; x + j < P.W; j++) dp[j] = sp[j];
     }
@@ -1336,7 +1344,7 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int32_t y = imin(imax(by0 + r0 + q, 0), P.H - 1);
-        v[q] = *reinterpret_cast<const uint32_t*>(sbase + (int64_t)y * P.pitch + xc);
+        v[q] = *reinterpret_cast<const uint32_t*>(sbase + row_off(y, P.pitch) + xc);
       }
 #pragma unroll
       for (int q = 0; q < 4; q++) {
@@ -1394,7 +1402,7 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
       const int rr = 4 * h + (lane >> 4);
       const int32_t y = imin(yw + rr, P.H - 1);
       const int32_t x = imin(xo, (int32_t)P.pitch - 8);  // rows are 256-byte pitched
-      if (rr < kRows) q[h] = *reinterpret_cast<const uint64_t*>(sbase + (int64_t)y * P.pitch + x);
+      if (rr < kRows) q[h] = *reinterpret_cast<const uint64_t*>(sbase + row_off(y, P.pitch) + x);
     }
 #pragma unroll
     for (int h = 0; h < 2; h++) {
@@ -1491,7 +1499,7 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
     const int32_t y = yw + rr, x = xo;
     if (rr < kRows && y < P.H && x < P.W) {
       const uint64_t q = *reinterpret_cast<const uint64_t*>(obuf + rr * kRFW + cb);
-      uint8_t* d = dbase + (int64_t)y * P.pitch + x;
+      uint8_t* d = dbase + row_off(y, P.pitch) + x;
       if (x + 8 <= P.W) {
         *reinterpret_cast<uint64_t*>(d) = q;
       } else {
@@ -1516,7 +1524,8 @@ void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateAr
   if (interp == UPHIP_INTERP_CUBIC && src.P.fmt == F_GRAY8) {
     const int rows = rotate_window_rows(max_abs_angle);
     const size_t lds = (sizeof(float) * kRFS + sizeof(uint64_t)) * (size_t)rows + kRFH * kRFW;
-    if (lds <= 56 * 1024 && !(diag_double() & 256)) {
+    if (lds <= 56 * 1024 && src.P.pitch * (int64_t)src.P.H < (1ll << 31) &&
+        !(diag_double() & 256)) {
       const dim3 fgrid((src.P.W + kRFW - 1) / kRFW, (src.P.H + kRFH - 1) / kRFH, count);
       UPH_LAUNCH_DIAG(2, k_rotate_cubic_g8f, fgrid, dim3(kRFT), lds, st, src, dst, args, rows,
                       diag_double() & (512 | 1024 | 2048), div_magic(fgrid.x * fgrid.y),
