@@ -593,12 +593,15 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
             default: out = shift_bytes16<3>(w, r); break;
           }
         } else if (cls[k] == 3) {
+          // unrolled with independent byte loads (one memory round trip,
+          // not sixteen); columns >= W stay 0 as before
           uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
           for (int j = 0; j < 16; j++) {
             const int32_t x = x0 + j;
-            if (x >= P.W) break;
-            const int c = cls_of(x);
-            const uint8_t bb = c == 0 ? srow[x] : c == 1 ? bg : mrow_p[x + delta];
+            const int c = x < P.W ? cls_of(x) : 1;
+            const uint8_t* p = c == 0 ? srow + x : mrow_p + (c == 2 ? x + delta : 0);
+            const uint8_t bb = c == 1 ? (x < P.W ? bg : 0) : *p;
             o[j >> 2] |= (uint32_t)bb << (8 * (j & 3));
           }
           out = make_uint4(o[0], o[1], o[2], o[3]);
