@@ -67,8 +67,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--pages", type=int, default=1000, help="pages per GPU")
     ap.add_argument("--batch", type=int, default=64, help="sheets per batch launch sequence")
-    ap.add_argument("--streams", type=int, default=12, help="batches (HIP streams) in flight")
-    ap.add_argument("--hw-queues", type=int, default=16,
+    ap.add_argument("--streams", type=int, default=16, help="batches (HIP streams) in flight")
+    ap.add_argument("--hw-queues", type=int, default=24,
                     help="GPU_MAX_HW_QUEUES for this process (HIP default 4, at most 32)")
     ap.add_argument("--cpu-pages", type=int, default=0,
                     help="CPU baseline sample (0 = 2 pages per host thread)")
