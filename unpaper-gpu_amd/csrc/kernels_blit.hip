@@ -539,7 +539,7 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
   const int32_t bp[5] = {a.tx, a.tx + aw, a.tx + sw, A.x0, A.x1 + 1};
   const int lane = threadIdx.x & 63;
   // one wave per destination row, kMoveVec vectors per lane, loads issued first
-  constexpr int kMoveVec = 4;
+  constexpr int kMoveVec = 3;  // 192 vector slots per row: 155 used at A4 width
   for (int32_t y = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); y < P.H;
        y += gridDim.x * (kThreads / 64)) {
     const uint8_t* srow = sbase + (int64_t)y * P.pitch;
