@@ -2,6 +2,9 @@
 #   make            -> both
 #   make lib        -> unpaper-gpu_amd/lib/libunpaper_hip.so   (product)
 #   make oracle     -> oracle/_build/liboracle.so              (test infrastructure)
+#   make lib DIAG=1 -> the same library with the timing diagnostics of
+#                      csrc/common.h (UPHIP_DIAG_*) compiled in; tuning only,
+#                      built into its own object dir.  The default build has none.
 # FP contraction is OFF everywhere: interpolation must round exactly like the
 # reference's x86-64 scalar float code (reference meson uses nvcc --fmad=false).
 
@@ -12,8 +15,6 @@ JOBS       ?= 8
 
 PKG        := unpaper-gpu_amd
 CSRC       := $(PKG)/csrc
-LIBDIR     := $(PKG)/lib
-LIB        := $(LIBDIR)/libunpaper_hip.so
 ORACLE_LIB := oracle/_build/liboracle.so
 
 HIP_SRCS   := $(wildcard $(CSRC)/*.hip)
@@ -21,13 +22,22 @@ CPP_SRCS   := $(wildcard $(CSRC)/*.cpp)
 C_SRCS     := $(wildcard $(CSRC)/*.c)
 HDRS       := $(wildcard $(CSRC)/*.h) $(wildcard $(CSRC)/*.cuh) include/unpaper_hip.h
 
+ifeq ($(DIAG),1)
+OBJDIR     := $(PKG)/build_diag
+LIBDIR     := $(PKG)/lib_diag
+DIAGFLAGS  := -DUPHIP_DIAG
+else
 OBJDIR     := $(PKG)/build
+LIBDIR     := $(PKG)/lib
+DIAGFLAGS  :=
+endif
+LIB        := $(LIBDIR)/libunpaper_hip.so
 HIP_OBJS   := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.hip.o,$(HIP_SRCS))
 CPP_OBJS   := $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.cpp.o,$(CPP_SRCS))
 C_OBJS     := $(patsubst $(CSRC)/%.c,$(OBJDIR)/%.c.o,$(C_SRCS))
 
 HIPFLAGS   := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
-              -fno-gpu-rdc -Iinclude -I$(CSRC) -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result \
+              -fno-gpu-rdc $(DIAGFLAGS) -Iinclude -I$(CSRC) -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result \
               -Wno-pass-failed  # occupancy hints tuned for GRAY8 miss on RGB instantiations
 CFLAGS_O   := -O2 -std=gnu11 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result
 
@@ -58,4 +68,4 @@ $(ORACLE_LIB): oracle/oracle.c oracle/oracle.h include/unpaper_hip.h
 	$(CC) $(CFLAGS_O) -shared -o $@ oracle/oracle.c -lm
 
 clean:
-	rm -rf $(OBJDIR) $(LIBDIR) oracle/_build
+	rm -rf $(PKG)/build $(PKG)/build_diag $(PKG)/lib $(PKG)/lib_diag oracle/_build

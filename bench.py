@@ -209,7 +209,7 @@ def main():
         print("sweep batch %d streams %d: %.1f pages/s" % (sb, ss, npages / t), file=sys.stderr,
               flush=True)
     bsz = max(1, min(args.batch, npages))
-    batches = [Batch(opts, bsz, W, H, A.FMT_GRAY8) for _ in range(max(1, args.streams))]
+    batches = [Batch(opts, bsz, W, H, A.FMT_GRAY8, timing=True) for _ in range(max(1, args.streams))]
     chunks = [(s, min(bsz, npages - s)) for s in range(0, npages, bsz)]
     launches = [0]
 

@@ -411,6 +411,10 @@ typedef struct {
 } UphipSheetReport;
 int uphip_batch_get_report(UphipBatch *batch, int32_t sheet,
                            UphipSheetReport *report);
+/* Stage timing (off by default): when on, every run records a HIP event at
+ * each stage boundary on the batch stream, kept until
+ * uphip_batch_kernel_times() reads and frees them. */
+int uphip_batch_set_timing(UphipBatch *batch, int32_t enable);
 /* Per-stage device time summed over every run since the previous call (HIP
  * events recorded between stages on the batch stream, cf. the reference's
  * --perf stage timers, lib/perf.c).  Synchronises the batch stream, returns

@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/bench_hashes.json: SHA-256 of the oracle's output for
+the synthetic A4 pages the benchmark processes.
+
+TEST INFRASTRUCTURE: runs in the build container (oracle/_build/liboracle.so,
+the C restatement of the reference CPU path, pinned to the reference goldens by
+tests/test_oracle_golden.py).  The GPU side (tests/test_bench_config_gpu.py and
+bench.py's verification after the timed region) compares the HIP pipeline's
+outputs with these hashes, so the exact benchmarked configuration is
+parity-checked without running the oracle on the GPU box.
+
+Pages: 0..255 (rank 0's first four 64-sheet batches) and, for ranks 1..7 of a
+sharded run (1000 pages per rank), the first 16 pages of each shard.
+Options: the reference defaults (uphip_options_init == lib/options.c).
+Hash: SHA-256 over the output rows' visible bytes (GRAY8, W bytes per row).
+
+usage: python3 tests/golden/make_bench_hashes.py [--threads N]
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import threading
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "unpaper-gpu_amd", "python"))
+
+from oracle_py import Oracle  # noqa: E402
+from unpaper_hip import ctypes_abi as A  # noqa: E402
+from unpaper_hip.hostimage import HostImage  # noqa: E402
+from unpaper_hip.pipeline import synth_page_host  # noqa: E402
+
+W, H = 2480, 3508
+
+
+def page_list():
+    pages = list(range(256))
+    for r in range(1, 8):
+        pages += [r * 1000 + i for i in range(16)]
+    return pages
+
+
+def page_hash(oracle, opts, page):
+    src = HostImage.from_array(synth_page_host(W, H, page), A.FMT_GRAY8)
+    sheet, fmt, _ = oracle.process_sheet(opts, [src])
+    out = oracle.convert_for_save(sheet, fmt)
+    assert (out.width, out.height, out.format) == (W, H, A.FMT_GRAY8)
+    return hashlib.sha256(out.payload().tobytes()).hexdigest()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--threads", type=int, default=os.cpu_count() or 1)
+    ap.add_argument("--out", default=os.path.join(HERE, "bench_hashes.json"))
+    args = ap.parse_args()
+    oracle = Oracle()
+    opts = oracle.default_options()
+    todo = page_list()
+    res = {}
+    lock = threading.Lock()
+    t0 = time.time()
+
+    def work():
+        while True:
+            with lock:
+                if not todo:
+                    return
+                p = todo.pop(0)
+            h = page_hash(oracle, opts, p)
+            with lock:
+                res[p] = h
+                if len(res) % 32 == 0:
+                    print("%d pages, %.0f s" % (len(res), time.time() - t0), flush=True)
+
+    ts = [threading.Thread(target=work) for _ in range(args.threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    doc = {
+        "generator": "tests/golden/make_bench_hashes.py (oracle/oracle.c, default options)",
+        "width": W, "height": H, "format": "GRAY8", "hash": "sha256 of visible output rows",
+        "pages": {str(p): res[p] for p in sorted(res)},
+    }
+    with open(args.out, "w") as f:
+        json.dump(doc, f, indent=0, sort_keys=False)
+        f.write("\n")
+    print("wrote %d hashes to %s in %.0f s" % (len(res), args.out, time.time() - t0))
+
+
+if __name__ == "__main__":
+    main()

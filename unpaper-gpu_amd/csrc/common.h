@@ -220,26 +220,48 @@ __device__ __forceinline__ uint8_t* sheet_plane(const Planes& P, int s, int k) {
   return P.base[k] + (int64_t)s * P.stride;
 }
 
-// TEMP timing diagnostics: UPHIP_DIAG_SKIP bit mask of sequential kernels
-// not launched (1 black, 2 noise resolve, 4 gray decide, 8 blur resolve).
+// Timing diagnostics, compiled only into a tuning build (make lib
+// DIAG=1 -> -DUPHIP_DIAG).  The product library has none of them: there the
+// helpers are the constant 0 and every launch below is a single launch.
+//   UPHIP_DIAG_SKIP   bit mask of sequential kernels not launched
+//                     (1 black, 2 noise resolve, 4 gray decide, 8 blur resolve)
+//   UPHIP_DIAG_DOUBLE bit mask of idempotent full-chip kernels launched twice,
+//                     so that the throughput drop under the multi-stream load
+//                     measures each kernel's marginal cost (1 rotation band,
+//                     2 rotate, 4 mask move, 8 decode copy, 16 rotation points,
+//                     32 gray cells, 64 blur counts, 128 rotation final + line
+//                     walk; 256/512/1024/2048 rotate variants)
+//   UPHIP_DIAG_NOISE  noise classify early exit (1, 2, 3)
+// Any of these gives wrong pages by design.
+#ifdef UPHIP_DIAG
+inline int diag_env(const char* name) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : 0;
+}
 inline int diag_skip() {
-  static const int v = getenv("UPHIP_DIAG_SKIP") ? atoi(getenv("UPHIP_DIAG_SKIP")) : 0;
+  static const int v = diag_env("UPHIP_DIAG_SKIP");
   return v;
 }
-
-// Timing diagnostics: UPHIP_DIAG_DOUBLE bit mask of idempotent full-chip
-// kernels launched twice, so that the throughput drop under the multi-stream
-// load measures each kernel's marginal cost (1 rotation band, 2 rotate,
-// 4 mask move, 8 decode copy, 16 rotation points, 32 gray cells,
-// 64 blur counts, 128 rotation final + line walk).
 inline int diag_double() {
-  static const int v = getenv("UPHIP_DIAG_DOUBLE") ? atoi(getenv("UPHIP_DIAG_DOUBLE")) : 0;
+  static const int v = diag_env("UPHIP_DIAG_DOUBLE");
   return v;
 }
+inline int diag_noise() {
+  static const int v = diag_env("UPHIP_DIAG_NOISE");
+  return v;
+}
+#define UPH_DIAG_BITS(d, m) ((d) & (m))
 #define UPH_LAUNCH_DIAG(bit, ...)                              \
   do {                                                         \
     hipLaunchKernelGGL(__VA_ARGS__);                           \
     if (::uph::diag_double() & (bit)) hipLaunchKernelGGL(__VA_ARGS__); \
   } while (0)
+#else
+constexpr int diag_skip() { return 0; }
+constexpr int diag_double() { return 0; }
+constexpr int diag_noise() { return 0; }
+#define UPH_DIAG_BITS(d, m) 0
+#define UPH_LAUNCH_DIAG(bit, ...) hipLaunchKernelGGL(__VA_ARGS__)
+#endif
 
 }  // namespace uph

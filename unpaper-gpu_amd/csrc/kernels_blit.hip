@@ -1326,7 +1326,7 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* obuf = reinterpret_cast<uint8_t*>(nw + max_rows) + wu * (kRFH / kRFWaves * kRFW);
-  if (staged && !(diag & 1024)) {
+  if (staged && !UPH_DIAG_BITS(diag, 1024)) {
     // a wave stages whole rows (lane = source dword), four in flight; nw[r]
     // bit j: dword j of window row r holds a non-white pixel
     // Branch-free: every lane loads the dword at its address clamped into the
@@ -1440,8 +1440,8 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
       for (int q = 0; q < 4; q++)
         if (4 * h + q < kRows && ((m >> (16 * q)) & 0xFFFFull) == 0) white_rows |= 1u << (4 * h + q);
     }
-    if (diag & 2048) white_rows = 0;
-    if (diag & 512) white_rows = ~0u;
+    if (UPH_DIAG_BITS(diag, 2048)) white_rows = 0;
+    if (UPH_DIAG_BITS(diag, 512)) white_rows = ~0u;
   }
 #pragma unroll
   for (int k = 0; k < kRows; k++) {

@@ -945,7 +945,7 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
   }
   __syncthreads();
   if (!any_dark) return;
-  if (g.diag == 1) return;
+  if (UPH_DIAG_BITS(g.diag, 3) == 1) return;
   // Pixels provably in a component of >= 5 pixels: L3 = dark pixels with >= 5
   // dark pixels in their 3x3 block (all 8-adjacent to the centre, so one
   // component); large = dark & (L3 | 8-dilation of L3) (8-adjacent to an L3
@@ -1012,7 +1012,7 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
     }
   }
   __syncthreads();
-  if (g.diag == 2) return;
+  if (UPH_DIAG_BITS(g.diag, 3) == 2) return;
   // small bit rows: the restricted flood of every candidate
   const int ncand = nwl;
   if (ncand <= kListCap) {
@@ -1042,7 +1042,7 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
     }
   }
   __syncthreads();
-  if (g.diag == 3) return;
+  if (UPH_DIAG_BITS(g.diag, 3) == 3) return;
   const int N = g.intensity;
   const bool zone_tile = g.all_seq || tx0 < kZone || ty0 < kZone;  // uniform
   if (zone_tile) {
@@ -1472,9 +1472,8 @@ static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr
                            const int32_t* active, SheetCtl* ctl, int count, hipStream_t st,
                            uint32_t* sortbuf, int64_t sort_stride) {
   dim3 grid((g.W + kNT - 1) / kNT, (g.H + kNT - 1) / kNT, count);
-  static const int diag = getenv("UPHIP_DIAG_NOISE") ? atoi(getenv("UPHIP_DIAG_NOISE")) : 0;
   NoiseGeom gd = g;
-  gd.diag = diag;
+  gd.diag = diag_noise();
   hipLaunchKernelGGL(k_noise_classify<FMT>, grid, dim3(256), 0, st, img, gd, scr, ss, active, ctl);
   hipLaunchKernelGGL(k_noise_apply<FMT>, dim3(64, count), dim3(256), 0, st, img, g, scr, ss,
                      active, ctl);

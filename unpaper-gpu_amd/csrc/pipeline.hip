@@ -52,6 +52,15 @@ __global__ void k_ctl_init(SheetCtl* ctl, int count, int32_t npoints, UphipPoint
   for (int i = 0; i < UPHIP_MAX_PAGES; i++) c.rotation[i] = 0.0f;
 }
 
+// Folds every sheet's status into the batch's sticky word at the end of a
+// run: k_ctl_init clears the per-sheet words at the start of the next run,
+// so without this a failure in an earlier of several runs enqueued before
+// one uphip_batch_wait would be lost.
+__global__ void k_status_fold(const SheetCtl* ctl, int count, int32_t* sticky) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < count && ctl[s].status) atomicOr(sticky, ctl[s].status);
+}
+
 __global__ void k_flip_all(SheetCtl* ctl, int count) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s < count) ctl[s].cur ^= 1;
@@ -305,7 +314,8 @@ struct UphipBatch {
   // stage boundary events of every run since the last kernel_times() query
   std::vector<std::vector<std::pair<const char*, hipEvent_t>>> runs;
   std::vector<std::string> time_names;
-  bool timing = true;
+  bool timing = false;                 // uphip_batch_set_timing
+  int32_t* sticky = nullptr;           // OR of every sheet status since the last wait
   // geometry records
   BlackGeom bgeo{};
   BlackBar* dbars = nullptr;
@@ -578,7 +588,9 @@ static bool allocate(UphipBatch* b) {
     b->rot_page = dalloc<uint8_t>(b, (size_t)rp * b->rp_h * cap);
   }
   b->ctl = dalloc<SheetCtl>(b, cap);
-  if (!b->inputs || !b->planes[0] || !b->planes[1] || !b->ctl) return false;
+  b->sticky = dalloc<int32_t>(b, 1);
+  if (!b->inputs || !b->planes[0] || !b->planes[1] || !b->ctl || !b->sticky) return false;
+  if (!UPH_HIP(hipMemset(b->sticky, 0, sizeof(int32_t)))) return false;
   // filter geometry + scratch (one region per sheet, reused stage after stage)
   const int32_t W = b->W, H = b->H;
   size_t need = 0;
@@ -1159,6 +1171,8 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
                     o.abs_black_threshold, b->st);
   }
   mark(b, "output");
+  hipLaunchKernelGGL(k_status_fold, dim3((count + 255) / 256), dim3(256), 0, b->st, b->ctl, count,
+                     b->sticky);
   b->last_count = count;
   return uphip_last_error() == nullptr;
 }
@@ -1246,7 +1260,12 @@ int uphip_batch_wait(UphipBatch* b) {
   if (!b) return -1;
   hipSetDevice(b->device);
   if (!UPH_HIP(hipStreamSynchronize(b->st))) return -1;
-  // surface device-side failures (overflowing candidate lists / DFS stack)
+  // surface device-side failures (overflowing candidate lists / DFS stack) of
+  // every run since the previous wait, then re-arm the sticky word
+  int32_t any = 0;
+  if (!UPH_HIP(hipMemcpy(&any, b->sticky, sizeof(any), hipMemcpyDeviceToHost))) return -1;
+  if (!any) return 0;
+  UPH_HIP(hipMemset(b->sticky, 0, sizeof(int32_t)));
   std::vector<SheetCtl> c(b->last_count > 0 ? b->last_count : 1);
   if (b->last_count > 0) {
     UPH_HIP(hipMemcpy(c.data(), b->ctl, sizeof(SheetCtl) * b->last_count,
@@ -1255,18 +1274,21 @@ int uphip_batch_wait(UphipBatch* b) {
       if (c[s].status)
         return fail("batch: sheet %d failed on the device (status 0x%x)", s, c[s].status), -1;
   }
-  return 0;
+  return fail("batch: a sheet of an earlier run since the last wait failed on the device "
+              "(status 0x%x)", any), -1;
 }
 
 void* uphip_batch_output_ptr(UphipBatch* b, int32_t sheet, int64_t* pitch) {
   if (!b || sheet < 0 || sheet >= b->cap) return nullptr;
+  // the pointer is handed out only once the batch's kernels have finished
+  // writing it (the caller may read it from any stream or the host)
+  hipSetDevice(b->device);
+  if (!UPH_HIP(hipStreamSynchronize(b->st))) return nullptr;
   if (b->out) {
     if (pitch) *pitch = b->out_pitch;
     return b->out + (int64_t)sheet * b->out_stride;
   }
   int32_t cur = 0;
-  hipSetDevice(b->device);
-  hipStreamSynchronize(b->st);
   hipMemcpy(&cur, &b->ctl[sheet].cur, 4, hipMemcpyDeviceToHost);
   if (pitch) *pitch = b->pitch;
   return b->planes[cur] + (int64_t)sheet * b->plane_stride;
@@ -1278,8 +1300,10 @@ int uphip_batch_get_output(UphipBatch* b, int32_t sheet, void* host, int64_t lin
   if (!p) return fail("batch_get_output: bad sheet"), -1;
   const int64_t rb = row_bytes(b->out_w, b->out_fmt);
   if (linesize < rb) return fail("batch_get_output: linesize too small"), -1;
-  return UPH_HIP(hipMemcpy2D(host, linesize, p, pitch, rb, b->out_h, hipMemcpyDeviceToHost)) ? 0
-                                                                                             : -1;
+  if (!UPH_HIP(hipMemcpy2DAsync(host, linesize, p, pitch, rb, b->out_h, hipMemcpyDeviceToHost,
+                                b->st)))
+    return -1;
+  return UPH_HIP(hipStreamSynchronize(b->st)) ? 0 : -1;
 }
 
 int uphip_batch_get_report(UphipBatch* b, int32_t sheet, UphipSheetReport* r) {
@@ -1298,6 +1322,12 @@ int uphip_batch_get_report(UphipBatch* b, int32_t sheet, UphipSheetReport* r) {
   r->width = b->out_w;
   r->height = b->out_h;
   r->flags = (uint32_t)c.status;
+  return 0;
+}
+
+int uphip_batch_set_timing(UphipBatch* b, int32_t enable) {
+  if (!b) return -1;
+  b->timing = enable != 0;
   return 0;
 }
 

@@ -51,7 +51,8 @@ T* stage_args(const T* host_items, size_t n, hipStream_t st) {
   return static_cast<T*>(b.dev);
 }
 
-// Device scratch (per thread, per device), grown on demand; stream-ordered.
+// Device scratch of the current stream (per device), grown on demand;
+// stream-ordered, so a thread may switch streams between ops.
 void* scratch(int slot, size_t bytes);
 
 // Frame helpers

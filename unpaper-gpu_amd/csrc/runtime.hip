@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -41,10 +42,19 @@ struct PerThreadDevice {
   int next = 0;
   int pending[kSlots] = {};
   int npending = 0;
-  // scratch
+};
+
+// Op-level scratch belongs to a STREAM, not to a thread: a worker that
+// switches streams per job (lib/batch_worker.c:197-202) must not hand the
+// next job's kernels a buffer the previous job's kernels, still queued on
+// another stream, are reading.  Everything on one stream is ordered, so
+// per-stream buffers need no further fencing.
+struct StreamScratch {
   void* scr[8] = {};
   size_t scr_bytes[8] = {};
 };
+std::mutex g_scr_mu;
+std::map<std::pair<int, hipStream_t>, StreamScratch*> g_scr;
 
 thread_local PerThreadDevice* t_dev[64] = {};
 
@@ -170,12 +180,21 @@ void arg_fence(hipStream_t st) {
 }
 
 void* scratch(int slot, size_t bytes) {
-  PerThreadDevice& p = ptd();
   if (slot < 0 || slot >= 8) return nullptr;
+  const int dev = current_device();
+  hipStream_t st = current_stream();
+  StreamScratch* ps;
+  {
+    std::lock_guard<std::mutex> lk(g_scr_mu);
+    StreamScratch*& e = g_scr[{dev, st}];
+    if (!e) e = new StreamScratch();
+    ps = e;
+  }
+  StreamScratch& p = *ps;
   if (p.scr_bytes[slot] < bytes) {
-    hipSetDevice(current_device());
+    hipSetDevice(dev);
     if (p.scr[slot]) {
-      hipStreamSynchronize(current_stream());
+      hipStreamSynchronize(st);  // the stream's earlier kernels are the only readers
       hipFree(p.scr[slot]);
     }
     size_t n = bytes < 4096 ? 4096 : bytes;
@@ -309,7 +328,13 @@ void uphip_clear_error(void) {
   t_error.clear();
 }
 void uphip_set_fatal_errors(bool fatal) { g_fatal = fatal; }
-const char* uphip_version(void) { return "unpaper-hip 0.1 (gfx950)"; }
+const char* uphip_version(void) {
+#ifdef UPHIP_DIAG
+  return "unpaper-hip 0.2 (gfx950, diag)";  // tuning build: UPHIP_DIAG_* honoured
+#else
+  return "unpaper-hip 0.2 (gfx950)";
+#endif
+}
 
 size_t uphip_abi_sizeof(const char* name) {
 #define S(T) \

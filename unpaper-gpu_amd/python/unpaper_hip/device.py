@@ -15,7 +15,9 @@ from . import ctypes_abi as A
 from .hostimage import HostImage, min_linesize
 
 _PKG = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-LIB_PATH = os.path.join(_PKG, "lib", "libunpaper_hip.so")
+# UNPAPER_HIP_LIB selects another build of the same library (the `make lib
+# DIAG=1` tuning build); uphip_version() names a diagnostics build.
+LIB_PATH = os.environ.get("UNPAPER_HIP_LIB") or os.path.join(_PKG, "lib", "libunpaper_hip.so")
 
 # every function the header declares (include/unpaper_hip.h)
 EXPORTED = [
@@ -36,7 +38,7 @@ EXPORTED = [
     "uphip_batch_output_info", "uphip_batch_input_ptr", "uphip_batch_set_input",
     "uphip_batch_run_device", "uphip_batch_run", "uphip_batch_wait",
     "uphip_batch_get_output", "uphip_batch_output_ptr", "uphip_batch_get_report",
-    "uphip_batch_kernel_times", "uphip_synth_pages", "uphip_synth_page_host",
+    "uphip_batch_kernel_times", "uphip_batch_set_timing", "uphip_synth_pages", "uphip_synth_page_host",
     "uphip_device_alloc", "uphip_device_free", "uphip_memcpy_htod", "uphip_memcpy_dtoh",
 ]
 
@@ -118,6 +120,7 @@ def load_library(path=LIB_PATH):
         "uphip_batch_get_output": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64]),
         "uphip_batch_output_ptr": (C.c_void_p, [C.c_void_p, C.c_int32, C.POINTER(C.c_int64)]),
         "uphip_batch_get_report": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(A.SheetReport)]),
+        "uphip_batch_set_timing": (C.c_int, [C.c_void_p, C.c_int32]),
         "uphip_batch_kernel_times": (C.c_int, [C.c_void_p, C.POINTER(C.c_char_p),
                                                C.POINTER(C.c_float), C.c_int]),
         "uphip_synth_pages": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int32, C.c_int32,

@@ -7,7 +7,7 @@ import numpy as np
 
 from . import ctypes_abi as A
 from .device import UnpaperHipError, _check, load_library
-from .hostimage import HostImage, min_linesize
+from .hostimage import HostImage
 
 
 def synth_page_host(width, height, page):
@@ -42,7 +42,7 @@ class DeviceBuffer:
 
 
 class Batch:
-    def __init__(self, options, capacity, page_width, page_height, page_format):
+    def __init__(self, options, capacity, page_width, page_height, page_format, timing=False):
         self.lib = L = load_library()
         self.options = options
         self.geometry = A.BatchGeometry(capacity, page_width, page_height, page_format)
@@ -53,6 +53,8 @@ class Batch:
             raise UnpaperHipError("batch_create failed")
         w, h, f, n = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
         L.uphip_batch_output_info(self.handle, C.byref(w), C.byref(h), C.byref(f), C.byref(n))
+        if timing:
+            self.set_timing(True)
         self.out_width, self.out_height, self.out_format = w.value, h.value, f.value
 
     def set_input(self, sheet, page_index, h: HostImage):
@@ -93,6 +95,10 @@ class Batch:
         self.lib.uphip_batch_get_report(self.handle, sheet, C.byref(r))
         return r
 
+    def set_timing(self, enable=True):
+        """Record per-stage HIP events on every run (uphip_batch_set_timing)."""
+        self.lib.uphip_batch_set_timing(self.handle, 1 if enable else 0)
+
     def stage_times(self):
         names = (C.c_char_p * 64)()
         ms = (C.c_float * 64)()
@@ -109,18 +115,3 @@ class Batch:
             self.close()
         except Exception:
             pass
-
-
-def split_outputs(lib_oracle_copy, sheet: HostImage, output_count):
-    """sheet_stages.c:612-624: --output-pages 2 cuts the sheet into halves."""
-    if output_count == 1:
-        return [sheet]
-    w = sheet.width // output_count
-    n = min_linesize(w, sheet.format)
-    outs = []
-    for j in range(output_count):
-        page = HostImage(w, sheet.height, sheet.format, background=sheet.background,
-                         abs_black_threshold=sheet.abs_black_threshold)
-        lib_oracle_copy(sheet, page, j * w)
-        outs.append(page)
-    return outs
