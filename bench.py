@@ -5,28 +5,46 @@ Workload (BASELINE.json configs[2], the metric's configuration): 1000
 deterministic synthetic GRAY8 A4@300dpi pages (2480x3508)
 per GPU, default unpaper options (the full sheet_process.c pipeline:
 blackfilter, noisefilter, blurfilter, grayfilter, mask scan, deskew with
-cubic rotation, mask centering, border scan), processed through the C-ABI
-batch pipeline (uphip_batch_run_device) with a pool of batches on separate
-HIP streams.  The pages are generated straight into HBM before the clock
-starts; outputs stay in HBM (no PCIe inside the timed region).
+cubic rotation, mask centering, border scan), driven by the native runner
+(uphip_runner_*, the lib/batch_worker.c peer): one host thread per device,
+`--streams` batches of `--batch` sheets in flight per device.  The pages are
+generated straight into HBM before the clock starts; `value` counts pages
+processed with inputs and outputs resident in HBM (figure 1 of BASELINE.md
+§3).  Figures 2 (+ H2D/D2H through pinned staging) and 3 (+ PNM write) are
+measured after it with the host-fed runner over the same pages.
 
-One step = one pass of the pipeline over every page of the rank's shard.
-N>1: one process per GPU (torch.distributed.run), pages sharded by rank with
-no data-path collective; the gloo process group only provides the barrier
-and the max-over-ranks of the elapsed time (weak scaling).
+One step = one pass of the pipeline over every page of each device's shard.
+N>1, driver style (torch.distributed.run): one process per GPU, pages sharded
+by rank, no data-path collective; a gloo group only provides the barrier and
+the max-over-ranks of the elapsed time.  N>1 without torchrun (`--gpus N`):
+one process, one runner thread per device (the reference's thread pool bound
+to devices), device d processing pages [d*P, (d+1)*P).
 
-Extra fields: `roofline` for the dominant stage, timed live with the HIP
-events the batch records on its own stream between stages; `cpu_baseline`
-= the oracle's restatement of the reference CPU path, threaded over the host
-cores, on a bounded sample of the same pages (rank 0, N=1 only).
+After the timed region every resident output page with a committed oracle
+hash (tests/golden/bench_hashes.json, tests/golden/make_bench_hashes.py) is
+hashed and compared; a mismatch fails the run.  A library built with the
+timing diagnostics (make lib DIAG=1) or an UPHIP_DIAG_* variable is refused
+unless --tuning (the line then says "valid": false).
+
+Extra fields: `roofline` for the dominant kernel (the bicubic rotation),
+timed with the HIP events its batch records on its own stream around the
+launch; `cpu_baseline` = the oracle's restatement of the reference CPU path
+on the host share of cores (rank 0, N=1 only); `latency_c2` = one A4 page
+alone through the pipeline; `host_io` = figures 2 and 3.
 """
 import argparse
 import ctypes as C
+import hashlib
 import json
 import os
+import shutil
+import statistics
 import sys
+import tempfile
 import threading
 import time
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "unpaper-gpu_amd", "python"))
@@ -35,15 +53,18 @@ sys.path.insert(0, os.path.join(ROOT, "unpaper-gpu_amd", "python"))
 # serves the process; torch is only used for torch.distributed (gloo).
 from unpaper_hip import ctypes_abi as A  # noqa: E402
 from unpaper_hip.device import load_library, UnpaperHipError  # noqa: E402
-from unpaper_hip.pipeline import Batch, DeviceBuffer  # noqa: E402
+from unpaper_hip.pipeline import (Batch, DeviceBuffer, Runner, sink_memory, sink_pnm,  # noqa: E402
+                                  source_memory)
+from unpaper_hip.workloads import A4_H, A4_W, C4_H, C4_W, c4_options  # noqa: E402
 
 METRIC = "pages/sec + Mpixel/s, 1000-page GRAY8 A4@300dpi batch, 1/2/4/8 GPU"
-W, H = 2480, 3508
+W, H = A4_W, A4_H
 HBM_PEAK_GBS = 8000.0                   # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 ALG_BYTES_PER_PAGE = 10 * W * H         # SURVEY.md §8(d) fixed credit (86 998 400 B)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 # Algorithmic HBM bytes per page of each timed stage (DESIGN.md "Kernels"):
-# the bytes the stage must move at minimum, in units of one W*H GRAY8 plane.
+# the bytes the stage must move at minimum, in units of one W*H plane.
 STAGE_PLANES = {
     "decode": 2.0,          # page -> sheet plane (read + write)
     "noisefilter": 1.0,     # classify reads the plane once
@@ -54,10 +75,8 @@ STAGE_PLANES = {
     "masks_center": 1.0,    # column sums over the plane
     "center": 2.0,          # mask move read + write
 }
-
-
 ROOFLINE_STAGE = "deskew_rotate"
-ROOFLINE_KERNEL = "k_rotate_cubic_g8f"
+ROOFLINE_KERNEL = {"c3": "k_rotate_cubic_g8f", "c4": "k_rotate_mask<F_RGB24> (bilinear)"}
 
 
 def parse():
@@ -65,24 +84,34 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--pages", type=int, default=1000, help="pages per GPU")
-    ap.add_argument("--batch", type=int, default=64, help="sheets per batch launch sequence")
-    ap.add_argument("--streams", type=int, default=16, help="batches (HIP streams) in flight")
+    ap.add_argument("--config", default="c3", choices=("c3", "c4"),
+                    help="c3: BASELINE configs[2] (the metric); c4: configs[3], RGB24 600dpi "
+                         "double-page sheets, layout double, bilinear, border wipe")
+    ap.add_argument("--pages", type=int, default=0,
+                    help="pages (c3) / sheets (c4) per GPU (default 1000 / 16)")
+    ap.add_argument("--batch", type=int, default=0, help="sheets per batch (default 64 / 4)")
+    ap.add_argument("--streams", type=int, default=16, help="batches (HIP streams) per device")
     ap.add_argument("--hw-queues", type=int, default=24,
                     help="GPU_MAX_HW_QUEUES for this process (HIP default 4, at most 32)")
     ap.add_argument("--cpu-pages", type=int, default=0,
-                    help="CPU baseline sample (0 = 2 pages per host thread)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, host cores)")
+                    help="CPU baseline sample (0 = 8 pages per host thread)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = the host share: OMP_NUM_THREADS, else os.cpu_count()")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--no-host-io", action="store_true", help="skip figures 2 and 3")
+    ap.add_argument("--no-latency", action="store_true", help="skip the C2 single-page latency")
+    ap.add_argument("--host-batch", type=int, default=32, help="sheets per batch, host-fed runs")
+    ap.add_argument("--host-streams", type=int, default=4, help="batches per device, host-fed")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC HBM bytes per stage launch from a rocprofv3 --pmc pass")
+                    help="PMC HBM bytes per launch / per page from rocprofv3 --pmc passes")
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--probe", type=int, default=3,
                     help="isolated single-stream launches after the timed region that time "
                          "the roofline kernel (0 = use the concurrent timed-region spans)")
-    ap.add_argument("--sweep", default="",
-                    help="tuning only: comma list of BATCHxSTREAMS, each timed over one step "
-                         "and printed to stderr before the main run")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the oracle-hash check of the resident outputs")
+    ap.add_argument("--tuning", action="store_true",
+                    help="allow a diagnostics build / UPHIP_DIAG_* (the line is marked invalid)")
     return ap.parse_args()
 
 
@@ -91,7 +120,6 @@ class Dist:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -102,43 +130,212 @@ class Dist:
         if self.world > 1:
             self.dist.barrier()
 
-    def max(self, v):
+    def _reduce(self, v, op):
         if self.world == 1:
             return v
         import torch
         t = torch.tensor([v], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(t, op=getattr(self.dist.ReduceOp, op))
         return float(t.item())
 
+    def max(self, v):
+        return self._reduce(v, "MAX")
+
     def sum(self, v):
-        if self.world == 1:
-            return v
-        import torch
-        t = torch.tensor([v], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
+        return self._reduce(v, "SUM")
 
     def close(self):
         if self.world > 1:
             self.dist.destroy_process_group()
 
 
-def shard(rank, pages):
-    """Pages of this rank: a contiguous block of the global job list."""
-    return rank * pages, pages
+def shard_plan(world, rank, local_rank, ngpus_flag, ndev, pages):
+    """(devices this process drives, first global page of each, n_gpus of the job)."""
+    if world > 1:
+        return [local_rank % max(ndev, 1)], [rank * pages], world
+    if ngpus_flag > ndev:
+        raise UnpaperHipError("--gpus %d but only %d HIP devices" % (ngpus_flag, ndev))
+    return list(range(ngpus_flag)), [i * pages for i in range(ngpus_flag)], ngpus_flag
 
 
-def cpu_baseline(first_page, npages, threads):
+def diag_guard(version, environ, tuning):
+    """Refuse timing-diagnostics builds and switches (they skip or repeat work).
+    Returns whether the measurement is valid."""
+    env = sorted(k for k in environ if k.startswith("UPHIP_DIAG"))
+    bad = ("diag" in version) or bool(env)
+    if bad and not tuning:
+        raise SystemExit("bench.py: refusing to time a diagnostics build or UPHIP_DIAG_* (%s; %s); "
+                         "use `make lib` without DIAG and unset the variables" % (version, env))
+    return not bad
+
+
+def load_hashes(name, key):
+    try:
+        with open(os.path.join(GOLDEN, name)) as f:
+            return json.load(f).get(key, {})
+    except (OSError, ValueError):
+        return {}
+
+
+def resident_chunks(nchunks, streams):
+    """(batch k, chunk c) pairs whose outputs are resident after a pass: chunk c
+    runs on batch c % streams, so batch k ends with the last chunk of its class."""
+    return [(k, k + ((nchunks - 1 - k) // streams) * streams)
+            for k in range(min(streams, nchunks))]
+
+
+def verify_resident(runner, devices, firsts, npages, bsz, hashes):
+    """Hash every resident output page that has a committed oracle hash."""
+    nchunks = (npages + bsz - 1) // bsz
+    checked = bad = 0
+    for i in range(len(devices)):
+        for k, c in resident_chunks(nchunks, runner.streams):
+            b = runner.batch(i, k)
+            for s in range(min(bsz, npages - c * bsz)):
+                g = str(firsts[i] + c * bsz + s)
+                if g not in hashes:
+                    continue
+                out = b.output(s)
+                checked += 1
+                if hashlib.sha256(out.payload().tobytes()).hexdigest() != hashes[g]:
+                    bad += 1
+                    print("bench: page %s differs from the oracle (device %d batch %d sheet %d)"
+                          % (g, devices[i], k, s), file=sys.stderr)
+    return checked, bad
+
+
+def stage_totals(runner, ndev):
+    totals = {}
+    for i in range(ndev):
+        for k in range(runner.streams):
+            for name, ms in runner.batch(i, k).stage_times():
+                totals[name] = totals.get(name, 0.0) + ms
+    return totals
+
+
+def probe_kernel(runner, shard, n0, stage, count):
+    """Isolated launches of one batch on one stream, the GPU otherwise idle."""
+    b = runner.batch(0, 0)
+    out = []
+    for _ in range(count):
+        b.run_device(n0, shard[0], shard[1], shard[2])
+        b.wait()
+        out.append(sum(ms for name, ms in b.stage_times() if name == stage))
+    return out
+
+
+def traffic_of(path, key, units):
+    try:
+        with open(path) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    per_page = doc.get("bytes_per_page", {}).get(key)
+    return (int(per_page * units) if per_page else None), doc.get("pipeline_bytes_per_page")
+
+
+def device_pages_to_host(L, pages, pitch, stride, npages, w, h, bpp=1):
+    """Copy device-resident pages into a dense host array (outside any clock)."""
+    out = np.empty((npages, h, w * bpp), np.uint8)
+    tmp = np.empty((h, pitch), np.uint8)
+    for p in range(npages):
+        if L.uphip_memcpy_dtoh(tmp.ctypes.data, pages.ptr + p * stride, pitch * h) != 0:
+            raise UnpaperHipError("memcpy_dtoh failed")
+        out[p] = tmp[:, :w * bpp]
+    return out
+
+
+def latency_c2(L, opts, page_host, pages_ptr, pitch, stride, reps=7):
+    """C2 (BASELINE configs[1]): one A4 page alone through the full pipeline
+    on an idle GPU, median of `reps` runs after one warm-up: input resident
+    in HBM, and with the host copies (set_input + run + get_output)."""
+    b = Batch(opts, 1, W, H, A.FMT_GRAY8)
+    try:
+        dev, host = [], []
+        for r in range(reps + 1):
+            t0 = time.perf_counter()
+            b.run_device(1, pages_ptr, pitch, stride)
+            b.wait()
+            if r:
+                dev.append((time.perf_counter() - t0) * 1e3)
+        for r in range(reps + 1):
+            t0 = time.perf_counter()
+            if L.uphip_batch_set_input(b.handle, 0, page_host.ctypes.data, W) != 0:
+                raise UnpaperHipError("set_input failed")
+            b.run(1)
+            b.wait()
+            b.output(0)
+            if r:
+                host.append((time.perf_counter() - t0) * 1e3)
+        return round(statistics.median(dev), 3), round(statistics.median(host), 3)
+    finally:
+        b.close()
+
+
+def host_io(opts, dev0, host_in, npages, args, threads):
+    """Figures 2 and 3 of BASELINE.md §3 on device `dev0`: the pages fed from
+    host RAM through pinned staging (H2D), processed, brought back (D2H) into
+    host RAM; then the same with the sheets written as PGM files (the encode
+    queue) into a tmpfs directory.  One untimed warm-up pass each."""
+    out = {}
+    r = Runner(opts, args.host_batch, W, H, A.FMT_GRAY8, devices=(dev0,),
+               streams=args.host_streams, host_threads=threads)
+    try:
+        host_out = np.empty((npages, H, r.out_linesize), np.uint8)
+        src = source_memory(host_in.ctypes.data, W, W * H, npages, keep=host_in)
+        snk = sink_memory(host_out.ctypes.data, r.out_linesize, r.out_linesize * H, npages,
+                          keep=host_out)
+        for rep in range(2):
+            t0 = time.perf_counter()
+            failed, err = r.run_host(npages, src, snk)
+            t = time.perf_counter() - t0
+            if failed:
+                raise UnpaperHipError("host-fed run: %d failed: %s" % (failed, err))
+        st = r.stats()
+        hashes = load_hashes("bench_hashes.json", "pages")
+        sample = [p for p in range(min(npages, 32)) if str(p) in hashes]
+        ok = sum(hashlib.sha256(np.ascontiguousarray(host_out[p][:, :W]).tobytes()).hexdigest()
+                 == hashes[str(p)] for p in sample)
+        if ok != len(sample):
+            raise SystemExit("bench.py: host-fed outputs differ from the oracle (%d of %d)"
+                             % (len(sample) - ok, len(sample)))
+        out["h2d_d2h"] = {"value": round(npages / t, 2), "unit": "pages/s",
+                          "load_s": round(st.load_s, 3), "store_s": round(st.store_s, 3),
+                          "verified": len(sample)}
+        del host_out, snk
+        tmpdir = tempfile.mkdtemp(prefix="uphip_bench_",
+                                  dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+        try:
+            snk = sink_pnm(os.path.join(tmpdir, "out_%04lld.pgm"), 64)
+            for rep in range(2):
+                t0 = time.perf_counter()
+                failed, err = r.run_host(npages, src, snk)
+                t = time.perf_counter() - t0
+                if failed:
+                    raise UnpaperHipError("PNM run: %d failed: %s" % (failed, err))
+            st = r.stats()
+            out["pnm_write"] = {"value": round(npages / t, 2), "unit": "pages/s",
+                                "load_s": round(st.load_s, 3), "store_s": round(st.store_s, 3),
+                                "files": "PGM (P5) into tmpfs, 64 names reused"}
+        finally:
+            shutil.rmtree(tmpdir, ignore_errors=True)
+        out["config"] = {"sheets_per_batch": args.host_batch, "streams": args.host_streams,
+                         "host_threads": threads, "staging": "pinned, per batch, in + out",
+                         "source": "pages in host RAM (decoded)"}
+    finally:
+        r.close()
+    return out
+
+
+def cpu_baseline(host_pages, npages, threads):
     """The oracle (C restatement of the reference --device=cpu path), one page
     per thread at a time; ctypes releases the GIL inside the C call."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle_py import Oracle
     from unpaper_hip.hostimage import HostImage
-    from unpaper_hip.pipeline import synth_page_host
     oracle = Oracle()
     opts = oracle.default_options()
-    pages = [HostImage.from_array(synth_page_host(W, H, first_page + i), A.FMT_GRAY8)
-             for i in range(npages)]
+    imgs = [HostImage.from_array(host_pages[p], A.FMT_GRAY8) for p in range(npages)]
     nxt = [0]
     lock = threading.Lock()
 
@@ -149,7 +346,7 @@ def cpu_baseline(first_page, npages, threads):
                 nxt[0] += 1
             if i >= npages:
                 return
-            oracle.process_sheet(opts, [pages[i]])
+            oracle.process_sheet(opts, [imgs[i]])
 
     ts = [threading.Thread(target=work) for _ in range(threads)]
     t0 = time.perf_counter()
@@ -160,23 +357,96 @@ def cpu_baseline(first_page, npages, threads):
     return npages / (time.perf_counter() - t0)
 
 
-def time_config(opts, pages, pitch, stride, npages, bsz, nstreams):
-    """Seconds for one pass over the pages with a given batch/stream shape
-    (after one warm-up pass)."""
-    bs = [Batch(opts, bsz, W, H, A.FMT_GRAY8) for _ in range(nstreams)]
-    chunks = [(s, min(bsz, npages - s)) for s in range(0, npages, bsz)]
+def host_threads_share():
+    """Host threads this job may use: the box sets OMP_NUM_THREADS to the
+    GPU's CPU share (os.cpu_count() reports the whole machine there)."""
+    v = os.environ.get("OMP_NUM_THREADS")
     try:
-        for rep in range(2):
-            t0 = time.perf_counter()
-            for i, (s, n) in enumerate(chunks):
-                bs[i % nstreams].run_device(n, pages.ptr + s * stride, pitch, stride)
-            for b in bs:
-                b.wait()
-            t = time.perf_counter() - t0
-        return t
+        return max(1, int(v)) if v else (os.cpu_count() or 1)
+    except ValueError:
+        return os.cpu_count() or 1
+
+
+def run_c4(args, L, d, devices, firsts, n_gpus, version, valid):
+    """BASELINE configs[3]: RGB24 600dpi double-page sheets, layout double,
+    bilinear deskew, border wipe; sheets/s and single-sheet latency."""
+    nsheets = args.pages or 16
+    bsz = max(1, min(args.batch or 4, nsheets))
+    opts = A.Options()
+    L.uphip_options_init(C.byref(opts))
+    c4_options(opts)
+    pitch = (3 * C4_W + 255) // 256 * 256
+    stride = pitch * C4_H
+    L.uphip_set_device(devices[0])
+    pages = DeviceBuffer(stride * nsheets)
+    if L.uphip_synth_sheets_rgb(pages.ptr, pitch, stride, C4_W, C4_H, firsts[0], nsheets) != 0:
+        raise UnpaperHipError("synth_sheets_rgb failed")
+    streams = min(args.streams, max(1, (nsheets + bsz - 1) // bsz))
+    r = Runner(opts, bsz, C4_W, C4_H, A.FMT_RGB24, devices=devices[:1], streams=streams,
+               timing=True)
+    shard = [(pages.ptr, pitch, stride, nsheets)]
+    if args.warmup:
+        r.run_device(shard, passes=args.warmup)
+    stage_totals(r, 1)
+    d.barrier()
+    t0 = time.perf_counter()
+    failed, err = r.run_device(shard, passes=args.steps)
+    d.barrier()
+    elapsed = d.max(time.perf_counter() - t0)
+    if failed:
+        raise UnpaperHipError("c4 run: %s" % err)
+    totals = stage_totals(r, 1)
+    checked = bad = 0
+    if not args.no_verify:
+        checked, bad = verify_resident(r, devices[:1], firsts, nsheets, bsz,
+                                       load_hashes("c4_hashes.json", "sheets"))
+    r.close()
+    # one sheet alone on an idle GPU: latency, and the rotate launch
+    lat, rot = [], []
+    b1 = Batch(opts, 1, C4_W, C4_H, A.FMT_RGB24, timing=True)
+    try:
+        for rep in range(4):
+            t1 = time.perf_counter()
+            b1.run_device(1, pages.ptr, pitch, stride)
+            b1.wait()
+            t2 = time.perf_counter()
+            st = dict(b1.stage_times())
+            if rep:
+                lat.append((t2 - t1) * 1e3)
+                rot.append(st.get(ROOFLINE_STAGE, 0.0))
     finally:
-        for b in bs:
-            b.close()
+        b1.close()
+    pages.close()
+    alg_sheet = 10 * C4_W * C4_H * 3
+    rot_alg = 2 * C4_W * C4_H * 3
+    sheets_s = nsheets * args.steps * n_gpus / elapsed
+    rot_ms = statistics.median(rot) if rot else 0.0
+    ach = rot_alg / (rot_ms * 1e-3) / 1e9 if rot_ms else None
+    if d.rank == 0:
+        print(json.dumps({
+            "metric": "sheets/s and per-sheet latency, RGB24 600dpi double-page scan (C4)",
+            "value": round(sheets_s, 3), "unit": "sheets/s", "n_gpus": n_gpus,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "latency_ms": round(statistics.median(lat), 2),
+            "config": {"workload": "%d synthetic RGB24 9920x7016 double-page sheets per GPU, "
+                                   "layout double, interpolate linear, border 60" % nsheets,
+                       "sheets_per_batch": bsz, "streams": streams},
+            "roofline": {"bound": "hbm", "kernel": ROOFLINE_KERNEL["c4"],
+                         "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
+                         "traffic": None, "avg_launch_ms": round(rot_ms, 3),
+                         "launch_ms_from": "3 single-sheet launches, idle GPU",
+                         "alg_bytes_per_launch": rot_alg,
+                         "pipeline_alg_bytes_per_sheet": alg_sheet,
+                         "pipeline_frac": round(sheets_s / n_gpus * alg_sheet /
+                                                (HBM_PEAK_GBS * 1e9), 5)},
+            "stages_ms_per_step": {k: round(v / args.steps, 2) for k, v in totals.items()},
+            "verified": checked, "mismatches": bad, "library": version, "valid": valid,
+        }), flush=True)
+    if bad:
+        raise SystemExit("bench.py: %d C4 sheets differ from the oracle" % bad)
 
 
 def main():
@@ -188,141 +458,135 @@ def main():
     os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, min(32, args.hw_queues)))
     d = Dist()
     L = load_library()
+    version = L.uphip_version().decode()
+    valid = diag_guard(version, os.environ, args.tuning)
     st = L.uphip_try_init()
     if st != 0:
         raise UnpaperHipError("no HIP device: " + L.uphip_init_status_string(st).decode())
     ndev = L.uphip_device_count()
-    L.uphip_set_device(d.local_rank % max(ndev, 1))
+    npages = args.pages or (16 if args.config == "c4" else 1000)
+    devices, firsts, n_gpus = shard_plan(d.world, d.rank, d.local_rank, args.gpus, ndev, npages)
+    if args.config == "c4":
+        return run_c4(args, L, d, devices, firsts, n_gpus, version, valid)
 
-    first, npages = shard(d.rank, args.pages)
+    bsz = max(1, min(args.batch or 64, npages))
     pitch = (W + 255) // 256 * 256
     stride = pitch * H
-    pages = DeviceBuffer(stride * npages)
-    if L.uphip_synth_pages(pages.ptr, pitch, stride, W, H, first, npages) != 0:
-        raise UnpaperHipError("synth_pages failed")
-
+    bufs, shards = [], []
+    for dev, first in zip(devices, firsts):
+        L.uphip_set_device(dev)
+        buf = DeviceBuffer(stride * npages)
+        if L.uphip_synth_pages(buf.ptr, pitch, stride, W, H, first, npages) != 0:
+            raise UnpaperHipError("synth_pages failed")
+        bufs.append(buf)
+        shards.append((buf.ptr, pitch, stride, npages))
+    L.uphip_set_device(devices[0])
     opts = A.Options()
     L.uphip_options_init(C.byref(opts))     # the reference's defaults (lib/options.c)
-    for cfg in filter(None, args.sweep.split(",")):
-        sb, ss = (int(v) for v in cfg.split("x"))
-        t = time_config(opts, pages, pitch, stride, npages, sb, ss)
-        print("sweep batch %d streams %d: %.1f pages/s" % (sb, ss, npages / t), file=sys.stderr,
-              flush=True)
-    bsz = max(1, min(args.batch, npages))
-    batches = [Batch(opts, bsz, W, H, A.FMT_GRAY8, timing=True) for _ in range(max(1, args.streams))]
-    chunks = [(s, min(bsz, npages - s)) for s in range(0, npages, bsz)]
-    launches = [0]
+    runner = Runner(opts, bsz, W, H, A.FMT_GRAY8, devices=devices, streams=max(1, args.streams),
+                    timing=True)
 
-    def step():
-        for i, (s, n) in enumerate(chunks):
-            batches[i % len(batches)].run_device(n, pages.ptr + s * stride, pitch, stride)
-            launches[0] += 1
-
-    def join():
-        for b in batches:
-            b.wait()
-
-    for _ in range(args.warmup):
-        step()
-    join()
-    for b in batches:
-        b.stage_times()          # drop the warm-up record
-    launches[0] = 0
-
+    if args.warmup:
+        failed, err = runner.run_device(shards, passes=args.warmup)
+        if failed:
+            raise UnpaperHipError("warm-up: %s" % err)
+    stage_totals(runner, len(devices))          # drop the warm-up record
     d.barrier()
-    join()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    join()
+    failed, err = runner.run_device(shards, passes=args.steps)
     d.barrier()
     elapsed = d.max(time.perf_counter() - t0)
-
-    # per-stage device time over the timed region (events on each batch's stream)
-    totals = {}
-    for b in batches:
-        for name, ms in b.stage_times():
-            totals[name] = totals.get(name, 0.0) + ms
-    nlaunch = launches[0]
-    total_pages = d.sum(float(npages * args.steps))
+    if failed:
+        raise UnpaperHipError("timed run: %d failed jobs: %s" % (failed, err))
+    total_pages = d.sum(float(npages * args.steps * len(devices)))
     pages_per_s = total_pages / elapsed
-    mpix = pages_per_s * W * H / 1e6
+    nchunks = (npages + bsz - 1) // bsz
+    nlaunch = nchunks * args.steps * len(devices)
 
+    checked = bad = 0
+    if not args.no_verify:
+        checked, bad = verify_resident(runner, devices, firsts, npages, bsz,
+                                       load_hashes("bench_hashes.json", "pages"))
+        checked, bad = int(d.sum(float(checked))), int(d.sum(float(bad)))
+
+    totals = stage_totals(runner, len(devices))
     roofline = None
-    if totals:
-        # the dominant full-chip kernel: the bicubic rotation (its stage events
-        # bracket exactly that launch); the one-wave/one-block sequential
-        # replays are latency bound and overlap other streams' work
-        dom = ROOFLINE_STAGE if ROOFLINE_STAGE in totals else max(totals, key=totals.get)
+    if ROOFLINE_STAGE in totals:
         # In the timed region `streams` batches share the GPU, so one launch's
-        # event span is stretched by the kernels of the other streams.  The
-        # kernel's own duration comes from probe launches right after the
-        # timed region: the same batch shape on one stream with the GPU
-        # otherwise idle (HIP events on that stream).
-        conc_ms = totals[dom] / max(nlaunch, 1)
-        n0 = chunks[0][1]
-        probe = []
-        for _ in range(args.probe):
-            batches[0].run_device(n0, pages.ptr, pitch, stride)
-            batches[0].wait()
-            probe.append(sum(ms for name, ms in batches[0].stage_times() if name == dom))
+        # event span is stretched by the kernels of the other streams; the
+        # kernel's own duration comes from probe launches right after it: the
+        # same batch shape on one stream with the GPU otherwise idle.
+        conc_ms = totals[ROOFLINE_STAGE] / max(nlaunch, 1)
+        probe = probe_kernel(runner, shards[0], bsz, ROOFLINE_STAGE, args.probe)
         avg_ms = sum(probe) / len(probe) if probe else conc_ms
-        units = n0 if probe else npages * args.steps / max(nlaunch, 1)
-        alg = STAGE_PLANES.get(dom, 1.0) * W * H * units
+        units = bsz if probe else npages * args.steps * len(devices) / max(nlaunch, 1)
+        alg = STAGE_PLANES[ROOFLINE_STAGE] * W * H * units
         achieved = alg / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        traffic = None
-        try:  # HBM bytes per page from the committed rocprofv3 --pmc passes
-            with open(args.traffic) as f:
-                per_page = json.load(f).get("bytes_per_page", {}).get(dom)
-            if per_page:
-                traffic = int(per_page * units)
-        except (OSError, ValueError):
-            pass
+        traffic, pipe_bytes = traffic_of(args.traffic, ROOFLINE_STAGE, units)
         roofline = {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": ROOFLINE_KERNEL if dom == ROOFLINE_STAGE else dom,
+            "kernel": ROOFLINE_KERNEL["c3"],
             "alg_bytes_per_launch": int(alg), "avg_launch_ms": round(avg_ms, 3),
-            "launch_ms_from": ("%d isolated probe launches of %d sheets" % (len(probe), n0)
+            "launch_ms_from": ("%d isolated probe launches of %d sheets" % (len(probe), bsz)
                                if probe else "timed region"),
             "concurrent_avg_launch_ms": round(conc_ms, 3),
-            "pipeline_frac": round(pages_per_s / max(d.world, 1) * ALG_BYTES_PER_PAGE /
+            "pipeline_alg_bytes_per_page": ALG_BYTES_PER_PAGE,
+            "pipeline_hbm_bytes_per_page": pipe_bytes,
+            "pipeline_frac": round(pages_per_s / max(n_gpus, 1) * ALG_BYTES_PER_PAGE /
                                    (HBM_PEAK_GBS * 1e9), 5),
         }
     if args.stages and d.rank == 0:
         for k, v in sorted(totals.items(), key=lambda kv: -kv[1]):
             print("stage %-14s %9.1f ms total %8.3f ms/launch" % (k, v, v / max(nlaunch, 1)),
                   file=sys.stderr)
+    runner.close()
 
-    cpu = None
-    if d.rank == 0 and d.world == 1 and not args.no_cpu:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        n = args.cpu_pages or 2 * threads
-        v = cpu_baseline(first, n, threads)
+    single = d.world == 1 and len(devices) == 1
+    threads = args.cpu_threads or host_threads_share()
+    latency = hio = cpu = None
+    host_pages = None
+    if single and not (args.no_host_io and args.no_cpu and args.no_latency):
+        host_pages = device_pages_to_host(L, bufs[0], pitch, stride, npages, W, H)
+    if single and not args.no_latency:
+        dev_ms, host_ms = latency_c2(L, opts, host_pages[0], bufs[0].ptr, pitch, stride)
+        latency = {"device_ms": dev_ms, "with_pcie_ms": host_ms,
+                   "what": "one A4 GRAY8 page alone, idle GPU, median of 7 (C2)"}
+    if single and not args.no_host_io:
+        hio = host_io(opts, devices[0], host_pages, npages, args, threads)
+    if single and not args.no_cpu:
+        n = min(args.cpu_pages or 8 * threads, npages)
+        v = cpu_baseline(host_pages, n, threads)
         cpu = {"value": round(v, 3), "unit": "pages/s", "cores": threads, "kind": "port",
+               "host_cpus": os.cpu_count(),
                "sample": "%d synthetic A4 GRAY8 pages (the first of the GPU workload), default "
                          "options, oracle/oracle.c on %d host threads" % (n, threads)}
-
-    for b in batches:
+    for b in bufs:
         b.close()
-    pages.close()
     if d.rank == 0:
         out = {
             "metric": METRIC, "value": round(pages_per_s, 2), "unit": "pages/s",
-            "n_gpus": d.world, "steps": args.steps, "warmup": args.warmup,
+            "n_gpus": n_gpus, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "mpixel_per_s": round(mpix, 1),
+            "mpixel_per_s": round(pages_per_s * W * H / 1e6, 1),
             "config": {"workload": "%d synthetic GRAY8 A4@300dpi pages (2480x3508) per GPU, "
-                                   "default pipeline, batch_run_device" % args.pages,
-                       "pages_per_gpu": args.pages, "sheets_per_batch": bsz,
-                       "streams": len(batches),
+                                   "default pipeline, inputs and outputs resident in HBM"
+                                   % npages,
+                       "pages_per_gpu": npages, "sheets_per_batch": bsz,
+                       "streams": max(1, args.streams),
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
-                       "parallelism": "pages sharded, no collective"},
-            "roofline": roofline, "cpu_baseline": cpu,
+                       "parallelism": ("one process per GPU (torchrun), pages sharded"
+                                       if d.world > 1 else
+                                       "one runner thread per device, pages sharded")
+                       + ", no collective"},
+            "roofline": roofline, "cpu_baseline": cpu, "latency_c2": latency, "host_io": hio,
+            "verified": checked, "mismatches": bad, "library": version, "valid": valid,
         }
         print(json.dumps(out), flush=True)
     d.close()
+    if bad:
+        raise SystemExit("bench.py: %d output pages differ from the oracle" % bad)
 
 
 if __name__ == "__main__":

@@ -411,6 +411,114 @@ typedef struct {
 } UphipSheetReport;
 int uphip_batch_get_report(UphipBatch *batch, int32_t sheet,
                            UphipSheetReport *report);
+/* Asynchronous staging for host-fed pipelines (the pinned, double-buffered
+ * staging of src/pipeline/image_pipeline.c:226-376; uphip_runner_* drives
+ * these).  All work is queued on the batch stream; with pinned host buffers
+ * the copies run on the DMA engines and overlap other batches' kernels.
+ *   upload_async:   pages i = 0 .. count*input_count-1 from host + i*page_stride
+ *                   (rows `linesize` apart) into the input slots.
+ *   download_async: every sheet s of the last run into host + s*sheet_stride;
+ *                   only after the run has finished (uphip_batch_query() == 1).
+ *   query:          1 = all queued work done, 0 = running, -1 = error.
+ *   stream:         the batch's hipStream_t (for events). */
+int uphip_batch_upload_async(UphipBatch *batch, int32_t count, const void *host,
+                             int64_t linesize, int64_t page_stride);
+int uphip_batch_download_async(UphipBatch *batch, void *host, int64_t linesize,
+                               int64_t sheet_stride);
+int uphip_batch_query(UphipBatch *batch);
+void *uphip_batch_stream(UphipBatch *batch);
+
+/* ---------------------------------------------------------------------------
+ * Host codec — the PNM half of loadImage/saveImage (file.c:29-259).
+ * P4/P1 -> MONOWHITE, P5/P2 -> GRAY8, P6/P3 -> RGB24 (8-bit samples); writing
+ * GRAY8 -> P5, RGB24 -> P6, MONOWHITE -> P4 (saveImageDirect, file.c:133-176).
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  int32_t width, height, format;
+} UphipPnmInfo;
+int uphip_pnm_probe(const char *path, UphipPnmInfo *info);
+/* Decode into `dst` (rows `linesize` apart); fails when `expect` is given and
+ * the file's geometry differs. */
+int uphip_pnm_read(const char *path, void *dst, int64_t linesize,
+                   const UphipPnmInfo *expect);
+int uphip_pnm_write(const char *path, const void *src, int64_t linesize,
+                    int32_t width, int32_t height, int32_t format);
+
+/* ---------------------------------------------------------------------------
+ * Multi-device runner — the peer of lib/batch_worker.c (batch_process_parallel,
+ * :273) + lib/threadpool.c + the decode/encode queues (lib/decode_queue.c,
+ * lib/encode_queue.c) + the pinned per-stream staging of
+ * src/pipeline/image_pipeline.c:226-376.  One host thread per device, each
+ * with `batches_per_device` batches (HIP streams) of `capacity` sheets in
+ * flight; jobs are pulled in chunks from one shared counter (BatchQueue),
+ * no collective.  Job j reads pages j*input_count .. j*input_count+input_count-1.
+ * ------------------------------------------------------------------------- */
+#define UPHIP_RUNNER_MAX_DEVICES 16
+typedef struct UphipRunner UphipRunner;
+typedef struct UphipSource UphipSource;
+typedef struct UphipSink UphipSink;
+typedef struct {
+  int32_t ndevices;            /* devices used */
+  const int32_t *devices;      /* their ids (NULL = 0 .. ndevices-1) */
+  int32_t batches_per_device;  /* HIP streams (in-flight batches) per device */
+  int32_t host_threads;        /* load/store worker threads (0 = 4 per device) */
+  int32_t timing;              /* stage timing on every batch */
+} UphipRunnerConfig;
+typedef struct {
+  const void *pages;           /* device-resident pages of this device's shard */
+  int64_t pitch, page_stride;
+  int64_t count;               /* sheets (jobs) in the shard */
+} UphipDevicePages;
+typedef struct {
+  int64_t jobs_done, jobs_failed;
+  int64_t jobs_per_device[UPHIP_RUNNER_MAX_DEVICES];
+  double wall_s;               /* last run */
+  double load_s, store_s;      /* summed over the device threads' host phases */
+} UphipRunnerStats;
+/* Sources fill page `page` of job `job` into pinned staging; sinks receive a
+ * finished sheet in the output format (pages side by side for output_count 2).
+ * Called concurrently from host worker threads; return 0 on success. */
+typedef int (*UphipLoadFn)(void *user, int64_t job, int32_t page, void *dst,
+                           int64_t linesize);
+typedef int (*UphipStoreFn)(void *user, int64_t job, const void *sheet,
+                            int64_t linesize, int32_t width, int32_t height,
+                            int32_t format);
+UphipSource *uphip_source_callback(UphipLoadFn load, void *user);
+/* page i at base + i*page_stride, rows `linesize` apart */
+UphipSource *uphip_source_memory(const void *base, int64_t linesize,
+                                 int64_t page_stride, int64_t npages);
+/* page i decoded from paths[i] (PNM) straight into the staging slot */
+UphipSource *uphip_source_pnm(const char *const *paths, int64_t npaths);
+void uphip_source_destroy(UphipSource *source);
+UphipSink *uphip_sink_callback(UphipStoreFn store, void *user);
+UphipSink *uphip_sink_memory(void *base, int64_t linesize, int64_t sheet_stride,
+                             int64_t nsheets);
+/* PNM files: printf(pattern, k) with k = job*output_count + page (mod wrap
+ * when wrap > 0) */
+UphipSink *uphip_sink_pnm(const char *pattern, int64_t wrap);
+UphipSink *uphip_sink_discard(void);
+void uphip_sink_destroy(UphipSink *sink);
+
+UphipRunner *uphip_runner_create(const UphipOptions *options,
+                                 const UphipBatchGeometry *geometry,
+                                 const UphipRunnerConfig *config);
+void uphip_runner_destroy(UphipRunner *runner);
+/* Device-resident shards: device i processes shards[i] in place, `passes`
+ * times back to back without draining between passes (benchmark steps);
+ * chunk c of the shard runs on batch c % batches_per_device, whose outputs
+ * stay resident (uphip_runner_batch).  Returns the number of failed jobs. */
+int uphip_runner_run_device(UphipRunner *runner, const UphipDevicePages *shards,
+                            int32_t passes);
+/* Host-fed run of jobs [0, njobs): source -> pinned staging -> device ->
+ * pinned staging -> sink.  Returns the number of failed jobs. */
+int uphip_runner_run_host(UphipRunner *runner, int64_t njobs, UphipSource *source,
+                          UphipSink *sink);
+int uphip_runner_get_stats(UphipRunner *runner, UphipRunnerStats *stats);
+int uphip_runner_output_info(UphipRunner *runner, int32_t *width, int32_t *height,
+                             int32_t *format, int64_t *linesize);
+UphipBatch *uphip_runner_batch(UphipRunner *runner, int32_t device_index,
+                               int32_t slot);
+
 /* Stage timing (off by default): when on, every run records a HIP event at
  * each stage boundary on the batch stream, kept until
  * uphip_batch_kernel_times() reads and frees them. */
@@ -430,12 +538,21 @@ int uphip_batch_kernel_times(UphipBatch *batch, const char **names, float *ms,
 int uphip_synth_pages(void *device_dst, int64_t pitch, int64_t page_stride,
                       int32_t width, int32_t height, uint32_t first_page,
                       int32_t count);
+/* C4 workload: RGB24 double-page sheets (two W/2 x H pages side by side). */
+int uphip_synth_sheets_rgb(void *device_dst, int64_t pitch, int64_t sheet_stride,
+                           int32_t width, int32_t height, uint32_t first_sheet,
+                           int32_t count);
+void uphip_synth_sheet_rgb_host(uint8_t *host, int64_t linesize, int32_t width,
+                                int32_t height, uint32_t sheet);
 void uphip_synth_page_host(uint8_t *host, int64_t linesize, int32_t width,
                            int32_t height, uint32_t page);
 void *uphip_device_alloc(size_t bytes);
 void uphip_device_free(void *ptr);
 int uphip_memcpy_htod(void *dst, const void *src, size_t bytes);
 int uphip_memcpy_dtoh(void *dst, const void *src, size_t bytes);
+/* Pinned (page-locked) host memory, DMA-capable from every device. */
+void *uphip_host_alloc(size_t bytes);
+void uphip_host_free(void *ptr);
 
 #ifdef __cplusplus
 }

@@ -14,7 +14,11 @@ sharded run (1000 pages per rank), the first 16 pages of each shard.
 Options: the reference defaults (uphip_options_init == lib/options.c).
 Hash: SHA-256 over the output rows' visible bytes (GRAY8, W bytes per row).
 
-usage: python3 tests/golden/make_bench_hashes.py [--threads N]
+C4 (--which c4 -> c4_hashes.json): RGB24 9920x7016 double-page sheets 0 and 1
+(synth.h synth_rgb_channel) with unpaper_hip.workloads.c4_options (layout
+double, bilinear deskew, border wipe); hash over the saved RGB24 rows.
+
+usage: python3 tests/golden/make_bench_hashes.py [--threads N] [--which a4|c4]
 """
 import argparse
 import hashlib
@@ -32,7 +36,8 @@ sys.path.insert(0, os.path.join(ROOT, "unpaper-gpu_amd", "python"))
 from oracle_py import Oracle  # noqa: E402
 from unpaper_hip import ctypes_abi as A  # noqa: E402
 from unpaper_hip.hostimage import HostImage  # noqa: E402
-from unpaper_hip.pipeline import synth_page_host  # noqa: E402
+from unpaper_hip.pipeline import synth_page_host, synth_sheet_rgb_host  # noqa: E402
+from unpaper_hip.workloads import C4_H, C4_W, c4_options  # noqa: E402
 
 W, H = 2480, 3508
 
@@ -52,11 +57,50 @@ def page_hash(oracle, opts, page):
     return hashlib.sha256(out.payload().tobytes()).hexdigest()
 
 
+def c4_hash(oracle, opts, sheet):
+    src = HostImage.from_array(synth_sheet_rgb_host(C4_W, C4_H, sheet), A.FMT_RGB24)
+    out_sheet, fmt, _ = oracle.process_sheet(opts, [src])
+    out = oracle.convert_for_save(out_sheet, fmt)
+    assert (out.width, out.height, out.format) == (C4_W, C4_H, A.FMT_RGB24)
+    return hashlib.sha256(out.payload().tobytes()).hexdigest()
+
+
+def main_c4(args):
+    oracle = Oracle()
+    opts = c4_options(oracle.default_options())
+    res = {}
+    t0 = time.time()
+
+    def work(k):
+        res[k] = c4_hash(oracle, opts, k)
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in (0, 1)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    doc = {
+        "generator": "tests/golden/make_bench_hashes.py --which c4 (oracle/oracle.c, "
+                     "unpaper_hip.workloads.c4_options)",
+        "width": C4_W, "height": C4_H, "format": "RGB24",
+        "hash": "sha256 of visible output rows",
+        "sheets": {str(k): res[k] for k in sorted(res)},
+    }
+    out = os.path.join(HERE, "c4_hashes.json")
+    with open(out, "w") as f:
+        json.dump(doc, f, indent=0)
+        f.write("\n")
+    print("wrote %d C4 hashes to %s in %.0f s" % (len(res), out, time.time() - t0))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 1)
     ap.add_argument("--out", default=os.path.join(HERE, "bench_hashes.json"))
+    ap.add_argument("--which", default="a4", choices=("a4", "c4"))
     args = ap.parse_args()
+    if args.which == "c4":
+        return main_c4(args)
     oracle = Oracle()
     opts = oracle.default_options()
     todo = page_list()

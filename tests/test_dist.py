@@ -2,7 +2,8 @@
 
 bench.py shards pages by rank with no data-path collective; the process group
 only provides the barrier and the max/sum reductions of the timing.  This
-checks that those pieces behave across real processes.
+checks that those pieces behave across real processes, and the single-process
+`--gpus N` plan (one runner thread per device, lib/batch_worker.c peer).
 """
 import os
 import socket
@@ -25,13 +26,16 @@ def _worker(rank, world, port, pages, q):
     sys.path.insert(0, ROOT)
     import bench
     d = bench.Dist()
-    first, n = bench.shard(d.rank, pages)
+    devices, firsts, n_gpus = bench.shard_plan(d.world, d.rank, d.local_rank, 1, 8, pages)
+    assert devices == [rank] and n_gpus == world
+    first, n = firsts[0], pages
     d.barrier()
     mx = d.max(float(rank + 1))
     tot = d.sum(float(n))
+    bad = d.sum(0.0)
     d.barrier()
     d.close()
-    q.put((rank, first, n, mx, tot))
+    q.put((rank, first, n, mx, tot + bad))
 
 
 @pytest.mark.parametrize("world", [2])
@@ -57,3 +61,48 @@ def test_gloo_sharding_and_reductions(world):
     # max over ranks and the whole-job page count are the same on every rank
     assert all(mx == float(world) for _, _, _, mx, _ in res)
     assert all(tot == float(world * pages) for _, _, _, _, tot in res)
+
+
+def test_single_process_device_fanout_plan():
+    sys.path.insert(0, ROOT)
+    import bench
+    devices, firsts, n = bench.shard_plan(1, 0, 0, 4, 8, 1000)
+    assert devices == [0, 1, 2, 3] and firsts == [0, 1000, 2000, 3000] and n == 4
+    with pytest.raises(Exception, match="only 2 HIP devices"):
+        bench.shard_plan(1, 0, 0, 4, 2, 1000)
+
+
+@pytest.mark.parametrize("nchunks,streams", [(16, 16), (16, 4), (4, 16), (5, 2), (1, 1)])
+def test_resident_chunks(nchunks, streams):
+    """The chunk whose outputs each batch still holds after a pass (the bench
+    verifies exactly these pages)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    got = bench.resident_chunks(nchunks, streams)
+    last = {}
+    for c in range(nchunks):
+        last[c % streams] = c
+    assert got == sorted(last.items())
+
+
+def test_diag_guard():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.diag_guard("unpaper-hip 0.2 (gfx950)", {}, False) is True
+    with pytest.raises(SystemExit):
+        bench.diag_guard("unpaper-hip 0.2 (gfx950, diag)", {}, False)
+    with pytest.raises(SystemExit):
+        bench.diag_guard("unpaper-hip 0.2 (gfx950)", {"UPHIP_DIAG_SKIP": "1"}, False)
+    assert bench.diag_guard("unpaper-hip 0.2 (gfx950, diag)", {}, True) is False
+
+
+def test_product_library_has_no_diagnostics():
+    """`make lib` builds without UPHIP_DIAG: the version string says so, and
+    the library does not read the UPHIP_DIAG_* variables at all."""
+    sys.path.insert(0, os.path.join(ROOT, "unpaper-gpu_amd", "python"))
+    from unpaper_hip.device import LIB_PATH, load_library
+    L = load_library()
+    assert "diag" not in L.uphip_version().decode()
+    with open(LIB_PATH, "rb") as f:
+        blob = f.read()
+    assert b"UPHIP_DIAG" not in blob

@@ -1,0 +1,275 @@
+"""The benchmarked configuration, the native runner and C4, on the GPU.
+
+* bench configuration: bench.py itself (16 batches x 64 A4 sheets on their own
+  streams, 24 HW queues, every batch re-run before the wait) in a subprocess
+  (GPU_MAX_HW_QUEUES is read at HIP init); it hashes the resident outputs
+  against tests/golden/bench_hashes.json (oracle, make_bench_hashes.py) and
+  must report every checked page equal.
+* runner (uphip_runner_*, the lib/batch_worker.c + decode/encode queue
+  peer): host-fed runs through pinned staging against the oracle, PNM
+  file-to-file, a failing source job isolated to itself, two runner threads
+  on one device.
+* C4 (BASELINE configs[3]): one RGB24 9920x7016 double-page sheet, layout
+  double, bilinear deskew, border wipe, against the oracle's hash
+  (tests/golden/c4_hashes.json).
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from helpers import assert_same
+from unpaper_hip import ctypes_abi as A
+from unpaper_hip.hostimage import HostImage
+from unpaper_hip.pipeline import (Batch, DeviceBuffer, Runner, pnm_read, pnm_write, sink_memory,
+                                  sink_pnm, source_callback, source_memory, source_pnm,
+                                  synth_page_host)
+from unpaper_hip.workloads import C4_H, C4_W, c4_options
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+SMALL = (620, 877)
+
+
+def _bench(*extra, timeout=300):
+    env = dict(os.environ)
+    for k in list(env):
+        if k.startswith("UPHIP_DIAG"):
+            del env[k]
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-host-io",
+           "--no-latency", "--probe", "0"] + list(extra)
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def test_bench_configuration_matches_oracle():
+    """The exact timed configuration: 1000 pages, 16 x 64-sheet batches, 2
+    passes before the wait; pages 0..255 (the every-4th-page band included)
+    are resident afterwards and hashed."""
+    out = _bench("--steps", "2", "--warmup", "1")
+    assert out["config"]["sheets_per_batch"] == 64 and out["config"]["streams"] == 16
+    assert out["config"]["hw_queues"] == 24
+    assert out["valid"] is True
+    assert out["verified"] == 256 and out["mismatches"] == 0
+
+
+def test_bench_four_streams_rerun_before_wait():
+    """4 batches of 64 over 256 pages, 3 passes enqueued before one wait."""
+    out = _bench("--pages", "256", "--streams", "4", "--steps", "3", "--warmup", "0")
+    assert out["verified"] == 256 and out["mismatches"] == 0
+
+
+def _pages(n, first, w, h):
+    return [HostImage.from_array(synth_page_host(w, h, first + i), A.FMT_GRAY8) for i in range(n)]
+
+
+def _oracle_out(oracle, opts, page):
+    sheet, fmt, _ = oracle.process_sheet(opts, [page])
+    return oracle.convert_for_save(sheet, fmt)
+
+
+def test_runner_host_fed_matches_oracle(hip, oracle):
+    w, h = SMALL
+    n = 11                                   # 3 chunks of 4, the last partial
+    opts = oracle.default_options()
+    pages = _pages(n, 40, w, h)
+    host_in = np.stack([p.payload() for p in pages])
+    r = Runner(opts, 4, w, h, A.FMT_GRAY8, devices=(0,), streams=2, host_threads=3)
+    try:
+        out = np.zeros((n, h, r.out_linesize), np.uint8)
+        src = source_memory(host_in.ctypes.data, w, w * h, n, keep=host_in)
+        snk = sink_memory(out.ctypes.data, r.out_linesize, r.out_linesize * h, n, keep=out)
+        failed, err = r.run_host(n, src, snk)
+        assert failed == 0, err
+        st = r.stats()
+        assert st.jobs_done == n and st.jobs_failed == 0 and st.jobs_per_device[0] == n
+    finally:
+        r.close()
+    for i, p in enumerate(pages):
+        exp = _oracle_out(oracle, opts, p)
+        got = HostImage(w, h, exp.format, out[i])
+        assert_same(got, exp, "runner job %d" % i)
+
+
+def test_runner_pnm_files(hip, oracle, tmp_path):
+    """Decode queue -> device -> encode queue: PGM in, PGM out."""
+    w, h = SMALL
+    n = 5
+    opts = oracle.default_options()
+    pages = _pages(n, 60, w, h)
+    paths = []
+    for i, p in enumerate(pages):
+        q = str(tmp_path / ("in_%d.pgm" % i))
+        pnm_write(q, p)
+        paths.append(q)
+    r = Runner(opts, 2, w, h, A.FMT_GRAY8, devices=(0,), streams=2, host_threads=2)
+    try:
+        failed, err = r.run_host(n, source_pnm(paths), sink_pnm(str(tmp_path / "out_%03lld.pgm")))
+        assert failed == 0, err
+    finally:
+        r.close()
+    for i, p in enumerate(pages):
+        got = pnm_read(str(tmp_path / ("out_%03d.pgm" % i)))
+        assert_same(got, _oracle_out(oracle, opts, p), "pnm job %d" % i)
+
+
+def test_runner_two_outputs_pbm(hip, oracle, tmp_path):
+    """--layout double --output-pages 2 with MONOWHITE output: the encode
+    queue splits every sheet into two PBM pages (sheet_stages.c:606-624)."""
+    w, h = SMALL
+    opts = oracle.default_options()
+    opts.layout = A.LAYOUT_DOUBLE
+    opts.output_count = 2
+    opts.output_pixel_format = A.FMT_MONOWHITE
+    pages = _pages(2, 80, w + 3, h)        # odd half width: unaligned PBM split
+    host_in = np.stack([p.payload() for p in pages])
+    r = Runner(opts, 2, w + 3, h, A.FMT_GRAY8, devices=(0,), streams=1, host_threads=2)
+    try:
+        src = source_memory(host_in.ctypes.data, w + 3, (w + 3) * h, 2, keep=host_in)
+        failed, err = r.run_host(2, src, sink_pnm(str(tmp_path / "p_%lld.pbm")))
+        assert failed == 0, err
+    finally:
+        r.close()
+    for i, p in enumerate(pages):
+        sheet = _oracle_out(oracle, opts, p)
+        half = sheet.width // 2
+        g = sheet.to_gray()
+        for j in range(2):
+            got = pnm_read(str(tmp_path / ("p_%d.pbm" % (2 * i + j))))
+            assert (got.width, got.height, got.format) == (half, h, A.FMT_MONOWHITE)
+            assert np.array_equal(got.to_gray(), g[:, j * half:(j + 1) * half]), (i, j)
+
+
+def test_runner_failed_job_is_isolated(hip, oracle):
+    """A job whose page cannot be loaded fails alone (batch_worker.c:214-231:
+    the job is marked failed, the others complete)."""
+    w, h = SMALL
+    n = 6
+    opts = oracle.default_options()
+    pages = _pages(n, 90, w, h)
+    import ctypes as C
+
+    def load(job, page, dst, linesize):
+        if job == 4:
+            return 1
+        a = pages[job].payload()
+        for y in range(h):
+            C.memmove(dst + y * linesize, a[y].ctypes.data, w)
+        return 0
+
+    r = Runner(opts, 3, w, h, A.FMT_GRAY8, devices=(0,), streams=2, host_threads=2)
+    try:
+        out = np.zeros((n, h, r.out_linesize), np.uint8)
+        snk = sink_memory(out.ctypes.data, r.out_linesize, r.out_linesize * h, n, keep=out)
+        failed, err = r.run_host(n, source_callback(load), snk)
+        assert failed == 1 and "could not be loaded" in err
+        assert r.stats().jobs_done == n - 1
+    finally:
+        r.close()
+    for i in (0, 3, 5):
+        exp = _oracle_out(oracle, opts, pages[i])
+        assert_same(HostImage(w, h, exp.format, out[i]), exp, "job %d" % i)
+    assert not out[4].any()
+
+
+def test_runner_two_threads_one_device(hip, oracle):
+    """Two runner device threads bound to the same GPU (the multi-device
+    fan-out path): disjoint device-resident shards, per-thread batches."""
+    w, h = SMALL
+    n = 6
+    opts = oracle.default_options()
+    pitch = (w + 255) // 256 * 256
+    bufs = []
+    for first in (100, 200):
+        b = DeviceBuffer(pitch * h * n)
+        assert b.lib.uphip_synth_pages(b.ptr, pitch, pitch * h, w, h, first, n) == 0
+        bufs.append(b)
+    r = Runner(opts, 4, w, h, A.FMT_GRAY8, devices=(0, 0), streams=2)
+    try:
+        failed, err = r.run_device([(b.ptr, pitch, pitch * h, n) for b in bufs], passes=2)
+        assert failed == 0, err
+        st = r.stats()
+        assert st.jobs_per_device[0] == 2 * n and st.jobs_per_device[1] == 2 * n
+        # chunk 0 (sheets 0..3) ran last on batch 0, chunk 1 (4..5) on batch 1
+        for i, first in enumerate((100, 200)):
+            for k, (c0, cnt) in enumerate(((0, 4), (4, 2))):
+                b = r.batch(i, k)
+                for s in range(cnt):
+                    exp = _oracle_out(oracle, opts, _pages(1, first + c0 + s, w, h)[0])
+                    assert_same(b.output(s), exp, "thread %d sheet %d" % (i, c0 + s))
+    finally:
+        r.close()
+        for b in bufs:
+            b.close()
+
+
+def test_output_right_after_run_monowhite(hip, oracle):
+    """output() straight after run(), no wait, with a converted
+    (MONOWHITE) output: the read must be ordered after the output kernel."""
+    w, h = SMALL
+    opts = oracle.default_options()
+    opts.output_pixel_format = A.FMT_MONOWHITE
+    pages = _pages(3, 7, w, h)
+    b = Batch(opts, 3, w, h, A.FMT_GRAY8)
+    try:
+        for s, p in enumerate(pages):
+            b.set_input(s, 0, p)
+        b.run(3)
+        outs = [b.output(s) for s in range(3)]
+    finally:
+        b.close()
+    for s, p in enumerate(pages):
+        assert_same(outs[s], _oracle_out(oracle, opts, p), "sheet %d" % s)
+
+
+def _c4_hashes():
+    with open(os.path.join(GOLDEN, "c4_hashes.json")) as f:
+        return json.load(f)["sheets"]
+
+
+def test_c4_double_page_rgb_matches_oracle(hip):
+    """BASELINE configs[3]: RGB24 600dpi double-page scans through the full
+    pipeline (layout double, bilinear deskew, border wipe)."""
+    import ctypes as C
+    L = hip.lib
+    opts = A.Options()
+    L.uphip_options_init(C.byref(opts))
+    c4_options(opts)
+    pitch = (3 * C4_W + 255) // 256 * 256
+    buf = DeviceBuffer(pitch * C4_H * 2)
+    assert L.uphip_synth_sheets_rgb(buf.ptr, pitch, pitch * C4_H, C4_W, C4_H, 0, 2) == 0
+    b = Batch(opts, 2, C4_W, C4_H, A.FMT_RGB24)
+    try:
+        b.run_device(2, buf.ptr, pitch, pitch * C4_H)
+        b.wait()
+        want = _c4_hashes()
+        for s in range(2):
+            out = b.output(s)
+            assert (out.width, out.height, out.format) == (C4_W, C4_H, A.FMT_RGB24)
+            assert hashlib.sha256(out.payload().tobytes()).hexdigest() == want[str(s)], s
+            rep = b.report(s)
+            assert rep.mask_count == 2            # one mask per page of the double layout
+    finally:
+        b.close()
+        buf.close()
+
+
+def test_c4_synth_device_matches_host(hip):
+    """The C4 generator is identical on host and device (a band of rows)."""
+    from unpaper_hip.pipeline import synth_sheet_rgb_host
+    w, h = 998, 64
+    pitch = (3 * w + 255) // 256 * 256
+    buf = DeviceBuffer(pitch * h)
+    L = buf.lib
+    assert L.uphip_synth_sheets_rgb(buf.ptr, pitch, pitch * h, w, h, 3, 1) == 0
+    host = np.empty((h, pitch), np.uint8)
+    assert L.uphip_memcpy_dtoh(host.ctypes.data, buf.ptr, host.nbytes) == 0
+    assert np.array_equal(host[:, :3 * w], synth_sheet_rgb_host(w, h, 3).reshape(h, 3 * w))
+    buf.close()

@@ -1325,6 +1325,66 @@ int uphip_batch_get_report(UphipBatch* b, int32_t sheet, UphipSheetReport* r) {
   return 0;
 }
 
+void* uphip_batch_stream(UphipBatch* b) { return b ? (void*)b->st : nullptr; }
+
+int uphip_batch_query(UphipBatch* b) {
+  if (!b) return -1;
+  hipSetDevice(b->device);
+  const hipError_t e = hipStreamQuery(b->st);
+  if (e == hipSuccess) return 1;
+  if (e == hipErrorNotReady) return 0;
+  return check_hip(e, "hipStreamQuery"), -1;
+}
+
+int uphip_batch_upload_async(UphipBatch* b, int32_t count, const void* host, int64_t linesize,
+                             int64_t page_stride) {
+  if (!b || !host || count <= 0 || count > b->cap)
+    return fail("batch_upload_async: bad arguments"), -1;
+  const int64_t rb = row_bytes(b->geo.page_width, b->geo.page_format);
+  if (linesize < rb) return fail("batch_upload_async: linesize too small"), -1;
+  hipSetDevice(b->device);
+  const int64_t n = (int64_t)count * b->n_in;
+  const uint8_t* h = (const uint8_t*)host;
+  if (linesize == b->in_pitch && page_stride == b->in_page_stride)  // staging laid out like the slots
+    return UPH_HIP(hipMemcpyAsync(b->inputs, h, (size_t)(n * page_stride), hipMemcpyHostToDevice,
+                                  b->st))
+               ? 0
+               : -1;
+  for (int64_t i = 0; i < n; i++)
+    if (!UPH_HIP(hipMemcpy2DAsync(b->inputs + i * b->in_page_stride, b->in_pitch,
+                                  h + i * page_stride, linesize, rb, b->geo.page_height,
+                                  hipMemcpyHostToDevice, b->st)))
+      return -1;
+  return 0;
+}
+
+int uphip_batch_download_async(UphipBatch* b, void* host, int64_t linesize, int64_t sheet_stride) {
+  if (!b || !host || b->last_count <= 0) return fail("batch_download_async: nothing to download"), -1;
+  const int64_t rb = row_bytes(b->out_w, b->out_fmt);
+  if (linesize < rb) return fail("batch_download_async: linesize too small"), -1;
+  hipSetDevice(b->device);
+  const hipError_t q = hipStreamQuery(b->st);
+  if (q == hipErrorNotReady) return fail("batch_download_async: the run has not finished"), -1;
+  if (!check_hip(q, "hipStreamQuery")) return -1;
+  const int n = b->last_count;
+  // which plane holds each sheet (ctl[s].cur; the stream is idle)
+  std::vector<int32_t> cur((size_t)n, 0);
+  if (!b->out &&
+      !UPH_HIP(hipMemcpy2D(cur.data(), sizeof(int32_t), &b->ctl[0].cur, sizeof(SheetCtl),
+                           sizeof(int32_t), n, hipMemcpyDeviceToHost)))
+    return -1;
+  uint8_t* h = (uint8_t*)host;
+  for (int s = 0; s < n; s++) {
+    const uint8_t* src = b->out ? b->out + (int64_t)s * b->out_stride
+                                : b->planes[cur[s] & 1] + (int64_t)s * b->plane_stride;
+    const int64_t sp = b->out ? b->out_pitch : b->pitch;
+    if (!UPH_HIP(hipMemcpy2DAsync(h + s * sheet_stride, linesize, src, sp, rb, b->out_h,
+                                  hipMemcpyDeviceToHost, b->st)))
+      return -1;
+  }
+  return 0;
+}
+
 int uphip_batch_set_timing(UphipBatch* b, int32_t enable) {
   if (!b) return -1;
   b->timing = enable != 0;

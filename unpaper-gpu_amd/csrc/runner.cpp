@@ -1,0 +1,662 @@
+// runner.cpp — multi-device batch scheduler: the MI355X peer of the reference's
+// lib/batch_worker.c + lib/threadpool.c + the decode/encode queues
+// (lib/decode_queue.c, lib/encode_queue.c) and the pinned per-stream staging of
+// src/pipeline/image_pipeline.c:226-376.
+//
+// Reference: batch_process_parallel (batch_worker.c:273) submits every job to
+// a thread pool; each worker binds a CUDA stream from the pool
+// (batch_worker.c:197-212) and runs process_sheet on one sheet.  Jobs are
+// independent (fresh SheetProcessState per job, sheet_process.c:29-84), so
+// pages shard across devices with no collective.
+//
+// Here: one host thread per device, each owning K batches (= K HIP streams,
+// K in-flight launch sequences of S sheets).  Jobs are pulled in chunks of S
+// from one shared counter (BatchQueue peer), so a faster device takes more.
+// Host-fed runs move every chunk through a slot's pinned staging:
+//   load (host pool: source -> pinned in)   [decode queue peer]
+//   H2D + pipeline + D2H on the slot stream [DMA engines + CUs]
+//   store (host pool: pinned out -> sink)   [encode queue peer]
+// with K slots per device in flight, so the host work of one slot overlaps the
+// device work of the others.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <memory>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "runtime.h"
+
+using Clock = std::chrono::steady_clock;
+
+namespace uph {
+namespace {
+
+double secs(Clock::time_point a, Clock::time_point b) {
+  return std::chrono::duration<double>(b - a).count();
+}
+
+// Fixed-size host thread pool with a blocking parallel-for; the calling
+// thread works too, so a pool shared by several device threads cannot
+// deadlock.
+class HostPool {
+ public:
+  explicit HostPool(int n) {
+    for (int i = 0; i < n; i++) th_.emplace_back([this] { loop(); });
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void parallel_for(int n, const std::function<void(int)>& fn) {
+    if (n <= 0) return;
+    struct Group {
+      std::atomic<int> next{0};
+      std::atomic<int> left;
+      std::mutex mu;
+      std::condition_variable cv;
+    };
+    auto g = std::make_shared<Group>();
+    g->left = n;
+    auto body = [g, n, &fn] {
+      for (;;) {
+        const int i = g->next.fetch_add(1);
+        if (i >= n) return;
+        fn(i);
+        if (g->left.fetch_sub(1) == 1) {
+          std::lock_guard<std::mutex> lk(g->mu);
+          g->cv.notify_all();
+        }
+      }
+    };
+    const int helpers = std::min<int>(n - 1, (int)th_.size());
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (int i = 0; i < helpers; i++) q_.push_back(body);
+    }
+    cv_.notify_all();
+    body();
+    std::unique_lock<std::mutex> lk(g->mu);
+    g->cv.wait(lk, [&] { return g->left.load() == 0; });
+    // queued helpers that start after this point find no index left and
+    // return without touching `fn`
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<void()> t;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (stop_ && q_.empty()) return;
+        t = std::move(q_.front());
+        q_.pop_front();
+      }
+      t();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::deque<std::function<void()>> q_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+};
+
+}  // namespace
+}  // namespace uph
+
+using namespace uph;
+
+// ---------------------------------------------------------------------------
+// sources and sinks
+// ---------------------------------------------------------------------------
+struct UphipSource {
+  UphipLoadFn load = nullptr;
+  void* user = nullptr;
+  // built-ins
+  const uint8_t* base = nullptr;
+  int64_t linesize = 0, page_stride = 0, npages = 0;
+  std::vector<std::string> paths;
+};
+
+struct UphipSink {
+  UphipStoreFn store = nullptr;
+  void* user = nullptr;
+  uint8_t* base = nullptr;
+  int64_t linesize = 0, sheet_stride = 0, nsheets = 0;
+  std::string pattern;
+  int64_t wrap = 0;
+};
+
+namespace {
+
+int mem_load(const UphipSource* s, int64_t idx, void* dst, int64_t linesize,
+             const UphipPnmInfo& geo) {
+  if (idx < 0 || idx >= s->npages) return fail("source_memory: page %lld out of range", (long long)idx), -1;
+  const int64_t rb = row_bytes(geo.width, geo.format);
+  const uint8_t* src = s->base + idx * s->page_stride;
+  uint8_t* d = (uint8_t*)dst;
+  if (linesize == s->linesize && linesize == rb) {
+    memcpy(d, src, (size_t)(rb * geo.height));
+  } else {
+    for (int32_t y = 0; y < geo.height; y++)
+      memcpy(d + (int64_t)y * linesize, src + (int64_t)y * s->linesize, (size_t)rb);
+  }
+  return 0;
+}
+
+int pnm_load(const UphipSource* s, int64_t idx, void* dst, int64_t linesize,
+             const UphipPnmInfo& geo) {
+  if (idx < 0 || idx >= (int64_t)s->paths.size())
+    return fail("source_pnm: page %lld out of range", (long long)idx), -1;
+  return uphip_pnm_read(s->paths[(size_t)idx].c_str(), dst, linesize, &geo);
+}
+
+}  // namespace
+
+extern "C" {
+
+UphipSource* uphip_source_callback(UphipLoadFn load, void* user) {
+  if (!load) return fail("source_callback: null function"), nullptr;
+  UphipSource* s = new UphipSource();
+  s->load = load;
+  s->user = user;
+  return s;
+}
+
+UphipSource* uphip_source_memory(const void* base, int64_t linesize, int64_t page_stride,
+                                 int64_t npages) {
+  if (!base || npages <= 0) return fail("source_memory: bad arguments"), nullptr;
+  UphipSource* s = new UphipSource();
+  s->base = (const uint8_t*)base;
+  s->linesize = linesize;
+  s->page_stride = page_stride;
+  s->npages = npages;
+  return s;
+}
+
+UphipSource* uphip_source_pnm(const char* const* paths, int64_t npaths) {
+  if (!paths || npaths <= 0) return fail("source_pnm: no files"), nullptr;
+  UphipSource* s = new UphipSource();
+  for (int64_t i = 0; i < npaths; i++) s->paths.emplace_back(paths[i] ? paths[i] : "");
+  return s;
+}
+
+void uphip_source_destroy(UphipSource* s) { delete s; }
+
+UphipSink* uphip_sink_callback(UphipStoreFn store, void* user) {
+  if (!store) return fail("sink_callback: null function"), nullptr;
+  UphipSink* k = new UphipSink();
+  k->store = store;
+  k->user = user;
+  return k;
+}
+
+UphipSink* uphip_sink_memory(void* base, int64_t linesize, int64_t sheet_stride, int64_t nsheets) {
+  if (!base || nsheets <= 0) return fail("sink_memory: bad arguments"), nullptr;
+  UphipSink* k = new UphipSink();
+  k->base = (uint8_t*)base;
+  k->linesize = linesize;
+  k->sheet_stride = sheet_stride;
+  k->nsheets = nsheets;
+  return k;
+}
+
+UphipSink* uphip_sink_pnm(const char* pattern, int64_t wrap) {
+  if (!pattern) return fail("sink_pnm: null pattern"), nullptr;
+  UphipSink* k = new UphipSink();
+  k->pattern = pattern;
+  k->wrap = wrap;
+  return k;
+}
+
+UphipSink* uphip_sink_discard(void) { return new UphipSink(); }
+
+void uphip_sink_destroy(UphipSink* k) { delete k; }
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// runner
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Slot {
+  UphipBatch* b = nullptr;
+  uint8_t* hin = nullptr;   // pinned input staging (count * input_count pages)
+  uint8_t* hout = nullptr;  // pinned output staging (count sheets)
+  int64_t first = 0;        // first job of the chunk in flight
+  int32_t count = 0;
+  std::vector<char> failed;  // per sheet of the chunk
+};
+
+struct DeviceCtx {
+  int device = 0;
+  std::vector<Slot> slots;
+  // per-run results
+  int64_t done = 0, failed = 0;
+  double busy_s = 0;
+  std::string error;
+};
+
+}  // namespace
+
+struct UphipRunner {
+  UphipOptions opts;
+  UphipBatchGeometry geo;  // capacity = sheets per batch
+  UphipRunnerConfig cfg;
+  std::vector<int> devices;
+  std::vector<DeviceCtx> dev;
+  HostPool* pool = nullptr;
+  int32_t out_w = 0, out_h = 0, out_fmt = 0;
+  int64_t in_pitch = 0, in_page_stride = 0;   // batch input slot layout (= staging layout)
+  int64_t out_linesize = 0, out_sheet_stride = 0;
+  bool staged = false;  // pinned staging allocated
+  UphipRunnerStats stats{};
+};
+
+namespace {
+
+void store_sheet(UphipRunner* r, const UphipSink* k, int64_t job, const uint8_t* sheet, bool* ok) {
+  const int oc = r->opts.output_count < 1 ? 1 : r->opts.output_count;
+  if (k->store) {
+    if (k->store(k->user, job, sheet, r->out_linesize, r->out_w, r->out_h, r->out_fmt) != 0) *ok = false;
+    return;
+  }
+  const int64_t rb = row_bytes(r->out_w, r->out_fmt);
+  if (k->base) {
+    if (job < 0 || job >= k->nsheets) {
+      *ok = fail("sink_memory: sheet %lld out of range", (long long)job);
+      return;
+    }
+    uint8_t* d = k->base + job * k->sheet_stride;
+    for (int32_t y = 0; y < r->out_h; y++)
+      memcpy(d + (int64_t)y * k->linesize, sheet + (int64_t)y * r->out_linesize, (size_t)rb);
+    return;
+  }
+  if (k->pattern.empty()) return;  // discard
+  // output pages side by side in the sheet (sheet_stages.c:606-624)
+  const int32_t pw = r->out_w / oc;
+  const int64_t prb = row_bytes(pw, r->out_fmt);
+  std::vector<uint8_t> tmp;
+  for (int j = 0; j < oc; j++) {
+    int64_t idx = job * oc + j;
+    if (k->wrap > 0) idx %= k->wrap;
+    char path[4096];
+    snprintf(path, sizeof(path), k->pattern.c_str(), (long long)idx);
+    const uint8_t* src = sheet;
+    int64_t ls = r->out_linesize;
+    const bool mono = r->out_fmt == UPHIP_FMT_MONOWHITE || r->out_fmt == UPHIP_FMT_MONOBLACK;
+    if (j > 0 || (oc > 1 && mono && (pw & 7))) {  // a page of its own (fresh padding bits)
+      const int64_t x0 = (int64_t)j * pw;
+      tmp.assign((size_t)(prb * r->out_h), 0);
+      for (int32_t y = 0; y < r->out_h; y++) {
+        const uint8_t* row = sheet + (int64_t)y * r->out_linesize;
+        uint8_t* t = tmp.data() + (int64_t)y * prb;
+        if (mono) {
+          for (int32_t x = 0; x < pw; x++) {
+            const int64_t sx = x0 + x;
+            if (row[sx >> 3] & (0x80 >> (sx & 7))) t[x >> 3] |= (uint8_t)(0x80 >> (x & 7));
+          }
+        } else {
+          const int64_t bpp = row_bytes(1, r->out_fmt);
+          memcpy(t, row + x0 * bpp, (size_t)prb);
+        }
+      }
+      src = tmp.data();
+      ls = prb;
+    }
+    if (uphip_pnm_write(path, src, ls, pw, r->out_h, r->out_fmt) != 0) *ok = false;
+  }
+}
+
+bool load_page(UphipRunner* r, const UphipSource* s, int64_t job, int32_t j, uint8_t* dst) {
+  const UphipPnmInfo geo{r->geo.page_width, r->geo.page_height, r->geo.page_format};
+  const int64_t idx = job * r->opts.input_count + j;
+  if (s->load) return s->load(s->user, job, j, dst, r->in_pitch) == 0;
+  if (s->base) return mem_load(s, idx, dst, r->in_pitch, geo) == 0;
+  return pnm_load(s, idx, dst, r->in_pitch, geo) == 0;
+}
+
+// per-sheet device status after a finished run: a failing wait names the
+// sheets through their reports
+void collect_failures(Slot& sl) {
+  sl.failed.assign((size_t)sl.count, 0);
+  if (uphip_batch_wait(sl.b) == 0) return;
+  uphip_clear_error();
+  for (int s = 0; s < sl.count; s++) {
+    UphipSheetReport rep;
+    if (uphip_batch_get_report(sl.b, s, &rep) != 0 || rep.flags) sl.failed[(size_t)s] = 1;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+UphipRunner* uphip_runner_create(const UphipOptions* options, const UphipBatchGeometry* geometry,
+                                 const UphipRunnerConfig* config) {
+  if (!options || !geometry || !config) return fail("runner_create: null argument"), nullptr;
+  if (!runtime_ready()) return fail("runner_create: no HIP device"), nullptr;
+  const int ndev_all = uphip_device_count();
+  if (config->ndevices <= 0 || config->batches_per_device <= 0 || geometry->capacity <= 0)
+    return fail("runner_create: invalid configuration"), nullptr;
+  UphipRunner* r = new UphipRunner();
+  r->opts = *options;
+  r->geo = *geometry;
+  r->cfg = *config;
+  for (int i = 0; i < config->ndevices; i++) {
+    const int d = config->devices ? config->devices[i] : i;
+    if (d < 0 || d >= ndev_all) {
+      delete r;
+      return fail("runner_create: device %d out of range (%d devices)", d, ndev_all), nullptr;
+    }
+    r->devices.push_back(d);
+  }
+  const int caller_dev = uphip_get_device();
+  r->dev.resize(r->devices.size());
+  bool ok = true;
+  for (size_t i = 0; ok && i < r->devices.size(); i++) {
+    DeviceCtx& dc = r->dev[i];
+    dc.device = r->devices[i];
+    if (uphip_set_device(dc.device) != 0) {
+      ok = false;
+      break;
+    }
+    dc.slots.resize((size_t)config->batches_per_device);
+    for (Slot& sl : dc.slots) {
+      sl.b = uphip_batch_create(options, geometry);
+      if (!sl.b) {
+        ok = false;
+        break;
+      }
+      if (config->timing) uphip_batch_set_timing(sl.b, 1);
+    }
+  }
+  uphip_set_device(caller_dev);
+  if (!ok) {
+    uphip_runner_destroy(r);
+    return nullptr;
+  }
+  UphipBatch* b0 = r->dev[0].slots[0].b;
+  int64_t bytes = 0;
+  uphip_batch_output_info(b0, &r->out_w, &r->out_h, &r->out_fmt, &bytes);
+  uphip_batch_input_ptr(b0, 0, &r->in_pitch);
+  r->in_page_stride = r->in_pitch * geometry->page_height;
+  r->out_linesize = round_pitch(row_bytes(r->out_w, r->out_fmt));
+  r->out_sheet_stride = r->out_linesize * r->out_h;
+  const int ht = config->host_threads > 0 ? config->host_threads : 4 * (int)r->devices.size();
+  r->pool = new HostPool(ht - 1 > 0 ? ht - 1 : 0);
+  return r;
+}
+
+void uphip_runner_destroy(UphipRunner* r) {
+  if (!r) return;
+  delete r->pool;
+  for (DeviceCtx& dc : r->dev) {
+    uphip_set_device(dc.device);
+    for (Slot& sl : dc.slots) {
+      if (sl.b) uphip_batch_destroy(sl.b);
+      if (sl.hin) hipHostFree(sl.hin);
+      if (sl.hout) hipHostFree(sl.hout);
+    }
+  }
+  delete r;
+}
+
+UphipBatch* uphip_runner_batch(UphipRunner* r, int32_t device_index, int32_t slot) {
+  if (!r || device_index < 0 || device_index >= (int)r->dev.size() || slot < 0 ||
+      slot >= (int)r->dev[(size_t)device_index].slots.size())
+    return nullptr;
+  return r->dev[(size_t)device_index].slots[(size_t)slot].b;
+}
+
+int uphip_runner_run_device(UphipRunner* r, const UphipDevicePages* shards, int32_t passes) {
+  if (!r || !shards || passes < 1) return fail("runner_run_device: bad arguments"), -1;
+  const auto t0 = Clock::now();
+  const int S = r->geo.capacity;
+  std::vector<std::thread> th;
+  for (size_t i = 0; i < r->dev.size(); i++) {
+    th.emplace_back([r, i, S, shards, passes] {
+      DeviceCtx& dc = r->dev[i];
+      dc.done = dc.failed = 0;
+      dc.error.clear();
+      const auto a = Clock::now();
+      uphip_set_device(dc.device);
+      const UphipDevicePages& sh = shards[i];
+      const int64_t nin = r->opts.input_count;
+      int k = 0;
+      std::vector<int32_t> used(dc.slots.size(), 0);
+      for (int32_t pass = 0; pass < passes; pass++, k = 0)
+      for (int64_t first = 0; first < sh.count; first += S, k++) {
+        const int32_t n = (int32_t)std::min<int64_t>(S, sh.count - first);
+        Slot& sl = dc.slots[(size_t)k % dc.slots.size()];
+        if (uphip_batch_run_device(sl.b, n, (const uint8_t*)sh.pages + first * nin * sh.page_stride,
+                                   sh.pitch, sh.page_stride) != 0) {
+          if (dc.error.empty()) dc.error = uphip_last_error() ? uphip_last_error() : "run failed";
+          uphip_clear_error();
+          dc.failed += n;
+          continue;
+        }
+        used[(size_t)k % dc.slots.size()] = n;
+        dc.done += n;
+      }
+      for (size_t s = 0; s < dc.slots.size(); s++) {
+        if (!used[s]) continue;
+        if (uphip_batch_wait(dc.slots[s].b) != 0) {
+          if (dc.error.empty()) dc.error = uphip_last_error() ? uphip_last_error() : "wait failed";
+          uphip_clear_error();
+          dc.failed += 1;  // at least one sheet; the sticky status does not say how many
+        }
+      }
+      dc.busy_s = secs(a, Clock::now());
+    });
+  }
+  for (auto& t : th) t.join();
+  memset(&r->stats, 0, sizeof(r->stats));
+  int64_t failed = 0;
+  std::string err;
+  for (DeviceCtx& dc : r->dev) {
+    r->stats.jobs_done += dc.done;
+    r->stats.jobs_failed += dc.failed;
+    failed += dc.failed;
+    if (err.empty() && !dc.error.empty()) err = dc.error;
+  }
+  for (size_t i = 0; i < r->dev.size() && i < UPHIP_RUNNER_MAX_DEVICES; i++)
+    r->stats.jobs_per_device[i] = r->dev[i].done;
+  r->stats.wall_s = secs(t0, Clock::now());
+  if (!err.empty()) fail("runner: %s", err.c_str());
+  return (int)std::min<int64_t>(failed, 1 << 30);
+}
+
+int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, UphipSink* sink) {
+  if (!r || !src || !sink || njobs < 0) return fail("runner_run_host: bad arguments"), -1;
+  const int S = r->geo.capacity;
+  const int nin = r->opts.input_count;
+  if (!r->staged) {  // pinned staging per slot, laid out like the batch's input slots
+    for (DeviceCtx& dc : r->dev) {
+      uphip_set_device(dc.device);
+      for (Slot& sl : dc.slots) {
+        if (!UPH_HIP(hipHostMalloc((void**)&sl.hin, (size_t)(r->in_page_stride * S * nin),
+                                   hipHostMallocDefault)) ||
+            !UPH_HIP(hipHostMalloc((void**)&sl.hout, (size_t)(r->out_sheet_stride * S),
+                                   hipHostMallocDefault)))
+          return -1;
+      }
+    }
+    r->staged = true;
+  }
+  const auto t0 = Clock::now();
+  std::atomic<int64_t> next{0};
+  std::atomic<int64_t> load_ns{0}, store_ns{0};
+  std::vector<std::thread> th;
+  for (size_t i = 0; i < r->dev.size(); i++) {
+    th.emplace_back([&, i] {
+      DeviceCtx& dc = r->dev[i];
+      dc.done = dc.failed = 0;
+      dc.error.clear();
+      uphip_set_device(dc.device);
+      auto note = [&dc](const char* what) {
+        if (dc.error.empty()) dc.error = uphip_last_error() ? uphip_last_error() : what;
+        uphip_clear_error();
+      };
+      std::deque<Slot*> freel, running, draining;
+      for (Slot& sl : dc.slots) freel.push_back(&sl);
+      for (;;) {
+        // 1. fill every free slot: load the chunk into pinned memory (host
+        //    pool), then H2D + pipeline on the slot's stream
+        while (!freel.empty()) {
+          const int64_t first = next.fetch_add(S);
+          if (first >= njobs) break;
+          Slot* sl = freel.front();
+          freel.pop_front();
+          sl->first = first;
+          sl->count = (int32_t)std::min<int64_t>(S, njobs - first);
+          sl->failed.assign((size_t)sl->count, 0);
+          std::vector<char> bad((size_t)sl->count, 0);
+          const auto a = Clock::now();
+          r->pool->parallel_for(sl->count * nin, [&](int t) {
+            const int s = t / nin, j = t % nin;
+            uint8_t* dst = sl->hin + (int64_t)t * r->in_page_stride;
+            if (!load_page(r, src, first + s, j, dst)) {
+              bad[(size_t)s] = 1;
+              uphip_clear_error();
+              // the slot still runs: give it a blank (white) page, cheap and
+              // deterministic, instead of stale staging bytes
+              memset(dst, r->geo.page_format == UPHIP_FMT_MONOWHITE ? 0x00 : 0xFF,
+                     (size_t)r->in_page_stride);
+            }
+          });
+          load_ns += (int64_t)(secs(a, Clock::now()) * 1e9);
+          for (int s = 0; s < sl->count; s++)
+            if (bad[(size_t)s]) {
+              sl->failed[(size_t)s] = 1;
+              if (dc.error.empty()) dc.error = "a page could not be loaded";
+            }
+          if (uphip_batch_upload_async(sl->b, sl->count, sl->hin, r->in_pitch, r->in_page_stride) != 0 ||
+              uphip_batch_run(sl->b, sl->count) != 0) {
+            note("run failed");
+            dc.failed += sl->count;
+            freel.push_back(sl);
+            continue;
+          }
+          running.push_back(sl);
+        }
+        // 2. a finished run: its status, then the D2H of its sheets on its stream;
+        // 3. a finished download: the sheets go to the sink (host pool).
+        // Ready work first; when nothing is ready, block on the oldest download
+        // (short) or else the oldest run.
+        auto drain = [&](Slot* sl) {
+          std::vector<char> pre = sl->failed;
+          collect_failures(*sl);  // synchronises the slot stream
+          for (size_t s = 0; s < pre.size(); s++) sl->failed[s] |= pre[s];
+          if (uphip_batch_download_async(sl->b, sl->hout, r->out_linesize, r->out_sheet_stride) != 0) {
+            note("download failed");
+            dc.failed += sl->count;
+            freel.push_back(sl);
+            return;
+          }
+          draining.push_back(sl);
+        };
+        auto store = [&](Slot* sl) {
+          if (uphip_batch_wait(sl->b) != 0) note("download failed");
+          std::vector<char> ok((size_t)sl->count, 1);
+          const auto a = Clock::now();
+          r->pool->parallel_for(sl->count, [&](int s) {
+            if (sl->failed[(size_t)s]) return;
+            bool good = true;
+            store_sheet(r, sink, sl->first + s, sl->hout + (int64_t)s * r->out_sheet_stride, &good);
+            if (!good) {
+              ok[(size_t)s] = 0;
+              uphip_clear_error();
+            }
+          });
+          store_ns += (int64_t)(secs(a, Clock::now()) * 1e9);
+          for (int s = 0; s < sl->count; s++) {
+            if (sl->failed[(size_t)s] || !ok[(size_t)s]) {
+              dc.failed++;
+              if (!ok[(size_t)s] && dc.error.empty()) dc.error = "a sheet could not be stored";
+            } else {
+              dc.done++;
+            }
+          }
+          freel.push_back(sl);
+        };
+        if (!draining.empty() && uphip_batch_query(draining.front()->b) == 1) {
+          Slot* sl = draining.front();
+          draining.pop_front();
+          store(sl);
+          continue;
+        }
+        if (!running.empty() && uphip_batch_query(running.front()->b) == 1) {
+          Slot* sl = running.front();
+          running.pop_front();
+          drain(sl);
+          continue;
+        }
+        if (!draining.empty()) {
+          Slot* sl = draining.front();
+          draining.pop_front();
+          store(sl);
+          continue;
+        }
+        if (!running.empty()) {
+          Slot* sl = running.front();
+          running.pop_front();
+          drain(sl);
+          continue;
+        }
+        if (running.empty() && draining.empty()) break;
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  memset(&r->stats, 0, sizeof(r->stats));
+  int64_t failed = 0;
+  std::string err;
+  for (size_t i = 0; i < r->dev.size(); i++) {
+    DeviceCtx& dc = r->dev[i];
+    r->stats.jobs_done += dc.done;
+    r->stats.jobs_failed += dc.failed;
+    if (i < UPHIP_RUNNER_MAX_DEVICES) r->stats.jobs_per_device[i] = dc.done;
+    failed += dc.failed;
+    if (err.empty() && !dc.error.empty()) err = dc.error;
+  }
+  r->stats.load_s = load_ns.load() * 1e-9;
+  r->stats.store_s = store_ns.load() * 1e-9;
+  r->stats.wall_s = secs(t0, Clock::now());
+  if (!err.empty()) fail("runner: %s", err.c_str());
+  return (int)std::min<int64_t>(failed, 1 << 30);
+}
+
+int uphip_runner_get_stats(UphipRunner* r, UphipRunnerStats* out) {
+  if (!r || !out) return -1;
+  *out = r->stats;
+  return 0;
+}
+
+int uphip_runner_output_info(UphipRunner* r, int32_t* width, int32_t* height, int32_t* format,
+                             int64_t* linesize) {
+  if (!r) return -1;
+  if (width) *width = r->out_w;
+  if (height) *height = r->out_h;
+  if (format) *format = r->out_fmt;
+  if (linesize) *linesize = r->out_linesize;
+  return 0;
+}
+
+}  // extern "C"

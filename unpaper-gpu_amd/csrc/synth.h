@@ -90,4 +90,17 @@ SYNTH_FN uint8_t synth_pixel(uint32_t page, int32_t W, int32_t H, int32_t x, int
   return val;
 }
 
+/* BASELINE configs[3] (C4): a 600 dpi RGB24 double-page scan, W x H = two
+ * pages of W/2 x H side by side (pages 2*sheet and 2*sheet + 1), each channel
+ * darkened by a per-page tint of 0..8 levels. */
+SYNTH_FN uint8_t synth_rgb_channel(uint32_t sheet, int32_t W, int32_t H, int32_t x, int32_t y,
+                                   int ch) {
+  const int32_t half = W / 2;
+  const int right = x >= half;
+  const uint32_t pg = 2u * sheet + (uint32_t)right;
+  const uint8_t v = synth_pixel(pg, half, H, x - (right ? half : 0), y);
+  const uint8_t t = (uint8_t)(synth_h(pg, 9, (uint64_t)ch, 0) % 9);
+  return v >= t ? (uint8_t)(v - t) : 0;
+}
+
 #endif

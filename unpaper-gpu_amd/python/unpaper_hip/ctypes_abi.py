@@ -206,6 +206,48 @@ class SheetReport(C.Structure):
     ]
 
 
+class PnmInfo(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("format", C.c_int32)]
+
+
+RUNNER_MAX_DEVICES = 16
+
+
+class RunnerConfig(C.Structure):
+    _fields_ = [
+        ("ndevices", C.c_int32),
+        ("devices", C.POINTER(C.c_int32)),
+        ("batches_per_device", C.c_int32),
+        ("host_threads", C.c_int32),
+        ("timing", C.c_int32),
+    ]
+
+
+class DevicePages(C.Structure):
+    _fields_ = [
+        ("pages", C.c_void_p),
+        ("pitch", C.c_int64),
+        ("page_stride", C.c_int64),
+        ("count", C.c_int64),
+    ]
+
+
+class RunnerStats(C.Structure):
+    _fields_ = [
+        ("jobs_done", C.c_int64),
+        ("jobs_failed", C.c_int64),
+        ("jobs_per_device", C.c_int64 * RUNNER_MAX_DEVICES),
+        ("wall_s", C.c_double),
+        ("load_s", C.c_double),
+        ("store_s", C.c_double),
+    ]
+
+
+LoadFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64)
+StoreFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int32,
+                      C.c_int32, C.c_int32)
+
+
 class BatchGeometry(C.Structure):
     _fields_ = [
         ("capacity", C.c_int32),

@@ -39,7 +39,15 @@ EXPORTED = [
     "uphip_batch_run_device", "uphip_batch_run", "uphip_batch_wait",
     "uphip_batch_get_output", "uphip_batch_output_ptr", "uphip_batch_get_report",
     "uphip_batch_kernel_times", "uphip_batch_set_timing", "uphip_synth_pages", "uphip_synth_page_host",
+    "uphip_synth_sheets_rgb", "uphip_synth_sheet_rgb_host",
     "uphip_device_alloc", "uphip_device_free", "uphip_memcpy_htod", "uphip_memcpy_dtoh",
+    "uphip_batch_upload_async", "uphip_batch_download_async", "uphip_batch_query",
+    "uphip_batch_stream", "uphip_pnm_probe", "uphip_pnm_read", "uphip_pnm_write",
+    "uphip_source_callback", "uphip_source_memory", "uphip_source_pnm", "uphip_source_destroy",
+    "uphip_sink_callback", "uphip_sink_memory", "uphip_sink_pnm", "uphip_sink_discard",
+    "uphip_sink_destroy", "uphip_runner_create", "uphip_runner_destroy",
+    "uphip_runner_run_device", "uphip_runner_run_host", "uphip_runner_get_stats",
+    "uphip_runner_output_info", "uphip_runner_batch", "uphip_host_alloc", "uphip_host_free",
 ]
 
 
@@ -127,6 +135,40 @@ def load_library(path=LIB_PATH):
                                         C.c_uint32, C.c_int32]),
         "uphip_synth_page_host": (None, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32,
                                          C.c_uint32]),
+        "uphip_batch_upload_async": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64,
+                                               C.c_int64]),
+        "uphip_batch_download_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64]),
+        "uphip_batch_query": (C.c_int, [C.c_void_p]),
+        "uphip_batch_stream": (C.c_void_p, [C.c_void_p]),
+        "uphip_pnm_probe": (C.c_int, [C.c_char_p, C.POINTER(A.PnmInfo)]),
+        "uphip_pnm_read": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int64, C.POINTER(A.PnmInfo)]),
+        "uphip_pnm_write": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32,
+                                      C.c_int32]),
+        "uphip_source_callback": (C.c_void_p, [A.LoadFn, C.c_void_p]),
+        "uphip_source_memory": (C.c_void_p, [C.c_void_p, C.c_int64, C.c_int64, C.c_int64]),
+        "uphip_source_pnm": (C.c_void_p, [C.POINTER(C.c_char_p), C.c_int64]),
+        "uphip_source_destroy": (None, [C.c_void_p]),
+        "uphip_sink_callback": (C.c_void_p, [A.StoreFn, C.c_void_p]),
+        "uphip_sink_memory": (C.c_void_p, [C.c_void_p, C.c_int64, C.c_int64, C.c_int64]),
+        "uphip_sink_pnm": (C.c_void_p, [C.c_char_p, C.c_int64]),
+        "uphip_sink_discard": (C.c_void_p, []),
+        "uphip_sink_destroy": (None, [C.c_void_p]),
+        "uphip_runner_create": (C.c_void_p, [C.POINTER(A.Options), C.POINTER(A.BatchGeometry),
+                                             C.POINTER(A.RunnerConfig)]),
+        "uphip_runner_destroy": (None, [C.c_void_p]),
+        "uphip_runner_run_device": (C.c_int, [C.c_void_p, C.POINTER(A.DevicePages), C.c_int32]),
+        "uphip_runner_run_host": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]),
+        "uphip_runner_get_stats": (C.c_int, [C.c_void_p, C.POINTER(A.RunnerStats)]),
+        "uphip_runner_output_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32),
+                                               C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                               C.POINTER(C.c_int64)]),
+        "uphip_runner_batch": (C.c_void_p, [C.c_void_p, C.c_int32, C.c_int32]),
+        "uphip_host_alloc": (C.c_void_p, [C.c_size_t]),
+        "uphip_host_free": (None, [C.c_void_p]),
+        "uphip_synth_sheets_rgb": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int32,
+                                             C.c_int32, C.c_uint32, C.c_int32]),
+        "uphip_synth_sheet_rgb_host": (None, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32,
+                                              C.c_uint32]),
         "uphip_device_alloc": (C.c_void_p, [C.c_size_t]),
         "uphip_device_free": (None, [C.c_void_p]),
         "uphip_memcpy_htod": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),

@@ -18,6 +18,14 @@ def synth_page_host(width, height, page):
     return arr
 
 
+def synth_sheet_rgb_host(width, height, sheet):
+    """C4 synthetic RGB24 double-page sheet (synth.h synth_rgb_channel), host copy."""
+    L = load_library()
+    arr = np.empty((height, width, 3), np.uint8)
+    L.uphip_synth_sheet_rgb_host(arr.ctypes.data, width * 3, width, height, sheet)
+    return arr
+
+
 class DeviceBuffer:
     """Raw HBM allocation (bench inputs)."""
 
@@ -115,3 +123,176 @@ class Batch:
             self.close()
         except Exception:
             pass
+
+
+class HostBuffer:
+    """Pinned host memory (uphip_host_alloc) viewed as a numpy uint8 array."""
+
+    def __init__(self, nbytes):
+        self.lib = load_library()
+        self.ptr = self.lib.uphip_host_alloc(nbytes)
+        _check(self.lib)
+        if not self.ptr:
+            raise UnpaperHipError("host_alloc failed")
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(self.ptr))
+
+    def close(self):
+        if self.ptr:
+            self.array = None
+            self.lib.uphip_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Runner:
+    """Multi-device runner (uphip_runner_*): the peer of lib/batch_worker.c's
+    batch_process_parallel with one host thread and `streams` batches of
+    `sheets` sheets per device; sources/sinks are the decode/encode queues."""
+
+    def __init__(self, options, sheets, page_width, page_height, page_format, devices=(0,),
+                 streams=4, host_threads=0, timing=False):
+        self.lib = L = load_library()
+        self.options = options
+        self.geometry = A.BatchGeometry(sheets, page_width, page_height, page_format)
+        self._devs = (C.c_int32 * len(devices))(*devices)
+        self.config = A.RunnerConfig(len(devices), self._devs, streams, host_threads,
+                                     1 if timing else 0)
+        self.ndevices = len(devices)
+        self.streams = streams
+        self.handle = L.uphip_runner_create(C.byref(options), C.byref(self.geometry),
+                                            C.byref(self.config))
+        _check(L)
+        if not self.handle:
+            raise UnpaperHipError("runner_create failed")
+        w, h, f, ls = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
+        L.uphip_runner_output_info(self.handle, C.byref(w), C.byref(h), C.byref(f), C.byref(ls))
+        self.out_width, self.out_height, self.out_format = w.value, h.value, f.value
+        self.out_linesize = ls.value
+
+    def batch(self, device_index, slot):
+        """The Batch object behind one stream (borrowed; not closed here)."""
+        h = self.lib.uphip_runner_batch(self.handle, device_index, slot)
+        if not h:
+            raise UnpaperHipError("no such batch")
+        b = Batch.__new__(Batch)
+        b.lib, b.options, b.capacity, b.handle = self.lib, self.options, self.geometry.capacity, h
+        b.out_width, b.out_height, b.out_format = self.out_width, self.out_height, self.out_format
+        b.close = lambda: None
+        return b
+
+    def run_device(self, shards, passes=1):
+        """shards: one (device_ptr, pitch, page_stride, count) per device.
+        Returns (failed jobs, the library's error message or None)."""
+        arr = (A.DevicePages * self.ndevices)(*[A.DevicePages(*s) for s in shards])
+        failed = self.lib.uphip_runner_run_device(self.handle, arr, passes)
+        err = self.lib.uphip_last_error()
+        self.lib.uphip_clear_error()
+        return failed, (err.decode() if err else None)
+
+    def run_host(self, njobs, source, sink):
+        failed = self.lib.uphip_runner_run_host(self.handle, njobs, source.handle, sink.handle)
+        err = self.lib.uphip_last_error()
+        self.lib.uphip_clear_error()
+        return failed, (err.decode() if err else None)
+
+    def stats(self):
+        s = A.RunnerStats()
+        self.lib.uphip_runner_get_stats(self.handle, C.byref(s))
+        return s
+
+    def close(self):
+        if self.handle:
+            self.lib.uphip_runner_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class _Handle:
+    def __init__(self, handle, destroy, keep=()):
+        self.handle = handle
+        self._destroy = destroy
+        self._keep = keep          # buffers / callbacks the C side points into
+
+    def close(self):
+        if self.handle:
+            self._destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def source_memory(ptr, linesize, page_stride, npages, keep=None):
+    L = load_library()
+    h = L.uphip_source_memory(ptr, linesize, page_stride, npages)
+    _check(L)
+    return _Handle(h, L.uphip_source_destroy, (keep,))
+
+
+def source_pnm(paths):
+    L = load_library()
+    arr = (C.c_char_p * len(paths))(*[p.encode() for p in paths])
+    h = L.uphip_source_pnm(arr, len(paths))
+    _check(L)
+    return _Handle(h, L.uphip_source_destroy, (arr,))
+
+
+def source_callback(fn):
+    """fn(job, page, dst_ptr, linesize) -> 0 on success (called from C threads)."""
+    L = load_library()
+    cb = A.LoadFn(lambda user, job, page, dst, ls: fn(job, page, dst, ls))
+    h = L.uphip_source_callback(cb, None)
+    _check(L)
+    return _Handle(h, L.uphip_source_destroy, (cb,))
+
+
+def sink_memory(ptr, linesize, sheet_stride, nsheets, keep=None):
+    L = load_library()
+    h = L.uphip_sink_memory(ptr, linesize, sheet_stride, nsheets)
+    _check(L)
+    return _Handle(h, L.uphip_sink_destroy, (keep,))
+
+
+def sink_pnm(pattern, wrap=0):
+    L = load_library()
+    h = L.uphip_sink_pnm(pattern.encode(), wrap)
+    _check(L)
+    return _Handle(h, L.uphip_sink_destroy)
+
+
+def sink_discard():
+    L = load_library()
+    return _Handle(L.uphip_sink_discard(), L.uphip_sink_destroy)
+
+
+def pnm_write(path, h: HostImage):
+    L = load_library()
+    arr = np.ascontiguousarray(h.data)
+    if L.uphip_pnm_write(path.encode(), arr.ctypes.data, arr.shape[1], h.width, h.height,
+                         h.format) != 0:
+        _check(L)
+
+
+def pnm_read(path) -> HostImage:
+    L = load_library()
+    info = A.PnmInfo()
+    if L.uphip_pnm_probe(path.encode(), C.byref(info)) != 0:
+        _check(L)
+    img = HostImage(info.width, info.height, info.format)
+    if L.uphip_pnm_read(path.encode(), img.data.ctypes.data, img.linesize, C.byref(info)) != 0:
+        _check(L)
+    return img
