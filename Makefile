@@ -2,6 +2,9 @@
 #   make            -> both
 #   make lib        -> unpaper-gpu_amd/lib/libunpaper_hip.so   (product)
 #   make oracle     -> oracle/_build/liboracle.so              (test infrastructure)
+#   make ctest      -> tests/c/_build/backend_ops              (C caller of the vtable; test)
+#   make sanitize   -> tests/c/_build/sanitize: the oracle + the host codec
+#                      under ASan/UBSan (host code only, no GPU)
 #   make lib DIAG=1 -> the same library with the timing diagnostics of
 #                      csrc/common.h (UPHIP_DIAG_*) compiled in; tuning only,
 #                      built into its own object dir.  The default build has none.
@@ -41,11 +44,19 @@ HIPFLAGS   := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
               -Wno-pass-failed  # occupancy hints tuned for GRAY8 miss on RGB instantiations
 CFLAGS_O   := -O2 -std=gnu11 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result
 
-.PHONY: all lib oracle clean
-all: lib oracle
+CTEST      := tests/c/_build/backend_ops
+
+SANITIZE   := tests/c/_build/sanitize
+LLVMCC     := /opt/rocm/lib/llvm/bin/clang
+SANFLAGS   := -fsanitize=address,undefined -fno-sanitize-recover=undefined \
+              -fno-omit-frame-pointer -g -O1
+
+.PHONY: all lib oracle ctest sanitize clean
+all: lib oracle ctest
 
 lib: $(LIB)
 oracle: $(ORACLE_LIB)
+ctest: $(CTEST)
 
 $(OBJDIR)/%.hip.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -67,5 +78,28 @@ $(ORACLE_LIB): oracle/oracle.c oracle/oracle.h include/unpaper_hip.h
 	@mkdir -p oracle/_build
 	$(CC) $(CFLAGS_O) -shared -o $@ oracle/oracle.c -lm
 
+# A plain C program: the reference's own callers are C (sheet_stages.c).
+$(CTEST): tests/c/backend_ops.c include/unpaper_hip.h oracle/oracle.h $(LIB) $(ORACLE_LIB)
+	@mkdir -p tests/c/_build
+	$(CC) -O2 -std=gnu11 -Wall -Iinclude $< -o $@ \
+	  -L$(PKG)/lib -L oracle/_build -lunpaper_hip -loracle -lm \
+	  -Wl,-rpath,'$$ORIGIN/../../../$(PKG)/lib' -Wl,-rpath,'$$ORIGIN/../../../oracle/_build'
+
+# One compiler (ROCm clang) for every object so that one sanitizer runtime
+# serves the program; the HIP sources are compiled for the host only.
+$(SANITIZE): tests/c/sanitize_main.c oracle/oracle.c oracle/oracle.h $(CSRC)/pnm.cpp \
+             $(CSRC)/runtime.hip $(HDRS)
+	@mkdir -p tests/c/_build/san
+	$(LLVMCC) $(SANFLAGS) -std=gnu11 -ffp-contract=off -c oracle/oracle.c -o tests/c/_build/san/oracle.o
+	$(LLVMCC) $(SANFLAGS) -std=gnu11 -Iinclude -c tests/c/sanitize_main.c -o tests/c/_build/san/main.o
+	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
+	  -Iinclude -I$(CSRC) -c $(CSRC)/pnm.cpp -o tests/c/_build/san/pnm.o
+	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
+	  -Iinclude -I$(CSRC) -c $(CSRC)/runtime.hip -o tests/c/_build/san/runtime.o
+	$(HIPCC) $(SANFLAGS) tests/c/_build/san/*.o -o $@ -lm
+
+sanitize: $(SANITIZE)
+	ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=print_stacktrace=1 $(SANITIZE) $(CURDIR)/tests/c/_build/san
+
 clean:
-	rm -rf $(PKG)/build $(PKG)/build_diag $(PKG)/lib $(PKG)/lib_diag oracle/_build
+	rm -rf $(PKG)/build $(PKG)/build_diag $(PKG)/lib $(PKG)/lib_diag oracle/_build tests/c/_build

@@ -291,6 +291,12 @@ const char *uphip_last_error(void);    /* NULL when no error since clear */
 void uphip_clear_error(void);
 void uphip_set_fatal_errors(bool fatal);
 const char *uphip_version(void);
+/* Layout introspection for the drop-in check: sizeof of a UphipXxx type and
+ * offsetof of one of its fields ("scan_depth.horizontal", "vertex[1].x"),
+ * (size_t)-1 if unknown; compared with the reference headers' layout in
+ * tests/test_abi.py (tests/golden/abi_layout.json). */
+size_t uphip_abi_sizeof(const char *type);
+size_t uphip_abi_offsetof(const char *type, const char *field);
 
 /* ---------------------------------------------------------------------------
  * Per-sheet options — lib/options.h:32-127 (processing subset) plus the

@@ -1,0 +1,101 @@
+/* sanitize_main.c — host code under AddressSanitizer + UndefinedBehavior-
+ * Sanitizer: the oracle's whole sheet pipeline on synthetic
+ * pages in every input format and layout, plus the product library's host
+ * PNM codec (pnm.cpp) on well-formed and malformed files.  No GPU involved.
+ * Built and run by `make sanitize` (tests/test_sanitize.py).
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/unpaper_hip.h"
+#include "../../oracle/oracle.h"
+#include "../../unpaper-gpu_amd/csrc/synth.h"
+
+static int g_fail;
+
+static OImage page(int fmt, int w, int h, uint32_t seed) {
+  OImage im = o_create_image((UphipRectangleSize){w, h}, fmt, false, (UphipPixel){255, 255, 255},
+                             170);
+  for (int y = 0; y < h; y++) {
+    uint8_t *row = im.data + (int64_t)y * im.linesize;
+    if (fmt >= UPHIP_FMT_MONOWHITE) memset(row, 0, (size_t)im.linesize);
+    for (int x = 0; x < w; x++) {
+      const uint8_t v = synth_pixel(seed, w, h, x, y);
+      if (fmt == UPHIP_FMT_GRAY8) row[x] = v;
+      else if (fmt == UPHIP_FMT_Y400A) { row[2 * x] = v; row[2 * x + 1] = 255; }
+      else if (fmt == UPHIP_FMT_RGB24) { row[3 * x] = v; row[3 * x + 1] = v / 2 + 100; row[3 * x + 2] = v; }
+      else if ((v < 128) == (fmt == UPHIP_FMT_MONOWHITE)) row[x >> 3] |= (uint8_t)(0x80 >> (x & 7));
+    }
+  }
+  return im;
+}
+
+static void sheet(const char *what, UphipOptions *o, int fmt, int w, int h, uint32_t seed) {
+  OImage pages[2] = {page(fmt, w, h, seed), page(fmt, w, h, seed + 1)};
+  OImage out;
+  int32_t ofmt = 0;
+  OReport rep;
+  if (o_process_sheet(o, pages, &out, &ofmt, &rep) != 0) {
+    fprintf(stderr, "process_sheet failed: %s\n", what);
+    g_fail++;
+  } else {
+    OImage saved = o_convert_for_save(out, ofmt);
+    o_free_image(&saved);
+    o_free_image(&out);
+  }
+  o_free_image(&pages[0]);
+  o_free_image(&pages[1]);
+}
+
+static void codec(const char *dir) {
+  char path[512];
+  snprintf(path, sizeof path, "%s/s.pgm", dir);
+  uint8_t img[7 * 5];
+  for (int i = 0; i < 35; i++) img[i] = (uint8_t)(i * 7);
+  if (uphip_pnm_write(path, img, 7, 7, 5, UPHIP_FMT_GRAY8) != 0) g_fail++;
+  uint8_t back[8 * 5];
+  UphipPnmInfo info;
+  if (uphip_pnm_probe(path, &info) != 0 || uphip_pnm_read(path, back, 8, &info) != 0) g_fail++;
+  for (int y = 0; y < 5; y++)
+    if (memcmp(back + 8 * y, img + 7 * y, 7)) g_fail++;
+  static const char *bad[] = {"P5\n4 4\n255\n\x01", "P6 99999999999 1 255 ", "P2 2 2 255 1 2 x",
+                              "P1 9 1 1 0 1", "P4\n16 2\n\xff", "P3 1 1 255", "#", ""};
+  for (size_t i = 0; i < sizeof bad / sizeof *bad; i++) {
+    snprintf(path, sizeof path, "%s/b%zu.pnm", dir, i);
+    FILE *f = fopen(path, "wb");
+    fwrite(bad[i], 1, strlen(bad[i]), f);
+    fclose(f);
+    uint8_t buf[64];
+    UphipPnmInfo want = {4, 4, UPHIP_FMT_GRAY8};
+    (void)uphip_pnm_probe(path, &info);
+    if (uphip_pnm_read(path, buf, 16, &want) == 0) {
+      fprintf(stderr, "malformed file %zu accepted\n", i);
+      g_fail++;
+    }
+    uphip_clear_error();
+  }
+}
+
+int main(int argc, char **argv) {
+  const char *dir = argc > 1 ? argv[1] : "/tmp";
+  UphipOptions o;
+  o_options_init(&o);
+  for (int fmt = UPHIP_FMT_GRAY8; fmt <= UPHIP_FMT_MONOBLACK; fmt++)
+    sheet("default", &o, fmt, 310, 440, 3);
+  o.layout = UPHIP_LAYOUT_DOUBLE;
+  o.interpolate_type = UPHIP_INTERP_LINEAR;
+  sheet("double", &o, UPHIP_FMT_RGB24, 420, 300, 7);
+  o.input_count = 2;
+  o.output_count = 2;
+  sheet("two pages", &o, UPHIP_FMT_GRAY8, 240, 330, 11);
+  o_options_init(&o);
+  o.interpolate_type = UPHIP_INTERP_NN;
+  o.pre_rotate = 90;
+  o.post_mirror = (UphipDirection){true, false};
+  o.noisefilter_intensity = 9;
+  sheet("geometry", &o, UPHIP_FMT_GRAY8, 300, 420, 15);
+  codec(dir);
+  printf("sanitize: %d failures\n", g_fail);
+  return g_fail ? 1 : 0;
+}

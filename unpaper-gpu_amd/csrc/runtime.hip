@@ -344,9 +344,88 @@ size_t uphip_abi_sizeof(const char* name) {
   S(UphipBlackfilterParameters) S(UphipBlurfilterParameters) S(UphipGrayfilterParameters)
   S(UphipMaskDetectionParameters) S(UphipMaskAlignmentParameters)
   S(UphipBorderScanParameters) S(UphipDeskewParameters) S(UphipOptions)
-  S(UphipSheetReport) S(UphipBatchGeometry)
+  S(UphipSheetReport) S(UphipBatchGeometry) S(UphipImage) S(UphipInterpolation) S(UphipLayout)
+  S(UphipRunnerConfig) S(UphipDevicePages) S(UphipRunnerStats) S(UphipPnmInfo)
 #undef S
   return 0;
+}
+
+size_t uphip_abi_offsetof(const char* type, const char* field) {
+  // every field of the value types the reference's backend.h signatures use
+  // (tests/golden/abi_layout.json holds the reference headers' offsets)
+  if (!type || !field) return (size_t)-1;
+#define O(T, F) \
+  if (!strcmp(type, #T) && !strcmp(field, #F)) return __builtin_offsetof(T, F);
+  O(UphipPoint, x)
+  O(UphipPoint, y)
+  O(UphipDelta, horizontal)
+  O(UphipDelta, vertical)
+  O(UphipDirection, horizontal)
+  O(UphipDirection, vertical)
+  O(UphipEdges, left)
+  O(UphipEdges, top)
+  O(UphipEdges, right)
+  O(UphipEdges, bottom)
+  O(UphipPixel, r)
+  O(UphipPixel, g)
+  O(UphipPixel, b)
+  O(UphipRectangle, vertex[0].x)
+  O(UphipRectangle, vertex[0].y)
+  O(UphipRectangle, vertex[1].x)
+  O(UphipRectangle, vertex[1].y)
+  O(UphipRectangleSize, width)
+  O(UphipRectangleSize, height)
+  O(UphipImage, frame)
+  O(UphipImage, background)
+  O(UphipImage, abs_black_threshold)
+  O(UphipBorder, left)
+  O(UphipBorder, top)
+  O(UphipBorder, right)
+  O(UphipBorder, bottom)
+  O(UphipWipes, count)
+  O(UphipWipes, areas)
+  O(UphipWipes, areas[99])
+  O(UphipBlurfilterParameters, scan_size)
+  O(UphipBlurfilterParameters, scan_step)
+  O(UphipBlurfilterParameters, intensity)
+  O(UphipGrayfilterParameters, scan_size)
+  O(UphipGrayfilterParameters, scan_step)
+  O(UphipGrayfilterParameters, abs_threshold)
+  O(UphipBlackfilterParameters, scan_size)
+  O(UphipBlackfilterParameters, scan_step)
+  O(UphipBlackfilterParameters, scan_depth.horizontal)
+  O(UphipBlackfilterParameters, scan_depth.vertical)
+  O(UphipBlackfilterParameters, scan_direction)
+  O(UphipBlackfilterParameters, abs_threshold)
+  O(UphipBlackfilterParameters, intensity)
+  O(UphipBlackfilterParameters, exclusions_count)
+  O(UphipBlackfilterParameters, exclusions)
+  O(UphipMaskDetectionParameters, scan_size)
+  O(UphipMaskDetectionParameters, scan_step)
+  O(UphipMaskDetectionParameters, scan_depth.horizontal)
+  O(UphipMaskDetectionParameters, scan_depth.vertical)
+  O(UphipMaskDetectionParameters, scan_direction)
+  O(UphipMaskDetectionParameters, scan_threshold.horizontal)
+  O(UphipMaskDetectionParameters, scan_threshold.vertical)
+  O(UphipMaskDetectionParameters, minimum_width)
+  O(UphipMaskDetectionParameters, maximum_width)
+  O(UphipMaskDetectionParameters, minimum_height)
+  O(UphipMaskDetectionParameters, maximum_height)
+  O(UphipMaskAlignmentParameters, alignment)
+  O(UphipMaskAlignmentParameters, margin)
+  O(UphipBorderScanParameters, scan_size)
+  O(UphipBorderScanParameters, scan_step)
+  O(UphipBorderScanParameters, scan_threshold.horizontal)
+  O(UphipBorderScanParameters, scan_threshold.vertical)
+  O(UphipBorderScanParameters, scan_direction)
+  O(UphipDeskewParameters, deskewScanRangeRad)
+  O(UphipDeskewParameters, deskewScanStepRad)
+  O(UphipDeskewParameters, deskewScanDeviationRad)
+  O(UphipDeskewParameters, deskewScanSize)
+  O(UphipDeskewParameters, deskewScanDepth)
+  O(UphipDeskewParameters, scan_edges)
+#undef O
+  return (size_t)-1;
 }
 
 }  // extern "C"

@@ -34,6 +34,7 @@ EXPORTED = [
     "uphip_get_device", "uphip_stream_acquire", "uphip_stream_release",
     "uphip_set_current_stream", "uphip_get_current_stream", "uphip_synchronize",
     "uphip_last_error", "uphip_clear_error", "uphip_set_fatal_errors", "uphip_version",
+    "uphip_abi_sizeof", "uphip_abi_offsetof",
     "uphip_options_init", "uphip_batch_create", "uphip_batch_destroy",
     "uphip_batch_output_info", "uphip_batch_input_ptr", "uphip_batch_set_input",
     "uphip_batch_run_device", "uphip_batch_run", "uphip_batch_wait",
@@ -114,6 +115,7 @@ def load_library(path=LIB_PATH):
         "uphip_version": (C.c_char_p, []),
         "uphip_options_init": (None, [C.POINTER(A.Options)]),
         "uphip_abi_sizeof": (C.c_size_t, [C.c_char_p]),
+        "uphip_abi_offsetof": (C.c_size_t, [C.c_char_p, C.c_char_p]),
         "uphip_batch_create": (C.c_void_p, [C.POINTER(A.Options), C.POINTER(A.BatchGeometry)]),
         "uphip_batch_destroy": (None, [C.c_void_p]),
         "uphip_batch_output_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32),
