@@ -11,7 +11,7 @@ import pytest
 
 from unpaper_hip import ctypes_abi as A
 from unpaper_hip.hostimage import HostImage
-from helpers import BYTE_FORMATS, assert_same, make_image
+from helpers import FORMATS, assert_same, make_image
 
 pytestmark = pytest.mark.gpu
 
@@ -71,7 +71,7 @@ def test_noisefilter_rgb_scene(hip, oracle):  # cuda_filters_test.c:77-90
          lambda o: oracle.noisefilter(o, 2, 200))
 
 
-@pytest.mark.parametrize("fmt", BYTE_FORMATS)
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("size,seed,specks", [((300, 200), 1, 400), ((640, 480), 2, 3000),
                                               ((129, 257), 3, 800), ((1000, 700), 4, 6000)])
 @pytest.mark.parametrize("intensity", [4, 2, 6])
@@ -120,7 +120,7 @@ def test_grayfilter_reference_scene(hip, oracle):  # cuda_filters_test.c:296-331
     both(hip, oracle, h, lambda d: hip.grayfilter(d, p), lambda o: oracle.grayfilter(o, p))
 
 
-@pytest.mark.parametrize("fmt", BYTE_FORMATS)
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("size", [(300, 200), (1001, 777), (50, 50), (7, 3)])
 @pytest.mark.parametrize("params", [((50, 50), (20, 20), 127), ((30, 20), (15, 8), 127),
                                     ((50, 50), (20, 20), 200), ((13, 7), (5, 3), 60)])
@@ -158,7 +158,7 @@ def test_blurfilter_reference_scene(hip, oracle):  # cuda_filters_test.c:337-383
          lambda o: oracle.blurfilter(o, p, 200))
 
 
-@pytest.mark.parametrize("fmt", BYTE_FORMATS)
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("size", [(2480 // 4, 3508 // 4), (1001, 777), (99, 300), (100, 100)])
 @pytest.mark.parametrize("params", [((100, 100), (50, 50), 0.01), ((40, 30), (15, 20), 0.05),
                                     ((64, 64), (64, 13), 0.2)])
@@ -201,10 +201,12 @@ def band_page(w, h, fmt, band, seed, noise=True):
         return HostImage.from_array(g, fmt)
     if fmt == A.FMT_RGB24:
         return HostImage.from_array(np.repeat(g[:, :, None], 3, axis=2), fmt)
-    return HostImage.from_array(np.stack([g, np.full_like(g, 255)], axis=2), fmt)
+    if fmt == A.FMT_Y400A:
+        return HostImage.from_array(np.stack([g, np.full_like(g, 255)], axis=2), fmt)
+    return HostImage.from_array(g >= 128, fmt)      # 1-bit: white where gray >= 128
 
 
-@pytest.mark.parametrize("fmt", BYTE_FORMATS)
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("band", [(0, 40, 0, 700), (0, 600, 0, 25), (560, 600, 100, 300),
                                   (0, 30, 200, 400)])
 def test_blackfilter_bands(hip, oracle, fmt, band):

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from unpaper_hip import ctypes_abi as A
-from helpers import BYTE_FORMATS, FORMATS, assert_same, make_image
+from helpers import FORMATS, assert_same, make_image
 
 pytestmark = pytest.mark.gpu
 
@@ -142,7 +142,7 @@ def test_apply_masks(hip, oracle, fmt, masks):
     assert_same(d.to_host(), h)
 
 
-@pytest.mark.parametrize("fmt", BYTE_FORMATS)
+@pytest.mark.parametrize("fmt", FORMATS)
 def test_apply_wipes_and_border(hip, oracle, fmt):
     h = make_image(97, 61, fmt, seed=13)
     w = A.Wipes()
@@ -168,7 +168,7 @@ def mask_params(oracle, direction=(True, False), thr=0.1, minimum=100, size=50):
     return p
 
 
-@pytest.mark.parametrize("fmt", BYTE_FORMATS)
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("direction", [(True, False), (False, True), (True, True)])
 @pytest.mark.parametrize("thr,minimum", [(0.1, 100), (0.8, 1), (0.5, 10)])
 def test_detect_masks(hip, oracle, fmt, direction, thr, minimum):
@@ -183,7 +183,7 @@ def test_detect_masks(hip, oracle, fmt, direction, thr, minimum):
     assert [m.tuple() for m in m1] == [m.tuple() for m in m2]
 
 
-@pytest.mark.parametrize("fmt", BYTE_FORMATS)
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("direction", [(False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("outside", [(0, 0, 399, 299), (0, 0, 200, 299), (200, 0, 399, 299),
                                      (10, 20, 350, 280)])
@@ -197,7 +197,7 @@ def test_detect_border(hip, oracle, fmt, direction, outside):
     assert b1.tuple() == b2.tuple()
 
 
-@pytest.mark.parametrize("fmt", BYTE_FORMATS)
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("inside,outside", [((30, 40, 300, 250), (0, 0, 399, 299)),
                                             ((0, 0, 398, 299), (0, 0, 399, 299)),
                                             ((-10, 5, 100, 320), (0, 0, 399, 299))])
@@ -214,7 +214,7 @@ def test_align_mask(hip, oracle, fmt, inside, outside, align):
     assert_same(d.to_host(), h)
 
 
-@pytest.mark.parametrize("fmt", BYTE_FORMATS)
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("interp", [A.INTERP_NN, A.INTERP_LINEAR, A.INTERP_CUBIC])
 @pytest.mark.parametrize("deg", [2.0, -0.7, 4.9])
 @pytest.mark.parametrize("mask", [(0, 0, 240, 178), (20, 15, 200, 150), (-5, 10, 250, 170)])
@@ -227,7 +227,7 @@ def test_deskew(hip, oracle, fmt, interp, deg, mask):
     assert_same(d.to_host(), h)
 
 
-@pytest.mark.parametrize("fmt", BYTE_FORMATS)
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("deg", [1.3, -12.0, 25.0, -44.0])
 @pytest.mark.parametrize("mask", [(0, 0, 1029, 299), (37, 21, 990, 280)])
 def test_deskew_cubic_wide(hip, oracle, fmt, deg, mask):

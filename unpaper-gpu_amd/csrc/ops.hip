@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "filters.h"
+#include "mono_proxy.h"
 #include "runtime.h"
 #include "scan.h"
 
@@ -29,12 +30,6 @@ static bool ok_image(const UphipImage& im, const char* op) {
   if (!im.frame) return fail("%s: image has no frame", op);
   if (!runtime_ready()) return fail("%s: no HIP device", op);
   hipSetDevice(im.frame->device);
-  return true;
-}
-
-static bool byte_format(const UphipImage& im, const char* op) {
-  if (is_mono(im.frame->format))
-    return fail("%s: 1-bit frames are not supported by this op on the HIP backend", op);
   return true;
 }
 
@@ -316,13 +311,16 @@ void uphip_apply_border(UphipImage image, const UphipBorder border, UphipPixel c
   uphip_apply_masks(image, &m, 1, color);
 }
 
-size_t uphip_detect_masks(UphipImage image, UphipMaskDetectionParameters params,
+size_t uphip_detect_masks(UphipImage image0, UphipMaskDetectionParameters params,
                           const UphipPoint points[], size_t points_count,
                           UphipRectangle masks[]) {
   // detect_masks_cpu / detect_mask / detect_edge, masks.c:54-209
   if (!params.scan_direction.horizontal && !params.scan_direction.vertical) return 0;
   if (points_count == 0) return 0;
-  if (!ok_image(image, "detect_masks") || !byte_format(image, "detect_masks")) return 0;
+  if (!ok_image(image0, "detect_masks")) return 0;
+  MonoProxy mp(image0, false, "detect_masks");  // 1-bit frames: GRAY8 proxy (mono_proxy.h)
+  if (!mp.ok()) return 0;
+  const UphipImage image = mp.image();
   UphipFrame* f = image.frame;
   const int32_t W = f->width, H = f->height;
   hipStream_t st = current_stream();
@@ -446,10 +444,13 @@ size_t uphip_detect_masks(UphipImage image, UphipMaskDetectionParameters params,
   return valid;
 }
 
-void uphip_align_mask(UphipImage image, const UphipRectangle inside_area,
+void uphip_align_mask(UphipImage image0, const UphipRectangle inside_area,
                       const UphipRectangle outside, UphipMaskAlignmentParameters params) {
   // align_mask_cpu, masks.c:265-300
-  if (!ok_image(image, "align_mask") || !byte_format(image, "align_mask")) return;
+  if (!ok_image(image0, "align_mask")) return;
+  MonoProxy mp(image0, true, "align_mask");  // 1-bit frames: GRAY8 proxy (mono_proxy.h)
+  if (!mp.ok()) return;
+  const UphipImage image = mp.image();
   const Rect in = to_rect(inside_area), out = to_rect(outside);
   const int32_t iw = iabs(in.x0 - in.x1) + 1, ih = iabs(in.y0 - in.y1) + 1;
   int32_t tx, ty;
@@ -469,13 +470,17 @@ void uphip_align_mask(UphipImage image, const UphipRectangle inside_area,
   launch_move_rect(ref_of(f), ref_of(n), d, 1, st);
   arg_fence(st);
   adopt_storage(f, n);
+  mp.finish();
 }
 
-UphipBorder uphip_detect_border(UphipImage image, UphipBorderScanParameters params,
+UphipBorder uphip_detect_border(UphipImage image0, UphipBorderScanParameters params,
                                 const UphipRectangle outside_mask) {
   // detect_border_cpu / detect_border_edge, masks.c:410-488
   UphipBorder b{0, 0, 0, 0};
-  if (!ok_image(image, "detect_border") || !byte_format(image, "detect_border")) return b;
+  if (!ok_image(image0, "detect_border")) return b;
+  MonoProxy mp(image0, false, "detect_border");  // 1-bit frames: GRAY8 proxy (mono_proxy.h)
+  if (!mp.ok()) return b;
+  const UphipImage image = mp.image();
   UphipFrame* f = image.frame;
   const int32_t W = f->width, H = f->height;
   const Rect o = to_rect(outside_mask);
@@ -534,11 +539,14 @@ UphipBorder uphip_detect_border(UphipImage image, UphipBorderScanParameters para
 // ---------------------------------------------------------------------------
 // deskew.c peers
 // ---------------------------------------------------------------------------
-void uphip_deskew(UphipImage source, UphipRectangle mask, float radians,
+void uphip_deskew(UphipImage source0, UphipRectangle mask, float radians,
                   UphipInterpolation interp) {
   // deskew_cpu, deskew.c:272-286 (sin/cos of -radians with the host libm,
   // exactly as the reference computes them, deskew.c:260-261)
-  if (!ok_image(source, "deskew") || !byte_format(source, "deskew")) return;
+  if (!ok_image(source0, "deskew")) return;
+  MonoProxy mp(source0, true, "deskew");  // 1-bit frames: GRAY8 proxy (mono_proxy.h)
+  if (!mp.ok()) return;
+  const UphipImage source = mp.image();
   UphipFrame* f = source.frame;
   RotateArgs a{to_rect(mask), sinf(-radians), cosf(-radians), 1};
   hipStream_t st = current_stream();
@@ -549,6 +557,7 @@ void uphip_deskew(UphipImage source, UphipRectangle mask, float radians,
   launch_rotate_mask(ref_of(f), ref_of(n), d, interp, 1, st, radians);
   arg_fence(st);
   adopt_storage(f, n);
+  mp.finish();
 }
 
 }  // extern "C"

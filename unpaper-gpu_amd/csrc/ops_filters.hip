@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "filters.h"
+#include "mono_proxy.h"
 #include "runtime.h"
 
 using namespace uph;
@@ -13,8 +14,6 @@ using namespace uph;
 static bool ready(const UphipImage& im, const char* op) {
   if (!im.frame) return fail("%s: image has no frame", op);
   if (!runtime_ready()) return fail("%s: no HIP device", op);
-  if (is_mono(im.frame->format))
-    return fail("%s: 1-bit frames are not supported by this op on the HIP backend", op);
   hipSetDevice(im.frame->device);
   return true;
 }
@@ -23,9 +22,12 @@ static PlaneRef ref1(const UphipFrame* f) { return fixed_ref(frame_planes(f), 0)
 
 extern "C" {
 
-void uphip_grayfilter(UphipImage image, UphipGrayfilterParameters params) {
+void uphip_grayfilter(UphipImage image0, UphipGrayfilterParameters params) {
   // grayfilter_cpu, filters.c:370-402
-  if (!ready(image, "grayfilter")) return;
+  if (!ready(image0, "grayfilter")) return;
+  MonoProxy mp(image0, true, "grayfilter");  // 1-bit frames: GRAY8 proxy (mono_proxy.h)
+  if (!mp.ok()) return;
+  const UphipImage image = mp.image();
   GrayGeom g;
   if (!gray_geometry(image.frame->width, image.frame->height, params, image.abs_black_threshold,
                      &g))
@@ -34,23 +36,31 @@ void uphip_grayfilter(UphipImage image, UphipGrayfilterParameters params) {
   void* scr = scratch(2, gray_scratch_bytes(g));
   if (!scr) return;
   launch_grayfilter(ref1(image.frame), g, scr, 0, nullptr, 1, st);
+  mp.finish();
 }
 
-void uphip_blurfilter(UphipImage image, UphipBlurfilterParameters params,
+void uphip_blurfilter(UphipImage image0, UphipBlurfilterParameters params,
                       uint8_t abs_white_threshold) {
   // blurfilter_cpu, filters.c:149-232
-  if (!ready(image, "blurfilter")) return;
+  if (!ready(image0, "blurfilter")) return;
+  MonoProxy mp(image0, true, "blurfilter");  // 1-bit frames: GRAY8 proxy (mono_proxy.h)
+  if (!mp.ok()) return;
+  const UphipImage image = mp.image();
   BlurGeom g;
   if (!blur_geometry(image.frame->width, image.frame->height, params, abs_white_threshold, &g))
     return (void)fail("blurfilter: invalid scan size");
   void* scr = scratch(2, blur_scratch_bytes(g));
   if (!scr) return;
   launch_blurfilter(ref1(image.frame), g, scr, 0, nullptr, 1, current_stream());
+  mp.finish();
 }
 
-void uphip_noisefilter(UphipImage image, uint64_t intensity, uint8_t min_white_level) {
+void uphip_noisefilter(UphipImage image0, uint64_t intensity, uint8_t min_white_level) {
   // noisefilter_cpu, filters.c:309-338
-  if (!ready(image, "noisefilter")) return;
+  if (!ready(image0, "noisefilter")) return;
+  MonoProxy mp(image0, true, "noisefilter");  // 1-bit frames: GRAY8 proxy (mono_proxy.h)
+  if (!mp.ok()) return;
+  const UphipImage image = mp.image();
   NoiseGeom g;
   noise_geometry(image.frame->width, image.frame->height, intensity, min_white_level, &g);
   if (intensity > 64) return (void)fail("noisefilter: intensity > 64 unsupported");
@@ -64,12 +74,16 @@ void uphip_noisefilter(UphipImage image, uint64_t intensity, uint8_t min_white_l
   int32_t status = 0;
   UPH_HIP(hipMemcpyAsync(&status, &ctl->status, 4, hipMemcpyDeviceToHost, st));
   UPH_HIP(hipStreamSynchronize(st));
-  if (status) fail("noisefilter: candidate list overflow (status %d)", status);
+  if (status) return (void)fail("noisefilter: candidate list overflow (status %d)", status);
+  mp.finish();
 }
 
-void uphip_blackfilter(UphipImage image, UphipBlackfilterParameters params) {
+void uphip_blackfilter(UphipImage image0, UphipBlackfilterParameters params) {
   // blackfilter_cpu, filters.c:111-127
-  if (!ready(image, "blackfilter")) return;
+  if (!ready(image0, "blackfilter")) return;
+  MonoProxy mp(image0, true, "blackfilter");  // 1-bit frames: GRAY8 proxy (mono_proxy.h)
+  if (!mp.ok()) return;
+  const UphipImage image = mp.image();
   const int32_t W = image.frame->width, H = image.frame->height;
   if (image.abs_black_threshold == 255)
     return (void)fail("blackfilter: abs_black_threshold 255 makes the reference fill recurse "
@@ -98,14 +112,18 @@ void uphip_blackfilter(UphipImage image, UphipBlackfilterParameters params) {
   int32_t status = 0;
   UPH_HIP(hipMemcpyAsync(&status, &ctl->status, 4, hipMemcpyDeviceToHost, st));
   UPH_HIP(hipStreamSynchronize(st));
-  if (status) fail("blackfilter: flood-fill stack overflow (status %d)", status);
+  if (status) return (void)fail("blackfilter: flood-fill stack overflow (status %d)", status);
+  mp.finish();
 }
 
-float uphip_detect_rotation(UphipImage image, UphipRectangle mask,
+float uphip_detect_rotation(UphipImage image0, UphipRectangle mask,
                             const UphipDeskewParameters params) {
   // detect_rotation_cpu, deskew.c:181-241: peaks on the GPU, the per-edge
   // argmax and the mean/deviation on the host exactly as the reference does
-  if (!ready(image, "detect_rotation")) return 0.0f;
+  if (!ready(image0, "detect_rotation")) return 0.0f;
+  MonoProxy mp(image0, false, "detect_rotation");  // 1-bit frames: GRAY8 proxy (mono_proxy.h)
+  if (!mp.ok()) return 0.0f;
+  const UphipImage image = mp.image();
   static thread_local RotTable table;
   if (rotation_angles(params, &table) < 0) {
     fail("detect_rotation: more than %d angles", kMaxAngles);
