@@ -1327,41 +1327,64 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* obuf = reinterpret_cast<uint8_t*>(nw + max_rows) + wu * (kRFH / kRFWaves * kRFW);
   if (staged && !UPH_DIAG_BITS(diag, 1024)) {
-    // a wave stages whole rows (lane = source dword), four in flight; nw[r]
-    // bit j: dword j of window row r holds a non-white pixel
-    // Branch-free: every lane loads the dword at its address clamped into the
-    // row; a dword across an image edge is then realigned by a shift and its
-    // bytes outside [0, W) made white.
-    const int32_t xd = xa + 4 * lane;
-    const bool colv = lane < nd;
-    const int32_t xc = imin(imax(xd, 0), (int32_t)P.pitch - 4);
-    // realignment as one 64-bit shift: (v << 24) >> (24 + 8 (xd - xc)); with
-    // |xd - xc| >= 4 every byte is outside anyway
-    const int fsh = imin(imax(24 + 8 * (xd - xc), 0), 56);
-    uint32_t outside = colv ? 0u : 0xFFFFFFFFu;
+    // A wave-instruction stages three window rows, 8 bytes per lane: lanes
+    // 18 q .. 18 q + 17 load row r + q (q < 3), lanes 54..63 idle.  nw[r] bit j:
+    // window bytes 8 j .. 8 j + 7 of row r hold a non-white pixel.  Interior
+    // tiles (the whole window inside the image) load straight; edge tiles
+    // load every dword clamped into the row, realign it by one 64-bit shift
+    // and make the bytes outside [0, W) x [0, H) white.
+    const int rq = (lane * 57) >> 10;  // lane / 18 for lane < 64
+    const int jq = lane - 18 * rq;
+    const int nq = (nd + 1) >> 1;
+    const bool qv = rq < 3 && jq < nq;
+    const int32_t xd = xa + 8 * jq;
+    const bool interior = xa >= 0 && xa + 8 * nq <= P.W && by0 >= 0 && by0 + bh <= P.H;
+    const int32_t xc0 = imin(imax(xd, 0), (int32_t)P.pitch - 4);
+    const int32_t xc1 = imin(imax(xd + 4, 0), (int32_t)P.pitch - 4);
+    const int fs0 = imin(imax(24 + 8 * (xd - xc0), 0), 56);
+    const int fs1 = imin(imax(24 + 8 * (xd + 4 - xc1), 0), 56);
+    uint32_t out0 = qv ? 0u : 0xFFFFFFFFu, out1 = out0;
 #pragma unroll
-    for (int k = 0; k < 4; k++)
-      if (xd + k < 0 || xd + k >= P.W) outside |= 0xFFu << (8 * k);
-    for (int r0 = 4 * wu; r0 < bh; r0 += 4 * kRFWaves) {
-      uint32_t v[4];
+    for (int k = 0; k < 4; k++) {
+      if (xd + k < 0 || xd + k >= P.W) out0 |= 0xFFu << (8 * k);
+      if (xd + 4 + k < 0 || xd + 4 + k >= P.W) out1 |= 0xFFu << (8 * k);
+    }
+    const int32_t xi = interior && qv ? xd : (interior ? xa : 0);  // idle lanes stay in the row
+    for (int rg = 3 * wu; rg < bh; rg += 3 * 3 * kRFWaves) {
+      uint2 v[3];
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int32_t y = imin(imax(by0 + r0 + q, 0), P.H - 1);
-        v[q] = *reinterpret_cast<const uint32_t*>(sbase + row_off(y, P.pitch) + xc);
+      for (int g = 0; g < 3; g++) {  // all loads of the group in flight
+        const int r = rg + 3 * kRFWaves * g + rq;
+        if (interior) {
+          const int32_t y = imin(by0 + r, P.H - 1);
+          v[g] = *reinterpret_cast<const uint2*>(sbase + row_off(y, P.pitch) + xi);
+        } else {
+          const int32_t y = imin(imax(by0 + r, 0), P.H - 1);
+          const uint8_t* row = sbase + row_off(y, P.pitch);
+          v[g].x = *reinterpret_cast<const uint32_t*>(row + xc0);
+          v[g].y = *reinterpret_cast<const uint32_t*>(row + xc1);
+        }
       }
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int r = r0 + q;
-        if (r >= bh) break;  // uniform
-        const int32_t y = by0 + r;
-        uint32_t w4 = (uint32_t)(((uint64_t)v[q] << 24) >> fsh);
-        w4 |= outside;
-        if ((y < 0) | (y >= P.H)) w4 = 0xFFFFFFFFu;
-        const unsigned long long m = __ballot(w4 != 0xFFFFFFFFu);
-        if (lane == 0) nw[r] = m;
-        if (colv)
-          *reinterpret_cast<float4*>(winf + r * kRFS + 4 * lane) =
-              make_float4(ubyte_f<0>(w4), ubyte_f<1>(w4), ubyte_f<2>(w4), ubyte_f<3>(w4));
+      for (int g = 0; g < 3; g++) {
+        const int rb = rg + 3 * kRFWaves * g;  // the wave's first row of this instruction
+        if (rb >= bh) break;                   // uniform
+        const int r = rb + rq;
+        uint32_t w0 = v[g].x, w1 = v[g].y;
+        if (!interior) {
+          const int32_t y = by0 + r;
+          w0 = (uint32_t)(((uint64_t)w0 << 24) >> fs0) | out0;
+          w1 = (uint32_t)(((uint64_t)w1 << 24) >> fs1) | out1;
+          if ((y < 0) | (y >= P.H)) w0 = w1 = 0xFFFFFFFFu;
+        }
+        const bool valid = qv && r < bh;
+        const unsigned long long m = __ballot(valid && (w0 & w1) != 0xFFFFFFFFu);
+        if (lane < 3 && rb + lane < bh) nw[rb + lane] = (m >> (18 * lane)) & 0x3FFFFull;
+        if (valid) {
+          float4* d = reinterpret_cast<float4*>(winf + r * kRFS + 8 * jq);
+          d[0] = make_float4(ubyte_f<0>(w0), ubyte_f<1>(w0), ubyte_f<2>(w0), ubyte_f<3>(w0));
+          d[1] = make_float4(ubyte_f<0>(w1), ubyte_f<1>(w1), ubyte_f<2>(w1), ubyte_f<3>(w1));
+        }
       }
     }
   }
@@ -1419,30 +1442,36 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
   // bounds and a ballot per row).
   uint32_t white_rows = 0;  // bit k: every tap of output row k is white
   if (staged) {
-#pragma unroll
-    for (int h = 0; h < (kRows + 3) / 4; h++) {
-      const int k = 4 * h + (lane >> 4), j = lane & 15;
-      bool hit = false;
-      if (k < kRows) {
-        const float cv = (yw + k - a.mask.y0) - tcy;
-        const float VS = cv * a.sinval, VC = scy + cv * a.cosval;
-        const int32_t xl = (int)(axL + VS), xr = (int)(axR + VS);
-        const int32_t yl = (int)(VC - bsL), yr = (int)(VC - bsR);
-        const int32_t c0 = imax((imin(xl, xr) - 1 - xa) >> 2, 0);
-        const int32_t c1 = imin((imax(xl, xr) + 2 - xa) >> 2, nd - 1);
-        const int32_t r0 = imax(imin(yl, yr) - 1 - by0, 0);
-        const int32_t r1 = imin(imax(yl, yr) + 2 - by0, bh - 1);
-        const uint64_t cm = c1 >= c0 ? ((2ull << c1) - 1ull) & ~((1ull << c0) - 1ull) : 0ull;
-        for (int r = r0 + j; r <= r1; r += 16) hit |= (nw[r] & cm) != 0;  // one pass at 5 deg
-      }
-      const uint64_t m = __ballot(hit);
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-        if (4 * h + q < kRows && ((m >> (16 * q)) & 0xFFFFull) == 0) white_rows |= 1u << (4 * h + q);
+    // one pass: lane 8 k + j tests output row k against window rows
+    // r0 + j, r0 + j + 8, ... of the row's tap band (8-byte column granules)
+    const int k = lane >> 3, j = lane & 7;
+    bool hit = false;
+    if (k < kRows) {
+      const float cv = (yw + k - a.mask.y0) - tcy;
+      const float VS = cv * a.sinval, VC = scy + cv * a.cosval;
+      const int32_t xl = (int)(axL + VS), xr = (int)(axR + VS);
+      const int32_t yl = (int)(VC - bsL), yr = (int)(VC - bsR);
+      const int32_t c0 = imax((imin(xl, xr) - 1 - xa) >> 3, 0);
+      const int32_t c1 = imin((imax(xl, xr) + 2 - xa) >> 3, ((nd + 1) >> 1) - 1);
+      const int32_t r0 = imax(imin(yl, yr) - 1 - by0, 0);
+      const int32_t r1 = imin(imax(yl, yr) + 2 - by0, bh - 1);
+      const uint64_t cm = c1 >= c0 ? ((2ull << c1) - 1ull) & ~((1ull << c0) - 1ull) : 0ull;
+      for (int r = r0 + j; r <= r1; r += 8) hit |= (nw[r] & cm) != 0;
     }
+    const uint64_t m = __ballot(hit);
+#pragma unroll
+    for (int q = 0; q < kRows; q++)
+      if (((m >> (8 * q)) & 0xFFull) == 0) white_rows |= 1u << q;
     if (UPH_DIAG_BITS(diag, 2048)) white_rows = 0;
     if (UPH_DIAG_BITS(diag, 512)) white_rows = ~0u;
   }
+  // Every source coordinate of the tile's in-mask pixels is >= 1 when the
+  // window starts inside the image: then (int)c == floor(c) and
+  // c - (int)c == fract(c) exactly (one instruction instead of three).
+  const bool posc = bx0 >= 0 && by0 >= 0;
+  // LDS byte address of window (row 0, column 0) minus the 4x4 tap offset,
+  // so a pixel's first tap sits at wbase + 4 (iy kRFS + ix)
+  const uint32_t wbase = lds0 - 4u * (uint32_t)((1 + by0) * kRFS + 1 + xa);
 #pragma unroll
   for (int k = 0; k < kRows; k++) {
     const int32_t y = yw + k;
@@ -1456,11 +1485,20 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
     if (!white && staged) {
       const float sxA = axA + VS, syA = VC - bsA, sxB = axB + VS, syB = VC - bsB;
       const int ixA = (int)sxA, iyA = (int)syA, ixB = (int)sxB, iyB = (int)syB;  // truncation
-      const float fxA = sxA - ixA, fyA = syA - iyA, fxB = sxB - ixB, fyB = syB - iyB;
-      // window row index times the stride as a full-rate 24-bit multiply
-      const uint32_t pA = 4u * (uint32_t)(inA ? __mul24(iyA - 1 - by0, kRFS) + ixA - 1 - xa : 0);
-      const uint32_t pB = 4u * (uint32_t)(inB ? __mul24(iyB - 1 - by0, kRFS) + ixB - 1 - xa : 0);
-      const uint32_t ta[4] = {lds0 + pA, lds0 + pA + 8 * kRFS, lds0 + pB, lds0 + pB + 8 * kRFS};
+      float fxA, fyA, fxB, fyB;
+      if (posc) {
+        fxA = __builtin_amdgcn_fractf(sxA);
+        fyA = __builtin_amdgcn_fractf(syA);
+        fxB = __builtin_amdgcn_fractf(sxB);
+        fyB = __builtin_amdgcn_fractf(syB);
+      } else {
+        fxA = sxA - ixA, fyA = syA - iyA, fxB = sxB - ixB, fyB = syB - iyB;
+      }
+      // window address as one full-rate 24-bit multiply-add; pixels outside
+      // the mask read (and discard) the window origin
+      const uint32_t pA = inA ? wbase + 4u * (uint32_t)(__mul24(iyA, kRFS) + ixA) : lds0;
+      const uint32_t pB = inB ? wbase + 4u * (uint32_t)(__mul24(iyB, kRFS) + ixB) : lds0;
+      const uint32_t ta[4] = {pA, pA + 8 * kRFS, pB, pB + 8 * kRFS};
       f2 t[4][4];
       lds_taps16(ta, t);
       // rows (0,1) and (2,3) of A, then of B: four packed row cubics
