@@ -258,6 +258,12 @@ def latency_c2(L, opts, page_host, pages_ptr, pitch, stride, reps=7):
             b.wait()
             if r:
                 dev.append((time.perf_counter() - t0) * 1e3)
+        # where a lone page's time goes: one more run with stage events
+        b.set_timing(True)
+        b.run_device(1, pages_ptr, pitch, stride)
+        b.wait()
+        stages = {k: round(v, 3) for k, v in b.stage_times()}
+        b.set_timing(False)
         for r in range(reps + 1):
             t0 = time.perf_counter()
             if L.uphip_batch_set_input(b.handle, 0, page_host.ctypes.data, W) != 0:
@@ -267,7 +273,7 @@ def latency_c2(L, opts, page_host, pages_ptr, pitch, stride, reps=7):
             b.output(0)
             if r:
                 host.append((time.perf_counter() - t0) * 1e3)
-        return round(statistics.median(dev), 3), round(statistics.median(host), 3)
+        return round(statistics.median(dev), 3), round(statistics.median(host), 3), stages
     finally:
         b.close()
 
@@ -402,7 +408,7 @@ def run_c4(args, L, d, devices, firsts, n_gpus, version, valid):
                                        load_hashes("c4_hashes.json", "sheets"))
     r.close()
     # one sheet alone on an idle GPU: latency, and the rotate launch
-    lat, rot = [], []
+    lat, rot, lat_stages = [], [], {}
     b1 = Batch(opts, 1, C4_W, C4_H, A.FMT_RGB24, timing=True)
     try:
         for rep in range(4):
@@ -414,6 +420,7 @@ def run_c4(args, L, d, devices, firsts, n_gpus, version, valid):
             if rep:
                 lat.append((t2 - t1) * 1e3)
                 rot.append(st.get(ROOFLINE_STAGE, 0.0))
+                lat_stages = st
     finally:
         b1.close()
     pages.close()
@@ -430,6 +437,7 @@ def run_c4(args, L, d, devices, firsts, n_gpus, version, valid):
             "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "latency_ms": round(statistics.median(lat), 2),
+            "latency_stages_ms": {k: round(v, 3) for k, v in lat_stages.items()},
             "config": {"workload": "%d synthetic RGB24 9920x7016 double-page sheets per GPU, "
                                    "layout double, interpolate linear, border 60" % nsheets,
                        "sheets_per_batch": bsz, "streams": streams},
@@ -549,9 +557,10 @@ def main():
     if single and not (args.no_host_io and args.no_cpu and args.no_latency):
         host_pages = device_pages_to_host(L, bufs[0], pitch, stride, npages, W, H)
     if single and not args.no_latency:
-        dev_ms, host_ms = latency_c2(L, opts, host_pages[0], bufs[0].ptr, pitch, stride)
+        dev_ms, host_ms, stages = latency_c2(L, opts, host_pages[0], bufs[0].ptr, pitch, stride)
         latency = {"device_ms": dev_ms, "with_pcie_ms": host_ms,
-                   "what": "one A4 GRAY8 page alone, idle GPU, median of 7 (C2)"}
+                   "what": "one A4 GRAY8 page alone, idle GPU, median of 7 (C2)",
+                   "stages_ms": stages}
     if single and not args.no_host_io:
         hio = host_io(opts, devices[0], host_pages, npages, args, threads)
     if single and not args.no_cpu:

@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Per-kernel effective clock (GRBM_GUI_ACTIVE / duration) and VALU issue
+fraction (SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x active cycles)) from a
+rocprofv3 --kernel-trace --pmc run (tools/pmc_clock.sh)."""
+import collections
+import csv
+import glob
+import os
+import sys
+
+d = sys.argv[1]
+cc = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+agg = collections.defaultdict(lambda: collections.defaultdict(float))
+for r in csv.DictReader(open(cc)):
+    k = r["Kernel_Name"][:56]
+    agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+    agg[k]["_n_" + r["Counter_Name"]] += 1
+kt = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+dur = collections.defaultdict(float)
+if kt:
+    for r in csv.DictReader(open(kt[0])):
+        dur[r["Kernel_Name"][:56]] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+print("%-56s %9s %9s %8s %8s" % ("kernel", "dur_ms", "GHz", "VALU%", "VALU/wave"))
+for k, v in sorted(agg.items(), key=lambda kv: -dur.get(kv[0], 0)):
+    t = dur.get(k, 0.0)
+    gui = v.get("GRBM_GUI_ACTIVE", 0.0)
+    gui /= 8  # GRBM_GUI_ACTIVE is summed over the 8 XCDs
+    ghz = gui / t / 1e9 if t > 0 else 0.0
+    valu = v.get("SQ_INSTS_VALU", 0.0)
+    frac = valu * 4 / (1024 * gui) if gui > 0 else 0.0
+    waves = v.get("SQ_WAVES", 0.0)
+    print("%-56s %9.3f %9.3f %8.1f %8.0f" % (k, t * 1e3, ghz, 100 * frac, valu / waves if waves else 0))

@@ -520,6 +520,9 @@ __device__ __forceinline__ uint4 shift_bytes16(const uint32_t* w, int r) {
                     __builtin_amdgcn_alignbyte(w[Q + 4], w[Q + 3], r));
 }
 
+constexpr int kMoveRows = 8;  // rows per wave of k_move_rect_g16
+static_assert(6 * kMoveRows * (kThreads / 64) <= kThreads, "one lane per deferred (row, vector)");
+
 __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneRef dst,
                                                             const MoveArgs* args) {
   const int s = blockIdx.z;
@@ -536,42 +539,85 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
   const int32_t nv = (P.W + 15) >> 4;                  // vectors per row (inside the pitch)
   const int32_t delta = A.x0 - a.tx;                   // source column - destination column
   const int r16 = delta & 15, q = r16 >> 2, r = r16 & 3;
+  // The class of a column changes only at five breakpoints (uniform per
+  // sheet).  Vectors holding a breakpoint strictly inside, and the row's last
+  // partial vector, are assembled byte by byte after the row's uniform
+  // vectors -- one lane each, so the wave runs that path once per row.
   const int32_t bp[5] = {a.tx, a.tx + aw, a.tx + sw, A.x0, A.x1 + 1};
+  // Deferred vectors (uniform): those holding a breakpoint strictly inside,
+  // and the row's last partial vector, deduplicated.
+  int32_t dvs[6];
+  int nd = 0;
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const int32_t b = k < 5 ? bp[k] : P.W;
+    const bool has = k < 5 ? (b > 0 && b < P.W && (b & 15)) : (P.W & 15) != 0;
+    bool dup = false;
+#pragma unroll
+    for (int m = 0; m < 6; m++)
+      if (m < nd && dvs[m] == (b >> 4)) dup = true;
+    if (has && !dup) dvs[nd++] = b >> 4;
+  }
   const int lane = threadIdx.x & 63;
-  // one wave per destination row, kMoveVec vectors per lane, loads issued first
-  constexpr int kMoveVec = 3;  // 192 vector slots per row: 155 used at A4 width
-  for (int32_t y = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); y < P.H;
-       y += gridDim.x * (kThreads / 64)) {
-    const uint8_t* srow = sbase + (int64_t)y * P.pitch;
-    uint8_t* drow = dbase + (int64_t)y * P.pitch;
+  // A column's class on a row is a function of three column facts (inside
+  // the pasted columns, inside its copied part, inside the wiped area) and
+  // three row facts; per row the eight column codes map to classes through
+  // one 16-bit table (2 bits per code), so the column work is done once.
+  auto col_code = [&](int32_t x) -> uint32_t {
+    const int32_t u = x - a.tx;
+    return (uint32_t)(u >= 0 && u < sw) | (uint32_t)(u < aw) << 1 |
+           (uint32_t)(x >= A.x0 && x <= A.x1) << 2;
+  };
+  auto row_table = [&](int32_t y) -> uint32_t {
     const int32_t v = y - a.ty;
-    const bool trow = v >= 0 && v < sh;              // row crosses the pasted rectangle
-    const bool mrow = trow && v < ah;                // ... and its copied extent
-    const bool arow = y >= A.y0 && y <= A.y1;        // row crosses the wiped area
-    const uint8_t* mrow_p = sbase + (int64_t)(A.y0 + (mrow ? v : 0)) * P.pitch;
-    auto cls_of = [&](int32_t x) -> int {
-      const int32_t u = x - a.tx;
-      if (trow && u >= 0 && u < sw) return (mrow && u < aw) ? 2 : 1;
-      return (arow && x >= A.x0 && x <= A.x1) ? 1 : 0;
-    };
-    for (int32_t vb = 0; vb < nv; vb += 64 * kMoveVec) {
+    const bool trow = v >= 0 && v < sh, mrow = trow && v < ah;
+    const bool arow = y >= A.y0 && y <= A.y1;
+    uint32_t t = 0;
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      const int cls = (trow && (c & 1)) ? ((mrow && (c & 2)) ? 2 : 1) : ((arow && (c & 4)) ? 1 : 0);
+      t |= (uint32_t)cls << (2 * c);
+    }
+    return t;
+  };
+  auto moved_row = [&](int32_t y) -> const uint8_t* {
+    const int32_t v = y - a.ty;
+    return sbase + (int64_t)(A.y0 + ((v >= 0 && v < ah) ? v : 0)) * P.pitch;
+  };
+  const int32_t yb = blockIdx.x * kMoveRows * (kThreads / 64);  // the block's first row
+  const int32_t y0 = blockIdx.x * kMoveRows * (kThreads / 64) + (threadIdx.x >> 6) * kMoveRows;
+  const int32_t y1 = imin(y0 + kMoveRows, P.H);
+  // kMoveVec vectors per lane per chunk of the row (192 slots: 155 used at A4 width)
+  constexpr int kMoveVec = 3;
+  for (int32_t vb = 0; vb < nv; vb += 64 * kMoveVec) {
+    uint32_t cc[kMoveVec];  // column code, bit 3: no uniform vector here
+#pragma unroll
+    for (int k = 0; k < kMoveVec; k++) {
+      const int32_t vi = vb + k * 64 + lane;
+      const int32_t x0 = 16 * vi;
+      bool deferred = vi >= nv || x0 + 16 > P.W;
+#pragma unroll
+      for (int j = 0; j < 5; j++) deferred |= bp[j] > x0 && bp[j] < x0 + 16;
+      cc[k] = col_code(x0) | (deferred ? 8u : 0u);
+    }
+    for (int32_t y = y0; y < y1; y++) {
+      const uint8_t* srow = sbase + (int64_t)y * P.pitch;
+      uint8_t* drow = dbase + (int64_t)y * P.pitch;
+      const uint8_t* mrow_p = moved_row(y);
+      const uint32_t tab = row_table(y);
       int cls[kMoveVec];
       uint4 lo[kMoveVec], hi[kMoveVec];
 #pragma unroll
       for (int k = 0; k < kMoveVec; k++) {
-        const int32_t vi = vb + k * 64 + lane;
-        const int32_t x0 = 16 * vi;
-        bool uni = vi < nv && x0 + 16 <= P.W;
-#pragma unroll
-        for (int j = 0; j < 5; j++) uni &= !(bp[j] > x0 && bp[j] < x0 + 16);
-        int c = vi < nv ? cls_of(x0) : -1;
-        if (c == 2 && !(uni && ((x0 + delta) & ~15) + (r16 ? 32 : 16) <= P.pitch)) uni = false;
-        cls[k] = vi >= nv ? -1 : uni ? c : 3;  // 3: byte by byte
+        const int32_t x0 = 16 * (vb + k * 64 + lane);
+        cls[k] = (cc[k] & 8u) ? -1 : (int)((tab >> (2 * (cc[k] & 7u))) & 3u);
         lo[k] = make_uint4(bg4, bg4, bg4, bg4);
         hi[k] = make_uint4(0, 0, 0, 0);
         if (cls[k] == 0) {
           lo[k] = *reinterpret_cast<const uint4*>(srow + x0);
         } else if (cls[k] == 2) {
+          // a whole class-2 vector reads source columns inside [0, W), so
+          // both aligned halves lie inside the (16-multiple) pitch
           const uint4* qp = reinterpret_cast<const uint4*>(mrow_p + ((x0 + delta) & ~15));
           lo[k] = qp[0];
           if (r16) hi[k] = qp[1];
@@ -579,8 +625,7 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
       }
 #pragma unroll
       for (int k = 0; k < kMoveVec; k++) {
-        const int32_t vi = vb + k * 64 + lane;
-        const int32_t x0 = 16 * vi;
+        const int32_t x0 = 16 * (vb + k * 64 + lane);
         if (cls[k] < 0) continue;
         uint4 out = lo[k];
         if (cls[k] == 2 && r16) {
@@ -592,23 +637,64 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
             case 2: out = shift_bytes16<2>(w, r); break;
             default: out = shift_bytes16<3>(w, r); break;
           }
-        } else if (cls[k] == 3) {
-          // unrolled with independent byte loads (one memory round trip,
-          // not sixteen); columns >= W stay 0 as before
-          uint32_t o[4] = {0, 0, 0, 0};
-#pragma unroll
-          for (int j = 0; j < 16; j++) {
-            const int32_t x = x0 + j;
-            const int c = x < P.W ? cls_of(x) : 1;
-            const uint8_t* p = c == 0 ? srow + x : mrow_p + (c == 2 ? x + delta : 0);
-            const uint8_t bb = c == 1 ? (x < P.W ? bg : 0) : *p;
-            o[j >> 2] |= (uint32_t)bb << (8 * (j & 3));
-          }
-          out = make_uint4(o[0], o[1], o[2], o[3]);
         }
         *reinterpret_cast<uint4*>(drow + x0) = out;
       }
     }
+  }
+  // Deferred vectors: per byte, the class picks a byte of the source vector,
+  // of the moved (realigned) vector or the background; columns >= W stay 0.
+  // The block's (row, deferred vector) pairs are spread over all its lanes,
+  // one pair each (<= 6 x kMoveRows x 4 <= kThreads), so the byte work runs
+  // once per block rather than once per row and wave.
+  const int tid = threadIdx.x;
+  const int32_t yr = yb + (nd ? tid / nd : 0);
+  if (tid < nd * kMoveRows * (kThreads / 64) && yr < P.H) {
+    const int di = tid - (tid / nd) * nd;
+    int32_t vi = dvs[0];
+#pragma unroll
+    for (int m = 1; m < 6; m++)
+      if (m == di) vi = dvs[m];
+    const int32_t x0 = 16 * vi;
+    const int32_t y = yr;
+    const uint8_t* srow = sbase + (int64_t)y * P.pitch;
+    const uint8_t* mrow_p = moved_row(y);
+    const uint32_t tab = row_table(y);
+    // the aligned source halves of the moved bytes, each clamped into the row
+    // (a clamped half only feeds bytes whose class is not 2)
+    const int32_t al = (x0 + delta) & ~15;
+    const int32_t alo = imin(imax(al, 0), (int32_t)P.pitch - 16);
+    const int32_t ahi = imin(imax(al + 16, 0), (int32_t)P.pitch - 16);
+    const uint4 sv = *reinterpret_cast<const uint4*>(srow + x0);
+    const uint4 l = *reinterpret_cast<const uint4*>(mrow_p + alo);
+    const uint4 h = *reinterpret_cast<const uint4*>(mrow_p + ahi);
+    const uint32_t w[8] = {l.x, l.y, l.z, l.w, h.x, h.y, h.z, h.w};
+    uint4 mv;
+    switch (q) {
+      case 0: mv = shift_bytes16<0>(w, r); break;
+      case 1: mv = shift_bytes16<1>(w, r); break;
+      case 2: mv = shift_bytes16<2>(w, r); break;
+      default: mv = shift_bytes16<3>(w, r); break;
+    }
+    const uint32_t sw4[4] = {sv.x, sv.y, sv.z, sv.w};
+    const uint32_t mw4[4] = {mv.x, mv.y, mv.z, mv.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      uint32_t m0 = 0, m2 = 0, mb = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int32_t x = x0 + 4 * d + j;
+        const uint32_t code = x < P.W ? col_code(x) : 8u;
+        const uint32_t cls = (code & 8u) ? 3u : (tab >> (2 * code)) & 3u;
+        const uint32_t byte = 0xFFu << (8 * j);
+        m0 |= cls == 0 ? byte : 0u;
+        m2 |= cls == 2 ? byte : 0u;
+        mb |= cls == 1 ? byte : 0u;
+      }
+      o[d] = (sw4[d] & m0) | (mw4[d] & m2) | (bg4 & mb);
+    }
+    *reinterpret_cast<uint4*>(dbase + (int64_t)y * P.pitch + x0) = make_uint4(o[0], o[1], o[2], o[3]);
   }
 }
 
@@ -616,8 +702,8 @@ void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* 
                       hipStream_t st) {
   int gx = src.P.H < 1 ? 1 : (src.P.H > 1024 ? 1024 : src.P.H);
   if (src.P.fmt == F_GRAY8) {
-    // one wave per row, about two rows per wave
-    const int64_t blocks = (src.P.H + 2 * (kThreads / 64) - 1) / (2 * (kThreads / 64));
+    // kMoveRows consecutive rows per wave
+    const int64_t blocks = (src.P.H + kMoveRows * (kThreads / 64) - 1) / (kMoveRows * (kThreads / 64));
     UPH_LAUNCH_DIAG(4, k_move_rect_g16, dim3((unsigned)(blocks < 1 ? 1 : blocks), 1, count),
                     dim3(kThreads), 0, st, src, dst, args);
   } else if (src.P.fmt == F_Y400A) {

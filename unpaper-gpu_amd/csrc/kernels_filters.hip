@@ -1200,136 +1200,162 @@ __device__ __forceinline__ Mask81 ring_part(int L, bool rows) {
   return m;
 }
 
-// The sequential replay for intensity N <= 4, scheduled by dependence:
-// trigger T reads pixels within Chebyshev N of itself and clears within N-1,
-// so it depends only on earlier triggers closer than 2N.  level(T) = 1 + the
-// highest level of those (0 if none); triggers of one level are pairwise >= 2N
-// apart and are replayed together, one lane each, level after level.  The
-// result equals the raster-order replay (filters.c:243-348).
+// One trigger of the raster replay for intensity N <= 4 (filters.c:309-338):
+// the 9x9 window read from the frame (dark = lightness < white), rings with
+// the reference loops' unsigned comparisons -- rows of ring L counted iff
+// x >= L, its columns iff y >= L-1 -- and the clears written straight back.
 template <int FMT>
-__device__ void noise_resolve_levels(const uint32_t* keys, int n, int N, const NoiseGeom& g,
-                                     uint8_t* base, int64_t pitch) {
-  __shared__ uint16_t lev[8192];
-  __shared__ int32_t max_level;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int R = 2 * N - 1;  // dependence radius
-  // levels by parallel relaxation: lev(T) = 1 + max lev(dependent earlier T');
-  // values only grow and stay <= the true level, so the sweep repeats until
-  // nothing changes (longest chain + 1 sweeps).  Predecessors of T are found
-  // per row of the window [y-R, y] by binary search in the sorted keys.
-  __shared__ int32_t changed;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) lev[i] = 0;
-  if (threadIdx.x == 0) max_level = 0;
-  __syncthreads();
-  for (;;) {
-    if (threadIdx.x == 0) changed = 0;
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-      const uint32_t key = keys[i];
-      const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
-      int mx = -1;
-      for (int yy = imax(y - R, 0); yy <= y; yy++) {
-        const uint32_t lo = ((uint32_t)yy << 16) | (uint32_t)imax(x - R, 0);
-        const uint32_t hi = ((uint32_t)yy << 16) | (uint32_t)(x + R);
-        int a = 0, b = i;  // first index in [0, i) with keys >= lo
-        while (a < b) {
-          const int mid = (a + b) >> 1;
-          if (keys[mid] < lo) a = mid + 1;
-          else b = mid;
-        }
-        for (int j = a; j < i && keys[j] <= hi; j++) mx = imax(mx, (int)lev[j]);
-      }
-      if (mx + 1 > (int)lev[i]) {
-        lev[i] = (uint16_t)(mx + 1);
-        changed = 1;
-        atomicMax(&max_level, mx + 1);
+__device__ __forceinline__ void replay_trigger4(int32_t x, int32_t y, int N, const NoiseGeom& g,
+                                                uint8_t* base, int64_t pitch,
+                                                const Mask81 (&rowp)[5], const Mask81 (&colp)[5]) {
+  uint64_t dlo = 0;
+  uint32_t dhi = 0;
+  bool ctr = false;
+#pragma unroll
+  for (int p = 0; p < 81; p++) {  // unconditional clamped loads: one round trip
+    const int32_t qx = x + p % 9 - 4, qy = y + p / 9 - 4;
+    const bool in = (qx >= 0) & (qy >= 0) & (qx < g.W) & (qy < g.H);
+    const Px q = load_px_row<FMT>(base + (int64_t)imin(imax(qy, 0), g.H - 1) * pitch,
+                                  imin(imax(qx, 0), g.W - 1));
+    const bool dk = in & (light_of(q) < g.white);
+    if (p < 64) dlo |= (uint64_t)dk << p;
+    else dhi |= (uint32_t)dk << (p - 64);
+    if (p == 40) ctr = dark_of(q) < g.white;
+  }
+  if (!ctr) return;  // cleared meanwhile
+  Mask81 mem[5];
+  int lc[5];
+#pragma unroll
+  for (int L = 1; L <= 4; L++) {
+    mem[L].lo = (x >= L ? rowp[L].lo : 0ull) | (y >= L - 1 ? colp[L].lo : 0ull);
+    mem[L].hi = (x >= L ? rowp[L].hi : 0u) | (y >= L - 1 ? colp[L].hi : 0u);
+    lc[L] = __popcll(dlo & mem[L].lo) + __popc(dhi & mem[L].hi);
+  }
+  // do { lc = ring(level); count += lc; level++ } while (lc && level <= N)
+  int count = 1, k = N + 1;  // k: first empty ring (N+1: none within N)
+  bool open = true;
+#pragma unroll
+  for (int L = 1; L <= 4; L++) {
+    if (open && L <= N) {
+      count += lc[L];
+      if (lc[L] == 0) {
+        k = L;
+        open = false;
       }
     }
-    __syncthreads();
-    const bool again = changed != 0;
-    __syncthreads();  // every thread has read the flag before it is reset
-    if (!again) break;
   }
+  if (count > N) return;
+  // the centre and rings 1..k-1 are cleared
+  white_px<FMT>(base + (int64_t)y * pitch, x);
+#pragma unroll
+  for (int Lc = 1; Lc <= 3; Lc++) {
+    if (Lc >= k) continue;
+    uint64_t clo = dlo & mem[Lc].lo;
+    uint32_t chi = dhi & mem[Lc].hi;
+    while (clo) {
+      const int p = __ffsll((long long)clo) - 1;
+      clo &= clo - 1;
+      white_px<FMT>(base + (int64_t)(y + p / 9 - 4) * pitch, x + p % 9 - 4);
+    }
+    while (chi) {
+      const int p = 64 + __ffs(chi) - 1;
+      chi &= chi - 1;
+      white_px<FMT>(base + (int64_t)(y + p / 9 - 4) * pitch, x + p % 9 - 4);
+    }
+  }
+}
+
+// Parallel union-find over the trigger indices (parents always point to a
+// smaller index, so the CAS links never form a cycle).
+__device__ __forceinline__ uint32_t uf_find(const uint32_t* parent, uint32_t i) {
+  uint32_t p = parent[i];
+  while (p != i) {
+    i = p;
+    p = parent[i];
+  }
+  return i;
+}
+__device__ __forceinline__ void uf_union(uint32_t* parent, uint32_t a, uint32_t b) {
+  for (;;) {
+    a = uf_find(parent, a);
+    b = uf_find(parent, b);
+    if (a == b) return;
+    if (a < b) {
+      const uint32_t t = a;
+      a = b;
+      b = t;
+    }
+    if (atomicCAS(&parent[a], a, b) == a) return;
+  }
+}
+
+// The raster-order replay for intensity N <= 4, split by dependence: trigger
+// T reads pixels within Chebyshev N of itself and clears within N-1, so it can
+// only see the clears of triggers closer than 2N.  The triggers linked by that
+// relation form components that never touch each other's windows; each
+// component is replayed in raster order by one thread, all components at
+// once.  The result equals the single raster-order scan (filters.c:243-348).
+//   keys: the n trigger keys (y << 16 | x) sorted, p2 = pow2 >= n entries;
+//   aux:  p2 entries of scratch (parents, then (root << 16 | index) pairs).
+template <int FMT>
+__device__ void noise_resolve_components(const uint32_t* keys, uint32_t* aux, int n, int p2, int N,
+                                         const NoiseGeom& g, uint8_t* base, int64_t pitch) {
+  const int R = 2 * N - 1;  // dependence radius
+  for (int i = threadIdx.x; i < n; i += blockDim.x) aux[i] = (uint32_t)i;
+  __syncthreads();
+  // link every trigger to the earlier ones within R: per row of the window
+  // [y-R, y] a binary search in the sorted keys, then a short scan
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t key = keys[i];
+    const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
+    for (int yy = imax(y - R, 0); yy <= y; yy++) {
+      const uint32_t lo = ((uint32_t)yy << 16) | (uint32_t)imax(x - R, 0);
+      const uint32_t hi = ((uint32_t)yy << 16) | (uint32_t)(x + R);
+      int a = 0, b = i;  // first index in [0, i) with keys >= lo
+      while (a < b) {
+        const int mid = (a + b) >> 1;
+        if (keys[mid] < lo) a = mid + 1;
+        else b = mid;
+      }
+      for (int j = a; j < i && keys[j] <= hi; j++) uf_union(aux, (uint32_t)i, (uint32_t)j);
+    }
+  }
+  __syncthreads();
+  // flatten (a concurrent reader sees either an old parent or the root: both
+  // ancestors), then (root, index) pairs sorted so that each component's
+  // triggers are contiguous and in raster order
+  for (int i = threadIdx.x; i < n; i += blockDim.x) aux[i] = uf_find(aux, (uint32_t)i);
+  __syncthreads();
+  for (int i = threadIdx.x; i < p2; i += blockDim.x) aux[i] = i < n ? (aux[i] << 16) | (uint32_t)i : 0xFFFFFFFFu;
+  __threadfence_block();
+  __syncthreads();
+  block_sort(aux, p2);
   Mask81 rowp[5], colp[5];
 #pragma unroll
   for (int L = 1; L <= 4; L++) {
     rowp[L] = ring_part(L, true);
     colp[L] = ring_part(L, false);
   }
-  const int levels = max_level;
-  for (int L0 = 0; L0 <= levels; L0++) {
-    for (int c = w * 64; c < n; c += nw * 64) {
-      const int i = c + lane;
-      if (i >= n || lev[i] != L0) continue;
-      const uint32_t key = keys[i];
-      const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
-      // the 9x9 window: unconditional clamped loads, dark = lightness < white
-      uint64_t dlo = 0;
-      uint32_t dhi = 0;
-      bool ctr = false;
-#pragma unroll
-      for (int p = 0; p < 81; p++) {
-        const int32_t qx = x + p % 9 - 4, qy = y + p / 9 - 4;
-        const bool in = (qx >= 0) & (qy >= 0) & (qx < g.W) & (qy < g.H);
-        const Px q = load_px_row<FMT>(base + (int64_t)imin(imax(qy, 0), g.H - 1) * pitch,
-                                      imin(imax(qx, 0), g.W - 1));
-        const bool dk = in & (light_of(q) < g.white);
-        if (p < 64) dlo |= (uint64_t)dk << p;
-        else dhi |= (uint32_t)dk << (p - 64);
-        if (p == 40) ctr = dark_of(q) < g.white;
-      }
-      if (!ctr) continue;  // cleared meanwhile
-      // rings with the reference loops' unsigned comparisons: rows of ring L
-      // counted iff x >= L, its columns iff y >= L-1 (all indices static)
-      Mask81 mem[5];
-      int lc[5];
-#pragma unroll
-      for (int L = 1; L <= 4; L++) {
-        mem[L].lo = (x >= L ? rowp[L].lo : 0ull) | (y >= L - 1 ? colp[L].lo : 0ull);
-        mem[L].hi = (x >= L ? rowp[L].hi : 0u) | (y >= L - 1 ? colp[L].hi : 0u);
-        lc[L] = __popcll(dlo & mem[L].lo) + __popc(dhi & mem[L].hi);
-      }
-      // do { lc = ring(level); count += lc; level++ } while (lc && level <= N)
-      int count = 1, k = N + 1;  // k: first empty ring (N+1: none within N)
-      bool open = true;
-#pragma unroll
-      for (int L = 1; L <= 4; L++) {
-        if (open && L <= N) {
-          count += lc[L];
-          if (lc[L] == 0) {
-            k = L;
-            open = false;
-          }
-        }
-      }
-      if (count > N) continue;
-      // the centre and rings 1..k-1 are cleared
-      white_px<FMT>(base + (int64_t)y * pitch, x);
-#pragma unroll
-      for (int Lc = 1; Lc <= 3; Lc++) {
-        if (Lc >= k) continue;
-        uint64_t clo = dlo & mem[Lc].lo;
-        uint32_t chi = dhi & mem[Lc].hi;
-        while (clo) {
-          const int p = __ffsll((long long)clo) - 1;
-          clo &= clo - 1;
-          white_px<FMT>(base + (int64_t)(y + p / 9 - 4) * pitch, x + p % 9 - 4);
-        }
-        while (chi) {
-          const int p = 64 + __ffs(chi) - 1;
-          chi &= chi - 1;
-          white_px<FMT>(base + (int64_t)(y + p / 9 - 4) * pitch, x + p % 9 - 4);
-        }
-      }
+  // thread t replays the components that start in its slice of the pairs
+  const int per = (n + (int)blockDim.x - 1) / (int)blockDim.x;
+  const int b0 = threadIdx.x * per, b1 = imin(b0 + per, n);
+  for (int c = b0; c < b1; c++) {
+    const uint32_t root = aux[c] >> 16;
+    if (c > 0 && (aux[c - 1] >> 16) == root) continue;  // not a component start
+    for (int m = c; m < n && (aux[m] >> 16) == root; m++) {
+      const uint32_t key = keys[aux[m] & 0xFFFFu];
+      __threadfence_block();  // this thread's earlier clears are visible to its loads
+      replay_trigger4<FMT>((int32_t)(key & 0xFFFF), (int32_t)(key >> 16), N, g, base, pitch, rowp,
+                           colp);
     }
-    // this level's clears are read by the next level's triggers
-    __threadfence_block();
-    __syncthreads();
   }
 }
 
+constexpr int kCompCap = 16384;  // triggers the component replay keeps in LDS
+constexpr int kResolveThreads = 1024;
+
 template <int FMT>
-__global__ void __launch_bounds__(256) k_noise_resolve(PlaneRef img, NoiseGeom g, uint8_t* scratch,
+__global__ void __launch_bounds__(kResolveThreads) k_noise_resolve(PlaneRef img, NoiseGeom g, uint8_t* scratch,
                                                        int64_t sstride, const int32_t* active,
                                                        SheetCtl* ctl, uint32_t* sortbuf,
                                                        int64_t sort_stride) {
@@ -1337,6 +1363,9 @@ __global__ void __launch_bounds__(256) k_noise_resolve(PlaneRef img, NoiseGeom g
   if (active && !active[s]) return;
   NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
   uint32_t n = *NP.nseq;
+#ifdef UPHIP_DIAG
+  if ((g.diag & 8) && threadIdx.x == 0) printf("uphip noise: sheet %d seq %u clear %u\n", s, n, *NP.nclear);
+#endif
   if (n == 0) return;
   if (n > (uint32_t)g.capacity) {
     if (threadIdx.x == 0 && ctl) atomicOr(&ctl[s].status, STATUS_NOISE_OVERFLOW);
@@ -1344,22 +1373,34 @@ __global__ void __launch_bounds__(256) k_noise_resolve(PlaneRef img, NoiseGeom g
   }
   int p2 = 1;
   while (p2 < (int)n) p2 <<= 1;
-  __shared__ uint32_t lk[8192];
+  extern __shared__ uint32_t nlds[];  // keys[kCompCap], aux[kCompCap]
   uint32_t* keys;
-  if (p2 <= 8192) {
-    keys = lk;
+  if (p2 <= kCompCap) {
+    keys = nlds;
   } else {
     keys = sortbuf + s * sort_stride;  // global fallback (rare: dark edge zones)
   }
+#ifdef UPHIP_DIAG
+  const uint64_t t_start = wall_clock64();
+#endif
   for (int i = threadIdx.x; i < p2; i += blockDim.x) keys[i] = i < (int)n ? NP.seq[i] : 0xFFFFFFFFu;
   __threadfence_block();
   __syncthreads();
   block_sort(keys, p2);
+#ifdef UPHIP_DIAG
+  if ((g.diag & 8) && threadIdx.x == 0)
+    printf("uphip noise: sheet %d sort %llu ticks\n", s, (unsigned long long)(wall_clock64() - t_start));
+#endif
   const int N = g.intensity;
   uint8_t* base = plane_ptr(img, s);
   const int64_t pitch = img.P.pitch;
-  if (N <= 4 && p2 <= 8192) {
-    noise_resolve_levels<FMT>(keys, (int)n, N, g, base, pitch);
+  if (N <= 4 && p2 <= kCompCap) {
+    noise_resolve_components<FMT>(keys, nlds + kCompCap, (int)n, p2, N, g, base, pitch);
+#ifdef UPHIP_DIAG
+    if ((g.diag & 8) && threadIdx.x == 0)
+      printf("uphip noise: sheet %d replay done %llu ticks\n", s,
+             (unsigned long long)(wall_clock64() - t_start));
+#endif
     return;
   }
   if (threadIdx.x >= 64) return;
@@ -1477,7 +1518,14 @@ static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr
   hipLaunchKernelGGL(k_noise_classify<FMT>, grid, dim3(256), 0, st, img, gd, scr, ss, active, ctl);
   hipLaunchKernelGGL(k_noise_apply<FMT>, dim3(64, count), dim3(256), 0, st, img, g, scr, ss,
                      active, ctl);
-  if (!(diag_skip() & 2)) hipLaunchKernelGGL(k_noise_resolve<FMT>, dim3(count), dim3(256), 0, st, img, g, scr, ss, active,
+  constexpr size_t kResolveLds = 2 * sizeof(uint32_t) * kCompCap;  // 128 KiB
+  static bool lds_set = false;  // per instantiation; the attribute is per function
+  if (!lds_set) {
+    hipFuncSetAttribute((const void*)k_noise_resolve<FMT>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLds);
+    lds_set = true;
+  }
+  if (!(diag_skip() & 2)) hipLaunchKernelGGL(k_noise_resolve<FMT>, dim3(count), dim3(kResolveThreads), kResolveLds, st, img, gd, scr, ss, active,
                      ctl, sortbuf, sort_stride);
 }
 
