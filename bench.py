@@ -101,7 +101,7 @@ def parse():
     ap.add_argument("--no-host-io", action="store_true", help="skip figures 2 and 3")
     ap.add_argument("--no-latency", action="store_true", help="skip the C2 single-page latency")
     ap.add_argument("--host-batch", type=int, default=32, help="sheets per batch, host-fed runs")
-    ap.add_argument("--host-streams", type=int, default=4, help="batches per device, host-fed")
+    ap.add_argument("--host-streams", type=int, default=8, help="batches per device, host-fed")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC HBM bytes per launch / per page from rocprofv3 --pmc passes")
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")

@@ -433,6 +433,9 @@ int uphip_batch_download_async(UphipBatch *batch, void *host, int64_t linesize,
                                int64_t sheet_stride);
 int uphip_batch_query(UphipBatch *batch);
 void *uphip_batch_stream(UphipBatch *batch);
+/* Row pitch of the output sheets on the device: host staging with this
+ * linesize (and pitch * height per sheet) downloads as linear DMA copies. */
+int uphip_batch_output_pitch(UphipBatch *batch, int64_t *pitch);
 
 /* ---------------------------------------------------------------------------
  * Host codec — the PNM half of loadImage/saveImage (file.c:29-259).

@@ -1327,6 +1327,12 @@ int uphip_batch_get_report(UphipBatch* b, int32_t sheet, UphipSheetReport* r) {
 
 void* uphip_batch_stream(UphipBatch* b) { return b ? (void*)b->st : nullptr; }
 
+int uphip_batch_output_pitch(UphipBatch* b, int64_t* pitch) {
+  if (!b || !pitch) return -1;
+  *pitch = b->out ? b->out_pitch : b->pitch;
+  return 0;
+}
+
 int uphip_batch_query(UphipBatch* b) {
   if (!b) return -1;
   hipSetDevice(b->device);
@@ -1374,14 +1380,28 @@ int uphip_batch_download_async(UphipBatch* b, void* host, int64_t linesize, int6
                            sizeof(int32_t), n, hipMemcpyDeviceToHost)))
     return -1;
   uint8_t* h = (uint8_t*)host;
-  for (int s = 0; s < n; s++) {
-    const uint8_t* src = b->out ? b->out + (int64_t)s * b->out_stride
-                                : b->planes[cur[s] & 1] + (int64_t)s * b->plane_stride;
-    const int64_t sp = b->out ? b->out_pitch : b->pitch;
-    if (!UPH_HIP(hipMemcpy2DAsync(h + s * sheet_stride, linesize, src, sp, rb, b->out_h,
+  const int64_t sp = b->out ? b->out_pitch : b->pitch;
+  const int64_t ss = b->out ? b->out_stride : b->plane_stride;
+  auto src_of = [&](int s) -> const uint8_t* {
+    return b->out ? b->out + (int64_t)s * ss : b->planes[cur[s] & 1] + (int64_t)s * ss;
+  };
+  if (linesize == sp && sheet_stride == sp * b->out_h && ss == sheet_stride) {
+    // host staging laid out like the planes: runs of sheets in the same plane
+    // go as one linear DMA copy (2D copies run far below the link rate)
+    for (int s = 0; s < n;) {
+      int e = s + 1;
+      while (e < n && (b->out || (cur[e] & 1) == (cur[s] & 1))) e++;
+      if (!UPH_HIP(hipMemcpyAsync(h + s * sheet_stride, src_of(s), (size_t)((e - s) * ss),
+                                  hipMemcpyDeviceToHost, b->st)))
+        return -1;
+      s = e;
+    }
+    return 0;
+  }
+  for (int s = 0; s < n; s++)
+    if (!UPH_HIP(hipMemcpy2DAsync(h + s * sheet_stride, linesize, src_of(s), sp, rb, b->out_h,
                                   hipMemcpyDeviceToHost, b->st)))
       return -1;
-  }
   return 0;
 }
 

@@ -61,6 +61,14 @@ class HostPool {
     cv_.notify_all();
     for (auto& t : th_) t.join();
   }
+  // fire-and-forget task (the caller tracks completion itself)
+  void submit(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
   void parallel_for(int n, const std::function<void(int)>& fn) {
     if (n <= 0) return;
     struct Group {
@@ -397,10 +405,18 @@ UphipRunner* uphip_runner_create(const UphipOptions* options, const UphipBatchGe
   uphip_batch_output_info(b0, &r->out_w, &r->out_h, &r->out_fmt, &bytes);
   uphip_batch_input_ptr(b0, 0, &r->in_pitch);
   r->in_page_stride = r->in_pitch * geometry->page_height;
-  r->out_linesize = round_pitch(row_bytes(r->out_w, r->out_fmt));
+  // output staging laid out like the batch's output rows, so a batch's
+  // sheets come back as linear DMA copies
+  {
+    int64_t op = 0;
+    UphipBatch* bb = r->dev[0].slots[0].b;
+    r->out_linesize = round_pitch(row_bytes(r->out_w, r->out_fmt));
+    if (uphip_batch_output_pitch(bb, &op) == 0 && op >= row_bytes(r->out_w, r->out_fmt))
+      r->out_linesize = op;
+  }
   r->out_sheet_stride = r->out_linesize * r->out_h;
   const int ht = config->host_threads > 0 ? config->host_threads : 4 * (int)r->devices.size();
-  r->pool = new HostPool(ht - 1 > 0 ? ht - 1 : 0);
+  r->pool = new HostPool(ht);
   return r;
 }
 
@@ -504,6 +520,13 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
   std::atomic<int64_t> next{0};
   std::atomic<int64_t> load_ns{0}, store_ns{0};
   std::vector<std::thread> th;
+  // A slot moves FREE -> LOADING (page tasks on the host pool) -> LOADED
+  // (last task) -> RUNNING (H2D + pipeline queued on its stream) -> DRAINING
+  // (status read, D2H queued) -> STORING (sheet tasks on the pool) -> FREE
+  // (last task).  The device thread only moves slots along and never does
+  // host copies itself, so decode, DMA, kernels and encode of different
+  // slots overlap.
+  enum : int { FREE = 0, LOADING, LOADED, RUNNING, DRAINING, STORING };
   for (size_t i = 0; i < r->dev.size(); i++) {
     th.emplace_back([&, i] {
       DeviceCtx& dc = r->dev[i];
@@ -514,113 +537,137 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
         if (dc.error.empty()) dc.error = uphip_last_error() ? uphip_last_error() : what;
         uphip_clear_error();
       };
-      std::deque<Slot*> freel, running, draining;
-      for (Slot& sl : dc.slots) freel.push_back(&sl);
+      const int K = (int)dc.slots.size();
+      std::unique_ptr<std::atomic<int>[]> state(new std::atomic<int>[K]);
+      std::unique_ptr<std::atomic<int>[]> pend(new std::atomic<int>[K]);
+      std::vector<int> phase(K, FREE);  // the device thread's view
+      for (int k = 0; k < K; k++) {
+        state[k] = FREE;
+        pend[k] = 0;
+      }
+      std::deque<int> inflight;  // RUNNING / DRAINING slots in submission order
+      bool jobs_left = true;
       for (;;) {
-        // 1. fill every free slot: load the chunk into pinned memory (host
-        //    pool), then H2D + pipeline on the slot's stream
-        while (!freel.empty()) {
-          const int64_t first = next.fetch_add(S);
-          if (first >= njobs) break;
-          Slot* sl = freel.front();
-          freel.pop_front();
-          sl->first = first;
-          sl->count = (int32_t)std::min<int64_t>(S, njobs - first);
-          sl->failed.assign((size_t)sl->count, 0);
-          std::vector<char> bad((size_t)sl->count, 0);
-          const auto a = Clock::now();
-          r->pool->parallel_for(sl->count * nin, [&](int t) {
-            const int s = t / nin, j = t % nin;
-            uint8_t* dst = sl->hin + (int64_t)t * r->in_page_stride;
-            if (!load_page(r, src, first + s, j, dst)) {
-              bad[(size_t)s] = 1;
-              uphip_clear_error();
-              // the slot still runs: give it a blank (white) page, cheap and
-              // deterministic, instead of stale staging bytes
-              memset(dst, r->geo.page_format == UPHIP_FMT_MONOWHITE ? 0x00 : 0xFF,
-                     (size_t)r->in_page_stride);
+        bool progress = false;
+        for (int k = 0; k < K; k++) {
+          Slot* sl = &dc.slots[(size_t)k];
+          const int st = state[k].load();
+          if (st == FREE && phase[k] == STORING) {  // stored: account the chunk
+            for (int s = 0; s < sl->count; s++) {
+              if (sl->failed[(size_t)s]) {
+                dc.failed++;
+                if ((sl->failed[(size_t)s] & 2) && dc.error.empty()) dc.error = "a sheet could not be stored";
+                if ((sl->failed[(size_t)s] & 4) && dc.error.empty()) dc.error = "a page could not be loaded";
+              } else {
+                dc.done++;
+              }
             }
-          });
-          load_ns += (int64_t)(secs(a, Clock::now()) * 1e9);
-          for (int s = 0; s < sl->count; s++)
-            if (bad[(size_t)s]) {
-              sl->failed[(size_t)s] = 1;
-              if (dc.error.empty()) dc.error = "a page could not be loaded";
+            phase[k] = FREE;
+            progress = true;
+          }
+          if (st == FREE && phase[k] == FREE && jobs_left) {
+            const int64_t first = next.fetch_add(S);
+            if (first >= njobs) {
+              jobs_left = false;
+              continue;
             }
-          if (uphip_batch_upload_async(sl->b, sl->count, sl->hin, r->in_pitch, r->in_page_stride) != 0 ||
-              uphip_batch_run(sl->b, sl->count) != 0) {
-            note("run failed");
-            dc.failed += sl->count;
-            freel.push_back(sl);
+            sl->first = first;
+            sl->count = (int32_t)std::min<int64_t>(S, njobs - first);
+            sl->failed.assign((size_t)sl->count, 0);
+            pend[k] = sl->count;
+            state[k] = LOADING;
+            phase[k] = LOADING;
+            for (int s = 0; s < sl->count; s++) {
+              r->pool->submit([&, sl, k, s, first] {
+                const auto a = Clock::now();
+                for (int j = 0; j < nin; j++) {
+                  uint8_t* dst = sl->hin + ((int64_t)s * nin + j) * r->in_page_stride;
+                  if (!load_page(r, src, first + s, j, dst)) {
+                    sl->failed[(size_t)s] |= 4;
+                    uphip_clear_error();
+                    // the slot still runs: a blank (white) page, cheap and
+                    // deterministic, instead of stale staging bytes
+                    memset(dst, r->geo.page_format == UPHIP_FMT_MONOWHITE ? 0x00 : 0xFF,
+                           (size_t)r->in_page_stride);
+                  }
+                }
+                load_ns += (int64_t)(secs(a, Clock::now()) * 1e9);
+                if (pend[k].fetch_sub(1) == 1) state[k] = LOADED;
+              });
+            }
+            progress = true;
+          }
+          if (st == LOADED && phase[k] == LOADING) {
+            if (uphip_batch_upload_async(sl->b, sl->count, sl->hin, r->in_pitch, r->in_page_stride) != 0 ||
+                uphip_batch_run(sl->b, sl->count) != 0) {
+              note("run failed");
+              for (int s = 0; s < sl->count; s++) sl->failed[(size_t)s] |= 1;
+              phase[k] = STORING;  // accounted (all failed) on the next pass
+              state[k] = FREE;
+            } else {
+              phase[k] = RUNNING;
+              state[k] = RUNNING;
+              inflight.push_back(k);
+            }
+            progress = true;
+          }
+        }
+        // the oldest slots on the GPU: a finished run -> its D2H; a finished
+        // D2H -> the sink, in submission order
+        for (size_t q = 0; q < inflight.size();) {
+          const int k = inflight[q];
+          Slot* sl = &dc.slots[(size_t)k];
+          if (uphip_batch_query(sl->b) != 1) break;
+          if (phase[k] == RUNNING) {
+            std::vector<char> pre = sl->failed;
+            collect_failures(*sl);  // the stream is idle: a status read only
+            for (size_t s = 0; s < pre.size(); s++) sl->failed[s] |= pre[s];
+            if (uphip_batch_download_async(sl->b, sl->hout, r->out_linesize, r->out_sheet_stride) != 0) {
+              note("download failed");
+              for (int s = 0; s < sl->count; s++) sl->failed[(size_t)s] |= 1;
+              inflight.erase(inflight.begin() + (long)q);
+              phase[k] = STORING;
+              state[k] = FREE;
+              progress = true;
+              continue;
+            }
+            phase[k] = DRAINING;
+            state[k] = DRAINING;
+            progress = true;
+            q++;
             continue;
           }
-          running.push_back(sl);
-        }
-        // 2. a finished run: its status, then the D2H of its sheets on its stream;
-        // 3. a finished download: the sheets go to the sink (host pool).
-        // Ready work first; when nothing is ready, block on the oldest download
-        // (short) or else the oldest run.
-        auto drain = [&](Slot* sl) {
-          std::vector<char> pre = sl->failed;
-          collect_failures(*sl);  // synchronises the slot stream
-          for (size_t s = 0; s < pre.size(); s++) sl->failed[s] |= pre[s];
-          if (uphip_batch_download_async(sl->b, sl->hout, r->out_linesize, r->out_sheet_stride) != 0) {
-            note("download failed");
-            dc.failed += sl->count;
-            freel.push_back(sl);
-            return;
-          }
-          draining.push_back(sl);
-        };
-        auto store = [&](Slot* sl) {
-          if (uphip_batch_wait(sl->b) != 0) note("download failed");
-          std::vector<char> ok((size_t)sl->count, 1);
-          const auto a = Clock::now();
-          r->pool->parallel_for(sl->count, [&](int s) {
-            if (sl->failed[(size_t)s]) return;
-            bool good = true;
-            store_sheet(r, sink, sl->first + s, sl->hout + (int64_t)s * r->out_sheet_stride, &good);
-            if (!good) {
-              ok[(size_t)s] = 0;
-              uphip_clear_error();
-            }
-          });
-          store_ns += (int64_t)(secs(a, Clock::now()) * 1e9);
-          for (int s = 0; s < sl->count; s++) {
-            if (sl->failed[(size_t)s] || !ok[(size_t)s]) {
-              dc.failed++;
-              if (!ok[(size_t)s] && dc.error.empty()) dc.error = "a sheet could not be stored";
-            } else {
-              dc.done++;
+          // DRAINING and the copy is done
+          inflight.erase(inflight.begin() + (long)q);
+          int nstore = 0;
+          for (int s = 0; s < sl->count; s++) nstore += !sl->failed[(size_t)s];
+          phase[k] = STORING;
+          if (nstore == 0) {
+            state[k] = FREE;
+          } else {
+            pend[k] = nstore;
+            state[k] = STORING;
+            for (int s = 0; s < sl->count; s++) {
+              if (sl->failed[(size_t)s]) continue;
+              r->pool->submit([&, sl, k, s] {
+                const auto a = Clock::now();
+                bool good = true;
+                store_sheet(r, sink, sl->first + s, sl->hout + (int64_t)s * r->out_sheet_stride, &good);
+                if (!good) {
+                  sl->failed[(size_t)s] |= 2;
+                  uphip_clear_error();
+                }
+                store_ns += (int64_t)(secs(a, Clock::now()) * 1e9);
+                if (pend[k].fetch_sub(1) == 1) state[k] = FREE;
+              });
             }
           }
-          freel.push_back(sl);
-        };
-        if (!draining.empty() && uphip_batch_query(draining.front()->b) == 1) {
-          Slot* sl = draining.front();
-          draining.pop_front();
-          store(sl);
-          continue;
+          progress = true;
         }
-        if (!running.empty() && uphip_batch_query(running.front()->b) == 1) {
-          Slot* sl = running.front();
-          running.pop_front();
-          drain(sl);
-          continue;
-        }
-        if (!draining.empty()) {
-          Slot* sl = draining.front();
-          draining.pop_front();
-          store(sl);
-          continue;
-        }
-        if (!running.empty()) {
-          Slot* sl = running.front();
-          running.pop_front();
-          drain(sl);
-          continue;
-        }
-        if (running.empty() && draining.empty()) break;
+        bool idle = !jobs_left;
+        for (int k = 0; k < K && idle; k++) idle = state[k].load() == FREE && phase[k] == FREE;
+        if (idle) break;
+        if (!progress) std::this_thread::sleep_for(std::chrono::microseconds(20));
       }
     });
   }
