@@ -45,18 +45,23 @@ HIPFLAGS   := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
 CFLAGS_O   := -O2 -std=gnu11 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result
 
 CTEST      := tests/c/_build/backend_ops
+# the reference-side adapter (integration/) compiled against the reference's
+# own headers, where they lie; skipped when the tree is absent (GPU box)
+REFERENCE  ?= /root/reference
+ADAPTER    := tests/c/_build/adapter_ops
 
 SANITIZE   := tests/c/_build/sanitize
 LLVMCC     := /opt/rocm/lib/llvm/bin/clang
 SANFLAGS   := -fsanitize=address,undefined -fno-sanitize-recover=undefined \
               -fno-omit-frame-pointer -g -O1
 
-.PHONY: all lib oracle ctest sanitize clean
+.PHONY: all lib oracle ctest adapter sanitize clean
 all: lib oracle ctest
 
 lib: $(LIB)
 oracle: $(ORACLE_LIB)
 ctest: $(CTEST)
+adapter: $(ADAPTER)
 
 $(OBJDIR)/%.hip.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -79,9 +84,18 @@ $(ORACLE_LIB): oracle/oracle.c oracle/oracle.h include/unpaper_hip.h
 	$(CC) $(CFLAGS_O) -shared -o $@ oracle/oracle.c -lm
 
 # A plain C program: the reference's own callers are C (sheet_stages.c).
-$(CTEST): tests/c/backend_ops.c include/unpaper_hip.h oracle/oracle.h $(LIB) $(ORACLE_LIB)
+$(CTEST): tests/c/backend_ops.c tests/c/pages.h include/unpaper_hip.h oracle/oracle.h $(LIB) $(ORACLE_LIB)
 	@mkdir -p tests/c/_build
 	$(CC) -O2 -std=gnu11 -Wall -Iinclude $< -o $@ \
+	  -L$(PKG)/lib -L oracle/_build -lunpaper_hip -loracle -lm \
+	  -Wl,-rpath,'$$ORIGIN/../../../$(PKG)/lib' -Wl,-rpath,'$$ORIGIN/../../../oracle/_build'
+
+$(ADAPTER): tests/c/adapter_main.c tests/c/pages.h integration/backend_hip.c integration/backend_hip.h \
+            integration/hip_frame.h include/unpaper_hip.h oracle/oracle.h $(LIB) $(ORACLE_LIB)
+	@test -f $(REFERENCE)/imageprocess/image.h || { echo "adapter: no reference headers under $(REFERENCE)"; exit 1; }
+	@mkdir -p tests/c/_build
+	$(CC) -O2 -std=gnu11 -Wall -Wno-unused-variable -I$(REFERENCE) -Iinclude -Iintegration \
+	  tests/c/adapter_main.c integration/backend_hip.c -o $@ \
 	  -L$(PKG)/lib -L oracle/_build -lunpaper_hip -loracle -lm \
 	  -Wl,-rpath,'$$ORIGIN/../../../$(PKG)/lib' -Wl,-rpath,'$$ORIGIN/../../../oracle/_build'
 
