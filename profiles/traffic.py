@@ -4,7 +4,12 @@ rocprofv3 --pmc passes of the same command: one with FETCH_SIZE, one with
 WRITE_SIZE (they do not fit in one pass on gfx950).
 
 usage: traffic.py <fetch-pass dir> <write-pass dir> <kernel-substring> <stage> \
-                  <alg-bytes-per-launch> <pages-per-launch> [out.json]
+                  <alg-bytes-per-launch> <pages-per-launch> <pages-in-run> [out.json]
+
+Besides the named kernel it sums every pipeline dispatch of the run (all
+kernels except the synthetic-page generator) into HBM bytes per page: the
+whole-pipeline FETCH+WRITE figure bench.py reports as
+roofline.pipeline_hbm_bytes_per_page.
 
 Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are
 in KiB; FETCH_SIZE tallies half of the bytes of coalesced streaming reads on
@@ -20,15 +25,23 @@ import os
 import sys
 
 
-def per_launch(path, counter):
+def dispatches(path, counter):
     if os.path.isdir(path):
-        path = glob.glob(os.path.join(path, "*counter_collection.csv"))[0]
+        path = glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True)[0]
     acc = collections.defaultdict(list)
     with open(path) as f:
         for r in csv.DictReader(f):
             if r["Counter_Name"] == counter:
                 acc[r["Kernel_Name"]].append(float(r["Counter_Value"]) * 1024.0)
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+    return acc
+
+
+def per_launch(path, counter):
+    return {k: sum(v) / len(v) for k, v in dispatches(path, counter).items()}
+
+
+def pipeline_total(path, counter):
+    return sum(sum(v) for k, v in dispatches(path, counter).items() if "synth" not in k)
 
 
 def pick(d, sub):
@@ -39,9 +52,9 @@ def pick(d, sub):
 
 
 def main():
-    fdir, wdir, kern, stage, alg, pages = sys.argv[1:7]
-    out = sys.argv[7] if len(sys.argv) > 7 else os.path.join(os.path.dirname(__file__), "traffic.json")
-    alg, pages = int(alg), int(pages)
+    fdir, wdir, kern, stage, alg, pages, run_pages = sys.argv[1:8]
+    out = sys.argv[8] if len(sys.argv) > 8 else os.path.join(os.path.dirname(__file__), "traffic.json")
+    alg, pages, run_pages = int(alg), int(pages), int(run_pages)
     fetch, write = per_launch(fdir, "FETCH_SIZE"), per_launch(wdir, "WRITE_SIZE")
     for ref in ("k_copy", "k_colsum_g"):
         try:
@@ -54,7 +67,8 @@ def main():
     name = kern.split("(")[0].split("::")[-1]
     doc = {
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) --kernel-trace "
-                  "-- python3 bench.py --pages 128 --steps 1 --warmup 1 --streams 1 --no-cpu; "
+                  "-- python3 bench.py --pages 128 --steps 1 --warmup 0 --streams 1 --probe 0 "
+                  "--no-cpu --no-host-io --no-latency --no-verify (tools/pmc_passes.sh); "
                   "1 MI355X; %d sheets per launch" % pages,
         "correction": "FETCH_SIZE x2 (gfx950 tallies half of coalesced streaming reads); "
                       "counter values are KiB",
@@ -64,6 +78,13 @@ def main():
                            "alg_bytes_per_launch": alg}},
         "bytes_per_page": {stage: int(hbm / pages)},
     }
+    pf, pw = pipeline_total(fdir, "FETCH_SIZE"), pipeline_total(wdir, "WRITE_SIZE")
+    doc["pipeline_fetch_bytes_per_page"] = int(2 * pf / run_pages)
+    doc["pipeline_write_bytes_per_page"] = int(pw / run_pages)
+    doc["pipeline_bytes_per_page"] = int((2 * pf + pw) / run_pages)
+    doc["pipeline_pages_in_run"] = run_pages
+    print("pipeline: fetch x2 %.1f MB + write %.1f MB = %.1f MB per page" %
+          (2 * pf / run_pages / 1e6, pw / run_pages / 1e6, (2 * pf + pw) / run_pages / 1e6))
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)
     print("%s: fetch %.1f MB (x2 %.1f) + write %.1f MB = %.1f MB/launch vs alg %.1f MB (%.3fx)" %

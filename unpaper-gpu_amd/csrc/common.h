@@ -13,11 +13,29 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <mutex>
+#include <set>
+#include <utility>
+
 #include "unpaper_hip.h"
 
 #define UPH_HD __host__ __device__ __forceinline__
 
 namespace uph {
+
+// Dynamic LDS above 64 KiB needs the kernel's attribute raised, once per
+// device and kernel (the whole CU's 160 KiB, so any size up to it launches).
+inline void allow_dynamic_lds(const void* kernel, size_t bytes) {
+  if (bytes <= 64 * 1024) return;
+  static std::mutex mu;
+  static std::set<std::pair<int, const void*>> done;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  if (done.insert({dev, kernel}).second)
+    (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
 
 // Pixel layouts the kernels address directly.  MONO* are only handled by the
 // conversion / copy / fill / geometry kernels (see kernels_blit.hip).

@@ -71,6 +71,7 @@ struct BlackGeom {
   uint8_t mask_max;       // image.abs_black_threshold
   uint64_t intensity;
   int32_t stack_capacity; // DFS frames per sheet
+  int32_t diag;           // tuning build only: bit 16 prints replay counters
 };
 // Enumerates the bars exactly as blackfilter_scan's loops visit them.
 bool black_geometry(int32_t W, int32_t H, const UphipBlackfilterParameters& p, uint8_t mask_max,

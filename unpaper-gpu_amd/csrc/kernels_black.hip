@@ -10,8 +10,9 @@
 // line position its two perpendicular neighbours, depth first) is order-
 // dependent (lines stop on painted pixels, and paint up to intensity-1
 // non-matching pixels), so one wave replays it: an explicit stack of frames in
-// HBM, every fill_line and every run of neighbour checks done 64 pixels per
-// step with ballots.
+// HBM, one workgroup per sheet: the four fill_lines of a frame together, and
+// the neighbour and bar-pixel checks in windows of 4096 read ahead, 64 pixels
+// per ballot, the window's slices spread over the workgroup's waves.
 #include <climits>
 
 #include "filters.h"
@@ -27,6 +28,7 @@ bool black_geometry(int32_t W, int32_t H, const UphipBlackfilterParameters& p, u
   g->intensity = (uint64_t)(int64_t)p.intensity;
   g->nbars = 0;
   g->nbars_h = 0;
+  g->diag = 0;
   g->hregion = Rect{0, 0, -1, -1};
   g->vregion = Rect{0, 0, -1, -1};
   int64_t cap = (int64_t)W * H;
@@ -84,13 +86,76 @@ size_t black_scratch_bytes(const BlackGeom& g) {
 struct Frame {
   int32_t x, y;
   int32_t dist[4];
-  int32_t dir;
-  int32_t idx;  // next child: 2*d + sub along line `dir`
+  int32_t cursor;  // next neighbour check, over the four lines' checks in order
+  int32_t pad;
 };
 
 // left, up, right, down (fill.c:92-106)
-__constant__ int kDX[4] = {-1, 0, 1, 0};
-__constant__ int kDY[4] = {0, -1, 0, 1};
+__device__ __forceinline__ constexpr int dir_dx(int d) { return d == 0 ? -1 : d == 2 ? 1 : 0; }
+__device__ __forceinline__ constexpr int dir_dy(int d) { return d == 1 ? -1 : d == 3 ? 1 : 0; }
+
+template <class T>
+__device__ __forceinline__ T pick4(const T (&a)[4], int d) {
+  return d == 0 ? a[0] : d == 1 ? a[1] : d == 2 ? a[2] : a[3];
+}
+template <class T>
+__device__ __forceinline__ void set4(T (&a)[4], int d, T v) {
+  if (d == 0) a[0] = v;
+  else if (d == 1) a[1] = v;
+  else if (d == 2) a[2] = v;
+  else a[3] = v;
+}
+
+// The replay is one workgroup of kWaves waves per sheet.  Control (the DFS
+// stack, the current frame, the bar loop) is uniform: every wave runs it on
+// the same values, read from LDS after a barrier.  The per-pixel work of a
+// round trip is a window of kSlices 64-pixel slices, kGroup per wave.
+constexpr int kWaves = 8;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kGroup = 8;
+constexpr int kSlices = kWaves * kGroup;  // 64 slices = 4096 pixels per round trip
+static_assert(kSlices == 64, "lane-parallel reads of the per-slice tables assume 64 slices");
+
+// Per-round-trip tables in LDS (the window's results of each wave).
+constexpr int kOffStop = 0;                       // i32[2 * kWaves]: last match, first stop
+constexpr int kOffFirst = kOffStop + kWaves;      // i32[2][kWaves] first matches
+constexpr int kOffRed = kOffFirst + kWaves;       // u64[kWaves] sums
+constexpr int kOffCand = kOffRed + kWaves;        // u64[kWaves] candidate bars
+constexpr int kReplayWords = kOffCand + kWaves;   // in 8-byte units
+
+__device__ __forceinline__ uint64_t* lds64() {
+  __shared__ uint64_t black_tables[kReplayWords];
+  return black_tables;
+}
+__device__ __forceinline__ int32_t* tab_stop() { return (int32_t*)(lds64() + kOffStop); }
+__device__ __forceinline__ int32_t* tab_first() { return (int32_t*)(lds64() + kOffFirst); }
+__device__ __forceinline__ uint64_t* tab_red() { return lds64() + kOffRed; }
+__device__ __forceinline__ uint64_t* tab_cand() { return lds64() + kOffCand; }
+
+// scalar (readfirstlane), so everything derived from it stays in SGPRs
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int32_t wave_min(int32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v = imin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// barrier with a workgroup fence: paints (image stores) of every wave are
+// visible to every wave after it
+__device__ __forceinline__ void block_sync() { __syncthreads(); }
+// replay counters, tuning build only (UPHIP_DIAG_NOISE bit 16)
+struct BlackStats {
+  uint32_t frames, fill_trips, check_trips, bar_trips, remeasures, lookups;
+  uint64_t t_fill, t_check, t_bar, t_remeasure, t_fa, t_fb, t_fc, t_fd, t_fa0, t_fa1;
+};
+#ifdef UPHIP_DIAG
+#define BSTAT(...) __VA_ARGS__
+#else
+#define BSTAT(...)
+#endif
 
 template <int FMT>
 struct Canvas {
@@ -98,190 +163,299 @@ struct Canvas {
   int64_t pitch;
   int32_t W, H;
   uint8_t mmax;  // mask_max (mask_min is 0)
+  BlackStats* bs;  // tuning build counters
   __device__ __forceinline__ bool inside(int32_t x, int32_t y) const {
     return x >= 0 && y >= 0 && x < W && y < H;
   }
-  __device__ __forceinline__ uint8_t gray(int32_t x, int32_t y) const {
-    if (!inside(x, y)) return 255;
-    return gray_of(load_px_row<FMT>(base + (int64_t)y * pitch, x));
-  }
-  __device__ __forceinline__ bool match(int32_t x, int32_t y) const { return gray(x, y) <= mmax; }
-  // match() as an unconditional load at a clamped position (no divergent
-  // branch around the load, so a batch of them is in flight together)
-  __device__ __forceinline__ bool match_nb(int32_t x, int32_t y) const {
-    const bool in = (x >= 0) & (y >= 0) & (x < W) & (y < H);
-    const int32_t cx = imin(imax(x, 0), W - 1), cy = imin(imax(y, 0), H - 1);
-    return in & (gray_of(load_px_row<FMT>(base + (int64_t)cy * pitch, cx)) <= mmax);
+  // kGroup matches of this wave: the loads of all slices are issued before
+  // any is used, so one memory round trip serves the group.  x < 0 means "no
+  // position" (no match).
+  __device__ __forceinline__ void match_group(const int32_t (&x)[kGroup],
+                                              const int32_t (&y)[kGroup],
+                                              bool (&m)[kGroup]) const {
+    uint8_t g[kGroup];
+#pragma unroll
+    for (int k = 0; k < kGroup; k++) {
+      const int32_t cy = imin(imax(y[k], 0), H - 1), cx = imin(imax(x[k], 0), W - 1);
+      g[k] = gray_of(load_px_row<FMT>(base + (int64_t)cy * pitch, cx));
+    }
+#pragma unroll
+    for (int k = 0; k < kGroup; k++) m[k] = inside(x[k], y[k]) && g[k] <= mmax;
+    BSTAT(bs->lookups += kGroup;)
   }
   __device__ __forceinline__ void paint(int32_t x, int32_t y) const {
     if (inside(x, y)) store_px_row<FMT>(base + (int64_t)y * pitch, x, Px{255, 255, 255});
   }
 };
 
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-}
-
-constexpr int kSlices = 8;  // 64-pixel slices evaluated per memory round trip
-
-// fill_line (fill.c:16-52) for one wave: returns the distance painted.  The
-// 512 positions of a round are loaded together; they are consumed slice by
-// slice in order (a line never revisits its pixels, so painting a slice does
-// not change the matches of the next).
+// The four fill_lines (fill.c:16-52) from (px,py); dist[d] = pixels painted.
+// Per line a counter starts at 1, resets to `intensity` on a match and
+// decrements otherwise; the line stops (unpainted) where it reaches 0 or
+// leaves the image.  The four lines touch disjoint pixels (left, up, right,
+// down of the start), so they share each round trip: the window's slices are
+// split evenly over the lines still running, whole waves per line (a line
+// gets 16, 32 or 64 slices, a wave 8).  A round trip is
+//   A: lookups; each wave posts the last match of its slices;
+//   B: each wave, given the last match of the line before its slices (from
+//      the posts of the line's earlier waves), posts its first stop;
+//   C: per line, the first stop posted, or the carry for the next trip;
+//   D: paint up to the stop.
 template <int FMT>
-__device__ int32_t fill_line(const Canvas<FMT>& C, int32_t px, int32_t py, int dir,
-                             uint64_t intensity) {
-  const int lane = threadIdx.x & 63;
-  const int dx = kDX[dir], dy = kDY[dir];
-  bool has_last = false;
-  int64_t last = 0;  // position of the last matching pixel so far
-  for (int64_t pos0 = 1;; pos0 += 64 * kSlices) {
-    bool mk[kSlices];
+__device__ __forceinline__ void fill_lines(const Canvas<FMT>& C, int32_t px, int32_t py,
+                                           uint64_t intensity, int32_t (&dist)[4],
+                                           BlackStats* bs) {
+  const int w = wave_id(), lane = lane_id();
+  int32_t* wlast = tab_stop();            // [kWaves] last match of a wave's slices, or -1
+  int32_t* wstop = tab_stop() + kWaves;   // [kWaves] first stop of a wave's slices, or INT_MAX
+  BSTAT(const uint64_t t0 = wall_clock64();)
+  uint32_t done = 0, has_last = 0;  // per line bits (bool arrays indexed by a
+                                    // run-time line would live in scratch)
+  int32_t last[4] = {0, 0, 0, 0};   // positions along a line fit 31 bits
+  int32_t pos0[4] = {1, 1, 1, 1};
+  const uint64_t upto_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+  for (;;) {
+    uint32_t actp = 0;  // running lines, a nibble each
+    int nact = 0;
 #pragma unroll
-    for (int k = 0; k < kSlices; k++) {
-      const int64_t j = pos0 + 64 * k + lane;
-      mk[k] = C.match_nb(px + (int32_t)(j * dx), py + (int32_t)(j * dy));
+    for (int d = 0; d < 4; d++)
+      if (!((done >> d) & 1)) actp |= (uint32_t)d << (4 * nact++);
+    if (nact == 0) break;
+    const int lg = nact == 1 ? 6 : nact == 2 ? 5 : 4;  // log2 slices per line
+    const int spd = 1 << lg, wpl = spd / kGroup;        // slices, waves per line
+    // this wave's line and first slice (uniform)
+    const int a = (w * kGroup) >> lg, k0 = (w * kGroup) & (spd - 1);
+    const bool valid = a < nact;
+    const int d = (int)((actp >> (4 * (valid ? a : 0))) & 15);
+    const int32_t base0 = pick4(pos0, d) + 64 * k0;  // position of lane 0, slice 0
+    BSTAT(uint64_t tp = wall_clock64();)
+    // A
+    int32_t qx[kGroup], qy[kGroup];
+    bool m[kGroup];
+#pragma unroll
+    for (int i = 0; i < kGroup; i++) {
+      const int32_t j = base0 + 64 * i + lane;
+      qx[i] = !valid ? -1 : d == 0 ? px - j : d == 2 ? px + j : px;
+      qy[i] = d == 1 ? py - j : d == 3 ? py + j : py;
     }
+    BSTAT(bs->t_fa0 += wall_clock64() - tp;)
+    C.match_group(qx, qy, m);
+    BSTAT(bs->t_fa1 += wall_clock64() - tp;)
+    uint64_t M[kGroup];
+    int32_t mylast = -1;
 #pragma unroll
-    for (int k = 0; k < kSlices; k++) {
-      const int64_t pos = pos0 + 64 * k, j = pos + lane;
-      const int32_t qx = px + (int32_t)(j * dx), qy = py + (int32_t)(j * dy);
-      const bool in = C.inside(qx, qy);
-      const unsigned long long M = __ballot(mk[k]);
-      // last match at or before this lane within the slice
-      const unsigned long long upto = M & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-      bool hl = has_last;
-      int64_t lm = last;
-      if (upto) {
+    for (int i = 0; i < kGroup; i++) {
+      M[i] = __ballot(m[i]);
+      if (M[i]) mylast = base0 + 64 * i + (63 - __clzll((long long)M[i]));
+    }
+    if (lane == 0) wlast[w] = valid ? mylast : -1;
+    block_sync();
+    BSTAT(bs->t_fa += wall_clock64() - tp; tp = wall_clock64();)
+    // B: carry from the line's earlier waves, then slice by slice
+    if (valid) {
+      const int wa0 = a * wpl;  // the line's first wave
+      const int32_t lv = (lane >= wa0 && lane < w) ? wlast[lane] : -1;
+      const unsigned long long nz = __ballot(lv >= 0);
+      bool hl = (has_last >> d) & 1;
+      int32_t lm = pick4(last, d);
+      if (nz) {
         hl = true;
-        lm = pos + (63 - __clzll((long long)upto));
+        lm = __shfl(lv, 63 - __clzll((long long)nz), 64);
       }
-      // counter starts at 1, resets to `intensity` on a match, decrements
-      // otherwise; the line stops (unpainted) where it reaches 0 or leaves
-      bool stop = !in;
-      if (hl) stop |= (uint64_t)(j - lm) >= intensity;
-      else stop |= j >= 1;
-      const unsigned long long S = __ballot(stop);
-      const int first = S ? __ffsll((long long)S) - 1 : 64;
-      if (lane < first) C.paint(qx, qy);
-      if (S) {
-        wave_sync();
-        return (int32_t)(pos + first - 1);
+      int32_t first_stop = INT_MAX;
+#pragma unroll
+      for (int i = 0; i < kGroup; i++) {
+        if (first_stop != INT_MAX) break;
+        const int32_t p0 = base0 + 64 * i, j = p0 + lane;
+        const unsigned long long upto = M[i] & upto_mask;
+        bool lhl = hl;
+        int32_t llm = lm;
+        if (upto) {
+          lhl = true;
+          llm = p0 + (63 - __clzll((long long)upto));
+        }
+        bool st = !C.inside(qx[i], qy[i]);
+        if (lhl) st |= (uint64_t)(uint32_t)(j - llm) >= intensity;
+        else st |= j >= 1;
+        const unsigned long long S = __ballot(st);
+        if (S) first_stop = p0 + __ffsll((long long)S) - 1;
+        if (M[i]) {
+          hl = true;
+          lm = p0 + (63 - __clzll((long long)M[i]));
+        }
       }
-      if (M) {
-        has_last = true;
-        last = pos + (63 - __clzll((long long)M));
+      if (lane == 0) wstop[w] = first_stop;
+    }
+    block_sync();
+    BSTAT(bs->t_fb += wall_clock64() - tp; tp = wall_clock64();)
+    // C (uniform): per line the first posted stop, else the carry
+    const int32_t vs = lane < kWaves ? wstop[lane] : INT_MAX;
+    const int32_t vl = lane < kWaves ? wlast[lane] : -1;
+    const unsigned long long stops = __ballot(vs != INT_MAX), lasts = __ballot(vl >= 0);
+    int32_t sd[4] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX};
+#pragma unroll
+    for (int aa = 0; aa < 4; aa++) {
+      if (aa >= nact) break;
+      const int dd = (int)((actp >> (4 * aa)) & 15);
+      const unsigned long long range = ((1ull << wpl) - 1) << (aa * wpl);
+      if (stops & range) {
+        const int32_t s = __shfl(vs, __ffsll((long long)(stops & range)) - 1, 64);
+        set4(sd, dd, s);
+        done |= 1u << dd;
+        set4(dist, dd, s - 1);
+      } else {
+        if (lasts & range) {
+          has_last |= 1u << dd;
+          set4(last, dd, __shfl(vl, 63 - __clzll((long long)(lasts & range)), 64));
+        }
+        set4(pos0, dd, pick4(pos0, dd) + 64 * spd);
       }
     }
-    wave_sync();
+    BSTAT(bs->t_fc += wall_clock64() - tp; tp = wall_clock64();)
+    // D
+    if (valid) {
+      const int32_t lim = pick4(sd, d);
+      uint32_t on = 0;
+#pragma unroll
+      for (int i = 0; i < kGroup; i++) on |= (uint32_t)(base0 + 64 * i + lane < lim) << i;
+#pragma unroll
+      for (int i = 0; i < kGroup; i++)
+        if ((on >> i) & 1) C.paint(qx[i], qy[i]);
+    }
+    block_sync();
+    BSTAT(bs->t_fd += wall_clock64() - tp; bs->fill_trips++;)
   }
+  BSTAT(bs->t_fill += wall_clock64() - t0;)
 }
 
 template <int FMT>
-__device__ bool frame_start(const Canvas<FMT>& C, int32_t x, int32_t y, uint64_t intensity,
-                            Frame* f) {
-  // first half of flood_fill (fill.c:81-96)
-  if (!C.match(x, y)) return false;
-  if ((threadIdx.x & 63) == 0) C.paint(x, y);
-  wave_sync();
+__device__ __forceinline__ void frame_start(const Canvas<FMT>& C, int32_t x, int32_t y, uint64_t intensity,
+                            Frame* f, BlackStats* bs) {
+  // first half of flood_fill (fill.c:81-96); the caller has just read the
+  // start pixel as matching (a neighbour check or a bar pixel) and nothing
+  // has painted since
+  if (threadIdx.x == 0) C.paint(x, y);
+  block_sync();
   f->x = x;
   f->y = y;
-  for (int d = 0; d < 4; d++) f->dist[d] = fill_line<FMT>(C, x, y, d, intensity);
-  f->dir = 0;
-  f->idx = 0;
-  return true;
+  fill_lines<FMT>(C, x, y, intensity, f->dist, bs);
+  f->cursor = 0;
+  BSTAT(bs->frames++;)
 }
 
-// flood_fill (fill.c:81-107) + flood_fill_around_line (fill.c:62-79), one wave.
+// Neighbour check number c of a frame (flood_fill_around_line, fill.c:62-79):
+// the checks of line 0, then 1, 2, 3; along a line two per position, below
+// then above (horizontal line) or right then left (vertical line).
+__device__ __forceinline__ void check_pos(const Frame& f, int32_t c, int32_t* qx, int32_t* qy) {
+  const int32_t n0 = 2 * f.dist[0], n1 = n0 + 2 * f.dist[1], n2 = n1 + 2 * f.dist[2];
+  const int d = c < n0 ? 0 : c < n1 ? 1 : c < n2 ? 2 : 3;
+  const int32_t cc = c - (d == 0 ? 0 : d == 1 ? n0 : d == 2 ? n1 : n2);
+  const int32_t t = (cc >> 1) + 1, sub = cc & 1;
+  const int dx = dir_dx(d), dy = dir_dy(d);
+  int32_t x = f.x + t * dx, y = f.y + t * dy;
+  if (dx != 0) y += sub == 0 ? 1 : -1;  // below, then above
+  else x += sub == 0 ? 1 : -1;           // right, then left
+  *qx = x;
+  *qy = y;
+}
+
+// First match of a window whose slices were looked up by every wave: each
+// wave posts the index of its first matching position (or INT_MAX) into the
+// buffer of this round trip's parity, then all read the minimum.
+__device__ __forceinline__ int32_t window_first(const uint64_t (&M)[kGroup], int parity) {
+  const int w = wave_id(), lane = lane_id();
+  int32_t lf = INT_MAX;
+#pragma unroll
+  for (int i = kGroup - 1; i >= 0; i--)
+    if (M[i]) lf = 64 * (w * kGroup + i) + __ffsll((long long)M[i]) - 1;
+  int32_t* first = tab_first() + parity * kWaves;
+  if (lane == 0) first[w] = lf;
+  block_sync();
+  // waves hold consecutive slices: the first wave that found one has the minimum
+  const int32_t v = lane < kWaves ? first[lane] : INT_MAX;
+  const unsigned long long any = __ballot(v != INT_MAX);
+  return any ? __shfl(v, __ffsll((long long)any) - 1, 64) : INT_MAX;
+}
+
+// flood_fill (fill.c:81-107) + flood_fill_around_line (fill.c:62-79), depth
+// first with an explicit stack in HBM; control is uniform over the workgroup.
 template <int FMT>
-__device__ bool flood_fill(const Canvas<FMT>& C, int32_t sx, int32_t sy, uint64_t intensity,
-                           Frame* stack, int32_t capacity, bool* painted) {
-  const int lane = threadIdx.x & 63;
+__device__ __forceinline__ bool flood_fill(const Canvas<FMT>& C, int32_t sx, int32_t sy,
+                                           uint64_t intensity, Frame* stack, int32_t capacity,
+                                           int* parity, BlackStats* bs) {
+  const int w = wave_id(), lane = lane_id();
   Frame top;
-  if (!frame_start<FMT>(C, sx, sy, intensity, &top)) return true;
-  *painted = true;
-  int32_t sp = 1;  // frames below `top` live in stack[0 .. sp-2]
-  while (sp > 0) {
-    while (top.dir < 4 && top.idx >= 2 * top.dist[top.dir]) {
-      top.dir++;
-      top.idx = 0;
-    }
-    if (top.dir >= 4) {
-      sp--;
-      if (sp > 0) top = stack[sp - 1];
-      continue;
-    }
-    const int dx = kDX[top.dir], dy = kDY[top.dir];
-    const int32_t n = 2 * top.dist[top.dir];
-    // the next 512 neighbour checks of the line in one round trip; the first
-    // match (in order) starts the child frame, later ones are re-read after it
-    bool mk[kSlices];
-#pragma unroll
-    for (int k = 0; k < kSlices; k++) {
-      const int32_t c = top.idx + 64 * k + lane;
-      const int32_t d = c >> 1, sub = c & 1;
-      int32_t qx = top.x + (d + 1) * dx, qy = top.y + (d + 1) * dy;
-      if (dx != 0) qy += sub == 0 ? 1 : -1;  // below, then above
-      else qx += sub == 0 ? 1 : -1;           // right, then left
-      mk[k] = (c < n) & C.match_nb(qx, qy);
-    }
-    int kf = -1;
-    unsigned long long M = 0;
-#pragma unroll
-    for (int k = kSlices - 1; k >= 0; k--) {
-      const unsigned long long b = __ballot(mk[k]);
-      if (b) {
-        kf = k;
-        M = b;
-      }
-    }
-    if (kf < 0) {
-      top.idx += 64 * kSlices;
-      continue;
-    }
-    const int first = __ffsll((long long)M) - 1;
-    const int32_t cidx = top.idx + 64 * kf + first;
-    int32_t cx, cy;
-    {
-      const int32_t d = cidx >> 1, sub = cidx & 1;
-      cx = top.x + (d + 1) * dx;
-      cy = top.y + (d + 1) * dy;
-      if (dx != 0) cy += sub == 0 ? 1 : -1;
-      else cx += sub == 0 ? 1 : -1;
-    }
-    top.idx = cidx + 1;
-    if (sp >= capacity) return false;  // stack overflow: flagged by the caller
-    Frame child;
-    if (frame_start<FMT>(C, cx, cy, intensity, &child)) {
-      if (lane == 0) stack[sp - 1] = top;
-      wave_sync();
-      top = child;
+  int32_t sp = 0;  // frames on the stack, `top` included; those below it live in stack[0 .. sp-2]
+  int32_t nx = sx, ny = sy;
+  bool start = true;
+  for (;;) {
+    if (start) {  // a new frame: save the parent, paint and fill the cross
+      if (sp >= capacity) return false;  // stack overflow: flagged by the caller
+      if (sp > 0 && threadIdx.x == 0) stack[sp - 1] = top;
+      frame_start<FMT>(C, nx, ny, intensity, &top, bs);  // its barriers publish the push
       sp++;
+      start = false;
     }
+    const int32_t n = 2 * (top.dist[0] + top.dist[1] + top.dist[2] + top.dist[3]);
+    if (top.cursor >= n) {
+      if (--sp == 0) return true;
+      top = stack[sp - 1];
+      continue;
+    }
+    BSTAT(const uint64_t tc = wall_clock64(); bs->check_trips++;)
+    int32_t qx[kGroup], qy[kGroup];
+    bool m[kGroup];
+#pragma unroll
+    for (int i = 0; i < kGroup; i++) {
+      const int32_t c = top.cursor + 64 * (w * kGroup + i) + lane;
+      check_pos(top, imin(c, n - 1), &qx[i], &qy[i]);
+      if (c >= n) qx[i] = -1;
+    }
+    C.match_group(qx, qy, m);
+    uint64_t M[kGroup];
+#pragma unroll
+    for (int i = 0; i < kGroup; i++) M[i] = __ballot(m[i]);
+    const int32_t f = window_first(M, (*parity)++ & 1);
+    BSTAT(bs->t_check += wall_clock64() - tc;)
+    if (f == INT_MAX) {
+      top.cursor += 64 * kSlices;
+      continue;
+    }
+    const int32_t cidx = top.cursor + f;
+    check_pos(top, cidx, &nx, &ny);
+    top.cursor = cidx + 1;
+    start = true;
   }
-  return true;
 }
 
 template <int FMT>
-__global__ void __launch_bounds__(64) k_black_resolve(PlaneRef img, BlackGeom g,
-                                                      const BlackBar* bars, uint8_t* scratch,
-                                                      int64_t sstride, const int32_t* active,
-                                                      SheetCtl* ctl) {
+__global__ void __launch_bounds__(kThreads) k_black_resolve(PlaneRef img, BlackGeom g,
+                                                            const BlackBar* bars,
+                                                            uint8_t* scratch, int64_t sstride,
+                                                            const int32_t* active,
+                                                            SheetCtl* ctl) {
   const int s = blockIdx.x;
   if (active && !active[s]) return;
-  const int lane = threadIdx.x;
+  const int w = wave_id(), lane = lane_id();
   uint8_t* scr = scratch + s * sstride;
   const uint32_t* hsum = (const uint32_t*)scr;        // W entries
   const uint32_t* vsum = hsum + g.W;                  // H entries
   size_t off = (((size_t)g.W + g.H) * 4 + 255) & ~(size_t)255;
   Frame* stack = (Frame*)(scr + off);
-  Canvas<FMT> C{plane_ptr(img, s), img.P.pitch, g.W, g.H, g.mask_max};
+  uint8_t* const base = plane_ptr(img, s);
+  BlackStats bstat{};
+  BlackStats* bs = &bstat;
+  (void)bs;
+  const Canvas<FMT> C{base, img.P.pitch, g.W, g.H, g.mask_max,
+                      bs};
+  BSTAT(const uint64_t t_all = wall_clock64();)
+  uint64_t* red = tab_red();
+  int parity = 0;
   bool dirty = false;
-  for (int32_t b0 = 0; b0 < g.nbars; b0 += 64) {
-    // darkness of 64 bars on the original image (darkness_rect, blit.c:131-146)
+  for (int32_t b0 = 0; b0 < g.nbars; b0 += kThreads) {
+    // darkness of kThreads bars on the original image (darkness_rect,
+    // blit.c:131-146)
     bool cand = false;
-    const int32_t bi = b0 + lane;
+    const int32_t bi = b0 + (int32_t)threadIdx.x;
     if (bi < g.nbars) {
       const BlackBar bb = bars[bi];
       const Rect c = clip(bb.r, g.W, g.H);
@@ -295,51 +469,103 @@ __global__ void __launch_bounds__(64) k_black_resolve(PlaneRef img, BlackGeom g,
       const uint8_t dark = (uint8_t)(0xFFull - sum / count_pixels(c));
       cand = dark >= g.abs_threshold && !bb.excluded;
     }
-    unsigned long long M = __ballot(cand);
-    while (M) {
-      const int k = __ffsll((long long)M) - 1;
-      M &= M - 1;
-      const BlackBar bb = bars[b0 + k];
-      if (dirty) {  // re-measure on the current image
-        const Rect c = clip(bb.r, g.W, g.H);
-        uint64_t sum = 0;
-        if (c.x0 <= c.x1 && c.y0 <= c.y1) {
-          const int32_t w = c.x1 - c.x0 + 1;
-          const int64_t npx = (int64_t)w * (c.y1 - c.y0 + 1);
-          for (int64_t i = lane; i < npx; i += 64) {
-            const int32_t yy = c.y0 + (int32_t)(i / w), xx = c.x0 + (int32_t)(i % w);
-            sum += dark_of(load_px_row<FMT>(C.base + (int64_t)yy * C.pitch, xx));
-          }
-        }
-        for (int o = 32; o > 0; o >>= 1) sum += __shfl_down(sum, o, 64);
-        sum = __shfl(sum, 0, 64);
-        const uint8_t dark = (uint8_t)(0xFFull - sum / count_pixels(c));
-        if (dark < g.abs_threshold) continue;
-      }
-      // flood fill from every pixel of the bar, in scan order (filters.c:81-86)
-      for (int32_t y = bb.r.y0; y <= bb.r.y1; y++) {
-        for (int32_t x0 = bb.r.x0; x0 <= bb.r.x1; x0 += 64) {
-          int32_t from = 0;
-          for (;;) {
-            const int32_t x = x0 + from + lane;
-            const bool m = (from + lane) < 64 && x <= bb.r.x1 && C.match(x, y);
-            const unsigned long long S = __ballot(m);
-            if (!S) break;
-            const int f = __ffsll((long long)S) - 1;
-            bool painted = false;
-            if (!flood_fill<FMT>(C, x0 + f, y, g.intensity, stack, g.stack_capacity,
-                                 &painted)) {
-              if (lane == 0 && ctl) atomicOr(&ctl[s].status, STATUS_FLOOD_OVERFLOW);
-              return;
+    const unsigned long long cw = __ballot(cand);
+    if (lane == 0) tab_cand()[w] = cw;
+    block_sync();
+#pragma unroll 1
+    for (int v = 0; v < kWaves; v++) {
+      uint64_t Mv = tab_cand()[v];
+      while (Mv) {
+        const int k = __ffsll((long long)Mv) - 1;
+        Mv &= Mv - 1;
+        const BlackBar bb = bars[b0 + v * 64 + k];
+        if (dirty) {  // re-measure on the current image, every thread a share
+          BSTAT(const uint64_t tr = wall_clock64(); bs->remeasures++;)
+          const Rect c = clip(bb.r, g.W, g.H);
+          uint64_t sum = 0;
+          if (c.x0 <= c.x1 && c.y0 <= c.y1) {
+            for (int32_t x0 = c.x0; x0 <= c.x1; x0 += 64) {
+              const int32_t xx = x0 + lane;
+              if (xx > c.x1) continue;
+              for (int32_t y0 = c.y0 + w * 4; y0 <= c.y1; y0 += 4 * kWaves) {
+                uint32_t d[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                  d[r] = dark_of(load_px_row<FMT>(C.base + (int64_t)imin(y0 + r, c.y1) * C.pitch, xx));
+#pragma unroll
+                for (int r = 0; r < 4; r++) sum += y0 + r <= c.y1 ? d[r] : 0u;
+              }
             }
-            dirty |= painted;
-            from = f + 1;
-            if (from >= 64) break;
           }
+          sum = wave_sum(sum);
+          if (lane == 0) red[w] = sum;
+          block_sync();
+          uint64_t tot = 0;
+#pragma unroll
+          for (int v2 = 0; v2 < kWaves; v2++) tot += red[v2];
+          block_sync();
+          const uint8_t dark = (uint8_t)(0xFFull - tot / count_pixels(c));
+          BSTAT(bs->t_remeasure += wall_clock64() - tr;)
+          if (dark < g.abs_threshold) continue;
+        }
+        // flood fill from every pixel of the bar, in scan order
+        // (filters.c:81-86): the bar's pixels row-major, a window at a time
+        const int32_t bw = bb.r.x1 - bb.r.x0 + 1;
+        const int64_t npx = (int64_t)bw * (bb.r.y1 - bb.r.y0 + 1);
+        if (bw <= 0 || npx <= 0) continue;
+        const int32_t q64 = 64 / bw, r64 = 64 % bw;  // one slice = q64 rows + r64 pixels
+        for (int64_t i0 = 0; i0 < npx;) {
+          BSTAT(const uint64_t tb = wall_clock64(); bs->bar_trips++;)
+          const int64_t i = i0 + 64 * (int64_t)(w * kGroup) + lane;
+          int32_t y = bb.r.y0 + (int32_t)(i / bw), x = bb.r.x0 + (int32_t)(i % bw);
+          int32_t qx[kGroup], qy[kGroup];
+          bool m[kGroup];
+#pragma unroll
+          for (int k2 = 0; k2 < kGroup; k2++) {
+            qx[k2] = i + 64 * k2 < npx ? x : -1;
+            qy[k2] = y;
+            x += r64;
+            y += q64;
+            if (x > bb.r.x1) {
+              x -= bw;
+              y++;
+            }
+          }
+          C.match_group(qx, qy, m);
+          uint64_t M[kGroup];
+#pragma unroll
+          for (int k2 = 0; k2 < kGroup; k2++) M[k2] = __ballot(m[k2]);
+          const int32_t f = window_first(M, parity++ & 1);
+          BSTAT(bs->t_bar += wall_clock64() - tb;)
+          if (f == INT_MAX) {
+            i0 += 64 * kSlices;
+            continue;
+          }
+          const int64_t hit = i0 + f;
+          if (!flood_fill<FMT>(C, bb.r.x0 + (int32_t)(hit % bw), bb.r.y0 + (int32_t)(hit / bw),
+                               g.intensity, stack, g.stack_capacity, &parity, bs)) {
+            if (threadIdx.x == 0 && ctl) atomicOr(&ctl[s].status, STATUS_FLOOD_OVERFLOW);
+            return;
+          }
+          dirty = true;
+          i0 = hit + 1;
         }
       }
     }
+    block_sync();  // the candidate table is rewritten by the next chunk
   }
+#ifdef UPHIP_DIAG
+  if ((g.diag & 16) && threadIdx.x == 0 && bstat.frames)
+    printf("uphip black: sheet %d frames %u fill %u (%.1f us) check %u (%.1f us) bar %u (%.1f us) "
+           "remeasure %u (%.1f us) total %.1f us lookups %u "
+           "fillA %.1f (pos %.1f lookup %.1f) B %.1f C %.1f D %.1f us\n",
+           s, bstat.frames, bstat.fill_trips, bstat.t_fill * 0.01, bstat.check_trips,
+           bstat.t_check * 0.01, bstat.bar_trips, bstat.t_bar * 0.01, bstat.remeasures,
+           bstat.t_remeasure * 0.01, (wall_clock64() - t_all) * 0.01, bstat.lookups * 64,
+           bstat.t_fa * 0.01, bstat.t_fa0 * 0.01,
+           bstat.t_fa1 * 0.01, bstat.t_fb * 0.01,
+           bstat.t_fc * 0.01, bstat.t_fd * 0.01);
+#endif
 }
 
 template <int FMT>
@@ -353,8 +579,11 @@ static void launch_black_t(const PlaneRef& img, const BlackGeom& g, const BlackB
   if (g.vregion.x1 >= g.vregion.x0 && g.vregion.y1 >= g.vregion.y0)
     launch_axis_reduce(img, vargs, 1, M_DARKINV_SUM, g.vregion.x1 - g.vregion.x0 + 1, g.H,
                        (uint32_t*)scr + g.W, ss / 4, count, st);
-  if (!(diag_skip() & 1)) hipLaunchKernelGGL(k_black_resolve<FMT>, dim3(count), dim3(64), 0, st, img, g, bars, scr, ss,
-                     active, ctl);
+  BlackGeom gd = g;
+  gd.diag = diag_noise();
+  if (!(diag_skip() & 1))
+    hipLaunchKernelGGL(k_black_resolve<FMT>, dim3(count), dim3(kThreads), 0, st, img, gd,
+                       bars, scr, ss, active, ctl);
 }
 
 __global__ void k_black_prep(uint8_t* scr, int64_t ss, int32_t words, int count) {

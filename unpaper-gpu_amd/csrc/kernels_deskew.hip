@@ -621,9 +621,7 @@ static void launch_rot_t(const PlaneRef& img, const RotGeom& g, const RotTable* 
   const int band_cap =
       imin(kBandCapMax, (int)ceilf((float)imax(max_scan, 1) * tn) + kDepth + 4);
   const size_t band_lds = sizeof(uint16_t) * kSliceRows * (size_t)band_cap;
-  if (band_lds > 64 * 1024)
-    hipFuncSetAttribute((const void*)k_rot_band_g, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)band_lds);
+  allow_dynamic_lds((const void*)k_rot_band_g, band_lds);
   UPH_LAUNCH_DIAG(1, k_rot_band_g, dim3(rot_slices(max_scan), g.nedges, count),
                   dim3(kBandThreads), band_lds, st, img, g, table, masks, mask_active, count,
                   max_scan, R, (int)FMT, band_cap);
@@ -631,9 +629,7 @@ static void launch_rot_t(const PlaneRef& img, const RotGeom& g, const RotTable* 
   UPH_LAUNCH_DIAG(128, k_rot_final, dim3((nlines + 3) / 4), dim3(256), 0, st, g, table, masks,
                   mask_active, mask_index, peaks, count, max_scan, R, band_cap);
   const size_t lds = sizeof(int32_t) * 2 * (size_t)(max_scan > 0 ? max_scan : 1);
-  if (lds > 64 * 1024)
-    hipFuncSetAttribute((const void*)k_rot_line<FMT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)lds);
+  allow_dynamic_lds((const void*)k_rot_line<FMT>, lds);
   UPH_LAUNCH_DIAG(128, k_rot_line<FMT>, dim3(imin(nlines, 1024)), dim3(256), lds, st, img, g,
                   table, masks, mask_active, mask_index, peaks, count, max_scan, R);
 }

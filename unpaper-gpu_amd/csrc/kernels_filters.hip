@@ -1519,12 +1519,7 @@ static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr
   hipLaunchKernelGGL(k_noise_apply<FMT>, dim3(64, count), dim3(256), 0, st, img, g, scr, ss,
                      active, ctl);
   constexpr size_t kResolveLds = 2 * sizeof(uint32_t) * kCompCap;  // 128 KiB
-  static bool lds_set = false;  // per instantiation; the attribute is per function
-  if (!lds_set) {
-    hipFuncSetAttribute((const void*)k_noise_resolve<FMT>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLds);
-    lds_set = true;
-  }
+  allow_dynamic_lds((const void*)k_noise_resolve<FMT>, kResolveLds);
   if (!(diag_skip() & 2)) hipLaunchKernelGGL(k_noise_resolve<FMT>, dim3(count), dim3(kResolveThreads), kResolveLds, st, img, gd, scr, ss, active,
                      ctl, sortbuf, sort_stride);
 }

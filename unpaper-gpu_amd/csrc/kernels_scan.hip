@@ -341,7 +341,7 @@ __global__ void __launch_bounds__(256) k_edge_scan(const EdgeArgs* args, const u
 // extent (a static 64 KB array held a CU's LDS for the whole scan).
 static size_t axis_lds(int32_t max_extent, const void* kernel) {
   const size_t b = sizeof(uint32_t) * (size_t)imax(max_extent, 1);
-  if (b > 64 * 1024) hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b);
+  allow_dynamic_lds(kernel, b);
   return b;
 }
 
