@@ -117,8 +117,8 @@ constexpr int kSlices = kWaves * kGroup;  // 64 slices = 4096 pixels per round t
 static_assert(kSlices == 64, "lane-parallel reads of the per-slice tables assume 64 slices");
 
 // Per-round-trip tables in LDS (the window's results of each wave).
-constexpr int kOffStop = 0;                       // i32[2 * kWaves]: last match, first stop
-constexpr int kOffFirst = kOffStop + kWaves;      // i32[2][kWaves] first matches
+constexpr int kOffStop = 0;                       // i32[2][4][kWaves] fill-trip posts
+constexpr int kOffFirst = kOffStop + 4 * kWaves;  // i32[2][kWaves] first matches
 constexpr int kOffRed = kOffFirst + kWaves;       // u64[kWaves] sums
 constexpr int kOffCand = kOffRed + kWaves;        // u64[kWaves] candidate bars
 constexpr int kReplayWords = kOffCand + kWaves;   // in 8-byte units
@@ -167,21 +167,21 @@ struct Canvas {
   __device__ __forceinline__ bool inside(int32_t x, int32_t y) const {
     return x >= 0 && y >= 0 && x < W && y < H;
   }
-  // kGroup matches of this wave: the loads of all slices are issued before
-  // any is used, so one memory round trip serves the group.  x < 0 means "no
-  // position" (no match).
-  __device__ __forceinline__ void match_group(const int32_t (&x)[kGroup],
-                                              const int32_t (&y)[kGroup],
-                                              bool (&m)[kGroup]) const {
-    uint8_t g[kGroup];
+  // N matches of this wave: the loads of all are issued before any is used,
+  // so one memory round trip serves the group.  x < 0 means "no position"
+  // (no match).
+  template <int N>
+  __device__ __forceinline__ void match_group(const int32_t (&x)[N], const int32_t (&y)[N],
+                                              bool (&m)[N]) const {
+    uint8_t g[N];
 #pragma unroll
-    for (int k = 0; k < kGroup; k++) {
+    for (int k = 0; k < N; k++) {
       const int32_t cy = imin(imax(y[k], 0), H - 1), cx = imin(imax(x[k], 0), W - 1);
       g[k] = gray_of(load_px_row<FMT>(base + (int64_t)cy * pitch, cx));
     }
 #pragma unroll
-    for (int k = 0; k < kGroup; k++) m[k] = inside(x[k], y[k]) && g[k] <= mmax;
-    BSTAT(bs->lookups += kGroup;)
+    for (int k = 0; k < N; k++) m[k] = inside(x[k], y[k]) && g[k] <= mmax;
+    BSTAT(bs->lookups += N;)
   }
   __device__ __forceinline__ void paint(int32_t x, int32_t y) const {
     if (inside(x, y)) store_px_row<FMT>(base + (int64_t)y * pitch, x, Px{255, 255, 255});
@@ -191,28 +191,33 @@ struct Canvas {
 // The four fill_lines (fill.c:16-52) from (px,py); dist[d] = pixels painted.
 // Per line a counter starts at 1, resets to `intensity` on a match and
 // decrements otherwise; the line stops (unpainted) where it reaches 0 or
-// leaves the image.  The four lines touch disjoint pixels (left, up, right,
-// down of the start), so they share each round trip: the window's slices are
-// split evenly over the lines still running, whole waves per line (a line
-// gets 16, 32 or 64 slices, a wave 8).  A round trip is
-//   A: lookups; each wave posts the last match of its slices;
-//   B: each wave, given the last match of the line before its slices (from
-//      the posts of the line's earlier waves), posts its first stop;
-//   C: per line, the first stop posted, or the carry for the next trip;
+// leaves the image: at the first position p that is outside, or does not
+// match and lies `intensity` or more past the last match (the first
+// non-matching position if there was none).  The four lines touch disjoint
+// pixels (left, up, right, down of the start), so they share each round trip:
+// the window's slices are split evenly over the lines still running, whole
+// waves per line (16, 32 or 64 slices a line, 8 a wave).  A round trip is
+//   A: each wave reads its slices and posts their first match F, last match
+//      L, and the first stop I after F (which needs no carry from before);
+//   C: one barrier, then every wave walks each line's posts in order with
+//      the carry (last match so far) to find the line's stop, uniformly;
 //   D: paint up to the stop.
+// The posts alternate between two buffers, so a round trip has one barrier;
+// the paints are published by the barrier after the four lines.
 template <int FMT>
 __device__ __forceinline__ void fill_lines(const Canvas<FMT>& C, int32_t px, int32_t py,
                                            uint64_t intensity, int32_t (&dist)[4],
                                            BlackStats* bs) {
   const int w = wave_id(), lane = lane_id();
-  int32_t* wlast = tab_stop();            // [kWaves] last match of a wave's slices, or -1
-  int32_t* wstop = tab_stop() + kWaves;   // [kWaves] first stop of a wave's slices, or INT_MAX
   BSTAT(const uint64_t t0 = wall_clock64();)
   uint32_t done = 0, has_last = 0;  // per line bits (bool arrays indexed by a
                                     // run-time line would live in scratch)
   int32_t last[4] = {0, 0, 0, 0};   // positions along a line fit 31 bits
   int32_t pos0[4] = {1, 1, 1, 1};
+  // first position outside the image, per line
+  const int32_t edge[4] = {px + 1, py + 1, C.W - px, C.H - py};
   const uint64_t upto_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+  int parity = 0;
   for (;;) {
     uint32_t actp = 0;  // running lines, a nibble each
     int nact = 0;
@@ -227,6 +232,8 @@ __device__ __forceinline__ void fill_lines(const Canvas<FMT>& C, int32_t px, int
     const bool valid = a < nact;
     const int d = (int)((actp >> (4 * (valid ? a : 0))) & 15);
     const int32_t base0 = pick4(pos0, d) + 64 * k0;  // position of lane 0, slice 0
+    int32_t* post = tab_stop() + parity * 3 * kWaves;  // F | L | I, per wave
+    parity ^= 1;
     BSTAT(uint64_t tp = wall_clock64();)
     // A
     int32_t qx[kGroup], qy[kGroup];
@@ -240,72 +247,78 @@ __device__ __forceinline__ void fill_lines(const Canvas<FMT>& C, int32_t px, int
     BSTAT(bs->t_fa0 += wall_clock64() - tp;)
     C.match_group(qx, qy, m);
     BSTAT(bs->t_fa1 += wall_clock64() - tp;)
-    uint64_t M[kGroup];
-    int32_t mylast = -1;
-#pragma unroll
-    for (int i = 0; i < kGroup; i++) {
-      M[i] = __ballot(m[i]);
-      if (M[i]) mylast = base0 + 64 * i + (63 - __clzll((long long)M[i]));
-    }
-    if (lane == 0) wlast[w] = valid ? mylast : -1;
-    block_sync();
-    BSTAT(bs->t_fa += wall_clock64() - tp; tp = wall_clock64();)
-    // B: carry from the line's earlier waves, then slice by slice
-    if (valid) {
-      const int wa0 = a * wpl;  // the line's first wave
-      const int32_t lv = (lane >= wa0 && lane < w) ? wlast[lane] : -1;
-      const unsigned long long nz = __ballot(lv >= 0);
-      bool hl = (has_last >> d) & 1;
-      int32_t lm = pick4(last, d);
-      if (nz) {
-        hl = true;
-        lm = __shfl(lv, 63 - __clzll((long long)nz), 64);
-      }
-      int32_t first_stop = INT_MAX;
+    int32_t F = -1, L = -1, I = INT_MAX;
+    {
+      bool hl = false;  // a match earlier in this wave's slices
+      int32_t lm = 0;
 #pragma unroll
       for (int i = 0; i < kGroup; i++) {
-        if (first_stop != INT_MAX) break;
+        const unsigned long long Mi = __ballot(m[i]);
         const int32_t p0 = base0 + 64 * i, j = p0 + lane;
-        const unsigned long long upto = M[i] & upto_mask;
-        bool lhl = hl;
-        int32_t llm = lm;
-        if (upto) {
-          lhl = true;
-          llm = p0 + (63 - __clzll((long long)upto));
+        if (I == INT_MAX) {
+          const unsigned long long upto = Mi & upto_mask;
+          bool lhl = hl;
+          int32_t llm = lm;
+          if (upto) {
+            lhl = true;
+            llm = p0 + (63 - __clzll((long long)upto));
+          }
+          // after the wave's first match only: before it the carry decides
+          const unsigned long long S = __ballot(lhl && (uint64_t)(uint32_t)(j - llm) >= intensity);
+          if (S) I = p0 + __ffsll((long long)S) - 1;
         }
-        bool st = !C.inside(qx[i], qy[i]);
-        if (lhl) st |= (uint64_t)(uint32_t)(j - llm) >= intensity;
-        else st |= j >= 1;
-        const unsigned long long S = __ballot(st);
-        if (S) first_stop = p0 + __ffsll((long long)S) - 1;
-        if (M[i]) {
+        if (Mi) {
+          if (F < 0) F = p0 + __ffsll((long long)Mi) - 1;
+          L = p0 + (63 - __clzll((long long)Mi));
           hl = true;
-          lm = p0 + (63 - __clzll((long long)M[i]));
+          lm = L;
         }
       }
-      if (lane == 0) wstop[w] = first_stop;
+    }
+    if (lane == 0) {
+      post[w] = valid ? F : -1;
+      post[kWaves + w] = valid ? L : -1;
+      post[2 * kWaves + w] = valid ? I : INT_MAX;
     }
     block_sync();
-    BSTAT(bs->t_fb += wall_clock64() - tp; tp = wall_clock64();)
-    // C (uniform): per line the first posted stop, else the carry
-    const int32_t vs = lane < kWaves ? wstop[lane] : INT_MAX;
-    const int32_t vl = lane < kWaves ? wlast[lane] : -1;
-    const unsigned long long stops = __ballot(vs != INT_MAX), lasts = __ballot(vl >= 0);
+    BSTAT(bs->t_fa += wall_clock64() - tp; tp = wall_clock64();)
+    // C (uniform): per line, lanes stand for its waves; each lane takes the
+    // carry from the line's earlier waves (or the previous round trip) and
+    // finds its wave's stop; the first lane with one has the line's stop
+    const int32_t vF = lane < kWaves ? post[lane] : -1;
+    const int32_t vL = lane < kWaves ? post[kWaves + lane] : -1;
+    const int32_t vI = lane < kWaves ? post[2 * kWaves + lane] : INT_MAX;
+    const unsigned long long withL = __ballot(vL >= 0);
     int32_t sd[4] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX};
 #pragma unroll
     for (int aa = 0; aa < 4; aa++) {
       if (aa >= nact) break;
       const int dd = (int)((actp >> (4 * aa)) & 15);
-      const unsigned long long range = ((1ull << wpl) - 1) << (aa * wpl);
-      if (stops & range) {
-        const int32_t s = __shfl(vs, __ffsll((long long)(stops & range)) - 1, 64);
-        set4(sd, dd, s);
+      const int lo = aa * wpl;
+      const unsigned long long range = ((1ull << wpl) - 1) << lo;
+      const bool inr = (range >> lane) & 1;
+      const unsigned long long before = withL & range & ((1ull << lane) - 1);
+      const int src = before ? 63 - __clzll((long long)before) : lane;
+      const int32_t lmv = __shfl(vL, src, 64);
+      const bool has = before ? true : ((has_last >> dd) & 1);
+      const int32_t lm = before ? lmv : pick4(last, dd);
+      const int32_t Pv = pick4(pos0, dd) + 64 * kGroup * (lane - lo);
+      const int32_t end = vF >= 0 ? vF : Pv + 64 * kGroup;  // no match in [Pv, end)
+      const int32_t cand =
+          has ? imax(Pv, (int32_t)imin((int64_t)lm + (int64_t)intensity, (int64_t)INT_MAX)) : Pv;
+      const int32_t sv = cand < end ? cand : vI;
+      const unsigned long long stops = __ballot(inr && sv != INT_MAX);
+      int32_t stop = stops ? __shfl(sv, __ffsll((long long)stops) - 1, 64) : INT_MAX;
+      stop = imin(stop, pick4(edge, dd));
+      if (stop < pick4(pos0, dd) + 64 * spd) {
+        set4(sd, dd, stop);
         done |= 1u << dd;
-        set4(dist, dd, s - 1);
+        set4(dist, dd, stop - 1);
       } else {
-        if (lasts & range) {
+        const unsigned long long mine = withL & range;
+        if (mine) {
           has_last |= 1u << dd;
-          set4(last, dd, __shfl(vl, 63 - __clzll((long long)(lasts & range)), 64));
+          set4(last, dd, __shfl(vL, 63 - __clzll((long long)mine), 64));
         }
         set4(pos0, dd, pick4(pos0, dd) + 64 * spd);
       }
@@ -314,16 +327,13 @@ __device__ __forceinline__ void fill_lines(const Canvas<FMT>& C, int32_t px, int
     // D
     if (valid) {
       const int32_t lim = pick4(sd, d);
-      uint32_t on = 0;
-#pragma unroll
-      for (int i = 0; i < kGroup; i++) on |= (uint32_t)(base0 + 64 * i + lane < lim) << i;
 #pragma unroll
       for (int i = 0; i < kGroup; i++)
-        if ((on >> i) & 1) C.paint(qx[i], qy[i]);
+        if (base0 + 64 * i + lane < lim) C.paint(qx[i], qy[i]);
     }
-    block_sync();
     BSTAT(bs->t_fd += wall_clock64() - tp; bs->fill_trips++;)
   }
+  block_sync();  // the lines' paints, before any check reads them
   BSTAT(bs->t_fill += wall_clock64() - t0;)
 }
 
@@ -360,13 +370,22 @@ __device__ __forceinline__ void check_pos(const Frame& f, int32_t c, int32_t* qx
 
 // First match of a window whose slices were looked up by every wave: each
 // wave posts the index of its first matching position (or INT_MAX) into the
-// buffer of this round trip's parity, then all read the minimum.
-__device__ __forceinline__ int32_t window_first(const uint64_t (&M)[kGroup], int parity) {
+// buffer of this round trip's parity, then all read the minimum.  M[i] is
+// the ballot of slice i; with pairs (every lane two consecutive positions),
+// M0[i] says which lanes matched their first one.
+template <bool kPairs>
+__device__ __forceinline__ int32_t window_first(const uint64_t (&M)[kGroup],
+                                                const uint64_t (&M0)[kGroup], int parity) {
   const int w = wave_id(), lane = lane_id();
   int32_t lf = INT_MAX;
 #pragma unroll
-  for (int i = kGroup - 1; i >= 0; i--)
-    if (M[i]) lf = 64 * (w * kGroup + i) + __ffsll((long long)M[i]) - 1;
+  for (int i = kGroup - 1; i >= 0; i--) {
+    if (M[i]) {
+      const int L = __ffsll((long long)M[i]) - 1;
+      const int32_t u = 64 * (w * kGroup + i) + L;
+      lf = kPairs ? 2 * u + (((M0[i] >> L) & 1) ? 0 : 1) : u;
+    }
+  }
   int32_t* first = tab_first() + parity * kWaves;
   if (lane == 0) first[w] = lf;
   block_sync();
@@ -414,7 +433,7 @@ __device__ __forceinline__ bool flood_fill(const Canvas<FMT>& C, int32_t sx, int
     uint64_t M[kGroup];
 #pragma unroll
     for (int i = 0; i < kGroup; i++) M[i] = __ballot(m[i]);
-    const int32_t f = window_first(M, (*parity)++ & 1);
+    const int32_t f = window_first<false>(M, M, (*parity)++ & 1);
     BSTAT(bs->t_check += wall_clock64() - tc;)
     if (f == INT_MAX) {
       top.cursor += 64 * kSlices;
@@ -535,7 +554,7 @@ __global__ void __launch_bounds__(kThreads) k_black_resolve(PlaneRef img, BlackG
           uint64_t M[kGroup];
 #pragma unroll
           for (int k2 = 0; k2 < kGroup; k2++) M[k2] = __ballot(m[k2]);
-          const int32_t f = window_first(M, parity++ & 1);
+          const int32_t f = window_first<false>(M, M, parity++ & 1);
           BSTAT(bs->t_bar += wall_clock64() - tb;)
           if (f == INT_MAX) {
             i0 += 64 * kSlices;
