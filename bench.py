@@ -102,6 +102,8 @@ def parse():
     ap.add_argument("--no-latency", action="store_true", help="skip the C2 single-page latency")
     ap.add_argument("--host-batch", type=int, default=32, help="sheets per batch, host-fed runs")
     ap.add_argument("--host-streams", type=int, default=8, help="batches per device, host-fed")
+    ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu.json"),
+                    help="per-kernel VALU instructions per sheet (profiles/clock_table.py)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC HBM bytes per launch / per page from rocprofv3 --pmc passes")
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
@@ -222,6 +224,20 @@ def probe_kernel(runner, shard, n0, stage, count):
         b.wait()
         out.append(sum(ms for name, ms in b.stage_times() if name == stage))
     return out
+
+
+def valu_frac_of(path, kernel, units, avg_ms):
+    """VALU-issue fraction of one launch of `units` sheets lasting avg_ms:
+    committed VALU instructions per sheet x 4 cycles / (1024 SIMDs x clock x
+    time), the clock being the one measured in the same PMC run."""
+    try:
+        with open(path) as f:
+            k = json.load(f)["kernels"][kernel]
+    except (OSError, ValueError, KeyError):
+        return None
+    if avg_ms <= 0:
+        return None
+    return round(k["valu_insts_per_sheet"] * units * 4 / (1024 * k["clock_ghz"] * 1e9 * avg_ms * 1e-3), 4)
 
 
 def traffic_of(path, key, units):
@@ -535,6 +551,7 @@ def main():
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": ROOFLINE_KERNEL["c3"],
+            "valu_issue_frac": valu_frac_of(args.valu, ROOFLINE_KERNEL["c3"], units, avg_ms),
             "alg_bytes_per_launch": int(alg), "avg_launch_ms": round(avg_ms, 3),
             "launch_ms_from": ("%d isolated probe launches of %d sheets" % (len(probe), bsz)
                                if probe else "timed region"),

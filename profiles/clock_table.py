@@ -1,7 +1,13 @@
 #!/usr/bin/env python3
 """Per-kernel effective clock (GRBM_GUI_ACTIVE / duration) and VALU issue
 fraction (SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x active cycles)) from a
-rocprofv3 --kernel-trace --pmc run (tools/pmc_clock.sh)."""
+rocprofv3 --kernel-trace --pmc run (tools/pmc_clock.sh).
+
+usage: clock_table.py <run dir> [sheets-per-launch out.json]
+With the last two arguments it also writes per-kernel VALU instructions per
+sheet and the effective clock, which bench.py reads (--valu) to report the
+roofline kernel's VALU-issue fraction next to its HBM fraction."""
+import json
 import collections
 import csv
 import glob
@@ -20,6 +26,15 @@ dur = collections.defaultdict(float)
 if kt:
     for r in csv.DictReader(open(kt[0])):
         dur[r["Kernel_Name"][:56]] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+doc = {"source": "rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_WAVES "
+              "SQ_INSTS_SALU SQ_BUSY_CYCLES (tools/pmc_clock.sh)",
+       "formula": "VALU issue fraction = SQ_INSTS_VALU x 4 cycles (wave64 on a 16-lane SIMD) / "
+                  "(1024 SIMDs x clock x kernel time)",
+       "kernels": {}}
+launches = collections.Counter()
+if kt:
+    for r in csv.DictReader(open(kt[0])):
+        launches[r["Kernel_Name"][:56]] += 1
 print("%-56s %9s %9s %8s %8s" % ("kernel", "dur_ms", "GHz", "VALU%", "VALU/wave"))
 for k, v in sorted(agg.items(), key=lambda kv: -dur.get(kv[0], 0)):
     t = dur.get(k, 0.0)
@@ -30,3 +45,11 @@ for k, v in sorted(agg.items(), key=lambda kv: -dur.get(kv[0], 0)):
     frac = valu * 4 / (1024 * gui) if gui > 0 else 0.0
     waves = v.get("SQ_WAVES", 0.0)
     print("%-56s %9.3f %9.3f %8.1f %8.0f" % (k, t * 1e3, ghz, 100 * frac, valu / waves if waves else 0))
+    n = launches.get(k, 0)
+    if len(sys.argv) > 3 and n:
+        doc["kernels"][k.split("(")[0].split("::")[-1].split("<")[0] + ("<" + k.split("<")[1].split(">")[0] + ">" if "<" in k else "")] = {
+            "launches": n, "ms_per_launch": round(t * 1e3 / n, 4), "clock_ghz": round(ghz, 3),
+            "valu_insts_per_sheet": int(valu / n / int(sys.argv[2])), "valu_issue_frac": round(frac, 4)}
+if len(sys.argv) > 3:
+    with open(sys.argv[3], "w") as f:
+        json.dump(doc, f, indent=1)
