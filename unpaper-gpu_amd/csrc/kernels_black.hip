@@ -117,7 +117,7 @@ constexpr int kSlices = kWaves * kGroup;  // 64 slices = 4096 pixels per round t
 static_assert(kSlices == 64, "lane-parallel reads of the per-slice tables assume 64 slices");
 
 // Per-round-trip tables in LDS (the window's results of each wave).
-constexpr int kOffStop = 0;                       // i32[2][4][kWaves] fill-trip posts
+constexpr int kOffStop = 0;                       // i32[2][3][kWaves] fill-trip posts + 12 more
 constexpr int kOffFirst = kOffStop + 4 * kWaves;  // i32[2][kWaves] first matches
 constexpr int kOffRed = kOffFirst + kWaves;       // u64[kWaves] sums
 constexpr int kOffCand = kOffRed + kWaves;        // u64[kWaves] candidate bars
@@ -217,6 +217,76 @@ __device__ __forceinline__ void fill_lines(const Canvas<FMT>& C, int32_t px, int
   // first position outside the image, per line
   const int32_t edge[4] = {px + 1, py + 1, C.W - px, C.H - py};
   const uint64_t upto_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+  // First round trip by wave 0 alone: the first 128 positions of each line
+  // (two slices a line, one wave's group).  Most lines of most frames end
+  // there, and a round trip with no cross-wave step is a third of the cost.
+  {
+    int32_t* lpost = tab_stop() + 6 * kWaves;  // [4] stop | [4] has_last | [4] last
+    if (w == 0) {
+      int32_t qx[kGroup], qy[kGroup];
+      bool m[kGroup];
+#pragma unroll
+      for (int i = 0; i < kGroup; i++) {
+        const int dd = i >> 1;
+        const int32_t j = 1 + 64 * (i & 1) + lane;
+        qx[i] = dd == 0 ? px - j : dd == 2 ? px + j : px;
+        qy[i] = dd == 1 ? py - j : dd == 3 ? py + j : py;
+      }
+      C.match_group(qx, qy, m);
+#pragma unroll
+      for (int dd = 0; dd < 4; dd++) {
+        bool hl = false;
+        int32_t lm = 0, stop = INT_MAX;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+          const int i = 2 * dd + k;
+          const unsigned long long Mi = __ballot(m[i]);
+          if (stop == INT_MAX) {
+            const int32_t p0 = 1 + 64 * k, j = p0 + lane;
+            const unsigned long long upto = Mi & upto_mask;
+            bool lhl = hl;
+            int32_t llm = lm;
+            if (upto) {
+              lhl = true;
+              llm = p0 + (63 - __clzll((long long)upto));
+            }
+            bool st = !C.inside(qx[i], qy[i]);
+            if (lhl) st |= (uint64_t)(uint32_t)(j - llm) >= intensity;
+            else st |= j >= 1;
+            const unsigned long long S = __ballot(st);
+            if (S) stop = p0 + __ffsll((long long)S) - 1;
+            if (Mi) {
+              hl = true;
+              lm = p0 + (63 - __clzll((long long)Mi));
+            }
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+          if (1 + 64 * k + lane < stop) C.paint(qx[2 * dd + k], qy[2 * dd + k]);
+        if (lane == 0) {
+          lpost[dd] = stop;
+          lpost[4 + dd] = hl;
+          lpost[8 + dd] = lm;
+        }
+      }
+    }
+    block_sync();
+    const int32_t v = lane < 12 ? lpost[lane] : 0;
+#pragma unroll
+    for (int dd = 0; dd < 4; dd++) {
+      const int32_t stop = __builtin_amdgcn_readlane(v, dd);
+      if (stop != INT_MAX) {
+        done |= 1u << dd;
+        set4(dist, dd, stop - 1);
+      } else {
+        if (__builtin_amdgcn_readlane(v, 4 + dd)) has_last |= 1u << dd;
+        set4(last, dd, __builtin_amdgcn_readlane(v, 8 + dd));
+        set4(pos0, dd, 129);
+      }
+    }
+    BSTAT(bs->fill_trips++;)
+  }
   int parity = 0;
   for (;;) {
     uint32_t actp = 0;  // running lines, a nibble each
