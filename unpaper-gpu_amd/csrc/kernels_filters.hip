@@ -135,8 +135,11 @@ __global__ void __launch_bounds__(256) k_gray_cells_g(PlaneRef img, GrayGeom g, 
   uint16_t* cdark = cols16;
   uint16_t* clight = cols16 + ((g.W + 3) & ~3);
   const int32_t nd = (g.W + 3) >> 2;
+  // the four columns of a dword accumulate as 16-bit lanes of two words
+  // (bytes 0/2 and 1/3); dark bits come from bit 8 of byte + 256 - (thr+1)
+  const uint32_t kadd = (256u - ((uint32_t)g.black_thr + 1u)) * 0x00010001u;
   for (int32_t d = threadIdx.x; d < nd; d += 256) {
-    uint32_t dk[4] = {0, 0, 0, 0}, lt[4] = {0, 0, 0, 0};
+    uint32_t l02 = 0, l13 = 0, d02 = 0, d13 = 0;
     for (int32_t y = y0; y < y1; y += 8) {
       uint32_t v[8];
 #pragma unroll
@@ -145,20 +148,22 @@ __global__ void __launch_bounds__(256) k_gray_cells_g(PlaneRef img, GrayGeom g, 
                                                   4 * d);
 #pragma unroll
       for (int k = 0; k < 8; k++) {
-        const uint32_t keep = y + k < y1 ? 1u : 0u;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const uint32_t px = (v[k] >> (8 * j)) & 0xFF;
-          dk[j] += keep & (px <= g.black_thr ? 1u : 0u);
-          lt[j] += keep * px;
-        }
+        if (y + k >= y1) continue;
+        const uint32_t lo = v[k] & 0x00FF00FFu, hi = (v[k] >> 8) & 0x00FF00FFu;
+        l02 += lo;
+        l13 += hi;
+        d02 += 0x00010001u - (((lo + kadd) >> 8) & 0x00010001u);
+        d13 += 0x00010001u - (((hi + kadd) >> 8) & 0x00010001u);
       }
     }
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      cdark[4 * d + j] = (uint16_t)dk[j];
-      clight[4 * d + j] = (uint16_t)lt[j];
-    }
+    cdark[4 * d + 0] = (uint16_t)d02;
+    cdark[4 * d + 1] = (uint16_t)d13;
+    cdark[4 * d + 2] = (uint16_t)(d02 >> 16);
+    cdark[4 * d + 3] = (uint16_t)(d13 >> 16);
+    clight[4 * d + 0] = (uint16_t)l02;
+    clight[4 * d + 1] = (uint16_t)l13;
+    clight[4 * d + 2] = (uint16_t)(l02 >> 16);
+    clight[4 * d + 3] = (uint16_t)(l13 >> 16);
   }
   __syncthreads();
   for (int32_t cx = threadIdx.x; cx < g.ncx; cx += 256) {

@@ -75,12 +75,6 @@ __global__ void __launch_bounds__(kRedThreads) k_rowsum(PlaneRef ref, const Axis
   }
 }
 
-// Gray planes: the measure of one byte (gray = lightness = darkness-inverse).
-template <int MEAS>
-__device__ __forceinline__ uint32_t measure_g(uint32_t v, uint8_t thr) {
-  return MEAS == M_DARK_COUNT ? (v <= thr ? 1u : 0u) : v;
-}
-
 // axis 0 on a gray plane: a lane owns 4 consecutive columns (one aligned
 // dword per row; rows start 256-byte aligned, so it lies in the row's pitch),
 // the 4 waves of a block take quarters of the block's rows (8 loads in flight
@@ -102,7 +96,12 @@ __global__ void __launch_bounds__(256) k_colsum_g(PlaneRef ref, const AxisArgs* 
   const bool col_ok = vx0 <= r.x1;
   const uint8_t* base = plane_ptr(ref, s) + (col_ok ? vx0 : (r.x0 & ~3));
   const int64_t pitch = ref.P.pitch;
-  uint32_t acc[4] = {0, 0, 0, 0};
+  // the four columns accumulate as 16-bit lanes of two words (bytes 0/2 and
+  // 1/3): a wave sums at most rows_per_block / 4 = 64 rows of <= 255, so no
+  // lane overflows; two masks and two adds per dword instead of four of each
+  static_assert(256 / 4 * 255 < 65536, "16-bit column lanes");
+  const uint32_t kadd = (256u - ((uint32_t)a.thr + 1u)) * 0x00010001u;
+  uint32_t a02 = 0, a13 = 0;
   for (int32_t y = y0; y <= y1; y += 8) {
     uint32_t v[8];
 #pragma unroll
@@ -110,11 +109,18 @@ __global__ void __launch_bounds__(256) k_colsum_g(PlaneRef ref, const AxisArgs* 
       v[k] = *reinterpret_cast<const uint32_t*>(base + (int64_t)imin(y + k, y1) * pitch);
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-      const uint32_t keep = (y + k <= y1) ? 1u : 0u;
-#pragma unroll
-      for (int j = 0; j < 4; j++) acc[j] += keep * measure_g<MEAS>((v[k] >> (8 * j)) & 0xFF, a.thr);
+      uint32_t lo = v[k] & 0x00FF00FFu, hi = (v[k] >> 8) & 0x00FF00FFu;
+      if (MEAS == M_DARK_COUNT) {  // byte <= thr: bit 8 of byte + 256 - (thr+1) clear
+        lo = 0x00010001u - (((lo + kadd) >> 8) & 0x00010001u);
+        hi = 0x00010001u - (((hi + kadd) >> 8) & 0x00010001u);
+      }
+      if (y + k <= y1) {
+        a02 += lo;
+        a13 += hi;
+      }
     }
   }
+  const uint32_t acc[4] = {a02 & 0xFFFFu, a13 & 0xFFFFu, a02 >> 16, a13 >> 16};
   __shared__ uint32_t red[4][64 * 4];
 #pragma unroll
   for (int j = 0; j < 4; j++) red[w][lane * 4 + j] = acc[j];
@@ -143,6 +149,17 @@ __device__ __forceinline__ uint32_t measure_g4(uint32_t x, uint32_t keep, uint32
     return acc + __popc(lt & kp);
   }
   return __builtin_amdgcn_sad_u8(x & keep, 0u, acc);
+}
+
+// a whole dword inside the region (no byte masks)
+template <int MEAS>
+__device__ __forceinline__ uint32_t measure_g4_full(uint32_t x, uint32_t kadd, uint32_t acc) {
+  if (MEAS == M_DARK_COUNT) {  // 4 - (bytes >= thr+1)
+    const uint32_t lo = ((x & 0x00FF00FFu) + kadd) & 0x01000100u;
+    const uint32_t hi = (((x >> 8) & 0x00FF00FFu) + kadd) & 0x01000100u;
+    return acc + 4u - __popc(lo | (hi << 1));
+  }
+  return __builtin_amdgcn_sad_u8(x, 0u, acc);
 }
 
 template <int MEAS>
@@ -176,14 +193,15 @@ __global__ void __launch_bounds__(256) k_rowsum_g(PlaneRef ref, const AxisArgs* 
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const int32_t x = c + 4 * j;
-        uint32_t keep = 0xFFFFFFFFu;
-        if (x < r.x0 || x + 3 > r.x1) {
-          keep = 0;
+        if (x >= r.x0 && x + 3 <= r.x1) {
+          acc = measure_g4_full<MEAS>(wd[j], kadd, acc);
+        } else {
+          uint32_t keep = 0;
 #pragma unroll
           for (int q = 0; q < 4; q++)
             if (x + q >= r.x0 && x + q <= r.x1) keep |= 0xFFu << (8 * q);
+          acc = measure_g4<MEAS>(wd[j], keep, kadd, acc);
         }
-        acc = measure_g4<MEAS>(wd[j], keep, kadd, acc);
       }
     }
   }
@@ -198,7 +216,7 @@ static void launch_axis_t(const PlaneRef& ref, const AxisArgs* args, int axis, i
   if (span_x <= 0 || span_y <= 0) return;
   if (FMT == F_GRAY8) {
     if (axis == 0) {
-      const int rpb = 256;
+      const int rpb = 256;  // k_colsum_g's 16-bit column lanes assume <= 256
       dim3 grid((span_x + 3 + 255) / 256, (span_y + rpb - 1) / rpb, count);
       hipLaunchKernelGGL((k_colsum_g<MEAS>), grid, dim3(256), 0, st, ref, args, out, out_stride,
                          rpb);
