@@ -121,7 +121,8 @@ constexpr int kOffStop = 0;                       // i32[2][3][kWaves] fill-trip
 constexpr int kOffFirst = kOffStop + 4 * kWaves;  // i32[2][kWaves] first matches
 constexpr int kOffRed = kOffFirst + kWaves;       // u64[kWaves] sums
 constexpr int kOffCand = kOffRed + kWaves;        // u64[kWaves] candidate bars
-constexpr int kReplayWords = kOffCand + kWaves;   // in 8-byte units
+constexpr int kOffMail = kOffCand + kWaves;       // i32[16] driver -> helper commands
+constexpr int kReplayWords = kOffMail + 8;        // in 8-byte units
 
 __device__ __forceinline__ uint64_t* lds64() {
   __shared__ uint64_t black_tables[kReplayWords];
@@ -131,6 +132,7 @@ __device__ __forceinline__ int32_t* tab_stop() { return (int32_t*)(lds64() + kOf
 __device__ __forceinline__ int32_t* tab_first() { return (int32_t*)(lds64() + kOffFirst); }
 __device__ __forceinline__ uint64_t* tab_red() { return lds64() + kOffRed; }
 __device__ __forceinline__ uint64_t* tab_cand() { return lds64() + kOffCand; }
+__device__ __forceinline__ int32_t* mailbox() { return (int32_t*)(lds64() + kOffMail); }
 
 // scalar (readfirstlane), so everything derived from it stays in SGPRs
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
@@ -204,74 +206,104 @@ struct Canvas {
 //   D: paint up to the stop.
 // The posts alternate between two buffers, so a round trip has one barrier;
 // the paints are published by the barrier after the four lines.
+// The four fill_lines (fill.c:16-52) from (px,py); dist[d] = pixels painted.
+// Per line a counter starts at 1, resets to `intensity` on a match and
+// decrements otherwise; the line stops (unpainted) where it reaches 0 or
+// leaves the image: at the first position p that is outside, or does not
+// match and lies `intensity` or more past the last match (the first
+// non-matching position if there was none).  The four lines touch disjoint
+// pixels (left, up, right, down of the start), so they share each round trip.
+//
+// fill_local: the first round trip, by the driving wave alone: the first 128
+// positions of each line (two slices a line, one wave's group).  Most lines
+// of most frames end there.  The lines' state goes to `lpost`; returns
+// whether a line runs on.
 template <int FMT>
-__device__ __forceinline__ void fill_lines(const Canvas<FMT>& C, int32_t px, int32_t py,
+__device__ __forceinline__ bool fill_local(const Canvas<FMT>& C, int32_t px, int32_t py,
                                            uint64_t intensity, int32_t (&dist)[4],
                                            BlackStats* bs) {
+  const int lane = lane_id();
+  const uint64_t upto_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+  int32_t* lpost = tab_stop() + 6 * kWaves;  // [4] stop | [4] has_last | [4] last
+  bool more = false;
+  int32_t qx[kGroup], qy[kGroup];
+  bool m[kGroup];
+#pragma unroll
+  for (int i = 0; i < kGroup; i++) {
+    const int dd = i >> 1;
+    const int32_t j = 1 + 64 * (i & 1) + lane;
+    qx[i] = dd == 0 ? px - j : dd == 2 ? px + j : px;
+    qy[i] = dd == 1 ? py - j : dd == 3 ? py + j : py;
+  }
+  C.match_group(qx, qy, m);
+#pragma unroll
+  for (int dd = 0; dd < 4; dd++) {
+    bool hl = false;
+    int32_t lm = 0, stop = INT_MAX;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int i = 2 * dd + k;
+      const unsigned long long Mi = __ballot(m[i]);
+      if (stop == INT_MAX) {
+        const int32_t p0 = 1 + 64 * k, j = p0 + lane;
+        const unsigned long long upto = Mi & upto_mask;
+        bool lhl = hl;
+        int32_t llm = lm;
+        if (upto) {
+          lhl = true;
+          llm = p0 + (63 - __clzll((long long)upto));
+        }
+        bool st = !C.inside(qx[i], qy[i]);
+        if (lhl) st |= (uint64_t)(uint32_t)(j - llm) >= intensity;
+        else st |= j >= 1;
+        const unsigned long long S = __ballot(st);
+        if (S) stop = p0 + __ffsll((long long)S) - 1;
+        if (Mi) {
+          hl = true;
+          lm = p0 + (63 - __clzll((long long)Mi));
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+      if (1 + 64 * k + lane < stop) C.paint(qx[2 * dd + k], qy[2 * dd + k]);
+    if (lane == 0) {
+      lpost[dd] = stop;
+      lpost[4 + dd] = hl;
+      lpost[8 + dd] = lm;
+    }
+    if (stop != INT_MAX) set4(dist, dd, stop - 1);
+    else more = true;
+  }
+  BSTAT(bs->fill_trips++;)
+  return more;
+}
+
+// fill_coop: the rest of the lines, by the whole workgroup, from the state in
+// `lpost`: the window's slices are split evenly over the lines still running,
+// whole waves per line (16, 32 or 64 slices a line, 8 a wave).  A round trip is
+//   A: each wave reads its slices and posts their first match F, last match
+//      L, and the first stop I after F (which needs no carry from before);
+//   C: one barrier, then every wave walks each line's posts in order with
+//      the carry (last match so far) to find the line's stop, uniformly;
+//   D: paint up to the stop.
+// The posts alternate between two buffers, so a round trip has one barrier;
+// the paints are published by the barrier after the four lines.
+template <int FMT>
+__device__ __forceinline__ void fill_coop(const Canvas<FMT>& C, int32_t px, int32_t py,
+                                          uint64_t intensity, int32_t (&dist)[4],
+                                          BlackStats* bs) {
   const int w = wave_id(), lane = lane_id();
   BSTAT(const uint64_t t0 = wall_clock64();)
   uint32_t done = 0, has_last = 0;  // per line bits (bool arrays indexed by a
                                     // run-time line would live in scratch)
   int32_t last[4] = {0, 0, 0, 0};   // positions along a line fit 31 bits
-  int32_t pos0[4] = {1, 1, 1, 1};
+  int32_t pos0[4] = {129, 129, 129, 129};
   // first position outside the image, per line
   const int32_t edge[4] = {px + 1, py + 1, C.W - px, C.H - py};
   const uint64_t upto_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-  // First round trip by wave 0 alone: the first 128 positions of each line
-  // (two slices a line, one wave's group).  Most lines of most frames end
-  // there, and a round trip with no cross-wave step is a third of the cost.
   {
-    int32_t* lpost = tab_stop() + 6 * kWaves;  // [4] stop | [4] has_last | [4] last
-    if (w == 0) {
-      int32_t qx[kGroup], qy[kGroup];
-      bool m[kGroup];
-#pragma unroll
-      for (int i = 0; i < kGroup; i++) {
-        const int dd = i >> 1;
-        const int32_t j = 1 + 64 * (i & 1) + lane;
-        qx[i] = dd == 0 ? px - j : dd == 2 ? px + j : px;
-        qy[i] = dd == 1 ? py - j : dd == 3 ? py + j : py;
-      }
-      C.match_group(qx, qy, m);
-#pragma unroll
-      for (int dd = 0; dd < 4; dd++) {
-        bool hl = false;
-        int32_t lm = 0, stop = INT_MAX;
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-          const int i = 2 * dd + k;
-          const unsigned long long Mi = __ballot(m[i]);
-          if (stop == INT_MAX) {
-            const int32_t p0 = 1 + 64 * k, j = p0 + lane;
-            const unsigned long long upto = Mi & upto_mask;
-            bool lhl = hl;
-            int32_t llm = lm;
-            if (upto) {
-              lhl = true;
-              llm = p0 + (63 - __clzll((long long)upto));
-            }
-            bool st = !C.inside(qx[i], qy[i]);
-            if (lhl) st |= (uint64_t)(uint32_t)(j - llm) >= intensity;
-            else st |= j >= 1;
-            const unsigned long long S = __ballot(st);
-            if (S) stop = p0 + __ffsll((long long)S) - 1;
-            if (Mi) {
-              hl = true;
-              lm = p0 + (63 - __clzll((long long)Mi));
-            }
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 2; k++)
-          if (1 + 64 * k + lane < stop) C.paint(qx[2 * dd + k], qy[2 * dd + k]);
-        if (lane == 0) {
-          lpost[dd] = stop;
-          lpost[4 + dd] = hl;
-          lpost[8 + dd] = lm;
-        }
-      }
-    }
-    block_sync();
+    const int32_t* lpost = tab_stop() + 6 * kWaves;
     const int32_t v = lane < 12 ? lpost[lane] : 0;
 #pragma unroll
     for (int dd = 0; dd < 4; dd++) {
@@ -282,10 +314,8 @@ __device__ __forceinline__ void fill_lines(const Canvas<FMT>& C, int32_t px, int
       } else {
         if (__builtin_amdgcn_readlane(v, 4 + dd)) has_last |= 1u << dd;
         set4(last, dd, __builtin_amdgcn_readlane(v, 8 + dd));
-        set4(pos0, dd, 129);
       }
     }
-    BSTAT(bs->fill_trips++;)
   }
   int parity = 0;
   for (;;) {
@@ -407,21 +437,6 @@ __device__ __forceinline__ void fill_lines(const Canvas<FMT>& C, int32_t px, int
   BSTAT(bs->t_fill += wall_clock64() - t0;)
 }
 
-template <int FMT>
-__device__ __forceinline__ void frame_start(const Canvas<FMT>& C, int32_t x, int32_t y, uint64_t intensity,
-                            Frame* f, BlackStats* bs) {
-  // first half of flood_fill (fill.c:81-96); the caller has just read the
-  // start pixel as matching (a neighbour check or a bar pixel) and nothing
-  // has painted since
-  if (threadIdx.x == 0) C.paint(x, y);
-  block_sync();
-  f->x = x;
-  f->y = y;
-  fill_lines<FMT>(C, x, y, intensity, f->dist, bs);
-  f->cursor = 0;
-  BSTAT(bs->frames++;)
-}
-
 // Neighbour check number c of a frame (flood_fill_around_line, fill.c:62-79):
 // the checks of line 0, then 1, 2, 3; along a line two per position, below
 // then above (horizontal line) or right then left (vertical line).
@@ -465,22 +480,108 @@ __device__ __forceinline__ int32_t window_first(const uint64_t (&M)[kGroup],
   return any ? __shfl(v, __ffsll((long long)any) - 1, 64) : INT_MAX;
 }
 
-// flood_fill (fill.c:81-107) + flood_fill_around_line (fill.c:62-79), depth
-// first with an explicit stack in HBM; control is uniform over the workgroup.
+// The flood fill is driven by wave 0 alone.  Its small steps (a frame's
+// first 128 pixels per line, a check window of at most 512 checks) need no
+// other wave and no barrier; a long line or a long run of checks is posted as
+// a command, and the other waves, parked in `flood_help`, join for it.
+// A command's operation ends in a barrier that every wave reaches, so the
+// driver never rewrites the mailbox before the helpers have read it.
+enum : int32_t { CMD_DONE = 0, CMD_FILL = 1, CMD_CHECK = 2 };
+// mailbox: [0] sequence, [1] command, [2..3] fill start, [4..11] frame
+// (x, y, dist[4], cursor, checks), [12] flood result
+
+__device__ __forceinline__ void post_command(int32_t* seq, int32_t cmd) {
+  int32_t* mb = mailbox();
+  if (lane_id() == 0) mb[1] = cmd;
+  // arguments and paints before the sequence number that publishes them
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane_id() == 0) __hip_atomic_store(&mb[0], ++*seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else ++*seq;
+}
+
+// One check window of the whole workgroup (64 slices, 4096 checks).
 template <int FMT>
-__device__ __forceinline__ bool flood_fill(const Canvas<FMT>& C, int32_t sx, int32_t sy,
-                                           uint64_t intensity, Frame* stack, int32_t capacity,
-                                           int* parity, BlackStats* bs) {
+__device__ __forceinline__ int32_t check_coop(const Canvas<FMT>& C, const Frame& top, int32_t n,
+                                              int* parity, BlackStats* bs) {
   const int w = wave_id(), lane = lane_id();
+  int32_t qx[kGroup], qy[kGroup];
+  bool m[kGroup];
+#pragma unroll
+  for (int i = 0; i < kGroup; i++) {
+    const int32_t c = top.cursor + 64 * (w * kGroup + i) + lane;
+    check_pos(top, imin(c, n - 1), &qx[i], &qy[i]);
+    if (c >= n) qx[i] = -1;
+  }
+  C.match_group(qx, qy, m);
+  uint64_t M[kGroup];
+#pragma unroll
+  for (int i = 0; i < kGroup; i++) M[i] = __ballot(m[i]);
+  return window_first<false>(M, M, (*parity)++ & 1);
+}
+
+// The helpers' side: run the driver's commands until CMD_DONE.
+template <int FMT>
+__device__ void flood_help(const Canvas<FMT>& C, uint64_t intensity, int32_t* seen, int* parity,
+                           BlackStats* bs) {
+  int32_t* mb = mailbox();
+  for (;;) {
+    int32_t sq;
+    while ((sq = __hip_atomic_load(&mb[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
+           *seen)
+      __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    *seen = sq;
+    const int32_t cmd = mb[1];
+    if (cmd == CMD_DONE) return;
+    if (cmd == CMD_FILL) {
+      int32_t dist[4];
+      fill_coop<FMT>(C, mb[2], mb[3], intensity, dist, bs);
+    } else {
+      Frame f;
+      f.x = mb[4];
+      f.y = mb[5];
+      f.dist[0] = mb[6];
+      f.dist[1] = mb[7];
+      f.dist[2] = mb[8];
+      f.dist[3] = mb[9];
+      f.cursor = mb[10];
+      check_coop<FMT>(C, f, mb[11], parity, bs);
+    }
+  }
+}
+
+// flood_fill (fill.c:81-107) + flood_fill_around_line (fill.c:62-79), depth
+// first with an explicit stack in HBM, driven by wave 0.  Returns false on a
+// stack overflow.
+template <int FMT>
+__device__ bool flood_drive(const Canvas<FMT>& C, int32_t sx, int32_t sy, uint64_t intensity,
+                            Frame* stack, int32_t capacity, int32_t* seq, int* parity,
+                            BlackStats* bs) {
+  const int lane = lane_id();
+  int32_t* mb = mailbox();
   Frame top;
   int32_t sp = 0;  // frames on the stack, `top` included; those below it live in stack[0 .. sp-2]
   int32_t nx = sx, ny = sy;
   bool start = true;
   for (;;) {
-    if (start) {  // a new frame: save the parent, paint and fill the cross
+    if (start) {  // a new frame: save the parent, paint the start, fill the cross
       if (sp >= capacity) return false;  // stack overflow: flagged by the caller
-      if (sp > 0 && threadIdx.x == 0) stack[sp - 1] = top;
-      frame_start<FMT>(C, nx, ny, intensity, &top, bs);  // its barriers publish the push
+      if (sp > 0 && lane == 0) stack[sp - 1] = top;
+      // the caller has just read the start pixel as matching (a neighbour
+      // check or a bar pixel) and nothing has painted since
+      if (lane == 0) C.paint(nx, ny);
+      top.x = nx;
+      top.y = ny;
+      if (fill_local<FMT>(C, nx, ny, intensity, top.dist, bs)) {
+        if (lane == 0) {
+          mb[2] = nx;
+          mb[3] = ny;
+        }
+        post_command(seq, CMD_FILL);
+        fill_coop<FMT>(C, nx, ny, intensity, top.dist, bs);
+      }
+      top.cursor = 0;
+      BSTAT(bs->frames++;)
       sp++;
       start = false;
     }
@@ -491,22 +592,48 @@ __device__ __forceinline__ bool flood_fill(const Canvas<FMT>& C, int32_t sx, int
       continue;
     }
     BSTAT(const uint64_t tc = wall_clock64(); bs->check_trips++;)
-    int32_t qx[kGroup], qy[kGroup];
-    bool m[kGroup];
+    int32_t f;
+    int32_t span;
+    if (n - top.cursor <= 64 * kGroup) {  // this wave's 8 slices cover the rest
+      span = 64 * kGroup;
+      const int nsl = (n - top.cursor + 63) >> 6;  // slices holding checks (uniform)
+      int32_t qx[kGroup], qy[kGroup];
+      bool m[kGroup];
 #pragma unroll
-    for (int i = 0; i < kGroup; i++) {
-      const int32_t c = top.cursor + 64 * (w * kGroup + i) + lane;
-      check_pos(top, imin(c, n - 1), &qx[i], &qy[i]);
-      if (c >= n) qx[i] = -1;
+      for (int i = 0; i < kGroup; i++) {
+        qx[i] = -1;
+        qy[i] = 0;
+        if (i < nsl) {
+          const int32_t c = top.cursor + 64 * i + lane;
+          check_pos(top, imin(c, n - 1), &qx[i], &qy[i]);
+          if (c >= n) qx[i] = -1;
+        }
+      }
+      C.match_group(qx, qy, m);
+      f = INT_MAX;
+#pragma unroll
+      for (int i = kGroup - 1; i >= 0; i--) {
+        const unsigned long long Mi = __ballot(m[i]);
+        if (Mi) f = 64 * i + __ffsll((long long)Mi) - 1;
+      }
+    } else {
+      span = 64 * kSlices;
+      if (lane == 0) {
+        mb[4] = top.x;
+        mb[5] = top.y;
+        mb[6] = top.dist[0];
+        mb[7] = top.dist[1];
+        mb[8] = top.dist[2];
+        mb[9] = top.dist[3];
+        mb[10] = top.cursor;
+        mb[11] = n;
+      }
+      post_command(seq, CMD_CHECK);
+      f = check_coop<FMT>(C, top, n, parity, bs);
     }
-    C.match_group(qx, qy, m);
-    uint64_t M[kGroup];
-#pragma unroll
-    for (int i = 0; i < kGroup; i++) M[i] = __ballot(m[i]);
-    const int32_t f = window_first<false>(M, M, (*parity)++ & 1);
     BSTAT(bs->t_check += wall_clock64() - tc;)
     if (f == INT_MAX) {
-      top.cursor += 64 * kSlices;
+      top.cursor += span;
       continue;
     }
     const int32_t cidx = top.cursor + f;
@@ -539,6 +666,9 @@ __global__ void __launch_bounds__(kThreads) k_black_resolve(PlaneRef img, BlackG
   BSTAT(const uint64_t t_all = wall_clock64();)
   uint64_t* red = tab_red();
   int parity = 0;
+  int32_t seq = 0;  // last command number (driver) / last one seen (helpers)
+  if (threadIdx.x == 0) mailbox()[0] = 0;
+  block_sync();
   bool dirty = false;
   for (int32_t b0 = 0; b0 < g.nbars; b0 += kThreads) {
     // darkness of kThreads bars on the original image (darkness_rect,
@@ -631,8 +761,18 @@ __global__ void __launch_bounds__(kThreads) k_black_resolve(PlaneRef img, BlackG
             continue;
           }
           const int64_t hit = i0 + f;
-          if (!flood_fill<FMT>(C, bb.r.x0 + (int32_t)(hit % bw), bb.r.y0 + (int32_t)(hit / bw),
-                               g.intensity, stack, g.stack_capacity, &parity, bs)) {
+          // wave 0 drives the fill, the others help on its commands
+          if (w == 0) {
+            const bool ok = flood_drive<FMT>(C, bb.r.x0 + (int32_t)(hit % bw),
+                                             bb.r.y0 + (int32_t)(hit / bw), g.intensity, stack,
+                                             g.stack_capacity, &seq, &parity, bs);
+            if (lane == 0) mailbox()[12] = ok;
+            post_command(&seq, CMD_DONE);
+          } else {
+            flood_help<FMT>(C, g.intensity, &seq, &parity, bs);
+          }
+          block_sync();  // the fill's paints, and the result, for every wave
+          if (!mailbox()[12]) {
             if (threadIdx.x == 0 && ctl) atomicOr(&ctl[s].status, STATUS_FLOOD_OVERFLOW);
             return;
           }
