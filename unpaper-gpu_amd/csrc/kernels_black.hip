@@ -134,6 +134,39 @@ __device__ __forceinline__ uint64_t* tab_red() { return lds64() + kOffRed; }
 __device__ __forceinline__ uint64_t* tab_cand() { return lds64() + kOffCand; }
 __device__ __forceinline__ int32_t* mailbox() { return (int32_t*)(lds64() + kOffMail); }
 
+// The lowest kStackLds frames of the DFS stack live in LDS (dynamic), the
+// rest in HBM: a pop is then an LDS read instead of a memory round trip.
+constexpr int kStackLds = 3072;
+constexpr size_t kStackLdsBytes = (size_t)kStackLds * 32;  // 96 KiB
+__device__ __forceinline__ int4* stack_lds() {
+  extern __shared__ int4 black_stack[];
+  return black_stack;
+}
+__device__ __forceinline__ void frame_put(int4* lds, Frame* hbm, int32_t i, const Frame& f) {
+  const int4 a = make_int4(f.x, f.y, f.dist[0], f.dist[1]);
+  const int4 b = make_int4(f.dist[2], f.dist[3], f.cursor, 0);
+  if (i < kStackLds) {
+    lds[2 * i] = a;
+    lds[2 * i + 1] = b;
+  } else {
+    hbm[i] = f;
+  }
+}
+__device__ __forceinline__ Frame frame_get(const int4* lds, const Frame* hbm, int32_t i) {
+  if (i >= kStackLds) return hbm[i];
+  const int4 a = lds[2 * i], b = lds[2 * i + 1];
+  Frame f;
+  f.x = a.x;
+  f.y = a.y;
+  f.dist[0] = a.z;
+  f.dist[1] = a.w;
+  f.dist[2] = b.x;
+  f.dist[3] = b.y;
+  f.cursor = b.z;
+  f.pad = 0;
+  return f;
+}
+
 // scalar (readfirstlane), so everything derived from it stays in SGPRs
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
@@ -151,7 +184,7 @@ __device__ __forceinline__ void block_sync() { __syncthreads(); }
 // replay counters, tuning build only (UPHIP_DIAG_NOISE bit 16)
 struct BlackStats {
   uint32_t frames, fill_trips, check_trips, bar_trips, remeasures, lookups;
-  uint64_t t_fill, t_check, t_bar, t_remeasure, t_fa, t_fb, t_fc, t_fd, t_fa0, t_fa1;
+  uint64_t t_fill, t_check, t_bar, t_remeasure, t_fa, t_fb, t_fc, t_fd, t_fa0, t_fa1, t_local, t_pop;
 };
 #ifdef UPHIP_DIAG
 #define BSTAT(...) __VA_ARGS__
@@ -214,10 +247,11 @@ struct Canvas {
 // non-matching position if there was none).  The four lines touch disjoint
 // pixels (left, up, right, down of the start), so they share each round trip.
 //
-// fill_local: the first round trip, by the driving wave alone: the first 128
-// positions of each line (two slices a line, one wave's group).  Most lines
-// of most frames end there.  The lines' state goes to `lpost`; returns
+// fill_local: the first round trip, by the driving wave alone: the first
+// 64 kLocalSl positions of each line.  Most lines of most frames end there.  The lines' state goes to `lpost`; returns
 // whether a line runs on.
+constexpr int kLocalSl = 2;  // slices per line of a frame's first round trip (1: more lines go cooperative, slower overall)
+
 template <int FMT>
 __device__ __forceinline__ bool fill_local(const Canvas<FMT>& C, int32_t px, int32_t py,
                                            uint64_t intensity, int32_t (&dist)[4],
@@ -226,12 +260,12 @@ __device__ __forceinline__ bool fill_local(const Canvas<FMT>& C, int32_t px, int
   const uint64_t upto_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
   int32_t* lpost = tab_stop() + 6 * kWaves;  // [4] stop | [4] has_last | [4] last
   bool more = false;
-  int32_t qx[kGroup], qy[kGroup];
-  bool m[kGroup];
+  int32_t qx[4 * kLocalSl], qy[4 * kLocalSl];
+  bool m[4 * kLocalSl];
 #pragma unroll
-  for (int i = 0; i < kGroup; i++) {
-    const int dd = i >> 1;
-    const int32_t j = 1 + 64 * (i & 1) + lane;
+  for (int i = 0; i < 4 * kLocalSl; i++) {
+    const int dd = i / kLocalSl;
+    const int32_t j = 1 + 64 * (i % kLocalSl) + lane;
     qx[i] = dd == 0 ? px - j : dd == 2 ? px + j : px;
     qy[i] = dd == 1 ? py - j : dd == 3 ? py + j : py;
   }
@@ -241,8 +275,8 @@ __device__ __forceinline__ bool fill_local(const Canvas<FMT>& C, int32_t px, int
     bool hl = false;
     int32_t lm = 0, stop = INT_MAX;
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
-      const int i = 2 * dd + k;
+    for (int k = 0; k < kLocalSl; k++) {
+      const int i = kLocalSl * dd + k;
       const unsigned long long Mi = __ballot(m[i]);
       if (stop == INT_MAX) {
         const int32_t p0 = 1 + 64 * k, j = p0 + lane;
@@ -265,8 +299,8 @@ __device__ __forceinline__ bool fill_local(const Canvas<FMT>& C, int32_t px, int
       }
     }
 #pragma unroll
-    for (int k = 0; k < 2; k++)
-      if (1 + 64 * k + lane < stop) C.paint(qx[2 * dd + k], qy[2 * dd + k]);
+    for (int k = 0; k < kLocalSl; k++)
+      if (1 + 64 * k + lane < stop) C.paint(qx[kLocalSl * dd + k], qy[kLocalSl * dd + k]);
     if (lane == 0) {
       lpost[dd] = stop;
       lpost[4 + dd] = hl;
@@ -298,7 +332,8 @@ __device__ __forceinline__ void fill_coop(const Canvas<FMT>& C, int32_t px, int3
   uint32_t done = 0, has_last = 0;  // per line bits (bool arrays indexed by a
                                     // run-time line would live in scratch)
   int32_t last[4] = {0, 0, 0, 0};   // positions along a line fit 31 bits
-  int32_t pos0[4] = {129, 129, 129, 129};
+  constexpr int32_t kFirst = 1 + 64 * kLocalSl;  // fill_local read positions 1 .. kFirst - 1
+  int32_t pos0[4] = {kFirst, kFirst, kFirst, kFirst};
   // first position outside the image, per line
   const int32_t edge[4] = {px + 1, py + 1, C.W - px, C.H - py};
   const uint64_t upto_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
@@ -566,13 +601,16 @@ __device__ bool flood_drive(const Canvas<FMT>& C, int32_t sx, int32_t sy, uint64
   for (;;) {
     if (start) {  // a new frame: save the parent, paint the start, fill the cross
       if (sp >= capacity) return false;  // stack overflow: flagged by the caller
-      if (sp > 0 && lane == 0) stack[sp - 1] = top;
+      if (sp > 0 && lane == 0) frame_put(stack_lds(), stack, sp - 1, top);
       // the caller has just read the start pixel as matching (a neighbour
       // check or a bar pixel) and nothing has painted since
       if (lane == 0) C.paint(nx, ny);
       top.x = nx;
       top.y = ny;
-      if (fill_local<FMT>(C, nx, ny, intensity, top.dist, bs)) {
+      BSTAT(const uint64_t tl = wall_clock64();)
+      const bool more = fill_local<FMT>(C, nx, ny, intensity, top.dist, bs);
+      BSTAT(bs->t_local += wall_clock64() - tl;)
+      if (more) {
         if (lane == 0) {
           mb[2] = nx;
           mb[3] = ny;
@@ -588,7 +626,9 @@ __device__ bool flood_drive(const Canvas<FMT>& C, int32_t sx, int32_t sy, uint64
     const int32_t n = 2 * (top.dist[0] + top.dist[1] + top.dist[2] + top.dist[3]);
     if (top.cursor >= n) {
       if (--sp == 0) return true;
-      top = stack[sp - 1];
+      BSTAT(const uint64_t tq = wall_clock64();)
+      top = frame_get(stack_lds(), stack, sp - 1);
+      BSTAT(bs->t_pop += wall_clock64() - tq;)
       continue;
     }
     BSTAT(const uint64_t tc = wall_clock64(); bs->check_trips++;)
@@ -610,11 +650,28 @@ __device__ bool flood_drive(const Canvas<FMT>& C, int32_t sx, int32_t sy, uint64
         }
       }
       C.match_group(qx, qy, m);
+      // the first match and the one after it: painting only turns pixels
+      // white, so checks that did not match now cannot match after the
+      // child's fill either, and the frame resumes at the second match (or,
+      // with none, is done) without reading its checks again
       f = INT_MAX;
+      int32_t f2 = INT_MAX;
 #pragma unroll
       for (int i = kGroup - 1; i >= 0; i--) {
         const unsigned long long Mi = __ballot(m[i]);
-        if (Mi) f = 64 * i + __ffsll((long long)Mi) - 1;
+        if (Mi) {
+          const unsigned long long rest = Mi & (Mi - 1);
+          f2 = rest ? 64 * i + __ffsll((long long)rest) - 1 : f;
+          f = 64 * i + __ffsll((long long)Mi) - 1;
+        }
+      }
+      if (f != INT_MAX) {
+        const int32_t cidx = top.cursor + f;
+        check_pos(top, cidx, &nx, &ny);
+        top.cursor = f2 != INT_MAX ? top.cursor + f2 : n;
+        BSTAT(bs->t_check += wall_clock64() - tc;)
+        start = true;
+        continue;
       }
     } else {
       span = 64 * kSlices;
@@ -787,13 +844,13 @@ __global__ void __launch_bounds__(kThreads) k_black_resolve(PlaneRef img, BlackG
   if ((g.diag & 16) && threadIdx.x == 0 && bstat.frames)
     printf("uphip black: sheet %d frames %u fill %u (%.1f us) check %u (%.1f us) bar %u (%.1f us) "
            "remeasure %u (%.1f us) total %.1f us lookups %u "
-           "fillA %.1f (pos %.1f lookup %.1f) B %.1f C %.1f D %.1f us\n",
+           "fillA %.1f (pos %.1f lookup %.1f) B %.1f C %.1f D %.1f us local %.1f pop %.1f us\n",
            s, bstat.frames, bstat.fill_trips, bstat.t_fill * 0.01, bstat.check_trips,
            bstat.t_check * 0.01, bstat.bar_trips, bstat.t_bar * 0.01, bstat.remeasures,
            bstat.t_remeasure * 0.01, (wall_clock64() - t_all) * 0.01, bstat.lookups * 64,
            bstat.t_fa * 0.01, bstat.t_fa0 * 0.01,
            bstat.t_fa1 * 0.01, bstat.t_fb * 0.01,
-           bstat.t_fc * 0.01, bstat.t_fd * 0.01);
+           bstat.t_fc * 0.01, bstat.t_fd * 0.01, bstat.t_local * 0.01, bstat.t_pop * 0.01);
 #endif
 }
 
@@ -810,8 +867,9 @@ static void launch_black_t(const PlaneRef& img, const BlackGeom& g, const BlackB
                        (uint32_t*)scr + g.W, ss / 4, count, st);
   BlackGeom gd = g;
   gd.diag = diag_noise();
+  allow_dynamic_lds((const void*)k_black_resolve<FMT>, kStackLdsBytes);
   if (!(diag_skip() & 1))
-    hipLaunchKernelGGL(k_black_resolve<FMT>, dim3(count), dim3(kThreads), 0, st, img, gd,
+    hipLaunchKernelGGL(k_black_resolve<FMT>, dim3(count), dim3(kThreads), kStackLdsBytes, st, img, gd,
                        bars, scr, ss, active, ctl);
 }
 
