@@ -634,9 +634,11 @@ __device__ bool flood_drive(const Canvas<FMT>& C, int32_t sx, int32_t sy, uint64
     BSTAT(const uint64_t tc = wall_clock64(); bs->check_trips++;)
     int32_t f;
     int32_t span;
-    if (n - top.cursor <= 64 * kGroup) {  // this wave's 8 slices cover the rest
+    // this wave alone when its 8 slices cover the rest, and for a frame's
+    // first window (a new frame's first checks usually start its child)
+    if (n - top.cursor <= 64 * kGroup || top.cursor == 0) {
       span = 64 * kGroup;
-      const int nsl = (n - top.cursor + 63) >> 6;  // slices holding checks (uniform)
+      const int nsl = imin((n - top.cursor + 63) >> 6, kGroup);  // slices holding checks
       int32_t qx[kGroup], qy[kGroup];
       bool m[kGroup];
 #pragma unroll
@@ -668,7 +670,7 @@ __device__ bool flood_drive(const Canvas<FMT>& C, int32_t sx, int32_t sy, uint64
       if (f != INT_MAX) {
         const int32_t cidx = top.cursor + f;
         check_pos(top, cidx, &nx, &ny);
-        top.cursor = f2 != INT_MAX ? top.cursor + f2 : n;
+        top.cursor = f2 != INT_MAX ? top.cursor + f2 : imin(n, top.cursor + 64 * nsl);
         BSTAT(bs->t_check += wall_clock64() - tc;)
         start = true;
         continue;
