@@ -482,7 +482,7 @@ typedef struct {
   int64_t jobs_done, jobs_failed;
   int64_t jobs_per_device[UPHIP_RUNNER_MAX_DEVICES];
   double wall_s;               /* last run */
-  double load_s, store_s;      /* summed over the device threads' host phases */
+  double load_s, store_s;      /* summed over the host pool's load / store tasks */
 } UphipRunnerStats;
 /* Sources fill page `page` of job `job` into pinned staging; sinks receive a
  * finished sheet in the output format (pages side by side for output_count 2).
