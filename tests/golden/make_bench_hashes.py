@@ -14,7 +14,7 @@ sharded run (1000 pages per rank), the first 16 pages of each shard.
 Options: the reference defaults (uphip_options_init == lib/options.c).
 Hash: SHA-256 over the output rows' visible bytes (GRAY8, W bytes per row).
 
-C4 (--which c4 -> c4_hashes.json): RGB24 9920x7016 double-page sheets 0 and 1
+C4 (--which c4 -> c4_hashes.json): RGB24 9920x7016 double-page sheets 0..15
 (synth.h synth_rgb_channel) with unpaper_hip.workloads.c4_options (layout
 double, bilinear deskew, border wipe); hash over the saved RGB24 rows.
 
@@ -71,10 +71,18 @@ def main_c4(args):
     res = {}
     t0 = time.time()
 
-    def work(k):
-        res[k] = c4_hash(oracle, opts, k)
+    todo = list(range(args.c4_sheets))
+    lock = threading.Lock()
 
-    ts = [threading.Thread(target=work, args=(k,)) for k in (0, 1)]
+    def work():
+        while True:
+            with lock:
+                if not todo:
+                    return
+                k = todo.pop(0)
+            res[k] = c4_hash(oracle, opts, k)
+
+    ts = [threading.Thread(target=work) for _ in range(min(args.threads, args.c4_sheets))]
     for t in ts:
         t.start()
     for t in ts:
@@ -98,6 +106,8 @@ def main():
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 1)
     ap.add_argument("--out", default=os.path.join(HERE, "bench_hashes.json"))
     ap.add_argument("--which", default="a4", choices=("a4", "c4"))
+    ap.add_argument("--c4-sheets", type=int, default=16,
+                    help="C4: hash sheets 0 .. N-1 (the bench's whole 16-sheet workload)")
     args = ap.parse_args()
     if args.which == "c4":
         return main_c4(args)

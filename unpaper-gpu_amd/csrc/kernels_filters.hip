@@ -407,11 +407,10 @@ __global__ void __launch_bounds__(256) k_blur_counts_g(PlaneRef img, BlurGeom g,
   const uint8_t* base = plane_ptr(img, s);
   extern __shared__ uint16_t ccount[];
   const int32_t nd = (g.W + 3) >> 2;
-  // dark bits of a dword's bytes 0/2 and 1/3 as 16-bit lanes: bit 8 of
-  // byte + 256 - (white+1) is clear for byte <= white
-  const uint32_t kadd = (256u - ((uint32_t)g.white + 1u)) * 0x00010001u;
+  // one compare per byte: the byte select of an SDWA compare and an add with
+  // carry-in make it two instructions, fewer than the 16-bit lane form
   for (int32_t d = threadIdx.x; d < nd; d += 256) {
-    uint32_t c02 = 0, c13 = 0;
+    uint32_t c[4] = {0, 0, 0, 0};
     for (int32_t y = y0; y < y1; y += 8) {
       uint32_t v[8];
 #pragma unroll
@@ -420,15 +419,13 @@ __global__ void __launch_bounds__(256) k_blur_counts_g(PlaneRef img, BlurGeom g,
                                                   4 * d);
 #pragma unroll
       for (int k = 0; k < 8; k++) {
-        if (y + k >= y1) continue;
-        c02 += 0x00010001u - ((((v[k] & 0x00FF00FFu) + kadd) >> 8) & 0x00010001u);
-        c13 += 0x00010001u - (((((v[k] >> 8) & 0x00FF00FFu) + kadd) >> 8) & 0x00010001u);
+        const uint32_t keep = y + k < y1 ? 1u : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; j++) c[j] += keep & (((v[k] >> (8 * j)) & 0xFF) <= g.white ? 1u : 0u);
       }
     }
-    ccount[4 * d + 0] = (uint16_t)c02;
-    ccount[4 * d + 1] = (uint16_t)c13;
-    ccount[4 * d + 2] = (uint16_t)(c02 >> 16);
-    ccount[4 * d + 3] = (uint16_t)(c13 >> 16);
+#pragma unroll
+    for (int j = 0; j < 4; j++) ccount[4 * d + j] = (uint16_t)c[j];
   }
   __syncthreads();
   const int32_t nr = row == 0 ? g.bpr : g.bpr + 1;
