@@ -79,7 +79,7 @@ size_t black_scratch_bytes(const BlackGeom& g) {
   // [sums: W (h-stripe columns) + H (v-stripe rows)] u32 + DFS stack frames
   size_t b = ((size_t)g.W + g.H) * 4;
   b = (b + 255) & ~(size_t)255;
-  b += (size_t)g.stack_capacity * 64;  // sizeof(Frame)
+  b += (size_t)g.stack_capacity * 32;
   return (b + 255) & ~(size_t)255;
 }
 
@@ -87,14 +87,8 @@ struct Frame {
   int32_t x, y;
   int32_t dist[4];
   int32_t cursor;  // next neighbour check, over the four lines' checks in order
-  // What the frame's last check window saw (driver's windows): the matches
-  // after the one that started the child (spec, up to 4), the window's end
-  // (or the 5th such match), and the paint epoch of the read.
-  int32_t wepoch, wend, nspec;
-  int32_t spec[4];
-  int32_t pad[2];
+  int32_t pad;
 };
-static_assert(sizeof(Frame) == 64, "Frame is four 16-byte words");
 
 // left, up, right, down (fill.c:92-106)
 __device__ __forceinline__ constexpr int dir_dx(int d) { return d == 0 ? -1 : d == 2 ? 1 : 0; }
@@ -142,33 +136,25 @@ __device__ __forceinline__ int32_t* mailbox() { return (int32_t*)(lds64() + kOff
 
 // The lowest kStackLds frames of the DFS stack live in LDS (dynamic), the
 // rest in HBM: a pop is then an LDS read instead of a memory round trip.
-// After the stack: the paint epochs, per pixel of a 128 x 128 torus (the
-// latest frame number that painted a pixel mapping there).
-constexpr int kStackLds = 1024;
-constexpr int kEpochs = 128 * 128;
-constexpr size_t kReplayDynLds = (size_t)kStackLds * sizeof(Frame) + kEpochs * 4;  // 128 KiB
+constexpr int kStackLds = 3072;
+constexpr size_t kStackLdsBytes = (size_t)kStackLds * 32;  // 96 KiB
 __device__ __forceinline__ int4* stack_lds() {
-  extern __shared__ int4 black_dyn[];
-  return black_dyn;
+  extern __shared__ int4 black_stack[];
+  return black_stack;
 }
-__device__ __forceinline__ int32_t* epoch_tab() {
-  extern __shared__ int4 black_dyn[];
-  return (int32_t*)(black_dyn + 4 * kStackLds);
-}
-__device__ __forceinline__ int32_t epoch_slot(int32_t x, int32_t y) {
-  return (x & 127) | ((y & 127) << 7);
-}
-// field by field (a reinterpreted local would live in scratch)
 __device__ __forceinline__ void frame_put(int4* lds, Frame* hbm, int32_t i, const Frame& f) {
-  int4* d = i < kStackLds ? lds + 4 * i : reinterpret_cast<int4*>(hbm + i);
-  d[0] = make_int4(f.x, f.y, f.dist[0], f.dist[1]);
-  d[1] = make_int4(f.dist[2], f.dist[3], f.cursor, f.wepoch);
-  d[2] = make_int4(f.wend, f.nspec, f.spec[0], f.spec[1]);
-  d[3] = make_int4(f.spec[2], f.spec[3], 0, 0);
+  const int4 a = make_int4(f.x, f.y, f.dist[0], f.dist[1]);
+  const int4 b = make_int4(f.dist[2], f.dist[3], f.cursor, 0);
+  if (i < kStackLds) {
+    lds[2 * i] = a;
+    lds[2 * i + 1] = b;
+  } else {
+    hbm[i] = f;
+  }
 }
 __device__ __forceinline__ Frame frame_get(const int4* lds, const Frame* hbm, int32_t i) {
-  const int4* d = i < kStackLds ? lds + 4 * i : reinterpret_cast<const int4*>(hbm + i);
-  const int4 a = d[0], b = d[1], c = d[2], e = d[3];
+  if (i >= kStackLds) return hbm[i];
+  const int4 a = lds[2 * i], b = lds[2 * i + 1];
   Frame f;
   f.x = a.x;
   f.y = a.y;
@@ -177,14 +163,7 @@ __device__ __forceinline__ Frame frame_get(const int4* lds, const Frame* hbm, in
   f.dist[2] = b.x;
   f.dist[3] = b.y;
   f.cursor = b.z;
-  f.wepoch = b.w;
-  f.wend = c.x;
-  f.nspec = c.y;
-  f.spec[0] = c.z;
-  f.spec[1] = c.w;
-  f.spec[2] = e.x;
-  f.spec[3] = e.y;
-  f.pad[0] = f.pad[1] = 0;
+  f.pad = 0;
   return f;
 }
 
@@ -239,11 +218,8 @@ struct Canvas {
     for (int k = 0; k < N; k++) m[k] = inside(x[k], y[k]) && g[k] <= mmax;
     BSTAT(bs->lookups += N;)
   }
-  // paint white and note the frame number that did it
-  __device__ __forceinline__ void paint(int32_t x, int32_t y, int32_t epoch) const {
-    if (!inside(x, y)) return;
-    store_px_row<FMT>(base + (int64_t)y * pitch, x, Px{255, 255, 255});
-    atomicMax(&epoch_tab()[epoch_slot(x, y)], epoch);
+  __device__ __forceinline__ void paint(int32_t x, int32_t y) const {
+    if (inside(x, y)) store_px_row<FMT>(base + (int64_t)y * pitch, x, Px{255, 255, 255});
   }
 };
 
@@ -278,8 +254,8 @@ constexpr int kLocalSl = 2;  // slices per line of a frame's first round trip (1
 
 template <int FMT>
 __device__ __forceinline__ bool fill_local(const Canvas<FMT>& C, int32_t px, int32_t py,
-                                           uint64_t intensity, int32_t epoch,
-                                           int32_t (&dist)[4], BlackStats* bs) {
+                                           uint64_t intensity, int32_t (&dist)[4],
+                                           BlackStats* bs) {
   const int lane = lane_id();
   const uint64_t upto_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
   int32_t* lpost = tab_stop() + 6 * kWaves;  // [4] stop | [4] has_last | [4] last
@@ -324,7 +300,7 @@ __device__ __forceinline__ bool fill_local(const Canvas<FMT>& C, int32_t px, int
     }
 #pragma unroll
     for (int k = 0; k < kLocalSl; k++)
-      if (1 + 64 * k + lane < stop) C.paint(qx[kLocalSl * dd + k], qy[kLocalSl * dd + k], epoch);
+      if (1 + 64 * k + lane < stop) C.paint(qx[kLocalSl * dd + k], qy[kLocalSl * dd + k]);
     if (lane == 0) {
       lpost[dd] = stop;
       lpost[4 + dd] = hl;
@@ -349,7 +325,7 @@ __device__ __forceinline__ bool fill_local(const Canvas<FMT>& C, int32_t px, int
 // the paints are published by the barrier after the four lines.
 template <int FMT>
 __device__ __forceinline__ void fill_coop(const Canvas<FMT>& C, int32_t px, int32_t py,
-                                          uint64_t intensity, int32_t epoch, int32_t (&dist)[4],
+                                          uint64_t intensity, int32_t (&dist)[4],
                                           BlackStats* bs) {
   const int w = wave_id(), lane = lane_id();
   BSTAT(const uint64_t t0 = wall_clock64();)
@@ -488,7 +464,7 @@ __device__ __forceinline__ void fill_coop(const Canvas<FMT>& C, int32_t px, int3
       const int32_t lim = pick4(sd, d);
 #pragma unroll
       for (int i = 0; i < kGroup; i++)
-        if (base0 + 64 * i + lane < lim) C.paint(qx[i], qy[i], epoch);
+        if (base0 + 64 * i + lane < lim) C.paint(qx[i], qy[i]);
     }
     BSTAT(bs->t_fd += wall_clock64() - tp; bs->fill_trips++;)
   }
@@ -547,7 +523,7 @@ __device__ __forceinline__ int32_t window_first(const uint64_t (&M)[kGroup],
 // driver never rewrites the mailbox before the helpers have read it.
 enum : int32_t { CMD_DONE = 0, CMD_FILL = 1, CMD_CHECK = 2 };
 // mailbox: [0] sequence, [1] command, [2..3] fill start, [4..11] frame
-// (x, y, dist[4], cursor, checks), [12] flood result, [13] fill epoch
+// (x, y, dist[4], cursor, checks), [12] flood result
 
 __device__ __forceinline__ void post_command(int32_t* seq, int32_t cmd) {
   int32_t* mb = mailbox();
@@ -594,7 +570,7 @@ __device__ void flood_help(const Canvas<FMT>& C, uint64_t intensity, int32_t* se
     if (cmd == CMD_DONE) return;
     if (cmd == CMD_FILL) {
       int32_t dist[4];
-      fill_coop<FMT>(C, mb[2], mb[3], intensity, mb[13], dist, bs);
+      fill_coop<FMT>(C, mb[2], mb[3], intensity, dist, bs);
     } else {
       Frame f;
       f.x = mb[4];
@@ -615,7 +591,7 @@ __device__ void flood_help(const Canvas<FMT>& C, uint64_t intensity, int32_t* se
 template <int FMT>
 __device__ bool flood_drive(const Canvas<FMT>& C, int32_t sx, int32_t sy, uint64_t intensity,
                             Frame* stack, int32_t capacity, int32_t* seq, int* parity,
-                            int32_t* fseq, BlackStats* bs) {
+                            BlackStats* bs) {
   const int lane = lane_id();
   int32_t* mb = mailbox();
   Frame top;
@@ -626,26 +602,23 @@ __device__ bool flood_drive(const Canvas<FMT>& C, int32_t sx, int32_t sy, uint64
     if (start) {  // a new frame: save the parent, paint the start, fill the cross
       if (sp >= capacity) return false;  // stack overflow: flagged by the caller
       if (sp > 0 && lane == 0) frame_put(stack_lds(), stack, sp - 1, top);
-      const int32_t epoch = ++*fseq;  // this frame's paints
       // the caller has just read the start pixel as matching (a neighbour
       // check or a bar pixel) and nothing has painted since
-      if (lane == 0) C.paint(nx, ny, epoch);
+      if (lane == 0) C.paint(nx, ny);
       top.x = nx;
       top.y = ny;
       BSTAT(const uint64_t tl = wall_clock64();)
-      const bool more = fill_local<FMT>(C, nx, ny, intensity, epoch, top.dist, bs);
+      const bool more = fill_local<FMT>(C, nx, ny, intensity, top.dist, bs);
       BSTAT(bs->t_local += wall_clock64() - tl;)
       if (more) {
         if (lane == 0) {
           mb[2] = nx;
           mb[3] = ny;
-          mb[13] = epoch;
         }
         post_command(seq, CMD_FILL);
-        fill_coop<FMT>(C, nx, ny, intensity, epoch, top.dist, bs);
+        fill_coop<FMT>(C, nx, ny, intensity, top.dist, bs);
       }
       top.cursor = 0;
-      top.nspec = 0;
       BSTAT(bs->frames++;)
       sp++;
       start = false;
@@ -657,26 +630,6 @@ __device__ bool flood_drive(const Canvas<FMT>& C, int32_t sx, int32_t sy, uint64
       top = frame_get(stack_lds(), stack, sp - 1);
       BSTAT(bs->t_pop += wall_clock64() - tq;)
       continue;
-    }
-    // Back at a match its window already saw: painting only turns pixels
-    // white, so it still matches unless something painted it since.  The
-    // epoch table says "not painted since the read" for sure (a slot holds
-    // the latest painter of every pixel mapping there), then the next child
-    // starts without reading the image.
-    if (top.nspec > 0 && top.cursor == top.spec[0]) {
-      int32_t px2, py2;
-      check_pos(top, top.spec[0], &px2, &py2);
-      if (epoch_tab()[epoch_slot(px2, py2)] <= top.wepoch) {
-#pragma unroll
-        for (int q = 0; q < 3; q++) top.spec[q] = top.spec[q + 1];
-        top.nspec--;
-        top.cursor = top.nspec > 0 ? top.spec[0] : top.wend;
-        nx = px2;
-        ny = py2;
-        start = true;
-        continue;
-      }
-      top.nspec = 0;  // maybe painted: read the window again from here
     }
     BSTAT(const uint64_t tc = wall_clock64(); bs->check_trips++;)
     int32_t f;
@@ -699,42 +652,25 @@ __device__ bool flood_drive(const Canvas<FMT>& C, int32_t sx, int32_t sy, uint64
         }
       }
       C.match_group(qx, qy, m);
-      // The first match starts the child.  Checks that did not match cannot
-      // match later (painting only turns pixels white), so the frame keeps the
-      // next matches of this read (up to 4) and resumes at them, and past the
-      // last of them at the window's end (or at a 5th match it did not keep).
-      uint64_t M[kGroup];
-#pragma unroll
-      for (int i = 0; i < kGroup; i++) M[i] = __ballot(m[i]);
+      // the first match and the one after it: painting only turns pixels
+      // white, so checks that did not match now cannot match after the
+      // child's fill either, and the frame resumes at the second match (or,
+      // with none, is done) without reading its checks again
       f = INT_MAX;
-      // the first 6 matches of the window, in order (scalar: ballots are uniform)
-      int32_t found[6] = {0, 0, 0, 0, 0, 0};
-      int nf = 0;
+      int32_t f2 = INT_MAX;
 #pragma unroll
-      for (int i = 0; i < kGroup; i++) {
-        uint64_t Mi = M[i];
-#pragma unroll
-        for (int r = 0; r < 6; r++) {
-          if (Mi && nf < 6) {
-            const int32_t v = 64 * i + __ffsll((long long)Mi) - 1;
-#pragma unroll
-            for (int q = 0; q < 6; q++)
-              if (q == nf) found[q] = v;
-            nf++;
-            Mi &= Mi - 1;
-          }
+      for (int i = kGroup - 1; i >= 0; i--) {
+        const unsigned long long Mi = __ballot(m[i]);
+        if (Mi) {
+          const unsigned long long rest = Mi & (Mi - 1);
+          f2 = rest ? 64 * i + __ffsll((long long)rest) - 1 : f;
+          f = 64 * i + __ffsll((long long)Mi) - 1;
         }
       }
-      if (nf > 0) {
-        const int32_t c0 = top.cursor;
-        f = found[0];
-        check_pos(top, c0 + f, &nx, &ny);
-        top.wepoch = *fseq;
-        top.wend = nf == 6 ? c0 + found[5] : imin(n, c0 + 64 * nsl);
-        top.nspec = imin(nf - 1, 4);
-#pragma unroll
-        for (int q = 0; q < 4; q++) top.spec[q] = q + 1 < nf ? c0 + found[q + 1] : INT_MAX;
-        top.cursor = top.nspec > 0 ? top.spec[0] : top.wend;
+      if (f != INT_MAX) {
+        const int32_t cidx = top.cursor + f;
+        check_pos(top, cidx, &nx, &ny);
+        top.cursor = f2 != INT_MAX ? top.cursor + f2 : imin(n, top.cursor + 64 * nsl);
         BSTAT(bs->t_check += wall_clock64() - tc;)
         start = true;
         continue;
@@ -789,10 +725,8 @@ __global__ void __launch_bounds__(kThreads) k_black_resolve(PlaneRef img, BlackG
   BSTAT(const uint64_t t_all = wall_clock64();)
   uint64_t* red = tab_red();
   int parity = 0;
-  int32_t seq = 0;   // last command number (driver) / last one seen (helpers)
-  int32_t fseq = 0;  // frames started (the driver's paint epochs)
+  int32_t seq = 0;  // last command number (driver) / last one seen (helpers)
   if (threadIdx.x == 0) mailbox()[0] = 0;
-  for (int i = threadIdx.x; i < kEpochs; i += kThreads) epoch_tab()[i] = 0;
   block_sync();
   bool dirty = false;
   for (int32_t b0 = 0; b0 < g.nbars; b0 += kThreads) {
@@ -890,7 +824,7 @@ __global__ void __launch_bounds__(kThreads) k_black_resolve(PlaneRef img, BlackG
           if (w == 0) {
             const bool ok = flood_drive<FMT>(C, bb.r.x0 + (int32_t)(hit % bw),
                                              bb.r.y0 + (int32_t)(hit / bw), g.intensity, stack,
-                                             g.stack_capacity, &seq, &parity, &fseq, bs);
+                                             g.stack_capacity, &seq, &parity, bs);
             if (lane == 0) mailbox()[12] = ok;
             post_command(&seq, CMD_DONE);
           } else {
@@ -935,9 +869,9 @@ static void launch_black_t(const PlaneRef& img, const BlackGeom& g, const BlackB
                        (uint32_t*)scr + g.W, ss / 4, count, st);
   BlackGeom gd = g;
   gd.diag = diag_noise();
-  allow_dynamic_lds((const void*)k_black_resolve<FMT>, kReplayDynLds);
+  allow_dynamic_lds((const void*)k_black_resolve<FMT>, kStackLdsBytes);
   if (!(diag_skip() & 1))
-    hipLaunchKernelGGL(k_black_resolve<FMT>, dim3(count), dim3(kThreads), kReplayDynLds, st, img, gd,
+    hipLaunchKernelGGL(k_black_resolve<FMT>, dim3(count), dim3(kThreads), kStackLdsBytes, st, img, gd,
                        bars, scr, ss, active, ctl);
 }
 
