@@ -1338,6 +1338,12 @@ __device__ __forceinline__ void cubic2x4(const f2 (&f)[4], const f2 (&h)[4],
                 __builtin_amdgcn_fmed3f(__builtin_truncf(u[i].y), 0.0f, 255.0f)};
 }
 
+// v from the lane given by the quad permutation CTRL (DPP quad_perm)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
 // Byte offset of row y (0 <= y < H) as a 32-bit product: the launcher only
 // picks k_rotate_cubic_g8f when pitch * H < 2^31 (one scalar multiply per row
 // instead of a 64-bit product).
@@ -1383,93 +1389,116 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
     }
     return;
   }
-  // source window of the tile's in-mask pixels (their 4x4 taps included)
-  int32_t bx0 = 0, by0 = 0, bw = 0, bh = 0;
-  {
-    float mnx = 3.0e38f, mxx = -3.0e38f, mny = 3.0e38f, mxy = -3.0e38f;
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const int32_t u = c & 1 ? cu1 : cu0, v = c & 2 ? cv1 : cv0;
-      const float X = scx + (u - tcx) * a.cosval + (v - tcy) * a.sinval;
-      const float Y = scy + (v - tcy) * a.cosval - (u - tcx) * a.sinval;
-      mnx = fminf(mnx, X);
-      mxx = fmaxf(mxx, X);
-      mny = fminf(mny, Y);
-      mxy = fmaxf(mxy, Y);
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // Source window of the tile's in-mask pixels (their 4x4 taps included).
+  // Every pixel's coordinate lies between the corners' (the same float
+  // expression, monotone in u and v); its taps span (int)c - 1 .. (int)c + 2,
+  // and (int)c <= floor(c) + 1 (truncation of negatives).  The window is a
+  // per-tile constant: wave 0 evaluates the four corners in lanes (c = lane
+  // & 3), reduces them across the quad and posts the bounds in LDS, instead
+  // of every wave running the float chain of all four corners.
+  __shared__ int32_t win_s[4];
+  if (wu == 0) {
+    const int c = lane & 3;
+    const int32_t u = c & 1 ? cu1 : cu0, v = c & 2 ? cv1 : cv0;
+    const float X = scx + (u - tcx) * a.cosval + (v - tcy) * a.sinval;
+    const float Y = scy + (v - tcy) * a.cosval - (u - tcx) * a.sinval;
+    float mnx = fminf(X, dpp_f<0xB1>(X)), mxx = fmaxf(X, dpp_f<0xB1>(X));
+    float mny = fminf(Y, dpp_f<0xB1>(Y)), mxy = fmaxf(Y, dpp_f<0xB1>(Y));
+    mnx = fminf(mnx, dpp_f<0x4E>(mnx));
+    mxx = fmaxf(mxx, dpp_f<0x4E>(mxx));
+    mny = fminf(mny, dpp_f<0x4E>(mny));
+    mxy = fmaxf(mxy, dpp_f<0x4E>(mxy));
+    if (lane < 4) {
+      const float q = lane == 0 ? mnx : lane == 1 ? mny : lane == 2 ? mxx : mxy;
+      win_s[lane] = (int32_t)floorf(q);
     }
-    // every pixel's coordinate lies between the corners' (the same float
-    // expression, monotone in u and v); its taps span (int)c - 1 .. (int)c + 2,
-    // and (int)c <= floor(c) + 1 (truncation of negatives)
-    bx0 = (int32_t)floorf(mnx) - 1;
-    by0 = (int32_t)floorf(mny) - 1;
-    bw = (int32_t)floorf(mxx) + 3 - bx0 + 1;
-    bh = (int32_t)floorf(mxy) + 3 - by0 + 1;
   }
+  __syncthreads();
+  const int32_t bx0 = __builtin_amdgcn_readfirstlane(win_s[0]) - 1;
+  const int32_t by0 = __builtin_amdgcn_readfirstlane(win_s[1]) - 1;
+  const int32_t bw = __builtin_amdgcn_readfirstlane(win_s[2]) + 3 - bx0 + 1;
+  const int32_t bh = __builtin_amdgcn_readfirstlane(win_s[3]) + 3 - by0 + 1;
   const int32_t xa = bx0 >= 0 ? (bx0 & ~3) : -((-bx0 + 3) & ~3);  // window start, dword aligned
   const int nd = (bx0 - xa + bw + 3) >> 2;                         // source dwords per row
   const bool staged = bw > 0 && bh > 0 && 4 * nd <= kRFS && bh <= max_rows;
   uint64_t* nw = reinterpret_cast<uint64_t*>(winf + kRFS * max_rows);
-  const int lane = threadIdx.x & 63;
-  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* obuf = reinterpret_cast<uint8_t*>(nw + max_rows) + wu * (kRFH / kRFWaves * kRFW);
   if (staged && !UPH_DIAG_BITS(diag, 1024)) {
     // A wave-instruction stages three window rows, 8 bytes per lane: lanes
     // 18 q .. 18 q + 17 load row r + q (q < 3), lanes 54..63 idle.  nw[r] bit j:
-    // window bytes 8 j .. 8 j + 7 of row r hold a non-white pixel.  Interior
-    // tiles (the whole window inside the image) load straight; edge tiles
-    // load every dword clamped into the row, realign it by one 64-bit shift
-    // and make the bytes outside [0, W) x [0, H) white.
+    // window bytes 8 j .. 8 j + 7 of row r hold a non-white pixel.
     const int rq = (lane * 57) >> 10;  // lane / 18 for lane < 64
     const int jq = lane - 18 * rq;
     const int nq = (nd + 1) >> 1;
     const bool qv = rq < 3 && jq < nq;
     const int32_t xd = xa + 8 * jq;
+    // one wave-instruction's rows: ballot, non-white flags, fp32 window row
+    auto stage = [&](int rb, uint32_t w0, uint32_t w1) {
+      const int r = rb + rq;
+      const bool valid = qv && r < bh;
+      const unsigned long long m = __ballot(valid && (w0 & w1) != 0xFFFFFFFFu);
+      if (lane < 3 && rb + lane < bh) nw[rb + lane] = (m >> (18 * lane)) & 0x3FFFFull;
+      if (valid) {
+        float4* d = reinterpret_cast<float4*>(winf + r * kRFS + 8 * jq);
+        d[0] = make_float4(ubyte_f<0>(w0), ubyte_f<1>(w0), ubyte_f<2>(w0), ubyte_f<3>(w0));
+        d[1] = make_float4(ubyte_f<0>(w1), ubyte_f<1>(w1), ubyte_f<2>(w1), ubyte_f<3>(w1));
+      }
+    };
     const bool interior = xa >= 0 && xa + 8 * nq <= P.W && by0 >= 0 && by0 + bh <= P.H;
-    const int32_t xc0 = imin(imax(xd, 0), (int32_t)P.pitch - 4);
-    const int32_t xc1 = imin(imax(xd + 4, 0), (int32_t)P.pitch - 4);
-    const int fs0 = imin(imax(24 + 8 * (xd - xc0), 0), 56);
-    const int fs1 = imin(imax(24 + 8 * (xd + 4 - xc1), 0), 56);
-    uint32_t out0 = qv ? 0u : 0xFFFFFFFFu, out1 = out0;
+    if (interior) {
+      // the whole window inside the image: straight loads.  A lane's byte
+      // offset is its row-rq offset plus a scalar row product per group;
+      // lanes past the window's rows (and idle lanes) read their row rq.
+      const uint32_t off0 = row_off(by0 + rq, P.pitch) + (uint32_t)(qv ? xd : xa);
+      for (int rg = 3 * wu; rg < bh; rg += 3 * 3 * kRFWaves) {
+        uint2 v[3];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      if (xd + k < 0 || xd + k >= P.W) out0 |= 0xFFu << (8 * k);
-      if (xd + 4 + k < 0 || xd + 4 + k >= P.W) out1 |= 0xFFu << (8 * k);
-    }
-    const int32_t xi = interior && qv ? xd : (interior ? xa : 0);  // idle lanes stay in the row
-    for (int rg = 3 * wu; rg < bh; rg += 3 * 3 * kRFWaves) {
-      uint2 v[3];
+        for (int g = 0; g < 3; g++) {  // all loads of the group in flight
+          const int rb = rg + 3 * kRFWaves * g;
+          const uint32_t o = rb + rq < bh ? off0 + (uint32_t)rb * (uint32_t)P.pitch : off0;
+          v[g] = *reinterpret_cast<const uint2*>(sbase + o);
+        }
 #pragma unroll
-      for (int g = 0; g < 3; g++) {  // all loads of the group in flight
-        const int r = rg + 3 * kRFWaves * g + rq;
-        if (interior) {
-          const int32_t y = imin(by0 + r, P.H - 1);
-          v[g] = *reinterpret_cast<const uint2*>(sbase + row_off(y, P.pitch) + xi);
-        } else {
+        for (int g = 0; g < 3; g++) {
+          const int rb = rg + 3 * kRFWaves * g;  // the wave's first row of this instruction
+          if (rb >= bh) break;                   // uniform
+          stage(rb, v[g].x, v[g].y);
+        }
+      }
+    } else {
+      // edge tiles load every dword clamped into the row, realign it by one
+      // 64-bit shift and make the bytes outside [0, W) x [0, H) white
+      const int32_t xc0 = imin(imax(xd, 0), (int32_t)P.pitch - 4);
+      const int32_t xc1 = imin(imax(xd + 4, 0), (int32_t)P.pitch - 4);
+      const int fs0 = imin(imax(24 + 8 * (xd - xc0), 0), 56);
+      const int fs1 = imin(imax(24 + 8 * (xd + 4 - xc1), 0), 56);
+      uint32_t out0 = qv ? 0u : 0xFFFFFFFFu, out1 = out0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (xd + k < 0 || xd + k >= P.W) out0 |= 0xFFu << (8 * k);
+        if (xd + 4 + k < 0 || xd + 4 + k >= P.W) out1 |= 0xFFu << (8 * k);
+      }
+      for (int rg = 3 * wu; rg < bh; rg += 3 * 3 * kRFWaves) {
+        uint2 v[3];
+#pragma unroll
+        for (int g = 0; g < 3; g++) {
+          const int r = rg + 3 * kRFWaves * g + rq;
           const int32_t y = imin(imax(by0 + r, 0), P.H - 1);
           const uint8_t* row = sbase + row_off(y, P.pitch);
           v[g].x = *reinterpret_cast<const uint32_t*>(row + xc0);
           v[g].y = *reinterpret_cast<const uint32_t*>(row + xc1);
         }
-      }
 #pragma unroll
-      for (int g = 0; g < 3; g++) {
-        const int rb = rg + 3 * kRFWaves * g;  // the wave's first row of this instruction
-        if (rb >= bh) break;                   // uniform
-        const int r = rb + rq;
-        uint32_t w0 = v[g].x, w1 = v[g].y;
-        if (!interior) {
-          const int32_t y = by0 + r;
-          w0 = (uint32_t)(((uint64_t)w0 << 24) >> fs0) | out0;
-          w1 = (uint32_t)(((uint64_t)w1 << 24) >> fs1) | out1;
+        for (int g = 0; g < 3; g++) {
+          const int rb = rg + 3 * kRFWaves * g;
+          if (rb >= bh) break;
+          const int32_t y = by0 + rb + rq;
+          uint32_t w0 = (uint32_t)(((uint64_t)v[g].x << 24) >> fs0) | out0;
+          uint32_t w1 = (uint32_t)(((uint64_t)v[g].y << 24) >> fs1) | out1;
           if ((y < 0) | (y >= P.H)) w0 = w1 = 0xFFFFFFFFu;
-        }
-        const bool valid = qv && r < bh;
-        const unsigned long long m = __ballot(valid && (w0 & w1) != 0xFFFFFFFFu);
-        if (lane < 3 && rb + lane < bh) nw[rb + lane] = (m >> (18 * lane)) & 0x3FFFFull;
-        if (valid) {
-          float4* d = reinterpret_cast<float4*>(winf + r * kRFS + 8 * jq);
-          d[0] = make_float4(ubyte_f<0>(w0), ubyte_f<1>(w0), ubyte_f<2>(w0), ubyte_f<3>(w0));
-          d[1] = make_float4(ubyte_f<0>(w1), ubyte_f<1>(w1), ubyte_f<2>(w1), ubyte_f<3>(w1));
+          stage(rb, w0, w1);
         }
       }
     }
