@@ -1517,14 +1517,13 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
   typedef __attribute__((address_space(3))) float lds_f32;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_f32*)winf;  // LDS byte address of winf
   const Src<F_GRAY8> S{sbase, P.pitch, P.W, P.H};
-  // Source coordinates are monotone along a row, so the taps of all 128
+  // Source coordinates are monotone along a row, so the tap rows of all 128
   // columns of a tile row lie between those of its end columns (computed
   // with the same expressions, wave-uniform).  When every tap there is white
   // (255) the bicubic result is exactly 255: all differences are zero, so
   // each cubic_scale returns b + (+-0) = b.
   const float cuL = (tx0 - a.mask.x0) - tcx, cuR = (tx0 + kRFW - 1 - a.mask.x0) - tcx;
-  const float axL = scx + cuL * a.cosval, bsL = cuL * a.sinval;
-  const float axR = scx + cuR * a.cosval, bsR = cuR * a.sinval;
+  const float bsL = cuL * a.sinval, bsR = cuR * a.sinval;
   constexpr int kRows = kRFH / kRFWaves;            // rows per wave
   const int32_t yw = ty0 + wu * kRows;              // the wave's rows: yw .. yw + kRows-1
   // Outside the mask a pixel is copied unchanged (deskew.c:268-286).  Those
@@ -1558,20 +1557,18 @@ __global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRe
   uint32_t white_rows = 0;  // bit k: every tap of output row k is white
   if (staged) {
     // one pass: lane 8 k + j tests output row k against window rows
-    // r0 + j, r0 + j + 8, ... of the row's tap band (8-byte column granules)
+    // r0 + j, r0 + j + 8, ... of the row's tap band, over the whole window
+    // width (a row's taps span all but the ~(kRFH sin) columns of the
+    // window's slant, so a column restriction would rarely change a flag)
     const int k = lane >> 3, j = lane & 7;
     bool hit = false;
     if (k < kRows) {
       const float cv = (yw + k - a.mask.y0) - tcy;
-      const float VS = cv * a.sinval, VC = scy + cv * a.cosval;
-      const int32_t xl = (int)(axL + VS), xr = (int)(axR + VS);
+      const float VC = scy + cv * a.cosval;
       const int32_t yl = (int)(VC - bsL), yr = (int)(VC - bsR);
-      const int32_t c0 = imax((imin(xl, xr) - 1 - xa) >> 3, 0);
-      const int32_t c1 = imin((imax(xl, xr) + 2 - xa) >> 3, ((nd + 1) >> 1) - 1);
       const int32_t r0 = imax(imin(yl, yr) - 1 - by0, 0);
       const int32_t r1 = imin(imax(yl, yr) + 2 - by0, bh - 1);
-      const uint64_t cm = c1 >= c0 ? ((2ull << c1) - 1ull) & ~((1ull << c0) - 1ull) : 0ull;
-      for (int r = r0 + j; r <= r1; r += 8) hit |= (nw[r] & cm) != 0;
+      for (int r = r0 + j; r <= r1; r += 8) hit |= nw[r] != 0;
     }
     const uint64_t m = __ballot(hit);
 #pragma unroll
