@@ -609,9 +609,16 @@ static size_t pow2_at_least(size_t n) {
   return p;
 }
 
+// 32-pixel words per row of the GRAY8 dark bit-plane
+static int32_t noise_bit_words(const NoiseGeom& g) { return (g.W + 31) >> 5; }
+
 size_t noise_scratch_bytes(const NoiseGeom& g) {
-  // lists + a global sort buffer for the rare > 8192-trigger sequential case
-  return noise_list_bytes(g) + 4 * pow2_at_least((size_t)g.capacity);
+  // lists + a global sort buffer for the rare > 8192-trigger sequential case;
+  // the GRAY8 dark bit-plane shares the sort buffer's space (it is read by
+  // k_noise_classify only, before k_noise_resolve may sort)
+  const size_t sort = 4 * pow2_at_least((size_t)g.capacity);
+  const size_t bits = 4 * (size_t)noise_bit_words(g) * (size_t)g.H;
+  return noise_list_bytes(g) + (sort > bits ? sort : bits);
 }
 
 struct NoisePtrs {
@@ -712,6 +719,33 @@ __device__ __forceinline__ uint32_t lt_nibble(uint32_t x, uint32_t k) {
   return ~(ge | (ge >> 14)) & 0xFu;
 }
 
+// GRAY8 dark bit-plane: bit b of word w of row y is (pixel 32 w + b < white);
+// columns >= W are 0.  One lane per word, two 16-byte loads (rows are
+// 256-byte pitched, so a row's last word reads inside the pitch).  The
+// classify tiles then read 92-bit region rows as five words each instead of
+// re-reading and re-comparing 2x-overlapping byte halos.
+__global__ void __launch_bounds__(256) k_noise_bits(PlaneRef img, NoiseGeom g, uint32_t* bits,
+                                                    int64_t bstride, int32_t nwr, float rnwr,
+                                                    const int32_t* active) {
+  const int s = blockIdx.y;
+  if (active && !active[s]) return;
+  const int32_t t = blockIdx.x * 256 + threadIdx.x;
+  // t / nwr from the float reciprocal, corrected by one either way
+  int32_t y = (int32_t)((float)t * rnwr);
+  if (y * nwr > t) y--;
+  else if ((y + 1) * nwr <= t) y++;
+  if (y >= g.H) return;
+  const int32_t wi = t - y * nwr, x0 = 32 * wi;
+  const uint4* p = reinterpret_cast<const uint4*>(plane_ptr(img, s) + (int64_t)y * img.P.pitch + x0);
+  const uint4 a = p[0], b = p[1];
+  const uint32_t k = (256u - g.white) * 0x00010001u;
+  uint32_t m = lt_nibble(a.x, k) | lt_nibble(a.y, k) << 4 | lt_nibble(a.z, k) << 8 |
+               lt_nibble(a.w, k) << 12 | lt_nibble(b.x, k) << 16 | lt_nibble(b.y, k) << 20 |
+               lt_nibble(b.z, k) << 24 | lt_nibble(b.w, k) << 28;
+  if (x0 + 32 > g.W) m &= (1u << (g.W - x0)) - 1u;  // g.W - x0 in [1, 31]
+  bits[s * bstride + t] = m;
+}
+
 // Whether the classification of a small dark pixel (tile coordinates rx, ry)
 // must go to the sequential replay, or clears it in parallel (see above).
 struct SmallVerdict {
@@ -789,7 +823,8 @@ constexpr int kListCap = 1024;  // LDS work list of one tile (else: row loops)
 template <int FMT>
 __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGeom g, uint8_t* scratch,
                                                         int64_t sstride, const int32_t* active,
-                                                        SheetCtl* ctl) {
+                                                        SheetCtl* ctl, const uint32_t* bits,
+                                                        int64_t bstride) {
   // XCD-aware tile order: neighbouring tiles' halos are fetched into one L2
   int bxi, byi, s;
   xcd_block(&bxi, &byi, &s);
@@ -819,68 +854,37 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
   }
   for (int i = threadIdx.x; i < kRW * 4; i += 256) (&srow[0][0])[i] = 0;
   if constexpr (kGray) {
-    // Bit rows straight from 16-byte loads: each vector becomes 16 dark bits
-    // (SWAR compare), kept as 16-bit slots of the region row; a row is then
-    // realigned by the region's lead (ox mod 16) into drow.
-    constexpr int kLead = (16 - kHalo % 16) % 16;   // ox = 64*bx - kHalo = kLead (mod 16)
-    constexpr int kVec = (kLead + kRW + 15) / 16;   // 16-byte vectors per region row
-    static_assert(kVec <= 7, "region row exceeds 7 vectors");
-    constexpr int kItems = kRW * kVec;
-    __shared__ uint16_t m16[kRW][8];  // slots [kVec, 8) unused
-    const int64_t a0 = (int64_t)ox - kLead;
-    const uint32_t kadd = (256u - g.white) * 0x00010001u;
-    uint4 v[(kItems + 255) / 256];
-    bool ok[(kItems + 255) / 256];
-#pragma unroll
-    for (int k = 0; k < (kItems + 255) / 256; k++) {
-      const int i = threadIdx.x + k * 256;
-      const int ry = i / kVec, vi = i - ry * kVec;
-      const int32_t gy = oy + ry;
-      const int64_t off = a0 + 16 * vi;
-      ok[k] = i < kItems && gy >= 0 && gy < g.H && off >= 0 && off < g.W;
-      v[k] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-      if (ok[k]) v[k] = *reinterpret_cast<const uint4*>(base + (int64_t)gy * pitch + off);
-    }
-#pragma unroll
-    for (int k = 0; k < (kItems + 255) / 256; k++) {
-      const int i = threadIdx.x + k * 256;
-      const int ry = i / kVec, vi = i - ry * kVec;
-      if (i < kItems) {
-        uint32_t m = 0;
-        if (ok[k]) {
-          const int64_t off = a0 + 16 * vi;
-          m = lt_nibble(v[k].x, kadd) | (lt_nibble(v[k].y, kadd) << 4) |
-              (lt_nibble(v[k].z, kadd) << 8) | (lt_nibble(v[k].w, kadd) << 12);
-          if (off + 16 > g.W) m &= (1u << (g.W - off)) - 1u;  // columns >= W
-        }
-        m16[ry][vi] = (uint16_t)m;
-      }
-    }
-    __syncthreads();
+    // Region rows from the dark bit-plane (k_noise_bits): row ry is bits
+    // [ox, ox + kRW) of plane row oy + ry, five words realigned by ox mod 32;
+    // words outside the row or the image read as 0
+    bool dark_here = false;
     if (threadIdx.x < kRW) {
       const int ry = threadIdx.x;
-      const uint32_t* q = reinterpret_cast<const uint32_t*>(m16[ry]);
+      const int32_t gy = oy + ry;
+      const int32_t nwr = (g.W + 31) >> 5;
+      const int32_t wb = ox >> 5;  // floor(ox / 32) (arithmetic shift)
+      const int sh = ox & 31;
+      uint32_t q[4] = {0u, 0u, 0u, 0u};
+      if (gy >= 0 && gy < g.H) {
+        const uint32_t* row = bits + s * bstride + (int64_t)gy * nwr;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (wb + j >= 0 && wb + j < nwr) q[j] = row[wb + j];
+      }
       uint32_t d[4];
-      uint32_t qw[5];
 #pragma unroll
-      for (int j = 0; j < 5; j++) {  // slots >= kVec are never written: zero
-        qw[j] = 2 * j < kVec ? q[j] : 0u;
-        if (2 * j + 1 >= kVec) qw[j] &= 0xFFFFu;
-      }
+      for (int j = 0; j < 3; j++) d[j] = __builtin_amdgcn_alignbit(q[j + 1], q[j], sh);
+      d[2] &= (1u << (kRW - 64)) - 1u;  // region columns >= kRW
+      d[3] = 0u;
+      static_assert(kRW > 64 && kRW <= 96, "three words per region row");
 #pragma unroll
-      for (int j = 0; j < 4; j++)
-        d[j] = kLead ? __builtin_amdgcn_alignbit(qw[j + 1], qw[j], kLead) : qw[j];
-      // region columns >= kRW (the lead pulls up to kLead of them in)
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int lo = 32 * j;
-        if (lo + 32 > kRW) d[j] &= lo >= kRW ? 0u : ((1u << (kRW - lo)) - 1u);
-        drow[ry][j] = d[j];
-      }
+      for (int j = 0; j < 4; j++) drow[ry][j] = d[j];
       // interior columns [kHalo, kHalo + kNT) = bits 14..63 | 64..77
       const uint64_t lo64 = ((uint64_t)d[1] << 32) | d[0], hi64 = ((uint64_t)d[3] << 32) | d[2];
-      if (ry >= kHalo && ry < kHalo + kNT && ((lo64 >> kHalo) | (hi64 & 0x3FFFull))) any_dark = 1;
+      dark_here = ry >= kHalo && ry < kHalo + kNT && ((lo64 >> kHalo) | (hi64 & 0x3FFFull));
     }
+    __syncthreads();  // any_dark's reset (thread 0, above) lands first
+    if (dark_here) any_dark = 1;
   } else {
     // Stage the region rows into LDS with 16-byte loads, all issued before
     // any is consumed.  Rows start 256-byte aligned, so every vector lies
@@ -1522,7 +1526,19 @@ static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr
   dim3 grid((g.W + kNT - 1) / kNT, (g.H + kNT - 1) / kNT, count);
   NoiseGeom gd = g;
   gd.diag = diag_noise();
-  hipLaunchKernelGGL(k_noise_classify<FMT>, grid, dim3(256), 0, st, img, gd, scr, ss, active, ctl);
+  uint32_t* bits = nullptr;
+  int64_t bstride = 0;
+  if (FMT == F_GRAY8) {
+    // the dark bit-plane in the sort buffer's space (noise_scratch_bytes)
+    const int32_t nwr = noise_bit_words(g);
+    bits = sortbuf;
+    bstride = sort_stride;
+    const int64_t words = (int64_t)nwr * g.H;
+    hipLaunchKernelGGL(k_noise_bits, dim3((unsigned)((words + 255) / 256), count), dim3(256), 0, st,
+                       img, g, bits, bstride, nwr, 1.0f / (float)nwr, active);
+  }
+  hipLaunchKernelGGL(k_noise_classify<FMT>, grid, dim3(256), 0, st, img, gd, scr, ss, active, ctl,
+                     bits, bstride);
   hipLaunchKernelGGL(k_noise_apply<FMT>, dim3(64, count), dim3(256), 0, st, img, g, scr, ss,
                      active, ctl);
   constexpr size_t kResolveLds = 2 * sizeof(uint32_t) * kCompCap;  // 128 KiB
