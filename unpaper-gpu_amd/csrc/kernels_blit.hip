@@ -1351,7 +1351,7 @@ __device__ __forceinline__ uint32_t row_off(int32_t y, int64_t pitch) {
   return (uint32_t)y * (uint32_t)pitch;
 }
 
-__global__ void __launch_bounds__(kRFT) k_rotate_cubic_g8f(PlaneRef src, PlaneRef dst,
+__global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, PlaneRef dst,
                                                                const RotateArgs* args,
                                                                int max_rows, int diag,
                                                                uint32_t m_gxy, uint32_t m_gx) {
