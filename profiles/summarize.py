@@ -48,6 +48,10 @@ def last_dispatches(path, kernel, k):
         return [(e - s) / 1e3 for s, e in rows[-k:]]
     with open(found[0]) as f:
         rows = [r for r in csv.DictReader(f) if kernel in r.get("Kernel_Name", "")]
+    # full-batch launches only: bench.py's single-page latency runs (grid z =
+    # 1) come after its probes
+    zmax = max((int(r.get("Grid_Size_Z", 1)) for r in rows), default=1)
+    rows = [r for r in rows if int(r.get("Grid_Size_Z", 1)) == zmax]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     return [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows[-k:]]
 
