@@ -1286,13 +1286,16 @@ constexpr int kRFWaves = kRFT / 64;
 #define UPH_ROWOFF_2 146
 #define UPH_ROWOFF_3 147
 static_assert(kRFS == 144, "tap pair offsets are spelled out for a 144-float row stride");
+// Issued in pair order t[0], t[1] (pixel A), t[2], t[3] (pixel B) with no
+// wait: the caller waits for A's eight (lds_wait_a) and computes A's row
+// cubics while B's are still in flight (LDS returns in order).
 __device__ __forceinline__ void lds_taps16(const uint32_t (&a)[4], f2 (&t)[4][4]) {
   asm volatile(UPH_TAP_PAIR(0, 16, 0) UPH_TAP_PAIR(1, 16, 1) UPH_TAP_PAIR(2, 16, 2)
                UPH_TAP_PAIR(3, 16, 3) UPH_TAP_PAIR(4, 17, 0) UPH_TAP_PAIR(5, 17, 1)
                UPH_TAP_PAIR(6, 17, 2) UPH_TAP_PAIR(7, 17, 3) UPH_TAP_PAIR(8, 18, 0)
                UPH_TAP_PAIR(9, 18, 1) UPH_TAP_PAIR(10, 18, 2) UPH_TAP_PAIR(11, 18, 3)
                UPH_TAP_PAIR(12, 19, 0) UPH_TAP_PAIR(13, 19, 1) UPH_TAP_PAIR(14, 19, 2)
-               UPH_TAP_PAIR(15, 19, 3) "s_waitcnt lgkmcnt(0)"
+               UPH_TAP_PAIR(15, 19, 3)
                : "=&v"(t[0][0]), "=&v"(t[0][1]), "=&v"(t[0][2]), "=&v"(t[0][3]),
                  "=&v"(t[1][0]), "=&v"(t[1][1]), "=&v"(t[1][2]), "=&v"(t[1][3]),
                  "=&v"(t[2][0]), "=&v"(t[2][1]), "=&v"(t[2][2]), "=&v"(t[2][3]),
@@ -1300,42 +1303,53 @@ __device__ __forceinline__ void lds_taps16(const uint32_t (&a)[4], f2 (&t)[4][4]
                : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3])
                : "memory");
 }
+// Wait until <= N LDS operations are outstanding; the taps of pairs p0, p0+1
+// become defined here (no use of them can be scheduled above the wait).
+template <int N>
+__device__ __forceinline__ void lds_wait_pairs(f2 (&u)[4], f2 (&v)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(%8)"
+               : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(v[0]), "+v"(v[1]),
+                 "+v"(v[2]), "+v"(v[3])
+               : "n"(N)
+               : "memory");
+}
 
-// cubic2 on four independent pairs, step by step, so the dependent packed
-// operations of one chain interleave with the others' (no wait states).
-__device__ __forceinline__ void cubic2x4(const f2 (&f)[4], const f2 (&h)[4],
-                                         const f2 (&t)[4][4], f2 (&out)[4]) {
-  f2 ba[4], ca[4], da[4], s1[4], s2[4], u[4];
+// cubic2 on two independent pairs, step by step, so the dependent packed
+// operations of one chain interleave with the other's.
+__device__ __forceinline__ void cubic2x2(f2 f, f2 h, const f2 (&t0)[4], const f2 (&t1)[4],
+                                         f2& out0, f2& out1) {
+  const f2* t[2] = {t0, t1};
+  f2 ba[2], ca[2], da[2], s1[2], s2[2], u[2];
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
+  for (int i = 0; i < 2; i++) {
     ba[i] = t[i][1] - t[i][0];
     ca[i] = t[i][2] - t[i][0];
     da[i] = t[i][3] - t[i][0];
   }
 #pragma unroll
-  for (int i = 0; i < 4; i++) s1[i] = fma2(splat2(4.0f), ca[i], -da[i]);                // exact
+  for (int i = 0; i < 2; i++) s1[i] = fma2(splat2(4.0f), ca[i], -da[i]);                // exact
 #pragma unroll
-  for (int i = 0; i < 4; i++) s2[i] = ba[i] - ca[i];
+  for (int i = 0; i < 2; i++) s2[i] = ba[i] - ca[i];
 #pragma unroll
-  for (int i = 0; i < 4; i++) s1[i] = fma2(splat2(-5.0f), ba[i], s1[i]);                // exact
+  for (int i = 0; i < 2; i++) s1[i] = fma2(splat2(-5.0f), ba[i], s1[i]);                // exact
 #pragma unroll
-  for (int i = 0; i < 4; i++) s2[i] = fma2(splat2(3.0f), s2[i], da[i]);                 // exact
+  for (int i = 0; i < 2; i++) s2[i] = fma2(splat2(3.0f), s2[i], da[i]);                 // exact
 #pragma unroll
-  for (int i = 0; i < 4; i++) u[i] = f[i] * s2[i];
+  for (int i = 0; i < 2; i++) u[i] = f * s2[i];
 #pragma unroll
-  for (int i = 0; i < 4; i++) u[i] = s1[i] + u[i];
+  for (int i = 0; i < 2; i++) u[i] = s1[i] + u[i];
 #pragma unroll
-  for (int i = 0; i < 4; i++) u[i] = f[i] * u[i];
+  for (int i = 0; i < 2; i++) u[i] = f * u[i];
 #pragma unroll
-  for (int i = 0; i < 4; i++) u[i] = ca[i] + u[i];
+  for (int i = 0; i < 2; i++) u[i] = ca[i] + u[i];
 #pragma unroll
-  for (int i = 0; i < 4; i++) u[i] = h[i] * u[i];
+  for (int i = 0; i < 2; i++) u[i] = h * u[i];
 #pragma unroll
-  for (int i = 0; i < 4; i++) u[i] = t[i][1] + u[i];
-#pragma unroll
-  for (int i = 0; i < 4; i++)
-    out[i] = f2{__builtin_amdgcn_fmed3f(__builtin_truncf(u[i].x), 0.0f, 255.0f),
-                __builtin_amdgcn_fmed3f(__builtin_truncf(u[i].y), 0.0f, 255.0f)};
+  for (int i = 0; i < 2; i++) u[i] = t[i][1] + u[i];
+  out0 = f2{__builtin_amdgcn_fmed3f(__builtin_truncf(u[0].x), 0.0f, 255.0f),
+            __builtin_amdgcn_fmed3f(__builtin_truncf(u[0].y), 0.0f, 255.0f)};
+  out1 = f2{__builtin_amdgcn_fmed3f(__builtin_truncf(u[1].x), 0.0f, 255.0f),
+            __builtin_amdgcn_fmed3f(__builtin_truncf(u[1].y), 0.0f, 255.0f)};
 }
 
 // v from the lane given by the quad permutation CTRL (DPP quad_perm)
@@ -1613,12 +1627,14 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
       const uint32_t ta[4] = {pA, pA + 8 * kRFS, pB, pB + 8 * kRFS};
       f2 t[4][4];
       lds_taps16(ta, t);
-      // rows (0,1) and (2,3) of A, then of B: four packed row cubics
+      // rows (0,1) and (2,3) of A once its eight tap pairs are in, then of B
       const f2 FA = splat2(fxA), HA = splat2(0.5f * fxA);
       const f2 FB = splat2(fxB), HB = splat2(0.5f * fxB);
-      const f2 F[4] = {FA, FA, FB, FB}, Hh[4] = {HA, HA, HB, HB};
       f2 c[4];
-      cubic2x4(F, Hh, t, c);
+      lds_wait_pairs<8>(t[0], t[1]);
+      cubic2x2(FA, HA, t[0], t[1], c[0], c[1]);
+      lds_wait_pairs<0>(t[2], t[3]);
+      cubic2x2(FB, HB, t[2], t[3], c[2], c[3]);
       // the column cubic of A and B as one pair
       const f2 o = cubic2(f2{fyA, fyB}, f2{0.5f * fyA, 0.5f * fyB}, f2{c[0].x, c[2].x},
                           f2{c[0].y, c[2].y}, f2{c[1].x, c[3].x}, f2{c[1].y, c[3].y});
