@@ -1314,6 +1314,41 @@ __device__ __forceinline__ void lds_wait_pairs(f2 (&u)[4], f2 (&v)[4]) {
                : "memory");
 }
 
+// Wait until <= N LDS operations are outstanding: tap pair t becomes
+// defined here; `prev` (the previous pair's result) must be computed above
+// the wait, so each pair's arithmetic overlaps the later pairs' reads.
+template <int N>
+__device__ __forceinline__ void lds_wait_pair(f2 (&t)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(%4)"
+               : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3])
+               : "n"(N)
+               : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lds_wait_pair_after(f2 (&t)[4], f2& prev) {
+  asm volatile("s_waitcnt lgkmcnt(%5)"
+               : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(prev)
+               : "n"(N)
+               : "memory");
+}
+
+// one packed row cubic (rows 2q, 2q+1 of one pixel), clamped like cubic_scale
+__device__ __forceinline__ f2 cubic2_row(f2 f, f2 h, const f2 (&t)[4]) {
+  const f2 ba = t[1] - t[0], ca = t[2] - t[0], da = t[3] - t[0];
+  f2 s1 = fma2(splat2(4.0f), ca, -da);  // exact
+  f2 s2 = ba - ca;
+  s1 = fma2(splat2(-5.0f), ba, s1);     // exact
+  s2 = fma2(splat2(3.0f), s2, da);      // exact
+  f2 u = f * s2;
+  u = s1 + u;
+  u = f * u;
+  u = ca + u;
+  u = h * u;
+  u = t[1] + u;
+  return f2{__builtin_amdgcn_fmed3f(__builtin_truncf(u.x), 0.0f, 255.0f),
+            __builtin_amdgcn_fmed3f(__builtin_truncf(u.y), 0.0f, 255.0f)};
+}
+
 // cubic2 on two independent pairs, step by step, so the dependent packed
 // operations of one chain interleave with the other's.
 __device__ __forceinline__ void cubic2x2(f2 f, f2 h, const f2 (&t0)[4], const f2 (&t1)[4],
@@ -1631,10 +1666,14 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
       const f2 FA = splat2(fxA), HA = splat2(0.5f * fxA);
       const f2 FB = splat2(fxB), HB = splat2(0.5f * fxB);
       f2 c[4];
-      lds_wait_pairs<8>(t[0], t[1]);
-      cubic2x2(FA, HA, t[0], t[1], c[0], c[1]);
-      lds_wait_pairs<0>(t[2], t[3]);
-      cubic2x2(FB, HB, t[2], t[3], c[2], c[3]);
+      lds_wait_pair<12>(t[0]);
+      c[0] = cubic2_row(FA, HA, t[0]);
+      lds_wait_pair_after<8>(t[1], c[0]);
+      c[1] = cubic2_row(FA, HA, t[1]);
+      lds_wait_pair_after<4>(t[2], c[1]);
+      c[2] = cubic2_row(FB, HB, t[2]);
+      lds_wait_pair_after<0>(t[3], c[2]);
+      c[3] = cubic2_row(FB, HB, t[3]);
       // the column cubic of A and B as one pair
       const f2 o = cubic2(f2{fyA, fyB}, f2{0.5f * fyA, 0.5f * fyB}, f2{c[0].x, c[2].x},
                           f2{c[0].y, c[2].y}, f2{c[1].x, c[3].x}, f2{c[1].y, c[3].y});
