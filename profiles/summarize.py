@@ -2,7 +2,7 @@
 """Summarise a rocprofv3 --kernel-trace --stats CSV directory.
 
 usage: summarize.py <rocprofv3 output dir or *_kernel_stats.csv> [launches]
-                    [--last KERNEL K]
+                    [--last KERNEL K [--per-stage N]]
 
 Prints kernels by total time; with `launches` (batch launches in the traced
 run) also the per-launch average of each kernel and of the whole pipeline.
@@ -75,8 +75,15 @@ def main():
     if launches:
         print("pipeline kernels per batch launch: %.3f ms (input generation excluded)"
               % (total / 1e6 / launches))
+    per = 1  # dispatches per stage: the GRAY8 bicubic rotation is two launches
+    if "--per-stage" in argv:  # (sheets split by window size), summed per stage
+        per = int(argv[argv.index("--per-stage") + 1])
     if last and os.path.isdir(argv[0]):
-        d = last_dispatches(argv[0], *last)
+        d = last_dispatches(argv[0], last[0], last[1] * per)
+        if per > 1 and d:
+            print("last %d dispatches of %s: %s us" % (len(d), last[0], " ".join("%.1f" % v for v in d)))
+            d = [sum(d[i:i + per]) for i in range(0, len(d) - per + 1, per)]
+            last = ("%s (stage = %d launches)" % (last[0], per), last[1])
         if d:
             print("last %d dispatches of %s: %s us, average %.1f us"
                   % (len(d), last[0], " ".join("%.1f" % v for v in d), sum(d) / len(d)))
