@@ -1400,20 +1400,30 @@ __device__ __forceinline__ uint32_t row_off(int32_t y, int64_t pitch) {
   return (uint32_t)y * (uint32_t)pitch;
 }
 
+template <bool LOOP>
 __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, PlaneRef dst,
                                                                const RotateArgs* args,
-                                                               int max_rows, int diag,
-                                                               uint32_t m_gxy, uint32_t m_gx) {
+                                                               int max_rows, int cls_rows,
+                                                               int diag,
+                                                               uint32_t m_gxy, uint32_t m_gx,
+                                                               int loop_count, int tgx, int tgy) {
   // dynamic LDS: window [max_rows][kRFS] floats, nw[max_rows] u64, then one
   // (kRFH / 8) x kRFW byte output buffer per wave
   extern __shared__ __attribute__((aligned(16))) float winf[];
-  int txi, tyi, s;
-  xcd_block_m(m_gxy, m_gx, &txi, &tyi, &s);
+  __shared__ int32_t win_s[4];
+  // one tile (txi, tyi) of sheet s; every return is block-uniform
+  auto tile = [&](int txi, int tyi, int s) {
   // the plane selectors and the arguments are loaded together (one round trip)
   const uint8_t* sbase = plane_ptr(src, s);
   uint8_t* dbase = plane_ptr(dst, s);
   const RotateArgs a = args[s];
   if (!a.active) return;
+  if (cls_rows != 0) {
+    // two launches split the sheets by the window rows their angle needs
+    // (cls_rows > 0: at most cls_rows; < 0: more than -cls_rows)
+    const int need = kRFH + (int)ceilf((kRFW - 1) * fabsf(a.sinval)) + 5;
+    if (cls_rows > 0 ? need > cls_rows : need <= -cls_rows) return;
+  }
   const Planes& P = src.P;
   const Rect nm = normalize(a.mask);
   const int32_t sw = nm.x1 - nm.x0 + 1, sh = nm.y1 - nm.y0 + 1;
@@ -1447,7 +1457,6 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
   // per-tile constant: wave 0 evaluates the four corners in lanes (c = lane
   // & 3), reduces them across the quad and posts the bounds in LDS, instead
   // of every wave running the float chain of all four corners.
-  __shared__ int32_t win_s[4];
   if (wu == 0) {
     const int c = lane & 3;
     const int32_t u = c & 1 ? cu1 : cu0, v = c & 2 ? cv1 : cv0;
@@ -1715,6 +1724,35 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
       }
     }
   }
+  };
+  if constexpr (!LOOP) {  // one tile per block, XCD-aware order
+    int txi, tyi, s;
+    xcd_block_m(m_gxy, m_gx, &txi, &tyi, &s);
+    tile(txi, tyi, s);
+  } else {
+  // Persistent form for the large-window class, usually empty: the lanes of
+  // every wave test 64 sheets at once (the same ballot in every wave), and
+  // the block walks the tiles of the sheets that belong here.
+  for (int s0 = 0; s0 < loop_count; s0 += 64) {
+    const int l = threadIdx.x & 63;
+    bool want = false;
+    if (s0 + l < loop_count) {
+      const RotateArgs q = args[s0 + l];
+      want = q.active && kRFH + (int)ceilf((kRFW - 1) * fabsf(q.sinval)) + 5 > -cls_rows;
+    }
+    uint64_t m = __ballot(want);
+    m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m >> 32)) << 32) |
+        __builtin_amdgcn_readfirstlane((uint32_t)m);
+    while (m) {
+      const int s = s0 + __ffsll((long long)m) - 1;
+      m &= m - 1;
+      for (int t = blockIdx.x; t < tgx * tgy; t += gridDim.x) {
+        tile(t % tgx, t / tgx, s);
+        __syncthreads();  // the next tile restages the LDS window
+      }
+    }
+  }
+  }
 }
 
 // Rows of source window a kRFW x kRFH tile needs at rotations up to |angle|.
@@ -1731,13 +1769,31 @@ void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateAr
   const dim3 ggrid((src.P.W + kRotTW - 1) / kRotTW, (src.P.H + kRotGH - 1) / kRotGH, count);
   if (interp == UPHIP_INTERP_CUBIC && src.P.fmt == F_GRAY8) {
     const int rows = rotate_window_rows(max_abs_angle);
-    const size_t lds = (sizeof(float) * kRFS + sizeof(uint64_t)) * (size_t)rows + kRFH * kRFW;
-    if (lds <= 56 * 1024 && src.P.pitch * (int64_t)src.P.H < (1ll << 31) &&
+    auto lds_of = [](int r) {
+      return (sizeof(float) * kRFS + sizeof(uint64_t)) * (size_t)r + kRFH * kRFW;
+    };
+    // the most window rows that still let four tiles (32 waves) share a CU's
+    // 160 KB of LDS (16 B of static LDS per tile); windows of up to ~2.4 deg
+    const int rows4 = (int)((40 * 1024 - 16 - kRFH * kRFW) / (sizeof(float) * kRFS + sizeof(uint64_t)));
+    if (lds_of(rows) <= 56 * 1024 && src.P.pitch * (int64_t)src.P.H < (1ll << 31) &&
         !(diag_double() & 256)) {
       const dim3 fgrid((src.P.W + kRFW - 1) / kRFW, (src.P.H + kRFH - 1) / kRFH, count);
-      UPH_LAUNCH_DIAG(2, k_rotate_cubic_g8f, fgrid, dim3(kRFT), lds, st, src, dst, args, rows,
-                      diag_double() & (512 | 1024 | 2048), div_magic(fgrid.x * fgrid.y),
-                      div_magic(fgrid.x));
+      const uint32_t mgxy = div_magic(fgrid.x * fgrid.y), mgx = div_magic(fgrid.x);
+      const int dd = diag_double() & (512 | 1024 | 2048);
+      if (rows > rows4) {
+        // sheets whose angle fits the small window at four tiles per CU, then
+        // the others at the scan range's window (three per CU); every sheet
+        // is taken by exactly one of the two launches
+        // (the second as a persistent grid: when no sheet needs the large
+        // window its blocks only read the arguments)
+        UPH_LAUNCH_DIAG(2, k_rotate_cubic_g8f<false>, fgrid, dim3(kRFT), lds_of(rows4), st, src, dst, args,
+                        rows4, rows4, dd, mgxy, mgx, 0, 0, 0);
+        UPH_LAUNCH_DIAG(2, k_rotate_cubic_g8f<true>, dim3(3 * 256), dim3(kRFT), lds_of(rows), st, src, dst,
+                        args, rows, -rows4, dd, 0u, 0u, count, (int)fgrid.x, (int)fgrid.y);
+      } else {
+        UPH_LAUNCH_DIAG(2, k_rotate_cubic_g8f<false>, fgrid, dim3(kRFT), lds_of(rows), st, src, dst, args,
+                        rows, 0, dd, mgxy, mgx, 0, 0, 0);
+      }
       return;
     }
     const dim3 qgrid((src.P.W + kRQW - 1) / kRQW, (src.P.H + kRQH - 1) / kRQH, count);
