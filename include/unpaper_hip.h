@@ -282,6 +282,9 @@ int uphip_get_device(void);
 void *uphip_stream_acquire(void);
 void uphip_stream_release(void *stream);
 void uphip_set_current_stream(void *stream); /* TLS; NULL = per-thread default */
+/* Before destroying a stream of your own that was current for ops: waits for
+ * it and frees the op scratch the library keeps per stream. */
+void uphip_stream_forget(void *stream);
 void *uphip_get_current_stream(void);
 int uphip_synchronize(void);           /* current stream */
 /* Error reporting.  The reference's errOutput() exits (lib/logging.h); here a

@@ -1,14 +1,15 @@
 #!/usr/bin/env python3
 """Diagnostic: how many rotation-detection lines of synthetic A4 pages leave
-the shared-band path for the direct walk (UPHIP_DEBUG_ROTATION=1 makes the
-op-level detect_rotation print the count).  Needs a GPU."""
+the shared-band path for the direct walk (UPHIP_DIAG_ROTATION=1 makes the
+op-level detect_rotation print the count).  Needs a GPU and the tuning
+build (make lib DIAG=1; UNPAPER_HIP_LIB=unpaper-gpu_amd/lib_diag/libunpaper_hip.so)."""
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "unpaper-gpu_amd", "python"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
-os.environ["UPHIP_DEBUG_ROTATION"] = "1"
+os.environ["UPHIP_DIAG_ROTATION"] = "1"
 
 from oracle_py import Oracle  # noqa: E402
 from unpaper_hip import ctypes_abi as A  # noqa: E402

@@ -60,7 +60,10 @@ static void codec(const char *dir) {
   for (int y = 0; y < 5; y++)
     if (memcmp(back + 8 * y, img + 7 * y, 7)) g_fail++;
   static const char *bad[] = {"P5\n4 4\n255\n\x01", "P6 99999999999 1 255 ", "P2 2 2 255 1 2 x",
-                              "P1 9 1 1 0 1", "P4\n16 2\n\xff", "P3 1 1 255", "#", ""};
+                              "P1 9 1 1 0 1", "P4\n16 2\n\xff", "P3 1 1 255", "#", "",
+                              /* 2^31 does not fit int32_t; a raster past the size bound */
+                              "P5 2147483648 1 255 ", "P5 2147483647 1 255 ",
+                              "P6 1048576 1048576 255 "};
   for (size_t i = 0; i < sizeof bad / sizeof *bad; i++) {
     snprintf(path, sizeof path, "%s/b%zu.pnm", dir, i);
     FILE *f = fopen(path, "wb");
@@ -68,7 +71,10 @@ static void codec(const char *dir) {
     fclose(f);
     uint8_t buf[64];
     UphipPnmInfo want = {4, 4, UPHIP_FMT_GRAY8};
-    (void)uphip_pnm_probe(path, &info);
+    if (uphip_pnm_probe(path, &info) == 0 && (info.width <= 0 || info.height <= 0)) {
+      fprintf(stderr, "malformed file %zu probed as %dx%d\n", i, info.width, info.height);
+      g_fail++;
+    }
     if (uphip_pnm_read(path, buf, 16, &want) == 0) {
       fprintf(stderr, "malformed file %zu accepted\n", i);
       g_fail++;

@@ -4,7 +4,7 @@ the synthetic A4 pages the benchmark processes.
 
 TEST INFRASTRUCTURE: runs in the build container (oracle/_build/liboracle.so,
 the C restatement of the reference CPU path, pinned to the reference goldens by
-tests/test_oracle_golden.py).  The GPU side (tests/test_bench_config_gpu.py and
+tests/test_oracle_golden.py).  The GPU side (tests/test_runner_gpu.py, __graft_entry__.smoke() and
 bench.py's verification after the timed region) compares the HIP pipeline's
 outputs with these hashes, so the exact benchmarked configuration is
 parity-checked without running the oracle on the GPU box.

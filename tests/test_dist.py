@@ -98,7 +98,8 @@ def test_diag_guard():
 
 def test_product_library_has_no_diagnostics():
     """`make lib` builds without UPHIP_DIAG: the version string says so, and
-    the library does not read the UPHIP_DIAG_* variables at all."""
+    the library reads no diagnostics or debug variable at all (UPHIP_DIAG_*,
+    UPHIP_DEBUG_*): no hidden sync or host print in the product path."""
     sys.path.insert(0, os.path.join(ROOT, "unpaper-gpu_amd", "python"))
     from unpaper_hip.device import LIB_PATH, load_library
     L = load_library()
@@ -106,3 +107,4 @@ def test_product_library_has_no_diagnostics():
     with open(LIB_PATH, "rb") as f:
         blob = f.read()
     assert b"UPHIP_DIAG" not in blob
+    assert b"UPHIP_DEBUG" not in blob

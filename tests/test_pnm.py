@@ -106,3 +106,20 @@ def test_geometry_mismatch_and_missing_file(tmp_path):
         pnm_read(os.path.join(str(tmp_path), "missing.pgm"))
     with pytest.raises(UnpaperHipError, match="no direct PNM"):
         pnm_write(str(tmp_path / "q.pnm"), HostImage(4, 4, AB.FMT_Y400A))
+
+
+def test_sink_pattern_integer_conversion_only():
+    """the output pattern becomes a format string; reference-style
+    "%04d" patterns are accepted (rewritten for the 64-bit page number), and
+    anything but one integer conversion is refused at sink creation."""
+    from unpaper_hip.device import load_library
+    L = load_library()
+    for good in (b"out%04d.pbm", b"p_%lld.pgm", b"x%u_%%.ppm", b"plain.pgm", b"o%-3ld.pgm"):
+        h = L.uphip_sink_pnm(good, 0)
+        assert h, good
+        L.uphip_sink_destroy(h)
+    for bad in (b"out%s.pgm", b"o%n.pgm", b"%d_%d.pgm", b"o%f.pgm", b"trail%"):
+        L.uphip_clear_error()
+        assert not L.uphip_sink_pnm(bad, 0), bad
+        assert b"sink_pnm" in L.uphip_last_error()
+    L.uphip_clear_error()

@@ -166,7 +166,8 @@ float uphip_detect_rotation(UphipImage image0, UphipRectangle mask,
   std::vector<int32_t> hp(4 * (size_t)(na > 0 ? na : 1));
   UPH_HIP(hipMemcpyAsync(hp.data(), peaks, sizeof(int32_t) * g.nedges * na,
                          hipMemcpyDeviceToHost, st));
-  if (getenv("UPHIP_DEBUG_ROTATION")) {  // diagnostics: lines left to the direct walk
+#ifdef UPHIP_DIAG
+  if (getenv("UPHIP_DIAG_ROTATION")) {  // tuning build only: lines left to the direct walk
     std::vector<int32_t> fl((size_t)g.nedges * na);
     UPH_HIP(hipMemcpyAsync(fl.data(), rotation_line_flags(lines, g.nedges * na, max_scan),
                            sizeof(int32_t) * fl.size(), hipMemcpyDeviceToHost, st));
@@ -175,6 +176,7 @@ float uphip_detect_rotation(UphipImage image0, UphipRectangle mask,
     for (int32_t f : fl) nf += f != 0;
     fprintf(stderr, "uphip: detect_rotation %d of %d lines walked directly\n", nf, (int)fl.size());
   }
+#endif
   if (!UPH_HIP(hipStreamSynchronize(st))) return 0.0f;
   float rot[4];
   int count = 0, e = 0;

@@ -1064,7 +1064,8 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
       launch_rotation_peaks(cur_ref(P, b->ctl), rg, b->dtable, b->pick_mask, b->pick_active,
                             (int)i, b->peaks, count, b->st, b->table.nangles, b->max_scan,
                             b->rot_lines, b->max_angle);
-      if (getenv("UPHIP_DEBUG_ROTATION")) {  // diagnostics: lines left to the direct walk
+#ifdef UPHIP_DIAG
+      if (getenv("UPHIP_DIAG_ROTATION")) {  // tuning build only: lines left to the direct walk
         const int nl = count * rg.nedges * b->table.nangles;
         std::vector<int32_t> fl((size_t)nl);
         UPH_HIP(hipMemcpyAsync(fl.data(), rotation_line_flags(b->rot_lines, nl, b->max_scan),
@@ -1081,6 +1082,7 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
           }
         fprintf(stderr, "uphip: batch rotation %d of %d lines walked directly\n", nf, nl);
       }
+#endif
       ra.mask_index = (int)i;
       hipLaunchKernelGGL(k_rot_select, dim3((count + 255) / 256), dim3(256), 0, b->st, b->ctl,
                          b->peaks, b->dtable, b->dcombo, ra, b->rot_args, count);

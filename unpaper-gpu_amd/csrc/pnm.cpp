@@ -11,6 +11,7 @@
 // converted the sheet to the output format (saveImage's conversions,
 // file.c:187-254, run on the GPU in the batch's output stage).
 #include <cerrno>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -51,7 +52,7 @@ struct Reader {
     int64_t n = 0;
     while (c >= '0' && c <= '9') {
       n = n * 10 + (c - '0');
-      if (n > (1ll << 31)) return false;
+      if (n > INT32_MAX) return false;  // widths/heights are int32_t downstream
       c = get();
     }
     peekc = c;
@@ -59,6 +60,10 @@ struct Reader {
     return true;
   }
 };
+
+// 1 M pixels a side (2.3x a 600 dpi A0 sheet), 16 GiB of RGB24 raster
+constexpr int64_t kMaxSide = 1 << 20;
+constexpr int64_t kMaxRaster = 1ll << 34;
 
 struct Header {
   int kind = 0;  // 1..6
@@ -72,6 +77,9 @@ bool read_header(Reader& r, Header* hd, const char* path) {
   hd->kind = k - '0';
   if (!r.number(&hd->w) || !r.number(&hd->h) || hd->w <= 0 || hd->h <= 0)
     return fail("pnm: %s: bad size", path);
+  // callers size staging from the probe: bound each side and the raster
+  if (hd->w > kMaxSide || hd->h > kMaxSide || 3 * hd->w * hd->h > kMaxRaster)
+    return fail("pnm: %s: %lldx%lld is too large", path, (long long)hd->w, (long long)hd->h);
   if (hd->kind != 1 && hd->kind != 4) {
     if (!r.number(&hd->maxval) || hd->maxval <= 0)
       return fail("pnm: %s: bad maxval", path);

@@ -174,6 +174,46 @@ int pnm_load(const UphipSource* s, int64_t idx, void* dst, int64_t linesize,
   return uphip_pnm_read(s->paths[(size_t)idx].c_str(), dst, linesize, &geo);
 }
 
+// The reference names output files with sprintf(buf, pattern, outputNr++)
+// (image_pipeline.c:742): an int conversion such as "out%04d.pbm".  The
+// pattern becomes a format string here, so it may hold at most one integer
+// conversion (flags, width and precision kept, any length modifier replaced
+// by ll to match the int64_t page number) and "%%"; anything else (%s, %n,
+// a second conversion) is refused.
+bool output_pattern(const char* p, std::string* out) {
+  int nconv = 0;
+  out->clear();
+  for (const char* c = p; *c; c++) {
+    if (*c != '%') {
+      out->push_back(*c);
+      continue;
+    }
+    if (c[1] == '%') {
+      out->append("%%");
+      c++;
+      continue;
+    }
+    std::string spec = "%";
+    const char* q = c + 1;
+    while (*q && strchr("-+ #0", *q)) spec.push_back(*q++);
+    while (*q >= '0' && *q <= '9') spec.push_back(*q++);
+    if (*q == '.') {
+      spec.push_back(*q++);
+      while (*q >= '0' && *q <= '9') spec.push_back(*q++);
+    }
+    while (*q && strchr("hljzt", *q)) q++;  // length modifiers: replaced below
+    if (!*q || !strchr("diuoxX", *q))
+      return fail("sink_pnm: pattern \"%s\": only one integer conversion (%%d, %%05d, ...) "
+                  "is allowed", p);
+    if (++nconv > 1) return fail("sink_pnm: pattern \"%s\" has more than one conversion", p);
+    spec.append("ll");
+    spec.push_back(*q);
+    out->append(spec);
+    c = q;
+  }
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
@@ -226,8 +266,10 @@ UphipSink* uphip_sink_memory(void* base, int64_t linesize, int64_t sheet_stride,
 
 UphipSink* uphip_sink_pnm(const char* pattern, int64_t wrap) {
   if (!pattern) return fail("sink_pnm: null pattern"), nullptr;
+  std::string fmt;
+  if (!output_pattern(pattern, &fmt)) return nullptr;
   UphipSink* k = new UphipSink();
-  k->pattern = pattern;
+  k->pattern = fmt;
   k->wrap = wrap;
   return k;
 }
@@ -305,7 +347,11 @@ void store_sheet(UphipRunner* r, const UphipSink* k, int64_t job, const uint8_t*
     int64_t idx = job * oc + j;
     if (k->wrap > 0) idx %= k->wrap;
     char path[4096];
+    // the pattern holds at most one ll integer conversion (output_pattern)
+#pragma GCC diagnostic push
+#pragma GCC diagnostic ignored "-Wformat-nonliteral"
     snprintf(path, sizeof(path), k->pattern.c_str(), (long long)idx);
+#pragma GCC diagnostic pop
     const uint8_t* src = sheet;
     int64_t ls = r->out_linesize;
     const bool mono = r->out_fmt == UPHIP_FMT_MONOWHITE || r->out_fmt == UPHIP_FMT_MONOBLACK;
@@ -504,16 +550,27 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
   const int S = r->geo.capacity;
   const int nin = r->opts.input_count;
   if (!r->staged) {  // pinned staging per slot, laid out like the batch's input slots
+    const int caller_dev = uphip_get_device();
+    bool ok = true;
     for (DeviceCtx& dc : r->dev) {
       uphip_set_device(dc.device);
       for (Slot& sl : dc.slots) {
-        if (!UPH_HIP(hipHostMalloc((void**)&sl.hin, (size_t)(r->in_page_stride * S * nin),
-                                   hipHostMallocDefault)) ||
-            !UPH_HIP(hipHostMalloc((void**)&sl.hout, (size_t)(r->out_sheet_stride * S),
-                                   hipHostMallocDefault)))
-          return -1;
+        ok = ok && UPH_HIP(hipHostMalloc((void**)&sl.hin, (size_t)(r->in_page_stride * S * nin),
+                                         hipHostMallocDefault));
+        ok = ok && UPH_HIP(hipHostMalloc((void**)&sl.hout, (size_t)(r->out_sheet_stride * S),
+                                         hipHostMallocDefault));
       }
     }
+    if (!ok) {  // all or nothing: a later call allocates afresh
+      for (DeviceCtx& dc : r->dev)
+        for (Slot& sl : dc.slots) {
+          if (sl.hin) hipHostFree(sl.hin);
+          if (sl.hout) hipHostFree(sl.hout);
+          sl.hin = sl.hout = nullptr;
+        }
+    }
+    uphip_set_device(caller_dev);
+    if (!ok) return -1;
     r->staged = true;
   }
   const auto t0 = Clock::now();

@@ -48,8 +48,13 @@ struct PerThreadDevice {
 // switches streams per job (lib/batch_worker.c:197-202) must not hand the
 // next job's kernels a buffer the previous job's kernels, still queued on
 // another stream, are reading.  Everything on one stream is ordered, so
-// per-stream buffers need no further fencing.
+// per-stream buffers need no further fencing.  As with the reference's TLS
+// stream, one stream is current on one thread at a time (two threads issuing
+// ops on one stream would share its scratch); resizes hold the entry's lock.
+// uphip_stream_forget frees a caller-owned stream's entry before the caller
+// destroys the stream (a recycled handle then starts empty).
 struct StreamScratch {
+  std::mutex mu;
   void* scr[8] = {};
   size_t scr_bytes[8] = {};
 };
@@ -191,6 +196,7 @@ void* scratch(int slot, size_t bytes) {
     ps = e;
   }
   StreamScratch& p = *ps;
+  std::lock_guard<std::mutex> lk(p.mu);
   if (p.scr_bytes[slot] < bytes) {
     hipSetDevice(dev);
     if (p.scr[slot]) {
@@ -312,6 +318,25 @@ void uphip_stream_release(void* stream) {
   if (!stream) return;
   std::lock_guard<std::mutex> lk(g_pool_mu);
   g_pool_free[current_device()].push_back((hipStream_t)stream);
+}
+
+void uphip_stream_forget(void* stream) {
+  if (!stream) return;
+  const int dev = current_device();
+  StreamScratch* e = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_scr_mu);
+    auto it = g_scr.find({dev, (hipStream_t)stream});
+    if (it == g_scr.end()) return;
+    e = it->second;
+    g_scr.erase(it);
+  }
+  hipSetDevice(dev);
+  hipStreamSynchronize((hipStream_t)stream);  // its kernels were the only readers
+  for (void* q : e->scr)
+    if (q) hipFree(q);
+  delete e;
+  if (t_stream == (hipStream_t)stream) t_stream = nullptr;
 }
 
 void uphip_set_current_stream(void* stream) { t_stream = (hipStream_t)stream; }

@@ -32,7 +32,8 @@ EXPORTED = [
     "uphip_grayfilter", "uphip_detect_rotation", "uphip_deskew", "uphip_backend",
     "uphip_try_init", "uphip_init_status_string", "uphip_device_count", "uphip_set_device",
     "uphip_get_device", "uphip_stream_acquire", "uphip_stream_release",
-    "uphip_set_current_stream", "uphip_get_current_stream", "uphip_synchronize",
+    "uphip_set_current_stream", "uphip_stream_forget", "uphip_get_current_stream",
+    "uphip_synchronize",
     "uphip_last_error", "uphip_clear_error", "uphip_set_fatal_errors", "uphip_version",
     "uphip_abi_sizeof", "uphip_abi_offsetof",
     "uphip_options_init", "uphip_batch_create", "uphip_batch_destroy",
@@ -109,6 +110,7 @@ def load_library(path=LIB_PATH):
         "uphip_set_device": (C.c_int, [C.c_int]),
         "uphip_get_device": (C.c_int, []),
         "uphip_synchronize": (C.c_int, []),
+        "uphip_stream_forget": (None, [C.c_void_p]),
         "uphip_last_error": (C.c_char_p, []),
         "uphip_clear_error": (None, []),
         "uphip_set_fatal_errors": (None, [C.c_bool]),
