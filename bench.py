@@ -30,7 +30,10 @@ Extra fields: `roofline` for the dominant kernel (the bicubic rotation),
 timed with the HIP events its batch records on its own stream around the
 launch; `cpu_baseline` = the oracle's restatement of the reference CPU path
 on the host share of cores (rank 0, N=1 only); `latency_c2` = one A4 page
-alone through the pipeline; `host_io` = figures 2 and 3.
+alone through the pipeline; `host_io` = figures 2 and 3; `c4` = BASELINE
+configs[3] (16 RGB24 600 dpi double-page sheets, 4 per batch, 3 timed passes)
+with its sheets/s, latency, bilinear-rotate roofline and every sheet checked
+against tests/golden/c4_hashes.json (N=1 only; `--config c4` prints it alone).
 """
 import argparse
 import ctypes as C
@@ -100,6 +103,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-host-io", action="store_true", help="skip figures 2 and 3")
     ap.add_argument("--no-latency", action="store_true", help="skip the C2 single-page latency")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="skip the C4 object of the default line (16 RGB24 sheets, verified)")
     ap.add_argument("--host-batch", type=int, default=32, help="sheets per batch, host-fed runs")
     ap.add_argument("--host-streams", type=int, default=8, help="batches per device, host-fed")
     ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu.json"),
@@ -391,11 +396,16 @@ def host_threads_share():
         return os.cpu_count() or 1
 
 
-def run_c4(args, L, d, devices, firsts, n_gpus, version, valid):
+def run_c4(args, L, d, devices, firsts, n_gpus, version, valid, nsheets=0, steps=0, warmup=-1,
+           batch=0):
     """BASELINE configs[3]: RGB24 600dpi double-page sheets, layout double,
-    bilinear deskew, border wipe; sheets/s and single-sheet latency."""
-    nsheets = args.pages or 16
-    bsz = max(1, min(args.batch or 4, nsheets))
+    bilinear deskew, border wipe; sheets/s and single-sheet latency.  Returns
+    the C4 line (printed by `--config c4`, embedded as "c4" in the default
+    line); every resident output sheet is checked against c4_hashes.json."""
+    nsheets = nsheets or args.pages or 16
+    steps = steps or args.steps
+    warmup = args.warmup if warmup < 0 else warmup
+    bsz = max(1, min(batch or args.batch or 4, nsheets))
     opts = A.Options()
     L.uphip_options_init(C.byref(opts))
     c4_options(opts)
@@ -409,12 +419,12 @@ def run_c4(args, L, d, devices, firsts, n_gpus, version, valid):
     r = Runner(opts, bsz, C4_W, C4_H, A.FMT_RGB24, devices=devices[:1], streams=streams,
                timing=True)
     shard = [(pages.ptr, pitch, stride, nsheets)]
-    if args.warmup:
-        r.run_device(shard, passes=args.warmup)
+    if warmup:
+        r.run_device(shard, passes=warmup)
     stage_totals(r, 1)
     d.barrier()
     t0 = time.perf_counter()
-    failed, err = r.run_device(shard, passes=args.steps)
+    failed, err = r.run_device(shard, passes=steps)
     d.barrier()
     elapsed = d.max(time.perf_counter() - t0)
     if failed:
@@ -444,15 +454,14 @@ def run_c4(args, L, d, devices, firsts, n_gpus, version, valid):
     pages.close()
     alg_sheet = 10 * C4_W * C4_H * 3
     rot_alg = 2 * C4_W * C4_H * 3
-    sheets_s = nsheets * args.steps * n_gpus / elapsed
+    sheets_s = nsheets * steps * n_gpus / elapsed
     rot_ms = statistics.median(rot) if rot else 0.0
     ach = rot_alg / (rot_ms * 1e-3) / 1e9 if rot_ms else None
-    if d.rank == 0:
-        print(json.dumps({
+    line = {
             "metric": "sheets/s and per-sheet latency, RGB24 600dpi double-page scan (C4)",
             "value": round(sheets_s, 3), "unit": "sheets/s", "n_gpus": n_gpus,
-            "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+            "steps": steps, "warmup": warmup,
+            "ms_per_step": round(elapsed / steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "latency_ms": round(statistics.median(lat), 2),
             "latency_stages_ms": {k: round(v, 3) for k, v in lat_stages.items()},
@@ -468,11 +477,14 @@ def run_c4(args, L, d, devices, firsts, n_gpus, version, valid):
                          "pipeline_alg_bytes_per_sheet": alg_sheet,
                          "pipeline_frac": round(sheets_s / n_gpus * alg_sheet /
                                                 (HBM_PEAK_GBS * 1e9), 5)},
-            "stages_ms_per_step": {k: round(v / args.steps, 2) for k, v in totals.items()},
+            "stages_ms_per_step": {k: round(v / steps, 2) for k, v in totals.items()},
             "verified": checked, "mismatches": bad, "library": version, "valid": valid,
-        }), flush=True)
+    }
     if bad:
+        if d.rank == 0:
+            print(json.dumps(line), flush=True)
         raise SystemExit("bench.py: %d C4 sheets differ from the oracle" % bad)
+    return line
 
 
 def main():
@@ -493,7 +505,10 @@ def main():
     npages = args.pages or (16 if args.config == "c4" else 1000)
     devices, firsts, n_gpus = shard_plan(d.world, d.rank, d.local_rank, args.gpus, ndev, npages)
     if args.config == "c4":
-        return run_c4(args, L, d, devices, firsts, n_gpus, version, valid)
+        line = run_c4(args, L, d, devices, firsts, n_gpus, version, valid)
+        if d.rank == 0:
+            print(json.dumps(line), flush=True)
+        return
 
     bsz = max(1, min(args.batch or 64, npages))
     pitch = (W + 255) // 256 * 256
@@ -570,6 +585,13 @@ def main():
     runner.close()
 
     single = d.world == 1 and len(devices) == 1
+    c4 = None
+    if single and not args.no_c4:
+        # BASELINE configs[3] measured and verified in every default run: the
+        # 16-sheet C4 workload, 1 warm-up + 3 timed passes
+        c4 = run_c4(args, L, d, devices, [0], 1, version, valid, nsheets=16, steps=3, warmup=1,
+                    batch=4)
+        L.uphip_set_device(devices[0])
     threads = args.cpu_threads or host_threads_share()
     latency = hio = cpu = None
     host_pages = None
@@ -609,6 +631,7 @@ def main():
                                        "one runner thread per device, pages sharded")
                        + ", no collective"},
             "roofline": roofline, "cpu_baseline": cpu, "latency_c2": latency, "host_io": hio,
+            "c4": c4,
             "verified": checked, "mismatches": bad, "library": version, "valid": valid,
         }
         print(json.dumps(out), flush=True)

@@ -430,3 +430,62 @@ def test_center_move_border_counts(hip, oracle):
     opts.wipes.count = 1
     opts.wipes.areas[0] = A.rect(5, 5, 40, 60)
     check(oracle, opts, sheets, "center + wipe + border")
+
+
+# ---------------------------------------------------------------------------
+# the two-launch GRAY8 bicubic rotation (kernels_blit.hip launch_rotate_mask)
+# ---------------------------------------------------------------------------
+def skewed_page(w, h, deg, seed):
+    """White page, a block of 3x3-cell text lines rotated by `deg` degrees
+    about the centre (nearest neighbour), so rotation detection finds about
+    `deg` and the deskew rotates by it."""
+    import math
+    rng = np.random.default_rng(seed)
+    cw, ch = int(w * 0.7), int(h * 0.7)
+    g = np.full((ch, cw), 255, np.uint8)
+    for y in range(0, ch - 10, 20):
+        cells = rng.random((3, cw // 3)) < 0.4
+        vals = rng.integers(0, 41, size=cells.shape)
+        blk = np.where(cells, vals, 255).astype(np.uint8)
+        g[y:y + 9, :cells.shape[1] * 3] = np.repeat(np.repeat(blk, 3, 0), 3, 1)
+    out = np.full((h, w), 255, np.uint8)
+    t = math.radians(deg)
+    yy, xx = np.mgrid[0:h, 0:w]
+    dx, dy = xx - w / 2, yy - h / 2
+    u = (math.cos(t) * dx + math.sin(t) * dy + cw / 2).astype(np.int64)
+    v = (-math.sin(t) * dx + math.cos(t) * dy + ch / 2).astype(np.int64)
+    ok = (u >= 0) & (u < cw) & (v >= 0) & (v < ch)
+    out[ok] = g[v[ok], u[ok]]
+    return out
+
+
+def test_rotate_window_classes_batch(hip, oracle):
+    """one batch of 70 sheets (more than the persistent launch's
+    64-sheet ballot) whose angles fall on both sides of the small-window
+    bound (59 window rows: |angle| <= ~2.7 deg at 128-column tiles), mixed
+    with blank sheets (no rotation) -- both launches take sheets, the
+    large-window one through its ballot/ffs sheet walk over two 64-sheet
+    groups.  Every sheet and detected angle against the oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+    opts = oracle.default_options()
+    w, h = 400, 560
+    degs = [1.0, 2.6, 2.8, 4.9, -4.9, -2.75, None, 2.65, -1.2, 3.9]
+    sheets = []
+    for i in range(70):
+        d = degs[i % len(degs)]
+        a = np.full((h, w), 255, np.uint8) if d is None else skewed_page(w, h, d, i)
+        sheets.append([HostImage.from_array(a, A.FMT_GRAY8)])
+    outs, reps = gpu_sheets(opts, sheets)
+    with ThreadPoolExecutor(8) as ex:
+        exps = list(ex.map(lambda p: oracle_sheet(oracle, opts, p), sheets))
+    large = small = 0
+    for s, (exp, erep) in enumerate(exps):
+        assert_same(outs[s], exp, "rotate class sheet %d" % s)
+        assert np.float32(reps[s].rotation[0]).tobytes() == \
+            np.float32(erep.rotation[0]).tobytes(), "rotation of sheet %d" % s
+        r = abs(float(erep.rotation[0]))
+        if r:
+            need = 48 + int(np.ceil(127 * np.sin(np.float32(r)))) + 5
+            large += need > 59
+            small += need <= 59
+    assert large >= 20 and small >= 20, (large, small)

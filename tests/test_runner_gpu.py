@@ -43,7 +43,7 @@ def _bench(*extra, timeout=300):
         if k.startswith("UPHIP_DIAG"):
             del env[k]
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-host-io",
-           "--no-latency", "--probe", "0"] + list(extra)
+           "--no-latency", "--no-c4", "--probe", "0"] + list(extra)
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, p.stderr[-3000:]
     return json.loads(p.stdout.strip().splitlines()[-1])
@@ -208,6 +208,45 @@ def test_runner_two_threads_one_device(hip, oracle):
         r.close()
         for b in bufs:
             b.close()
+
+
+def test_runner_four_device_threads_host_fed(hip, tmp_path):
+    """Multi-GPU readiness on one GPU: run_host with four device
+    threads (devices=(0,0,0,0)) pulling 2-sheet chunks from the one shared job
+    counter (the BatchQueue peer, batch_worker.c:174-263), PGM files in and
+    out, one job whose file is missing.  The failed job is isolated, every
+    other output file is named by its job index and equals the oracle's hash
+    of that A4 page, and the per-device counters add up."""
+    hashes = json.load(open(os.path.join(GOLDEN, "bench_hashes.json")))["pages"]
+    from unpaper_hip.workloads import A4_H, A4_W
+    import ctypes as C
+    L = hip.lib
+    opts = A.Options()
+    L.uphip_options_init(C.byref(opts))
+    n, bad = 22, 13
+    paths = []
+    for p in range(n):
+        q = str(tmp_path / ("in_%02d.pgm" % p))
+        if p != bad:
+            pnm_write(q, HostImage.from_array(synth_page_host(A4_W, A4_H, p), A.FMT_GRAY8))
+        paths.append(q)
+    r = Runner(opts, 2, A4_W, A4_H, A.FMT_GRAY8, devices=(0, 0, 0, 0), streams=2, host_threads=8)
+    try:
+        failed, err = r.run_host(n, source_pnm(paths), sink_pnm(str(tmp_path / "out_%03d.pgm")))
+        st = r.stats()
+    finally:
+        r.close()
+    assert failed == 1 and "could not be loaded" in err
+    assert st.jobs_done == n - 1 and st.jobs_failed == 1
+    per = [st.jobs_per_device[i] for i in range(4)]
+    assert sum(per) == n - 1 and sum(1 for v in per if v) >= 2, per
+    assert not os.path.exists(str(tmp_path / ("out_%03d.pgm" % bad)))
+    for p in range(n):
+        if p == bad:
+            continue
+        got = pnm_read(str(tmp_path / ("out_%03d.pgm" % p)))
+        assert (got.width, got.height, got.format) == (A4_W, A4_H, A.FMT_GRAY8)
+        assert hashlib.sha256(got.payload().tobytes()).hexdigest() == hashes[str(p)], p
 
 
 def test_output_right_after_run_monowhite(hip, oracle):
