@@ -73,10 +73,38 @@ void launch_stretch(const PlaneRef& src, const PlaneRef& dst, int interp, int co
                     hipStream_t st);
 void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* args,
                       int count, hipStream_t st);
+// Work folded into a gray move (k_move_rect_g16), each optional:
+//  * masks: apply_masks with masks[s].m[0] (one mask) right before the move
+//    (sheet_stages.c:478-488: apply_masks, then align_mask); a sheet whose
+//    move is the identity is masked in place;
+//  * rows: per row y, the number of pixels <= thr in columns [rx0, rx1] of
+//    the sheet's resulting plane (moved, or the current one when the move is
+//    the identity) at rows[s * rows_stride + y] -- detect_border's row sums
+//    (masks.c:410-449), no other pass over the plane.
+struct MoveExtra {
+  const MaskArgs* masks;
+  uint32_t* rows;
+  int64_t rows_stride;
+  int32_t rx0, rx1;
+  uint8_t thr;
+};
+// Returns false (nothing launched) unless the plane is GRAY8.
+bool launch_move_rect_fused(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* args,
+                            const MoveExtra& x, int count, hipStream_t st);
 // max_abs_angle bounds |rotation| of every active sheet (sizes the staged
 // source window; tiles whose window does not fit take a slower exact path).
 void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
                         int interp, int count, hipStream_t st, float max_abs_angle);
+// Bilinear rotation (kernels_rotlin.hip), GRAY8 and RGB24: up to two masks
+// per sheet, args[m * mstride + s]; mask m >= 1 only where indep[s] (or
+// indep == null).  Sheets with no active mask are left alone (not flipped).
+// Returns false (nothing launched) for other formats.
+struct LinWindow {
+  int32_t cols, rows, stride;  // staged source window bound (floats) per tile
+};
+bool launch_rotate_linear(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
+                          int nmask, int64_t mstride, const int32_t* indep, int count,
+                          hipStream_t st, float max_abs_angle);
 // Flip `cur` of every sheet whose args[s].active (int at byte offset) is set.
 void launch_flip_if_active(SheetCtl* ctl, const int32_t* active, int64_t stride_bytes,
                            int count, hipStream_t st);

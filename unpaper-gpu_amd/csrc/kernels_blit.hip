@@ -5,6 +5,8 @@
 // one thread, so mono (1 bit per pixel) targets need no atomics (a thread owns
 // a whole byte = 8 pixels).  Rows start 256-byte aligned, so the interior of a
 // row is written with 16-byte stores.
+#include <climits>
+
 #include "interp.h"
 #include "kernels.h"
 
@@ -521,61 +523,157 @@ __device__ __forceinline__ uint4 shift_bytes16(const uint32_t* w, int r) {
 }
 
 constexpr int kMoveRows = 8;  // rows per wave of k_move_rect_g16
-static_assert(6 * kMoveRows * (kThreads / 64) <= kThreads, "one lane per deferred (row, vector)");
+constexpr int kMoveBp = 7;    // column breakpoints: five of the move, two of a folded mask
+constexpr int kMoveBlockRows = kMoveRows * (kThreads / 64);
+static_assert((kMoveBp + 1) * kMoveBlockRows <= kThreads, "one lane per deferred (row, vector)");
 
+// bytes <= thr among four (kadd = (256 - (thr + 1)) * 0x00010001), keeping
+// the bytes whose bit is set in `keep4` (bits 0..3 = bytes 0..3)
+__device__ __forceinline__ uint32_t dark4(uint32_t x, uint32_t kadd, uint32_t keep4) {
+  const uint32_t lo = ((x & 0x00FF00FFu) + kadd) & 0x01000100u;  // bytes 0, 2 > thr: bits 8, 24
+  const uint32_t hi = (((x >> 8) & 0x00FF00FFu) + kadd) & 0x01000100u;  // bytes 1, 3
+  const uint32_t kb = ((keep4 & 1u) << 8) | ((keep4 & 2u) << 8) | ((keep4 & 4u) << 22) |
+                      ((keep4 & 8u) << 22);  // keep bits at 8, 9, 24, 25
+  return __popc(kb) - __popc((lo | (hi << 1)) & kb);
+}
+// dark bytes of a 16-byte vector, bytes selected by a 16-bit mask
+__device__ __forceinline__ uint32_t dark16(const uint4& v, uint32_t m16, uint32_t kadd) {
+  return dark4(v.x, kadd, m16 & 15u) + dark4(v.y, kadd, (m16 >> 4) & 15u) +
+         dark4(v.z, kadd, (m16 >> 8) & 15u) + dark4(v.w, kadd, m16 >> 12);
+}
+// 16-bit mask of the columns x0 .. x0+15 inside [c0, c1]
+__device__ __forceinline__ uint32_t cols16(int32_t x0, int32_t c0, int32_t c1) {
+  const int32_t lo = imax(c0 - x0, 0), hi = imin(c1 - x0, 15);
+  return lo > hi ? 0u : ((2u << hi) - 1u) & ~((1u << lo) - 1u);
+}
+// byte mask of the four bits b (bit j -> byte j)
+__device__ __forceinline__ uint32_t bytes_of4(uint32_t b) {
+  return ((b * 0x00204081u) & 0x01010101u) * 0xFFu;
+}
+
+template <int MODE>
 __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneRef dst,
-                                                            const MoveArgs* args) {
+                                                            const MoveArgs* args, MoveExtra X) {
+  constexpr bool kMask = (MODE & 1) != 0, kRows = (MODE & 2) != 0;
   const int s = blockIdx.z;
   const MoveArgs a = args[s];
-  if (!a.active) return;
+  if (!kMask && !kRows && !a.active) return;
   const Planes& P = src.P;
   const uint8_t* sbase = plane_ptr(src, s);
   uint8_t* dbase = plane_ptr(dst, s);
+  const int lane = threadIdx.x & 63;
+  const int32_t nv = (P.W + 15) >> 4;                  // vectors per row (inside the pitch)
+  const int32_t yb = blockIdx.x * kMoveBlockRows;       // the block's first row
+  const int32_t y0 = yb + (threadIdx.x >> 6) * kMoveRows;
+  const int32_t y1 = imin(y0 + kMoveRows, P.H);
+  // folded apply_masks (one mask, masks.c:306-322 semantics: normalized,
+  // pixels outside it <- colour)
+  Rect mk{INT_MIN / 2, INT_MIN / 2, INT_MAX / 2, INT_MAX / 2};
+  uint8_t mcol = 0;
+  if (kMask) {
+    const MaskArgs* ma = X.masks + s;
+    if (ma->n > 0) mk = normalize(ma->m[0]);
+    mcol = gray_of(Px{ma->color[0], ma->color[1], ma->color[2]});
+  }
+  const uint32_t mcol4 = mcol * 0x01010101u;
+  const uint32_t kadd = (256u - ((uint32_t)X.thr + 1u)) * 0x00010001u;
+  __shared__ uint32_t rowcnt[kMoveBlockRows];
+  if (kRows) {
+    if (threadIdx.x < kMoveBlockRows) rowcnt[threadIdx.x] = 0;
+    __syncthreads();
+  }
+  uint32_t acc[kMoveRows];
+#pragma unroll
+  for (int k = 0; k < kMoveRows; k++) acc[k] = 0;
+  auto finish_rows = [&]() {
+    if (!kRows) return;
+#pragma unroll
+    for (int k = 0; k < kMoveRows; k++) {
+      uint32_t v = acc[k];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == 0 && v) atomicAdd(&rowcnt[y0 - yb + k], v);
+    }
+    __syncthreads();
+    const int32_t y = yb + (int32_t)threadIdx.x;
+    if (threadIdx.x < kMoveBlockRows && y < P.H) X.rows[(int64_t)s * X.rows_stride + y] = rowcnt[threadIdx.x];
+  };
+  if (!a.active) {
+    // the identity move: mask the current plane in place and/or count it
+    for (int32_t vi = lane; vi < nv; vi += 64) {
+      const int32_t x0 = 16 * vi;
+      const uint32_t valid = cols16(x0, 0, P.W - 1);
+      const uint32_t incol = cols16(x0, mk.x0, mk.x1) & valid;
+      const uint32_t reg = kRows ? cols16(x0, X.rx0, X.rx1) : 0u;
+#pragma unroll
+      for (int k = 0; k < kMoveRows; k++) {
+        const int32_t y = y0 + k;
+        if (y >= y1) break;
+        uint8_t* row = const_cast<uint8_t*>(sbase) + (int64_t)y * P.pitch;
+        const uint32_t out16 = kMask ? valid & ~((y >= mk.y0 && y <= mk.y1) ? incol : 0u) : 0u;
+        uint4 v = make_uint4(mcol4, mcol4, mcol4, mcol4);
+        if ((kRows && reg) || out16 != valid || valid != 0xFFFFu)
+          v = *reinterpret_cast<const uint4*>(row + x0);
+        if (out16) {
+          v.x = (v.x & ~bytes_of4(out16 & 15u)) | (mcol4 & bytes_of4(out16 & 15u));
+          v.y = (v.y & ~bytes_of4((out16 >> 4) & 15u)) | (mcol4 & bytes_of4((out16 >> 4) & 15u));
+          v.z = (v.z & ~bytes_of4((out16 >> 8) & 15u)) | (mcol4 & bytes_of4((out16 >> 8) & 15u));
+          v.w = (v.w & ~bytes_of4(out16 >> 12)) | (mcol4 & bytes_of4(out16 >> 12));
+          *reinterpret_cast<uint4*>(row + x0) = v;
+        }
+        if (kRows && reg) acc[k] += dark16(v, reg, kadd);
+      }
+    }
+    finish_rows();
+    return;
+  }
   const Rect A = clip(a.area, P.W, P.H);
   const int32_t aw = A.x1 - A.x0 + 1, ah = A.y1 - A.y0 + 1;
   const int32_t sw = iabs(a.area.x0 - a.area.x1) + 1, sh = iabs(a.area.y0 - a.area.y1) + 1;
   const uint8_t bg = gray_of(Px{a.bg[0], a.bg[1], a.bg[2]});
   const uint32_t bg4 = bg * 0x01010101u;
-  const int32_t nv = (P.W + 15) >> 4;                  // vectors per row (inside the pitch)
   const int32_t delta = A.x0 - a.tx;                   // source column - destination column
   const int r16 = delta & 15, q = r16 >> 2, r = r16 & 3;
-  // The class of a column changes only at five breakpoints (uniform per
-  // sheet).  Vectors holding a breakpoint strictly inside, and the row's last
+  // The class of a column changes only at the breakpoints (uniform per
+  // sheet): five of the move, and the mask's two when one is folded in.
+  // Vectors holding a breakpoint strictly inside, and the row's last
   // partial vector, are assembled byte by byte after the row's uniform
   // vectors -- one lane each, so the wave runs that path once per row.
-  const int32_t bp[5] = {a.tx, a.tx + aw, a.tx + sw, A.x0, A.x1 + 1};
+  const int32_t bp[kMoveBp] = {a.tx, a.tx + aw, a.tx + sw, A.x0, A.x1 + 1,
+                               kMask ? mk.x0 : 0, kMask ? mk.x1 + 1 : 0};
   // Deferred vectors (uniform): those holding a breakpoint strictly inside,
   // and the row's last partial vector, deduplicated.
-  int32_t dvs[6];
+  int32_t dvs[kMoveBp + 1];
   int nd = 0;
 #pragma unroll
-  for (int k = 0; k < 6; k++) {
-    const int32_t b = k < 5 ? bp[k] : P.W;
-    const bool has = k < 5 ? (b > 0 && b < P.W && (b & 15)) : (P.W & 15) != 0;
+  for (int k = 0; k < kMoveBp + 1; k++) {
+    const int32_t b = k < kMoveBp ? bp[k] : P.W;
+    const bool has = k < kMoveBp ? (b > 0 && b < P.W && (b & 15)) : (P.W & 15) != 0;
     bool dup = false;
 #pragma unroll
-    for (int m = 0; m < 6; m++)
+    for (int m = 0; m < kMoveBp + 1; m++)
       if (m < nd && dvs[m] == (b >> 4)) dup = true;
     if (has && !dup) dvs[nd++] = b >> 4;
   }
-  const int lane = threadIdx.x & 63;
-  // A column's class on a row is a function of three column facts (inside
-  // the pasted columns, inside its copied part, inside the wiped area) and
-  // three row facts; per row the eight column codes map to classes through
-  // one 16-bit table (2 bits per code), so the column work is done once.
+  // A column's class on a row is a function of four column facts (inside
+  // the pasted columns, inside its copied part, inside the wiped area, inside
+  // the mask) and four row facts; per row the sixteen column codes map to
+  // classes (0 source, 1 background, 2 moved, 3 mask colour) through one
+  // 32-bit table, so the column work is done once.
   auto col_code = [&](int32_t x) -> uint32_t {
     const int32_t u = x - a.tx;
     return (uint32_t)(u >= 0 && u < sw) | (uint32_t)(u < aw) << 1 |
-           (uint32_t)(x >= A.x0 && x <= A.x1) << 2;
+           (uint32_t)(x >= A.x0 && x <= A.x1) << 2 | (uint32_t)(x >= mk.x0 && x <= mk.x1) << 3;
   };
   auto row_table = [&](int32_t y) -> uint32_t {
     const int32_t v = y - a.ty;
     const bool trow = v >= 0 && v < sh, mrow = trow && v < ah;
     const bool arow = y >= A.y0 && y <= A.y1;
+    const bool krow = y >= mk.y0 && y <= mk.y1;
     uint32_t t = 0;
 #pragma unroll
-    for (int c = 0; c < 8; c++) {
-      const int cls = (trow && (c & 1)) ? ((mrow && (c & 2)) ? 2 : 1) : ((arow && (c & 4)) ? 1 : 0);
+    for (int c = 0; c < 16; c++) {
+      int cls = (trow && (c & 1)) ? ((mrow && (c & 2)) ? 2 : 1) : ((arow && (c & 4)) ? 1 : 0);
+      if (kMask && cls == 0 && !(krow && (c & 8))) cls = 3;
       t |= (uint32_t)cls << (2 * c);
     }
     return t;
@@ -584,23 +682,25 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
     const int32_t v = y - a.ty;
     return sbase + (int64_t)(A.y0 + ((v >= 0 && v < ah) ? v : 0)) * P.pitch;
   };
-  const int32_t yb = blockIdx.x * kMoveRows * (kThreads / 64);  // the block's first row
-  const int32_t y0 = blockIdx.x * kMoveRows * (kThreads / 64) + (threadIdx.x >> 6) * kMoveRows;
-  const int32_t y1 = imin(y0 + kMoveRows, P.H);
   // kMoveVec vectors per lane per chunk of the row (192 slots: 155 used at A4 width)
   constexpr int kMoveVec = 3;
   for (int32_t vb = 0; vb < nv; vb += 64 * kMoveVec) {
-    uint32_t cc[kMoveVec];  // column code, bit 3: no uniform vector here
+    uint32_t cc[kMoveVec];   // column code, bit 4: no uniform vector here
+    uint32_t reg[kMoveVec];  // counted columns (kRows)
 #pragma unroll
     for (int k = 0; k < kMoveVec; k++) {
       const int32_t vi = vb + k * 64 + lane;
       const int32_t x0 = 16 * vi;
       bool deferred = vi >= nv || x0 + 16 > P.W;
 #pragma unroll
-      for (int j = 0; j < 5; j++) deferred |= bp[j] > x0 && bp[j] < x0 + 16;
-      cc[k] = col_code(x0) | (deferred ? 8u : 0u);
+      for (int j = 0; j < kMoveBp; j++) deferred |= bp[j] > x0 && bp[j] < x0 + 16;
+      cc[k] = col_code(x0) | (deferred ? 16u : 0u);
+      reg[k] = kRows ? cols16(x0, X.rx0, X.rx1) : 0u;
     }
-    for (int32_t y = y0; y < y1; y++) {
+#pragma unroll
+    for (int ky = 0; ky < kMoveRows; ky++) {
+      const int32_t y = y0 + ky;
+      if (y >= y1) break;
       const uint8_t* srow = sbase + (int64_t)y * P.pitch;
       uint8_t* drow = dbase + (int64_t)y * P.pitch;
       const uint8_t* mrow_p = moved_row(y);
@@ -610,8 +710,8 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
 #pragma unroll
       for (int k = 0; k < kMoveVec; k++) {
         const int32_t x0 = 16 * (vb + k * 64 + lane);
-        cls[k] = (cc[k] & 8u) ? -1 : (int)((tab >> (2 * (cc[k] & 7u))) & 3u);
-        lo[k] = make_uint4(bg4, bg4, bg4, bg4);
+        cls[k] = (cc[k] & 16u) ? -1 : (int)((tab >> (2 * (cc[k] & 15u))) & 3u);
+        lo[k] = cls[k] == 3 ? make_uint4(mcol4, mcol4, mcol4, mcol4) : make_uint4(bg4, bg4, bg4, bg4);
         hi[k] = make_uint4(0, 0, 0, 0);
         if (cls[k] == 0) {
           lo[k] = *reinterpret_cast<const uint4*>(srow + x0);
@@ -639,21 +739,23 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
           }
         }
         *reinterpret_cast<uint4*>(drow + x0) = out;
+        if (kRows && reg[k]) acc[ky] += dark16(out, reg[k], kadd);
       }
     }
   }
   // Deferred vectors: per byte, the class picks a byte of the source vector,
-  // of the moved (realigned) vector or the background; columns >= W stay 0.
-  // The block's (row, deferred vector) pairs are spread over all its lanes,
-  // one pair each (<= 6 x kMoveRows x 4 <= kThreads), so the byte work runs
-  // once per block rather than once per row and wave.
+  // of the moved (realigned) vector, the background or the mask colour;
+  // columns >= W stay 0.  The block's (row, deferred vector) pairs are
+  // spread over all its lanes, one pair each (<= 8 x kMoveBlockRows <=
+  // kThreads), so the byte work runs once per block rather than once per row
+  // and wave.
   const int tid = threadIdx.x;
   const int32_t yr = yb + (nd ? tid / nd : 0);
-  if (tid < nd * kMoveRows * (kThreads / 64) && yr < P.H) {
+  if (tid < nd * kMoveBlockRows && yr < P.H) {
     const int di = tid - (tid / nd) * nd;
     int32_t vi = dvs[0];
 #pragma unroll
-    for (int m = 1; m < 6; m++)
+    for (int m = 1; m < kMoveBp + 1; m++)
       if (m == di) vi = dvs[m];
     const int32_t x0 = 16 * vi;
     const int32_t y = yr;
@@ -681,21 +783,28 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
     uint32_t o[4];
 #pragma unroll
     for (int d = 0; d < 4; d++) {
-      uint32_t m0 = 0, m2 = 0, mb = 0;
+      uint32_t m0 = 0, m2 = 0, mb = 0, mc = 0;
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const int32_t x = x0 + 4 * d + j;
-        const uint32_t code = x < P.W ? col_code(x) : 8u;
-        const uint32_t cls = (code & 8u) ? 3u : (tab >> (2 * code)) & 3u;
+        const uint32_t code = x < P.W ? col_code(x) : 16u;
+        const uint32_t cls = (code & 16u) ? 4u : (tab >> (2 * code)) & 3u;
         const uint32_t byte = 0xFFu << (8 * j);
         m0 |= cls == 0 ? byte : 0u;
         m2 |= cls == 2 ? byte : 0u;
         mb |= cls == 1 ? byte : 0u;
+        mc |= cls == 3 ? byte : 0u;
       }
-      o[d] = (sw4[d] & m0) | (mw4[d] & m2) | (bg4 & mb);
+      o[d] = (sw4[d] & m0) | (mw4[d] & m2) | (bg4 & mb) | (mcol4 & mc);
     }
-    *reinterpret_cast<uint4*>(dbase + (int64_t)y * P.pitch + x0) = make_uint4(o[0], o[1], o[2], o[3]);
+    const uint4 ov = make_uint4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<uint4*>(dbase + (int64_t)y * P.pitch + x0) = ov;
+    if (kRows) {
+      const uint32_t rg = cols16(x0, X.rx0, X.rx1);
+      if (rg) atomicAdd(&rowcnt[y - yb], dark16(ov, rg, kadd));
+    }
   }
+  finish_rows();
 }
 
 void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* args, int count,
@@ -703,9 +812,9 @@ void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* 
   int gx = src.P.H < 1 ? 1 : (src.P.H > 1024 ? 1024 : src.P.H);
   if (src.P.fmt == F_GRAY8) {
     // kMoveRows consecutive rows per wave
-    const int64_t blocks = (src.P.H + kMoveRows * (kThreads / 64) - 1) / (kMoveRows * (kThreads / 64));
-    UPH_LAUNCH_DIAG(4, k_move_rect_g16, dim3((unsigned)(blocks < 1 ? 1 : blocks), 1, count),
-                    dim3(kThreads), 0, st, src, dst, args);
+    const int64_t blocks = (src.P.H + kMoveBlockRows - 1) / kMoveBlockRows;
+    UPH_LAUNCH_DIAG(4, k_move_rect_g16<0>, dim3((unsigned)(blocks < 1 ? 1 : blocks), 1, count),
+                    dim3(kThreads), 0, st, src, dst, args, MoveExtra{});
   } else if (src.P.fmt == F_Y400A) {
     hipLaunchKernelGGL(k_move_rect<F_Y400A>, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst,
                        args);
@@ -713,6 +822,21 @@ void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* 
     hipLaunchKernelGGL(k_move_rect<F_RGB24>, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst,
                        args);
   }
+}
+
+bool launch_move_rect_fused(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* args,
+                            const MoveExtra& x, int count, hipStream_t st) {
+  if (src.P.fmt != F_GRAY8) return false;
+  const int64_t blocks = (src.P.H + kMoveBlockRows - 1) / kMoveBlockRows;
+  const dim3 grid((unsigned)(blocks < 1 ? 1 : blocks), 1, count);
+  const int mode = (x.masks ? 1 : 0) | (x.rows ? 2 : 0);
+  switch (mode) {
+    case 1: UPH_LAUNCH_DIAG(4, k_move_rect_g16<1>, grid, dim3(kThreads), 0, st, src, dst, args, x); break;
+    case 2: UPH_LAUNCH_DIAG(4, k_move_rect_g16<2>, grid, dim3(kThreads), 0, st, src, dst, args, x); break;
+    case 3: UPH_LAUNCH_DIAG(4, k_move_rect_g16<3>, grid, dim3(kThreads), 0, st, src, dst, args, x); break;
+    default: UPH_LAUNCH_DIAG(4, k_move_rect_g16<0>, grid, dim3(kThreads), 0, st, src, dst, args, x); break;
+  }
+  return true;
 }
 
 // ---------------------------------------------------------------------------

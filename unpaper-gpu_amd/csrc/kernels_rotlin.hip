@@ -1,0 +1,311 @@
+// kernels_rotlin.hip — deskew rotation with bilinear interpolation
+// (deskew.c:248-286 + interp_bilinear, interpolate.c:76-117): the --interpolate
+// linear path, BASELINE configs[3]'s RGB24 double-page scans.
+//
+// One workgroup per 64 x 32 output tile, one output pixel per lane and row.
+// The tile's source window is staged once in LDS as C float planes (one per
+// channel; white outside the image, which is get_pixel's value there), so the
+// four taps of a channel are two ds_read2_b32.  Red and green run as packed
+// pairs, every rounding of linear_scale kept:  (uint8)((1.0f - x) * a + x * b).
+// Output rows are assembled in LDS (pixels outside every rotated mask keep the
+// source bytes) and leave as 16-byte stores.
+//
+// Up to two masks per sheet in one launch (the double layout): mask 1 is
+// rotated here only when the caller marked the sheet independent -- its
+// rotation was detected on the same image and its source window does not reach
+// into mask 0 (k_rot_independent) -- so the result equals the reference's
+// one-mask-after-the-other order (sheet_stages.c:401-412); otherwise mask 1
+// takes a second launch after mask 0's.
+#include "interp.h"
+#include "kernels.h"
+
+namespace uph {
+
+typedef float lf2 __attribute__((ext_vector_type(2)));
+
+constexpr int kLW = 64;                    // output columns per tile (one per lane)
+constexpr int kLH = 32;                    // output rows per tile
+constexpr int kLT = 256;                   // 4 waves, kLH / 4 consecutive rows each
+constexpr int kLRows = kLH / (kLT / 64);
+
+// linear_scale (interpolate.c:62-65) on the pair (r, g): separate roundings of
+// (1 - x) * a, x * b and their sum, then the uint8 truncation
+__device__ __forceinline__ lf2 lin2(float xm, float x, lf2 a, lf2 b) {
+  const lf2 t = lf2{xm, xm} * a;
+  const lf2 u = lf2{x, x} * b;
+  const lf2 s = t + u;
+  return lf2{__builtin_truncf(s.x), __builtin_truncf(s.y)};
+}
+__device__ __forceinline__ float lin1(float xm, float x, float a, float b) {
+  const float t = xm * a, u = x * b;
+  return __builtin_truncf(t + u);
+}
+
+// In-mask part of a tile for one mask, in mask coordinates; false when empty.
+struct MaskPart {
+  int32_t cu0, cu1, cv0, cv1;
+};
+__device__ __forceinline__ bool mask_part(const RotateArgs& a, int32_t tx0, int32_t ty0, int32_t W,
+                                          int32_t H, MaskPart* mp) {
+  const Rect nm = normalize(a.mask);
+  const int32_t sw = nm.x1 - nm.x0 + 1, sh = nm.y1 - nm.y0 + 1;
+  const int32_t u0 = imax(tx0, 0) - a.mask.x0, u1 = imin(tx0 + kLW, W) - 1 - a.mask.x0;
+  const int32_t v0 = imax(ty0, 0) - a.mask.y0, v1 = imin(ty0 + kLH, H) - 1 - a.mask.y0;
+  mp->cu0 = imax(u0, 0);
+  mp->cu1 = imin(u1, sw - 1);
+  mp->cv0 = imax(v0, 0);
+  mp->cv1 = imin(v1, sh - 1);
+  return mp->cu0 <= mp->cu1 && mp->cv0 <= mp->cv1;
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(kLT) k_rotate_lin(PlaneRef src, PlaneRef dst, const RotateArgs* args,
+                                                    int nmask, int64_t mstride, const int32_t* indep,
+                                                    LinWindow win, uint32_t m_gxy, uint32_t m_gx) {
+  constexpr int C = FMT == F_RGB24 ? 3 : 1;
+  constexpr int kRowB = kLW * C;            // output bytes per tile row
+  extern __shared__ __attribute__((aligned(16))) float lw[];  // C planes [rows][stride], then obuf
+  __shared__ int32_t wb[4];
+  int txi, tyi, s;
+  xcd_block_m(m_gxy, m_gx, &txi, &tyi, &s);
+  bool on[2] = {false, false};
+  RotateArgs am[2];
+#pragma unroll
+  for (int m = 0; m < 2; m++) {
+    if (m >= nmask) break;
+    am[m] = args[m * mstride + s];
+    on[m] = am[m].active && (m == 0 || !indep || indep[s]);
+  }
+  if (!on[0] && !on[1]) return;  // not rotated here: the plane is not flipped
+  const Planes& P = src.P;
+  const uint8_t* sbase = plane_ptr(src, s);
+  uint8_t* dbase = plane_ptr(dst, s);
+  const int32_t tx0 = txi * kLW, ty0 = tyi * kLH;
+  const int32_t th = imin(kLH, P.H - ty0);
+  const int64_t xb0 = (int64_t)tx0 * C;                     // tile's first byte in a row
+  const int32_t rowb = (int32_t)imin((int64_t)kRowB, (int64_t)P.W * C - xb0);  // its bytes per row
+  MaskPart mp[2];
+  bool hit[2] = {false, false};
+#pragma unroll
+  for (int m = 0; m < 2; m++)
+    if (on[m]) hit[m] = mask_part(am[m], tx0, ty0, P.W, P.H, &mp[m]);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // 16-byte vectors of a tile row that lie inside the row's pitch
+  auto vec_ok = [&](int j) { return xb0 + 16 * (j + 1) <= P.pitch; };
+  if (!hit[0] && !hit[1]) {
+    // no rotated pixel: the tile's bytes copied unchanged (deskew.c:268-286)
+    constexpr int NV = kRowB / 16;
+    for (int i = tid; i < th * NV; i += kLT) {
+      const int r = i / NV, j = i - r * NV;
+      if (16 * j >= rowb) continue;
+      const uint8_t* sp = sbase + (int64_t)(ty0 + r) * P.pitch + xb0 + 16 * j;
+      uint8_t* dp = dbase + (int64_t)(ty0 + r) * P.pitch + xb0 + 16 * j;
+      if (vec_ok(j) && 16 * (j + 1) <= rowb) {
+        *reinterpret_cast<uint4*>(dp) = *reinterpret_cast<const uint4*>(sp);
+      } else {
+        for (int k = 0; k < 16 && 16 * j + k < rowb; k++) dp[k] = sp[k];
+      }
+    }
+    return;
+  }
+  const int32_t plane_f = win.rows * win.stride;            // floats per channel plane
+  uint8_t* obuf = reinterpret_cast<uint8_t*>(lw + C * plane_f);  // kLH x kRowB bytes
+  // 1. the tile's source bytes (kept where no mask rotates)
+  {
+    constexpr int NV = kRowB / 16;
+    for (int i = tid; i < th * NV; i += kLT) {
+      const int r = i / NV, j = i - r * NV;
+      const uint8_t* sp = sbase + (int64_t)(ty0 + r) * P.pitch + xb0 + 16 * j;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (16 * j < rowb) {
+        if (vec_ok(j)) {
+          v = *reinterpret_cast<const uint4*>(sp);
+        } else {
+          uint8_t t[16];
+          for (int k = 0; k < 16; k++) t[k] = 16 * j + k < rowb ? sp[k] : 0;
+          v = *reinterpret_cast<const uint4*>(t);
+        }
+      }
+      *reinterpret_cast<uint4*>(obuf + r * kRowB + 16 * j) = v;
+    }
+  }
+  // 2. every mask that rotates part of the tile (disjoint when both do)
+#pragma unroll 1
+  for (int m = 0; m < 2; m++) {
+    if (!hit[m]) continue;
+    const RotateArgs a = am[m];
+    const Rect nm = normalize(a.mask);
+    const int32_t sw = nm.x1 - nm.x0 + 1, sh = nm.y1 - nm.y0 + 1;
+    const float scx = nm.x0 + sw / 2.0f, scy = nm.y0 + sh / 2.0f;  // primitives.c:137-145
+    const float tcx = 0 + sw / 2.0f, tcy = 0 + sh / 2.0f;
+    // source window of the in-mask pixels: coordinates are monotone in u
+    // and v (the same float expressions), so the corners bound them; the
+    // taps are floor(c) .. ceil(c) <= floor(c) + 1
+    if (wv == 0) {
+      const int c = lane & 3;
+      const int32_t u = c & 1 ? mp[m].cu1 : mp[m].cu0, v = c & 2 ? mp[m].cv1 : mp[m].cv0;
+      const float X = scx + (u - tcx) * a.cosval + (v - tcy) * a.sinval;
+      const float Y = scy + (v - tcy) * a.cosval - (u - tcx) * a.sinval;
+      float mnx = X, mxx = X, mny = Y, mxy = Y;
+#pragma unroll
+      for (int o = 1; o < 4; o <<= 1) {
+        mnx = fminf(mnx, __shfl_xor(mnx, o, 64));
+        mxx = fmaxf(mxx, __shfl_xor(mxx, o, 64));
+        mny = fminf(mny, __shfl_xor(mny, o, 64));
+        mxy = fmaxf(mxy, __shfl_xor(mxy, o, 64));
+      }
+      if (lane < 4) wb[lane] = (int32_t)floorf(lane == 0 ? mnx : lane == 1 ? mny : lane == 2 ? mxx : mxy);
+    }
+    __syncthreads();
+    const int32_t bx0 = wb[0], by0 = wb[1];
+    const int32_t bw = wb[2] + 1 - bx0 + 1, bh = wb[3] + 1 - by0 + 1;
+    const bool staged = bw <= win.cols && bh <= win.rows;
+    if (staged) {
+      // window bytes [bx0 C, (bx0 + bw) C) of rows by0 .. by0 + bh - 1, one
+      // aligned dword per lane: each byte to its channel plane as a float
+      const int64_t b0 = (int64_t)bx0 * C, b1 = (int64_t)(bx0 + bw) * C;
+      const int64_t da = b0 >= 0 ? (b0 & ~(int64_t)3) : -((-b0 + 3) & ~(int64_t)3);
+      const int32_t nd = (int32_t)((b1 - da + 3) >> 2);
+      const int64_t rowmax = (int64_t)P.W * C;
+      for (int i = tid; i < bh * nd; i += kLT) {
+        const int r = i / nd, k = i - r * nd;
+        const int32_t y = by0 + r;
+        const int64_t bo = da + 4 * k;
+        uint32_t w = 0xFFFFFFFFu;
+        if (y >= 0 && y < P.H && bo >= 0 && bo + 4 <= P.pitch)
+          w = *reinterpret_cast<const uint32_t*>(sbase + (int64_t)y * P.pitch + bo);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int64_t b = bo + j;
+          if (b < b0 || b >= b1) continue;
+          const uint32_t v = (b >= 0 && b < rowmax && y >= 0 && y < P.H) ? (w >> (8 * j)) & 0xFFu : 255u;
+          // window byte bb = b - b0 (b0 is bx0 * C): column bb / C, channel bb % C
+          const uint32_t bb = (uint32_t)(b - b0);
+          const uint32_t col = C == 3 ? (bb * 0xAAABu) >> 17 : bb;  // bb / 3 for bb < 2^16
+          const uint32_t ch = bb - C * col;
+          lw[ch * plane_f + r * win.stride + col] = (float)v;
+        }
+      }
+    }
+    __syncthreads();
+    // 3. the in-mask pixels of this wave's rows
+    const int32_t x = tx0 + lane;
+    const int32_t u = x - a.mask.x0;
+    const bool colin = x < P.W && u >= 0 && u < sw;
+    const float cu = u - tcx;
+    const float ax = scx + cu * a.cosval, bs = cu * a.sinval;
+    const Src<FMT> S{sbase, P.pitch, P.W, P.H};
+#pragma unroll 2
+    for (int k = 0; k < kLRows; k++) {
+      const int r = wv * kLRows + k;
+      const int32_t y = ty0 + r;
+      const int32_t v = y - a.mask.y0;
+      if (!(colin && y < P.H && v >= 0 && v < sh)) continue;
+      const float cv = v - tcy;
+      const float cx = ax + cv * a.sinval;          // scx + (u-tcx) cos + (v-tcy) sin
+      const float cy = (scy + cv * a.cosval) - bs;  // scy + (v-tcy) cos - (u-tcx) sin
+      uint8_t* o = obuf + r * kRowB + lane * C;
+      if (!staged) {
+        const Px p = interp_bilinear(S, cx, cy);
+        o[0] = p.r;
+        if (C == 3) {
+          o[1] = p.g;
+          o[2] = p.b;
+        }
+        continue;
+      }
+      const float fx1 = floorf(cx), fy1 = floorf(cy);
+      const int32_t x1 = (int32_t)fx1, y1 = (int32_t)fy1;
+      const int32_t x2 = (int32_t)ceilf(cx), y2 = (int32_t)ceilf(cy);
+      const int32_t i11 = (y1 - by0) * win.stride + (x1 - bx0);
+      // interp_bilinear (interpolate.c:77-118): outside the image or with an
+      // integral coordinate the result is the pixel (x1, y1) -- the one-axis
+      // cases use the other axis' zero fraction
+      const bool plain = !(x2 >= 0 && x2 <= P.W - 1 && y2 >= 0 && y2 <= P.H - 1) || x1 == x2 || y1 == y2;
+      if (plain) {
+#pragma unroll
+        for (int c = 0; c < C; c++) o[c] = (uint8_t)lw[c * plane_f + i11];
+        continue;
+      }
+      const float fx = cx - fx1, fy = cy - fy1;
+      const float fxm = 1.0f - fx, fym = 1.0f - fy;
+      const int32_t i21 = i11 + win.stride;
+      if (C == 3) {
+        const lf2 a11{lw[i11], lw[plane_f + i11]}, a21{lw[i11 + 1], lw[plane_f + i11 + 1]};
+        const lf2 a12{lw[i21], lw[plane_f + i21]}, a22{lw[i21 + 1], lw[plane_f + i21 + 1]};
+        const float b11 = lw[2 * plane_f + i11], b21 = lw[2 * plane_f + i11 + 1];
+        const float b12 = lw[2 * plane_f + i21], b22 = lw[2 * plane_f + i21 + 1];
+        const lf2 h1 = lin2(fxm, fx, a11, a21), h2 = lin2(fxm, fx, a12, a22);
+        const lf2 rg = lin2(fym, fy, h1, h2);
+        const float hb1 = lin1(fxm, fx, b11, b21), hb2 = lin1(fxm, fx, b12, b22);
+        const float bb = lin1(fym, fy, hb1, hb2);
+        o[0] = (uint8_t)(uint32_t)rg.x;
+        o[1] = (uint8_t)(uint32_t)rg.y;
+        o[2] = (uint8_t)(uint32_t)bb;
+      } else {
+        // (h1, h2) as one pair: rows y1 and y2, columns x1 then x2
+        const lf2 c1{lw[i11], lw[i21]}, c2{lw[i11 + 1], lw[i21 + 1]};
+        const lf2 h = lin2(fxm, fx, c1, c2);
+        o[0] = (uint8_t)(uint32_t)lin1(fym, fy, h.x, h.y);
+      }
+    }
+    __syncthreads();  // the next mask restages the window
+  }
+  // 4. the tile's rows out of LDS, 16 bytes per lane
+  {
+    constexpr int NV = kRowB / 16;
+    for (int i = tid; i < th * NV; i += kLT) {
+      const int r = i / NV, j = i - r * NV;
+      if (16 * j >= rowb) continue;
+      uint8_t* dp = dbase + (int64_t)(ty0 + r) * P.pitch + xb0 + 16 * j;
+      const uint4 v = *reinterpret_cast<const uint4*>(obuf + r * kRowB + 16 * j);
+      if (vec_ok(j) && 16 * (j + 1) <= rowb) {
+        *reinterpret_cast<uint4*>(dp) = v;
+      } else {
+        const uint8_t* t = reinterpret_cast<const uint8_t*>(&v);
+        for (int k = 0; k < 16 && 16 * j + k < rowb; k++) dp[k] = t[k];
+      }
+    }
+  }
+}
+
+LinWindow lin_window(float max_abs_angle) {
+  const float a = fminf(fabsf(max_abs_angle), 1.5707964f);
+  const float sn = sinf(a), cs = cosf(a);
+  LinWindow w;
+  // (n-1) cos + (m-1) sin pixel centres, + 1 for ceil, + 2 for the floor of
+  // the bounds and the rounding of the corner products
+  w.cols = (int32_t)ceilf((kLW - 1) * cs + (kLH - 1) * sn) + 4;
+  w.rows = (int32_t)ceilf((kLH - 1) * cs + (kLW - 1) * sn) + 4;
+  w.stride = (w.cols + 7) & ~7;
+  return w;
+}
+
+size_t lin_lds_bytes(const LinWindow& w, int fmt) {
+  const int C = fmt == F_RGB24 ? 3 : 1;
+  return sizeof(float) * (size_t)C * w.rows * w.stride + (size_t)kLH * kLW * C;
+}
+
+bool launch_rotate_linear(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
+                          int nmask, int64_t mstride, const int32_t* indep, int count,
+                          hipStream_t st, float max_abs_angle) {
+  if (src.P.fmt != F_GRAY8 && src.P.fmt != F_RGB24) return false;
+  const LinWindow w = lin_window(max_abs_angle);
+  const size_t lds = lin_lds_bytes(w, src.P.fmt);
+  if (lds > 64 * 1024) return false;
+  const dim3 grid((src.P.W + kLW - 1) / kLW, (src.P.H + kLH - 1) / kLH, count);
+  const uint32_t mgxy = div_magic(grid.x * grid.y), mgx = div_magic(grid.x);
+  if (src.P.fmt == F_RGB24) {
+    allow_dynamic_lds((const void*)k_rotate_lin<F_RGB24>, lds);
+    hipLaunchKernelGGL(k_rotate_lin<F_RGB24>, grid, dim3(kLT), lds, st, src, dst, args, nmask,
+                       mstride, indep, w, mgxy, mgx);
+  } else {
+    allow_dynamic_lds((const void*)k_rotate_lin<F_GRAY8>, lds);
+    hipLaunchKernelGGL(k_rotate_lin<F_GRAY8>, grid, dim3(kLT), lds, st, src, dst, args, nmask,
+                       mstride, indep, w, mgxy, mgx);
+  }
+  return true;
+}
+
+}  // namespace uph

@@ -554,7 +554,9 @@ void uphip_deskew(UphipImage source0, UphipRectangle mask, float radians,
   if (!n) return;
   RotateArgs* d = stage_args(&a, 1, st);
   if (!d) return;
-  launch_rotate_mask(ref_of(f), ref_of(n), d, interp, 1, st, radians);
+  if (!(interp == UPHIP_INTERP_LINEAR &&
+        launch_rotate_linear(ref_of(f), ref_of(n), d, 1, 1, nullptr, 1, st, radians)))
+    launch_rotate_mask(ref_of(f), ref_of(n), d, interp, 1, st, radians);
   arg_fence(st);
   adopt_storage(f, n);
   mp.finish();

@@ -115,11 +115,67 @@ __global__ void k_mask_assemble(SheetCtl* ctl, const int32_t* edges, MaskAssembl
 }
 
 // masks[i] -> a Rect array + active flags for the rotation-peak kernel
-__global__ void k_mask_pick(const SheetCtl* ctl, int i, Rect* out, int32_t* active, int count) {
+// only (may be null): sheets outside it are marked inactive
+__global__ void k_mask_pick(const SheetCtl* ctl, int i, Rect* out, int32_t* active, int count,
+                            const int32_t* only) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= count) return;
   out[s] = to_rect(ctl[s].masks[i]);
-  active[s] = i < ctl[s].mask_count;
+  active[s] = i < ctl[s].mask_count && (!only || only[s]);
+}
+
+// Two masks rotated in one launch (the double layout): the reference detects
+// and deskews mask 1 after deskewing mask 0 (sheet_stages.c:401-412).  Doing
+// both detections first and both rotations from the same image is the same
+// thing unless deskew 0 changes a pixel that mask 1's detection or rotation
+// reads: detection reads only pixels inside its mask (deskew.c:127-131), and
+// the rotation the source window of its mask (a rotated rectangle, bounded
+// here by its corners with two taps of margin either side).  dep[s] = 1 for
+// the sheets where that may happen: mask 1 is then detected and rotated again
+// after mask 0 (second pass); indep[s] = 1 where mask 1 rotates in the first.
+__global__ void k_rot_independent(const SheetCtl* ctl, const RotateArgs* args, int64_t mstride,
+                                  int32_t* indep, int32_t* dep, int count) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= count) return;
+  const SheetCtl& c = ctl[s];
+  const RotateArgs a0 = args[s], a1 = args[mstride + s];
+  bool d = false;
+  if (c.mask_count >= 2 && a0.active) {
+    const Rect m0 = normalize(to_rect(c.masks[0])), m1 = normalize(to_rect(c.masks[1]));
+    auto meets = [](const Rect& p, const Rect& q) {
+      return p.x0 <= q.x1 && q.x0 <= p.x1 && p.y0 <= q.y1 && q.y0 <= p.y1;
+    };
+    d = meets(m0, m1);
+    if (!d && a1.active) {
+      const Rect nm = normalize(a1.mask);
+      const int32_t sw = nm.x1 - nm.x0 + 1, sh = nm.y1 - nm.y0 + 1;
+      const float scx = nm.x0 + sw / 2.0f, scy = nm.y0 + sh / 2.0f;
+      const float tcx = 0 + sw / 2.0f, tcy = 0 + sh / 2.0f;
+      float mnx = 3.0e38f, mxx = -3.0e38f, mny = 3.0e38f, mxy = -3.0e38f;
+      for (int k = 0; k < 4; k++) {
+        const int32_t u = k & 1 ? sw - 1 : 0, v = k & 2 ? sh - 1 : 0;
+        const float X = scx + (u - tcx) * a1.cosval + (v - tcy) * a1.sinval;
+        const float Y = scy + (v - tcy) * a1.cosval - (u - tcx) * a1.sinval;
+        mnx = fminf(mnx, X);
+        mxx = fmaxf(mxx, X);
+        mny = fminf(mny, Y);
+        mxy = fmaxf(mxy, Y);
+      }
+      const Rect w{(int32_t)floorf(mnx) - 2, (int32_t)floorf(mny) - 2, (int32_t)floorf(mxx) + 3,
+                   (int32_t)floorf(mxy) + 3};
+      d = meets(w, m0);
+    }
+  }
+  dep[s] = d;
+  indep[s] = !d;
+}
+
+// flip every sheet the two-mask launch rotated
+__global__ void k_flip_rot2(SheetCtl* ctl, const RotateArgs* args, int64_t mstride,
+                            const int32_t* indep, int count) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= count) return;
+  if (args[s].active || (args[mstride + s].active && indep[s])) ctl[s].cur ^= 1;
 }
 
 struct RotCombo {
@@ -136,11 +192,16 @@ struct RotSelectArgs {
 
 // detect_edge_rotation's argmax + detect_rotation_cpu's combination (exact via
 // the host-computed table for <= 2 edges) -> RotateArgs for deskew
+// only (may be null): other sheets get an inactive RotateArgs and keep their ctl
 __global__ void k_rot_select(SheetCtl* ctl, const int32_t* peaks, const RotTable* table,
                              const RotCombo* combo, RotSelectArgs a, RotateArgs* out,
-                             int count) {
+                             int count, const int32_t* only) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= count) return;
+  if (only && !only[s]) {
+    out[s].active = 0;
+    return;
+  }
   SheetCtl& c = ctl[s];
   const int i = a.mask_index;
   const bool active = i < c.mask_count;
@@ -332,7 +393,9 @@ struct UphipBatch {
   int32_t* rot_lines = nullptr;  // scan-line point lists (k_rot_points)
   Rect* pick_mask = nullptr;
   int32_t* pick_active = nullptr;
-  RotateArgs* rot_args = nullptr;
+  RotateArgs* rot_args = nullptr;      // [UPHIP_MAX_PAGES][cap]
+  int32_t* rot_indep = nullptr;        // two-mask launch: mask 1 independent of deskew 0
+  int32_t* rot_dep = nullptr;          // ... or redone after it
   MoveArgs* move_args = nullptr;      // cap * MAX_PAGES
   MaskArgs* border_mask_args = nullptr;
   int32_t* edge_res = nullptr;        // cap * npoints * 4
@@ -643,7 +706,9 @@ static bool allocate(UphipBatch* b) {
   b->border_res = dalloc<int32_t>(b, (size_t)cap * imax(nout, 1) * 4);
   b->move_args = dalloc<MoveArgs>(b, (size_t)cap * UPHIP_MAX_PAGES);
   b->border_mask_args = dalloc<MaskArgs>(b, cap);
-  b->rot_args = dalloc<RotateArgs>(b, cap);
+  b->rot_args = dalloc<RotateArgs>(b, (size_t)cap * UPHIP_MAX_PAGES);
+  b->rot_indep = dalloc<int32_t>(b, cap);
+  b->rot_dep = dalloc<int32_t>(b, cap);
   b->pick_mask = dalloc<Rect>(b, cap);
   b->pick_active = dalloc<int32_t>(b, cap);
   // rotation tables
@@ -840,12 +905,39 @@ static void detect_masks_all(UphipBatch* b, int assign, int count) {
                      b->edge_res, ma, count);
 }
 
-static void border_all(UphipBatch* b, int count) {
+// The border scan's row sums can come out of the last mask-centering move
+// (k_move_rect_g16 counts the dark pixels of every row it writes): one
+// outside rectangle, a vertical scan only, a gray plane, and nothing between
+// the centering and the border scan that writes the sheet (sheet_stages.c:
+// 425-473: explicit wipes, the middle wipe, the explicit border).
+static bool border_rows_from_center(const UphipBatch* b) {
+  const UphipOptions& o = b->o;
+  const uint32_t dis = o.disable;
+  const UphipBorderScanParameters& p = o.border_scan_parameters;
+  if ((dis & UPHIP_NO_MASK_CENTER) || b->points.empty()) return false;
+  if ((dis & UPHIP_NO_BORDER_SCAN) || b->outside.size() != 1) return false;
+  if (p.scan_direction.horizontal || !p.scan_direction.vertical) return false;
+  if (b->work_fmt != F_GRAY8) return false;
+  if (b->outside[0].x0 > b->outside[0].x1) return false;
+  if (!(dis & UPHIP_NO_WIPE)) {
+    if (o.wipes.count > 0) return false;
+    if (o.layout == UPHIP_LAYOUT_DOUBLE && (o.middle_wipe[0] > 0 || o.middle_wipe[1] > 0)) return false;
+  }
+  if (!(dis & UPHIP_NO_BORDER) &&
+      (o.border.left || o.border.top || o.border.right || o.border.bottom))
+    return false;
+  return true;
+}
+
+// rows_ready: the vertical scan's row sums are already in b->sums
+// (border_rows_from_center)
+static void border_all(UphipBatch* b, int count, bool rows_ready) {
   const UphipBorderScanParameters& p = b->o.border_scan_parameters;
   const int nout = (int)b->outside.size();
   const int32_t W = b->W, H = b->H;
   const Planes P = planes_of(b, W, H);
-  UPH_HIP(hipMemsetAsync(b->sums, 0, sizeof(uint32_t) * b->sums_stride * count, b->st));
+  if (!rows_ready)
+    UPH_HIP(hipMemsetAsync(b->sums, 0, sizeof(uint32_t) * b->sums_stride * count, b->st));
   std::vector<BorderEdgeArgs> ea((size_t)nout * 4);
   memset(ea.data(), 0, sizeof(BorderEdgeArgs) * ea.size());
   for (int i = 0; i < nout; i++) {
@@ -866,7 +958,7 @@ static void border_all(UphipBatch* b, int count) {
       const int32_t off = (2 * i + 1) * imax(W, H);
       AxisArgs a{clip(Rect{o.x0, 0, o.x1, H - 1}, W, H), b->o.abs_black_threshold,
                  o.x0 <= o.x1 ? 1 : 0};
-      if (a.active && a.region.x1 >= a.region.x0)
+      if (a.active && a.region.x1 >= a.region.x0 && !rows_ready)
         launch_axis_reduce(cur_ref(P, b->ctl), replicate(b, a), 1, M_DARK_COUNT, W, H,
                            b->sums + off, b->sums_stride, count, b->st);
       const int32_t sz = p.scan_size.height, stp = p.scan_step.vertical;
@@ -901,12 +993,24 @@ static void border_all(UphipBatch* b, int count) {
   ba.bg[2] = b->o.sheet_background.b;
   hipLaunchKernelGGL(k_border_assemble, dim3((count + 255) / 256), dim3(256), 0, b->st, b->ctl,
                      b->border_res, ba, b->border_mask_args, b->move_args, count);
-  launch_apply_masks_thr(cur_ref(P, b->ctl), b->border_mask_args, count, b->o.abs_black_threshold,
-                         b->st);
-  for (int i = 0; i < nout; i++) {
-    if (b->o.disable & UPHIP_NO_BORDER_ALIGN) break;
+  // apply_masks then align_mask (sheet_stages.c:478-488): with one outside
+  // rectangle on a gray plane, one pass -- the move writes the mask colour
+  // outside the border mask (and masks in place where the move is the
+  // identity)
+  const bool align = !(b->o.disable & UPHIP_NO_BORDER_ALIGN);
+  const bool fold = align && nout == 1 && P.fmt == F_GRAY8;
+  if (!fold)
+    launch_apply_masks_thr(cur_ref(P, b->ctl), b->border_mask_args, count,
+                           b->o.abs_black_threshold, b->st);
+  for (int i = 0; i < nout && align; i++) {
     MoveArgs* mv = b->move_args + (int64_t)i * b->cap;
-    launch_move_rect(cur_ref(P, b->ctl), other_ref(P, b->ctl), mv, count, b->st);
+    if (fold) {
+      MoveExtra x{};
+      x.masks = b->border_mask_args;
+      launch_move_rect_fused(cur_ref(P, b->ctl), other_ref(P, b->ctl), mv, x, count, b->st);
+    } else {
+      launch_move_rect(cur_ref(P, b->ctl), other_ref(P, b->ctl), mv, count, b->st);
+    }
     launch_flip_if_active(b->ctl, &mv->active, sizeof(MoveArgs), count, b->st);
   }
 }
@@ -1058,12 +1162,13 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
     ra.nedges = rg.nedges;
     ra.max_masks = UPHIP_MAX_PAGES;
     ra.deviation_rad = o.deskew_parameters.deskewScanDeviationRad;
-    for (size_t i = 0; i < b->points.size(); i++) {
-      hipLaunchKernelGGL(k_mask_pick, dim3((count + 255) / 256), dim3(256), 0, b->st, b->ctl,
-                         (int)i, b->pick_mask, b->pick_active, count);
-      launch_rotation_peaks(cur_ref(P, b->ctl), rg, b->dtable, b->pick_mask, b->pick_active,
-                            (int)i, b->peaks, count, b->st, b->table.nangles, b->max_scan,
-                            b->rot_lines, b->max_angle);
+    // detection of mask i (mask_pick, peaks, select) into rot_args[i]
+    auto detect = [&](int i, const int32_t* only) {
+      hipLaunchKernelGGL(k_mask_pick, dim3((count + 255) / 256), dim3(256), 0, b->st, b->ctl, i,
+                         b->pick_mask, b->pick_active, count, only);
+      launch_rotation_peaks(cur_ref(P, b->ctl), rg, b->dtable, b->pick_mask, b->pick_active, i,
+                            b->peaks, count, b->st, b->table.nangles, b->max_scan, b->rot_lines,
+                            b->max_angle);
 #ifdef UPHIP_DIAG
       if (getenv("UPHIP_DIAG_ROTATION")) {  // tuning build only: lines left to the direct walk
         const int nl = count * rg.nedges * b->table.nangles;
@@ -1072,29 +1177,55 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
                                sizeof(int32_t) * nl, hipMemcpyDeviceToHost, b->st));
         UPH_HIP(hipStreamSynchronize(b->st));
         int nf = 0;
-        for (int t = 0; t < nl; t++)
-          if (fl[t]) {
-            if (nf < 8)
-              fprintf(stderr, "uphip: line sheet %d edge %d angle %d walked directly\n",
-                      t / (rg.nedges * b->table.nangles), (t / b->table.nangles) % rg.nedges,
-                      t % b->table.nangles);
-            nf++;
-          }
+        for (int t = 0; t < nl; t++) nf += fl[t] != 0;
         fprintf(stderr, "uphip: batch rotation %d of %d lines walked directly\n", nf, nl);
       }
 #endif
-      ra.mask_index = (int)i;
+      ra.mask_index = i;
       hipLaunchKernelGGL(k_rot_select, dim3((count + 255) / 256), dim3(256), 0, b->st, b->ctl,
-                         b->peaks, b->dtable, b->dcombo, ra, b->rot_args, count);
+                         b->peaks, b->dtable, b->dcombo, ra, b->rot_args + (int64_t)i * b->cap,
+                         count, only);
+    };
+    const bool linear = o.interpolate_type == UPHIP_INTERP_LINEAR &&
+                        (P.fmt == F_GRAY8 || P.fmt == F_RGB24);
+    // rotations are angles of the scan table, |angle| <= scan range
+    auto rotate = [&](const RotateArgs* args, int nmask, const int32_t* indep) {
+      if (!(linear && launch_rotate_linear(cur_ref(P, b->ctl), other_ref(P, b->ctl), args, nmask,
+                                           b->cap, indep, count, b->st, b->max_angle)))
+        launch_rotate_mask(cur_ref(P, b->ctl), other_ref(P, b->ctl), args, o.interpolate_type,
+                           count, b->st, b->max_angle);
+    };
+    if (linear && b->points.size() == 2) {
+      // both masks detected on the same image, rotated in one launch where
+      // independent (k_rot_independent); mask 1 again after mask 0 elsewhere
+      detect(0, nullptr);
+      detect(1, nullptr);
+      hipLaunchKernelGGL(k_rot_independent, dim3((count + 255) / 256), dim3(256), 0, b->st,
+                         b->ctl, b->rot_args, (int64_t)b->cap, b->rot_indep, b->rot_dep, count);
       mark(b, "deskew_detect");
-      // rotations are angles of the scan table, |angle| <= scan range
-      launch_rotate_mask(cur_ref(P, b->ctl), other_ref(P, b->ctl), b->rot_args,
-                         o.interpolate_type, count, b->st, b->max_angle);
+      rotate(b->rot_args, 2, b->rot_indep);
       mark(b, "deskew_rotate");  // brackets exactly the rotation kernel
-      launch_flip_if_active(b->ctl, &b->rot_args->active, sizeof(RotateArgs), count, b->st);
+      hipLaunchKernelGGL(k_flip_rot2, dim3((count + 255) / 256), dim3(256), 0, b->st, b->ctl,
+                         b->rot_args, (int64_t)b->cap, b->rot_indep, count);
+      RotateArgs* a1 = b->rot_args + b->cap;
+      detect(1, b->rot_dep);
+      mark(b, "deskew_detect");
+      rotate(a1, 1, nullptr);
+      mark(b, "deskew_rotate");
+      launch_flip_if_active(b->ctl, &a1->active, sizeof(RotateArgs), count, b->st);
+    } else {
+      for (size_t i = 0; i < b->points.size(); i++) {
+        detect((int)i, nullptr);
+        mark(b, "deskew_detect");
+        RotateArgs* ai = b->rot_args + (int64_t)i * b->cap;
+        rotate(ai, 1, nullptr);
+        mark(b, "deskew_rotate");  // brackets exactly the rotation kernel
+        launch_flip_if_active(b->ctl, &ai->active, sizeof(RotateArgs), count, b->st);
+      }
     }
   }
   // ---- post (sheet_stages.c:415-534) -------------------------------------
+  const bool rows_fused = border_rows_from_center(b);
   if (!(dis & UPHIP_NO_MASK_CENTER)) {
     if (!(dis & UPHIP_NO_MASK_SCAN)) {
       detect_masks_all(b, 1, count);
@@ -1104,7 +1235,19 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
       MoveArgs* mv = b->move_args;  // reuse the first cap entries
       hipLaunchKernelGGL(k_center_args, dim3((count + 255) / 256), dim3(256), 0, b->st, b->ctl,
                          (int)i, b->W, b->H, o.sheet_background, mv, count);
-      launch_move_rect(cur_ref(P, b->ctl), other_ref(P, b->ctl), mv, count, b->st);
+      if (rows_fused && i + 1 == b->points.size()) {
+        // the last move also counts the border scan's dark pixels per row
+        const Rect oc = clip(b->outside[0], b->W, b->H);
+        MoveExtra x{};
+        x.rows = b->sums + imax(b->W, b->H);  // border_all's vertical offset, outside rect 0
+        x.rows_stride = b->sums_stride;
+        x.rx0 = oc.x0;
+        x.rx1 = oc.x1;
+        x.thr = o.abs_black_threshold;
+        launch_move_rect_fused(cur_ref(P, b->ctl), other_ref(P, b->ctl), mv, x, count, b->st);
+      } else {
+        launch_move_rect(cur_ref(P, b->ctl), other_ref(P, b->ctl), mv, count, b->st);
+      }
       launch_flip_if_active(b->ctl, &mv->active, sizeof(MoveArgs), count, b->st);
     }
     mark(b, "center");
@@ -1120,7 +1263,7 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
   }
   if (!(dis & UPHIP_NO_BORDER)) border_uniform(b, P, o.border, count);
   if (!(dis & UPHIP_NO_BORDER_SCAN) && !b->outside.empty()) {
-    border_all(b, count);
+    border_all(b, count, rows_fused);
     mark(b, "border");
   }
   if (!(dis & UPHIP_NO_WIPE)) wipes_uniform(b, P, o.post_wipes, count);
