@@ -132,6 +132,33 @@ using namespace uph;
 // ---------------------------------------------------------------------------
 // sources and sinks
 // ---------------------------------------------------------------------------
+// Memory sources and sinks are page-locked (hipHostRegister) on their first
+// run, so the runner's DMA copies read and write the caller's buffers
+// directly instead of going through pinned staging and a host memcpy each way
+// (image_pipeline.c:226-376 stages through pinned buffers because its decode
+// produces frames in pageable memory).  Unregistered on destroy.
+struct HostRegistration {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  bool tried = false;
+  bool ok = false;
+  bool ensure(const void* p, size_t n) {
+    if (tried) return ok;
+    tried = true;
+    ok = hipHostRegister(const_cast<void*>(p), n, hipHostRegisterDefault) == hipSuccess;
+    if (ok) {
+      ptr = const_cast<void*>(p);
+      bytes = n;
+    } else {
+      (void)hipGetLastError();  // registration is an optimisation: staged copies otherwise
+    }
+    return ok;
+  }
+  ~HostRegistration() {
+    if (ok) hipHostUnregister(ptr);
+  }
+};
+
 struct UphipSource {
   UphipLoadFn load = nullptr;
   void* user = nullptr;
@@ -139,6 +166,7 @@ struct UphipSource {
   const uint8_t* base = nullptr;
   int64_t linesize = 0, page_stride = 0, npages = 0;
   std::vector<std::string> paths;
+  HostRegistration reg;
 };
 
 struct UphipSink {
@@ -148,6 +176,7 @@ struct UphipSink {
   int64_t linesize = 0, sheet_stride = 0, nsheets = 0;
   std::string pattern;
   int64_t wrap = 0;
+  HostRegistration reg;
 };
 
 namespace {
@@ -289,6 +318,9 @@ struct Slot {
   UphipBatch* b = nullptr;
   uint8_t* hin = nullptr;   // pinned input staging (count * input_count pages)
   uint8_t* hout = nullptr;  // pinned output staging (count sheets)
+  uint8_t* din = nullptr;   // device copy of a registered memory source's chunk
+  size_t din_bytes = 0;
+  bool direct_out = false;  // this chunk's D2H went straight into the sink
   int64_t first = 0;        // first job of the chunk in flight
   int32_t count = 0;
   std::vector<char> failed;  // per sheet of the chunk
@@ -475,6 +507,7 @@ void uphip_runner_destroy(UphipRunner* r) {
       if (sl.b) uphip_batch_destroy(sl.b);
       if (sl.hin) hipHostFree(sl.hin);
       if (sl.hout) hipHostFree(sl.hout);
+      if (sl.din) hipFree(sl.din);
     }
   }
   delete r;
@@ -573,6 +606,38 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
     if (!ok) return -1;
     r->staged = true;
   }
+  // Direct paths: a memory source whose pages all exist is copied H2D from
+  // the caller's (registered) buffer into a dense device chunk that the batch
+  // reads in place (uphip_batch_run_device takes any pitch); a memory sink
+  // laid out like the batch's output rows receives the D2H copy itself.
+  const int oc = r->opts.output_count < 1 ? 1 : r->opts.output_count;
+  const bool dsrc = src->base && !src->load && src->npages >= njobs * nin && njobs > 0 &&
+                    src->reg.ensure(src->base, (size_t)(src->npages * src->page_stride));
+  const bool dsnk = sink->base && !sink->store && oc == 1 && sink->nsheets >= njobs && njobs > 0 &&
+                    sink->linesize == r->out_linesize && sink->sheet_stride == r->out_sheet_stride &&
+                    sink->reg.ensure(sink->base, (size_t)(sink->nsheets * sink->sheet_stride));
+  if (dsrc) {
+    const size_t need = (size_t)(src->page_stride * S * nin);
+    const int caller_dev = uphip_get_device();
+    bool ok = true;
+    for (DeviceCtx& dc : r->dev) {
+      uphip_set_device(dc.device);
+      for (Slot& sl : dc.slots) {
+        if (sl.din && sl.din_bytes >= need) continue;
+        if (sl.din) hipFree(sl.din);
+        sl.din = nullptr;
+        sl.din_bytes = 0;
+        if (!UPH_HIP(hipMalloc((void**)&sl.din, need))) {
+          sl.din = nullptr;
+          ok = false;
+        } else {
+          sl.din_bytes = need;
+        }
+      }
+    }
+    uphip_set_device(caller_dev);
+    if (!ok) return -1;
+  }
   const auto t0 = Clock::now();
   std::atomic<int64_t> next{0};
   std::atomic<int64_t> load_ns{0}, store_ns{0};
@@ -631,6 +696,25 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
             sl->first = first;
             sl->count = (int32_t)std::min<int64_t>(S, njobs - first);
             sl->failed.assign((size_t)sl->count, 0);
+            if (dsrc) {  // one DMA copy from the caller's pages, then the run
+              const size_t bytes = (size_t)(sl->count * nin * src->page_stride);
+              hipStream_t bst = (hipStream_t)uphip_batch_stream(sl->b);
+              if (!UPH_HIP(hipMemcpyAsync(sl->din, src->base + first * nin * src->page_stride, bytes,
+                                          hipMemcpyHostToDevice, bst)) ||
+                  uphip_batch_run_device(sl->b, sl->count, sl->din, src->linesize,
+                                         src->page_stride) != 0) {
+                note("run failed");
+                for (int s = 0; s < sl->count; s++) sl->failed[(size_t)s] |= 1;
+                phase[k] = STORING;
+                state[k] = FREE;
+              } else {
+                phase[k] = RUNNING;
+                state[k] = RUNNING;
+                inflight.push_back(k);
+              }
+              progress = true;
+              continue;
+            }
             pend[k] = sl->count;
             state[k] = LOADING;
             phase[k] = LOADING;
@@ -679,7 +763,13 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
             std::vector<char> pre = sl->failed;
             collect_failures(*sl);  // the stream is idle: a status read only
             for (size_t s = 0; s < pre.size(); s++) sl->failed[s] |= pre[s];
-            if (uphip_batch_download_async(sl->b, sl->hout, r->out_linesize, r->out_sheet_stride) != 0) {
+            // straight into a memory sink unless a sheet failed (its slot in
+            // the sink stays untouched, as with the store tasks)
+            bool clean = true;
+            for (int s = 0; s < sl->count; s++) clean &= !sl->failed[(size_t)s];
+            sl->direct_out = dsnk && clean;
+            uint8_t* dst = sl->direct_out ? sink->base + sl->first * sink->sheet_stride : sl->hout;
+            if (uphip_batch_download_async(sl->b, dst, r->out_linesize, r->out_sheet_stride) != 0) {
               note("download failed");
               for (int s = 0; s < sl->count; s++) sl->failed[(size_t)s] |= 1;
               inflight.erase(inflight.begin() + (long)q);
@@ -699,7 +789,9 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
           int nstore = 0;
           for (int s = 0; s < sl->count; s++) nstore += !sl->failed[(size_t)s];
           phase[k] = STORING;
-          if (nstore == 0) {
+          if (sl->direct_out) {  // the copy went straight into the sink
+            state[k] = FREE;
+          } else if (nstore == 0) {
             state[k] = FREE;
           } else {
             pend[k] = nstore;
