@@ -152,7 +152,9 @@ __global__ void __launch_bounds__(kThreads) k_copy(CopyLaunch L) {
       // byte copy: dst bytes [tx0*bpp, (tx1+1)*bpp) from src shifted by delta
       const int64_t db0 = (int64_t)tx0 * bpp, db1 = ((int64_t)tx1 + 1) * bpp;
       const int64_t delta = ((int64_t)a.a.x0 - a.tx) * bpp;  // src byte = dst byte + delta
-      if ((delta & 15) == 0) {
+      // 16-byte vectors when source and target rows share their alignment
+      // (pages read in place may come with any pitch)
+      if ((delta & 15) == 0 && (((uintptr_t)srow - (uintptr_t)drow) & 15) == 0) {
         const int64_t c0 = db0 >> 4, c1 = (db1 + 15) >> 4;
         for (int64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) {
           const int64_t b = c << 4;
