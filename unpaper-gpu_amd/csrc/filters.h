@@ -22,8 +22,12 @@ struct GrayGeom {
 bool gray_geometry(int32_t W, int32_t H, const UphipGrayfilterParameters& p, uint8_t black_thr,
                    GrayGeom* g);
 size_t gray_scratch_bytes(const GrayGeom& g);  // per sheet
-void launch_grayfilter(const PlaneRef& img, const GrayGeom& g, void* scratch,
-                       int64_t scratch_stride, const int32_t* active, int count, hipStream_t st);
+// colsum (optional, zeroed by the caller): per-column gray sums over all rows
+// of the image the grayfilter leaves, added into colsum[s * colsum_stride + x]
+// (gray planes only).  Returns whether colsum was produced.
+bool launch_grayfilter(const PlaneRef& img, const GrayGeom& g, void* scratch,
+                       int64_t scratch_stride, const int32_t* active, int count, hipStream_t st,
+                       uint32_t* colsum = nullptr, int64_t colsum_stride = 0);
 
 // ---- blurfilter (filters.c:149-232) -------------------------------------
 struct BlurGeom {

@@ -121,20 +121,32 @@ __global__ void __launch_bounds__(256) k_gray_cells(PlaneRef img, GrayGeom g, ui
 // lane sums aligned dwords of the strip's rows (all of a round's loads in
 // flight) into per-column 16-bit totals in LDS (ch <= 257 keeps 255*ch in
 // 16 bits), then one lane per cell adds its cw columns.
+// With `colsum`, the block's strips also add up per-column gray sums over all
+// rows: the sums the next mask scan takes (detect_mask, masks.c:54-100, on
+// the image the grayfilter leaves; k_gray_wipe adds what its wipes change), so
+// that scan needs no pass of its own.  kGrayStrips strips per block keep the
+// atomics at W per kGrayStrips * ch rows.
 constexpr int kGrayStripMaxW = 16384;
+constexpr int kGrayStrips = 8;
 __global__ void __launch_bounds__(256) k_gray_cells_g(PlaneRef img, GrayGeom g, uint8_t* scratch,
-                                                      int64_t sstride, const int32_t* active) {
+                                                      int64_t sstride, const int32_t* active,
+                                                      uint32_t* colsum, int64_t colsum_stride) {
   const int s = blockIdx.z;
   if (active && !active[s]) return;
-  const int32_t cy = blockIdx.x;
   GrayPtrs P = gray_ptrs(g, scratch + s * sstride);
-  if (cy == 0 && threadIdx.x == 0) *P.nund = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *P.nund = 0;
   const uint8_t* base = plane_ptr(img, s);
-  const int32_t y0 = cy * g.ch, y1 = imin(y0 + g.ch, g.H);
-  extern __shared__ uint16_t cols16[];  // [W] dark counts, then [W] lightness sums
+  extern __shared__ uint16_t cols16[];  // [W] dark counts, [W] lightness sums, then [W] u32 totals
+  const int32_t wq = (g.W + 3) & ~3;
   uint16_t* cdark = cols16;
-  uint16_t* clight = cols16 + ((g.W + 3) & ~3);
+  uint16_t* clight = cols16 + wq;
+  uint32_t* ctot = reinterpret_cast<uint32_t*>(cols16 + 2 * wq);
+  if (colsum)
+    for (int32_t x = threadIdx.x; x < g.W; x += 256) ctot[x] = 0;
   const int32_t nd = (g.W + 3) >> 2;
+  for (int32_t cy = blockIdx.x * kGrayStrips; cy < imin((int32_t)(blockIdx.x + 1) * kGrayStrips, g.ncy);
+       cy++) {
+  const int32_t y0 = cy * g.ch, y1 = imin(y0 + g.ch, g.H);
   // the four columns of a dword accumulate as 16-bit lanes of two words
   // (bytes 0/2 and 1/3); dark bits come from bit 8 of byte + 256 - (thr+1)
   const uint32_t kadd = (256u - ((uint32_t)g.black_thr + 1u)) * 0x00010001u;
@@ -176,6 +188,15 @@ __global__ void __launch_bounds__(256) k_gray_cells_g(PlaneRef img, GrayGeom g, 
     const size_t c = (size_t)cy * g.ncx + cx;
     P.dark[c] = dark;
     P.light[c] = light;
+  }
+  if (colsum)
+    for (int32_t x = threadIdx.x; x < g.W; x += 256) ctot[x] += clight[x];
+  __syncthreads();  // the next strip rewrites the column tables
+  }
+  if (colsum) {
+    uint32_t* out = colsum + (int64_t)s * colsum_stride;
+    for (int32_t x = threadIdx.x; x < g.W; x += 256)
+      if (ctot[x]) atomicAdd(out + x, ctot[x]);
   }
 }
 
@@ -305,7 +326,8 @@ __global__ void __launch_bounds__(1024) k_gray_decide(GrayGeom g, uint8_t* scrat
 
 template <int FMT>
 __global__ void __launch_bounds__(256) k_gray_wipe(PlaneRef img, GrayGeom g, uint8_t* scratch,
-                                                   int64_t sstride, const int32_t* active) {
+                                                   int64_t sstride, const int32_t* active,
+                                                   uint32_t* colsum, int64_t colsum_stride) {
   const int s = blockIdx.z;
   if (active && !active[s]) return;
   const int32_t cx = blockIdx.x * 256 + threadIdx.x, cy = blockIdx.y;
@@ -318,6 +340,15 @@ __global__ void __launch_bounds__(256) k_gray_wipe(PlaneRef img, GrayGeom g, uin
   uint8_t* base = plane_ptr(img, s);
   const int32_t x0 = cx * g.cw, x1 = imin(x0 + g.cw, g.W);
   const int32_t y0 = cy * g.ch, y1 = imin(y0 + g.ch, g.H);
+  if (FMT == F_GRAY8 && colsum) {
+    // the column gray sums (k_gray_cells_g) follow the wipe: + (255 - old)
+    uint32_t* out = colsum + (int64_t)s * colsum_stride;
+    for (int32_t x = x0; x < x1; x++) {
+      uint32_t add = 0;
+      for (int32_t y = y0; y < y1; y++) add += 255u - base[(int64_t)y * img.P.pitch + x];
+      if (add) atomicAdd(out + x, add);
+    }
+  }
   for (int32_t y = y0; y < y1; y++) {
     uint8_t* row = base + (int64_t)y * img.P.pitch;
     for (int32_t x = x0; x < x1; x++) white_px<FMT>(row, x);
@@ -325,28 +356,39 @@ __global__ void __launch_bounds__(256) k_gray_wipe(PlaneRef img, GrayGeom g, uin
 }
 
 template <int FMT>
-static void launch_gray_t(const PlaneRef& img, const GrayGeom& g, uint8_t* scr, int64_t ss,
-                          const int32_t* active, int count, hipStream_t st) {
+static bool launch_gray_t(const PlaneRef& img, const GrayGeom& g, uint8_t* scr, int64_t ss,
+                          const int32_t* active, int count, hipStream_t st, uint32_t* colsum,
+                          int64_t cs) {
   dim3 grid((g.ncx + 255) / 256, g.ncy, count);
-  if (FMT == F_GRAY8 && g.W <= kGrayStripMaxW && g.ch <= 257)
-    UPH_LAUNCH_DIAG(32, k_gray_cells_g, dim3(g.ncy, 1, count), dim3(256),
-                    4 * (size_t)((g.W + 3) & ~3), st, img, g, scr, ss, active);
-  else
+  const bool strips = FMT == F_GRAY8 && g.W <= kGrayStripMaxW && g.ch <= 257;
+  if (!strips) colsum = nullptr;
+  if (strips) {
+    const size_t wq = (size_t)((g.W + 3) & ~3);
+    UPH_LAUNCH_DIAG(32, k_gray_cells_g, dim3((g.ncy + kGrayStrips - 1) / kGrayStrips, 1, count),
+                    dim3(256), 4 * wq + (colsum ? 4 * wq : 0), st, img, g, scr, ss, active, colsum, cs);
+  } else {
     hipLaunchKernelGGL(k_gray_cells<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active);
+  }
   const int32_t ntiles = g.ntx * g.nty;
   hipLaunchKernelGGL(k_gray_tiles, dim3((ntiles + 255) / 256, count), dim3(256), 0, st, g, scr, ss,
                      active);
   if (!(diag_skip() & 4)) hipLaunchKernelGGL(k_gray_decide, dim3(count), dim3(1024), 0, st, g, scr, ss, active);
-  hipLaunchKernelGGL(k_gray_wipe<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active);
+  hipLaunchKernelGGL(k_gray_wipe<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active, colsum, cs);
+  return colsum != nullptr;
 }
 
-void launch_grayfilter(const PlaneRef& img, const GrayGeom& g, void* scratch,
-                       int64_t scratch_stride, const int32_t* active, int count, hipStream_t st) {
+bool launch_grayfilter(const PlaneRef& img, const GrayGeom& g, void* scratch,
+                       int64_t scratch_stride, const int32_t* active, int count, hipStream_t st,
+                       uint32_t* colsum, int64_t colsum_stride) {
   uint8_t* scr = (uint8_t*)scratch;
   switch (img.P.fmt) {
-    case F_GRAY8: launch_gray_t<F_GRAY8>(img, g, scr, scratch_stride, active, count, st); break;
-    case F_Y400A: launch_gray_t<F_Y400A>(img, g, scr, scratch_stride, active, count, st); break;
-    default: launch_gray_t<F_RGB24>(img, g, scr, scratch_stride, active, count, st); break;
+    case F_GRAY8:
+      return launch_gray_t<F_GRAY8>(img, g, scr, scratch_stride, active, count, st, colsum,
+                                    colsum_stride);
+    case F_Y400A:
+      return launch_gray_t<F_Y400A>(img, g, scr, scratch_stride, active, count, st, nullptr, 0);
+    default:
+      return launch_gray_t<F_RGB24>(img, g, scr, scratch_stride, active, count, st, nullptr, 0);
   }
 }
 

@@ -847,14 +847,32 @@ static void resize_all(UphipBatch* b, int32_t& w, int32_t& h, int32_t pw, int32_
   h = ph;
 }
 
-// detect_masks on every sheet -> ctl.masks / ctl.mask_count (masks.c:54-209)
-static void detect_masks_all(UphipBatch* b, int assign, int count) {
+// The first mask scan (sheet_stages.c:393-399) runs on the image the
+// grayfilter leaves; with one point, a horizontal-only scan over every row
+// and a gray plane, its column sums come out of the grayfilter's cell pass
+// (plus its wipes' changes) instead of a pass of their own.
+static bool mask_sums_from_gray(const UphipBatch* b) {
+  const UphipOptions& o = b->o;
+  const UphipMaskDetectionParameters& p = b->mask_params;
+  if (o.disable & (UPHIP_NO_DESKEW | UPHIP_NO_MASK_SCAN | UPHIP_NO_GRAYFILTER)) return false;
+  if (b->points.size() != 1 || !p.scan_direction.horizontal || p.scan_direction.vertical) return false;
+  if (b->work_fmt != F_GRAY8) return false;
+  const int32_t depth = p.scan_depth.horizontal == -1 ? b->H : p.scan_depth.horizontal;
+  const int32_t c0 = b->points[0].y - depth / 2, c1 = c0 + depth - 1;
+  return c0 <= 0 && c1 >= b->H - 1;
+}
+
+// detect_masks on every sheet -> ctl.masks / ctl.mask_count (masks.c:54-209).
+// sums_ready: point 0's horizontal column sums are already in b->sums
+// (mask_sums_from_gray).
+static void detect_masks_all(UphipBatch* b, int assign, int count, bool sums_ready = false) {
   const UphipMaskDetectionParameters& p = b->mask_params;
   if (!p.scan_direction.horizontal && !p.scan_direction.vertical) return;
   const int np = (int)b->points.size();
   const int32_t W = b->W, H = b->H;
   const Planes P = planes_of(b, W, H);
-  UPH_HIP(hipMemsetAsync(b->sums, 0, sizeof(uint32_t) * b->sums_stride * count, b->st));
+  if (!sums_ready)
+    UPH_HIP(hipMemsetAsync(b->sums, 0, sizeof(uint32_t) * b->sums_stride * count, b->st));
   std::vector<EdgeArgs> ea((size_t)np * 4);
   for (int i = 0; i < np; i++) {
     const UphipPoint o = b->points[i];
@@ -864,7 +882,7 @@ static void detect_masks_all(UphipBatch* b, int assign, int count) {
       const int32_t c0 = o.y - depth / 2, c1 = c0 + depth - 1;
       const Rect reg = clip(Rect{0, c0, W - 1, c1}, W, H);
       const int32_t off = (2 * i) * imax(W, H);
-      if (reg.y1 >= reg.y0) {
+      if (reg.y1 >= reg.y0 && !(sums_ready && i == 0)) {
         AxisArgs* aa = replicate(b, AxisArgs{reg, 0, 1});
         launch_axis_reduce(cur_ref(P, b->ctl), aa, 0, M_GRAY_SUM, W, H, b->sums + off,
                            b->sums_stride, count, b->st);
@@ -1126,17 +1144,24 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
     launch_blurfilter(cur_ref(P, b->ctl), b->blgeo, b->scr, b->scr_stride, nullptr, count, b->st);
     mark(b, "blurfilter");
   }
+  bool mask_sums_ready = false;
   // ---- masks (sheet_stages.c:359-386): the first detection is dead for a
   // fresh job (its count is discarded and its masks are overwritten before
   // any read), so it is skipped; mask_count is 0 -> no apply_masks.
   if (!(dis & UPHIP_NO_GRAYFILTER)) {
-    launch_grayfilter(cur_ref(P, b->ctl), b->ggeo, b->scr, b->scr_stride, nullptr, count, b->st);
+    uint32_t* cs = nullptr;
+    if (mask_sums_from_gray(b)) {
+      UPH_HIP(hipMemsetAsync(b->sums, 0, sizeof(uint32_t) * b->sums_stride * count, b->st));
+      cs = b->sums;  // point 0, horizontal: offset 0
+    }
+    mask_sums_ready = launch_grayfilter(cur_ref(P, b->ctl), b->ggeo, b->scr, b->scr_stride, nullptr,
+                                        count, b->st, cs, b->sums_stride);
     mark(b, "grayfilter");
   }
   // ---- deskew (sheet_stages.c:388-413) ---------------------------------
   if (!(dis & UPHIP_NO_DESKEW)) {
     if (!(dis & UPHIP_NO_MASK_SCAN)) {
-      detect_masks_all(b, 1, count);
+      detect_masks_all(b, 1, count, mask_sums_ready);
       mark(b, "masks_deskew");
     }
     const UphipEdges& E = o.deskew_parameters.scan_edges;
