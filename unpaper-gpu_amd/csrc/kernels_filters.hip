@@ -619,9 +619,15 @@ void launch_blurfilter(const PlaneRef& img, const BlurGeom& g, void* scratch,
 //       literally, in raster order, by one wave per sheet.
 //   The parallel path is used for N <= 4 (radius constants below).
 // =========================================================================
-constexpr int kNT = 64;                    // tile edge
+constexpr int kNT = 64;                    // tile height (and width for byte planes)
 constexpr int kHalo = 14;                  // 4 (ring) + 7 (cluster) + 3 (component)
-constexpr int kRW = kNT + 2 * kHalo;       // 92
+constexpr int kRW = kNT + 2 * kHalo;       // 92 region rows
+// GRAY8 tiles are 100 wide: their region rows (from the bit-plane) fill the
+// 128-bit row tables, so the per-row phases cover 100 interior columns
+// instead of 64 for the same work (halo share 2.07 -> 1.84)
+constexpr int kNTG = 100;
+template <int FMT>
+constexpr int noise_tile_w() { return FMT == F_GRAY8 ? kNTG : kNT; }
 constexpr int kZone = 32;                  // sequential edge zone (x or y < 32)
 constexpr int kEligible = kZone + 8;       // parallel only for components at >= 40
 
@@ -871,7 +877,10 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
   int bxi, byi, s;
   xcd_block(&bxi, &byi, &s);
   if (active && !active[s]) return;
-  const int32_t tx0 = bxi * kNT, ty0 = byi * kNT;
+  constexpr int NTX = noise_tile_w<FMT>();  // tile width
+  constexpr int RWX = NTX + 2 * kHalo;       // region columns (<= 128)
+  static_assert(RWX > 64 && RWX <= 128, "region rows are two 64-bit halves");
+  const int32_t tx0 = bxi * NTX, ty0 = byi * kNT;
   const int32_t ox = tx0 - kHalo, oy = ty0 - kHalo;  // region origin
   const uint8_t* base = plane_ptr(img, s);
   NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
@@ -881,6 +890,9 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
   //   bits for gray planes), srow small (component <= 4 pixels)
   constexpr bool kGray = FMT == F_GRAY8;
   constexpr bool kSplit = FMT == F_RGB24;
+  // interior columns [kHalo, kHalo + NTX) of a region row's halves
+  constexpr uint64_t kIn0 = ~0ull << kHalo;
+  constexpr uint64_t kIn1 = (1ull << (kHalo + NTX - 64)) - 1ull;
   __shared__ uint32_t drow[kRW][4];
   __shared__ uint32_t trow_s[kSplit ? kRW : 1][4];
   __shared__ uint32_t srow[kRW][4];
@@ -897,7 +909,7 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
   for (int i = threadIdx.x; i < kRW * 4; i += 256) (&srow[0][0])[i] = 0;
   if constexpr (kGray) {
     // Region rows from the dark bit-plane (k_noise_bits): row ry is bits
-    // [ox, ox + kRW) of plane row oy + ry, five words realigned by ox mod 32;
+    // [ox, ox + RWX) of plane row oy + ry, five words realigned by ox mod 32;
     // words outside the row or the image read as 0
     bool dark_here = false;
     if (threadIdx.x < kRW) {
@@ -906,24 +918,28 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
       const int32_t nwr = (g.W + 31) >> 5;
       const int32_t wb = ox >> 5;  // floor(ox / 32) (arithmetic shift)
       const int sh = ox & 31;
-      uint32_t q[4] = {0u, 0u, 0u, 0u};
+      uint32_t q[5] = {0u, 0u, 0u, 0u, 0u};
       if (gy >= 0 && gy < g.H) {
         const uint32_t* row = bits + s * bstride + (int64_t)gy * nwr;
 #pragma unroll
-        for (int j = 0; j < 4; j++)
+        for (int j = 0; j < 5; j++)
           if (wb + j >= 0 && wb + j < nwr) q[j] = row[wb + j];
       }
       uint32_t d[4];
 #pragma unroll
-      for (int j = 0; j < 3; j++) d[j] = __builtin_amdgcn_alignbit(q[j + 1], q[j], sh);
-      d[2] &= (1u << (kRW - 64)) - 1u;  // region columns >= kRW
-      d[3] = 0u;
-      static_assert(kRW > 64 && kRW <= 96, "three words per region row");
+      for (int j = 0; j < 4; j++) d[j] = __builtin_amdgcn_alignbit(q[j + 1], q[j], sh);
+      if (RWX < 128) {  // region columns >= RWX
+        if (RWX <= 96) {
+          d[2] &= RWX > 64 ? (1u << (RWX - 64)) - 1u : 0u;
+          d[3] = 0u;
+        } else {
+          d[3] &= (1u << (RWX - 96)) - 1u;
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 4; j++) drow[ry][j] = d[j];
-      // interior columns [kHalo, kHalo + kNT) = bits 14..63 | 64..77
       const uint64_t lo64 = ((uint64_t)d[1] << 32) | d[0], hi64 = ((uint64_t)d[3] << 32) | d[2];
-      dark_here = ry >= kHalo && ry < kHalo + kNT && ((lo64 >> kHalo) | (hi64 & 0x3FFFull));
+      dark_here = ry >= kHalo && ry < kHalo + kNT && ((lo64 & kIn0) | (hi64 & kIn1));
     }
     __syncthreads();  // any_dark's reset (thread 0, above) lands first
     if (dark_here) any_dark = 1;
@@ -931,7 +947,7 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
     // Stage the region rows into LDS with 16-byte loads, all issued before
     // any is consumed.  Rows start 256-byte aligned, so every vector lies
     // inside its row's pitch; out-of-image pixels are masked below.
-    constexpr int NV = (kRW * B + 30) / 16;             // vectors per region row
+    constexpr int NV = (RWX * B + 30) / 16;             // vectors per region row
     constexpr int NLOAD = (kRW * NV + 255) / 256;       // loads per thread
     __shared__ uint4 stage[kRW][NV];
     const int64_t sb = (int64_t)ox * B;
@@ -961,8 +977,8 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int rx = h * 64 + lane;
-      colok[h] = (rx < kRW) & (ox + rx >= 0) & (ox + rx < g.W);
-      rxc[h] = rx < kRW ? rx : 0;
+      colok[h] = (rx < RWX) & (ox + rx >= 0) & (ox + rx < g.W);
+      rxc[h] = rx < RWX ? rx : 0;
     }
     bool tile_dark = false;
     for (int ry = w; ry < kRW; ry += 4) {
@@ -990,9 +1006,7 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
           trow[ry][lane] = (uint32_t)(lane & 1 ? t >> 32 : t);
         }
       }
-      // interior columns [kHalo, kHalo + kNT) = bits 14..63 | 64..77
-      if (ry >= kHalo && ry < kHalo + kNT && ((md[0] >> kHalo) | (md[1] & 0x3FFFull)))
-        tile_dark = true;
+      if (ry >= kHalo && ry < kHalo + kNT && ((md[0] & kIn0) | (md[1] & kIn1))) tile_dark = true;
     }
     if (lane == 0 && tile_dark) any_dark = 1;
   }
@@ -1039,19 +1053,20 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
     l3[hr][hh] = dark64(hr, hh) & (c3 | (c2 & (c1 | c0)));  // count >= 5: 8 | (4 & (2 | 1))
   }
   __syncthreads();
-  // candidates within radius 10 of the tile (region rows/cols [4, 88)),
-  // appended to the tile's work list as (row << 8 | column)
+  // candidates within radius 10 of the tile (region rows [4, kRW - 4),
+  // columns [4, RWX - 4)), appended to the tile's work list as
+  // (row << 8 | column)
   if (threadIdx.x < 2 * kRW) {
     uint64_t c = 0;
-    if (hr >= 4 && hr < 88) {
+    if (hr >= 4 && hr < kRW - 4) {
       uint64_t dil = 0;
 #pragma unroll
       for (int d = -1; d <= 1; d++) {
         const uint64_t a0 = l3[hr + d][0], a1 = l3[hr + d][1];
         dil |= hh ? a1 | (a1 << 1) | (a0 >> 63) | (a1 >> 1) : a0 | (a0 << 1) | (a0 >> 1) | (a1 << 63);
       }
-      // bits 4..63 of word 0, 64..87 of word 1
-      c = dark64(hr, hh) & ~dil & (hh ? 0xFFFFFFull : ~0xFull);
+      // bits 4..63 of half 0, 64..RWX-5 of half 1
+      c = dark64(hr, hh) & ~dil & (hh ? (1ull << (RWX - 4 - 64)) - 1ull : ~0xFull);
     }
     cand[hr][hh] = c;
     if (c) {
@@ -1102,20 +1117,26 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
     // edge zone (and intensity > 4): every trigger there is replayed in
     // order; the tile's rows, one wave per row, lanes on the tile's columns
     for (int t = w; t < kNT; t += 4) {
-      const int ry = kHalo + t, rx = kHalo + lane;
-      const int32_t gy = oy + ry, gx = ox + rx;
-      const bool trig = (trow[ry][rx >> 5] >> (rx & 31)) & 1;
-      const bool zone = g.all_seq || gx < kZone || gy < kZone;
-      const bool dark = (drow[ry][rx >> 5] >> (rx & 31)) & 1;
-      wave_append(dark & zone & trig, gx, gy, NP.nseq, NP.seq, g.capacity);
+#pragma unroll 1
+      for (int h = 0; h < (NTX + 63) / 64; h++) {
+        const int ry = kHalo + t, cx = h * 64 + lane, rx = kHalo + (cx < NTX ? cx : 0);
+        const int32_t gy = oy + ry, gx = ox + rx;
+        const bool trig = (trow[ry][rx >> 5] >> (rx & 31)) & 1;
+        const bool zone = g.all_seq || gx < kZone || gy < kZone;
+        const bool dark = (drow[ry][rx >> 5] >> (rx & 31)) & 1;
+        wave_append(cx < NTX && dark & zone & trig, gx, gy, NP.nseq, NP.seq, g.capacity);
+      }
     }
   }
   // small pixels of the tile outside the zone: one lane each
   if (threadIdx.x == 0) nwl = 0;
   __syncthreads();
-  if (threadIdx.x < 2 * kNT) {
-    const int ry = kHalo + (threadIdx.x >> 1), h = threadIdx.x & 1;
-    uint32_t m = row_bits(srow[ry], kHalo + 32 * h, 32);
+  // (row, 32-column chunk) per thread: 2 or 4 chunks a row
+  constexpr int kChunks = (NTX + 31) / 32;
+  static_assert(kChunks * kNT <= 256, "one thread per chunk");
+  if (threadIdx.x < kChunks * kNT) {
+    const int ry = kHalo + (threadIdx.x / kChunks), h = threadIdx.x % kChunks;
+    uint32_t m = row_bits(srow[ry], kHalo + 32 * h, imin(32, NTX - 32 * h));
     if (m && !g.all_seq && oy + ry >= kZone) {
       const int32_t gx0 = ox + kHalo + 32 * h;  // column of bit 0
       if (gx0 < kZone) m &= kZone - gx0 >= 32 ? 0u : ~((1u << (kZone - gx0)) - 1u);
@@ -1149,18 +1170,25 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
     }
   } else {
     for (int t = w; t < kNT; t += 4) {
-      const int ry = kHalo + t, rx = kHalo + lane;
-      const int32_t gy = oy + ry, gx = ox + rx;
-      if (!(row_bits(srow[ry], kHalo, 32) | row_bits(srow[ry], kHalo + 32, 32))) continue;  // uniform
-      const bool zone = g.all_seq || gx < kZone || gy < kZone;
-      const bool small = !zone && ((srow[ry][rx >> 5] >> (rx & 31)) & 1);
-      SmallVerdict v{false, false};
-      if (small) {
-        const bool trig = (trow[ry][rx >> 5] >> (rx & 31)) & 1;
-        v = small_verdict(drow, trow, srow, rx, ry, gx, gy, trig, N);
+      const int ry = kHalo + t;
+      uint32_t any = 0;
+#pragma unroll
+      for (int h = 0; h < kChunks; h++) any |= row_bits(srow[ry], kHalo + 32 * h, imin(32, NTX - 32 * h));
+      if (!any) continue;  // uniform
+#pragma unroll 1
+      for (int h = 0; h < (NTX + 63) / 64; h++) {
+        const int cx = h * 64 + lane, rx = kHalo + (cx < NTX ? cx : 0);
+        const int32_t gy = oy + ry, gx = ox + rx;
+        const bool zone = g.all_seq || gx < kZone || gy < kZone;
+        const bool small = cx < NTX && !zone && ((srow[ry][rx >> 5] >> (rx & 31)) & 1);
+        SmallVerdict v{false, false};
+        if (small) {
+          const bool trig = (trow[ry][rx >> 5] >> (rx & 31)) & 1;
+          v = small_verdict(drow, trow, srow, rx, ry, gx, gy, trig, N);
+        }
+        wave_append(v.seq, gx, gy, NP.nseq, NP.seq, g.capacity);
+        wave_append(v.clear, gx, gy, NP.nclear, NP.clear, g.capacity);
       }
-      wave_append(v.seq, gx, gy, NP.nseq, NP.seq, g.capacity);
-      wave_append(v.clear, gx, gy, NP.nclear, NP.clear, g.capacity);
     }
   }
 }
@@ -1565,7 +1593,8 @@ template <int FMT>
 static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr, int64_t ss,
                            const int32_t* active, SheetCtl* ctl, int count, hipStream_t st,
                            uint32_t* sortbuf, int64_t sort_stride) {
-  dim3 grid((g.W + kNT - 1) / kNT, (g.H + kNT - 1) / kNT, count);
+  constexpr int ntx = noise_tile_w<FMT>();
+  dim3 grid((g.W + ntx - 1) / ntx, (g.H + kNT - 1) / kNT, count);
   NoiseGeom gd = g;
   gd.diag = diag_noise();
   uint32_t* bits = nullptr;
