@@ -23,6 +23,12 @@ namespace uph {
 
 typedef float lf2 __attribute__((ext_vector_type(2)));
 
+// byte K of w as a float (one v_cvt_f32_ubyteK)
+template <int K>
+__device__ __forceinline__ float ubyte_f(uint32_t w) {
+  return (float)((w >> (8 * K)) & 0xFFu);
+}
+
 constexpr int kLW = 64;                    // output columns per tile (one per lane)
 constexpr int kLH = 32;                    // output rows per tile
 constexpr int kLT = 256;                   // 4 waves, kLH / 4 consecutive rows each
@@ -160,32 +166,46 @@ __global__ void __launch_bounds__(kLT) k_rotate_lin(PlaneRef src, PlaneRef dst, 
     __syncthreads();
     const int32_t bx0 = wb[0], by0 = wb[1];
     const int32_t bw = wb[2] + 1 - bx0 + 1, bh = wb[3] + 1 - by0 + 1;
-    const bool staged = bw <= win.cols && bh <= win.rows;
+    const int32_t bxa = bx0 & ~3;  // staged from a multiple of 4 (floor for negatives)
+    const bool staged = bx0 + bw - bxa <= win.cols && bh <= win.rows;
     if (staged) {
-      // window bytes [bx0 C, (bx0 + bw) C) of rows by0 .. by0 + bh - 1, one
-      // aligned dword per lane: each byte to its channel plane as a float
-      const int64_t b0 = (int64_t)bx0 * C, b1 = (int64_t)(bx0 + bw) * C;
-      const int64_t da = b0 >= 0 ? (b0 & ~(int64_t)3) : -((-b0 + 3) & ~(int64_t)3);
-      const int32_t nd = (int32_t)((b1 - da + 3) >> 2);
-      const int64_t rowmax = (int64_t)P.W * C;
-      for (int i = tid; i < bh * nd; i += kLT) {
-        const int r = i / nd, k = i - r * nd;
-        const int32_t y = by0 + r;
-        const int64_t bo = da + 4 * k;
-        uint32_t w = 0xFFFFFFFFu;
-        if (y >= 0 && y < P.H && bo >= 0 && bo + 4 <= P.pitch)
-          w = *reinterpret_cast<const uint32_t*>(sbase + (int64_t)y * P.pitch + bo);
+      // window columns [bxa, bx0 + bw) (bxa = bx0 rounded down to 4) of rows
+      // by0 .. by0 + bh - 1, four pixels per item: one 4- or 12-byte load,
+      // one 16-byte LDS store per channel plane
+      const int32_t ngrp = (bx0 + bw - bxa + 3) >> 2;
+      for (int i = tid; i < bh * ngrp; i += kLT) {
+        const int r = i / ngrp, gq = i - r * ngrp;
+        const int32_t y = by0 + r, x = bxa + 4 * gq;
+        const bool rowok = y >= 0 && y < P.H;
+        const uint8_t* row = sbase + (int64_t)(rowok ? y : 0) * P.pitch;
+        float4 q[C];
+        if (rowok && x >= 0 && x + 4 <= P.W) {
+          if constexpr (C == 3) {
+            const uint32_t* p3 = reinterpret_cast<const uint32_t*>(row + 3 * (int64_t)x);
+            const uint32_t w0 = p3[0], w1 = p3[1], w2 = p3[2];  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
+            q[0] = make_float4(ubyte_f<0>(w0), ubyte_f<3>(w0), ubyte_f<2>(w1), ubyte_f<1>(w2));
+            q[1] = make_float4(ubyte_f<1>(w0), ubyte_f<0>(w1), ubyte_f<3>(w1), ubyte_f<2>(w2));
+            q[2] = make_float4(ubyte_f<2>(w0), ubyte_f<1>(w1), ubyte_f<0>(w2), ubyte_f<3>(w2));
+          } else {
+            const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + x);
+            q[0] = make_float4(ubyte_f<0>(w0), ubyte_f<1>(w0), ubyte_f<2>(w0), ubyte_f<3>(w0));
+          }
+        } else {
+          // window edge: pixels outside the image are white (get_pixel)
+          float v[C][4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int64_t b = bo + j;
-          if (b < b0 || b >= b1) continue;
-          const uint32_t v = (b >= 0 && b < rowmax && y >= 0 && y < P.H) ? (w >> (8 * j)) & 0xFFu : 255u;
-          // window byte bb = b - b0 (b0 is bx0 * C): column bb / C, channel bb % C
-          const uint32_t bb = (uint32_t)(b - b0);
-          const uint32_t col = C == 3 ? (bb * 0xAAABu) >> 17 : bb;  // bb / 3 for bb < 2^16
-          const uint32_t ch = bb - C * col;
-          lw[ch * plane_f + r * win.stride + col] = (float)v;
+          for (int j = 0; j < 4; j++) {
+            const int32_t xx = x + j;
+            const bool in = rowok && xx >= 0 && xx < P.W;
+#pragma unroll
+            for (int c = 0; c < C; c++) v[c][j] = in ? (float)row[(int64_t)xx * C + c] : 255.0f;
+          }
+#pragma unroll
+          for (int c = 0; c < C; c++) q[c] = make_float4(v[c][0], v[c][1], v[c][2], v[c][3]);
         }
+#pragma unroll
+        for (int c = 0; c < C; c++)
+          *reinterpret_cast<float4*>(lw + c * plane_f + r * win.stride + 4 * gq) = q[c];
       }
     }
     __syncthreads();
@@ -218,7 +238,7 @@ __global__ void __launch_bounds__(kLT) k_rotate_lin(PlaneRef src, PlaneRef dst, 
       const float fx1 = floorf(cx), fy1 = floorf(cy);
       const int32_t x1 = (int32_t)fx1, y1 = (int32_t)fy1;
       const int32_t x2 = (int32_t)ceilf(cx), y2 = (int32_t)ceilf(cy);
-      const int32_t i11 = (y1 - by0) * win.stride + (x1 - bx0);
+      const int32_t i11 = (y1 - by0) * win.stride + (x1 - bxa);
       // interp_bilinear (interpolate.c:77-118): outside the image or with an
       // integral coordinate the result is the pixel (x1, y1) -- the one-axis
       // cases use the other axis' zero fraction
@@ -275,10 +295,11 @@ LinWindow lin_window(float max_abs_angle) {
   const float sn = sinf(a), cs = cosf(a);
   LinWindow w;
   // (n-1) cos + (m-1) sin pixel centres, + 1 for ceil, + 2 for the floor of
-  // the bounds and the rounding of the corner products
-  w.cols = (int32_t)ceilf((kLW - 1) * cs + (kLH - 1) * sn) + 4;
+  // the bounds and the rounding of the corner products; columns + 3 for the
+  // start rounded down to a multiple of 4 and up to whole groups of 4
+  w.cols = ((int32_t)ceilf((kLW - 1) * cs + (kLH - 1) * sn) + 4 + 3 + 3) & ~3;
   w.rows = (int32_t)ceilf((kLH - 1) * cs + (kLW - 1) * sn) + 4;
-  w.stride = (w.cols + 7) & ~7;
+  w.stride = w.cols;
   return w;
 }
 

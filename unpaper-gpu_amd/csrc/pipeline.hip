@@ -147,23 +147,43 @@ __global__ void k_rot_independent(const SheetCtl* ctl, const RotateArgs* args, i
     };
     d = meets(m0, m1);
     if (!d && a1.active) {
+      // mask 1's source footprint is a rotated rectangle: in source space
+      // (deskew.c:264-268) the point of mask pixel (u, v) is C + (u - tcx) e_u
+      // + (v - tcy) e_v with e_u = (cos, -sin), e_v = (sin, cos).  It meets
+      // mask 0 unless an axis of either separates them (x, y, e_u, e_v);
+      // 4 px of margin cover the interpolation taps and float rounding.
       const Rect nm = normalize(a1.mask);
       const int32_t sw = nm.x1 - nm.x0 + 1, sh = nm.y1 - nm.y0 + 1;
       const float scx = nm.x0 + sw / 2.0f, scy = nm.y0 + sh / 2.0f;
       const float tcx = 0 + sw / 2.0f, tcy = 0 + sh / 2.0f;
+      const float cs = a1.cosval, sn = a1.sinval, mg = 4.0f;
       float mnx = 3.0e38f, mxx = -3.0e38f, mny = 3.0e38f, mxy = -3.0e38f;
       for (int k = 0; k < 4; k++) {
         const int32_t u = k & 1 ? sw - 1 : 0, v = k & 2 ? sh - 1 : 0;
-        const float X = scx + (u - tcx) * a1.cosval + (v - tcy) * a1.sinval;
-        const float Y = scy + (v - tcy) * a1.cosval - (u - tcx) * a1.sinval;
+        const float X = scx + (u - tcx) * cs + (v - tcy) * sn;
+        const float Y = scy + (v - tcy) * cs - (u - tcx) * sn;
         mnx = fminf(mnx, X);
         mxx = fmaxf(mxx, X);
         mny = fminf(mny, Y);
         mxy = fmaxf(mxy, Y);
       }
-      const Rect w{(int32_t)floorf(mnx) - 2, (int32_t)floorf(mny) - 2, (int32_t)floorf(mxx) + 3,
-                   (int32_t)floorf(mxy) + 3};
-      d = meets(w, m0);
+      bool sep = mxx + mg < (float)m0.x0 || mnx - mg > (float)m0.x1 || mxy + mg < (float)m0.y0 ||
+                 mny - mg > (float)m0.y1;
+      if (!sep) {
+        // mask 0's corners on the footprint's own axes
+        float au = 3.0e38f, bu = -3.0e38f, av = 3.0e38f, bv = -3.0e38f;
+        for (int k = 0; k < 4; k++) {
+          const float dx = (float)(k & 1 ? m0.x1 : m0.x0) - scx;
+          const float dy = (float)(k & 2 ? m0.y1 : m0.y0) - scy;
+          const float pu = dx * cs - dy * sn, pv = dx * sn + dy * cs;
+          au = fminf(au, pu);
+          bu = fmaxf(bu, pu);
+          av = fminf(av, pv);
+          bv = fmaxf(bv, pv);
+        }
+        sep = bu + mg < -tcx || au - mg > (sw - 1) - tcx || bv + mg < -tcy || av - mg > (sh - 1) - tcy;
+      }
+      d = !sep;
     }
   }
   dep[s] = d;
