@@ -42,6 +42,13 @@ __device__ __forceinline__ lf2 lin2(float xm, float x, lf2 a, lf2 b) {
   const lf2 s = t + u;
   return lf2{__builtin_truncf(s.x), __builtin_truncf(s.y)};
 }
+// the same on two pixels, each with its own fraction
+__device__ __forceinline__ lf2 lin2v(lf2 xm, lf2 x, lf2 a, lf2 b) {
+  const lf2 t = xm * a;
+  const lf2 u = x * b;
+  const lf2 s = t + u;
+  return lf2{__builtin_truncf(s.x), __builtin_truncf(s.y)};
+}
 __device__ __forceinline__ float lin1(float xm, float x, float a, float b) {
   const float t = xm * a, u = x * b;
   return __builtin_truncf(t + u);
@@ -127,10 +134,12 @@ __global__ void __launch_bounds__(kLT) k_rotate_lin(PlaneRef src, PlaneRef dst, 
       if (16 * j < rowb) {
         if (vec_ok(j)) {
           v = *reinterpret_cast<const uint4*>(sp);
-        } else {
-          uint8_t t[16];
-          for (int k = 0; k < 16; k++) t[k] = 16 * j + k < rowb ? sp[k] : 0;
-          v = *reinterpret_cast<const uint4*>(t);
+        } else {  // the row's last bytes, one at a time (no array: it would live in scratch)
+          uint32_t wv4[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+          for (int k = 0; k < 16; k++)
+            if (16 * j + k < rowb) wv4[k >> 2] |= (uint32_t)sp[k] << (8 * (k & 3));
+          v = make_uint4(wv4[0], wv4[1], wv4[2], wv4[3]);
         }
       }
       *reinterpret_cast<uint4*>(obuf + r * kRowB + 16 * j) = v;
@@ -139,8 +148,10 @@ __global__ void __launch_bounds__(kLT) k_rotate_lin(PlaneRef src, PlaneRef dst, 
   // 2. every mask that rotates part of the tile (disjoint when both do)
 #pragma unroll 1
   for (int m = 0; m < 2; m++) {
-    if (!hit[m]) continue;
-    const RotateArgs a = am[m];
+    // static indices only (a run-time index would put the arrays in scratch)
+    if (!(m == 0 ? hit[0] : hit[1])) continue;
+    const RotateArgs a = m == 0 ? am[0] : am[1];
+    const MaskPart mpm = m == 0 ? mp[0] : mp[1];
     const Rect nm = normalize(a.mask);
     const int32_t sw = nm.x1 - nm.x0 + 1, sh = nm.y1 - nm.y0 + 1;
     const float scx = nm.x0 + sw / 2.0f, scy = nm.y0 + sh / 2.0f;  // primitives.c:137-145
@@ -150,7 +161,7 @@ __global__ void __launch_bounds__(kLT) k_rotate_lin(PlaneRef src, PlaneRef dst, 
     // taps are floor(c) .. ceil(c) <= floor(c) + 1
     if (wv == 0) {
       const int c = lane & 3;
-      const int32_t u = c & 1 ? mp[m].cu1 : mp[m].cu0, v = c & 2 ? mp[m].cv1 : mp[m].cv0;
+      const int32_t u = c & 1 ? mpm.cu1 : mpm.cu0, v = c & 2 ? mpm.cv1 : mpm.cv0;
       const float X = scx + (u - tcx) * a.cosval + (v - tcy) * a.sinval;
       const float Y = scy + (v - tcy) * a.cosval - (u - tcx) * a.sinval;
       float mnx = X, mxx = X, mny = Y, mxy = Y;
@@ -215,59 +226,69 @@ __global__ void __launch_bounds__(kLT) k_rotate_lin(PlaneRef src, PlaneRef dst, 
     const bool colin = x < P.W && u >= 0 && u < sw;
     const float cu = u - tcx;
     const float ax = scx + cu * a.cosval, bs = cu * a.sinval;
-    const Src<FMT> S{sbase, P.pitch, P.W, P.H};
-#pragma unroll 2
-    for (int k = 0; k < kLRows; k++) {
-      const int r = wv * kLRows + k;
-      const int32_t y = ty0 + r;
-      const int32_t v = y - a.mask.y0;
-      if (!(colin && y < P.H && v >= 0 && v < sh)) continue;
+    // source coordinates of the pixel in tile row r (deskew.c:264-268)
+    auto coords = [&](int r, float* cx, float* cy) -> bool {
+      const int32_t y = ty0 + r, v = y - a.mask.y0;
       const float cv = v - tcy;
-      const float cx = ax + cv * a.sinval;          // scx + (u-tcx) cos + (v-tcy) sin
-      const float cy = (scy + cv * a.cosval) - bs;  // scy + (v-tcy) cos - (u-tcx) sin
-      uint8_t* o = obuf + r * kRowB + lane * C;
-      if (!staged) {
+      *cx = ax + cv * a.sinval;          // scx + (u-tcx) cos + (v-tcy) sin
+      *cy = (scy + cv * a.cosval) - bs;  // scy + (v-tcy) cos - (u-tcx) sin
+      return colin && y < P.H && v >= 0 && v < sh;
+    };
+    if (!staged) {
+      // window too large for LDS (angles far beyond the scan range): taps
+      // from the frame
+      const Src<FMT> S{sbase, P.pitch, P.W, P.H};
+#pragma unroll 1
+      for (int k = 0; k < kLRows; k++) {
+        const int r = wv * kLRows + k;
+        float cx, cy;
+        if (!coords(r, &cx, &cy)) continue;
         const Px p = interp_bilinear(S, cx, cy);
+        uint8_t* o = obuf + r * kRowB + lane * C;
         o[0] = p.r;
         if (C == 3) {
           o[1] = p.g;
           o[2] = p.b;
         }
-        continue;
       }
-      const float fx1 = floorf(cx), fy1 = floorf(cy);
-      const int32_t x1 = (int32_t)fx1, y1 = (int32_t)fy1;
-      const int32_t x2 = (int32_t)ceilf(cx), y2 = (int32_t)ceilf(cy);
-      const int32_t i11 = (y1 - by0) * win.stride + (x1 - bxa);
-      // interp_bilinear (interpolate.c:77-118): outside the image or with an
-      // integral coordinate the result is the pixel (x1, y1) -- the one-axis
-      // cases use the other axis' zero fraction
-      const bool plain = !(x2 >= 0 && x2 <= P.W - 1 && y2 >= 0 && y2 <= P.H - 1) || x1 == x2 || y1 == y2;
-      if (plain) {
+    } else {
+      // rows r and r + kLRows/2 as one packed pair (A, B): every operation of
+      // linear_scale on both pixels at once, each channel in turn
+#pragma unroll 1
+      for (int k = 0; k < kLRows / 2; k++) {
+        const int rA = wv * kLRows + k, rB = rA + kLRows / 2;
+        float cxA, cyA, cxB, cyB;
+        const bool inA = coords(rA, &cxA, &cyA), inB = coords(rB, &cxB, &cyB);
+        if (!(inA || inB)) continue;
+        // interp_bilinear (interpolate.c:77-118): x2 = ceil = x1 + 1 unless
+        // the coordinate is integral; outside the image or with an integral
+        // coordinate the result is the pixel (x1, y1) -- the one-axis cases
+        // use the other axis' zero fraction
+        const float fxA1 = floorf(cxA), fyA1 = floorf(cyA), fxB1 = floorf(cxB), fyB1 = floorf(cyB);
+        const lf2 FX{cxA - fxA1, cxB - fxB1}, FY{cyA - fyA1, cyB - fyB1};
+        const int32_t xA = (int32_t)fxA1, yA = (int32_t)fyA1, xB = (int32_t)fxB1, yB = (int32_t)fyB1;
+        const bool plainA = FX.x == 0.0f || FY.x == 0.0f || xA + 1 < 0 || xA + 1 > P.W - 1 ||
+                            yA + 1 < 0 || yA + 1 > P.H - 1;
+        const bool plainB = FX.y == 0.0f || FY.y == 0.0f || xB + 1 < 0 || xB + 1 > P.W - 1 ||
+                            yB + 1 < 0 || yB + 1 > P.H - 1;
+        const lf2 FXM = lf2{1.0f, 1.0f} - FX, FYM = lf2{1.0f, 1.0f} - FY;
+        // (x1, y1) .. (x1 + 1, y1 + 1) lie in the window for every in-mask
+        // pixel; pixels outside the mask read the window origin
+        const int32_t iA = inA ? (yA - by0) * win.stride + (xA - bxa) : 0;
+        const int32_t iB = inB ? (yB - by0) * win.stride + (xB - bxa) : 0;
+        uint8_t* oA = obuf + rA * kRowB + lane * C;
+        uint8_t* oB = obuf + rB * kRowB + lane * C;
 #pragma unroll
-        for (int c = 0; c < C; c++) o[c] = (uint8_t)lw[c * plane_f + i11];
-        continue;
-      }
-      const float fx = cx - fx1, fy = cy - fy1;
-      const float fxm = 1.0f - fx, fym = 1.0f - fy;
-      const int32_t i21 = i11 + win.stride;
-      if (C == 3) {
-        const lf2 a11{lw[i11], lw[plane_f + i11]}, a21{lw[i11 + 1], lw[plane_f + i11 + 1]};
-        const lf2 a12{lw[i21], lw[plane_f + i21]}, a22{lw[i21 + 1], lw[plane_f + i21 + 1]};
-        const float b11 = lw[2 * plane_f + i11], b21 = lw[2 * plane_f + i11 + 1];
-        const float b12 = lw[2 * plane_f + i21], b22 = lw[2 * plane_f + i21 + 1];
-        const lf2 h1 = lin2(fxm, fx, a11, a21), h2 = lin2(fxm, fx, a12, a22);
-        const lf2 rg = lin2(fym, fy, h1, h2);
-        const float hb1 = lin1(fxm, fx, b11, b21), hb2 = lin1(fxm, fx, b12, b22);
-        const float bb = lin1(fym, fy, hb1, hb2);
-        o[0] = (uint8_t)(uint32_t)rg.x;
-        o[1] = (uint8_t)(uint32_t)rg.y;
-        o[2] = (uint8_t)(uint32_t)bb;
-      } else {
-        // (h1, h2) as one pair: rows y1 and y2, columns x1 then x2
-        const lf2 c1{lw[i11], lw[i21]}, c2{lw[i11 + 1], lw[i21 + 1]};
-        const lf2 h = lin2(fxm, fx, c1, c2);
-        o[0] = (uint8_t)(uint32_t)lin1(fym, fy, h.x, h.y);
+        for (int c = 0; c < C; c++) {
+          const float* q = lw + c * plane_f;
+          const lf2 p11{q[iA], q[iB]}, p21{q[iA + 1], q[iB + 1]};
+          const lf2 p12{q[iA + win.stride], q[iB + win.stride]};
+          const lf2 p22{q[iA + win.stride + 1], q[iB + win.stride + 1]};
+          const lf2 h1 = lin2v(FXM, FX, p11, p21), h2 = lin2v(FXM, FX, p12, p22);
+          const lf2 o = lin2v(FYM, FY, h1, h2);
+          if (inA) oA[c] = (uint8_t)(uint32_t)(plainA ? p11.x : o.x);
+          if (inB) oB[c] = (uint8_t)(uint32_t)(plainB ? p11.y : o.y);
+        }
       }
     }
     __syncthreads();  // the next mask restages the window
@@ -283,8 +304,10 @@ __global__ void __launch_bounds__(kLT) k_rotate_lin(PlaneRef src, PlaneRef dst, 
       if (vec_ok(j) && 16 * (j + 1) <= rowb) {
         *reinterpret_cast<uint4*>(dp) = v;
       } else {
-        const uint8_t* t = reinterpret_cast<const uint8_t*>(&v);
-        for (int k = 0; k < 16 && 16 * j + k < rowb; k++) dp[k] = t[k];
+        const uint32_t wv4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+          if (16 * j + k < rowb) dp[k] = (uint8_t)(wv4[k >> 2] >> (8 * (k & 3)));
       }
     }
   }
