@@ -252,42 +252,35 @@ __global__ void __launch_bounds__(kLT) k_rotate_lin(PlaneRef src, PlaneRef dst, 
         }
       }
     } else {
-      // rows r and r + kLRows/2 as one packed pair (A, B): every operation of
-      // linear_scale on both pixels at once, each channel in turn
-#pragma unroll 1
-      for (int k = 0; k < kLRows / 2; k++) {
-        const int rA = wv * kLRows + k, rB = rA + kLRows / 2;
-        float cxA, cyA, cxB, cyB;
-        const bool inA = coords(rA, &cxA, &cyA), inB = coords(rB, &cxB, &cyB);
-        if (!(inA || inB)) continue;
+      // linear_scale as one packed multiply of (1 - f, f) by the tap pair
+      // (a, b) -- the pair one ds_read2_b32 returns -- then the add and the
+      // truncation: every rounding of (1.0f - f) * a + f * b kept
+#pragma unroll 2
+      for (int k = 0; k < kLRows; k++) {
+        const int r = wv * kLRows + k;
+        float cx, cy;
+        if (!coords(r, &cx, &cy)) continue;
         // interp_bilinear (interpolate.c:77-118): x2 = ceil = x1 + 1 unless
         // the coordinate is integral; outside the image or with an integral
         // coordinate the result is the pixel (x1, y1) -- the one-axis cases
         // use the other axis' zero fraction
-        const float fxA1 = floorf(cxA), fyA1 = floorf(cyA), fxB1 = floorf(cxB), fyB1 = floorf(cyB);
-        const lf2 FX{cxA - fxA1, cxB - fxB1}, FY{cyA - fyA1, cyB - fyB1};
-        const int32_t xA = (int32_t)fxA1, yA = (int32_t)fyA1, xB = (int32_t)fxB1, yB = (int32_t)fyB1;
-        const bool plainA = FX.x == 0.0f || FY.x == 0.0f || xA + 1 < 0 || xA + 1 > P.W - 1 ||
-                            yA + 1 < 0 || yA + 1 > P.H - 1;
-        const bool plainB = FX.y == 0.0f || FY.y == 0.0f || xB + 1 < 0 || xB + 1 > P.W - 1 ||
-                            yB + 1 < 0 || yB + 1 > P.H - 1;
-        const lf2 FXM = lf2{1.0f, 1.0f} - FX, FYM = lf2{1.0f, 1.0f} - FY;
-        // (x1, y1) .. (x1 + 1, y1 + 1) lie in the window for every in-mask
-        // pixel; pixels outside the mask read the window origin
-        const int32_t iA = inA ? (yA - by0) * win.stride + (xA - bxa) : 0;
-        const int32_t iB = inB ? (yB - by0) * win.stride + (xB - bxa) : 0;
-        uint8_t* oA = obuf + rA * kRowB + lane * C;
-        uint8_t* oB = obuf + rB * kRowB + lane * C;
+        const float fx1 = floorf(cx), fy1 = floorf(cy);
+        const float fx = cx - fx1, fy = cy - fy1;
+        const int32_t x1 = (int32_t)fx1, y1 = (int32_t)fy1;
+        const bool plain = fx == 0.0f || fy == 0.0f || x1 + 1 < 0 || x1 + 1 > P.W - 1 ||
+                           y1 + 1 < 0 || y1 + 1 > P.H - 1;
+        const lf2 FX{1.0f - fx, fx}, FY{1.0f - fy, fy};
+        // (x1, y1) .. (x1 + 1, y1 + 1) lie in the window
+        const int32_t i11 = __mul24(y1 - by0, win.stride) + (x1 - bxa);
+        uint8_t* o = obuf + r * kRowB + lane * C;
 #pragma unroll
         for (int c = 0; c < C; c++) {
-          const float* q = lw + c * plane_f;
-          const lf2 p11{q[iA], q[iB]}, p21{q[iA + 1], q[iB + 1]};
-          const lf2 p12{q[iA + win.stride], q[iB + win.stride]};
-          const lf2 p22{q[iA + win.stride + 1], q[iB + win.stride + 1]};
-          const lf2 h1 = lin2v(FXM, FX, p11, p21), h2 = lin2v(FXM, FX, p12, p22);
-          const lf2 o = lin2v(FYM, FY, h1, h2);
-          if (inA) oA[c] = (uint8_t)(uint32_t)(plainA ? p11.x : o.x);
-          if (inB) oB[c] = (uint8_t)(uint32_t)(plainB ? p11.y : o.y);
+          const float* q = lw + c * plane_f + i11;
+          const lf2 top{q[0], q[1]}, bot{q[win.stride], q[win.stride + 1]};
+          const lf2 t = FX * top, b = FX * bot;
+          const lf2 h{__builtin_truncf(t.x + t.y), __builtin_truncf(b.x + b.y)};
+          const lf2 f = FY * h;
+          o[c] = (uint8_t)(uint32_t)(plain ? top.x : __builtin_truncf(f.x + f.y));
         }
       }
     }
