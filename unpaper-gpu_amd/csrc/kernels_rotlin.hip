@@ -122,8 +122,12 @@ __global__ void __launch_bounds__(kLT) k_rotate_lin(PlaneRef src, PlaneRef dst, 
     }
     return;
   }
-  const int32_t plane_f = win.rows * win.stride;            // floats per channel plane
-  uint8_t* obuf = reinterpret_cast<uint8_t*>(lw + C * plane_f);  // kLH x kRowB bytes
+  // the window: GRAY8 as floats; RGB24 as one 32-bit word per pixel
+  // (r | g << 8 | b << 16), converted per tap -- a third of three float
+  // planes' LDS, so eight tiles share a CU instead of three
+  const int32_t plane_f = win.rows * win.stride;            // words per window
+  uint32_t* lwu = reinterpret_cast<uint32_t*>(lw);
+  uint8_t* obuf = reinterpret_cast<uint8_t*>(lw + plane_f);  // kLH x kRowB bytes
   // 1. the tile's source bytes (kept where no mask rotates)
   {
     constexpr int NV = kRowB / 16;
@@ -189,34 +193,43 @@ __global__ void __launch_bounds__(kLT) k_rotate_lin(PlaneRef src, PlaneRef dst, 
         const int32_t y = by0 + r, x = bxa + 4 * gq;
         const bool rowok = y >= 0 && y < P.H;
         const uint8_t* row = sbase + (int64_t)(rowok ? y : 0) * P.pitch;
-        float4 q[C];
-        if (rowok && x >= 0 && x + 4 <= P.W) {
-          if constexpr (C == 3) {
+        const bool full = rowok && x >= 0 && x + 4 <= P.W;
+        if constexpr (C == 3) {
+          uint4 q;
+          if (full) {
             const uint32_t* p3 = reinterpret_cast<const uint32_t*>(row + 3 * (int64_t)x);
             const uint32_t w0 = p3[0], w1 = p3[1], w2 = p3[2];  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
-            q[0] = make_float4(ubyte_f<0>(w0), ubyte_f<3>(w0), ubyte_f<2>(w1), ubyte_f<1>(w2));
-            q[1] = make_float4(ubyte_f<1>(w0), ubyte_f<0>(w1), ubyte_f<3>(w1), ubyte_f<2>(w2));
-            q[2] = make_float4(ubyte_f<2>(w0), ubyte_f<1>(w1), ubyte_f<0>(w2), ubyte_f<3>(w2));
+            q = make_uint4(w0, __builtin_amdgcn_alignbyte(w1, w0, 3),
+                           __builtin_amdgcn_alignbyte(w2, w1, 2), w2 >> 8);
           } else {
-            const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + x);
-            q[0] = make_float4(ubyte_f<0>(w0), ubyte_f<1>(w0), ubyte_f<2>(w0), ubyte_f<3>(w0));
+            // window edge: pixels outside the image are white (get_pixel)
+            uint32_t v[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+              const int32_t xx = x + j;
+              const uint8_t* px = row + 3 * (int64_t)xx;
+              v[j] = rowok && xx >= 0 && xx < P.W ? (uint32_t)px[0] | (uint32_t)px[1] << 8 | (uint32_t)px[2] << 16
+                                                   : 0xFFFFFFu;
+            }
+            q = make_uint4(v[0], v[1], v[2], v[3]);
           }
+          *reinterpret_cast<uint4*>(lwu + r * win.stride + 4 * gq) = q;
         } else {
-          // window edge: pixels outside the image are white (get_pixel)
-          float v[C][4];
+          float4 q;
+          if (full) {
+            const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + x);
+            q = make_float4(ubyte_f<0>(w0), ubyte_f<1>(w0), ubyte_f<2>(w0), ubyte_f<3>(w0));
+          } else {
+            float v[4];
 #pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const int32_t xx = x + j;
-            const bool in = rowok && xx >= 0 && xx < P.W;
-#pragma unroll
-            for (int c = 0; c < C; c++) v[c][j] = in ? (float)row[(int64_t)xx * C + c] : 255.0f;
+            for (int j = 0; j < 4; j++) {
+              const int32_t xx = x + j;
+              v[j] = rowok && xx >= 0 && xx < P.W ? (float)row[xx] : 255.0f;
+            }
+            q = make_float4(v[0], v[1], v[2], v[3]);
           }
-#pragma unroll
-          for (int c = 0; c < C; c++) q[c] = make_float4(v[c][0], v[c][1], v[c][2], v[c][3]);
+          *reinterpret_cast<float4*>(lw + r * win.stride + 4 * gq) = q;
         }
-#pragma unroll
-        for (int c = 0; c < C; c++)
-          *reinterpret_cast<float4*>(lw + c * plane_f + r * win.stride + 4 * gq) = q[c];
       }
     }
     __syncthreads();
@@ -273,14 +286,26 @@ __global__ void __launch_bounds__(kLT) k_rotate_lin(PlaneRef src, PlaneRef dst, 
         // (x1, y1) .. (x1 + 1, y1 + 1) lie in the window
         const int32_t i11 = __mul24(y1 - by0, win.stride) + (x1 - bxa);
         uint8_t* o = obuf + r * kRowB + lane * C;
+        if constexpr (C == 3) {
+          // one ds_read2_b32 per tap row: pixels (x1, x2) as rgb words
+          const uint32_t* q = lwu + i11;
+          const uint32_t w11 = q[0], w21 = q[1], w12 = q[win.stride], w22 = q[win.stride + 1];
 #pragma unroll
-        for (int c = 0; c < C; c++) {
-          const float* q = lw + c * plane_f + i11;
+          for (int c = 0; c < 3; c++) {
+            const lf2 top{(float)((w11 >> (8 * c)) & 0xFFu), (float)((w21 >> (8 * c)) & 0xFFu)};
+            const lf2 bot{(float)((w12 >> (8 * c)) & 0xFFu), (float)((w22 >> (8 * c)) & 0xFFu)};
+            const lf2 t = FX * top, b = FX * bot;
+            const lf2 h{__builtin_truncf(t.x + t.y), __builtin_truncf(b.x + b.y)};
+            const lf2 f = FY * h;
+            o[c] = plain ? (uint8_t)(w11 >> (8 * c)) : (uint8_t)(uint32_t)__builtin_truncf(f.x + f.y);
+          }
+        } else {
+          const float* q = lw + i11;
           const lf2 top{q[0], q[1]}, bot{q[win.stride], q[win.stride + 1]};
           const lf2 t = FX * top, b = FX * bot;
           const lf2 h{__builtin_truncf(t.x + t.y), __builtin_truncf(b.x + b.y)};
           const lf2 f = FY * h;
-          o[c] = (uint8_t)(uint32_t)(plain ? top.x : __builtin_truncf(f.x + f.y));
+          o[0] = (uint8_t)(uint32_t)(plain ? top.x : __builtin_truncf(f.x + f.y));
         }
       }
     }
@@ -321,7 +346,7 @@ LinWindow lin_window(float max_abs_angle) {
 
 size_t lin_lds_bytes(const LinWindow& w, int fmt) {
   const int C = fmt == F_RGB24 ? 3 : 1;
-  return sizeof(float) * (size_t)C * w.rows * w.stride + (size_t)kLH * kLW * C;
+  return sizeof(float) * (size_t)w.rows * w.stride + (size_t)kLH * kLW * C;
 }
 
 bool launch_rotate_linear(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
