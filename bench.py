@@ -79,7 +79,8 @@ STAGE_PLANES = {
     "center": 2.0,          # mask move read + write
 }
 ROOFLINE_STAGE = "deskew_rotate"
-ROOFLINE_KERNEL = {"c3": "k_rotate_cubic_g8f", "c4": "k_rotate_mask<F_RGB24> (bilinear)"}
+ROOFLINE_KERNEL = {"c3": "k_rotate_cubic_g8f",
+                   "c4": "k_rotate_lin<F_RGB24> (bilinear, both masks of a sheet in one launch)"}
 
 
 def parse():
@@ -472,7 +473,9 @@ def run_c4(args, L, d, devices, firsts, n_gpus, version, valid, nsheets=0, steps
                          "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
                          "traffic": None, "avg_launch_ms": round(rot_ms, 3),
-                         "launch_ms_from": "3 single-sheet launches, idle GPU",
+                         "launch_ms_from": "3 single-sheet runs, idle GPU (the deskew_rotate "
+                                           "stage: the two-mask launch + the launch for sheets "
+                                           "whose mask 1 depends on deskew 0)",
                          "alg_bytes_per_launch": rot_alg,
                          "pipeline_alg_bytes_per_sheet": alg_sheet,
                          "pipeline_frac": round(sheets_s / n_gpus * alg_sheet /

@@ -56,9 +56,14 @@ struct NoiseGeom {
 };
 bool noise_geometry(int32_t W, int32_t H, uint64_t intensity, uint8_t white, NoiseGeom* g);
 size_t noise_scratch_bytes(const NoiseGeom& g);
+// bits (optional): the GRAY8 dark bit-plane of the image as it stands, one
+// u32 per 32 pixels, bits_stride words per sheet (k_decode_gray made it and
+// the blackfilter kept it current): k_noise_bits is then skipped.
 void launch_noisefilter(const PlaneRef& img, const NoiseGeom& g, void* scratch,
                         int64_t scratch_stride, const int32_t* active, SheetCtl* ctl, int count,
-                        hipStream_t st);
+                        hipStream_t st, const uint32_t* bits = nullptr, int64_t bits_stride = 0);
+// 32-pixel words per row of the GRAY8 dark bit-plane
+inline int32_t noise_bit_words(int32_t W) { return (W + 31) >> 5; }
 
 // ---- blackfilter (filters.c:49-127, fill.c) -----------------------------
 struct BlackBar {
@@ -113,9 +118,19 @@ const int32_t* rotation_line_flags(const int32_t* lines, int nlines, int max_sca
 int rotation_angles(const UphipDeskewParameters& p, RotTable* t);
 // Host: detect_rotation_cpu's combination of per-edge results (deskew.c:219-240)
 float combine_edge_rotations(const float* rot, int count, float deviation_rad);
+// vsum_ready: the v-stripe row sums are already in the scratch (k_decode_gray);
+// nbits (optional): the noisefilter's dark bit-plane, cleared where fills paint.
 void launch_blackfilter_impl(const PlaneRef& img, const BlackGeom& g, const BlackBar* bars,
                              void* scratch, int64_t ss, const int32_t* active, SheetCtl* ctl,
                              int count, hipStream_t st, const AxisArgs* hargs,
-                             const AxisArgs* vargs);
+                             const AxisArgs* vargs, bool vsum_ready = false,
+                             uint32_t* nbits = nullptr, int64_t nbits_stride = 0);
+// GRAY8 page -> sheet plane (same size), plus on the way: the noisefilter's
+// dark bit-plane (pixel < white) and the blackfilter's v-stripe row sums over
+// columns [vx0, vx1] (vsum: H entries per sheet after W, vx0 > vx1 = none).
+// Pages 16-byte aligned with a 16-multiple pitch.
+void launch_decode_gray(const uint8_t* src, int64_t spitch, int64_t sstride, const PlaneRef& dst,
+                        uint8_t white, uint32_t* bits, int64_t bits_stride, uint32_t* vsum,
+                        int64_t vsum_stride, int32_t vx0, int32_t vx1, int count, hipStream_t st);
 
 }  // namespace uph

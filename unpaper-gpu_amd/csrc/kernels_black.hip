@@ -199,6 +199,8 @@ struct Canvas {
   int32_t W, H;
   uint8_t mmax;  // mask_max (mask_min is 0)
   BlackStats* bs;  // tuning build counters
+  uint32_t* nbits;  // the noisefilter's dark bit-plane of this sheet (or null)
+  int32_t nwr;      // its words per row
   __device__ __forceinline__ bool inside(int32_t x, int32_t y) const {
     return x >= 0 && y >= 0 && x < W && y < H;
   }
@@ -219,7 +221,10 @@ struct Canvas {
     BSTAT(bs->lookups += N;)
   }
   __device__ __forceinline__ void paint(int32_t x, int32_t y) const {
-    if (inside(x, y)) store_px_row<FMT>(base + (int64_t)y * pitch, x, Px{255, 255, 255});
+    if (!inside(x, y)) return;
+    store_px_row<FMT>(base + (int64_t)y * pitch, x, Px{255, 255, 255});
+    // white is not dark: the bit-plane follows the fill
+    if (nbits) atomicAnd(nbits + (int64_t)y * nwr + (x >> 5), ~(1u << (x & 31)));
   }
 };
 
@@ -707,7 +712,8 @@ __global__ void __launch_bounds__(kThreads) k_black_resolve(PlaneRef img, BlackG
                                                             const BlackBar* bars,
                                                             uint8_t* scratch, int64_t sstride,
                                                             const int32_t* active,
-                                                            SheetCtl* ctl) {
+                                                            SheetCtl* ctl, uint32_t* nbits,
+                                                            int64_t nbits_stride) {
   const int s = blockIdx.x;
   if (active && !active[s]) return;
   const int w = wave_id(), lane = lane_id();
@@ -721,7 +727,7 @@ __global__ void __launch_bounds__(kThreads) k_black_resolve(PlaneRef img, BlackG
   BlackStats* bs = &bstat;
   (void)bs;
   const Canvas<FMT> C{base, img.P.pitch, g.W, g.H, g.mask_max,
-                      bs};
+                      bs, nbits ? nbits + s * nbits_stride : nullptr, (g.W + 31) >> 5};
   BSTAT(const uint64_t t_all = wall_clock64();)
   uint64_t* red = tab_red();
   int parity = 0;
@@ -860,11 +866,12 @@ template <int FMT>
 static void launch_black_t(const PlaneRef& img, const BlackGeom& g, const BlackBar* bars,
                            uint8_t* scr, int64_t ss, const int32_t* active, SheetCtl* ctl,
                            int count, hipStream_t st, const AxisArgs* hargs,
-                           const AxisArgs* vargs) {
+                           const AxisArgs* vargs, bool vsum_ready, uint32_t* nbits,
+                           int64_t nbits_stride) {
   // column sums of max(rgb) over the h-stripe rows, row sums over the v-stripe cols
   if (g.hregion.x1 >= g.hregion.x0 && g.hregion.y1 >= g.hregion.y0)
     launch_axis_reduce(img, hargs, 0, M_DARKINV_SUM, g.W, g.H, (uint32_t*)scr, ss / 4, count, st);
-  if (g.vregion.x1 >= g.vregion.x0 && g.vregion.y1 >= g.vregion.y0)
+  if (g.vregion.x1 >= g.vregion.x0 && g.vregion.y1 >= g.vregion.y0 && !vsum_ready)
     launch_axis_reduce(img, vargs, 1, M_DARKINV_SUM, g.vregion.x1 - g.vregion.x0 + 1, g.H,
                        (uint32_t*)scr + g.W, ss / 4, count, st);
   BlackGeom gd = g;
@@ -872,7 +879,7 @@ static void launch_black_t(const PlaneRef& img, const BlackGeom& g, const BlackB
   allow_dynamic_lds((const void*)k_black_resolve<FMT>, kStackLdsBytes);
   if (!(diag_skip() & 1))
     hipLaunchKernelGGL(k_black_resolve<FMT>, dim3(count), dim3(kThreads), kStackLdsBytes, st, img, gd,
-                       bars, scr, ss, active, ctl);
+                       bars, scr, ss, active, ctl, FMT == F_GRAY8 ? nbits : nullptr, nbits_stride);
 }
 
 __global__ void k_black_prep(uint8_t* scr, int64_t ss, int32_t words, int count) {
@@ -886,18 +893,22 @@ __global__ void k_black_prep(uint8_t* scr, int64_t ss, int32_t words, int count)
 void launch_blackfilter_impl(const PlaneRef& img, const BlackGeom& g, const BlackBar* bars,
                              void* scratch, int64_t ss, const int32_t* active, SheetCtl* ctl,
                              int count, hipStream_t st, const AxisArgs* hargs,
-                             const AxisArgs* vargs) {
+                             const AxisArgs* vargs, bool vsum_ready, uint32_t* nbits,
+                             int64_t nbits_stride) {
   uint8_t* scr = (uint8_t*)scratch;
   hipLaunchKernelGGL(k_black_prep, dim3(8, count), dim3(256), 0, st, scr, ss, g.W, count);
   switch (img.P.fmt) {
     case F_GRAY8:
-      launch_black_t<F_GRAY8>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs);
+      launch_black_t<F_GRAY8>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs, vsum_ready,
+                         nbits, nbits_stride);
       break;
     case F_Y400A:
-      launch_black_t<F_Y400A>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs);
+      launch_black_t<F_Y400A>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs, vsum_ready,
+                         nbits, nbits_stride);
       break;
     default:
-      launch_black_t<F_RGB24>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs);
+      launch_black_t<F_RGB24>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs, vsum_ready,
+                         nbits, nbits_stride);
       break;
   }
 }

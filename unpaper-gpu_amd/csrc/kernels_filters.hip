@@ -658,7 +658,7 @@ static size_t pow2_at_least(size_t n) {
 }
 
 // 32-pixel words per row of the GRAY8 dark bit-plane
-static int32_t noise_bit_words(const NoiseGeom& g) { return (g.W + 31) >> 5; }
+static int32_t noise_bit_words(const NoiseGeom& g) { return noise_bit_words(g.W); }
 
 size_t noise_scratch_bytes(const NoiseGeom& g) {
   // lists + a global sort buffer for the rare > 8192-trigger sequential case;
@@ -792,6 +792,73 @@ __global__ void __launch_bounds__(256) k_noise_bits(PlaneRef img, NoiseGeom g, u
                lt_nibble(b.z, k) << 24 | lt_nibble(b.w, k) << 28;
   if (x0 + 32 > g.W) m &= (1u << (g.W - x0)) - 1u;  // g.W - x0 in [1, 31]
   bits[s * bstride + t] = m;
+}
+
+// The decode of a GRAY8 page into its sheet (sheet_stages.c:151-165 with the
+// page covering the sheet: a plain copy) fused with the first passes that
+// read the result: the noisefilter's dark bit-plane (k_noise_bits) and the
+// blackfilter's v-stripe row sums (darkness_rect's sums over the stripe's
+// columns, filters.c:49-104).  One wave per row at a time, a lane per
+// 32-pixel word: two 16-byte loads, two 16-byte stores (the row's last word
+// byte by byte up to W), one bit-plane word; the row sum as one wave sum.
+__global__ void __launch_bounds__(256) k_decode_gray(const uint8_t* src, int64_t spitch,
+                                                     int64_t sstride, PlaneRef dst, uint8_t white,
+                                                     uint32_t* bits, int64_t bstride,
+                                                     uint32_t* vsum, int64_t vstride, int32_t vx0,
+                                                     int32_t vx1) {
+  const int s = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int32_t y = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const Planes& P = dst.P;
+  if (y >= P.H) return;
+  const uint8_t* srow = src + s * sstride + (int64_t)y * spitch;
+  uint8_t* drow = plane_ptr(dst, s) + (int64_t)y * P.pitch;
+  const int32_t nwr = (P.W + 31) >> 5;
+  const uint32_t k = (256u - white) * 0x00010001u;
+  uint32_t vs = 0;
+  for (int32_t wi = lane; wi < nwr; wi += 64) {
+    const int32_t x0 = 32 * wi;
+    const uint4 a = *reinterpret_cast<const uint4*>(srow + x0);
+    const uint4 b = *reinterpret_cast<const uint4*>(srow + x0 + 16);
+    uint32_t m = lt_nibble(a.x, k) | lt_nibble(a.y, k) << 4 | lt_nibble(a.z, k) << 8 |
+                 lt_nibble(a.w, k) << 12 | lt_nibble(b.x, k) << 16 | lt_nibble(b.y, k) << 20 |
+                 lt_nibble(b.z, k) << 24 | lt_nibble(b.w, k) << 28;
+    if (x0 + 32 <= P.W) {
+      *reinterpret_cast<uint4*>(drow + x0) = a;
+      *reinterpret_cast<uint4*>(drow + x0 + 16) = b;
+    } else {
+      m &= (1u << (P.W - x0)) - 1u;  // P.W - x0 in [1, 31]
+      const uint32_t w8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int j = 0; j < 32; j++)
+        if (x0 + j < P.W) drow[x0 + j] = (uint8_t)(w8[j >> 2] >> (8 * (j & 3)));
+    }
+    if (bits) bits[s * bstride + (int64_t)y * nwr + wi] = m;
+    if (vsum && x0 <= vx1 && x0 + 31 >= vx0) {
+      const uint32_t w8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int d = 0; d < 8; d++) {
+        const int32_t xd = x0 + 4 * d;
+        uint32_t keep = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+          if (xd + q >= vx0 && xd + q <= vx1) keep |= 0xFFu << (8 * q);
+        vs = __builtin_amdgcn_sad_u8(w8[d] & keep, 0u, vs);
+      }
+    }
+  }
+  if (vsum) {
+    for (int o = 32; o > 0; o >>= 1) vs += __shfl_xor(vs, o, 64);
+    if (lane == 0) vsum[s * vstride + y] = vs;
+  }
+}
+
+void launch_decode_gray(const uint8_t* src, int64_t spitch, int64_t sstride, const PlaneRef& dst,
+                        uint8_t white, uint32_t* bits, int64_t bits_stride, uint32_t* vsum,
+                        int64_t vsum_stride, int32_t vx0, int32_t vx1, int count, hipStream_t st) {
+  hipLaunchKernelGGL(k_decode_gray, dim3((unsigned)((dst.P.H + 3) / 4), count), dim3(256), 0, st,
+                     src, spitch, sstride, dst, white, bits, bits_stride, vsum, vsum_stride, vx0,
+                     vx1);
 }
 
 // Whether the classification of a small dark pixel (tile coordinates rx, ry)
@@ -1592,14 +1659,18 @@ __global__ void k_noise_zero(uint8_t* scr, int64_t stride, int count) {
 template <int FMT>
 static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr, int64_t ss,
                            const int32_t* active, SheetCtl* ctl, int count, hipStream_t st,
-                           uint32_t* sortbuf, int64_t sort_stride) {
+                           uint32_t* sortbuf, int64_t sort_stride, const uint32_t* bits_ready,
+                           int64_t bits_stride) {
   constexpr int ntx = noise_tile_w<FMT>();
   dim3 grid((g.W + ntx - 1) / ntx, (g.H + kNT - 1) / kNT, count);
   NoiseGeom gd = g;
   gd.diag = diag_noise();
   uint32_t* bits = nullptr;
   int64_t bstride = 0;
-  if (FMT == F_GRAY8) {
+  if (FMT == F_GRAY8 && bits_ready) {
+    bits = const_cast<uint32_t*>(bits_ready);
+    bstride = bits_stride;
+  } else if (FMT == F_GRAY8) {
     // the dark bit-plane in the sort buffer's space (noise_scratch_bytes)
     const int32_t nwr = noise_bit_words(g);
     bits = sortbuf;
@@ -1620,7 +1691,7 @@ static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr
 
 void launch_noisefilter(const PlaneRef& img, const NoiseGeom& g, void* scratch,
                         int64_t scratch_stride, const int32_t* active, SheetCtl* ctl, int count,
-                        hipStream_t st) {
+                        hipStream_t st, const uint32_t* bits, int64_t bits_stride) {
   // layout of `scratch` per sheet: [noise lists][sort buffer (capacity pow2)]
   uint8_t* scr = (uint8_t*)scratch;
   const size_t lists = noise_list_bytes(g);
@@ -1631,15 +1702,15 @@ void launch_noisefilter(const PlaneRef& img, const NoiseGeom& g, void* scratch,
   switch (img.P.fmt) {
     case F_GRAY8:
       launch_noise_t<F_GRAY8>(img, g, scr, scratch_stride, active, ctl, count, st, sortbuf,
-                              sort_stride);
+                              sort_stride, bits, bits_stride);
       break;
     case F_Y400A:
       launch_noise_t<F_Y400A>(img, g, scr, scratch_stride, active, ctl, count, st, sortbuf,
-                              sort_stride);
+                              sort_stride, nullptr, 0);
       break;
     default:
       launch_noise_t<F_RGB24>(img, g, scr, scratch_stride, active, ctl, count, st, sortbuf,
-                              sort_stride);
+                              sort_stride, nullptr, 0);
       break;
   }
 }

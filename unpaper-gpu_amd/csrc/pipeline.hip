@@ -416,6 +416,8 @@ struct UphipBatch {
   RotateArgs* rot_args = nullptr;      // [UPHIP_MAX_PAGES][cap]
   int32_t* rot_indep = nullptr;        // two-mask launch: mask 1 independent of deskew 0
   int32_t* rot_dep = nullptr;          // ... or redone after it
+  uint32_t* nbits = nullptr;           // GRAY8 noisefilter dark bit-plane (k_decode_gray)
+  int64_t nbits_stride = 0;            // words per sheet
   MoveArgs* move_args = nullptr;      // cap * MAX_PAGES
   MaskArgs* border_mask_args = nullptr;
   int32_t* edge_res = nullptr;        // cap * npoints * 4
@@ -700,6 +702,11 @@ static bool allocate(UphipBatch* b) {
   if (!(o.disable & UPHIP_NO_NOISEFILTER)) {
     noise_geometry(W, H, o.noisefilter_intensity, o.abs_white_threshold, &b->ngeo);
     need = std::max(need, noise_scratch_bytes(b->ngeo));
+    if (b->work_fmt == F_GRAY8) {
+      b->nbits_stride = ((int64_t)noise_bit_words(W) * H + 63) & ~(int64_t)63;
+      b->nbits = dalloc<uint32_t>(b, (size_t)b->nbits_stride * cap);
+      if (!b->nbits) return false;
+    }
   }
   if (!(o.disable & UPHIP_NO_BLURFILTER)) {
     if (!blur_geometry(W, H, o.blurfilter_parameters, o.abs_white_threshold, &b->blgeo))
@@ -1056,6 +1063,27 @@ static void border_all(UphipBatch* b, int count, bool rows_ready) {
 // ---------------------------------------------------------------------------
 // run
 // ---------------------------------------------------------------------------
+// The decode may also produce the noisefilter's dark bit-plane and the
+// blackfilter's v-stripe row sums (k_decode_gray) when a GRAY8 page becomes
+// the sheet unchanged and nothing writes the sheet between the decode and
+// the filters (sheet_stages.c:187-325: pre-mirror, -shift, -masks,
+// -stretch/size, -wipes, -border all off).
+static bool decode_fused(const UphipBatch* b, const uint8_t* src, int64_t spitch) {
+  const UphipOptions& o = b->o;
+  const uint32_t dis = o.disable;
+  if (b->work_fmt != F_GRAY8 || b->geo.page_format != F_GRAY8 || b->n_in != 1) return false;
+  if (b->rp_w != b->sheet_w || b->rp_h != b->sheet_h || o.pre_rotate != 0) return false;
+  if (b->sheet_w != b->W || b->sheet_h != b->H) return false;  // stretch / page size
+  if (((uintptr_t)src & 15) || (spitch & 15)) return false;
+  if (o.pre_mirror.horizontal || o.pre_mirror.vertical) return false;
+  if (o.pre_shift.horizontal != 0 || o.pre_shift.vertical != 0 || o.pre_mask_count > 0) return false;
+  if (!(dis & UPHIP_NO_WIPE) && o.pre_wipes.count > 0) return false;
+  if (!(dis & UPHIP_NO_BORDER) &&
+      (o.pre_border.left || o.pre_border.top || o.pre_border.right || o.pre_border.bottom))
+    return false;
+  return true;
+}
+
 static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spitch,
                       int64_t sstride) {
   const UphipOptions& o = b->o;
@@ -1072,8 +1100,18 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
   int32_t w = b->sheet_w, h = b->sheet_h;
   Planes S0 = planes_of(b, w, h);
   const bool covered = n == 1 && b->rp_w == w && b->rp_h == h;
+  const bool fused = decode_fused(b, src, spitch);
+  // what the fused decode hands on
+  const bool black_on = !(dis & UPHIP_NO_BLACKFILTER) && b->bgeo.nbars > 0;
+  const bool vsum_ready = fused && black_on && b->bgeo.vregion.x1 >= b->bgeo.vregion.x0;
+  uint32_t* bits_ready = fused && !(dis & UPHIP_NO_NOISEFILTER) ? b->nbits : nullptr;
+  if (fused) {
+    launch_decode_gray(src, spitch, sstride, cur_ref(S0, b->ctl), o.abs_white_threshold, bits_ready,
+                       b->nbits_stride, vsum_ready ? (uint32_t*)b->scr + b->bgeo.W : nullptr,
+                       b->scr_stride / 4, b->bgeo.vregion.x0, b->bgeo.vregion.x1, count, b->st);
+  }
   if (!covered) fill_uniform(b, S0, 0, Rect{0, 0, w - 1, h - 1}, o.sheet_background, count);
-  for (int j = 0; j < n; j++) {
+  for (int j = 0; j < n && !fused; j++) {
     Planes pg;
     pg.base[0] = pg.base[1] = const_cast<uint8_t*>(src) + j * sstride;
     pg.pitch = spitch;
@@ -1152,12 +1190,13 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
   // ---- filters (sheet_stages.c:327-357) ---------------------------------
   if (!(dis & UPHIP_NO_BLACKFILTER) && b->bgeo.nbars > 0) {
     launch_blackfilter_impl(cur_ref(P, b->ctl), b->bgeo, b->dbars, b->scr, b->scr_stride, nullptr,
-                            b->ctl, count, b->st, b->black_h, b->black_v);
+                            b->ctl, count, b->st, b->black_h, b->black_v, vsum_ready, bits_ready,
+                            b->nbits_stride);
     mark(b, "blackfilter");
   }
   if (!(dis & UPHIP_NO_NOISEFILTER)) {
     launch_noisefilter(cur_ref(P, b->ctl), b->ngeo, b->scr, b->scr_stride, nullptr, b->ctl, count,
-                       b->st);
+                       b->st, bits_ready, b->nbits_stride);
     mark(b, "noisefilter");
   }
   if (!(dis & UPHIP_NO_BLURFILTER)) {
