@@ -9,10 +9,19 @@
 // Flood fill: the reference recursion (paint, four fill_lines, then for each
 // line position its two perpendicular neighbours, depth first) is order-
 // dependent (lines stop on painted pixels, and paint up to intensity-1
-// non-matching pixels), so one wave replays it: an explicit stack of frames in
-// HBM, one workgroup per sheet: the four fill_lines of a frame together, and
-// the neighbour and bar-pixel checks in windows of 4096 read ahead, 64 pixels
-// per ballot, the window's slices spread over the workgroup's waves.
+// non-matching pixels), so it is replayed in order by one wave per sheet,
+// with an explicit stack of frames.  The replay never reads the image: the
+// only question the fill asks of a pixel is "gray <= mask_max" (fill.c:29,
+// :85) and the only change it makes is painting white, so it runs on bit
+// planes M (the pixel matched before the fill) and P (painted): a pixel
+// matches now iff M and not P (for mask_max < 255; white still matches
+// otherwise).  Both are kept twice, row-major and column-major (one u64 per
+// 64 pixels of a row / of a column), so that a lane reads 64 positions of a
+// line in either direction with two words, and a round trip of one wave
+// reads 16 windows (1024 positions) of each of a frame's four lines, or 8
+// windows of each neighbour side: a line's stop, or its first matching
+// neighbour, is a few 64-bit operations per lane.  The image is painted from
+// P afterwards.
 #include <climits>
 
 #include "filters.h"
@@ -75,13 +84,187 @@ bool black_geometry(int32_t W, int32_t H, const UphipBlackfilterParameters& p, u
   return true;
 }
 
-size_t black_scratch_bytes(const BlackGeom& g) {
-  // [sums: W (h-stripe columns) + H (v-stripe rows)] u32 + DFS stack frames
-  size_t b = ((size_t)g.W + g.H) * 4;
-  b = (b + 255) & ~(size_t)255;
-  b += (size_t)g.stack_capacity * 32;
-  return (b + 255) & ~(size_t)255;
+// ---------------------------------------------------------------------------
+// Per-sheet scratch: [hsum: W | vsum: H] u32, the head (u32 "some bar is a
+// candidate" flag, then the candidate bits of the bars from byte 8), the
+// planes RM, RP (H rows of wpr words: x = 64w + bit) and CM, CP (W columns of
+// hpc words: y = 64w + bit), the DFS stack frames.
+UPH_HD int32_t black_wpr(const BlackGeom& g) { return (g.W + 63) >> 6; }
+UPH_HD int32_t black_hpc(const BlackGeom& g) { return (g.H + 63) >> 6; }
+UPH_HD size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+UPH_HD size_t black_head_off(const BlackGeom& g) { return align256(((size_t)g.W + g.H) * 4); }
+UPH_HD size_t black_rows_bytes(const BlackGeom& g) { return align256((size_t)g.H * black_wpr(g) * 8); }
+UPH_HD size_t black_cols_bytes(const BlackGeom& g) { return align256((size_t)g.W * black_hpc(g) * 8); }
+UPH_HD size_t black_rm_off(const BlackGeom& g) {
+  return black_head_off(g) + align256(8 + (((size_t)g.nbars + 63) / 64) * 8);
 }
+UPH_HD size_t black_rp_off(const BlackGeom& g) { return black_rm_off(g) + black_rows_bytes(g); }
+UPH_HD size_t black_cm_off(const BlackGeom& g) { return black_rp_off(g) + black_rows_bytes(g); }
+UPH_HD size_t black_cp_off(const BlackGeom& g) { return black_cm_off(g) + black_cols_bytes(g); }
+UPH_HD size_t black_stack_off(const BlackGeom& g) { return black_cp_off(g) + black_cols_bytes(g); }
+size_t black_scratch_bytes(const BlackGeom& g) {
+  return align256(black_stack_off(g) + (size_t)g.stack_capacity * 32);
+}
+
+// darkness of a bar on the original image (darkness_rect, blit.c:131-146)
+// from the stripe's column / row sums, and the scan's test (filters.c:76-78)
+__device__ __forceinline__ bool bar_candidate(const BlackGeom& g, const BlackBar& bb,
+                                              const uint32_t* hsum, const uint32_t* vsum) {
+  const Rect c = clip(bb.r, g.W, g.H);
+  uint64_t sum = 0;
+  if (c.x0 <= c.x1 && c.y0 <= c.y1) {
+    if (bb.dir == 0)
+      for (int32_t x = c.x0; x <= c.x1; x++) sum += hsum[x];
+    else
+      for (int32_t y = c.y0; y <= c.y1; y++) sum += vsum[y];
+  }
+  const uint8_t dark = (uint8_t)(0xFFull - sum / count_pixels(c));
+  return dark >= g.abs_threshold && !bb.excluded;
+}
+
+// The candidate bits of every bar, and whether a sheet has any: only those
+// sheets get planes, a replay and a paint pass.
+constexpr int kCandThreads = 256;
+__global__ void __launch_bounds__(kCandThreads) k_black_cand(BlackGeom g, const BlackBar* bars,
+                                                             uint8_t* scratch, int64_t sstride,
+                                                             const int32_t* active) {
+  const int s = blockIdx.x;
+  if (active && !active[s]) return;
+  uint8_t* scr = scratch + s * sstride;
+  const uint32_t* hsum = (const uint32_t*)scr;
+  uint8_t* head = scr + black_head_off(g);
+  uint64_t* cand = (uint64_t*)(head + 8);
+  bool any = false;
+  for (int32_t b0 = 0; b0 < g.nbars; b0 += kCandThreads) {
+    const int32_t bi = b0 + (int32_t)threadIdx.x;
+    const bool c = bi < g.nbars && bar_candidate(g, bars[bi], hsum, hsum + g.W);
+    const unsigned long long m = __ballot(c);
+    if ((threadIdx.x & 63) == 0 && bi < g.nbars) cand[bi >> 6] = m;
+    any |= c;
+  }
+  any = __syncthreads_or(any);
+  if (threadIdx.x == 0) *(int32_t*)head = any;
+}
+
+__device__ __forceinline__ bool sheet_has_candidate(const BlackGeom& g, const uint8_t* scr) {
+  return *(const int32_t*)(scr + black_head_off(g)) != 0;
+}
+
+// The planes of the candidate sheets: one wave per 64x64 tile; lane t makes
+// the row word of row y0+t (M from the image, P clear), then 64 ballots
+// transpose the tile into its 64 column words.
+template <int FMT>
+__global__ void __launch_bounds__(256) k_black_planes(PlaneRef img, BlackGeom g, uint8_t* scratch,
+                                                      int64_t sstride, const int32_t* active) {
+  const int s = blockIdx.z;
+  if (active && !active[s]) return;
+  uint8_t* scr = scratch + s * sstride;
+  if (!sheet_has_candidate(g, scr)) return;
+  const int32_t wpr = black_wpr(g), hpc = black_hpc(g);
+  const int lane = threadIdx.x & 63;
+  const int32_t xw = blockIdx.x * 4 + (threadIdx.x >> 6), yw = blockIdx.y;
+  if (xw >= wpr) return;  // whole wave
+  const int32_t x0 = 64 * xw, y = 64 * yw + lane;
+  uint64_t m = 0;
+  if (y < g.H) {
+    const uint8_t* row = plane_ptr(img, s) + (int64_t)y * img.P.pitch;
+    if (FMT == F_GRAY8 && x0 + 64 <= g.W && ((uintptr_t)(row + x0) & 15) == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint4 v = *(const uint4*)(row + x0 + 16 * q);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int c = 0; c < 16; c++)
+          m |= (uint64_t)(((w4[c >> 2] >> (8 * (c & 3))) & 0xFFu) <= g.mask_max) << (16 * q + c);
+      }
+    } else {
+      for (int c = 0; c < 64 && x0 + c < g.W; c++)
+        m |= (uint64_t)(gray_of(load_px_row<FMT>(row, x0 + c)) <= g.mask_max) << c;
+    }
+    const int64_t i = (int64_t)y * wpr + xw;
+    ((uint64_t*)(scr + black_rm_off(g)))[i] = m;
+    ((uint64_t*)(scr + black_rp_off(g)))[i] = 0;
+  }
+  // column x0 + c: bit t = row y0 + t's bit c
+  uint64_t col = 0;
+  for (int c = 0; c < 64; c++) {
+    const uint64_t b = __ballot((m >> c) & 1);
+    if (c == lane) col = b;
+  }
+  if (x0 + lane < g.W) {
+    const int64_t i = (int64_t)(x0 + lane) * hpc + yw;
+    ((uint64_t*)(scr + black_cm_off(g)))[i] = col;
+    ((uint64_t*)(scr + black_cp_off(g)))[i] = 0;
+  }
+}
+
+// The image from RP: painted pixels become white; the noisefilter's dark
+// bit-plane (GRAY8, one u32 per 32 pixels of a row) loses them too.  One
+// thread per row word.
+template <int FMT>
+__global__ void __launch_bounds__(256) k_black_paint(PlaneRef img, BlackGeom g, uint8_t* scratch,
+                                                     int64_t sstride, const int32_t* active,
+                                                     uint32_t* nbits, int64_t nbits_stride) {
+  const int s = blockIdx.z;
+  if (active && !active[s]) return;
+  uint8_t* scr = scratch + s * sstride;
+  if (!sheet_has_candidate(g, scr)) return;
+  const int32_t wpr = black_wpr(g);
+  const int32_t xw = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (xw >= wpr || y >= g.H) return;
+  const uint64_t p = ((const uint64_t*)(scr + black_rp_off(g)))[(int64_t)y * wpr + xw];
+  if (!p) return;
+  uint8_t* row = plane_ptr(img, s) + (int64_t)y * img.P.pitch;
+  const int32_t x0 = 64 * xw;
+  if (FMT == F_GRAY8 && x0 + 64 <= g.W && ((uintptr_t)(row + x0) & 15) == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t b16 = (uint32_t)(p >> (16 * q)) & 0xFFFFu;
+      if (!b16) continue;
+      uint4* a = (uint4*)(row + x0 + 16 * q);
+      const uint4 v = *a;
+      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int c = 0; c < 16; c++)
+        if ((b16 >> c) & 1) w4[c >> 2] |= 0xFFu << (8 * (c & 3));
+      *a = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+  } else {
+    for (uint64_t r = p; r; r &= r - 1)
+      store_px_row<FMT>(row, x0 + __ffsll((long long)r) - 1, Px{255, 255, 255});
+  }
+  if (FMT == F_GRAY8 && nbits) {
+    const int32_t nwr = (g.W + 31) >> 5;
+    uint32_t* nb = nbits + s * nbits_stride + (int64_t)y * nwr + 2 * xw;
+    nb[0] &= ~(uint32_t)p;
+    if (2 * xw + 1 < nwr) nb[1] &= ~(uint32_t)(p >> 32);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The replay: one wave per sheet.  Control values are uniform (scalar).
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+// Values the whole wave holds alike but loaded from memory (frames, bars)
+// count as per-lane to the compiler: made scalar, the control built on them
+// stays on the scalar unit instead of exec-masked vector code.
+__device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)(uint32_t)uni((int32_t)(v >> 32)) << 32) | (uint32_t)uni((int32_t)v);
+}
+__device__ __forceinline__ Rect uni_rect(Rect r) { return Rect{uni(r.x0), uni(r.y0), uni(r.x1), uni(r.y1)}; }
+__device__ __forceinline__ int ctz64(uint64_t v) { return __ffsll((long long)v) - 1; }
+__device__ __forceinline__ int hib64(uint64_t v) { return 63 - __clzll((long long)v); }
+template <class T>
+__device__ __forceinline__ T pick4(const T (&a)[4], int d) {
+  return d == 0 ? a[0] : d == 1 ? a[1] : d == 2 ? a[2] : a[3];
+}
+// lanes [lo, lo + n)
+__device__ __forceinline__ uint64_t lane_range(int lo, int n) {
+  return (n >= 64 ? ~0ull : ((1ull << n) - 1)) << lo;
+}
+
+constexpr int kStackLds = 3072;  // the lowest frames of the DFS stack live in LDS
+constexpr size_t kStackLdsBytes = (size_t)kStackLds * 32;  // 96 KiB
 
 struct Frame {
   int32_t x, y;
@@ -90,101 +273,46 @@ struct Frame {
   int32_t pad;
 };
 
-// left, up, right, down (fill.c:92-106)
-__device__ __forceinline__ constexpr int dir_dx(int d) { return d == 0 ? -1 : d == 2 ? 1 : 0; }
-__device__ __forceinline__ constexpr int dir_dy(int d) { return d == 1 ? -1 : d == 3 ? 1 : 0; }
-
-template <class T>
-__device__ __forceinline__ T pick4(const T (&a)[4], int d) {
-  return d == 0 ? a[0] : d == 1 ? a[1] : d == 2 ? a[2] : a[3];
-}
-template <class T>
-__device__ __forceinline__ void set4(T (&a)[4], int d, T v) {
-  if (d == 0) a[0] = v;
-  else if (d == 1) a[1] = v;
-  else if (d == 2) a[2] = v;
-  else a[3] = v;
-}
-
-// The replay is one workgroup of kWaves waves per sheet.  Control (the DFS
-// stack, the current frame, the bar loop) is uniform: every wave runs it on
-// the same values, read from LDS after a barrier.  The per-pixel work of a
-// round trip is a window of kSlices 64-pixel slices, kGroup per wave.
-constexpr int kWaves = 8;
-constexpr int kThreads = 64 * kWaves;
-constexpr int kGroup = 8;
-constexpr int kSlices = kWaves * kGroup;  // 64 slices = 4096 pixels per round trip
-static_assert(kSlices == 64, "lane-parallel reads of the per-slice tables assume 64 slices");
-
-// Per-round-trip tables in LDS (the window's results of each wave).
-constexpr int kOffStop = 0;                       // i32[2][3][kWaves] fill-trip posts + 12 more
-constexpr int kOffFirst = kOffStop + 4 * kWaves;  // i32[2][kWaves] first matches
-constexpr int kOffRed = kOffFirst + kWaves;       // u64[kWaves] sums
-constexpr int kOffCand = kOffRed + kWaves;        // u64[kWaves] candidate bars
-constexpr int kOffMail = kOffCand + kWaves;       // i32[16] driver -> helper commands
-constexpr int kReplayWords = kOffMail + 8;        // in 8-byte units
-
-__device__ __forceinline__ uint64_t* lds64() {
-  __shared__ uint64_t black_tables[kReplayWords];
-  return black_tables;
-}
-__device__ __forceinline__ int32_t* tab_stop() { return (int32_t*)(lds64() + kOffStop); }
-__device__ __forceinline__ int32_t* tab_first() { return (int32_t*)(lds64() + kOffFirst); }
-__device__ __forceinline__ uint64_t* tab_red() { return lds64() + kOffRed; }
-__device__ __forceinline__ uint64_t* tab_cand() { return lds64() + kOffCand; }
-__device__ __forceinline__ int32_t* mailbox() { return (int32_t*)(lds64() + kOffMail); }
-
-// The lowest kStackLds frames of the DFS stack live in LDS (dynamic), the
-// rest in HBM: a pop is then an LDS read instead of a memory round trip.
-constexpr int kStackLds = 3072;
-constexpr size_t kStackLdsBytes = (size_t)kStackLds * 32;  // 96 KiB
 __device__ __forceinline__ int4* stack_lds() {
   extern __shared__ int4 black_stack[];
   return black_stack;
 }
-__device__ __forceinline__ void frame_put(int4* lds, Frame* hbm, int32_t i, const Frame& f) {
+__device__ __forceinline__ void frame_put(Frame* hbm, int32_t i, const Frame& f) {
   const int4 a = make_int4(f.x, f.y, f.dist[0], f.dist[1]);
   const int4 b = make_int4(f.dist[2], f.dist[3], f.cursor, 0);
   if (i < kStackLds) {
-    lds[2 * i] = a;
-    lds[2 * i + 1] = b;
+    stack_lds()[2 * i] = a;
+    stack_lds()[2 * i + 1] = b;
   } else {
     hbm[i] = f;
   }
 }
-__device__ __forceinline__ Frame frame_get(const int4* lds, const Frame* hbm, int32_t i) {
-  if (i >= kStackLds) return hbm[i];
-  const int4 a = lds[2 * i], b = lds[2 * i + 1];
+__device__ __forceinline__ Frame frame_pop(const Frame* hbm, int32_t i) {
   Frame f;
-  f.x = a.x;
-  f.y = a.y;
-  f.dist[0] = a.z;
-  f.dist[1] = a.w;
-  f.dist[2] = b.x;
-  f.dist[3] = b.y;
-  f.cursor = b.z;
+  if (i >= kStackLds) {
+    f = hbm[i];
+  } else {
+    const int4 a = stack_lds()[2 * i], b = stack_lds()[2 * i + 1];
+    f.x = a.x;
+    f.y = a.y;
+    f.dist[0] = a.z;
+    f.dist[1] = a.w;
+    f.dist[2] = b.x;
+    f.dist[3] = b.y;
+    f.cursor = b.z;
+  }
+  f.x = uni(f.x);
+  f.y = uni(f.y);
+#pragma unroll
+  for (int d = 0; d < 4; d++) f.dist[d] = uni(f.dist[d]);
+  f.cursor = uni(f.cursor);
   f.pad = 0;
   return f;
 }
 
-// scalar (readfirstlane), so everything derived from it stays in SGPRs
-__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
-__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-__device__ __forceinline__ int32_t wave_min(int32_t v) {
-  for (int o = 32; o > 0; o >>= 1) v = imin(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-// barrier with a workgroup fence: paints (image stores) of every wave are
-// visible to every wave after it
-__device__ __forceinline__ void block_sync() { __syncthreads(); }
-// replay counters, tuning build only (UPHIP_DIAG_NOISE bit 16)
 struct BlackStats {
-  uint32_t frames, fill_trips, check_trips, bar_trips, remeasures, lookups;
-  uint64_t t_fill, t_check, t_bar, t_remeasure, t_fa, t_fb, t_fc, t_fd, t_fa0, t_fa1, t_local, t_pop;
+  uint32_t frames, fill_trips, check_trips, bar_trips, remeasures;
+  uint64_t t_fill, t_check, t_bar, t_remeasure;
 };
 #ifdef UPHIP_DIAG
 #define BSTAT(...) __VA_ARGS__
@@ -192,673 +320,467 @@ struct BlackStats {
 #define BSTAT(...)
 #endif
 
-template <int FMT>
-struct Canvas {
-  uint8_t* base;
-  int64_t pitch;
-  int32_t W, H;
-  uint8_t mmax;  // mask_max (mask_min is 0)
-  BlackStats* bs;  // tuning build counters
-  uint32_t* nbits;  // the noisefilter's dark bit-plane of this sheet (or null)
-  int32_t nwr;      // its words per row
-  __device__ __forceinline__ bool inside(int32_t x, int32_t y) const {
-    return x >= 0 && y >= 0 && x < W && y < H;
+// left, up, right, down (fill.c:88-95)
+__device__ __forceinline__ constexpr int dir_dx(int d) { return d == 0 ? -1 : d == 2 ? 1 : 0; }
+__device__ __forceinline__ constexpr int dir_dy(int d) { return d == 1 ? -1 : d == 3 ? 1 : 0; }
+
+struct Sheet {
+  const uint64_t* RM;
+  uint64_t* RP;
+  const uint64_t* CM;
+  uint64_t* CP;
+  int32_t wpr, hpc, W, H;
+  int32_t I;  // intensity, clamped to 2^30 (lines are shorter)
+  bool live;  // mask_max < 255: a painted (white) pixel stops matching
+  // P is read and written by this wave alone.  Paints are no-return atomics
+  // (they execute at the memory side: issued and forgotten, and in order
+  // with the wave's later loads of the same word); loads bypass L1.
+  __device__ __forceinline__ static uint64_t pload(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // N matches of this wave: the loads of all are issued before any is used,
-  // so one memory round trip serves the group.  x < 0 means "no position"
-  // (no match).
-  template <int N>
-  __device__ __forceinline__ void match_group(const int32_t (&x)[N], const int32_t (&y)[N],
-                                              bool (&m)[N]) const {
-    uint8_t g[N];
-#pragma unroll
-    for (int k = 0; k < N; k++) {
-      const int32_t cy = imin(imax(y[k], 0), H - 1), cx = imin(imax(x[k], 0), W - 1);
-      g[k] = gray_of(load_px_row<FMT>(base + (int64_t)cy * pitch, cx));
-    }
-#pragma unroll
-    for (int k = 0; k < N; k++) m[k] = inside(x[k], y[k]) && g[k] <= mmax;
-    BSTAT(bs->lookups += N;)
-  }
-  __device__ __forceinline__ void paint(int32_t x, int32_t y) const {
-    if (!inside(x, y)) return;
-    store_px_row<FMT>(base + (int64_t)y * pitch, x, Px{255, 255, 255});
-    // white is not dark: the bit-plane follows the fill
-    if (nbits) atomicAnd(nbits + (int64_t)y * nwr + (x >> 5), ~(1u << (x & 31)));
+  __device__ __forceinline__ static void por(uint64_t* p, uint64_t bits) {
+    __hip_atomic_fetch_or(p, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 };
 
-// The four fill_lines (fill.c:16-52) from (px,py); dist[d] = pixels painted.
-// Per line a counter starts at 1, resets to `intensity` on a match and
-// decrements otherwise; the line stops (unpainted) where it reaches 0 or
-// leaves the image: at the first position p that is outside, or does not
-// match and lies `intensity` or more past the last match (the first
-// non-matching position if there was none).  The four lines touch disjoint
-// pixels (left, up, right, down of the start), so they share each round trip:
-// the window's slices are split evenly over the lines still running, whole
-// waves per line (16, 32 or 64 slices a line, 8 a wave).  A round trip is
-//   A: each wave reads its slices and posts their first match F, last match
-//      L, and the first stop I after F (which needs no carry from before);
-//   C: one barrier, then every wave walks each line's posts in order with
-//      the carry (last match so far) to find the line's stop, uniformly;
-//   D: paint up to the stop.
-// The posts alternate between two buffers, so a round trip has one barrier;
-// the paints are published by the barrier after the four lines.
-// The four fill_lines (fill.c:16-52) from (px,py); dist[d] = pixels painted.
-// Per line a counter starts at 1, resets to `intensity` on a match and
-// decrements otherwise; the line stops (unpainted) where it reaches 0 or
-// leaves the image: at the first position p that is outside, or does not
-// match and lies `intensity` or more past the last match (the first
-// non-matching position if there was none).  The four lines touch disjoint
-// pixels (left, up, right, down of the start), so they share each round trip.
-//
-// fill_local: the first round trip, by the driving wave alone: the first
-// 64 kLocalSl positions of each line.  Most lines of most frames end there.  The lines' state goes to `lpost`; returns
-// whether a line runs on.
-constexpr int kLocalSl = 2;  // slices per line of a frame's first round trip (1: more lines go cooperative, slower overall)
+// A lane's window: 64 positions of a line, loaded as two words of M and P of
+// the line's plane (row lines: the row planes, column lines: the column
+// planes), issued by `issue` and combined by `bits` so that the loads of a
+// round trip are in flight together.  Line `ln` (row y or column x) holds
+// coordinates 0 .. len-1; the window holds coordinates s .. s+63 (bit i is
+// s + i; zero outside).
+struct Win {
+  uint64_t m0, m1, p0, p1;
+  int32_t sh;
+  bool ok0, ok1;
+  __device__ __forceinline__ void issue(const Sheet& S, bool col, int32_t ln, int32_t s) {
+    // plain values first: a per-lane choice between two members of S would
+    // otherwise become a per-lane address into a private copy of S
+    const int32_t W = S.W, H = S.H, hpc = S.hpc, wpr = S.wpr;
+    const uint64_t *CM = S.CM, *RM = S.RM, *CP = S.CP, *RP = S.RP;
+    const int32_t nl = col ? W : H, nw = col ? hpc : wpr;
+    const uint64_t* M = col ? CM : RM;
+    const uint64_t* P = col ? CP : RP;
+    const int32_t w0 = s >> 6;  // floor
+    const bool lok = ln >= 0 && ln < nl;
+    ok0 = lok && w0 >= 0 && w0 < nw;
+    ok1 = lok && w0 + 1 >= 0 && w0 + 1 < nw;
+    sh = s & 63;
+    const int64_t b = (int64_t)(lok ? ln : 0) * nw;
+    const int64_t i0 = b + (ok0 ? w0 : 0), i1 = b + (ok1 ? w0 + 1 : 0);
+    m0 = M[i0];
+    m1 = M[i1];
+    p0 = Sheet::pload(P + i0);
+    p1 = Sheet::pload(P + i1);
+  }
+  __device__ __forceinline__ uint64_t bits(const Sheet& S) const {
+    const uint64_t e0 = ok0 ? (S.live ? m0 & ~p0 : m0) : 0;
+    const uint64_t e1 = ok1 ? (S.live ? m1 & ~p1 : m1) : 0;
+    return sh ? (e0 >> sh) | (e1 << (64 - sh)) : e0;
+  }
+};
 
-template <int FMT>
-__device__ __forceinline__ bool fill_local(const Canvas<FMT>& C, int32_t px, int32_t py,
-                                           uint64_t intensity, int32_t (&dist)[4],
-                                           BlackStats* bs) {
+// Positions j = base .. base+63 along a line from (cx, cy) in direction d,
+// at perpendicular offset `off` (a neighbour side): the lane's window issue,
+// and its bits in position order.
+__device__ __forceinline__ void ray_issue(const Sheet& S, Win& w, int d, int32_t cx, int32_t cy,
+                                          int32_t off, int32_t base) {
+  const bool col = d & 1;
+  const int32_t ln = col ? cx + off : cy + off;  // the row / column the positions lie on
+  const int32_t c0 = col ? cy : cx;
+  const bool dec = d < 2;  // left, up: coordinates fall with the position
+  w.issue(S, col, ln, dec ? c0 - base - 63 : c0 + base);
+}
+__device__ __forceinline__ uint64_t ray_bits(const Sheet& S, const Win& w, int d) {
+  const uint64_t v = w.bits(S);
+  return d < 2 ? __builtin_bitreverse64(v) : v;
+}
+
+// A window of 64 positions base .. base+63 of a fill line (E: bit k set iff
+// position base+k matches), with L the last matching position before it
+// (1 - I when none: the counter starts at 1, fill.c:20): the line's stop in
+// this window, or INT_MAX.  The counter reaches 0 at the first non-matching
+// position j with j - L >= I; before the window's first match f that is
+// max(base, L + I) if it lies below base + f, after it the first position
+// with no match in the I positions ending at it (the smear of E over I - 1
+// positions, exact inside the window since a run reaching back past f holds f).
+__device__ __forceinline__ int32_t window_stop(uint64_t E, int32_t base, int32_t L, int32_t I) {
+  const int f = E ? ctz64(E) : 64;
+  const int32_t j = imax(base, L + I);
+  if (j < base + f) return j;
+  if (I >= 64 || f >= 63) return INT_MAX;
+  uint64_t cur = E;
+  int len = 1;
+  while (2 * len <= I) {
+    cur |= cur << len;
+    len *= 2;
+  }
+  if (len < I) cur |= cur << (I - len);
+  const uint64_t cand = ~cur & (~0ull << (f + 1));
+  return cand ? base + ctz64(cand) : INT_MAX;
+}
+
+// Paint the cross at (px, py): the start and positions 1 .. dist[d] of its
+// four lines.  In the own planes (row py: [px - dist0, px + dist2], column
+// px: [py - dist1, py + dist3]) a word per lane; in the crossing planes a bit
+// per lane (column words of the row's pixels, row words of the column's).
+__device__ __forceinline__ void paint_cross(const Sheet& S, int32_t px, int32_t py,
+                                            const int32_t (&dist)[4]) {
   const int lane = lane_id();
-  const uint64_t upto_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-  int32_t* lpost = tab_stop() + 6 * kWaves;  // [4] stop | [4] has_last | [4] last
-  bool more = false;
-  int32_t qx[4 * kLocalSl], qy[4 * kLocalSl];
-  bool m[4 * kLocalSl];
-#pragma unroll
-  for (int i = 0; i < 4 * kLocalSl; i++) {
-    const int dd = i / kLocalSl;
-    const int32_t j = 1 + 64 * (i % kLocalSl) + lane;
-    qx[i] = dd == 0 ? px - j : dd == 2 ? px + j : px;
-    qy[i] = dd == 1 ? py - j : dd == 3 ? py + j : py;
-  }
-  C.match_group(qx, qy, m);
-#pragma unroll
-  for (int dd = 0; dd < 4; dd++) {
-    bool hl = false;
-    int32_t lm = 0, stop = INT_MAX;
-#pragma unroll
-    for (int k = 0; k < kLocalSl; k++) {
-      const int i = kLocalSl * dd + k;
-      const unsigned long long Mi = __ballot(m[i]);
-      if (stop == INT_MAX) {
-        const int32_t p0 = 1 + 64 * k, j = p0 + lane;
-        const unsigned long long upto = Mi & upto_mask;
-        bool lhl = hl;
-        int32_t llm = lm;
-        if (upto) {
-          lhl = true;
-          llm = p0 + (63 - __clzll((long long)upto));
-        }
-        bool st = !C.inside(qx[i], qy[i]);
-        if (lhl) st |= (uint64_t)(uint32_t)(j - llm) >= intensity;
-        else st |= j >= 1;
-        const unsigned long long S = __ballot(st);
-        if (S) stop = p0 + __ffsll((long long)S) - 1;
-        if (Mi) {
-          hl = true;
-          lm = p0 + (63 - __clzll((long long)Mi));
-        }
-      }
+  const int32_t xa = px - dist[0], xb = px + dist[2], ya = py - dist[1], yb = py + dist[3];
+  const int32_t nrw = (xb >> 6) - (xa >> 6) + 1, nown = nrw + (yb >> 6) - (ya >> 6) + 1;
+  const int32_t nrx = dist[0] + dist[2], ncross = nrx + dist[1] + dist[3];
+  uint64_t *RP = S.RP, *CP = S.CP;
+  const int32_t wpr = S.wpr, hpc = S.hpc;
+  for (int32_t i0 = 0; i0 < imax(nown, ncross); i0 += 64) {
+    const int32_t i = i0 + lane;
+    if (i < nown) {
+      const bool row = i < nrw;
+      const int32_t lo = row ? xa : ya, hi = row ? xb : yb;
+      const int32_t w = (lo >> 6) + (row ? i : i - nrw);
+      const int a = imax(lo - 64 * w, 0), b = imin(hi - 64 * w, 63);
+      Sheet::por(row ? RP + (int64_t)py * wpr + w : CP + (int64_t)px * hpc + w,
+                 (~0ull >> (63 - b)) & (~0ull << a));
     }
-#pragma unroll
-    for (int k = 0; k < kLocalSl; k++)
-      if (1 + 64 * k + lane < stop) C.paint(qx[kLocalSl * dd + k], qy[kLocalSl * dd + k]);
-    if (lane == 0) {
-      lpost[dd] = stop;
-      lpost[4 + dd] = hl;
-      lpost[8 + dd] = lm;
-    }
-    if (stop != INT_MAX) set4(dist, dd, stop - 1);
-    else more = true;
-  }
-  BSTAT(bs->fill_trips++;)
-  return more;
-}
-
-// fill_coop: the rest of the lines, by the whole workgroup, from the state in
-// `lpost`: the window's slices are split evenly over the lines still running,
-// whole waves per line (16, 32 or 64 slices a line, 8 a wave).  A round trip is
-//   A: each wave reads its slices and posts their first match F, last match
-//      L, and the first stop I after F (which needs no carry from before);
-//   C: one barrier, then every wave walks each line's posts in order with
-//      the carry (last match so far) to find the line's stop, uniformly;
-//   D: paint up to the stop.
-// The posts alternate between two buffers, so a round trip has one barrier;
-// the paints are published by the barrier after the four lines.
-template <int FMT>
-__device__ __forceinline__ void fill_coop(const Canvas<FMT>& C, int32_t px, int32_t py,
-                                          uint64_t intensity, int32_t (&dist)[4],
-                                          BlackStats* bs) {
-  const int w = wave_id(), lane = lane_id();
-  BSTAT(const uint64_t t0 = wall_clock64();)
-  uint32_t done = 0, has_last = 0;  // per line bits (bool arrays indexed by a
-                                    // run-time line would live in scratch)
-  int32_t last[4] = {0, 0, 0, 0};   // positions along a line fit 31 bits
-  constexpr int32_t kFirst = 1 + 64 * kLocalSl;  // fill_local read positions 1 .. kFirst - 1
-  int32_t pos0[4] = {kFirst, kFirst, kFirst, kFirst};
-  // first position outside the image, per line
-  const int32_t edge[4] = {px + 1, py + 1, C.W - px, C.H - py};
-  const uint64_t upto_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-  {
-    const int32_t* lpost = tab_stop() + 6 * kWaves;
-    const int32_t v = lane < 12 ? lpost[lane] : 0;
-#pragma unroll
-    for (int dd = 0; dd < 4; dd++) {
-      const int32_t stop = __builtin_amdgcn_readlane(v, dd);
-      if (stop != INT_MAX) {
-        done |= 1u << dd;
-        set4(dist, dd, stop - 1);
-      } else {
-        if (__builtin_amdgcn_readlane(v, 4 + dd)) has_last |= 1u << dd;
-        set4(last, dd, __builtin_amdgcn_readlane(v, 8 + dd));
-      }
-    }
-  }
-  int parity = 0;
-  for (;;) {
-    uint32_t actp = 0;  // running lines, a nibble each
-    int nact = 0;
-#pragma unroll
-    for (int d = 0; d < 4; d++)
-      if (!((done >> d) & 1)) actp |= (uint32_t)d << (4 * nact++);
-    if (nact == 0) break;
-    const int lg = nact == 1 ? 6 : nact == 2 ? 5 : 4;  // log2 slices per line
-    const int spd = 1 << lg, wpl = spd / kGroup;        // slices, waves per line
-    // this wave's line and first slice (uniform)
-    const int a = (w * kGroup) >> lg, k0 = (w * kGroup) & (spd - 1);
-    const bool valid = a < nact;
-    const int d = (int)((actp >> (4 * (valid ? a : 0))) & 15);
-    const int32_t base0 = pick4(pos0, d) + 64 * k0;  // position of lane 0, slice 0
-    int32_t* post = tab_stop() + parity * 3 * kWaves;  // F | L | I, per wave
-    parity ^= 1;
-    BSTAT(uint64_t tp = wall_clock64();)
-    // A
-    int32_t qx[kGroup], qy[kGroup];
-    bool m[kGroup];
-#pragma unroll
-    for (int i = 0; i < kGroup; i++) {
-      const int32_t j = base0 + 64 * i + lane;
-      qx[i] = !valid ? -1 : d == 0 ? px - j : d == 2 ? px + j : px;
-      qy[i] = d == 1 ? py - j : d == 3 ? py + j : py;
-    }
-    BSTAT(bs->t_fa0 += wall_clock64() - tp;)
-    C.match_group(qx, qy, m);
-    BSTAT(bs->t_fa1 += wall_clock64() - tp;)
-    int32_t F = -1, L = -1, I = INT_MAX;
-    {
-      bool hl = false;  // a match earlier in this wave's slices
-      int32_t lm = 0;
-#pragma unroll
-      for (int i = 0; i < kGroup; i++) {
-        const unsigned long long Mi = __ballot(m[i]);
-        const int32_t p0 = base0 + 64 * i, j = p0 + lane;
-        if (I == INT_MAX) {
-          const unsigned long long upto = Mi & upto_mask;
-          bool lhl = hl;
-          int32_t llm = lm;
-          if (upto) {
-            lhl = true;
-            llm = p0 + (63 - __clzll((long long)upto));
-          }
-          // after the wave's first match only: before it the carry decides
-          const unsigned long long S = __ballot(lhl && (uint64_t)(uint32_t)(j - llm) >= intensity);
-          if (S) I = p0 + __ffsll((long long)S) - 1;
-        }
-        if (Mi) {
-          if (F < 0) F = p0 + __ffsll((long long)Mi) - 1;
-          L = p0 + (63 - __clzll((long long)Mi));
-          hl = true;
-          lm = L;
-        }
-      }
-    }
-    if (lane == 0) {
-      post[w] = valid ? F : -1;
-      post[kWaves + w] = valid ? L : -1;
-      post[2 * kWaves + w] = valid ? I : INT_MAX;
-    }
-    block_sync();
-    BSTAT(bs->t_fa += wall_clock64() - tp; tp = wall_clock64();)
-    // C (uniform): per line, lanes stand for its waves; each lane takes the
-    // carry from the line's earlier waves (or the previous round trip) and
-    // finds its wave's stop; the first lane with one has the line's stop
-    const int32_t vF = lane < kWaves ? post[lane] : -1;
-    const int32_t vL = lane < kWaves ? post[kWaves + lane] : -1;
-    const int32_t vI = lane < kWaves ? post[2 * kWaves + lane] : INT_MAX;
-    const unsigned long long withL = __ballot(vL >= 0);
-    int32_t sd[4] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX};
-#pragma unroll
-    for (int aa = 0; aa < 4; aa++) {
-      if (aa >= nact) break;
-      const int dd = (int)((actp >> (4 * aa)) & 15);
-      const int lo = aa * wpl;
-      const unsigned long long range = ((1ull << wpl) - 1) << lo;
-      const bool inr = (range >> lane) & 1;
-      const unsigned long long before = withL & range & ((1ull << lane) - 1);
-      const int src = before ? 63 - __clzll((long long)before) : lane;
-      const int32_t lmv = __shfl(vL, src, 64);
-      const bool has = before ? true : ((has_last >> dd) & 1);
-      const int32_t lm = before ? lmv : pick4(last, dd);
-      const int32_t Pv = pick4(pos0, dd) + 64 * kGroup * (lane - lo);
-      const int32_t end = vF >= 0 ? vF : Pv + 64 * kGroup;  // no match in [Pv, end)
-      const int32_t cand =
-          has ? imax(Pv, (int32_t)imin((int64_t)lm + (int64_t)intensity, (int64_t)INT_MAX)) : Pv;
-      const int32_t sv = cand < end ? cand : vI;
-      const unsigned long long stops = __ballot(inr && sv != INT_MAX);
-      int32_t stop = stops ? __shfl(sv, __ffsll((long long)stops) - 1, 64) : INT_MAX;
-      stop = imin(stop, pick4(edge, dd));
-      if (stop < pick4(pos0, dd) + 64 * spd) {
-        set4(sd, dd, stop);
-        done |= 1u << dd;
-        set4(dist, dd, stop - 1);
-      } else {
-        const unsigned long long mine = withL & range;
-        if (mine) {
-          has_last |= 1u << dd;
-          set4(last, dd, __shfl(vL, 63 - __clzll((long long)mine), 64));
-        }
-        set4(pos0, dd, pick4(pos0, dd) + 64 * spd);
-      }
-    }
-    BSTAT(bs->t_fc += wall_clock64() - tp; tp = wall_clock64();)
-    // D
-    if (valid) {
-      const int32_t lim = pick4(sd, d);
-#pragma unroll
-      for (int i = 0; i < kGroup; i++)
-        if (base0 + 64 * i + lane < lim) C.paint(qx[i], qy[i]);
-    }
-    BSTAT(bs->t_fd += wall_clock64() - tp; bs->fill_trips++;)
-  }
-  block_sync();  // the lines' paints, before any check reads them
-  BSTAT(bs->t_fill += wall_clock64() - t0;)
-}
-
-// Neighbour check number c of a frame (flood_fill_around_line, fill.c:62-79):
-// the checks of line 0, then 1, 2, 3; along a line two per position, below
-// then above (horizontal line) or right then left (vertical line).
-__device__ __forceinline__ void check_pos(const Frame& f, int32_t c, int32_t* qx, int32_t* qy) {
-  const int32_t n0 = 2 * f.dist[0], n1 = n0 + 2 * f.dist[1], n2 = n1 + 2 * f.dist[2];
-  const int d = c < n0 ? 0 : c < n1 ? 1 : c < n2 ? 2 : 3;
-  const int32_t cc = c - (d == 0 ? 0 : d == 1 ? n0 : d == 2 ? n1 : n2);
-  const int32_t t = (cc >> 1) + 1, sub = cc & 1;
-  const int dx = dir_dx(d), dy = dir_dy(d);
-  int32_t x = f.x + t * dx, y = f.y + t * dy;
-  if (dx != 0) y += sub == 0 ? 1 : -1;  // below, then above
-  else x += sub == 0 ? 1 : -1;           // right, then left
-  *qx = x;
-  *qy = y;
-}
-
-// First match of a window whose slices were looked up by every wave: each
-// wave posts the index of its first matching position (or INT_MAX) into the
-// buffer of this round trip's parity, then all read the minimum.  M[i] is
-// the ballot of slice i; with pairs (every lane two consecutive positions),
-// M0[i] says which lanes matched their first one.
-template <bool kPairs>
-__device__ __forceinline__ int32_t window_first(const uint64_t (&M)[kGroup],
-                                                const uint64_t (&M0)[kGroup], int parity) {
-  const int w = wave_id(), lane = lane_id();
-  int32_t lf = INT_MAX;
-#pragma unroll
-  for (int i = kGroup - 1; i >= 0; i--) {
-    if (M[i]) {
-      const int L = __ffsll((long long)M[i]) - 1;
-      const int32_t u = 64 * (w * kGroup + i) + L;
-      lf = kPairs ? 2 * u + (((M0[i] >> L) & 1) ? 0 : 1) : u;
-    }
-  }
-  int32_t* first = tab_first() + parity * kWaves;
-  if (lane == 0) first[w] = lf;
-  block_sync();
-  // waves hold consecutive slices: the first wave that found one has the minimum
-  const int32_t v = lane < kWaves ? first[lane] : INT_MAX;
-  const unsigned long long any = __ballot(v != INT_MAX);
-  return any ? __shfl(v, __ffsll((long long)any) - 1, 64) : INT_MAX;
-}
-
-// The flood fill is driven by wave 0 alone.  Its small steps (a frame's
-// first 128 pixels per line, a check window of at most 512 checks) need no
-// other wave and no barrier; a long line or a long run of checks is posted as
-// a command, and the other waves, parked in `flood_help`, join for it.
-// A command's operation ends in a barrier that every wave reaches, so the
-// driver never rewrites the mailbox before the helpers have read it.
-enum : int32_t { CMD_DONE = 0, CMD_FILL = 1, CMD_CHECK = 2 };
-// mailbox: [0] sequence, [1] command, [2..3] fill start, [4..11] frame
-// (x, y, dist[4], cursor, checks), [12] flood result
-
-__device__ __forceinline__ void post_command(int32_t* seq, int32_t cmd) {
-  int32_t* mb = mailbox();
-  if (lane_id() == 0) mb[1] = cmd;
-  // arguments and paints before the sequence number that publishes them
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if (lane_id() == 0) __hip_atomic_store(&mb[0], ++*seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  else ++*seq;
-}
-
-// One check window of the whole workgroup (64 slices, 4096 checks).
-template <int FMT>
-__device__ __forceinline__ int32_t check_coop(const Canvas<FMT>& C, const Frame& top, int32_t n,
-                                              int* parity, BlackStats* bs) {
-  const int w = wave_id(), lane = lane_id();
-  int32_t qx[kGroup], qy[kGroup];
-  bool m[kGroup];
-#pragma unroll
-  for (int i = 0; i < kGroup; i++) {
-    const int32_t c = top.cursor + 64 * (w * kGroup + i) + lane;
-    check_pos(top, imin(c, n - 1), &qx[i], &qy[i]);
-    if (c >= n) qx[i] = -1;
-  }
-  C.match_group(qx, qy, m);
-  uint64_t M[kGroup];
-#pragma unroll
-  for (int i = 0; i < kGroup; i++) M[i] = __ballot(m[i]);
-  return window_first<false>(M, M, (*parity)++ & 1);
-}
-
-// The helpers' side: run the driver's commands until CMD_DONE.
-template <int FMT>
-__device__ void flood_help(const Canvas<FMT>& C, uint64_t intensity, int32_t* seen, int* parity,
-                           BlackStats* bs) {
-  int32_t* mb = mailbox();
-  for (;;) {
-    int32_t sq;
-    while ((sq = __hip_atomic_load(&mb[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
-           *seen)
-      __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    *seen = sq;
-    const int32_t cmd = mb[1];
-    if (cmd == CMD_DONE) return;
-    if (cmd == CMD_FILL) {
-      int32_t dist[4];
-      fill_coop<FMT>(C, mb[2], mb[3], intensity, dist, bs);
-    } else {
-      Frame f;
-      f.x = mb[4];
-      f.y = mb[5];
-      f.dist[0] = mb[6];
-      f.dist[1] = mb[7];
-      f.dist[2] = mb[8];
-      f.dist[3] = mb[9];
-      f.cursor = mb[10];
-      check_coop<FMT>(C, f, mb[11], parity, bs);
+    if (i < nrx) {
+      const int32_t x = i < dist[0] ? px - 1 - i : px + 1 + (i - dist[0]);
+      Sheet::por(CP + (int64_t)x * hpc + (py >> 6), 1ull << (py & 63));
+    } else if (i < ncross) {
+      const int32_t j = i - nrx;
+      const int32_t y = j < dist[1] ? py - 1 - j : py + 1 + (j - dist[1]);
+      Sheet::por(RP + (int64_t)y * wpr + (px >> 6), 1ull << (px & 63));
     }
   }
 }
 
-// flood_fill (fill.c:81-107) + flood_fill_around_line (fill.c:62-79), depth
-// first with an explicit stack in HBM, driven by wave 0.  Returns false on a
-// stack overflow.
-template <int FMT>
-__device__ bool flood_drive(const Canvas<FMT>& C, int32_t sx, int32_t sy, uint64_t intensity,
-                            Frame* stack, int32_t capacity, int32_t* seq, int* parity,
-                            BlackStats* bs) {
+// The four fill_lines of a frame at (px, py) (fill.c:16-43, :88-95): left,
+// up, right, down.  They touch disjoint pixels, so they run together: lanes
+// 16d .. 16d+15 hold line d's windows of a round trip (1024 positions), each
+// lane finds its window's stop given the last match of the lanes before it
+// (or of the trips before), and the first lane with a stop has the line's.
+// `w` holds the first trip's windows, issued by the caller (fill_issue).
+// dist[d]: pixels painted (positions 1 .. dist); the paints (the start too)
+// are issued here.
+__device__ __forceinline__ void fill_issue(const Sheet& S, Win& w, int32_t px, int32_t py) {
   const int lane = lane_id();
-  int32_t* mb = mailbox();
+  ray_issue(S, w, lane >> 4, px, py, 0, 1 + 64 * (lane & 15));
+}
+__device__ __forceinline__ void fill_cross(const Sheet& S, int32_t px, int32_t py, int32_t (&dist)[4],
+                                           Win& w, BlackStats* bs) {
+  const int lane = lane_id(), ln = lane >> 4, k = lane & 15;
+  if (S.I == 0) {  // the counter is 0 after the first position, whatever it holds
+#pragma unroll
+    for (int d = 0; d < 4; d++) dist[d] = 0;
+    paint_cross(S, px, py, dist);  // the start
+    return;
+  }
+  const int32_t edge[4] = {px + 1, py + 1, S.W - px, S.H - py};  // first position outside
+  int32_t pos0[4] = {1, 1, 1, 1}, carry[4], stop[4];
+#pragma unroll
+  for (int d = 0; d < 4; d++) carry[d] = 1 - S.I;
+  uint32_t done = 0;
+  for (int trip = 0; done != 15; trip++) {
+    BSTAT(bs->fill_trips++;)
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      pos0[d] = uni(pos0[d]);
+      carry[d] = uni(carry[d]);
+    }
+    done = uni(done);
+    const bool run = !((done >> ln) & 1);
+    const int32_t base = pick4(pos0, ln) + 64 * k;
+    if (trip > 0 && run) ray_issue(S, w, ln, px, py, 0, base);
+    const uint64_t E = run ? ray_bits(S, w, ln) : 0;
+    // the last match of this line's lanes before this one, or the carry
+    const int32_t lastabs = E ? base + hib64(E) : INT_MIN;
+    const uint64_t hasb = __ballot(E != 0);
+    const uint64_t before = hasb & lane_range(16 * ln, k);
+    const int32_t lsrc = __shfl(lastabs, before ? hib64(before) : lane, 64);
+    const int32_t L = before ? lsrc : pick4(carry, ln);
+    const int32_t st = run ? window_stop(E, base, L, S.I) : INT_MAX;
+    const uint64_t stb = __ballot(st != INT_MAX);
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      if ((done >> d) & 1) continue;
+      const uint64_t rng = lane_range(16 * d, 16);
+      int32_t sd = (stb & rng) ? __builtin_amdgcn_readlane(st, ctz64(stb & rng)) : INT_MAX;
+      const int32_t end = pos0[d] + 64 * 16;  // first position not read
+      if (sd == INT_MAX && end > edge[d]) sd = edge[d];
+      if (sd != INT_MAX) {
+        stop[d] = imin(sd, edge[d]);
+        done |= 1u << d;
+      } else {
+        if (hasb & rng) carry[d] = __builtin_amdgcn_readlane(lastabs, hib64(hasb & rng));
+        pos0[d] = end;
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 4; d++) dist[d] = uni(stop[d] - 1);
+  paint_cross(S, px, py, dist);
+}
+
+// Neighbour checks (flood_fill_around_line, fill.c:54-74): the checks of line
+// 0, then 1, 2, 3; along a line two per position, below then above (row line)
+// or right then left (column line).  A round trip reads 8 windows of both
+// sides of the cursor's line dc from position p[dc] and of each later line
+// from its start (lanes 16d + 8side + k).  Checks that do not match now
+// cannot match later (paints only clear), and the cross's own paints touch
+// none of its checks, so a frame's first round trip is issued with its fill.
+constexpr int kChkWin = 8;
+__device__ __forceinline__ void check_issue(const Sheet& S, Win& w, const Frame& f, int dc,
+                                            const int32_t (&p)[4], bool dist_known) {
+  const int lane = lane_id(), ln = lane >> 4, side = (lane >> 3) & 1, k = lane & 7;
+  const int32_t base = pick4(p, ln) + 64 * k;
+  if (ln >= dc && (!dist_known || base <= pick4(f.dist, ln)))
+    ray_issue(S, w, ln, f.x, f.y, side == 0 ? 1 : -1, base);
+}
+// The loaded windows' first match at or after the cursor (line dc, position
+// t, side sub), in check order; INT_MAX when none, with *next the first check
+// not read.  *resume: where the frame goes on after that match's child: the
+// next check, or, when the windows hold no other match, the first check not
+// read (the checks between stay non-matching).
+__device__ __forceinline__ int32_t check_eval(const Sheet& S, const Win& w, const Frame& f,
+                                              const int32_t (&cs)[5], int dc, int32_t sub,
+                                              const int32_t (&p)[4], int32_t* resume,
+                                              int32_t* next) {
+  const int lane = lane_id(), ln = lane >> 4, side = (lane >> 3) & 1, k = lane & 7;
+  const int32_t dl = pick4(f.dist, ln);
+  const int32_t base = pick4(p, ln) + 64 * k;
+  const bool on = ln >= dc && base <= dl;
+  uint64_t E = on ? ray_bits(S, w, ln) : 0;
+  const int32_t lim = dl - base + 1;  // this window's positions on the line
+  if (lim < 64) E &= lim > 0 ? (1ull << lim) - 1 : 0;
+  if (ln == dc && side == 0 && k == 0 && sub) E &= ~1ull;  // behind the cursor
+  const int32_t fp = E ? base + ctz64(E) : INT_MAX;
+  const uint64_t hasb = __ballot(E != 0);
+  const bool multi = __ballot(__popcll(E) >= 2) != 0 || __popcll(hasb) >= 2;
+  int32_t cov = cs[4];  // the first check not read
+#pragma unroll
+  for (int d = 3; d >= 0; d--)
+    if (d >= dc && p[d] + 64 * kChkWin <= f.dist[d]) cov = cs[d] + 2 * (p[d] + 64 * kChkWin - 1);
+  *next = cov;
+#pragma unroll
+  for (int d = 0; d < 4; d++) {
+    if (d < dc) continue;
+    const uint64_t r0 = hasb & lane_range(16 * d, 8), r1 = hasb & lane_range(16 * d + 8, 8);
+    const int32_t f0 = r0 ? __builtin_amdgcn_readlane(fp, ctz64(r0)) : INT_MAX;
+    const int32_t f1 = r1 ? __builtin_amdgcn_readlane(fp, ctz64(r1)) : INT_MAX;
+    if (f0 != INT_MAX || f1 != INT_MAX) {
+      const int32_t c = f0 <= f1 ? cs[d] + 2 * (f0 - 1) : cs[d] + 2 * (f1 - 1) + 1;
+      *resume = multi ? c + 1 : cov;
+      return c;
+    }
+    if (p[d] + 64 * kChkWin <= f.dist[d]) return INT_MAX;  // the line goes on past the windows
+  }
+  return INT_MAX;
+}
+__device__ __forceinline__ void check_cursor(const int32_t (&cs)[5], int32_t c, int* dc,
+                                             int32_t (&p)[4], int32_t* sub) {
+  *dc = c < cs[1] ? 0 : c < cs[2] ? 1 : c < cs[3] ? 2 : 3;
+  const int32_t cd = *dc == 0 ? 0 : *dc == 1 ? cs[1] : *dc == 2 ? cs[2] : cs[3];
+#pragma unroll
+  for (int d = 0; d < 4; d++) p[d] = d == *dc ? ((c - cd) >> 1) + 1 : 1;
+  *sub = (c - cd) & 1;
+}
+// The first matching check of frame f at or after check c, or n (none).
+__device__ __forceinline__ int32_t check_scan(const Sheet& S, const Frame& f,
+                                              const int32_t (&cs)[5], int32_t c, int32_t* resume,
+                                              BlackStats* bs) {
+  while (c < cs[4]) {
+    BSTAT(bs->check_trips++;)
+    c = uni(c);
+    int dc;
+    int32_t p[4], sub;
+    check_cursor(cs, c, &dc, p, &sub);
+    Win w;
+    check_issue(S, w, f, dc, p, true);
+    int32_t nx;
+    const int32_t r = check_eval(S, w, f, cs, dc, sub, p, resume, &nx);
+    if (r != INT_MAX) return r;
+    c = nx;
+  }
+  return cs[4];
+}
+
+// flood_fill (fill.c:81-107) + flood_fill_around_line (fill.c:54-74), depth
+// first with an explicit stack.  The caller has just read (sx, sy) as
+// matching.  Returns false on a stack overflow.
+__device__ __forceinline__ bool flood(const Sheet& S, int32_t sx, int32_t sy, Frame* stack,
+                                      int32_t capacity, BlackStats* bs) {
   Frame top;
-  int32_t sp = 0;  // frames on the stack, `top` included; those below it live in stack[0 .. sp-2]
+  int32_t sp = 0;  // frames on the stack, `top` included; those below it in stack[0 .. sp-2]
   int32_t nx = sx, ny = sy;
   bool start = true;
   for (;;) {
-    if (start) {  // a new frame: save the parent, paint the start, fill the cross
-      if (sp >= capacity) return false;  // stack overflow: flagged by the caller
-      if (sp > 0 && lane == 0) frame_put(stack_lds(), stack, sp - 1, top);
-      // the caller has just read the start pixel as matching (a neighbour
-      // check or a bar pixel) and nothing has painted since
-      if (lane == 0) C.paint(nx, ny);
+    sp = uni(sp);
+    nx = uni(nx);
+    ny = uni(ny);
+    int32_t c, resume = 0;
+    int32_t cs[5];
+    if (start) {
+      // a new frame: save the parent; one round trip for the fill's first
+      // windows and the first check windows
+      if (sp >= capacity) return false;
+      if (sp > 0 && lane_id() == 0) frame_put(stack, sp - 1, top);
       top.x = nx;
       top.y = ny;
-      BSTAT(const uint64_t tl = wall_clock64();)
-      const bool more = fill_local<FMT>(C, nx, ny, intensity, top.dist, bs);
-      BSTAT(bs->t_local += wall_clock64() - tl;)
-      if (more) {
-        if (lane == 0) {
-          mb[2] = nx;
-          mb[3] = ny;
-        }
-        post_command(seq, CMD_FILL);
-        fill_coop<FMT>(C, nx, ny, intensity, top.dist, bs);
-      }
-      top.cursor = 0;
-      BSTAT(bs->frames++;)
+      Win wf, wc;
+      fill_issue(S, wf, nx, ny);
+      const int32_t p1[4] = {1, 1, 1, 1};
+      check_issue(S, wc, top, 0, p1, false);
+      BSTAT(const uint64_t t0 = wall_clock64();)
+      fill_cross(S, nx, ny, top.dist, wf, bs);
+      BSTAT(bs->t_fill += wall_clock64() - t0; bs->frames++;)
+      cs[0] = 0;
+#pragma unroll
+      for (int d = 0; d < 4; d++) cs[d + 1] = cs[d] + 2 * top.dist[d];
+      BSTAT(const uint64_t t1 = wall_clock64(); bs->check_trips++;)
+      int32_t nxt;
+      c = uni(check_eval(S, wc, top, cs, 0, 0, p1, &resume, &nxt));
+      if (c == INT_MAX) c = uni(check_scan(S, top, cs, nxt, &resume, bs));
+      BSTAT(bs->t_check += wall_clock64() - t1;)
       sp++;
       start = false;
-    }
-    const int32_t n = 2 * (top.dist[0] + top.dist[1] + top.dist[2] + top.dist[3]);
-    if (top.cursor >= n) {
-      if (--sp == 0) return true;
-      BSTAT(const uint64_t tq = wall_clock64();)
-      top = frame_get(stack_lds(), stack, sp - 1);
-      BSTAT(bs->t_pop += wall_clock64() - tq;)
-      continue;
-    }
-    BSTAT(const uint64_t tc = wall_clock64(); bs->check_trips++;)
-    int32_t f;
-    int32_t span;
-    // this wave alone when its 8 slices cover the rest, and for a frame's
-    // first window (a new frame's first checks usually start its child)
-    if (n - top.cursor <= 64 * kGroup || top.cursor == 0) {
-      span = 64 * kGroup;
-      const int nsl = imin((n - top.cursor + 63) >> 6, kGroup);  // slices holding checks
-      int32_t qx[kGroup], qy[kGroup];
-      bool m[kGroup];
-#pragma unroll
-      for (int i = 0; i < kGroup; i++) {
-        qx[i] = -1;
-        qy[i] = 0;
-        if (i < nsl) {
-          const int32_t c = top.cursor + 64 * i + lane;
-          check_pos(top, imin(c, n - 1), &qx[i], &qy[i]);
-          if (c >= n) qx[i] = -1;
-        }
-      }
-      C.match_group(qx, qy, m);
-      // the first match and the one after it: painting only turns pixels
-      // white, so checks that did not match now cannot match after the
-      // child's fill either, and the frame resumes at the second match (or,
-      // with none, is done) without reading its checks again
-      f = INT_MAX;
-      int32_t f2 = INT_MAX;
-#pragma unroll
-      for (int i = kGroup - 1; i >= 0; i--) {
-        const unsigned long long Mi = __ballot(m[i]);
-        if (Mi) {
-          const unsigned long long rest = Mi & (Mi - 1);
-          f2 = rest ? 64 * i + __ffsll((long long)rest) - 1 : f;
-          f = 64 * i + __ffsll((long long)Mi) - 1;
-        }
-      }
-      if (f != INT_MAX) {
-        const int32_t cidx = top.cursor + f;
-        check_pos(top, cidx, &nx, &ny);
-        top.cursor = f2 != INT_MAX ? top.cursor + f2 : imin(n, top.cursor + 64 * nsl);
-        BSTAT(bs->t_check += wall_clock64() - tc;)
-        start = true;
-        continue;
-      }
     } else {
-      span = 64 * kSlices;
-      if (lane == 0) {
-        mb[4] = top.x;
-        mb[5] = top.y;
-        mb[6] = top.dist[0];
-        mb[7] = top.dist[1];
-        mb[8] = top.dist[2];
-        mb[9] = top.dist[3];
-        mb[10] = top.cursor;
-        mb[11] = n;
-      }
-      post_command(seq, CMD_CHECK);
-      f = check_coop<FMT>(C, top, n, parity, bs);
+      cs[0] = 0;
+#pragma unroll
+      for (int d = 0; d < 4; d++) cs[d + 1] = cs[d] + 2 * top.dist[d];
+      BSTAT(const uint64_t t1 = wall_clock64();)
+      c = uni(check_scan(S, top, cs, top.cursor, &resume, bs));
+      BSTAT(bs->t_check += wall_clock64() - t1;)
     }
-    BSTAT(bs->t_check += wall_clock64() - tc;)
-    if (f == INT_MAX) {
-      top.cursor += span;
+    if (c >= cs[4]) {
+      if (--sp == 0) return true;
+      top = frame_pop(stack, sp - 1);
       continue;
     }
-    const int32_t cidx = top.cursor + f;
-    check_pos(top, cidx, &nx, &ny);
-    top.cursor = cidx + 1;
+    int d = 0;
+    int32_t cl = c;
+    while (cl >= 2 * pick4(top.dist, d)) cl -= 2 * pick4(top.dist, d++);
+    const int32_t pos = (cl >> 1) + 1, sd = cl & 1;
+    if (d & 1) {
+      nx = sd == 0 ? top.x + 1 : top.x - 1;
+      ny = top.y + dir_dy(d) * pos;
+    } else {
+      nx = top.x + dir_dx(d) * pos;
+      ny = sd == 0 ? top.y + 1 : top.y - 1;
+    }
+    top.cursor = uni(resume);
     start = true;
   }
 }
 
 template <int FMT>
-__global__ void __launch_bounds__(kThreads) k_black_resolve(PlaneRef img, BlackGeom g,
-                                                            const BlackBar* bars,
-                                                            uint8_t* scratch, int64_t sstride,
-                                                            const int32_t* active,
-                                                            SheetCtl* ctl, uint32_t* nbits,
-                                                            int64_t nbits_stride) {
+__global__ void __launch_bounds__(64) k_black_resolve(PlaneRef img, BlackGeom g,
+                                                      const BlackBar* bars, uint8_t* scratch,
+                                                      int64_t sstride, const int32_t* active,
+                                                      SheetCtl* ctl) {
   const int s = blockIdx.x;
   if (active && !active[s]) return;
-  const int w = wave_id(), lane = lane_id();
   uint8_t* scr = scratch + s * sstride;
-  const uint32_t* hsum = (const uint32_t*)scr;        // W entries
-  const uint32_t* vsum = hsum + g.W;                  // H entries
-  size_t off = (((size_t)g.W + g.H) * 4 + 255) & ~(size_t)255;
-  Frame* stack = (Frame*)(scr + off);
-  uint8_t* const base = plane_ptr(img, s);
+  if (!sheet_has_candidate(g, scr)) return;
+  const int lane = lane_id();
+  const uint64_t* cand = (const uint64_t*)(scr + black_head_off(g) + 8);
+  Frame* stack = (Frame*)(scr + black_stack_off(g));
+  const uint8_t* const base = plane_ptr(img, s);
+  const int64_t pitch = img.P.pitch;
+  const Sheet S{(const uint64_t*)(scr + black_rm_off(g)), (uint64_t*)(scr + black_rp_off(g)),
+                (const uint64_t*)(scr + black_cm_off(g)), (uint64_t*)(scr + black_cp_off(g)),
+                black_wpr(g), black_hpc(g), g.W, g.H,
+                (int32_t)(g.intensity > (1u << 30) ? (1u << 30) : g.intensity), g.mask_max < 255};
   BlackStats bstat{};
   BlackStats* bs = &bstat;
   (void)bs;
-  const Canvas<FMT> C{base, img.P.pitch, g.W, g.H, g.mask_max,
-                      bs, nbits ? nbits + s * nbits_stride : nullptr, (g.W + 31) >> 5};
   BSTAT(const uint64_t t_all = wall_clock64();)
-  uint64_t* red = tab_red();
-  int parity = 0;
-  int32_t seq = 0;  // last command number (driver) / last one seen (helpers)
-  if (threadIdx.x == 0) mailbox()[0] = 0;
-  block_sync();
   bool dirty = false;
-  for (int32_t b0 = 0; b0 < g.nbars; b0 += kThreads) {
-    // darkness of kThreads bars on the original image (darkness_rect,
-    // blit.c:131-146)
-    bool cand = false;
-    const int32_t bi = b0 + (int32_t)threadIdx.x;
-    if (bi < g.nbars) {
-      const BlackBar bb = bars[bi];
-      const Rect c = clip(bb.r, g.W, g.H);
-      uint64_t sum = 0;
-      if (c.x0 <= c.x1 && c.y0 <= c.y1) {
-        if (bb.dir == 0)
-          for (int32_t x = c.x0; x <= c.x1; x++) sum += hsum[x];
-        else
-          for (int32_t y = c.y0; y <= c.y1; y++) sum += vsum[y];
-      }
-      const uint8_t dark = (uint8_t)(0xFFull - sum / count_pixels(c));
-      cand = dark >= g.abs_threshold && !bb.excluded;
-    }
-    const unsigned long long cw = __ballot(cand);
-    if (lane == 0) tab_cand()[w] = cw;
-    block_sync();
-#pragma unroll 1
-    for (int v = 0; v < kWaves; v++) {
-      uint64_t Mv = tab_cand()[v];
-      while (Mv) {
-        const int k = __ffsll((long long)Mv) - 1;
-        Mv &= Mv - 1;
-        const BlackBar bb = bars[b0 + v * 64 + k];
-        if (dirty) {  // re-measure on the current image, every thread a share
-          BSTAT(const uint64_t tr = wall_clock64(); bs->remeasures++;)
-          const Rect c = clip(bb.r, g.W, g.H);
-          uint64_t sum = 0;
-          if (c.x0 <= c.x1 && c.y0 <= c.y1) {
-            for (int32_t x0 = c.x0; x0 <= c.x1; x0 += 64) {
-              const int32_t xx = x0 + lane;
-              if (xx > c.x1) continue;
-              for (int32_t y0 = c.y0 + w * 4; y0 <= c.y1; y0 += 4 * kWaves) {
-                uint32_t d[4];
-#pragma unroll
-                for (int r = 0; r < 4; r++)
-                  d[r] = dark_of(load_px_row<FMT>(C.base + (int64_t)imin(y0 + r, c.y1) * C.pitch, xx));
-#pragma unroll
-                for (int r = 0; r < 4; r++) sum += y0 + r <= c.y1 ? d[r] : 0u;
-              }
-            }
-          }
-          sum = wave_sum(sum);
-          if (lane == 0) red[w] = sum;
-          block_sync();
-          uint64_t tot = 0;
-#pragma unroll
-          for (int v2 = 0; v2 < kWaves; v2++) tot += red[v2];
-          block_sync();
-          const uint8_t dark = (uint8_t)(0xFFull - tot / count_pixels(c));
-          BSTAT(bs->t_remeasure += wall_clock64() - tr;)
-          if (dark < g.abs_threshold) continue;
-        }
-        // flood fill from every pixel of the bar, in scan order
-        // (filters.c:81-86): the bar's pixels row-major, a window at a time
-        const int32_t bw = bb.r.x1 - bb.r.x0 + 1;
-        const int64_t npx = (int64_t)bw * (bb.r.y1 - bb.r.y0 + 1);
-        if (bw <= 0 || npx <= 0) continue;
-        const int32_t q64 = 64 / bw, r64 = 64 % bw;  // one slice = q64 rows + r64 pixels
-        for (int64_t i0 = 0; i0 < npx;) {
-          BSTAT(const uint64_t tb = wall_clock64(); bs->bar_trips++;)
-          const int64_t i = i0 + 64 * (int64_t)(w * kGroup) + lane;
-          int32_t y = bb.r.y0 + (int32_t)(i / bw), x = bb.r.x0 + (int32_t)(i % bw);
-          int32_t qx[kGroup], qy[kGroup];
-          bool m[kGroup];
-#pragma unroll
-          for (int k2 = 0; k2 < kGroup; k2++) {
-            qx[k2] = i + 64 * k2 < npx ? x : -1;
-            qy[k2] = y;
+  for (int32_t cw = 0; cw < (g.nbars + 63) / 64; cw++) {
+    for (uint64_t cm = uni64(cand[cw]); cm; cm &= cm - 1) {
+      BlackBar bb = bars[64 * cw + ctz64(cm)];
+      bb.r = uni_rect(bb.r);
+      if (dirty) {
+        // darkness on the current image: painted pixels are white
+        BSTAT(const uint64_t tr = wall_clock64(); bs->remeasures++;)
+        const Rect c = clip(bb.r, g.W, g.H);
+        uint64_t sum = 0;
+        if (c.x0 <= c.x1 && c.y0 <= c.y1) {
+          const int32_t cwid = c.x1 - c.x0 + 1;
+          const int64_t npx = (int64_t)cwid * (c.y1 - c.y0 + 1);
+          const int32_t q64 = 64 / cwid, r64 = 64 % cwid;
+          int32_t y = c.y0 + lane / cwid, x = c.x0 + lane % cwid;
+          for (int64_t i = lane; i < npx; i += 64) {
+            const uint64_t pw = Sheet::pload(S.RP + (int64_t)y * S.wpr + (x >> 6));
+            const uint32_t v = dark_of(load_px_row<FMT>(base + (int64_t)y * pitch, x));
+            sum += ((pw >> (x & 63)) & 1) ? 255u : v;
             x += r64;
             y += q64;
-            if (x > bb.r.x1) {
-              x -= bw;
+            if (x > c.x1) {
+              x -= cwid;
               y++;
             }
           }
-          C.match_group(qx, qy, m);
-          uint64_t M[kGroup];
-#pragma unroll
-          for (int k2 = 0; k2 < kGroup; k2++) M[k2] = __ballot(m[k2]);
-          const int32_t f = window_first<false>(M, M, parity++ & 1);
-          BSTAT(bs->t_bar += wall_clock64() - tb;)
-          if (f == INT_MAX) {
-            i0 += 64 * kSlices;
-            continue;
-          }
-          const int64_t hit = i0 + f;
-          // wave 0 drives the fill, the others help on its commands
-          if (w == 0) {
-            const bool ok = flood_drive<FMT>(C, bb.r.x0 + (int32_t)(hit % bw),
-                                             bb.r.y0 + (int32_t)(hit / bw), g.intensity, stack,
-                                             g.stack_capacity, &seq, &parity, bs);
-            if (lane == 0) mailbox()[12] = ok;
-            post_command(&seq, CMD_DONE);
-          } else {
-            flood_help<FMT>(C, g.intensity, &seq, &parity, bs);
-          }
-          block_sync();  // the fill's paints, and the result, for every wave
-          if (!mailbox()[12]) {
-            if (threadIdx.x == 0 && ctl) atomicOr(&ctl[s].status, STATUS_FLOOD_OVERFLOW);
-            return;
-          }
-          dirty = true;
-          i0 = hit + 1;
+        }
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+        sum = uni64(sum);  // every lane holds the total: the decision is the wave's
+        const uint8_t dark = (uint8_t)(0xFFull - sum / count_pixels(c));
+        BSTAT(bs->t_remeasure += wall_clock64() - tr;)
+        if (dark < g.abs_threshold) continue;
+      }
+      // flood fill from every pixel of the bar in scan order (filters.c:86-89):
+      // lanes are 64-pixel segments of the bar's rows, row-major
+      const int32_t bw = bb.r.x1 - bb.r.x0 + 1, bh = bb.r.y1 - bb.r.y0 + 1;
+      if (bw <= 0 || bh <= 0) continue;
+      const int32_t nseg = (bw + 63) >> 6;
+      const int32_t total = nseg * bh;
+      int32_t cy = bb.r.y0, cx = bb.r.x0;  // next pixel to look at
+      for (;;) {
+        BSTAT(const uint64_t tb = wall_clock64(); bs->bar_trips++;)
+        cy = uni(cy);
+        cx = uni(cx);
+        const int32_t k0 = (cy - bb.r.y0) * nseg + ((cx - bb.r.x0) >> 6);
+        if (k0 >= total) break;
+        const int32_t kk = k0 + lane;
+        const int32_t ry = bb.r.y0 + kk / nseg, sx = bb.r.x0 + 64 * (kk % nseg);
+        Win w;
+        const bool on = kk < total;
+        if (on) w.issue(S, false, ry, sx);
+        uint64_t e = on ? w.bits(S) : 0;
+        const int32_t wlim = bb.r.x1 - sx + 1;  // pixels of this segment in the bar
+        if (wlim < 64) e &= (1ull << wlim) - 1;
+        if (lane == 0 && cx > sx) e &= ~0ull << (cx - sx);  // before the cursor: done
+        const uint64_t hit = __ballot(e != 0);
+        BSTAT(bs->t_bar += wall_clock64() - tb;)
+        if (!hit) {
+          const int32_t kn = k0 + 64;
+          if (kn >= total) break;
+          cy = bb.r.y0 + kn / nseg;
+          cx = bb.r.x0 + 64 * (kn % nseg);
+          continue;
+        }
+        const int hl = ctz64(hit);
+        const int32_t fx = __builtin_amdgcn_readlane(sx + (e ? ctz64(e) : 0), hl);
+        const int32_t fy = __builtin_amdgcn_readlane(ry, hl);
+        if (!flood(S, fx, fy, stack, g.stack_capacity, bs)) {
+          if (lane == 0 && ctl) atomicOr(&ctl[s].status, STATUS_FLOOD_OVERFLOW);
+          return;
+        }
+        dirty = true;
+        cy = fy;
+        cx = fx + 1;
+        if (cx > bb.r.x1) {
+          cx = bb.r.x0;
+          cy++;
         }
       }
     }
-    block_sync();  // the candidate table is rewritten by the next chunk
   }
 #ifdef UPHIP_DIAG
-  if ((g.diag & 16) && threadIdx.x == 0 && bstat.frames)
+  if ((g.diag & 16) && lane == 0 && bstat.frames)
     printf("uphip black: sheet %d frames %u fill %u (%.1f us) check %u (%.1f us) bar %u (%.1f us) "
-           "remeasure %u (%.1f us) total %.1f us lookups %u "
-           "fillA %.1f (pos %.1f lookup %.1f) B %.1f C %.1f D %.1f us local %.1f pop %.1f us\n",
+           "remeasure %u (%.1f us) total %.1f us\n",
            s, bstat.frames, bstat.fill_trips, bstat.t_fill * 0.01, bstat.check_trips,
            bstat.t_check * 0.01, bstat.bar_trips, bstat.t_bar * 0.01, bstat.remeasures,
-           bstat.t_remeasure * 0.01, (wall_clock64() - t_all) * 0.01, bstat.lookups * 64,
-           bstat.t_fa * 0.01, bstat.t_fa0 * 0.01,
-           bstat.t_fa1 * 0.01, bstat.t_fb * 0.01,
-           bstat.t_fc * 0.01, bstat.t_fd * 0.01, bstat.t_local * 0.01, bstat.t_pop * 0.01);
+           bstat.t_remeasure * 0.01, (wall_clock64() - t_all) * 0.01);
 #endif
 }
 
@@ -874,12 +796,18 @@ static void launch_black_t(const PlaneRef& img, const BlackGeom& g, const BlackB
   if (g.vregion.x1 >= g.vregion.x0 && g.vregion.y1 >= g.vregion.y0 && !vsum_ready)
     launch_axis_reduce(img, vargs, 1, M_DARKINV_SUM, g.vregion.x1 - g.vregion.x0 + 1, g.H,
                        (uint32_t*)scr + g.W, ss / 4, count, st);
+  hipLaunchKernelGGL(k_black_cand, dim3(count), dim3(kCandThreads), 0, st, g, bars, scr, ss, active);
+  hipLaunchKernelGGL(k_black_planes<FMT>, dim3((black_wpr(g) + 3) / 4, black_hpc(g), count),
+                     dim3(256), 0, st, img, g, scr, ss, active);
   BlackGeom gd = g;
   gd.diag = diag_noise();
   allow_dynamic_lds((const void*)k_black_resolve<FMT>, kStackLdsBytes);
   if (!(diag_skip() & 1))
-    hipLaunchKernelGGL(k_black_resolve<FMT>, dim3(count), dim3(kThreads), kStackLdsBytes, st, img, gd,
-                       bars, scr, ss, active, ctl, FMT == F_GRAY8 ? nbits : nullptr, nbits_stride);
+    hipLaunchKernelGGL(k_black_resolve<FMT>, dim3(count), dim3(64), kStackLdsBytes, st, img, gd,
+                       bars, scr, ss, active, ctl);
+  hipLaunchKernelGGL(k_black_paint<FMT>, dim3((black_wpr(g) + 63) / 64, (g.H + 3) / 4, count),
+                     dim3(256), 0, st, img, g, scr, ss, active, FMT == F_GRAY8 ? nbits : nullptr,
+                     nbits_stride);
 }
 
 __global__ void k_black_prep(uint8_t* scr, int64_t ss, int32_t words, int count) {
@@ -899,16 +827,16 @@ void launch_blackfilter_impl(const PlaneRef& img, const BlackGeom& g, const Blac
   hipLaunchKernelGGL(k_black_prep, dim3(8, count), dim3(256), 0, st, scr, ss, g.W, count);
   switch (img.P.fmt) {
     case F_GRAY8:
-      launch_black_t<F_GRAY8>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs, vsum_ready,
-                         nbits, nbits_stride);
+      launch_black_t<F_GRAY8>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs,
+                              vsum_ready, nbits, nbits_stride);
       break;
     case F_Y400A:
-      launch_black_t<F_Y400A>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs, vsum_ready,
-                         nbits, nbits_stride);
+      launch_black_t<F_Y400A>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs,
+                              vsum_ready, nbits, nbits_stride);
       break;
     default:
-      launch_black_t<F_RGB24>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs, vsum_ready,
-                         nbits, nbits_stride);
+      launch_black_t<F_RGB24>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs,
+                              vsum_ready, nbits, nbits_stride);
       break;
   }
 }
