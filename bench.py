@@ -248,6 +248,16 @@ def valu_frac_of(path, kernel, units, avg_ms):
     return round(k["valu_insts_per_sheet"] * units * 4 / (1024 * k["clock_ghz"] * 1e9 * avg_ms * 1e-3), 4)
 
 
+def c4_traffic(path):
+    """HBM bytes per sheet of the C4 rotate (FETCH_SIZE x2 + WRITE_SIZE,
+    tools/traffic_c4.sh), the same unit as its alg_bytes_per_launch."""
+    try:
+        with open(path) as f:
+            return json.load(f).get("c4", {}).get("hbm_bytes_per_sheet")
+    except (OSError, ValueError):
+        return None
+
+
 def traffic_of(path, key, units):
     try:
         with open(path) as f:
@@ -472,7 +482,7 @@ def run_c4(args, L, d, devices, firsts, n_gpus, version, valid, nsheets=0, steps
             "roofline": {"bound": "hbm", "kernel": ROOFLINE_KERNEL["c4"],
                          "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
-                         "traffic": None, "avg_launch_ms": round(rot_ms, 3),
+                         "traffic": c4_traffic(args.traffic), "avg_launch_ms": round(rot_ms, 3),
                          "launch_ms_from": "3 single-sheet runs, idle GPU (the deskew_rotate "
                                            "stage: the two-mask launch + the launch for sheets "
                                            "whose mask 1 depends on deskew 0)",
