@@ -93,8 +93,12 @@ bool launch_move_rect_fused(const PlaneRef& src, const PlaneRef& dst, const Move
                             const MoveExtra& x, int count, hipStream_t st);
 // max_abs_angle bounds |rotation| of every active sheet (sizes the staged
 // source window; tiles whose window does not fit take a slower exact path).
-void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
-                        int interp, int count, hipStream_t st, float max_abs_angle);
+// colsum (optional, zeroed by the caller for the rotated sheets): the
+// output's column sums over all rows added into colsum[s * cs_stride + x];
+// returns whether they were (GRAY8 cubic, staged window only).
+bool launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
+                        int interp, int count, hipStream_t st, float max_abs_angle,
+                        uint32_t* colsum = nullptr, int64_t cs_stride = 0);
 // Bilinear rotation (kernels_rotlin.hip), GRAY8 and RGB24: up to two masks
 // per sheet, args[m * mstride + s]; mask m >= 1 only where indep[s] (or
 // indep == null).  Sheets with no active mask are left alone (not flipped).

@@ -87,8 +87,10 @@ bool black_geometry(int32_t W, int32_t H, const UphipBlackfilterParameters& p, u
 // ---------------------------------------------------------------------------
 // Per-sheet scratch: [hsum: W | vsum: H] u32, the head (u32 "some bar is a
 // candidate" flag, then the candidate bits of the bars from byte 8), the
-// planes RM, RP (H rows of wpr words: x = 64w + bit) and CM, CP (W columns of
-// hpc words: y = 64w + bit), the DFS stack frames.
+// planes RM, RP (H rows of wpr words: x = 64w + bit, word w of row y at
+// y * wpr + w) and CM, CP (W columns of hpc words: y = 64w + bit, word w of
+// column x at w * W + x, so that neighbouring columns' words are adjacent),
+// the DFS stack frames.
 UPH_HD int32_t black_wpr(const BlackGeom& g) { return (g.W + 63) >> 6; }
 UPH_HD int32_t black_hpc(const BlackGeom& g) { return (g.H + 63) >> 6; }
 UPH_HD size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -150,9 +152,10 @@ __device__ __forceinline__ bool sheet_has_candidate(const BlackGeom& g, const ui
   return *(const int32_t*)(scr + black_head_off(g)) != 0;
 }
 
-// The planes of the candidate sheets: one wave per 64x64 tile; lane t makes
-// the row word of row y0+t (M from the image, P clear), then 64 ballots
-// transpose the tile into its 64 column words.
+// The planes of the candidate sheets, a block per 256x64 pixels: thread t
+// makes row word t & 3 of row t >> 2 (M from the image, P clear; a row's
+// four words from 256 contiguous bytes), then the column word of column t
+// from the 64 row words in LDS.  Both planes are written in whole lines.
 template <int FMT>
 __global__ void __launch_bounds__(256) k_black_planes(PlaneRef img, BlackGeom g, uint8_t* scratch,
                                                       int64_t sstride, const int32_t* active) {
@@ -160,22 +163,21 @@ __global__ void __launch_bounds__(256) k_black_planes(PlaneRef img, BlackGeom g,
   if (active && !active[s]) return;
   uint8_t* scr = scratch + s * sstride;
   if (!sheet_has_candidate(g, scr)) return;
-  const int32_t wpr = black_wpr(g), hpc = black_hpc(g);
-  const int lane = threadIdx.x & 63;
-  const int32_t xw = blockIdx.x * 4 + (threadIdx.x >> 6), yw = blockIdx.y;
-  if (xw >= wpr) return;  // whole wave
-  const int32_t x0 = 64 * xw, y = 64 * yw + lane;
+  __shared__ uint64_t rw[64][4];
+  const int32_t wpr = black_wpr(g);
+  const int t = threadIdx.x, r = t >> 2, q = t & 3;
+  const int32_t xw = 4 * blockIdx.x + q, y = 64 * blockIdx.y + r, x0 = 64 * xw;
   uint64_t m = 0;
-  if (y < g.H) {
+  if (y < g.H && xw < wpr) {
     const uint8_t* row = plane_ptr(img, s) + (int64_t)y * img.P.pitch;
     if (FMT == F_GRAY8 && x0 + 64 <= g.W && ((uintptr_t)(row + x0) & 15) == 0) {
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const uint4 v = *(const uint4*)(row + x0 + 16 * q);
+      for (int k = 0; k < 4; k++) {
+        const uint4 v = *(const uint4*)(row + x0 + 16 * k);
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int c = 0; c < 16; c++)
-          m |= (uint64_t)(((w4[c >> 2] >> (8 * (c & 3))) & 0xFFu) <= g.mask_max) << (16 * q + c);
+          m |= (uint64_t)(((w4[c >> 2] >> (8 * (c & 3))) & 0xFFu) <= g.mask_max) << (16 * k + c);
       }
     } else {
       for (int c = 0; c < 64 && x0 + c < g.W; c++)
@@ -185,14 +187,17 @@ __global__ void __launch_bounds__(256) k_black_planes(PlaneRef img, BlackGeom g,
     ((uint64_t*)(scr + black_rm_off(g)))[i] = m;
     ((uint64_t*)(scr + black_rp_off(g)))[i] = 0;
   }
-  // column x0 + c: bit t = row y0 + t's bit c
+  rw[r][q] = m;
+  __syncthreads();
+  // column x: bit k = row 64 blockIdx.y + k's bit x & 63 (a wave reads one
+  // word of each row: LDS broadcasts)
+  const int32_t x = 256 * blockIdx.x + t;
+  const int qc = t >> 6, c = t & 63;
   uint64_t col = 0;
-  for (int c = 0; c < 64; c++) {
-    const uint64_t b = __ballot((m >> c) & 1);
-    if (c == lane) col = b;
-  }
-  if (x0 + lane < g.W) {
-    const int64_t i = (int64_t)(x0 + lane) * hpc + yw;
+#pragma unroll 16
+  for (int k = 0; k < 64; k++) col |= ((rw[k][qc] >> c) & 1ull) << k;
+  if (x < g.W) {
+    const int64_t i = (int64_t)blockIdx.y * g.W + x;
     ((uint64_t*)(scr + black_cm_off(g)))[i] = col;
     ((uint64_t*)(scr + black_cp_off(g)))[i] = 0;
   }
@@ -366,8 +371,11 @@ struct Win {
     ok0 = lok && w0 >= 0 && w0 < nw;
     ok1 = lok && w0 + 1 >= 0 && w0 + 1 < nw;
     sh = s & 63;
-    const int64_t b = (int64_t)(lok ? ln : 0) * nw;
-    const int64_t i0 = b + (ok0 ? w0 : 0), i1 = b + (ok1 ? w0 + 1 : 0);
+    // row planes: word w of row ln at ln * wpr + w; column planes: word w of
+    // column ln at w * W + ln
+    const int32_t l = lok ? ln : 0, wa = ok0 ? w0 : 0, wb = ok1 ? w0 + 1 : 0;
+    const int64_t i0 = col ? (int64_t)wa * W + l : (int64_t)l * wpr + wa;
+    const int64_t i1 = col ? (int64_t)wb * W + l : (int64_t)l * wpr + wb;
     m0 = M[i0];
     m1 = M[i1];
     p0 = Sheet::pload(P + i0);
@@ -431,7 +439,7 @@ __device__ __forceinline__ void paint_cross(const Sheet& S, int32_t px, int32_t 
   const int32_t nrw = (xb >> 6) - (xa >> 6) + 1, nown = nrw + (yb >> 6) - (ya >> 6) + 1;
   const int32_t nrx = dist[0] + dist[2], ncross = nrx + dist[1] + dist[3];
   uint64_t *RP = S.RP, *CP = S.CP;
-  const int32_t wpr = S.wpr, hpc = S.hpc;
+  const int32_t wpr = S.wpr, W = S.W;
   for (int32_t i0 = 0; i0 < imax(nown, ncross); i0 += 64) {
     const int32_t i = i0 + lane;
     if (i < nown) {
@@ -439,12 +447,12 @@ __device__ __forceinline__ void paint_cross(const Sheet& S, int32_t px, int32_t 
       const int32_t lo = row ? xa : ya, hi = row ? xb : yb;
       const int32_t w = (lo >> 6) + (row ? i : i - nrw);
       const int a = imax(lo - 64 * w, 0), b = imin(hi - 64 * w, 63);
-      Sheet::por(row ? RP + (int64_t)py * wpr + w : CP + (int64_t)px * hpc + w,
+      Sheet::por(row ? RP + (int64_t)py * wpr + w : CP + (int64_t)w * W + px,
                  (~0ull >> (63 - b)) & (~0ull << a));
     }
     if (i < nrx) {
       const int32_t x = i < dist[0] ? px - 1 - i : px + 1 + (i - dist[0]);
-      Sheet::por(CP + (int64_t)x * hpc + (py >> 6), 1ull << (py & 63));
+      Sheet::por(CP + (int64_t)(py >> 6) * W + x, 1ull << (py & 63));
     } else if (i < ncross) {
       const int32_t j = i - nrx;
       const int32_t y = j < dist[1] ? py - 1 - j : py + 1 + (j - dist[1]);

@@ -1532,11 +1532,17 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
                                                                int max_rows, int cls_rows,
                                                                int diag,
                                                                uint32_t m_gxy, uint32_t m_gx,
-                                                               int loop_count, int tgx, int tgy) {
+                                                               int loop_count, int tgx, int tgy,
+                                                               uint32_t* colsum, int64_t cs_stride) {
   // dynamic LDS: window [max_rows][kRFS] floats, nw[max_rows] u64, then one
   // (kRFH / 8) x kRFW byte output buffer per wave
   extern __shared__ __attribute__((aligned(16))) float winf[];
   __shared__ int32_t win_s[4];
+  // colsum (optional): the output's column sums over all rows, added into
+  // colsum[s * cs_stride + x] (the next mask scan's, masks.c:54-209), so that
+  // scan need not read the rotated plane again; per tile summed in LDS, then
+  // one atomic per column
+  __shared__ uint32_t csum_s[kRFW];
   // one tile (txi, tyi) of sheet s; every return is block-uniform
   auto tile = [&](int txi, int tyi, int s) {
   // the plane selectors and the arguments are loaded together (one round trip)
@@ -1560,17 +1566,42 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
   const int32_t v0 = imax(ty0, 0) - a.mask.y0, v1 = imin(ty0 + kRFH, P.H) - 1 - a.mask.y0;
   const int32_t cu0 = imax(u0, 0), cu1 = imin(u1, sw - 1);
   const int32_t cv0 = imax(v0, 0), cv1 = imin(v1, sh - 1);
+  // the tile's column sums (colsum): zeroed here, added per row below
+  auto csum_flush = [&]() {
+    __syncthreads();
+    if (threadIdx.x < kRFW && tx0 + (int)threadIdx.x < P.W)
+      atomicAdd(colsum + s * cs_stride + tx0 + threadIdx.x, csum_s[threadIdx.x]);
+  };
+  if (colsum) {
+    if (threadIdx.x < kRFW) csum_s[threadIdx.x] = 0;
+    __syncthreads();
+  }
   if (!(cu0 <= cu1 && cv0 <= cv1)) {
     // no pixel of the tile inside the mask: copied unchanged (deskew.c:268-286)
     const int cb = 8 * (threadIdx.x & 15);
     const int32_t x = tx0 + cb;
+    uint32_t cs8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int r = threadIdx.x >> 4; r < kRFH; r += kRFT / 16) {
       const int32_t y = ty0 + r;
       if (y >= P.H || x >= P.W) continue;
       const uint8_t* sp = sbase + row_off(y, P.pitch) + x;
       uint8_t* dp = dbase + row_off(y, P.pitch) + x;
-      if (x + 8 <= P.W) *reinterpret_cast<uint64_t*>(dp) = *reinterpret_cast<const uint64_t*>(sp);
-      else for (int j = 0; x + j < P.W; j++) dp[j] = sp[j];
+      if (x + 8 <= P.W) {
+        const uint64_t q = *reinterpret_cast<const uint64_t*>(sp);
+        *reinterpret_cast<uint64_t*>(dp) = q;
+#pragma unroll
+        for (int j = 0; j < 8; j++) cs8[j] += (uint32_t)(q >> (8 * j)) & 0xFFu;
+      } else {
+        for (int j = 0; x + j < P.W; j++) {
+          dp[j] = sp[j];
+          cs8[j & 7] += sp[j];
+        }
+      }
+    }
+    if (colsum) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) atomicAdd(&csum_s[cb + j], cs8[j]);
+      csum_flush();
     }
     return;
   }
@@ -1850,6 +1881,19 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
       }
     }
   }
+  if (colsum) {
+    // this wave's rows of columns lane and 64 + lane, then the tile's
+    uint32_t sA = 0, sB = 0;
+#pragma unroll
+    for (int k = 0; k < kRows; k++) {
+      if (yw + k >= P.H) break;
+      sA += obuf[k * kRFW + lane];
+      sB += obuf[k * kRFW + 64 + lane];
+    }
+    atomicAdd(&csum_s[lane], sA);
+    atomicAdd(&csum_s[64 + lane], sB);
+    csum_flush();
+  }
   };
   if constexpr (!LOOP) {  // one tile per block, XCD-aware order
     int txi, tyi, s;
@@ -1889,8 +1933,9 @@ static int rotate_window_rows(float max_abs_angle) {
   return kRFH + (int)ceilf((kRFW - 1) * sinf(a)) + 5;
 }
 
-void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
-                        int interp, int count, hipStream_t st, float max_abs_angle) {
+bool launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateArgs* args,
+                        int interp, int count, hipStream_t st, float max_abs_angle,
+                        uint32_t* colsum, int64_t cs_stride) {
   const dim3 grid((src.P.W + kRotTW - 1) / kRotTW, (src.P.H + kRotTH - 1) / kRotTH, count);
   const dim3 ggrid((src.P.W + kRotTW - 1) / kRotTW, (src.P.H + kRotGH - 1) / kRotGH, count);
   if (interp == UPHIP_INTERP_CUBIC && src.P.fmt == F_GRAY8) {
@@ -1899,8 +1944,9 @@ void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateAr
       return (sizeof(float) * kRFS + sizeof(uint64_t)) * (size_t)r + kRFH * kRFW;
     };
     // the most window rows that still let four tiles (32 waves) share a CU's
-    // 160 KB of LDS (16 B of static LDS per tile); windows of up to ~2.4 deg
-    const int rows4 = (int)((40 * 1024 - 16 - kRFH * kRFW) / (sizeof(float) * kRFS + sizeof(uint64_t)));
+    // 160 KB of LDS (16 + 512 B of static LDS per tile); windows of up to ~2.4 deg
+    const int rows4 = (int)((40 * 1024 - 16 - 4 * kRFW - kRFH * kRFW) /
+                            (sizeof(float) * kRFS + sizeof(uint64_t)));
     if (lds_of(rows) <= 56 * 1024 && src.P.pitch * (int64_t)src.P.H < (1ll << 31) &&
         !(diag_double() & 256)) {
       const dim3 fgrid((src.P.W + kRFW - 1) / kRFW, (src.P.H + kRFH - 1) / kRFH, count);
@@ -1913,22 +1959,23 @@ void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateAr
         // (the second as a persistent grid: when no sheet needs the large
         // window its blocks only read the arguments)
         UPH_LAUNCH_DIAG(2, k_rotate_cubic_g8f<false>, fgrid, dim3(kRFT), lds_of(rows4), st, src, dst, args,
-                        rows4, rows4, dd, mgxy, mgx, 0, 0, 0);
+                        rows4, rows4, dd, mgxy, mgx, 0, 0, 0, colsum, cs_stride);
         UPH_LAUNCH_DIAG(2, k_rotate_cubic_g8f<true>, dim3(3 * 256), dim3(kRFT), lds_of(rows), st, src, dst,
-                        args, rows, -rows4, dd, 0u, 0u, count, (int)fgrid.x, (int)fgrid.y);
+                        args, rows, -rows4, dd, 0u, 0u, count, (int)fgrid.x, (int)fgrid.y, colsum,
+                        cs_stride);
       } else {
         UPH_LAUNCH_DIAG(2, k_rotate_cubic_g8f<false>, fgrid, dim3(kRFT), lds_of(rows), st, src, dst, args,
-                        rows, 0, dd, mgxy, mgx, 0, 0, 0);
+                        rows, 0, dd, mgxy, mgx, 0, 0, 0, colsum, cs_stride);
       }
-      return;
+      return colsum != nullptr;
     }
     const dim3 qgrid((src.P.W + kRQW - 1) / kRQW, (src.P.H + kRQH - 1) / kRQH, count);
     UPH_LAUNCH_DIAG(2, k_rotate_cubic_g8, qgrid, dim3(kThreads), 0, st, src, dst, args);
-    return;
+    return false;
   }
   if (interp == UPHIP_INTERP_CUBIC && src.P.fmt == F_Y400A) {
     hipLaunchKernelGGL(k_rotate_cubic_gray<F_Y400A>, ggrid, dim3(kThreads), 0, st, src, dst, args);
-    return;
+    return false;
   }
   if (src.P.fmt == F_GRAY8)
     hipLaunchKernelGGL(k_rotate_mask<F_GRAY8>, grid, dim3(kThreads), 0, st, src, dst, args,
@@ -1939,6 +1986,7 @@ void launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateAr
   else
     hipLaunchKernelGGL(k_rotate_mask<F_RGB24>, grid, dim3(kThreads), 0, st, src, dst, args,
                        interp);
+  return false;
 }
 
 __global__ void k_flip_if_active(SheetCtl* ctl, const int32_t* active, int64_t stride_ints,

@@ -191,6 +191,16 @@ __global__ void k_rot_independent(const SheetCtl* ctl, const RotateArgs* args, i
 }
 
 // flip every sheet the two-mask launch rotated
+// Zero the first n column sums of the sheets whose rotation is active (the
+// rotate kernel accumulates theirs; the others keep the previous scan's).
+__global__ void k_zero_sums_if_active(const RotateArgs* args, uint32_t* sums, int64_t stride,
+                                      int32_t n) {
+  const int s = blockIdx.y;
+  if (!args[s].active) return;
+  for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    sums[s * stride + i] = 0;
+}
+
 __global__ void k_flip_rot2(SheetCtl* ctl, const RotateArgs* args, int64_t mstride,
                             const int32_t* indep, int count) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -878,15 +888,28 @@ static void resize_all(UphipBatch* b, int32_t& w, int32_t& h, int32_t pw, int32_
 // grayfilter leaves; with one point, a horizontal-only scan over every row
 // and a gray plane, its column sums come out of the grayfilter's cell pass
 // (plus its wipes' changes) instead of a pass of their own.
-static bool mask_sums_from_gray(const UphipBatch* b) {
-  const UphipOptions& o = b->o;
+// One point, a horizontal-only scan over every row, a gray plane: the scan's
+// sums are plain column sums of the whole image.
+static bool mask_scan_all_rows(const UphipBatch* b) {
   const UphipMaskDetectionParameters& p = b->mask_params;
-  if (o.disable & (UPHIP_NO_DESKEW | UPHIP_NO_MASK_SCAN | UPHIP_NO_GRAYFILTER)) return false;
   if (b->points.size() != 1 || !p.scan_direction.horizontal || p.scan_direction.vertical) return false;
   if (b->work_fmt != F_GRAY8) return false;
   const int32_t depth = p.scan_depth.horizontal == -1 ? b->H : p.scan_depth.horizontal;
   const int32_t c0 = b->points[0].y - depth / 2, c1 = c0 + depth - 1;
   return c0 <= 0 && c1 >= b->H - 1;
+}
+static bool mask_sums_from_gray(const UphipBatch* b) {
+  const UphipOptions& o = b->o;
+  if (o.disable & (UPHIP_NO_DESKEW | UPHIP_NO_MASK_SCAN | UPHIP_NO_GRAYFILTER)) return false;
+  return mask_scan_all_rows(b);
+}
+// The second mask scan (sheet_stages.c:415-421) runs on the deskewed image:
+// its column sums are the rotate kernel's output sums for the rotated sheets
+// and, for the others (unchanged since), the first scan's, still in b->sums.
+static bool mask_sums_from_rotate(const UphipBatch* b) {
+  const UphipOptions& o = b->o;
+  if (o.disable & (UPHIP_NO_DESKEW | UPHIP_NO_MASK_SCAN | UPHIP_NO_MASK_CENTER)) return false;
+  return mask_scan_all_rows(b);
 }
 
 // detect_masks on every sheet -> ctl.masks / ctl.mask_count (masks.c:54-209).
@@ -1204,6 +1227,7 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
     mark(b, "blurfilter");
   }
   bool mask_sums_ready = false;
+  bool center_sums_ready = false;  // the second scan's sums came with the rotation
   // ---- masks (sheet_stages.c:359-386): the first detection is dead for a
   // fresh job (its count is discarded and its masks are overwritten before
   // any read), so it is skipped; mask_count is 0 -> no apply_masks.
@@ -1273,11 +1297,14 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
     const bool linear = o.interpolate_type == UPHIP_INTERP_LINEAR &&
                         (P.fmt == F_GRAY8 || P.fmt == F_RGB24);
     // rotations are angles of the scan table, |angle| <= scan range
-    auto rotate = [&](const RotateArgs* args, int nmask, const int32_t* indep) {
-      if (!(linear && launch_rotate_linear(cur_ref(P, b->ctl), other_ref(P, b->ctl), args, nmask,
-                                           b->cap, indep, count, b->st, b->max_angle)))
-        launch_rotate_mask(cur_ref(P, b->ctl), other_ref(P, b->ctl), args, o.interpolate_type,
-                           count, b->st, b->max_angle);
+    auto rotate = [&](const RotateArgs* args, int nmask, const int32_t* indep,
+                      uint32_t* colsum = nullptr) {
+      if (linear && launch_rotate_linear(cur_ref(P, b->ctl), other_ref(P, b->ctl), args, nmask,
+                                         b->cap, indep, count, b->st, b->max_angle))
+        return false;
+      return launch_rotate_mask(cur_ref(P, b->ctl), other_ref(P, b->ctl), args,
+                                o.interpolate_type, count, b->st, b->max_angle, colsum,
+                                b->sums_stride);
     };
     if (linear && b->points.size() == 2) {
       // both masks detected on the same image, rotated in one launch where
@@ -1300,9 +1327,13 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
     } else {
       for (size_t i = 0; i < b->points.size(); i++) {
         detect((int)i, nullptr);
-        mark(b, "deskew_detect");
         RotateArgs* ai = b->rot_args + (int64_t)i * b->cap;
-        rotate(ai, 1, nullptr);
+        const bool fuse = mask_sums_from_rotate(b);
+        if (fuse)
+          hipLaunchKernelGGL(k_zero_sums_if_active, dim3(4, count), dim3(256), 0, b->st, ai,
+                             b->sums, b->sums_stride, b->W);
+        mark(b, "deskew_detect");
+        center_sums_ready = rotate(ai, 1, nullptr, fuse ? b->sums : nullptr);
         mark(b, "deskew_rotate");  // brackets exactly the rotation kernel
         launch_flip_if_active(b->ctl, &ai->active, sizeof(RotateArgs), count, b->st);
       }
@@ -1312,7 +1343,7 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
   const bool rows_fused = border_rows_from_center(b);
   if (!(dis & UPHIP_NO_MASK_CENTER)) {
     if (!(dis & UPHIP_NO_MASK_SCAN)) {
-      detect_masks_all(b, 1, count);
+      detect_masks_all(b, 1, count, center_sums_ready);
       mark(b, "masks_center");
     }
     for (size_t i = 0; i < b->points.size(); i++) {
