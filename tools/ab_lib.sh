@@ -10,7 +10,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 for rep in $(seq "$reps"); do
   for v in old new; do
     cp ab/$v.so unpaper-gpu_amd/lib/libunpaper_hip.so
-    timeout -k 10 200 python3 bench.py --no-cpu --no-host-io --no-latency --no-verify --probe 0 --steps 6 > gpurun_out/ab_$v.json 2>&1 || exit 1
+    timeout -k 10 200 python3 bench.py --no-cpu --no-host-io --no-latency --no-verify --probe 0 --no-c4 --steps 6 > gpurun_out/ab_$v.json 2>&1 || exit 1
     python3 -c "import json; d=json.loads(open('gpurun_out/ab_$v.json').read().strip().splitlines()[-1]); print('$v', d['value'])"
   done
 done

@@ -268,8 +268,8 @@ __device__ __forceinline__ uint64_t lane_range(int lo, int n) {
   return (n >= 64 ? ~0ull : ((1ull << n) - 1)) << lo;
 }
 
-constexpr int kStackLds = 3072;  // the lowest frames of the DFS stack live in LDS
-constexpr size_t kStackLdsBytes = (size_t)kStackLds * 32;  // 96 KiB
+constexpr int kStackLds = 1024;  // the lowest frames of the DFS stack live in LDS
+constexpr size_t kStackLdsBytes = (size_t)kStackLds * 32;  // 32 KiB: deeper frames go to HBM
 
 struct Frame {
   int32_t x, y;
