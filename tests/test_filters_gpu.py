@@ -232,6 +232,77 @@ def test_blackfilter_irregular(hip, oracle, intensity, size):
     both(hip, oracle, h, lambda d: hip.blackfilter(d, p), lambda o: oracle.blackfilter(o, p))
 
 
+def as_format(g, fmt, rng, thr=None):
+    """A gray array in `fmt`: RGB24 channels tinted apart (as the C4 pages),
+    Y400A with a random alpha."""
+    kw = {} if thr is None else {"abs_black_threshold": thr}
+    if fmt == A.FMT_RGB24:
+        t = rng.integers(0, 9, size=3)
+        rgb = np.stack([np.maximum(g.astype(int) - int(t[c]), 0) for c in range(3)], axis=2)
+        return HostImage.from_array(rgb.astype(np.uint8), fmt, **kw)
+    if fmt == A.FMT_Y400A:
+        a = rng.integers(0, 256, size=g.shape, dtype=np.uint8)
+        return HostImage.from_array(np.stack([g, a], axis=2), fmt, **kw)
+    return HostImage.from_array(g, fmt, **kw)
+
+
+def speck_page(w, h, density, seed, band=(5, 25)):
+    """A dark band for the bars to find, and dark specks a fill line can
+    reach through up to intensity-1 light pixels: the pattern of the heavy
+    C4 sheets, where one fill percolates through the page's salt specks."""
+    rng = np.random.default_rng(seed)
+    g = np.full((h, w), 255, np.uint8)
+    g[:, band[0]:band[1]] = rng.integers(0, 12, size=(h, band[1] - band[0]))
+    m = rng.random((h, w)) < density
+    g[m] = rng.integers(0, 60, size=int(m.sum()))
+    return g, rng
+
+
+@pytest.mark.parametrize("fmt", [A.FMT_GRAY8, A.FMT_RGB24, A.FMT_Y400A])
+@pytest.mark.parametrize("density,intensity", [(0.08, 20), (0.2, 6), (0.1, 30)])  # 383, 687, 3818 frames
+def test_blackfilter_percolation(hip, oracle, fmt, density, intensity):
+    # thousands of short frames, most with several matching neighbours: the
+    # replay's resume-past-the-windows rule and its stack run every path
+    g, rng = speck_page(400, 300, density, seed=int(density * 1000) + intensity)
+    h = as_format(g, fmt, rng)
+    p = black_params(oracle, intensity=intensity, depth=(100, 100))
+    both(hip, oracle, h, lambda d: hip.blackfilter(d, p), lambda o: oracle.blackfilter(o, p))
+
+
+@pytest.mark.parametrize("intensity", [0, 63, 64, 65, 1000])
+def test_blackfilter_intensity_edges(hip, oracle, intensity):
+    # 0: the counter is 0 after the first position whatever it holds (every
+    # line empty); 63 / 64 / 65: the window's run test switches from the
+    # in-window smear to the cross-window carry; 1000: lines run to the edge
+    g, rng = speck_page(300, 200, 0.05, seed=intensity)
+    h = as_format(g, A.FMT_GRAY8, rng)
+    p = black_params(oracle, intensity=intensity, depth=(100, 100))
+    both(hip, oracle, h, lambda d: hip.blackfilter(d, p), lambda o: oracle.blackfilter(o, p))
+
+
+@pytest.mark.parametrize("fmt", [A.FMT_GRAY8, A.FMT_RGB24])
+def test_blackfilter_long_lines(hip, oracle, fmt):
+    # fill lines over 1024 positions (several round trips a line) and
+    # neighbour runs over 512 (several check windows), in both directions
+    g, rng = speck_page(2600, 1300, 0.01, seed=7, band=(0, 30))
+    g[600:606, :] = rng.integers(0, 20, size=(6, 2600))   # a row band across the page
+    g[:, 1800:1804] = rng.integers(0, 20, size=(1300, 4))  # a column band down it
+    h = as_format(g, fmt, rng)
+    p = black_params(oracle, intensity=20, depth=(200, 200))
+    both(hip, oracle, h, lambda d: hip.blackfilter(d, p), lambda o: oracle.blackfilter(o, p))
+
+
+@pytest.mark.parametrize("thr", [0, 30, 254])
+def test_blackfilter_mask_max(hip, oracle, thr):
+    # the image's abs_black_threshold is the fill's match bound (fill.c:85):
+    # 0 matches only black, 254 everything but white
+    g, rng = speck_page(300, 200, 0.05, seed=thr + 1)
+    g[rng.random(g.shape) < 0.3] = rng.integers(0, 255)
+    h = as_format(g, A.FMT_GRAY8, rng, thr=thr)
+    p = black_params(oracle, intensity=8, depth=(100, 100), thr=200)
+    both(hip, oracle, h, lambda d: hip.blackfilter(d, p), lambda o: oracle.blackfilter(o, p))
+
+
 # ---------------------------------------------------------- rotation detection
 def skewed_edge(w, h, radians, fmt=A.FMT_GRAY8):  # cuda_deskew_test.c:18-33
     cx = np.float32(w) * np.float32(0.35)
