@@ -866,44 +866,55 @@ void launch_decode_gray(const uint8_t* src, int64_t spitch, int64_t sstride, con
 struct SmallVerdict {
   bool seq, clear;
 };
-__device__ __forceinline__ SmallVerdict small_verdict(const uint32_t (*drow)[4],
-                                                      const uint32_t (*trow)[4],
-                                                      const uint32_t (*srow)[4], int rx, int ry,
-                                                      int32_t gx, int32_t gy, bool trig, int N) {
-  SmallVerdict v{false, false};
-  uint32_t comp[9];
-  flood9(drow, rx, ry, comp);
-  // component pixels (<= 4) relative to (rx, ry), and their bounding box
-  int cxs[4], cys[4], nc = 0;
-  int bx0 = 9, bx1 = -1, by0 = 9, by1 = -1;
+// A small component (<= 4 pixels) as offsets from one of its pixels, packed
+// one byte a pixel (dx + 4 | (dy + 4) << 4, 0xFF = none): the restricted
+// flood's result, kept from the candidate pass for the verdict pass.
+constexpr uint32_t kNotSmall = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t pack_comp(const uint32_t (&comp)[9]) {
+  uint32_t rec = kNotSmall;
+  int nc = 0;
 #pragma unroll
   for (int r = 0; r < 9; r++) {
     uint32_t mm = comp[r];
-    if (mm) {
-      by0 = imin(by0, r);
-      by1 = r;
-      bx0 = imin(bx0, __ffs(mm) - 1);
-      bx1 = imax(bx1, 31 - __clz(mm));
-    }
     while (mm) {
       const int b = __ffs(mm) - 1;
       mm &= mm - 1;
-      if (nc < 4) {
-        cxs[nc] = b - 4;
-        cys[nc] = r - 4;
-      }
+      if (nc < 4) rec = (rec & ~(0xFFu << (8 * nc))) | ((uint32_t)(b | (r << 4)) << (8 * nc));
       nc++;
     }
   }
-  bool eligible = nc <= 4 && gx - 4 + bx0 >= kEligible && gy - 4 + by0 >= kEligible;
+  return nc <= 4 ? rec : kNotSmall;
+}
+// The verdict from the component's pixels (offsets cxs, cys from (rx, ry)).
+__device__ __forceinline__ SmallVerdict small_verdict_pixels(const uint32_t (*drow)[4],
+                                                             const uint32_t (*trow)[4],
+                                                             const uint32_t (*srow)[4], int rx,
+                                                             int ry, int32_t gx, int32_t gy,
+                                                             bool trig, int N, int nc,
+                                                             const int (&cxs)[4],
+                                                             const int (&cys)[4]) {
+  SmallVerdict v{false, false};
+  int bx0 = 4, bx1 = -4, by0 = 4, by1 = -4;  // bounding box, offsets from (rx, ry)
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if (k < nc) {
+      bx0 = imin(bx0, cxs[k]);
+      bx1 = imax(bx1, cxs[k]);
+      by0 = imin(by0, cys[k]);
+      by1 = imax(by1, cys[k]);
+    }
+  bool eligible = nc <= 4 && gx + bx0 >= kEligible && gy + by0 >= kEligible;
   // no foreign small pixel within Chebyshev 7 of the component: checked on
   // the bounding box dilated by 7 (a superset, so a component rejected here
-  // merely takes the exact sequential path)
+  // merely takes the exact sequential path).  At most 4 + 14 rows: a fixed,
+  // unrolled count, so the row reads are in flight together.
   if (eligible) {
-    const int X0 = rx - 4 + bx0 - 7, n = bx1 - bx0 + 15;
+    const int X0 = rx + bx0 - 7, n = bx1 - bx0 + 15;
+    const int r0 = ry + by0 - 7, r1 = ry + by1 + 7;
     int cnt = 0;
-    for (int r = ry - 4 + by0 - 7; r <= ry - 4 + by1 + 7; r++)
-      cnt += __popc(row_bits(srow[r], X0, n));
+#pragma unroll
+    for (int j = 0; j < 18; j++)
+      if (r0 + j <= r1) cnt += __popc(row_bits(srow[r0 + j], X0, n));
     eligible = cnt == nc;
   }
   if (!eligible) {
@@ -912,25 +923,59 @@ __device__ __forceinline__ SmallVerdict small_verdict(const uint32_t (*drow)[4],
   }
   // cleared iff some trigger of the component passes the ring test on the
   // original image (eligible pixels are >= 40 from the edges, so the
-  // reference's unsigned ring-loop skips never apply)
+  // reference's unsigned ring-loop skips never apply).  Rings up to N <= 4
+  // (larger intensities take the sequential path): the pixel's 9x9 dark
+  // window read once, every ring's count from it in registers.
   for (int k = 0; k < nc && k < 4 && !v.clear; k++) {
-    const int cx = rx + cxs[k], cy = ry + cys[k];
+    const int cx = rx + (k == 0 ? cxs[0] : k == 1 ? cxs[1] : k == 2 ? cxs[2] : cxs[3]);
+    const int cy = ry + (k == 0 ? cys[0] : k == 1 ? cys[1] : k == 2 ? cys[2] : cys[3]);
     if (!((trow[cy][cx >> 5] >> (cx & 31)) & 1)) continue;
-    int count = 1, lc;
-    int level = 1;
-    do {
-      lc = __popc(row_bits(drow[cy - level], cx - level, 2 * level + 1)) +
-           __popc(row_bits(drow[cy + level], cx - level, 2 * level + 1));
-      for (int d = -(level - 1); d <= level - 1; d++) {
-        lc += (drow[cy + d][(cx - level) >> 5] >> ((cx - level) & 31)) & 1;
-        lc += (drow[cy + d][(cx + level) >> 5] >> ((cx + level) & 31)) & 1;
-      }
+    uint32_t D[9];  // bit i of D[r]: pixel (cx - 4 + i, cy - 4 + r)
+#pragma unroll
+    for (int r = 0; r < 9; r++) D[r] = row_bits(drow[cy - 4 + r], cx - 4, 9);
+    // noisefilter_count_pixel_neighbors (filters.c:256-300): count 1, then each level's ring until
+    // an empty one or past N
+    int count = 1;
+    bool go = true;
+#pragma unroll
+    for (int L = 1; L <= 4; L++) {
+      if (!go || L > N) break;
+      const uint32_t span = ((1u << (2 * L + 1)) - 1u) << (4 - L);
+      const uint32_t ends = (1u << (4 - L)) | (1u << (4 + L));
+      int lc = __popc(D[4 - L] & span) + __popc(D[4 + L] & span);
+#pragma unroll
+      for (int r = 4 - L + 1; r <= 4 + L - 1; r++) lc += __popc(D[r] & ends);
       count += lc;
-      level++;
-    } while (lc != 0 && level <= N);
+      go = lc != 0;
+    }
     v.clear = count <= N;
   }
   return v;
+}
+__device__ __forceinline__ SmallVerdict small_verdict_rec(const uint32_t (*drow)[4],
+                                                          const uint32_t (*trow)[4],
+                                                          const uint32_t (*srow)[4], int rx, int ry,
+                                                          int32_t gx, int32_t gy, bool trig, int N,
+                                                          uint32_t rec) {
+  int cxs[4], cys[4], nc = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t b = (rec >> (8 * k)) & 0xFFu;
+    cxs[k] = (int)(b & 15u) - 4;
+    cys[k] = (int)(b >> 4) - 4;
+    nc += b != 0xFFu;
+  }
+  return small_verdict_pixels(drow, trow, srow, rx, ry, gx, gy, trig, N, nc, cxs, cys);
+}
+__device__ __forceinline__ SmallVerdict small_verdict(const uint32_t (*drow)[4],
+                                                      const uint32_t (*trow)[4],
+                                                      const uint32_t (*srow)[4], int rx, int ry,
+                                                      int32_t gx, int32_t gy, bool trig, int N) {
+  uint32_t comp[9];
+  flood9(drow, rx, ry, comp);
+  const uint32_t rec = pack_comp(comp);
+  if (rec == kNotSmall) return SmallVerdict{trig, false};  // more than 4: not eligible
+  return small_verdict_rec(drow, trow, srow, rx, ry, gx, gy, trig, N, rec);
 }
 
 constexpr int kListCap = 1024;  // LDS work list of one tile (else: row loops)
@@ -965,6 +1010,7 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
   __shared__ uint32_t srow[kRW][4];
   __shared__ uint64_t l3[kRW][2], cand[kRW][2];
   __shared__ uint16_t wl[kListCap];
+  __shared__ uint32_t crec[kListCap];  // the candidates' components (pack_comp)
   __shared__ int32_t any_dark, nwl;
   uint32_t (*trow)[4] = kSplit ? trow_s : drow;
   constexpr int B = FMT == F_GRAY8 ? 1 : FMT == F_Y400A ? 2 : 3;
@@ -1154,7 +1200,9 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
     for (int i = threadIdx.x; i < ncand; i += 256) {
       const int e = wl[i], ry = e >> 8, rx = e & 0xFF;
       uint32_t comp[9];
-      if (flood9(drow, rx, ry, comp) <= 4) atomicOr(&srow[ry][rx >> 5], 1u << (rx & 31));
+      const bool small = flood9(drow, rx, ry, comp) <= 4;
+      crec[i] = small ? pack_comp(comp) : kNotSmall;
+      if (small) atomicOr(&srow[ry][rx >> 5], 1u << (rx & 31));
     }
   } else {
     for (int ry = w; ry < kRW; ry += 4) {
@@ -1194,6 +1242,31 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
         wave_append(cx < NTX && dark & zone & trig, gx, gy, NP.nseq, NP.seq, g.capacity);
       }
     }
+  }
+  // small pixels of the tile outside the zone: one lane each, their
+  // components kept from the candidate pass (the candidates hold every small
+  // pixel: a pixel of a component of <= 4 has < 5 dark pixels in its 3x3 and
+  // no large neighbour)
+  if (ncand <= kListCap) {
+    for (int b0 = 0; b0 < ncand; b0 += 256) {  // uniform trip count
+      const int i = b0 + threadIdx.x;
+      SmallVerdict v{false, false};
+      int32_t gx = 0, gy = 0;
+      if (i < ncand) {
+        const uint32_t rec = crec[i];
+        const int e = wl[i], ry = e >> 8, rx = e & 0xFF;
+        gx = ox + rx;
+        gy = oy + ry;
+        const bool inside = ry >= kHalo && ry < kHalo + kNT && rx >= kHalo && rx < kHalo + NTX;
+        if (rec != kNotSmall && inside && !g.all_seq && gx >= kZone && gy >= kZone) {
+          const bool trig = (trow[ry][rx >> 5] >> (rx & 31)) & 1;
+          v = small_verdict_rec(drow, trow, srow, rx, ry, gx, gy, trig, N, rec);
+        }
+      }
+      wave_append(v.seq, gx, gy, NP.nseq, NP.seq, g.capacity);
+      wave_append(v.clear, gx, gy, NP.nclear, NP.clear, g.capacity);
+    }
+    return;
   }
   // small pixels of the tile outside the zone: one lane each
   if (threadIdx.x == 0) nwl = 0;
