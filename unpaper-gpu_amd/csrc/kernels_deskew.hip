@@ -298,27 +298,34 @@ __global__ void __launch_bounds__(kBandThreads, 4)
   const uint8_t* base = plane_ptr(img, s);
   const int rows = i1 - i0, n = rows * bw;
   // blackness 255-max(rgb) of in-mask, in-image pixels (0 elsewhere,
-  // get_pixel's white); unconditional clamped loads, masked arithmetically
-  for (int b0 = 0; b0 < n; b0 += 8 * kBandThreads) {
-    uint8_t v[8];
+  // get_pixel's white); a wave per row, lanes along it (no index division),
+  // unconditional clamped loads masked arithmetically, all of a row's in
+  // flight
+  {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    constexpr int kPer = kBandCapMax / 64;
+    for (int r = w; r < rows; r += kBandThreads / 64) {
+      const int32_t y = ystart + i0 + r;
+      const bool rok = (y >= ylo) & (y <= yhi);
+      const uint8_t* row = base + (int64_t)(rok ? y : ylo) * img.P.pitch;
+      uint8_t v[kPer];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int q = b0 + k * kBandThreads + threadIdx.x;
-      const int r = q / bw, c = q - r * bw;
-      const int32_t y = ystart + i0 + r, x = bx0 + c;
-      const bool ok = (q < n) & (y >= ylo) & (y <= yhi) & (x >= xlo) & (x <= xhi);
-      const int64_t ro = (int64_t)(ok ? y : ylo) * img.P.pitch;
-      const int32_t xo = ok ? x : xlo;
-      uint32_t d;
-      if (fmt == F_GRAY8) d = base[ro + xo];
-      else if (fmt == F_Y400A) d = base[ro + 2 * xo];
-      else d = dark_of(load_px_row<F_RGB24>(base + ro, xo));
-      v[k] = (uint8_t)((255 - d) & -(int)ok);
-    }
+      for (int k = 0; k < kPer; k++) {
+        const int c = lane + 64 * k;
+        const int32_t x = bx0 + c;
+        const bool ok = rok & (c < bw) & (x >= xlo) & (x <= xhi);
+        const int32_t xo = ok ? x : xlo;
+        uint32_t d;
+        if (fmt == F_GRAY8) d = row[xo];
+        else if (fmt == F_Y400A) d = row[2 * xo];
+        else d = dark_of(load_px_row<F_RGB24>(row, xo));
+        v[k] = (uint8_t)((255 - d) & -(int)ok);
+      }
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int q = b0 + k * kBandThreads + threadIdx.x;
-      if (q < n) raw[q] = v[k];
+      for (int k = 0; k < kPer; k++) {
+        const int c = lane + 64 * k;
+        if (c < bw) raw[r * bw + c] = v[k];
+      }
     }
   }
   __syncthreads();

@@ -117,10 +117,13 @@ __global__ void __launch_bounds__(256) k_gray_cells(PlaneRef img, GrayGeom g, ui
   P.light[c] = light;
 }
 
-// k_gray_cells for a gray plane: one workgroup per strip of cell rows.  Each
-// lane sums aligned dwords of the strip's rows (all of a round's loads in
-// flight) into per-column 16-bit totals in LDS (ch <= 257 keeps 255*ch in
-// 16 bits), then one lane per cell adds its cw columns.
+// k_gray_cells for a gray plane: one workgroup per kGrayStrips strips of cell
+// rows, a lane per 8-byte column group (the block is as wide as a row's
+// groups, so nearly every lane has one).  A lane adds its columns over the
+// strip's rows as 16-bit lanes of four words (bytes 0/2 and 1/3 of each
+// dword), counting bytes above the dark threshold as bit 8 of byte + 256 -
+// (thr+1) (ch <= 255 keeps both in 16 bits), and posts the 16-bit column
+// totals to LDS; then one lane per cell adds its cw columns.
 // With `colsum`, the block's strips also add up per-column gray sums over all
 // rows: the sums the next mask scan takes (detect_mask, masks.c:54-100, on
 // the image the grayfilter leaves; k_gray_wipe adds what its wipes change), so
@@ -128,74 +131,87 @@ __global__ void __launch_bounds__(256) k_gray_cells(PlaneRef img, GrayGeom g, ui
 // atomics at W per kGrayStrips * ch rows.
 constexpr int kGrayStripMaxW = 16384;
 constexpr int kGrayStrips = 8;
-__global__ void __launch_bounds__(256) k_gray_cells_g(PlaneRef img, GrayGeom g, uint8_t* scratch,
-                                                      int64_t sstride, const int32_t* active,
-                                                      uint32_t* colsum, int64_t colsum_stride) {
+constexpr int kGrayMaxCh = 255;
+__global__ void __launch_bounds__(1024) k_gray_cells_g(PlaneRef img, GrayGeom g, uint8_t* scratch,
+                                                       int64_t sstride, const int32_t* active,
+                                                       uint32_t* colsum, int64_t colsum_stride) {
   const int s = blockIdx.z;
   if (active && !active[s]) return;
   GrayPtrs P = gray_ptrs(g, scratch + s * sstride);
   if (blockIdx.x == 0 && threadIdx.x == 0) *P.nund = 0;
   const uint8_t* base = plane_ptr(img, s);
-  extern __shared__ uint16_t cols16[];  // [W] dark counts, [W] lightness sums, then [W] u32 totals
-  const int32_t wq = (g.W + 3) & ~3;
+  const int64_t pitch = img.P.pitch;
+  // [wq] dark counts, [wq] lightness sums (u16), then [W] u32 totals
+  extern __shared__ __attribute__((aligned(16))) uint16_t cols16[];
+  const int32_t wq = (g.W + 7) & ~7;
   uint16_t* cdark = cols16;
   uint16_t* clight = cols16 + wq;
   uint32_t* ctot = reinterpret_cast<uint32_t*>(cols16 + 2 * wq);
   if (colsum)
-    for (int32_t x = threadIdx.x; x < g.W; x += 256) ctot[x] = 0;
-  const int32_t nd = (g.W + 3) >> 2;
-  for (int32_t cy = blockIdx.x * kGrayStrips; cy < imin((int32_t)(blockIdx.x + 1) * kGrayStrips, g.ncy);
-       cy++) {
-  const int32_t y0 = cy * g.ch, y1 = imin(y0 + g.ch, g.H);
-  // the four columns of a dword accumulate as 16-bit lanes of two words
-  // (bytes 0/2 and 1/3); dark bits come from bit 8 of byte + 256 - (thr+1)
+    for (int32_t x = threadIdx.x; x < g.W; x += blockDim.x) ctot[x] = 0;
+  const int32_t n8 = (g.W + 7) >> 3;
   const uint32_t kadd = (256u - ((uint32_t)g.black_thr + 1u)) * 0x00010001u;
-  for (int32_t d = threadIdx.x; d < nd; d += 256) {
-    uint32_t l02 = 0, l13 = 0, d02 = 0, d13 = 0;
-    for (int32_t y = y0; y < y1; y += 8) {
-      uint32_t v[8];
+  const int32_t cy_end = imin((int32_t)(blockIdx.x + 1) * kGrayStrips, g.ncy);
+  for (int32_t cy = blockIdx.x * kGrayStrips; cy < cy_end; cy++) {
+    const int32_t y0 = cy * g.ch, y1 = imin(y0 + g.ch, g.H);
+    for (int32_t d = threadIdx.x; d < n8; d += blockDim.x) {
+      // words: bytes 0/2 and 1/3 of the group's dword 0, then of dword 1
+      uint32_t l[4] = {0, 0, 0, 0}, ge[4] = {0, 0, 0, 0};
+      auto add = [&](uint2 v) {
+        const uint32_t w[4] = {v.x & 0x00FF00FFu, (v.x >> 8) & 0x00FF00FFu, v.y & 0x00FF00FFu,
+                               (v.y >> 8) & 0x00FF00FFu};
 #pragma unroll
-      for (int k = 0; k < 8; k++)
-        v[k] = *reinterpret_cast<const uint32_t*>(base + (int64_t)imin(y + k, y1 - 1) * img.P.pitch +
-                                                  4 * d);
+        for (int j = 0; j < 4; j++) {
+          l[j] += w[j];
+          ge[j] += (w[j] + kadd) & 0x01000100u;
+        }
+      };
+      const uint8_t* p = base + (int64_t)y0 * pitch + 8 * d;
+      int32_t y = y0;
+      for (; y + 4 <= y1; y += 4, p += 4 * pitch) {
+        uint2 v[4];
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        if (y + k >= y1) continue;
-        const uint32_t lo = v[k] & 0x00FF00FFu, hi = (v[k] >> 8) & 0x00FF00FFu;
-        l02 += lo;
-        l13 += hi;
-        d02 += 0x00010001u - (((lo + kadd) >> 8) & 0x00010001u);
-        d13 += 0x00010001u - (((hi + kadd) >> 8) & 0x00010001u);
+        for (int k = 0; k < 4; k++) v[k] = *reinterpret_cast<const uint2*>(p + k * pitch);
+#pragma unroll
+        for (int k = 0; k < 4; k++) add(v[k]);
       }
+      for (; y < y1; y++, p += pitch) add(*reinterpret_cast<const uint2*>(p));
+      const uint32_t rows2 = (uint32_t)(y1 - y0) * 0x00010001u;
+      uint32_t dk[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) dk[j] = rows2 - (ge[j] >> 8);
+      // columns 8d + 4k + b sit in word 2k + (b & 1), half b >> 1
+      const uint32_t sel_lo = 0x05040100u, sel_hi = 0x07060302u;  // (a.lo, b.lo), (a.hi, b.hi)
+      const uint4 dv = make_uint4(__builtin_amdgcn_perm(dk[1], dk[0], sel_lo),
+                                  __builtin_amdgcn_perm(dk[1], dk[0], sel_hi),
+                                  __builtin_amdgcn_perm(dk[3], dk[2], sel_lo),
+                                  __builtin_amdgcn_perm(dk[3], dk[2], sel_hi));
+      const uint4 lv = make_uint4(__builtin_amdgcn_perm(l[1], l[0], sel_lo),
+                                  __builtin_amdgcn_perm(l[1], l[0], sel_hi),
+                                  __builtin_amdgcn_perm(l[3], l[2], sel_lo),
+                                  __builtin_amdgcn_perm(l[3], l[2], sel_hi));
+      *reinterpret_cast<uint4*>(cdark + 8 * d) = dv;
+      *reinterpret_cast<uint4*>(clight + 8 * d) = lv;
     }
-    cdark[4 * d + 0] = (uint16_t)d02;
-    cdark[4 * d + 1] = (uint16_t)d13;
-    cdark[4 * d + 2] = (uint16_t)(d02 >> 16);
-    cdark[4 * d + 3] = (uint16_t)(d13 >> 16);
-    clight[4 * d + 0] = (uint16_t)l02;
-    clight[4 * d + 1] = (uint16_t)l13;
-    clight[4 * d + 2] = (uint16_t)(l02 >> 16);
-    clight[4 * d + 3] = (uint16_t)(l13 >> 16);
-  }
-  __syncthreads();
-  for (int32_t cx = threadIdx.x; cx < g.ncx; cx += 256) {
-    const int32_t x0 = cx * g.cw, x1 = imin(x0 + g.cw, g.W);
-    uint32_t dark = 0, light = 0;
-    for (int32_t x = x0; x < x1; x++) {
-      dark += cdark[x];
-      light += clight[x];
+    __syncthreads();
+    for (int32_t cx = threadIdx.x; cx < g.ncx; cx += blockDim.x) {
+      const int32_t x0 = cx * g.cw, x1 = imin(x0 + g.cw, g.W);
+      uint32_t dark = 0, light = 0;
+      for (int32_t x = x0; x < x1; x++) {
+        dark += cdark[x];
+        light += clight[x];
+      }
+      const size_t c = (size_t)cy * g.ncx + cx;
+      P.dark[c] = dark;
+      P.light[c] = light;
     }
-    const size_t c = (size_t)cy * g.ncx + cx;
-    P.dark[c] = dark;
-    P.light[c] = light;
-  }
-  if (colsum)
-    for (int32_t x = threadIdx.x; x < g.W; x += 256) ctot[x] += clight[x];
-  __syncthreads();  // the next strip rewrites the column tables
+    if (colsum)
+      for (int32_t x = threadIdx.x; x < g.W; x += blockDim.x) ctot[x] += clight[x];
+    __syncthreads();  // the next strip rewrites the column tables
   }
   if (colsum) {
     uint32_t* out = colsum + (int64_t)s * colsum_stride;
-    for (int32_t x = threadIdx.x; x < g.W; x += 256)
+    for (int32_t x = threadIdx.x; x < g.W; x += blockDim.x)
       if (ctot[x]) atomicAdd(out + x, ctot[x]);
   }
 }
@@ -360,12 +376,16 @@ static bool launch_gray_t(const PlaneRef& img, const GrayGeom& g, uint8_t* scr, 
                           const int32_t* active, int count, hipStream_t st, uint32_t* colsum,
                           int64_t cs) {
   dim3 grid((g.ncx + 255) / 256, g.ncy, count);
-  const bool strips = FMT == F_GRAY8 && g.W <= kGrayStripMaxW && g.ch <= 257;
+  const bool strips = FMT == F_GRAY8 && g.W <= kGrayStripMaxW && g.ch <= kGrayMaxCh;
   if (!strips) colsum = nullptr;
   if (strips) {
-    const size_t wq = (size_t)((g.W + 3) & ~3);
+    const size_t wq = (size_t)((g.W + 7) & ~7);
+    // a lane per 8-byte column group, up to 1024
+    const int n8 = (g.W + 7) >> 3;
+    const int threads = imin(1024, (n8 + 63) & ~63);
     UPH_LAUNCH_DIAG(32, k_gray_cells_g, dim3((g.ncy + kGrayStrips - 1) / kGrayStrips, 1, count),
-                    dim3(256), 4 * wq + (colsum ? 4 * wq : 0), st, img, g, scr, ss, active, colsum, cs);
+                    dim3(threads), 4 * wq + (colsum ? 4 * (size_t)g.W : 0), st, img, g, scr, ss,
+                    active, colsum, cs);
   } else {
     hipLaunchKernelGGL(k_gray_cells<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active);
   }
@@ -798,28 +818,36 @@ __global__ void __launch_bounds__(256) k_noise_bits(PlaneRef img, NoiseGeom g, u
 // page covering the sheet: a plain copy) fused with the first passes that
 // read the result: the noisefilter's dark bit-plane (k_noise_bits) and the
 // blackfilter's v-stripe row sums (darkness_rect's sums over the stripe's
-// columns, filters.c:49-104).  One wave per row at a time, a lane per
-// 32-pixel word: two 16-byte loads, two 16-byte stores (the row's last word
-// byte by byte up to W), one bit-plane word; the row sum as one wave sum.
+// columns, filters.c:49-104).  A lane per 32-pixel word of the whole sheet
+// (rows are ceil(W/32) words, not a multiple of 64: a wave per row would
+// leave most lanes of its second pass idle): two 16-byte loads, two 16-byte
+// stores (the row's last word byte by byte up to W), one bit-plane word.
+// The stripe sums: each lane's bytes inside the stripe, summed per row over
+// the wave's lanes (a wave spans few rows) and added to the row sum, which
+// the caller zeroes.
 __global__ void __launch_bounds__(256) k_decode_gray(const uint8_t* src, int64_t spitch,
                                                      int64_t sstride, PlaneRef dst, uint8_t white,
                                                      uint32_t* bits, int64_t bstride,
                                                      uint32_t* vsum, int64_t vstride, int32_t vx0,
-                                                     int32_t vx1) {
+                                                     int32_t vx1, int32_t nwr, float rnwr) {
   const int s = blockIdx.y;
-  const int lane = threadIdx.x & 63;
-  const int32_t y = blockIdx.x * 4 + (threadIdx.x >> 6);
   const Planes& P = dst.P;
-  if (y >= P.H) return;
-  const uint8_t* srow = src + s * sstride + (int64_t)y * spitch;
-  uint8_t* drow = plane_ptr(dst, s) + (int64_t)y * P.pitch;
-  const int32_t nwr = (P.W + 31) >> 5;
-  const uint32_t k = (256u - white) * 0x00010001u;
-  uint32_t vs = 0;
-  for (int32_t wi = lane; wi < nwr; wi += 64) {
-    const int32_t x0 = 32 * wi;
+  const int32_t t = blockIdx.x * 256 + threadIdx.x;
+  // t / nwr from the float reciprocal, corrected by one either way
+  int32_t y = (int32_t)((float)t * rnwr);
+  if (y * nwr > t) y--;
+  else if ((y + 1) * nwr <= t) y++;
+  const bool live = y < P.H;
+  uint32_t part = 0;
+  if (live) {
+    const int32_t wi = t - y * nwr, x0 = 32 * wi;
+    const uint8_t* srow = src + s * sstride + (int64_t)y * spitch;
+    uint8_t* drow = plane_ptr(dst, s) + (int64_t)y * P.pitch;
+    const uint32_t k = (256u - white) * 0x00010001u;
+    // a 16-byte chunk starting before W lies inside the 16-aligned pitch
     const uint4 a = *reinterpret_cast<const uint4*>(srow + x0);
-    const uint4 b = *reinterpret_cast<const uint4*>(srow + x0 + 16);
+    const uint4 b = x0 + 16 < P.W ? *reinterpret_cast<const uint4*>(srow + x0 + 16)
+                                  : make_uint4(~0u, ~0u, ~0u, ~0u);
     uint32_t m = lt_nibble(a.x, k) | lt_nibble(a.y, k) << 4 | lt_nibble(a.z, k) << 8 |
                  lt_nibble(a.w, k) << 12 | lt_nibble(b.x, k) << 16 | lt_nibble(b.y, k) << 20 |
                  lt_nibble(b.z, k) << 24 | lt_nibble(b.w, k) << 28;
@@ -833,32 +861,49 @@ __global__ void __launch_bounds__(256) k_decode_gray(const uint8_t* src, int64_t
       for (int j = 0; j < 32; j++)
         if (x0 + j < P.W) drow[x0 + j] = (uint8_t)(w8[j >> 2] >> (8 * (j & 3)));
     }
-    if (bits) bits[s * bstride + (int64_t)y * nwr + wi] = m;
+    if (bits) bits[s * bstride + t] = m;
     if (vsum && x0 <= vx1 && x0 + 31 >= vx0) {
       const uint32_t w8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      if (x0 >= vx0 && x0 + 31 <= vx1) {
 #pragma unroll
-      for (int d = 0; d < 8; d++) {
-        const int32_t xd = x0 + 4 * d;
-        uint32_t keep = 0;
+        for (int d = 0; d < 8; d++) part = __builtin_amdgcn_sad_u8(w8[d], 0u, part);
+      } else {
 #pragma unroll
-        for (int q = 0; q < 4; q++)
-          if (xd + q >= vx0 && xd + q <= vx1) keep |= 0xFFu << (8 * q);
-        vs = __builtin_amdgcn_sad_u8(w8[d] & keep, 0u, vs);
+        for (int d = 0; d < 8; d++) {
+          const int32_t xd = x0 + 4 * d;
+          uint32_t keep = 0;
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            if (xd + q >= vx0 && xd + q <= vx1) keep |= 0xFFu << (8 * q);
+          part = __builtin_amdgcn_sad_u8(w8[d] & keep, 0u, part);
+        }
       }
     }
   }
   if (vsum) {
-    for (int o = 32; o > 0; o >>= 1) vs += __shfl_xor(vs, o, 64);
-    if (lane == 0) vsum[s * vstride + y] = vs;
+    // one wave sum per row among the lanes holding stripe bytes
+    const int lane = threadIdx.x & 63;
+    uint64_t pend = __ballot(part != 0);
+    while (pend) {  // uniform
+      const int l0 = __ffsll((long long)pend) - 1;
+      const int32_t yr = __shfl(y, l0, 64);
+      const bool mine = ((pend >> lane) & 1) && y == yr;
+      uint32_t v = mine ? part : 0u;
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == l0) atomicAdd(vsum + s * vstride + yr, v);
+      pend &= ~__ballot(mine);
+    }
   }
 }
 
 void launch_decode_gray(const uint8_t* src, int64_t spitch, int64_t sstride, const PlaneRef& dst,
                         uint8_t white, uint32_t* bits, int64_t bits_stride, uint32_t* vsum,
                         int64_t vsum_stride, int32_t vx0, int32_t vx1, int count, hipStream_t st) {
-  hipLaunchKernelGGL(k_decode_gray, dim3((unsigned)((dst.P.H + 3) / 4), count), dim3(256), 0, st,
+  const int32_t nwr = (dst.P.W + 31) >> 5;
+  const int64_t words = (int64_t)nwr * dst.P.H;
+  hipLaunchKernelGGL(k_decode_gray, dim3((unsigned)((words + 255) / 256), count), dim3(256), 0, st,
                      src, spitch, sstride, dst, white, bits, bits_stride, vsum, vsum_stride, vx0,
-                     vx1);
+                     vx1, nwr, 1.0f / (float)nwr);
 }
 
 // Whether the classification of a small dark pixel (tile coordinates rx, ry)
