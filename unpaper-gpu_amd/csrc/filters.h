@@ -127,8 +127,7 @@ void launch_blackfilter_impl(const PlaneRef& img, const BlackGeom& g, const Blac
                              uint32_t* nbits = nullptr, int64_t nbits_stride = 0);
 // GRAY8 page -> sheet plane (same size), plus on the way: the noisefilter's
 // dark bit-plane (pixel < white) and the blackfilter's v-stripe row sums over
-// columns [vx0, vx1] (vsum: H entries per sheet after W, added into, so the
-// caller zeroes them; vx0 > vx1 = none).
+// columns [vx0, vx1] (vsum: H entries per sheet after W, vx0 > vx1 = none).
 // Pages 16-byte aligned with a 16-multiple pitch.
 void launch_decode_gray(const uint8_t* src, int64_t spitch, int64_t sstride, const PlaneRef& dst,
                         uint8_t white, uint32_t* bits, int64_t bits_stride, uint32_t* vsum,

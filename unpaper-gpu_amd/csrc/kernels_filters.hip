@@ -778,13 +778,29 @@ __device__ __forceinline__ void wave_append(bool want, int32_t gx, int32_t gy, u
   }
 }
 
-// Dark bits of 4 gray bytes (byte < t) as a nibble: 16-bit SWAR lanes hold
-// b + 256 - t, whose bit 8 is (b >= t); no lane carries into the next.
-__device__ __forceinline__ uint32_t lt_nibble(uint32_t x, uint32_t k) {
-  const uint32_t lo = ((x & 0x00FF00FFu) + k) & 0x01000100u;
-  const uint32_t hi = (((x >> 8) & 0x00FF00FFu) + k) & 0x01000100u;
-  const uint32_t ge = (lo >> 8) | (hi >> 7);  // bits 0,1 (bytes 0,1), 16,17 (bytes 2,3)
-  return ~(ge | (ge >> 14)) & 0xFu;
+// Dark bits (byte < t) of 32 gray bytes (eight dwords) as one word, bit
+// 4 d + q = byte q of dword d.  Per dword: 16-bit SWAR lanes hold
+// (0x100 + t - 1) - byte, whose bit 8 is (byte < t) with nothing above it, so
+// one byte permute gathers the four flags as bytes of 0 or 1; the eight
+// dwords' flag bytes are stacked (bit 8 q + d), and four delta swaps
+// transpose that 4 x 8 bit matrix into pixel order.
+__device__ __forceinline__ uint32_t dark_bits32(const uint32_t (&w)[8], uint32_t white) {
+  const uint32_t K = (0x100u + white - 1u) * 0x00010001u;
+  uint32_t g = 0;
+#pragma unroll
+  for (int d = 0; d < 8; d++) {
+    const uint32_t lo = K - (w[d] & 0x00FF00FFu);          // bits 8, 24: bytes 0, 2
+    const uint32_t hi = K - ((w[d] >> 8) & 0x00FF00FFu);   // bits 8, 24: bytes 1, 3
+    g |= __builtin_amdgcn_perm(hi, lo, 0x07030501u) << d;  // bytes: flags of bytes 0..3
+  }
+  auto dswap = [](uint32_t x, uint32_t m, int delta) {
+    const uint32_t t = ((x >> delta) ^ x) & m;
+    return x ^ t ^ (t << delta);
+  };
+  g = dswap(g, 0x0000F0F0u, 12);
+  g = dswap(g, 0x00CC00CCu, 6);
+  g = dswap(g, 0x0A0A0A0Au, 3);
+  return dswap(g, 0x22222222u, 1);
 }
 
 // GRAY8 dark bit-plane: bit b of word w of row y is (pixel 32 w + b < white);
@@ -806,30 +822,22 @@ __global__ void __launch_bounds__(256) k_noise_bits(PlaneRef img, NoiseGeom g, u
   const int32_t wi = t - y * nwr, x0 = 32 * wi;
   const uint4* p = reinterpret_cast<const uint4*>(plane_ptr(img, s) + (int64_t)y * img.P.pitch + x0);
   const uint4 a = p[0], b = p[1];
-  const uint32_t k = (256u - g.white) * 0x00010001u;
-  uint32_t m = lt_nibble(a.x, k) | lt_nibble(a.y, k) << 4 | lt_nibble(a.z, k) << 8 |
-               lt_nibble(a.w, k) << 12 | lt_nibble(b.x, k) << 16 | lt_nibble(b.y, k) << 20 |
-               lt_nibble(b.z, k) << 24 | lt_nibble(b.w, k) << 28;
+  uint32_t m = dark_bits32({a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}, g.white);
   if (x0 + 32 > g.W) m &= (1u << (g.W - x0)) - 1u;  // g.W - x0 in [1, 31]
   bits[s * bstride + t] = m;
 }
 
 // The decode of a GRAY8 page into its sheet (sheet_stages.c:151-165 with the
-// page covering the sheet: a plain copy) fused with the first passes that
-// read the result: the noisefilter's dark bit-plane (k_noise_bits) and the
-// blackfilter's v-stripe row sums (darkness_rect's sums over the stripe's
-// columns, filters.c:49-104).  A lane per 32-pixel word of the whole sheet
-// (rows are ceil(W/32) words, not a multiple of 64: a wave per row would
-// leave most lanes of its second pass idle): two 16-byte loads, two 16-byte
-// stores (the row's last word byte by byte up to W), one bit-plane word.
-// The stripe sums: each lane's bytes inside the stripe, summed per row over
-// the wave's lanes (a wave spans few rows) and added to the row sum, which
-// the caller zeroes.
+// page covering the sheet: a plain copy) fused with the first pass that reads
+// the result: the noisefilter's dark bit-plane (k_noise_bits).  A lane per
+// 32-pixel word of the whole sheet (rows are ceil(W/32) words, not a multiple
+// of 64: a wave per row would leave most lanes of its second pass idle): two
+// 16-byte loads, two 16-byte stores (the row's last word in pieces up to W),
+// one bit-plane word.
 __global__ void __launch_bounds__(256) k_decode_gray(const uint8_t* src, int64_t spitch,
                                                      int64_t sstride, PlaneRef dst, uint8_t white,
-                                                     uint32_t* bits, int64_t bstride,
-                                                     uint32_t* vsum, int64_t vstride, int32_t vx0,
-                                                     int32_t vx1, int32_t nwr, float rnwr) {
+                                                     uint32_t* bits, int64_t bstride, int32_t nwr,
+                                                     float rnwr) {
   const int s = blockIdx.y;
   const Planes& P = dst.P;
   const int32_t t = blockIdx.x * 256 + threadIdx.x;
@@ -837,62 +845,87 @@ __global__ void __launch_bounds__(256) k_decode_gray(const uint8_t* src, int64_t
   int32_t y = (int32_t)((float)t * rnwr);
   if (y * nwr > t) y--;
   else if ((y + 1) * nwr <= t) y++;
-  const bool live = y < P.H;
-  uint32_t part = 0;
-  if (live) {
-    const int32_t wi = t - y * nwr, x0 = 32 * wi;
-    const uint8_t* srow = src + s * sstride + (int64_t)y * spitch;
-    uint8_t* drow = plane_ptr(dst, s) + (int64_t)y * P.pitch;
-    const uint32_t k = (256u - white) * 0x00010001u;
-    // a 16-byte chunk starting before W lies inside the 16-aligned pitch
-    const uint4 a = *reinterpret_cast<const uint4*>(srow + x0);
-    const uint4 b = x0 + 16 < P.W ? *reinterpret_cast<const uint4*>(srow + x0 + 16)
-                                  : make_uint4(~0u, ~0u, ~0u, ~0u);
-    uint32_t m = lt_nibble(a.x, k) | lt_nibble(a.y, k) << 4 | lt_nibble(a.z, k) << 8 |
-                 lt_nibble(a.w, k) << 12 | lt_nibble(b.x, k) << 16 | lt_nibble(b.y, k) << 20 |
-                 lt_nibble(b.z, k) << 24 | lt_nibble(b.w, k) << 28;
-    if (x0 + 32 <= P.W) {
-      *reinterpret_cast<uint4*>(drow + x0) = a;
-      *reinterpret_cast<uint4*>(drow + x0 + 16) = b;
-    } else {
-      m &= (1u << (P.W - x0)) - 1u;  // P.W - x0 in [1, 31]
-      const uint32_t w8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-      for (int j = 0; j < 32; j++)
-        if (x0 + j < P.W) drow[x0 + j] = (uint8_t)(w8[j >> 2] >> (8 * (j & 3)));
+  if (y >= P.H) return;
+  const int32_t wi = t - y * nwr, x0 = 32 * wi;
+  const uint8_t* srow = src + s * sstride + (int64_t)y * spitch;
+  uint8_t* d = plane_ptr(dst, s) + (int64_t)y * P.pitch + x0;
+  // a 16-byte chunk starting before W lies inside the 16-aligned pitch
+  const uint4 a = *reinterpret_cast<const uint4*>(srow + x0);
+  const uint4 b = x0 + 16 < P.W ? *reinterpret_cast<const uint4*>(srow + x0 + 16)
+                                : make_uint4(~0u, ~0u, ~0u, ~0u);
+  uint32_t m = dark_bits32({a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}, white);
+  if (x0 + 32 <= P.W) {
+    *reinterpret_cast<uint4*>(d) = a;
+    *reinterpret_cast<uint4*>(d + 16) = b;
+  } else {
+    // the row's last word: n = W - x0 in [1, 31] bytes, as a 16-byte chunk,
+    // dwords and the last dword's bytes
+    const int32_t n = P.W - x0;
+    m &= (1u << n) - 1u;
+    uint4 q = a;
+    int32_t j = 0;
+    if (n >= 16) {
+      *reinterpret_cast<uint4*>(d) = a;
+      q = b;
+      j = 16;
     }
-    if (bits) bits[s * bstride + t] = m;
-    if (vsum && x0 <= vx1 && x0 + 31 >= vx0) {
-      const uint32_t w8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-      if (x0 >= vx0 && x0 + 31 <= vx1) {
+    const int32_t r = n - j;  // 0..15
+    if (r >= 4) *reinterpret_cast<uint32_t*>(d + j) = q.x;
+    if (r >= 8) *reinterpret_cast<uint32_t*>(d + j + 4) = q.y;
+    if (r >= 12) *reinterpret_cast<uint32_t*>(d + j + 8) = q.z;
+    uint32_t last = r < 4 ? q.x : r < 8 ? q.y : r < 12 ? q.z : q.w;
+    for (int32_t i = j + (r & ~3); i < n; i++, last >>= 8) d[i] = (uint8_t)last;
+  }
+  if (bits) bits[s * bstride + t] = m;
+}
+
+// The blackfilter's v-stripe row sums (darkness_rect's sums over the stripe's
+// columns [vx0, vx1], filters.c:49-104) straight from the GRAY8 pages the
+// decode copies unchanged.  A half-wave per row (32 lanes x 16 bytes cover a
+// 500-column stripe in one load each), eight rows per wave with all their
+// loads in flight, SAD byte sums, then a 32-lane sum per row.
+constexpr int kStripeRowsPerWave = 8;
+__global__ void __launch_bounds__(256) k_stripe_sums(const uint8_t* src, int64_t spitch,
+                                                     int64_t sstride, int32_t H, uint32_t* vsum,
+                                                     int64_t vstride, int32_t vx0, int32_t vx1) {
+  const int s = blockIdx.y;
+  const int lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
+  const int32_t yw = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kStripeRowsPerWave;
+  if (yw >= H) return;
+  const uint8_t* page = src + s * sstride;
+  const int32_t xa = vx0 & ~15;
+  constexpr int kR = kStripeRowsPerWave / 2;  // rows per half-wave
+  uint32_t acc[kR] = {};
+  for (int32_t x = xa + 16 * hl; x <= vx1; x += 16 * 32) {  // one pass for stripes <= 512 columns
+    uint32_t keep[4];
 #pragma unroll
-        for (int d = 0; d < 8; d++) part = __builtin_amdgcn_sad_u8(w8[d], 0u, part);
-      } else {
+    for (int q = 0; q < 4; q++) {
+      const int32_t xq = x + 4 * q;
+      keep[q] = 0;
 #pragma unroll
-        for (int d = 0; d < 8; d++) {
-          const int32_t xd = x0 + 4 * d;
-          uint32_t keep = 0;
+      for (int j = 0; j < 4; j++)
+        if (xq + j >= vx0 && xq + j <= vx1) keep[q] |= 0xFFu << (8 * j);
+    }
+    uint4 v[kR];
 #pragma unroll
-          for (int q = 0; q < 4; q++)
-            if (xd + q >= vx0 && xd + q <= vx1) keep |= 0xFFu << (8 * q);
-          part = __builtin_amdgcn_sad_u8(w8[d] & keep, 0u, part);
-        }
-      }
+    for (int r = 0; r < kR; r++) {
+      const int32_t y = imin(yw + 2 * r + half, H - 1);
+      v[r] = *reinterpret_cast<const uint4*>(page + (int64_t)y * spitch + x);
+    }
+#pragma unroll
+    for (int r = 0; r < kR; r++) {
+      acc[r] = __builtin_amdgcn_sad_u8(v[r].x & keep[0], 0u, acc[r]);
+      acc[r] = __builtin_amdgcn_sad_u8(v[r].y & keep[1], 0u, acc[r]);
+      acc[r] = __builtin_amdgcn_sad_u8(v[r].z & keep[2], 0u, acc[r]);
+      acc[r] = __builtin_amdgcn_sad_u8(v[r].w & keep[3], 0u, acc[r]);
     }
   }
-  if (vsum) {
-    // one wave sum per row among the lanes holding stripe bytes
-    const int lane = threadIdx.x & 63;
-    uint64_t pend = __ballot(part != 0);
-    while (pend) {  // uniform
-      const int l0 = __ffsll((long long)pend) - 1;
-      const int32_t yr = __shfl(y, l0, 64);
-      const bool mine = ((pend >> lane) & 1) && y == yr;
-      uint32_t v = mine ? part : 0u;
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      if (lane == l0) atomicAdd(vsum + s * vstride + yr, v);
-      pend &= ~__ballot(mine);
-    }
+#pragma unroll
+  for (int r = 0; r < kR; r++) {
+    uint32_t a = acc[r];
+    for (int o = 16; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);  // within the half-wave
+    const int32_t y = yw + 2 * r + half;
+    if (hl == 0 && y < H) vsum[s * vstride + y] = a;
   }
 }
 
@@ -902,8 +935,13 @@ void launch_decode_gray(const uint8_t* src, int64_t spitch, int64_t sstride, con
   const int32_t nwr = (dst.P.W + 31) >> 5;
   const int64_t words = (int64_t)nwr * dst.P.H;
   hipLaunchKernelGGL(k_decode_gray, dim3((unsigned)((words + 255) / 256), count), dim3(256), 0, st,
-                     src, spitch, sstride, dst, white, bits, bits_stride, vsum, vsum_stride, vx0,
-                     vx1, nwr, 1.0f / (float)nwr);
+                     src, spitch, sstride, dst, white, bits, bits_stride, nwr, 1.0f / (float)nwr);
+  if (vsum && vx0 <= vx1)
+    hipLaunchKernelGGL(k_stripe_sums,
+                       dim3((unsigned)((dst.P.H + 4 * kStripeRowsPerWave - 1) / (4 * kStripeRowsPerWave)),
+                            count),
+                       dim3(256), 0, st,
+                       src, spitch, sstride, dst.P.H, vsum, vsum_stride, vx0, vx1);
 }
 
 // Whether the classification of a small dark pixel (tile coordinates rx, ry)

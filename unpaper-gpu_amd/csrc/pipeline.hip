@@ -1129,9 +1129,6 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
   const bool vsum_ready = fused && black_on && b->bgeo.vregion.x1 >= b->bgeo.vregion.x0;
   uint32_t* bits_ready = fused && !(dis & UPHIP_NO_NOISEFILTER) ? b->nbits : nullptr;
   if (fused) {
-    if (vsum_ready)  // the decode adds into the v-stripe row sums
-      UPH_HIP(hipMemset2DAsync((uint32_t*)b->scr + b->bgeo.W, b->scr_stride, 0,
-                               sizeof(uint32_t) * h, count, b->st));
     launch_decode_gray(src, spitch, sstride, cur_ref(S0, b->ctl), o.abs_white_threshold, bits_ready,
                        b->nbits_stride, vsum_ready ? (uint32_t*)b->scr + b->bgeo.W : nullptr,
                        b->scr_stride / 4, b->bgeo.vregion.x0, b->bgeo.vregion.x1, count, b->st);
