@@ -77,7 +77,7 @@ $(OBJDIR)/%.c.o: $(CSRC)/%.c $(HDRS)
 
 $(LIB): $(HIP_OBJS) $(CPP_OBJS) $(C_OBJS)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread -lz
 
 $(ORACLE_LIB): oracle/oracle.c oracle/oracle.h include/unpaper_hip.h
 	@mkdir -p oracle/_build
@@ -101,7 +101,7 @@ $(ADAPTER): tests/c/adapter_main.c tests/c/pages.h integration/backend_hip.c int
 
 # One compiler (ROCm clang) for every object so that one sanitizer runtime
 # serves the program; the HIP sources are compiled for the host only.
-$(SANITIZE): tests/c/sanitize_main.c oracle/oracle.c oracle/oracle.h $(CSRC)/pnm.cpp \
+$(SANITIZE): tests/c/sanitize_main.c oracle/oracle.c oracle/oracle.h $(CSRC)/pnm.cpp $(CSRC)/png.cpp \
              $(CSRC)/runtime.hip $(HDRS)
 	@mkdir -p tests/c/_build/san
 	$(LLVMCC) $(SANFLAGS) -std=gnu11 -ffp-contract=off -c oracle/oracle.c -o tests/c/_build/san/oracle.o
@@ -109,11 +109,13 @@ $(SANITIZE): tests/c/sanitize_main.c oracle/oracle.c oracle/oracle.h $(CSRC)/pnm
 	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
 	  -Iinclude -I$(CSRC) -c $(CSRC)/pnm.cpp -o tests/c/_build/san/pnm.o
 	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
+	  -Iinclude -I$(CSRC) -c $(CSRC)/png.cpp -o tests/c/_build/san/png.o
+	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
 	  -Iinclude -I$(CSRC) -c $(CSRC)/runtime.hip -o tests/c/_build/san/runtime.o
-	$(HIPCC) $(SANFLAGS) tests/c/_build/san/*.o -o $@ -lm
+	$(HIPCC) $(SANFLAGS) tests/c/_build/san/*.o -o $@ -lm -lz
 
 sanitize: $(SANITIZE)
-	ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=print_stacktrace=1 $(SANITIZE) $(CURDIR)/tests/c/_build/san
+	ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=print_stacktrace=1 $(SANITIZE) $(CURDIR)/tests/c/_build/san $(CURDIR)/tests/golden/reference
 
 clean:
 	rm -rf $(PKG)/build $(PKG)/build_diag $(PKG)/lib $(PKG)/lib_diag oracle/_build tests/c/_build

@@ -455,6 +455,19 @@ int uphip_pnm_read(const char *path, void *dst, int64_t linesize,
                    const UphipPnmInfo *expect);
 int uphip_pnm_write(const char *path, const void *src, int64_t linesize,
                     int32_t width, int32_t height, int32_t format);
+/* PNG half of loadImage (file.c:29-131; the reference's test sources are
+ * PNG), formats as FFmpeg's PNG decoder reports them: 1-bit gray ->
+ * MONOBLACK, 2/4/8-bit gray -> GRAY8, gray+alpha (or 8-bit gray + tRNS) ->
+ * Y400A, RGB -> RGB24, palette -> RGB24 (the PAL8 case, file.c:110-120);
+ * 16-bit samples and RGBA fail like loadImage's "unsupported pixel format".
+ * Adam7 interlacing supported.  Output stays PNM (saveImage, file.c:260-300). */
+int uphip_png_probe(const char *path, UphipPnmInfo *info);
+int uphip_png_read(const char *path, void *dst, int64_t linesize,
+                   const UphipPnmInfo *expect);
+/* Either codec, picked by the file's signature (PNG or PNM). */
+int uphip_image_probe(const char *path, UphipPnmInfo *info);
+int uphip_image_read(const char *path, void *dst, int64_t linesize,
+                     const UphipPnmInfo *expect);
 
 /* ---------------------------------------------------------------------------
  * Multi-device runner — the peer of lib/batch_worker.c (batch_process_parallel,
@@ -499,7 +512,8 @@ UphipSource *uphip_source_callback(UphipLoadFn load, void *user);
 /* page i at base + i*page_stride, rows `linesize` apart */
 UphipSource *uphip_source_memory(const void *base, int64_t linesize,
                                  int64_t page_stride, int64_t npages);
-/* page i decoded from paths[i] (PNM) straight into the staging slot */
+/* page i decoded from paths[i] (PNM or PNG, uphip_image_read) straight into
+ * the staging slot */
 UphipSource *uphip_source_pnm(const char *const *paths, int64_t npaths);
 void uphip_source_destroy(UphipSource *source);
 UphipSink *uphip_sink_callback(UphipStoreFn store, void *user);

@@ -1,7 +1,8 @@
 /* sanitize_main.c — host code under AddressSanitizer + UndefinedBehavior-
  * Sanitizer: the oracle's whole sheet pipeline on synthetic
  * pages in every input format and layout, plus the product library's host
- * PNM codec (pnm.cpp) on well-formed and malformed files.  No GPU involved.
+ * PNM codec (pnm.cpp) and PNG decoder (png.cpp) on well-formed and
+ * malformed files.  No GPU involved.
  * Built and run by `make sanitize` (tests/test_sanitize.py).
  */
 #include <stdio.h>
@@ -83,6 +84,54 @@ static void codec(const char *dir) {
   }
 }
 
+/* the PNG decoder (png.cpp) on the reference's own sources and on
+ * truncated / bit-flipped copies of one */
+static void png(const char *dir, const char *fixtures) {
+  static const char *names[] = {"imgsrc002.png", "imgsrc003.png", "imgsrc004.png", "imgsrc006.png"};
+  char path[512];
+  for (size_t i = 0; i < sizeof names / sizeof *names; i++) {
+    snprintf(path, sizeof path, "%s/%s", fixtures, names[i]);
+    UphipPnmInfo info;
+    if (uphip_image_probe(path, &info) != 0) {
+      fprintf(stderr, "png probe %s: %s\n", path, uphip_last_error());
+      g_fail++;
+      continue;
+    }
+    const int64_t ls = info.format == UPHIP_FMT_RGB24 ? 3 * (int64_t)info.width
+                       : info.format == UPHIP_FMT_MONOBLACK ? (info.width + 7) / 8
+                                                            : (int64_t)info.width;
+    uint8_t *buf = (uint8_t *)malloc((size_t)(ls * info.height));
+    if (uphip_image_read(path, buf, ls, &info) != 0) g_fail++;
+    if (i == 3) {  /* damaged copies of the small RGB source */
+      FILE *f = fopen(path, "rb");
+      static uint8_t raw[1 << 20];
+      const size_t n = fread(raw, 1, sizeof raw, f);
+      fclose(f);
+      for (size_t cut = 9; cut < n; cut += n / 13) {
+        for (int flip = 0; flip < 2; flip++) {
+          snprintf(path, sizeof path, "%s/bad.png", dir);
+          f = fopen(path, "wb");
+          if (flip) {
+            raw[cut] ^= 0x41;
+            fwrite(raw, 1, n, f);
+            raw[cut] ^= 0x41;
+          } else {
+            fwrite(raw, 1, cut, f);
+          }
+          fclose(f);
+          if (!flip && uphip_image_read(path, buf, ls, &info) == 0) {
+            fprintf(stderr, "truncated png (%zu bytes) accepted\n", cut);
+            g_fail++;
+          }
+          if (flip) uphip_image_read(path, buf, ls, &info);  /* must not crash */
+          uphip_clear_error();
+        }
+      }
+    }
+    free(buf);
+  }
+}
+
 int main(int argc, char **argv) {
   const char *dir = argc > 1 ? argv[1] : "/tmp";
   UphipOptions o;
@@ -102,6 +151,7 @@ int main(int argc, char **argv) {
   o.noisefilter_intensity = 9;
   sheet("geometry", &o, UPHIP_FMT_GRAY8, 300, 420, 15);
   codec(dir);
+  png(dir, argc > 2 ? argv[2] : "tests/golden/reference");
   printf("sanitize: %d failures\n", g_fail);
   return g_fail ? 1 : 0;
 }

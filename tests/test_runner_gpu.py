@@ -120,6 +120,31 @@ def test_runner_pnm_files(hip, oracle, tmp_path):
         assert_same(got, _oracle_out(oracle, opts, p), "pnm job %d" % i)
 
 
+@pytest.mark.parametrize("names,fmt,out_ext", [
+    (("imgsrc002.png", "imgsrc005.png"), A.FMT_MONOBLACK, "pbm"),
+    (("imgsrc004.png",), A.FMT_GRAY8, "pgm"),
+    (("imgsrc003.png",), A.FMT_RGB24, "ppm")])
+def test_runner_png_reference_sources(hip, oracle, ref_path, tmp_path, names, fmt, out_ext):
+    """The reference's own PNG test sources (1-bit -> MONOBLACK, gray, RGB)
+    decoded by the native PNG codec straight into staging, processed with
+    default options and written as PNM, against the oracle on the same pages
+    loaded through PIL."""
+    opts = oracle.default_options()
+    pages = [HostImage.load(ref_path(n)) for n in names]
+    w, h = pages[0].width, pages[0].height
+    assert all(p.format == fmt for p in pages)
+    r = Runner(opts, 2, w, h, fmt, devices=(0,), streams=1, host_threads=2)
+    try:
+        failed, err = r.run_host(len(names), source_pnm([ref_path(n) for n in names]),
+                                 sink_pnm(str(tmp_path / ("out_%02d." + out_ext))))
+        assert failed == 0, err
+    finally:
+        r.close()
+    for i, p in enumerate(pages):
+        got = pnm_read(str(tmp_path / ("out_%02d.%s" % (i, out_ext))))
+        assert_same(got, _oracle_out(oracle, opts, p), "png job %s" % names[i])
+
+
 def test_runner_two_outputs_pbm(hip, oracle, tmp_path):
     """--layout double --output-pages 2 with MONOWHITE output: the encode
     queue splits every sheet into two PBM pages (sheet_stages.c:606-624)."""

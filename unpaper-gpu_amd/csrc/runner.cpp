@@ -200,7 +200,7 @@ int pnm_load(const UphipSource* s, int64_t idx, void* dst, int64_t linesize,
              const UphipPnmInfo& geo) {
   if (idx < 0 || idx >= (int64_t)s->paths.size())
     return fail("source_pnm: page %lld out of range", (long long)idx), -1;
-  return uphip_pnm_read(s->paths[(size_t)idx].c_str(), dst, linesize, &geo);
+  return uphip_image_read(s->paths[(size_t)idx].c_str(), dst, linesize, &geo);
 }
 
 // The reference names output files with sprintf(buf, pattern, outputNr++)

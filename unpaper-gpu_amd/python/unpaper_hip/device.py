@@ -45,6 +45,7 @@ EXPORTED = [
     "uphip_device_alloc", "uphip_device_free", "uphip_memcpy_htod", "uphip_memcpy_dtoh",
     "uphip_batch_upload_async", "uphip_batch_download_async", "uphip_batch_query",
     "uphip_batch_stream", "uphip_batch_output_pitch", "uphip_pnm_probe", "uphip_pnm_read", "uphip_pnm_write",
+    "uphip_png_probe", "uphip_png_read", "uphip_image_probe", "uphip_image_read",
     "uphip_source_callback", "uphip_source_memory", "uphip_source_pnm", "uphip_source_destroy",
     "uphip_sink_callback", "uphip_sink_memory", "uphip_sink_pnm", "uphip_sink_discard",
     "uphip_sink_destroy", "uphip_runner_create", "uphip_runner_destroy",
@@ -147,6 +148,10 @@ def load_library(path=LIB_PATH):
         "uphip_batch_output_pitch": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
         "uphip_pnm_probe": (C.c_int, [C.c_char_p, C.POINTER(A.PnmInfo)]),
         "uphip_pnm_read": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int64, C.POINTER(A.PnmInfo)]),
+        "uphip_png_probe": (C.c_int, [C.c_char_p, C.POINTER(A.PnmInfo)]),
+        "uphip_png_read": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int64, C.POINTER(A.PnmInfo)]),
+        "uphip_image_probe": (C.c_int, [C.c_char_p, C.POINTER(A.PnmInfo)]),
+        "uphip_image_read": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int64, C.POINTER(A.PnmInfo)]),
         "uphip_pnm_write": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32,
                                       C.c_int32]),
         "uphip_source_callback": (C.c_void_p, [A.LoadFn, C.c_void_p]),

@@ -296,3 +296,15 @@ def pnm_read(path) -> HostImage:
     if L.uphip_pnm_read(path.encode(), img.data.ctypes.data, img.linesize, C.byref(info)) != 0:
         _check(L)
     return img
+
+
+def image_read(path) -> HostImage:
+    """loadImage's peer (file.c:29-131): PNG or PNM, picked by signature."""
+    L = load_library()
+    info = A.PnmInfo()
+    if L.uphip_image_probe(path.encode(), C.byref(info)) != 0:
+        _check(L)
+    img = HostImage(info.width, info.height, info.format)
+    if L.uphip_image_read(path.encode(), img.data.ctypes.data, img.linesize, C.byref(info)) != 0:
+        _check(L)
+    return img
