@@ -317,7 +317,7 @@ __device__ __forceinline__ Frame frame_pop(const Frame* hbm, int32_t i) {
 
 struct BlackStats {
   uint32_t frames, fill_trips, check_trips, bar_trips, remeasures;
-  uint64_t t_fill, t_check, t_bar, t_remeasure;
+  uint64_t t_fill, t_check, t_bar, t_remeasure, t_wait0, t_paint, t_wait1;
 };
 #ifdef UPHIP_DIAG
 #define BSTAT(...) __VA_ARGS__
@@ -482,6 +482,7 @@ __device__ __forceinline__ void fill_cross(const Sheet& S, int32_t px, int32_t p
     paint_cross(S, px, py, dist);  // the start
     return;
   }
+  BSTAT({ const uint64_t tw = wall_clock64(); __builtin_amdgcn_s_waitcnt(0); bs->t_wait0 += wall_clock64() - tw; })
   const int32_t edge[4] = {px + 1, py + 1, S.W - px, S.H - py};  // first position outside
   int32_t pos0[4] = {1, 1, 1, 1}, carry[4], stop[4];
 #pragma unroll
@@ -525,7 +526,9 @@ __device__ __forceinline__ void fill_cross(const Sheet& S, int32_t px, int32_t p
   }
 #pragma unroll
   for (int d = 0; d < 4; d++) dist[d] = uni(stop[d] - 1);
+  BSTAT(const uint64_t tp = wall_clock64();)
   paint_cross(S, px, py, dist);
+  BSTAT(bs->t_paint += wall_clock64() - tp;)
 }
 
 // Neighbour checks (flood_fill_around_line, fill.c:54-74): the checks of line
@@ -643,6 +646,7 @@ __device__ __forceinline__ bool flood(const Sheet& S, int32_t sx, int32_t sy, Fr
       cs[0] = 0;
 #pragma unroll
       for (int d = 0; d < 4; d++) cs[d + 1] = cs[d] + 2 * top.dist[d];
+      BSTAT({ const uint64_t tw = wall_clock64(); __builtin_amdgcn_s_waitcnt(0); bs->t_wait1 += wall_clock64() - tw; })
       BSTAT(const uint64_t t1 = wall_clock64(); bs->check_trips++;)
       int32_t nxt;
       c = uni(check_eval(S, wc, top, cs, 0, 0, p1, &resume, &nxt));
@@ -785,10 +789,11 @@ __global__ void __launch_bounds__(64) k_black_resolve(PlaneRef img, BlackGeom g,
 #ifdef UPHIP_DIAG
   if ((g.diag & 16) && lane == 0 && bstat.frames)
     printf("uphip black: sheet %d frames %u fill %u (%.1f us) check %u (%.1f us) bar %u (%.1f us) "
-           "remeasure %u (%.1f us) total %.1f us\n",
+           "remeasure %u (%.1f us) wait0 %.1f paint %.1f wait1 %.1f total %.1f us\n",
            s, bstat.frames, bstat.fill_trips, bstat.t_fill * 0.01, bstat.check_trips,
            bstat.t_check * 0.01, bstat.bar_trips, bstat.t_bar * 0.01, bstat.remeasures,
-           bstat.t_remeasure * 0.01, (wall_clock64() - t_all) * 0.01);
+           bstat.t_remeasure * 0.01, bstat.t_wait0 * 0.01, bstat.t_paint * 0.01,
+           bstat.t_wait1 * 0.01, (wall_clock64() - t_all) * 0.01);
 #endif
 }
 
