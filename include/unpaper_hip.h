@@ -439,6 +439,8 @@ void *uphip_batch_stream(UphipBatch *batch);
 /* Row pitch of the output sheets on the device: host staging with this
  * linesize (and pitch * height per sheet) downloads as linear DMA copies. */
 int uphip_batch_output_pitch(UphipBatch *batch, int64_t *pitch);
+/* Device memory the batch holds (planes, inputs, scratch, tables). */
+int uphip_batch_device_bytes(UphipBatch *batch, int64_t *bytes);
 
 /* ---------------------------------------------------------------------------
  * Host codec — the PNM half of loadImage/saveImage (file.c:29-259).
@@ -482,10 +484,19 @@ int uphip_image_read(const char *path, void *dst, int64_t linesize,
 typedef struct UphipRunner UphipRunner;
 typedef struct UphipSource UphipSource;
 typedef struct UphipSink UphipSink;
+/* Auto-sizing (the reference's VRAM tiers, src/pipeline/image_pipeline.c:
+ * 237-285, there 1 stream per 3 GB capped at 8, 3 buffers per stream):
+ *   geometry->capacity <= 0: sheets per batch = 2 GiB / (the sheet's input
+ *     pages + its two working planes), clamped to [1, 64];
+ *   batches_per_device <= 0: in-flight batches per device = as many as fit
+ *     in half of the device's free memory after the first, clamped to
+ *     [1, 16] (16 x 64 A4 sheets is where one MI355X stops gaining,
+ *     profiles/r01_bench_sweep.txt).
+ * uphip_runner_layout() reports what was chosen. */
 typedef struct {
   int32_t ndevices;            /* devices used */
   const int32_t *devices;      /* their ids (NULL = 0 .. ndevices-1) */
-  int32_t batches_per_device;  /* HIP streams (in-flight batches) per device */
+  int32_t batches_per_device;  /* HIP streams (in-flight batches) per device; <= 0: auto */
   int32_t host_threads;        /* load/store worker threads (0 = 4 per device) */
   int32_t timing;              /* stage timing on every batch */
 } UphipRunnerConfig;
@@ -540,6 +551,10 @@ int uphip_runner_run_device(UphipRunner *runner, const UphipDevicePages *shards,
 int uphip_runner_run_host(UphipRunner *runner, int64_t njobs, UphipSource *source,
                           UphipSink *sink);
 int uphip_runner_get_stats(UphipRunner *runner, UphipRunnerStats *stats);
+/* The batch layout in use (after auto-sizing): batches per device, sheets
+ * per batch, device bytes per batch. */
+int uphip_runner_layout(UphipRunner *runner, int32_t *batches_per_device,
+                        int32_t *capacity, int64_t *batch_bytes);
 int uphip_runner_output_info(UphipRunner *runner, int32_t *width, int32_t *height,
                              int32_t *format, int64_t *linesize);
 UphipBatch *uphip_runner_batch(UphipRunner *runner, int32_t device_index,

@@ -7,8 +7,9 @@
   must report every checked page equal.
 * runner (uphip_runner_*, the lib/batch_worker.c + decode/encode queue
   peer): host-fed runs through pinned staging against the oracle, PNM
-  file-to-file, a failing source job isolated to itself, two runner threads
-  on one device.
+  file-to-file, the reference's own PNG sources through the PNG decoder, the
+  auto-sized batch layout, a failing source job isolated to itself, two and
+  four runner threads on one device.
 * C4 (BASELINE configs[3]): one RGB24 9920x7016 double-page sheet, layout
   double, bilinear deskew, border wipe, against the oracle's hash
   (tests/golden/c4_hashes.json).
@@ -118,6 +119,41 @@ def test_runner_pnm_files(hip, oracle, tmp_path):
     for i, p in enumerate(pages):
         got = pnm_read(str(tmp_path / ("out_%03d.pgm" % i)))
         assert_same(got, _oracle_out(oracle, opts, p), "pnm job %d" % i)
+
+
+def test_runner_auto_layout(hip, oracle):
+    """sheets=0, streams=0: the runner sizes its batches (the reference's VRAM
+    tiers, image_pipeline.c:237-285): 2 GiB of input + two planes per batch
+    at most 64 sheets, batches until half the free memory, at most 16."""
+    w, h = SMALL
+    opts = oracle.default_options()
+    r = Runner(opts, 0, w, h, A.FMT_GRAY8, devices=(0,), streams=0, host_threads=2)
+    try:
+        per_sheet = ((w + 255) & ~255) * h + 2 * w * h
+        assert r.geometry.capacity == min(64, (2 << 30) // per_sheet)
+        assert 1 <= r.streams <= 16 and r.batch_bytes >= per_sheet * r.geometry.capacity
+        n = 5
+        pages = _pages(n, 70, w, h)
+        host_in = np.stack([p.payload() for p in pages])
+        out = np.zeros((n, h, r.out_linesize), np.uint8)
+        failed, err = r.run_host(n, source_memory(host_in.ctypes.data, w, w * h, n, keep=host_in),
+                                 sink_memory(out.ctypes.data, r.out_linesize, r.out_linesize * h,
+                                             n, keep=out))
+        assert failed == 0, err
+    finally:
+        r.close()
+    for i, p in enumerate(pages):
+        exp = _oracle_out(oracle, opts, p)
+        assert_same(HostImage(w, h, exp.format, out[i]), exp, "auto layout job %d" % i)
+    # a C4-sized RGB24 sheet pair gets few sheets per batch
+    big = Runner(c4_options(oracle.default_options()), 0, C4_W, C4_H, A.FMT_RGB24, devices=(0,),
+                 streams=2)
+    try:
+        per_sheet = ((C4_W * 3 + 255) & ~255) * C4_H + 2 * 3 * C4_W * C4_H
+        assert big.geometry.capacity == max(1, min(64, (2 << 30) // per_sheet))
+        assert big.streams == 2
+    finally:
+        big.close()
 
 
 @pytest.mark.parametrize("names,fmt,out_ext", [

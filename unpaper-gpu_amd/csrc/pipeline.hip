@@ -376,6 +376,7 @@ struct UphipBatch {
   int device = 0;
   hipStream_t st = nullptr;
   int cap = 0, n_in = 1;
+  size_t dev_bytes = 0;                // device memory this batch allocated
   // geometry (host-planned)
   int32_t rp_w = 0, rp_h = 0;          // page after pre_rotate
   int32_t sheet_w = 0, sheet_h = 0;    // after decode
@@ -453,6 +454,7 @@ T* dalloc(UphipBatch* b, size_t n) {
   void* p = nullptr;
   if (!UPH_HIP(hipMalloc(&p, sizeof(T) * (n ? n : 1)))) return nullptr;
   b->allocs.push_back(p);
+  b->dev_bytes += sizeof(T) * (n ? n : 1);
   return (T*)p;
 }
 
@@ -463,6 +465,7 @@ void* upload_cached(UphipBatch* b, const void* host, size_t bytes) {
   void* d = nullptr;
   if (!UPH_HIP(hipMalloc(&d, bytes ? bytes : 1))) return nullptr;
   b->allocs.push_back(d);
+  b->dev_bytes += bytes ? bytes : 1;
   if (host) UPH_HIP(hipMemcpy(d, host, bytes, hipMemcpyHostToDevice));
   b->cache.push_back(d);
   b->cache_pos++;
@@ -1481,6 +1484,12 @@ int uphip_batch_output_info(UphipBatch* b, int32_t* width, int32_t* height, int3
   if (height) *height = b->out_h;
   if (format) *format = b->out_fmt;
   if (bytes_per_sheet) *bytes_per_sheet = row_bytes(b->out_w, b->out_fmt) * b->out_h;
+  return 0;
+}
+
+int uphip_batch_device_bytes(UphipBatch* b, int64_t* bytes) {
+  if (!b || !bytes) return fail("batch_device_bytes: null argument"), -1;
+  *bytes = (int64_t)b->dev_bytes;
   return 0;
 }
 

@@ -348,6 +348,7 @@ struct UphipRunner {
   int64_t in_pitch = 0, in_page_stride = 0;   // batch input slot layout (= staging layout)
   int64_t out_linesize = 0, out_sheet_stride = 0;
   bool staged = false;  // pinned staging allocated
+  int64_t batch_bytes = 0;  // device memory of one batch
   UphipRunnerStats stats{};
 };
 
@@ -430,6 +431,21 @@ void collect_failures(Slot& sl) {
   }
 }
 
+// Sheets per batch when the caller leaves it to the runner: the sheet's
+// input pages plus its two working planes (GRAY8 for gray inputs, RGB24
+// otherwise, as the batch plans them) within 2 GiB, at most 64 (the batch
+// size the A4 measurements use) and at least 1.
+int32_t auto_capacity(const UphipOptions& o, const UphipBatchGeometry& g) {
+  const int64_t w = g.page_width, h = g.page_height;
+  const int n_in = o.input_count > 0 ? o.input_count : 1;
+  const bool gray = g.page_format == UPHIP_FMT_GRAY8 || g.page_format == UPHIP_FMT_MONOWHITE ||
+                    g.page_format == UPHIP_FMT_MONOBLACK;
+  const int64_t in = round_pitch(row_bytes((int32_t)w, g.page_format)) * h * n_in;
+  const int64_t plane = (gray ? 1 : 3) * w * n_in * h;
+  const int64_t per_sheet = std::max<int64_t>(in + 2 * plane, 1);
+  return (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, (2ll << 30) / per_sheet));
+}
+
 }  // namespace
 
 extern "C" {
@@ -439,12 +455,13 @@ UphipRunner* uphip_runner_create(const UphipOptions* options, const UphipBatchGe
   if (!options || !geometry || !config) return fail("runner_create: null argument"), nullptr;
   if (!runtime_ready()) return fail("runner_create: no HIP device"), nullptr;
   const int ndev_all = uphip_device_count();
-  if (config->ndevices <= 0 || config->batches_per_device <= 0 || geometry->capacity <= 0)
+  if (config->ndevices <= 0 || geometry->page_width <= 0 || geometry->page_height <= 0)
     return fail("runner_create: invalid configuration"), nullptr;
   UphipRunner* r = new UphipRunner();
   r->opts = *options;
   r->geo = *geometry;
   r->cfg = *config;
+  if (r->geo.capacity <= 0) r->geo.capacity = auto_capacity(*options, *geometry);
   for (int i = 0; i < config->ndevices; i++) {
     const int d = config->devices ? config->devices[i] : i;
     if (d < 0 || d >= ndev_all) {
@@ -463,9 +480,30 @@ UphipRunner* uphip_runner_create(const UphipOptions* options, const UphipBatchGe
       ok = false;
       break;
     }
-    dc.slots.resize((size_t)config->batches_per_device);
+    // the first batch measures the footprint the auto layout divides by
+    if (i == 0) {
+      UphipBatch* b = uphip_batch_create(options, &r->geo);
+      if (!b) {
+        ok = false;
+        break;
+      }
+      int64_t bb = 0;
+      uphip_batch_device_bytes(b, &bb);
+      r->batch_bytes = bb;
+      if (config->batches_per_device <= 0) {
+        size_t fr = 0, tot = 0;
+        int n = 1;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && bb > 0)
+          n = 1 + (int)std::min<int64_t>((int64_t)(fr / 2) / bb, 15);
+        r->cfg.batches_per_device = n;
+      }
+      dc.slots.resize((size_t)r->cfg.batches_per_device);
+      dc.slots[0].b = b;
+    } else {
+      dc.slots.resize((size_t)r->cfg.batches_per_device);
+    }
     for (Slot& sl : dc.slots) {
-      sl.b = uphip_batch_create(options, geometry);
+      if (!sl.b) sl.b = uphip_batch_create(options, &r->geo);
       if (!sl.b) {
         ok = false;
         break;
@@ -482,7 +520,7 @@ UphipRunner* uphip_runner_create(const UphipOptions* options, const UphipBatchGe
   int64_t bytes = 0;
   uphip_batch_output_info(b0, &r->out_w, &r->out_h, &r->out_fmt, &bytes);
   uphip_batch_input_ptr(b0, 0, &r->in_pitch);
-  r->in_page_stride = r->in_pitch * geometry->page_height;
+  r->in_page_stride = r->in_pitch * r->geo.page_height;
   // output staging laid out like the batch's output rows, so a batch's
   // sheets come back as linear DMA copies
   {
@@ -511,6 +549,15 @@ void uphip_runner_destroy(UphipRunner* r) {
     }
   }
   delete r;
+}
+
+int uphip_runner_layout(UphipRunner* r, int32_t* batches_per_device, int32_t* capacity,
+                        int64_t* batch_bytes) {
+  if (!r) return fail("runner_layout: null runner"), -1;
+  if (batches_per_device) *batches_per_device = r->cfg.batches_per_device;
+  if (capacity) *capacity = r->geo.capacity;
+  if (batch_bytes) *batch_bytes = r->batch_bytes;
+  return 0;
 }
 
 UphipBatch* uphip_runner_batch(UphipRunner* r, int32_t device_index, int32_t slot) {

@@ -50,7 +50,7 @@ EXPORTED = [
     "uphip_sink_callback", "uphip_sink_memory", "uphip_sink_pnm", "uphip_sink_discard",
     "uphip_sink_destroy", "uphip_runner_create", "uphip_runner_destroy",
     "uphip_runner_run_device", "uphip_runner_run_host", "uphip_runner_get_stats",
-    "uphip_runner_output_info", "uphip_runner_batch", "uphip_host_alloc", "uphip_host_free",
+    "uphip_runner_output_info", "uphip_runner_batch", "uphip_runner_layout", "uphip_batch_device_bytes", "uphip_host_alloc", "uphip_host_free",
 ]
 
 
@@ -169,6 +169,9 @@ def load_library(path=LIB_PATH):
         "uphip_runner_run_device": (C.c_int, [C.c_void_p, C.POINTER(A.DevicePages), C.c_int32]),
         "uphip_runner_run_host": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]),
         "uphip_runner_get_stats": (C.c_int, [C.c_void_p, C.POINTER(A.RunnerStats)]),
+        "uphip_runner_layout": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                          C.POINTER(C.c_int64)]),
+        "uphip_batch_device_bytes": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
         "uphip_runner_output_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32),
                                                C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                                C.POINTER(C.c_int64)]),

@@ -153,7 +153,9 @@ class HostBuffer:
 class Runner:
     """Multi-device runner (uphip_runner_*): the peer of lib/batch_worker.c's
     batch_process_parallel with one host thread and `streams` batches of
-    `sheets` sheets per device; sources/sinks are the decode/encode queues."""
+    `sheets` sheets per device; sources/sinks are the decode/encode queues.
+    sheets=0 / streams=0: the runner sizes them from the geometry and the
+    device's free memory (uphip_runner_layout reports the choice)."""
 
     def __init__(self, options, sheets, page_width, page_height, page_format, devices=(0,),
                  streams=4, host_threads=0, timing=False):
@@ -174,6 +176,10 @@ class Runner:
         L.uphip_runner_output_info(self.handle, C.byref(w), C.byref(h), C.byref(f), C.byref(ls))
         self.out_width, self.out_height, self.out_format = w.value, h.value, f.value
         self.out_linesize = ls.value
+        k, cap, bb = C.c_int32(), C.c_int32(), C.c_int64()
+        L.uphip_runner_layout(self.handle, C.byref(k), C.byref(cap), C.byref(bb))
+        self.streams, self.batch_bytes = k.value, bb.value
+        self.geometry.capacity = cap.value
 
     def batch(self, device_index, slot):
         """The Batch object behind one stream (borrowed; not closed here)."""
