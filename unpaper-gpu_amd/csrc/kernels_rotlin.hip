@@ -57,6 +57,7 @@ __device__ __forceinline__ float lin1(float xm, float x, float a, float b) {
 // In-mask part of a tile for one mask, in mask coordinates; false when empty.
 struct MaskPart {
   int32_t cu0, cu1, cv0, cv1;
+  bool full;  // every pixel of the tile lies in the mask
 };
 __device__ __forceinline__ bool mask_part(const RotateArgs& a, int32_t tx0, int32_t ty0, int32_t W,
                                           int32_t H, MaskPart* mp) {
@@ -68,6 +69,7 @@ __device__ __forceinline__ bool mask_part(const RotateArgs& a, int32_t tx0, int3
   mp->cu1 = imin(u1, sw - 1);
   mp->cv0 = imax(v0, 0);
   mp->cv1 = imin(v1, sh - 1);
+  mp->full = mp->cu0 == u0 && mp->cu1 == u1 && mp->cv0 == v0 && mp->cv1 == v1;
   return mp->cu0 <= mp->cu1 && mp->cv0 <= mp->cv1;
 }
 
@@ -128,8 +130,9 @@ __global__ void __launch_bounds__(kLT) k_rotate_lin(PlaneRef src, PlaneRef dst, 
   const int32_t plane_f = win.rows * win.stride;            // words per window
   uint32_t* lwu = reinterpret_cast<uint32_t*>(lw);
   uint8_t* obuf = reinterpret_cast<uint8_t*>(lw + plane_f);  // kLH x kRowB bytes
-  // 1. the tile's source bytes (kept where no mask rotates)
-  {
+  // 1. the tile's source bytes (kept where no mask rotates); a tile wholly
+  // inside one rotating mask is overwritten pixel by pixel and skips this
+  if (!((hit[0] && mp[0].full) || (hit[1] && mp[1].full))) {
     constexpr int NV = kRowB / 16;
     for (int i = tid; i < th * NV; i += kLT) {
       const int r = i / NV, j = i - r * NV;
@@ -290,15 +293,27 @@ __global__ void __launch_bounds__(kLT) k_rotate_lin(PlaneRef src, PlaneRef dst, 
           // one ds_read2_b32 per tap row: pixels (x1, x2) as rgb words
           const uint32_t* q = lwu + i11;
           const uint32_t w11 = q[0], w21 = q[1], w12 = q[win.stride], w22 = q[win.stride + 1];
-#pragma unroll
-          for (int c = 0; c < 3; c++) {
-            const lf2 top{(float)((w11 >> (8 * c)) & 0xFFu), (float)((w21 >> (8 * c)) & 0xFFu)};
-            const lf2 bot{(float)((w12 >> (8 * c)) & 0xFFu), (float)((w22 >> (8 * c)) & 0xFFu)};
-            const lf2 t = FX * top, b = FX * bot;
-            const lf2 h{__builtin_truncf(t.x + t.y), __builtin_truncf(b.x + b.y)};
-            const lf2 f = FY * h;
-            o[c] = plain ? (uint8_t)(w11 >> (8 * c)) : (uint8_t)(uint32_t)__builtin_truncf(f.x + f.y);
-          }
+          // red and green as packed pairs across the channels, blue as the
+          // (x1, x2) pair; branch-free, the plain case selected at the end
+          const lf2 FX0{FX.x, FX.x}, FX1{FX.y, FX.y}, FY0{FY.x, FY.x}, FY1{FY.y, FY.y};
+          const lf2 rg11{ubyte_f<0>(w11), ubyte_f<1>(w11)}, rg21{ubyte_f<0>(w21), ubyte_f<1>(w21)};
+          const lf2 rg12{ubyte_f<0>(w12), ubyte_f<1>(w12)}, rg22{ubyte_f<0>(w22), ubyte_f<1>(w22)};
+          const lf2 st = FX0 * rg11 + FX1 * rg21, sb = FX0 * rg12 + FX1 * rg22;
+          const lf2 ht{__builtin_truncf(st.x), __builtin_truncf(st.y)};
+          const lf2 hb{__builtin_truncf(sb.x), __builtin_truncf(sb.y)};
+          const lf2 sv = FY0 * ht + FY1 * hb;
+          const lf2 tb = FX * lf2{ubyte_f<2>(w11), ubyte_f<2>(w21)};
+          const lf2 bb = FX * lf2{ubyte_f<2>(w12), ubyte_f<2>(w22)};
+          const lf2 hbl{__builtin_truncf(tb.x + tb.y), __builtin_truncf(bb.x + bb.y)};
+          const lf2 fb = FY * hbl;
+          // integral values: the byte conversion's rounding is exact
+          uint32_t px = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_truncf(sv.x), 0, 0u);
+          px = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_truncf(sv.y), 1, px);
+          px = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_truncf(fb.x + fb.y), 2, px);
+          if (plain) px = w11;
+          o[0] = (uint8_t)px;
+          o[1] = (uint8_t)(px >> 8);
+          o[2] = (uint8_t)(px >> 16);
         } else {
           const float* q = lw + i11;
           const lf2 top{q[0], q[1]}, bot{q[win.stride], q[win.stride + 1]};
