@@ -576,6 +576,191 @@ __global__ void __launch_bounds__(256) k_blur_resolve(BlurGeom g, uint8_t* scrat
   }
 }
 
+// The same recurrence on the scalar unit, one wave per sheet, for rows of at
+// most 56 blocks.  All three pointers of blurfilter_cpu index one array A
+// (prev, cur, next at offsets op, oc, on, a rotation of 0, 1, 2), so block k
+// of a row reads and writes only A[k-1 .. k+3]: that window lives in scalar
+// registers and slides one entry a block.  A itself is one VGPR (lane j holds
+// A[j]): the entry leaving the window is written into its lane, the one
+// entering (untouched so far in this row) read from its lane; the row's
+// counts are a second VGPR.  No memory access inside a row.  With the row's
+// rotation the reads are
+//   (0,1,2): next[k+1] = A[k+3]; the rest A[k-1], A[k+1] (three times); wipe A[k+1]
+//   (1,2,0): next[k+1] = A[k+1]; A[k], A[k+2] (twice), A[k-1];          wipe A[k+2]
+//   (2,0,1): next[k+1] = A[k+2]; A[k+1], A[k+3], A[k] (twice);          wipe A[k]
+// and the float test ((float)max / total <= intensity) is monotone in max, so
+// it is the integer compare max <= tmax with tmax found once per sheet.
+constexpr int kBlurLanesMax = 56;  // bpr + 8 lanes of A
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t lane_get(uint32_t v, int32_t l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int32_t)v, l);
+}
+__device__ __forceinline__ uint32_t lane_set(uint32_t v, uint32_t x, int32_t l) {
+  return (int32_t)(threadIdx.x & 63) == l ? x : v;
+}
+
+// one row of type OP: blocks 1 .. bpr; returns the row's wipe bits (bit k-1)
+template <int OP>
+__device__ __forceinline__ uint64_t blur_row(uint32_t& Av, uint32_t rowv, int32_t bpr,
+                                             uint32_t total, int32_t tmax) {
+  constexpr int ON = OP == 0 ? 2 : OP == 1 ? 0 : 1;
+  uint32_t W0 = lane_get(Av, 0), W1 = lane_get(Av, 1), W2 = lane_get(Av, 2);
+  uint32_t W3 = lane_get(Av, 3), W4 = lane_get(Av, 4);
+  const uint32_t n0 = lane_get(rowv, 0);  // next[0] = A[on]
+  if (ON == 0) W0 = n0;
+  else if (ON == 1) W1 = n0;
+  else W2 = n0;
+  uint64_t wipes = 0;
+#pragma unroll 4
+  for (int32_t k = 1;; k++) {
+    const uint32_t e = lane_get(rowv, k);
+    uint32_t mx;
+    bool w;
+    if (OP == 0) {
+      W4 = e;
+      mx = umax(W0, umax(W2, W4));
+      w = (int32_t)mx <= tmax;
+      W2 = w ? total : W2;
+    } else if (OP == 1) {
+      W2 = e;
+      mx = umax(umax(W0, W1), umax(W2, W3));
+      w = (int32_t)mx <= tmax;
+      W3 = w ? total : W3;
+    } else {
+      W3 = e;
+      mx = umax(umax(W1, W2), umax(W3, W4));
+      w = (int32_t)mx <= tmax;
+      W1 = w ? total : W1;
+    }
+    wipes |= (uint64_t)w << (k - 1);
+    if (k == bpr) break;
+    Av = lane_set(Av, W0, k - 1);
+    W0 = W1;
+    W1 = W2;
+    W2 = W3;
+    W3 = W4;
+    W4 = lane_get(Av, k + 4);
+  }
+  Av = lane_set(Av, W0, bpr - 1);
+  Av = lane_set(Av, W1, bpr);
+  Av = lane_set(Av, W2, bpr + 1);
+  Av = lane_set(Av, W3, bpr + 2);
+  Av = lane_set(Av, W4, bpr + 3);
+  return wipes;
+}
+
+// The same row for a row length known at compile time: the whole row's A in
+// scalar registers (read from its lanes once, written back once), every
+// block a handful of scalar operations.
+template <int OP, int BPR>
+__device__ __forceinline__ uint64_t blur_row_fixed(uint32_t& Av, uint32_t rowv, uint32_t total,
+                                                   int32_t tmax) {
+  constexpr int ON = OP == 0 ? 2 : OP == 1 ? 0 : 1;
+  uint32_t a[BPR + 4];
+#pragma unroll
+  for (int j = 0; j < BPR + 4; j++) a[j] = lane_get(Av, j);
+  a[ON] = lane_get(rowv, 0);  // next[0]
+  uint64_t wipes = 0;
+#pragma unroll
+  for (int k = 1; k <= BPR; k++) {
+    const uint32_t e = lane_get(rowv, k);
+    uint32_t mx;
+    if (OP == 0) {
+      a[k + 3] = e;
+      mx = umax(a[k - 1], umax(a[k + 1], a[k + 3]));
+    } else if (OP == 1) {
+      a[k + 1] = e;
+      mx = umax(umax(a[k - 1], a[k]), umax(a[k + 1], a[k + 2]));
+    } else {
+      a[k + 2] = e;
+      mx = umax(umax(a[k], a[k + 1]), umax(a[k + 2], a[k + 3]));
+    }
+    const bool w = (int32_t)mx <= tmax;
+    if (OP == 0) a[k + 1] = w ? total : a[k + 1];
+    else if (OP == 1) a[k + 2] = w ? total : a[k + 2];
+    else a[k] = w ? total : a[k];
+    wipes |= (uint64_t)w << (k - 1);
+  }
+#pragma unroll
+  for (int j = 0; j < BPR + 4; j++) Av = lane_set(Av, a[j], j);
+  return wipes;
+}
+
+template <int BPR>
+__device__ __forceinline__ void blur_rows_fixed(uint32_t Av, const uint32_t* counts, uint8_t* wipe,
+                                                int32_t T, uint32_t total, int32_t tmax) {
+  const int lane = threadIdx.x & 63;
+  constexpr int32_t rl = BPR + 1;
+  uint32_t rowv = T > 0 && lane < rl ? counts[BPR + lane] : 0;
+  for (int32_t t = 0; t < T; t++) {
+    const uint32_t cur = rowv;
+    if (t + 1 < T) rowv = lane < rl ? counts[BPR + (t + 1) * rl + lane] : 0;
+    const int op = t % 3;
+    const uint64_t wipes = op == 0   ? blur_row_fixed<0, BPR>(Av, cur, total, tmax)
+                           : op == 1 ? blur_row_fixed<1, BPR>(Av, cur, total, tmax)
+                                     : blur_row_fixed<2, BPR>(Av, cur, total, tmax);
+    if (lane < BPR) wipe[t * BPR + lane] = (uint8_t)((wipes >> lane) & 1);
+  }
+}
+
+__global__ void __launch_bounds__(64) k_blur_resolve_w(BlurGeom g, uint8_t* scratch,
+                                                       int64_t sstride, const int32_t* active) {
+  const int s = blockIdx.x;
+  if (active && !active[s]) return;
+  const uint32_t* counts = (const uint32_t*)(scratch + s * sstride);
+  uint8_t* wipe = scratch + s * sstride + (size_t)g.nrect * 4;
+  const int lane = threadIdx.x;
+  const int32_t bpr = g.bpr;
+  const uint32_t total = (uint32_t)(g.sw * g.sh);
+  // blurfilter_cpu's set-up (A zero where the reference reads uninitialised
+  // stack, as the other resolver): cur[0], cur[bpr], next[0], next[bpr], then
+  // cur[1 .. bpr] = the first row's counts (A[2] and A[bpr + 1] overwritten)
+  uint32_t Av = 0;
+  if (lane == 1 || lane == bpr + 1 || lane == 2 || lane == bpr + 2) Av = total;
+  if (lane >= 2 && lane < 2 + bpr) Av = counts[lane - 2];
+  // the largest max that is wiped (-1: none)
+  auto wiped = [&](uint32_t m) { return ((float)m) / (float)(uint64_t)total <= g.intensity; };
+  int32_t tmax = -1;
+  if (wiped(0u)) {
+    uint32_t lo = 0, hi = total;
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo + 1) / 2;
+      if (wiped(mid)) lo = mid;
+      else hi = mid - 1;
+    }
+    tmax = (int32_t)lo;
+  }
+  tmax = __builtin_amdgcn_readfirstlane(tmax);
+  // row lengths of 150-400 dpi pages at the default 100-pixel blocks
+  switch (bpr) {
+#define UPH_BLUR_FIXED(n) \
+  case n:                 \
+    blur_rows_fixed<n>(Av, counts, wipe, g.T, total, tmax); \
+    return;
+    UPH_BLUR_FIXED(12) UPH_BLUR_FIXED(13) UPH_BLUR_FIXED(14) UPH_BLUR_FIXED(15)
+    UPH_BLUR_FIXED(16) UPH_BLUR_FIXED(17) UPH_BLUR_FIXED(18) UPH_BLUR_FIXED(19)
+    UPH_BLUR_FIXED(20) UPH_BLUR_FIXED(21) UPH_BLUR_FIXED(22) UPH_BLUR_FIXED(23)
+    UPH_BLUR_FIXED(24) UPH_BLUR_FIXED(25) UPH_BLUR_FIXED(26) UPH_BLUR_FIXED(27)
+    UPH_BLUR_FIXED(28) UPH_BLUR_FIXED(29) UPH_BLUR_FIXED(30) UPH_BLUR_FIXED(31)
+    UPH_BLUR_FIXED(32)
+#undef UPH_BLUR_FIXED
+    default:
+      break;
+  }
+  // the next row's counts one row ahead
+  const int32_t rl = bpr + 1;
+  uint32_t rowv = g.T > 0 && lane < rl ? counts[bpr + lane] : 0;
+  for (int32_t t = 0; t < g.T; t++) {
+    const uint32_t cur = rowv;
+    if (t + 1 < g.T) rowv = lane < rl ? counts[bpr + (t + 1) * rl + lane] : 0;
+    const int op = t % 3;
+    const uint64_t wipes = op == 0   ? blur_row<0>(Av, cur, bpr, total, tmax)
+                           : op == 1 ? blur_row<1>(Av, cur, bpr, total, tmax)
+                                     : blur_row<2>(Av, cur, bpr, total, tmax);
+    if (lane < bpr) wipe[t * bpr + lane] = (uint8_t)((wipes >> lane) & 1);
+  }
+}
+
 template <int FMT>
 __global__ void __launch_bounds__(256) k_blur_wipe(PlaneRef img, BlurGeom g, uint8_t* scratch,
                                                    int64_t sstride, const int32_t* active) {
@@ -606,7 +791,13 @@ static void launch_blur_t(const PlaneRef& img, const BlurGeom& g, uint8_t* scr, 
     hipLaunchKernelGGL(k_blur_counts<FMT>, dim3(g.nrect, count), dim3(256), 0, st, img, g, scr, ss,
                        active);
   const size_t lds = sizeof(uint64_t) * ((size_t)g.nrect + 3 * (size_t)(g.bpr + 2));
-  if (!(diag_skip() & 8)) hipLaunchKernelGGL(k_blur_resolve, dim3(count), dim3(256), lds, st, g, scr, ss, active);
+  const bool scalar = g.bpr >= 1 && g.bpr + 8 <= kBlurLanesMax && (int64_t)g.sw * g.sh < (1ll << 31);
+  if (diag_skip() & 8) {
+  } else if (scalar) {
+    hipLaunchKernelGGL(k_blur_resolve_w, dim3(count), dim3(64), 0, st, g, scr, ss, active);
+  } else {
+    hipLaunchKernelGGL(k_blur_resolve, dim3(count), dim3(256), lds, st, g, scr, ss, active);
+  }
   if (g.T * g.bpr > 0)
     hipLaunchKernelGGL(k_blur_wipe<FMT>, dim3(g.T * g.bpr, count), dim3(256), 0, st, img, g, scr,
                        ss, active);
