@@ -1,15 +1,9 @@
 #!/bin/bash
-# noisefilter parity (filters + pipeline + bench hashes), then the classify
-# kernel's time in a 1-stream C3 trace, then the default bench line
-set -o pipefail
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-out=gpurun_out/nchk; rm -rf $out; mkdir -p $out
-timeout -k 10 500 python3 -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
-  -k "noise or bench or c4 or pipeline" > $out/t.log 2>&1 || { tail -30 $out/t.log; exit 1; }
-tail -1 $out/t.log
-timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d $out/tr -- python3 bench.py --no-cpu --no-host-io --no-latency --no-verify --no-c4 --pages 128 --steps 1 --warmup 0 --streams 1 --probe 0 > $out/tr.log 2>&1 || { tail -5 $out/tr.log; exit 1; }
-python3 profiles/summarize.py $out/tr 2 | grep -E "noise|pipeline kernels"
-timeout -k 10 300 python3 bench.py --no-cpu --no-host-io --no-latency > $out/b.json 2> $out/b.err || { tail $out/b.err; exit 1; }
-python3 -c "
-import json; d=json.loads(open('$out/b.json').read().strip().splitlines()[-1]); c=d['c4']
-print('C3', d['value'], d['verified'], d['mismatches'], 'C4', c['value'], c['verified'], c['mismatches'], 'C4 noise ms', c['latency_stages_ms']['noisefilter'])"
+# noisefilter parity tests, the resolve phases (tuning build), and kernel durations
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
+  -k "${1:-noise or golden or A1 or C1 or E1 or bench_configuration}" > gpurun_out/noise_t.log 2>&1 || { tail -30 gpurun_out/noise_t.log; exit 1; }
+tail -1 gpurun_out/noise_t.log
+bash tools/noise_diag.sh | head -4
+bash tools/blur_prof.sh | grep noise_resolve

@@ -1627,9 +1627,15 @@ __global__ void __launch_bounds__(256) k_noise_apply(PlaneRef img, NoiseGeom g, 
 }
 
 // In-LDS / in-global bitonic sort of n uint32 keys by one 256-thread block.
+// Bitonic sort of a[0 .. n_pow2) in LDS by the whole block (blockDim.x a
+// multiple of 64).  Steps whose partners lie 64 or more apart go through LDS
+// with a block barrier each; the steps below 64 of a merge run in registers
+// (partners in the same wave: element i belongs to lane i % 64 of one wave),
+// with one barrier per merge instead of one per step.
 __device__ void block_sort(uint32_t* a, int n_pow2) {
   for (int k = 2; k <= n_pow2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
+    int j = k >> 1;
+    for (; j >= 64; j >>= 1) {
       for (int i = threadIdx.x; i < n_pow2; i += blockDim.x) {
         const int l = i ^ j;
         if (l > i) {
@@ -1644,6 +1650,18 @@ __device__ void block_sort(uint32_t* a, int n_pow2) {
       __threadfence_block();
       __syncthreads();
     }
+    for (int i = threadIdx.x; i < n_pow2; i += blockDim.x) {
+      uint32_t x = a[i];
+      const bool up = (i & k) == 0;
+      for (int jj = j; jj > 0; jj >>= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)x, jj, 64);
+        const bool lower = (i & jj) == 0;  // keeps the smaller one when sorting up
+        x = lower == up ? (x < y ? x : y) : (x < y ? y : x);
+      }
+      a[i] = x;
+    }
+    __threadfence_block();
+    __syncthreads();
   }
 }
 
@@ -1794,7 +1812,11 @@ __device__ __forceinline__ void uf_union(uint32_t* parent, uint32_t a, uint32_t 
 //   aux:  p2 entries of scratch (parents, then (root << 16 | index) pairs).
 template <int FMT>
 __device__ void noise_resolve_components(const uint32_t* keys, uint32_t* aux, int n, int p2, int N,
-                                         const NoiseGeom& g, uint8_t* base, int64_t pitch) {
+                                         const NoiseGeom& g, uint8_t* base, int64_t pitch
+#ifdef UPHIP_DIAG
+                                         , uint64_t* ph, int* maxrun
+#endif
+                                         ) {
   const int R = 2 * N - 1;  // dependence radius
   for (int i = threadIdx.x; i < n; i += blockDim.x) aux[i] = (uint32_t)i;
   __syncthreads();
@@ -1816,6 +1838,9 @@ __device__ void noise_resolve_components(const uint32_t* keys, uint32_t* aux, in
     }
   }
   __syncthreads();
+#ifdef UPHIP_DIAG
+  ph[0] = wall_clock64();
+#endif
   // flatten (a concurrent reader sees either an old parent or the root: both
   // ancestors), then (root, index) pairs sorted so that each component's
   // triggers are contiguous and in raster order
@@ -1825,6 +1850,10 @@ __device__ void noise_resolve_components(const uint32_t* keys, uint32_t* aux, in
   __threadfence_block();
   __syncthreads();
   block_sort(aux, p2);
+#ifdef UPHIP_DIAG
+  ph[1] = wall_clock64();
+  int run = 0;
+#endif
   Mask81 rowp[5], colp[5];
 #pragma unroll
   for (int L = 1; L <= 4; L++) {
@@ -1842,8 +1871,14 @@ __device__ void noise_resolve_components(const uint32_t* keys, uint32_t* aux, in
       __threadfence_block();  // this thread's earlier clears are visible to its loads
       replay_trigger4<FMT>((int32_t)(key & 0xFFFF), (int32_t)(key >> 16), N, g, base, pitch, rowp,
                            colp);
+#ifdef UPHIP_DIAG
+      run++;
+#endif
     }
   }
+#ifdef UPHIP_DIAG
+  *maxrun = run;
+#endif
 }
 
 constexpr int kCompCap = 16384;  // triggers the component replay keeps in LDS
@@ -1883,18 +1918,30 @@ __global__ void __launch_bounds__(kResolveThreads) k_noise_resolve(PlaneRef img,
   __syncthreads();
   block_sort(keys, p2);
 #ifdef UPHIP_DIAG
-  if ((g.diag & 8) && threadIdx.x == 0)
-    printf("uphip noise: sheet %d sort %llu ticks\n", s, (unsigned long long)(wall_clock64() - t_start));
+  const uint64_t t_sorted = wall_clock64();
 #endif
   const int N = g.intensity;
   uint8_t* base = plane_ptr(img, s);
   const int64_t pitch = img.P.pitch;
   if (N <= 4 && p2 <= kCompCap) {
-    noise_resolve_components<FMT>(keys, nlds + kCompCap, (int)n, p2, N, g, base, pitch);
 #ifdef UPHIP_DIAG
+    uint64_t ph[3];
+    int maxrun = 0;
+    noise_resolve_components<FMT>(keys, nlds + kCompCap, (int)n, p2, N, g, base, pitch, ph, &maxrun);
+    __syncthreads();
+    const uint64_t t_end = wall_clock64();
+    // the longest run of replayed triggers of one thread
+    __shared__ int mr;
+    if (threadIdx.x == 0) mr = 0;
+    __syncthreads();
+    atomicMax(&mr, maxrun);
+    __syncthreads();
     if ((g.diag & 8) && threadIdx.x == 0)
-      printf("uphip noise: sheet %d replay done %llu ticks\n", s,
-             (unsigned long long)(wall_clock64() - t_start));
+      printf("uphip noise: sheet %d n %u sort %llu link %llu sort2 %llu replay %llu ticks, longest run %d\n",
+             s, n, (unsigned long long)(t_sorted - t_start), (unsigned long long)(ph[0] - t_sorted),
+             (unsigned long long)(ph[1] - ph[0]), (unsigned long long)(t_end - ph[1]), mr);
+#else
+    noise_resolve_components<FMT>(keys, nlds + kCompCap, (int)n, p2, N, g, base, pitch);
 #endif
     return;
   }
