@@ -1724,16 +1724,46 @@ __device__ __forceinline__ void replay_trigger4(int32_t x, int32_t y, int N, con
   uint64_t dlo = 0;
   uint32_t dhi = 0;
   bool ctr = false;
+  if constexpr (FMT == F_GRAY8) {
+    // a box row as three aligned dwords (rows are pitched in whole dwords,
+    // so clamped addresses stay inside the row): 27 loads instead of 81
+    const int32_t c0 = x - 4;
+    const int32_t d0 = c0 >= 0 ? (c0 & ~3) : -(((-c0) + 3) & ~3);  // floor to a multiple of 4
+    const int32_t dmax = (int32_t)pitch - 4;
+    uint32_t w[9][3];
 #pragma unroll
-  for (int p = 0; p < 81; p++) {  // unconditional clamped loads: one round trip
-    const int32_t qx = x + p % 9 - 4, qy = y + p / 9 - 4;
-    const bool in = (qx >= 0) & (qy >= 0) & (qx < g.W) & (qy < g.H);
-    const Px q = load_px_row<FMT>(base + (int64_t)imin(imax(qy, 0), g.H - 1) * pitch,
-                                  imin(imax(qx, 0), g.W - 1));
-    const bool dk = in & (light_of(q) < g.white);
-    if (p < 64) dlo |= (uint64_t)dk << p;
-    else dhi |= (uint32_t)dk << (p - 64);
-    if (p == 40) ctr = dark_of(q) < g.white;
+    for (int r = 0; r < 9; r++) {
+      const uint8_t* row = base + (int64_t)imin(imax(y + r - 4, 0), g.H - 1) * pitch;
+#pragma unroll
+      for (int j = 0; j < 3; j++)
+        w[r][j] = *reinterpret_cast<const uint32_t*>(row + imin(imax(d0 + 4 * j, 0), dmax));
+    }
+    const int o = c0 - d0;  // 0 .. 3
+#pragma unroll
+    for (int p = 0; p < 81; p++) {
+      const int r = p / 9, c = p % 9;
+      const int32_t qx = c0 + c, qy = y + r - 4;
+      const bool in = (qx >= 0) & (qy >= 0) & (qx < g.W) & (qy < g.H);
+      const int b = o + c;  // byte of the row's 12
+      const uint32_t wd = b < 4 ? w[r][0] : b < 8 ? w[r][1] : w[r][2];
+      const uint32_t v = (wd >> (8 * (b & 3))) & 0xFFu;
+      const bool dk = in & (v < g.white);
+      if (p < 64) dlo |= (uint64_t)dk << p;
+      else dhi |= (uint32_t)dk << (p - 64);
+      if (p == 40) ctr = v < g.white;
+    }
+  } else {
+#pragma unroll
+    for (int p = 0; p < 81; p++) {  // unconditional clamped loads: one round trip
+      const int32_t qx = x + p % 9 - 4, qy = y + p / 9 - 4;
+      const bool in = (qx >= 0) & (qy >= 0) & (qx < g.W) & (qy < g.H);
+      const Px q = load_px_row<FMT>(base + (int64_t)imin(imax(qy, 0), g.H - 1) * pitch,
+                                    imin(imax(qx, 0), g.W - 1));
+      const bool dk = in & (light_of(q) < g.white);
+      if (p < 64) dlo |= (uint64_t)dk << p;
+      else dhi |= (uint32_t)dk << (p - 64);
+      if (p == 40) ctr = dark_of(q) < g.white;
+    }
   }
   if (!ctr) return;  // cleared meanwhile
   Mask81 mem[5];
@@ -1820,21 +1850,22 @@ __device__ void noise_resolve_components(const uint32_t* keys, uint32_t* aux, in
   const int R = 2 * N - 1;  // dependence radius
   for (int i = threadIdx.x; i < n; i += blockDim.x) aux[i] = (uint32_t)i;
   __syncthreads();
-  // link every trigger to the earlier ones within R: per row of the window
-  // [y-R, y] a binary search in the sorted keys, then a short scan
+  // link every trigger to the earlier ones within R: one binary search for
+  // the first trigger of row y-R in the sorted keys, then a scan of the
+  // band's earlier triggers (rows y-R .. y, raster order) for |dx| <= R
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const uint32_t key = keys[i];
     const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
-    for (int yy = imax(y - R, 0); yy <= y; yy++) {
-      const uint32_t lo = ((uint32_t)yy << 16) | (uint32_t)imax(x - R, 0);
-      const uint32_t hi = ((uint32_t)yy << 16) | (uint32_t)(x + R);
-      int a = 0, b = i;  // first index in [0, i) with keys >= lo
-      while (a < b) {
-        const int mid = (a + b) >> 1;
-        if (keys[mid] < lo) a = mid + 1;
-        else b = mid;
-      }
-      for (int j = a; j < i && keys[j] <= hi; j++) uf_union(aux, (uint32_t)i, (uint32_t)j);
+    const uint32_t lo = (uint32_t)imax(y - R, 0) << 16;
+    int a = 0, b = i;  // first index in [0, i) with keys >= lo
+    while (a < b) {
+      const int mid = (a + b) >> 1;
+      if (keys[mid] < lo) a = mid + 1;
+      else b = mid;
+    }
+    for (int j = a; j < i; j++) {
+      const int32_t xj = (int32_t)(keys[j] & 0xFFFF);
+      if (xj >= x - R && xj <= x + R) uf_union(aux, (uint32_t)i, (uint32_t)j);
     }
   }
   __syncthreads();
