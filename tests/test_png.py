@@ -233,10 +233,13 @@ def test_expect_mismatch_and_dispatch(tmp_path):
     wrong = AB.PnmInfo(8, 6, AB.FMT_RGB24)
     buf = np.zeros((6, 64), dtype=np.uint8)
     assert L.uphip_png_read(str(p).encode(), buf.ctypes.data, 64, C.byref(wrong)) != 0
+    L.uphip_clear_error()
     assert L.uphip_png_read(str(p).encode(), buf.ctypes.data, 4, None) != 0  # linesize too small
+    L.uphip_clear_error()
     # image_* picks the codec by signature: a PGM through the same entry point
     q = tmp_path / "g.pgm"
     pnm_write(str(q), HostImage.from_array(s[:, :, 0].astype(np.uint8), AB.FMT_GRAY8))
     a, b = image_read(str(p)), image_read(str(q))
     assert np.array_equal(a.payload(), b.payload())
     assert L.uphip_image_probe(b"/nonexistent.png", C.byref(info)) != 0
+    L.uphip_clear_error()
