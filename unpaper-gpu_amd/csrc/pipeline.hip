@@ -222,14 +222,19 @@ struct RotSelectArgs {
 
 // detect_edge_rotation's argmax + detect_rotation_cpu's combination (exact via
 // the host-computed table for <= 2 edges) -> RotateArgs for deskew
-// only (may be null): other sheets get an inactive RotateArgs and keep their ctl
-__global__ void k_rot_select(SheetCtl* ctl, const int32_t* peaks, const RotTable* table,
-                             const RotCombo* combo, RotSelectArgs a, RotateArgs* out,
-                             int count, const int32_t* only) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+// only (may be null): other sheets get an inactive RotateArgs and keep their ctl.
+// One wave per sheet: the lanes scan the angles in strides, then a wave
+// reduction keeps the largest peak and, among equal ones, the first angle --
+// the reference loop's `if (peak > max_peak)` from max_peak = 0 (an edge with
+// no positive peak keeps angle 0).
+__global__ void __launch_bounds__(64) k_rot_select(SheetCtl* ctl, const int32_t* peaks,
+                                                   const RotTable* table, const RotCombo* combo,
+                                                   RotSelectArgs a, RotateArgs* out, int count,
+                                                   const int32_t* only) {
+  const int s = blockIdx.x, lane = threadIdx.x;
   if (s >= count) return;
   if (only && !only[s]) {
-    out[s].active = 0;
+    if (lane == 0) out[s].active = 0;
     return;
   }
   SheetCtl& c = ctl[s];
@@ -238,13 +243,24 @@ __global__ void k_rot_select(SheetCtl* ctl, const int32_t* peaks, const RotTable
   int idx[4] = {0, 0, 0, 0};
   for (int e = 0; e < a.nedges; e++) {
     const int32_t* pk = peaks + (((int64_t)s * a.max_masks + i) * 4 + e) * a.nangles;
-    int max_peak = 0;
-    for (int k = 0; k < a.nangles; k++)
-      if (pk[k] > max_peak) {
-        max_peak = pk[k];
-        idx[e] = k;
+    int best = 0, bi = 0;
+    for (int k = lane; k < a.nangles; k += 64) {
+      const int v = pk[k];
+      if (v > best) {
+        best = v;
+        bi = k;
       }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const int ob = __shfl_xor(best, o, 64), oi = __shfl_xor(bi, o, 64);
+      if (ob > best || (ob == best && oi < bi)) {
+        best = ob;
+        bi = oi;
+      }
+    }
+    idx[e] = best > 0 ? bi : 0;
   }
+  if (lane != 0) return;
   RotCombo r;
   if (a.nedges <= 2) {
     int key = 0;
@@ -1293,7 +1309,7 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
       }
 #endif
       ra.mask_index = i;
-      hipLaunchKernelGGL(k_rot_select, dim3((count + 255) / 256), dim3(256), 0, b->st, b->ctl,
+      hipLaunchKernelGGL(k_rot_select, dim3(count), dim3(64), 0, b->st, b->ctl,
                          b->peaks, b->dtable, b->dcombo, ra, b->rot_args + (int64_t)i * b->cap,
                          count, only);
     };
