@@ -1752,6 +1752,36 @@ __device__ __forceinline__ void replay_trigger4(int32_t x, int32_t y, int N, con
       else dhi |= (uint32_t)dk << (p - 64);
       if (p == 40) ctr = v < g.white;
     }
+  } else if constexpr (FMT == F_RGB24) {
+    // a box row (27 bytes) as eight aligned dwords, realigned to its first
+    // byte: 72 loads instead of 243
+    const int32_t b0 = 3 * (x - 4);
+    const int32_t d0 = b0 >= 0 ? (b0 & ~3) : -(((-b0) + 3) & ~3);
+    const int32_t dmax = (int32_t)pitch - 4;
+    const int o = b0 - d0;  // 0 .. 3
+#pragma unroll
+    for (int r = 0; r < 9; r++) {
+      const uint8_t* row = base + (int64_t)imin(imax(y + r - 4, 0), g.H - 1) * pitch;
+      uint32_t w[8], a[7];
+#pragma unroll
+      for (int j = 0; j < 8; j++)
+        w[j] = *reinterpret_cast<const uint32_t*>(row + imin(imax(d0 + 4 * j, 0), dmax));
+#pragma unroll
+      for (int j = 0; j < 7; j++) a[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], o);
+#pragma unroll
+      for (int c = 0; c < 9; c++) {
+        const int p = 9 * r + c;
+        const int32_t qx = x + c - 4, qy = y + r - 4;
+        const bool in = (qx >= 0) & (qy >= 0) & (qx < g.W) & (qy < g.H);
+        const int k = 3 * c;  // the pixel's first byte in the realigned row
+        const Px q{(uint8_t)(a[k >> 2] >> (8 * (k & 3))), (uint8_t)(a[(k + 1) >> 2] >> (8 * ((k + 1) & 3))),
+                   (uint8_t)(a[(k + 2) >> 2] >> (8 * ((k + 2) & 3)))};
+        const bool dk = in & (light_of(q) < g.white);
+        if (p < 64) dlo |= (uint64_t)dk << p;
+        else dhi |= (uint32_t)dk << (p - 64);
+        if (p == 40) ctr = dark_of(q) < g.white;
+      }
+    }
   } else {
 #pragma unroll
     for (int p = 0; p < 81; p++) {  // unconditional clamped loads: one round trip
