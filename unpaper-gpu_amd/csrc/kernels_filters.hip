@@ -590,7 +590,7 @@ __global__ void __launch_bounds__(256) k_blur_resolve(BlurGeom g, uint8_t* scrat
 //   (2,0,1): next[k+1] = A[k+2]; A[k+1], A[k+3], A[k] (twice);          wipe A[k]
 // and the float test ((float)max / total <= intensity) is monotone in max, so
 // it is the integer compare max <= tmax with tmax found once per sheet.
-constexpr int kBlurLanesMax = 56;  // bpr + 8 lanes of A
+constexpr int kBlurLanesMax = 120;  // bpr + 8 entries of A in two VGPRs
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
 __device__ __forceinline__ uint32_t lane_get(uint32_t v, int32_t l) {
   return (uint32_t)__builtin_amdgcn_readlane((int32_t)v, l);
@@ -600,9 +600,22 @@ __device__ __forceinline__ uint32_t lane_set(uint32_t v, uint32_t x, int32_t l) 
 }
 
 // one row of type OP: blocks 1 .. bpr; returns the row's wipe bits (bit k-1)
+// entries 0 .. 127 of an array over two VGPRs (lane l: entries l and 64 + l)
+struct Lanes2 {
+  uint32_t v0, v1;
+};
+__device__ __forceinline__ uint32_t lane_get(const Lanes2& v, int32_t l) {
+  const uint32_t a = lane_get(v.v0, l & 63), b = lane_get(v.v1, l & 63);
+  return l < 64 ? a : b;
+}
+__device__ __forceinline__ void lane_set(Lanes2& v, uint32_t x, int32_t l) {
+  v.v0 = lane_set(v.v0, x, l);
+  v.v1 = lane_set(v.v1, x, l - 64);
+}
+
 template <int OP>
-__device__ __forceinline__ uint64_t blur_row(uint32_t& Av, uint32_t rowv, int32_t bpr,
-                                             uint32_t total, int32_t tmax) {
+__device__ __forceinline__ void blur_row(Lanes2& Av, Lanes2 rowv, int32_t bpr, uint32_t total,
+                                         int32_t tmax, uint64_t (&wipes)[2]) {
   constexpr int ON = OP == 0 ? 2 : OP == 1 ? 0 : 1;
   uint32_t W0 = lane_get(Av, 0), W1 = lane_get(Av, 1), W2 = lane_get(Av, 2);
   uint32_t W3 = lane_get(Av, 3), W4 = lane_get(Av, 4);
@@ -610,7 +623,7 @@ __device__ __forceinline__ uint64_t blur_row(uint32_t& Av, uint32_t rowv, int32_
   if (ON == 0) W0 = n0;
   else if (ON == 1) W1 = n0;
   else W2 = n0;
-  uint64_t wipes = 0;
+  wipes[0] = wipes[1] = 0;  // bit k-1 of the pair: block k
 #pragma unroll 4
   for (int32_t k = 1;; k++) {
     const uint32_t e = lane_get(rowv, k);
@@ -632,21 +645,22 @@ __device__ __forceinline__ uint64_t blur_row(uint32_t& Av, uint32_t rowv, int32_
       w = (int32_t)mx <= tmax;
       W1 = w ? total : W1;
     }
-    wipes |= (uint64_t)w << (k - 1);
+    const uint64_t bit = (uint64_t)w << ((k - 1) & 63);
+    if (k <= 64) wipes[0] |= bit;
+    else wipes[1] |= bit;
     if (k == bpr) break;
-    Av = lane_set(Av, W0, k - 1);
+    lane_set(Av, W0, k - 1);
     W0 = W1;
     W1 = W2;
     W2 = W3;
     W3 = W4;
     W4 = lane_get(Av, k + 4);
   }
-  Av = lane_set(Av, W0, bpr - 1);
-  Av = lane_set(Av, W1, bpr);
-  Av = lane_set(Av, W2, bpr + 1);
-  Av = lane_set(Av, W3, bpr + 2);
-  Av = lane_set(Av, W4, bpr + 3);
-  return wipes;
+  lane_set(Av, W0, bpr - 1);
+  lane_set(Av, W1, bpr);
+  lane_set(Av, W2, bpr + 1);
+  lane_set(Av, W3, bpr + 2);
+  lane_set(Av, W4, bpr + 3);
 }
 
 // The same row for a row length known at compile time: the whole row's A in
@@ -715,9 +729,14 @@ __global__ void __launch_bounds__(64) k_blur_resolve_w(BlurGeom g, uint8_t* scra
   // blurfilter_cpu's set-up (A zero where the reference reads uninitialised
   // stack, as the other resolver): cur[0], cur[bpr], next[0], next[bpr], then
   // cur[1 .. bpr] = the first row's counts (A[2] and A[bpr + 1] overwritten)
-  uint32_t Av = 0;
-  if (lane == 1 || lane == bpr + 1 || lane == 2 || lane == bpr + 2) Av = total;
-  if (lane >= 2 && lane < 2 + bpr) Av = counts[lane - 2];
+  // entries l (and 64 + l, for rows past 56 blocks) of A in lane l
+  auto a_init = [&](int32_t j) -> uint32_t {
+    uint32_t v = 0;
+    if (j == 1 || j == bpr + 1 || j == 2 || j == bpr + 2) v = total;
+    if (j >= 2 && j < 2 + bpr) v = counts[j - 2];
+    return v;
+  };
+  uint32_t Av = a_init(lane);
   // the largest max that is wiped (-1: none)
   auto wiped = [&](uint32_t m) { return ((float)m) / (float)(uint64_t)total <= g.intensity; };
   int32_t tmax = -1;
@@ -747,17 +766,24 @@ __global__ void __launch_bounds__(64) k_blur_resolve_w(BlurGeom g, uint8_t* scra
     default:
       break;
   }
-  // the next row's counts one row ahead
+  // the next row's counts one row ahead (entries l and 64 + l in lane l)
   const int32_t rl = bpr + 1;
-  uint32_t rowv = g.T > 0 && lane < rl ? counts[bpr + lane] : 0;
+  Lanes2 A2{Av, a_init(64 + lane)};
+  auto row_of = [&](int32_t t) {
+    const int64_t r0 = bpr + (int64_t)t * rl;
+    return Lanes2{lane < rl ? counts[r0 + lane] : 0u, 64 + lane < rl ? counts[r0 + 64 + lane] : 0u};
+  };
+  Lanes2 rowv = g.T > 0 ? row_of(0) : Lanes2{0u, 0u};
   for (int32_t t = 0; t < g.T; t++) {
-    const uint32_t cur = rowv;
-    if (t + 1 < g.T) rowv = lane < rl ? counts[bpr + (t + 1) * rl + lane] : 0;
+    const Lanes2 cur = rowv;
+    if (t + 1 < g.T) rowv = row_of(t + 1);
     const int op = t % 3;
-    const uint64_t wipes = op == 0   ? blur_row<0>(Av, cur, bpr, total, tmax)
-                           : op == 1 ? blur_row<1>(Av, cur, bpr, total, tmax)
-                                     : blur_row<2>(Av, cur, bpr, total, tmax);
-    if (lane < bpr) wipe[t * bpr + lane] = (uint8_t)((wipes >> lane) & 1);
+    uint64_t wipes[2];
+    if (op == 0) blur_row<0>(A2, cur, bpr, total, tmax, wipes);
+    else if (op == 1) blur_row<1>(A2, cur, bpr, total, tmax, wipes);
+    else blur_row<2>(A2, cur, bpr, total, tmax, wipes);
+    if (lane < bpr) wipe[t * bpr + lane] = (uint8_t)((wipes[0] >> lane) & 1);
+    if (64 + lane < bpr) wipe[t * bpr + 64 + lane] = (uint8_t)((wipes[1] >> lane) & 1);
   }
 }
 
