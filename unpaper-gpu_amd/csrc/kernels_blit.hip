@@ -510,6 +510,73 @@ __global__ void __launch_bounds__(kThreads) k_move_rect(PlaneRef src, PlaneRef d
   }
 }
 
+// k_move_rect for RGB24 planes, a destination dword per lane.  A moved
+// pixel's bytes come from the same row offset 3 (A.x0 - tx) away, so a dword
+// whose bytes all share one class (unchanged / background / moved) is one
+// aligned load, a constant pattern, or two aligned loads realigned by that
+// offset; dwords across a class change, and the row's tail, go byte by byte.
+// RGB24 has no alpha: set_pixel and the raw paste write the same bytes.
+__global__ void __launch_bounds__(kThreads) k_move_rect_rgb(PlaneRef src, PlaneRef dst,
+                                                            const MoveArgs* args) {
+  const int s = blockIdx.z;
+  const MoveArgs a = args[s];
+  if (!a.active) return;
+  const Planes& P = src.P;
+  const uint8_t* sbase = plane_ptr(src, s);
+  uint8_t* dbase = plane_ptr(dst, s);
+  const Rect A = clip(a.area, P.W, P.H);
+  const int32_t aw = A.x1 - A.x0 + 1, ah = A.y1 - A.y0 + 1;
+  const int32_t sw = iabs(a.area.x0 - a.area.x1) + 1, sh = iabs(a.area.y0 - a.area.y1) + 1;
+  const int32_t rowb = 3 * P.W, ndw = (rowb + 3) >> 2;
+  const int32_t shift = 3 * (A.x0 - a.tx);  // source byte - destination byte, moved pixels
+  // the background as bytes of a dword starting at a byte of phase 0, 1, 2
+  uint32_t bgw[3];
+#pragma unroll
+  for (int ph = 0; ph < 3; ph++) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) w |= (uint32_t)a.bg[(ph + k) % 3] << (8 * k);
+    bgw[ph] = w;
+  }
+  for (int32_t y = blockIdx.x; y < P.H; y += gridDim.x) {
+    const uint8_t* srow = sbase + (int64_t)y * P.pitch;
+    uint8_t* drow = dbase + (int64_t)y * P.pitch;
+    const int32_t v = y - a.ty;
+    const bool vin = v >= 0 && v < sh, vsrc = vin && v < ah;
+    const bool wrow = y >= A.y0 && y <= A.y1;
+    const uint8_t* srow_m = sbase + (int64_t)(A.y0 + (vsrc ? v : 0)) * P.pitch;
+    // 0 unchanged, 1 background, 2 moved
+    auto cls = [&](int32_t x) {
+      const int32_t u = x - a.tx;
+      if (vin && u >= 0 && u < sw) return vsrc && u < aw ? 2 : 1;
+      return wrow && x >= A.x0 && x <= A.x1 ? 1 : 0;
+    };
+    for (int32_t d = threadIdx.x; d < ndw; d += blockDim.x) {
+      const int32_t xb = 4 * d;
+      const int c0 = cls(xb / 3), c1 = cls(imin(xb + 3, rowb - 1) / 3);
+      if (c0 == c1 && xb + 4 <= rowb) {
+        uint32_t out;
+        if (c0 == 0) {
+          out = *reinterpret_cast<const uint32_t*>(srow + xb);
+        } else if (c0 == 1) {
+          out = bgw[xb % 3];
+        } else {
+          const int32_t sb = xb + shift, sa = sb & ~3, r = sb & 3;
+          const uint32_t w0 = *reinterpret_cast<const uint32_t*>(srow_m + sa);
+          out = r ? __builtin_amdgcn_alignbyte(*reinterpret_cast<const uint32_t*>(srow_m + sa + 4), w0, r)
+                  : w0;
+        }
+        *reinterpret_cast<uint32_t*>(drow + xb) = out;
+      } else {
+        for (int k = 0; k < 4 && xb + k < rowb; k++) {
+          const int32_t b = xb + k, x = b / 3, c = cls(x);
+          drow[b] = c == 0 ? srow[b] : c == 1 ? a.bg[b % 3] : srow_m[b + shift];
+        }
+      }
+    }
+  }
+}
+
 // k_move_rect for gray planes, 16 bytes of the destination per lane.  The
 // class of a column (unchanged / background / moved) only changes at five
 // breakpoints, so a vector not straddling one is one aligned 16-byte load, a
@@ -821,7 +888,7 @@ void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* 
     hipLaunchKernelGGL(k_move_rect<F_Y400A>, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst,
                        args);
   } else {
-    hipLaunchKernelGGL(k_move_rect<F_RGB24>, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst,
+    hipLaunchKernelGGL(k_move_rect_rgb, dim3(gx, 1, count), dim3(kThreads), 0, st, src, dst,
                        args);
   }
 }
