@@ -3,6 +3,8 @@
 #   make lib        -> unpaper-gpu_amd/lib/libunpaper_hip.so   (product)
 #   make oracle     -> oracle/_build/liboracle.so              (test infrastructure)
 #   make ctest      -> tests/c/_build/backend_ops              (C caller of the vtable; test)
+#   make libm_check -> tests/c/_build/libm_check: the device's glibc sinf/cosf/powf
+#                      restatement against the host libm (test)
 #   make sanitize   -> tests/c/_build/sanitize: the oracle + the host codec
 #                      under ASan/UBSan (host code only, no GPU)
 #   make lib DIAG=1 -> the same library with the timing diagnostics of
@@ -50,13 +52,14 @@ CTEST      := tests/c/_build/backend_ops
 REFERENCE  ?= /root/reference
 ADAPTER    := tests/c/_build/adapter_ops
 
+LIBM_CHECK := tests/c/_build/libm_check
 SANITIZE   := tests/c/_build/sanitize
 LLVMCC     := /opt/rocm/lib/llvm/bin/clang
 SANFLAGS   := -fsanitize=address,undefined -fno-sanitize-recover=undefined \
               -fno-omit-frame-pointer -g -O1
 
-.PHONY: all lib oracle ctest adapter sanitize clean
-all: lib oracle ctest
+.PHONY: all lib oracle ctest adapter sanitize libm_check clean
+all: lib oracle ctest libm_check
 
 lib: $(LIB)
 oracle: $(ORACLE_LIB)
@@ -99,10 +102,17 @@ $(ADAPTER): tests/c/adapter_main.c tests/c/pages.h integration/backend_hip.c int
 	  -L$(PKG)/lib -L oracle/_build -lunpaper_hip -loracle -lm \
 	  -Wl,-rpath,'$$ORIGIN/../../../$(PKG)/lib' -Wl,-rpath,'$$ORIGIN/../../../oracle/_build'
 
+# glibc sinf/cosf/powf(x, 2) restatement (csrc/libm_glibc.h) against this
+# host's libm; plain g++, contraction off like the device build.
+libm_check: $(LIBM_CHECK)
+$(LIBM_CHECK): tests/c/libm_check.cpp $(CSRC)/libm_glibc.h
+	@mkdir -p tests/c/_build
+	g++ -O2 -std=c++17 -ffp-contract=off -Wall -I$(CSRC) $< -o $@ -lm -lpthread
+
 # One compiler (ROCm clang) for every object so that one sanitizer runtime
 # serves the program; the HIP sources are compiled for the host only.
 $(SANITIZE): tests/c/sanitize_main.c oracle/oracle.c oracle/oracle.h $(CSRC)/pnm.cpp $(CSRC)/png.cpp \
-             $(CSRC)/runtime.hip $(HDRS)
+             $(CSRC)/jpeg.cpp tests/c/san_stubs.cpp $(CSRC)/runtime.hip $(HDRS)
 	@mkdir -p tests/c/_build/san
 	$(LLVMCC) $(SANFLAGS) -std=gnu11 -ffp-contract=off -c oracle/oracle.c -o tests/c/_build/san/oracle.o
 	$(LLVMCC) $(SANFLAGS) -std=gnu11 -Iinclude -c tests/c/sanitize_main.c -o tests/c/_build/san/main.o
@@ -110,6 +120,10 @@ $(SANITIZE): tests/c/sanitize_main.c oracle/oracle.c oracle/oracle.h $(CSRC)/pnm
 	  -Iinclude -I$(CSRC) -c $(CSRC)/pnm.cpp -o tests/c/_build/san/pnm.o
 	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
 	  -Iinclude -I$(CSRC) -c $(CSRC)/png.cpp -o tests/c/_build/san/png.o
+	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
+	  -Iinclude -I$(CSRC) -c $(CSRC)/jpeg.cpp -o tests/c/_build/san/jpeg.o
+	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
+	  -Iinclude -I$(CSRC) -c tests/c/san_stubs.cpp -o tests/c/_build/san/san_stubs.o
 	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
 	  -Iinclude -I$(CSRC) -c $(CSRC)/runtime.hip -o tests/c/_build/san/runtime.o
 	$(HIPCC) $(SANFLAGS) tests/c/_build/san/*.o -o $@ -lm -lz

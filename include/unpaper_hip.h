@@ -400,7 +400,10 @@ int uphip_batch_set_input(UphipBatch *batch, int32_t slot, const void *host,
 int uphip_batch_run(UphipBatch *batch, int32_t count);
 /* Same, reading the pages in place from device memory: page j of sheet s is
  * at pages + (s*input_count + j)*page_stride, rows `pitch` bytes apart
- * (pre-staged / device-decoded inputs, no copy). */
+ * (pre-staged / device-decoded inputs, no copy).  When pages, pitch and
+ * page_stride are 16-byte aligned the GRAY8 decode reads rows as 16-byte
+ * vectors: the buffer must then extend to round_up(row bytes, 16) past the
+ * last page's last row start. */
 int uphip_batch_run_device(UphipBatch *batch, int32_t count, const void *pages,
                            int64_t pitch, int64_t page_stride);
 int uphip_batch_wait(UphipBatch *batch);
@@ -466,7 +469,30 @@ int uphip_pnm_write(const char *path, const void *src, int64_t linesize,
 int uphip_png_probe(const char *path, UphipPnmInfo *info);
 int uphip_png_read(const char *path, void *dst, int64_t linesize,
                    const UphipPnmInfo *expect);
-/* Either codec, picked by the file's signature (PNG or PNM). */
+/* JPEG decode peer of nvimgcodec_decode / _decode_file
+ * (imageprocess/nvimgcodec.c:679-1007) and of loadImage's FFmpeg JPEG path
+ * (file.c:29-128): baseline / extended-sequential Huffman, 8-bit; 1 component
+ * -> GRAY8, 3 components (YCbCr, or RGB per the Adobe marker) -> RGB24 (the
+ * batch decode queue's swscale conversion, sheet_stages.c:99-122); sampling
+ * factors 1 or 2.  Huffman decoding on the host; dequantisation, IDCT, chroma
+ * upsampling and colour conversion on the current device (libjpeg's islow
+ * IDCT, fancy upsampling and ycc_rgb_convert).  Progressive, arithmetic,
+ * 12-bit and CMYK files fail.  uphip_jpeg_read returns pixels in host memory;
+ * uphip_jpeg_decode decodes a file image in memory into device memory (rows
+ * `pitch` apart; info: in = expected geometry when width > 0, out = geometry).
+ * Both synchronise the current stream. */
+int uphip_jpeg_probe(const char *path, UphipPnmInfo *info);
+int uphip_jpeg_read(const char *path, void *dst, int64_t linesize,
+                    const UphipPnmInfo *expect);
+int uphip_jpeg_decode(const void *data, size_t size, void *device_dst, int64_t pitch,
+                      UphipPnmInfo *info);
+/* The host half alone (no device needed): the packed coefficient image of
+ * csrc/jpeg.h (header, per-block counts, per-MCU-row offsets, zigzag
+ * coefficient prefixes) written to `packed` when `capacity` suffices.
+ * Returns its size in bytes, or -1. */
+int64_t uphip_jpeg_entropy_decode(const void *data, size_t size, void *packed,
+                                  int64_t capacity);
+/* Any codec, picked by the file's signature (PNG, JPEG or PNM). */
 int uphip_image_probe(const char *path, UphipPnmInfo *info);
 int uphip_image_read(const char *path, void *dst, int64_t linesize,
                      const UphipPnmInfo *expect);
@@ -520,10 +546,15 @@ typedef int (*UphipStoreFn)(void *user, int64_t job, const void *sheet,
                             int64_t linesize, int32_t width, int32_t height,
                             int32_t format);
 UphipSource *uphip_source_callback(UphipLoadFn load, void *user);
-/* page i at base + i*page_stride, rows `linesize` apart */
+/* page i at base + i*page_stride, rows `linesize` apart.  Memory sources and
+ * sinks are page-locked (hipHostRegister) over the extent the runner reads or
+ * writes on their first run and unregistered by uphip_source_destroy /
+ * uphip_sink_destroy: the buffer must outlive the source or sink.  Pages that
+ * overlap (page_stride 0 included) or rows shorter than the page are read
+ * through the staged path. */
 UphipSource *uphip_source_memory(const void *base, int64_t linesize,
                                  int64_t page_stride, int64_t npages);
-/* page i decoded from paths[i] (PNM or PNG, uphip_image_read) straight into
+/* page i decoded from paths[i] (PNM, PNG or JPEG, uphip_image_read) straight into
  * the staging slot */
 UphipSource *uphip_source_pnm(const char *const *paths, int64_t npaths);
 void uphip_source_destroy(UphipSource *source);
@@ -591,6 +622,12 @@ void *uphip_device_alloc(size_t bytes);
 void uphip_device_free(void *ptr);
 int uphip_memcpy_htod(void *dst, const void *src, size_t bytes);
 int uphip_memcpy_dtoh(void *dst, const void *src, size_t bytes);
+/* Self-check of the device's restatement of glibc sinf/cosf/powf(x, 2)
+ * (csrc/libm_glibc.h; the batch path's rotation select for more than two
+ * deskew edges, deskew.c:226,260-261) against this host's libm: every
+ * `stride`-th float of |x| < 120 (sin/cos) and 2^-60 <= |x| < 2^61 (pow),
+ * both signs.  counts = {sinf, cosf, powf mismatches, inputs}.  */
+int uphip_check_libm(uint32_t stride, uint64_t counts[4]);
 /* Pinned (page-locked) host memory, DMA-capable from every device. */
 void *uphip_host_alloc(size_t bytes);
 void uphip_host_free(void *ptr);

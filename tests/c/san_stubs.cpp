@@ -1,0 +1,10 @@
+// Sanitizer build only (make sanitize): the host codecs are linked without the
+// device kernels, so the JPEG device half is a stub that reports no device.
+#include "jpeg.h"
+#include "runtime.h"
+
+namespace uph {
+bool jpeg_launch(const JpegHeader&, const uint8_t*, uint8_t*, uint8_t*, int64_t, hipStream_t) {
+  return fail("jpeg: no device in the sanitizer build");
+}
+}  // namespace uph

@@ -132,6 +132,51 @@ static void png(const char *dir, const char *fixtures) {
   }
 }
 
+/* the JPEG host decoder (jpeg.cpp: markers + Huffman) on small PIL-encoded
+ * files (tests/golden/jpeg), a refused progressive one, and truncated /
+ * bit-flipped copies (truncated ones must fail, none may crash) */
+static void jpeg(const char *fixtures) {
+  static const char *good[] = {"gray.jpg", "rgb420_rst.jpg", "rgb444_opt.jpg"};
+  static uint8_t raw[1 << 16], tmp[1 << 16];
+  char path[512];
+  for (size_t i = 0; i <= sizeof good / sizeof *good; i++) {
+    const int refuse = i == sizeof good / sizeof *good;
+    snprintf(path, sizeof path, "%s/../jpeg/%s", fixtures, refuse ? "progressive.jpg" : good[i]);
+    FILE *f = fopen(path, "rb");
+    if (!f) {
+      fprintf(stderr, "jpeg fixture %s missing\n", path);
+      g_fail++;
+      continue;
+    }
+    const size_t n = fread(raw, 1, sizeof raw, f);
+    fclose(f);
+    const int64_t need = uphip_jpeg_entropy_decode(raw, n, NULL, 0);
+    if ((need < 0) != refuse) {
+      fprintf(stderr, "jpeg %s: %s\n", path, need < 0 ? uphip_last_error() : "accepted");
+      g_fail++;
+    }
+    uphip_clear_error();
+    if (need > 0) {
+      void *packed = malloc((size_t)need);
+      if (uphip_jpeg_entropy_decode(raw, n, packed, need) != need) g_fail++;
+      free(packed);
+    }
+    if (refuse) continue;
+    for (size_t cut = 3; cut < n; cut += n / 17 + 1) {
+      /* cut inside the entropy-coded data (not the trailing EOI alone) */
+      if (cut + 2 < n && uphip_jpeg_entropy_decode(raw, cut, NULL, 0) >= 0) {
+        fprintf(stderr, "truncated jpeg %s (%zu of %zu bytes) accepted\n", path, cut, n);
+        g_fail++;
+      }
+      uphip_clear_error();
+      memcpy(tmp, raw, n);
+      tmp[cut] ^= 0x5A;
+      uphip_jpeg_entropy_decode(tmp, n, NULL, 0); /* must not crash */
+      uphip_clear_error();
+    }
+  }
+}
+
 int main(int argc, char **argv) {
   const char *dir = argc > 1 ? argv[1] : "/tmp";
   UphipOptions o;
@@ -152,6 +197,7 @@ int main(int argc, char **argv) {
   sheet("geometry", &o, UPHIP_FMT_GRAY8, 300, 420, 15);
   codec(dir);
   png(dir, argc > 2 ? argv[2] : "tests/golden/reference");
+  jpeg(argc > 2 ? argv[2] : "tests/golden/reference");
   printf("sanitize: %d failures\n", g_fail);
   return g_fail ? 1 : 0;
 }

@@ -163,6 +163,48 @@ def test_deskew_edges(hip, oracle, edges):
     check(oracle, opts, [[synth(*SMALL, p)] for p in (0, 1)], "edges %r" % (edges,))
 
 
+def frame_page(w, h, deg, seed=1):
+    """White page with a 12-px dark rectangular frame (60 % of the page)
+    rotated by `deg` about the centre: all four mask edges see the same
+    slope, so every edge set agrees within the deviation and the combined
+    rotation is non-zero (the synthetic text pages' top/bottom edges do not
+    agree with the left/right ones)."""
+    import math
+    rng = np.random.default_rng(seed)
+    bw, bh = int(w * 0.6), int(h * 0.6)
+    t = math.radians(deg)
+    yy, xx = np.mgrid[0:h, 0:w]
+    dx, dy = xx - w / 2 + 0.5, yy - h / 2 + 0.5
+    u = math.cos(t) * dx + math.sin(t) * dy
+    v = -math.sin(t) * dx + math.cos(t) * dy
+    frame = (np.abs(u) < bw / 2) & (np.abs(v) < bh / 2) & \
+        ~((np.abs(u) < bw / 2 - 12) & (np.abs(v) < bh / 2 - 12))
+    g = np.where(frame, rng.integers(0, 40, size=(h, w)), 255).astype(np.uint8)
+    return HostImage.from_array(g, A.FMT_GRAY8, abs_black_threshold=170)
+
+
+@pytest.mark.parametrize("edges", [(True, True, True, False), (True, True, True, True),
+                                   (False, True, False, True)])
+@pytest.mark.parametrize("interp", [A.INTERP_CUBIC, A.INTERP_LINEAR])
+def test_deskew_multi_edge_nonzero(hip, oracle, edges, interp):
+    """the batch path's rotation select with 3 and 4 edges
+    (device glibc sinf/cosf/powf, libm_glibc.h) and the top/bottom edges
+    (deskew.c:96-97 sideOffset), with NON-ZERO oracle rotations, whole
+    sheets against the oracle."""
+    opts = oracle.default_options()
+    opts.interpolate_type = interp
+    opts.deskew_parameters.scan_edges = A.Edges(*edges)
+    degs = (1.3, 0.65, -2.2, 3.7)
+    sheets = [[frame_page(*SMALL, d)] for d in degs]
+    check(oracle, opts, sheets, "edges %r" % (edges,))
+    rots = [float(oracle_sheet(oracle, opts, p)[1].rotation[0]) for p in sheets]
+    assert sum(r != 0.0 for r in rots) >= 2, rots
+    if sum(edges) > 2:
+        # an average of disagreeing edges: not itself an angle of the scan table
+        step = np.float32(np.radians(0.1))
+        assert any(r != 0.0 and abs(r / step - round(r / step)) > 1e-3 for r in rots), rots
+
+
 @pytest.mark.parametrize("rot", [90, -90])
 def test_pre_post_rotate(hip, oracle, rot):
     opts = oracle.default_options()

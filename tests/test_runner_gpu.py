@@ -99,6 +99,37 @@ def test_runner_host_fed_matches_oracle(hip, oracle):
         assert_same(got, exp, "runner job %d" % i)
 
 
+@pytest.mark.parametrize("stride_kind", ["zero", "overlap"])
+def test_runner_memory_source_overlapping_pages(hip, oracle, stride_kind):
+    """a memory source whose pages overlap (page_stride 0 = one
+    repeated page, or half a page) cannot be read in place by the batch; the
+    runner takes the staged path and every job still gets its own page."""
+    w, h = SMALL
+    n = 3
+    opts = oracle.default_options()
+    stride = 0 if stride_kind == "zero" else w * (h // 2)
+    rows = h + (n - 1) * (h // 2) if stride else h
+    buf = np.full((rows, w), 255, np.uint8)
+    buf[:h] = synth_page_host(w, h, 70)
+    if stride:
+        buf[h // 2:h // 2 + h] = np.minimum(buf[h // 2:h // 2 + h], synth_page_host(w, h, 71))
+    flat = buf.reshape(-1)
+    pages = [HostImage.from_array(flat[i * stride:i * stride + w * h].reshape(h, w).copy(),
+                                  A.FMT_GRAY8) for i in range(n)]
+    r = Runner(opts, 2, w, h, A.FMT_GRAY8, devices=(0,), streams=2, host_threads=2)
+    try:
+        out = np.zeros((n, h, r.out_linesize), np.uint8)
+        src = source_memory(flat.ctypes.data, w, stride, n, keep=flat)
+        snk = sink_memory(out.ctypes.data, r.out_linesize, r.out_linesize * h, n, keep=out)
+        failed, err = r.run_host(n, src, snk)
+        assert failed == 0, err
+    finally:
+        r.close()
+    for i, p in enumerate(pages):
+        exp = _oracle_out(oracle, opts, p)
+        assert_same(HostImage(w, h, exp.format, out[i]), exp, "%s page %d" % (stride_kind, i))
+
+
 def test_runner_pnm_files(hip, oracle, tmp_path):
     """Decode queue -> device -> encode queue: PGM in, PGM out."""
     w, h = SMALL
@@ -179,6 +210,79 @@ def test_runner_png_reference_sources(hip, oracle, ref_path, tmp_path, names, fm
     for i, p in enumerate(pages):
         got = pnm_read(str(tmp_path / ("out_%02d.%s" % (i, out_ext))))
         assert_same(got, _oracle_out(oracle, opts, p), "png job %s" % names[i])
+
+
+def _no_filters(opts):
+    """The reference JPEG test's option set (unpaper_tests.py:941-948)."""
+    opts.disable |= (A.NO_BLACKFILTER | A.NO_NOISEFILTER | A.NO_BLURFILTER | A.NO_GRAYFILTER |
+                     A.NO_DESKEW)
+    return opts
+
+
+def test_runner_jpeg_reference_acceptance(hip, oracle, ref_path, tmp_path):
+    """The reference's own JPEG acceptance test (tests/unpaper_tests.py:921-955)
+    through the runner's JPEG path (host entropy decode into pinned memory,
+    device IDCT into the batch's input slot): imgsrc001 saved by PIL as JPEG
+    quality 95 (a grayscale JPEG: PIL writes mode "1" as L), filters and
+    deskew off, output within 10 % (binarised compare_images) of the PNG run.
+    Stronger: the JPEG run equals the oracle on PIL's decode of the same file
+    byte for byte (device pixels == libjpeg's, pipeline == oracle)."""
+    from PIL import Image
+    from unpaper_hip.hostimage import binarized_diff_ratio
+    opts = _no_filters(oracle.default_options())
+    src = ref_path("imgsrc001.png")
+    jpg = tmp_path / "source.jpg"
+    Image.open(src).save(jpg, "JPEG", quality=95)
+    pil = np.asarray(Image.open(jpg))
+    assert pil.ndim == 2
+    h, w = pil.shape
+    r = Runner(opts, 1, w, h, A.FMT_GRAY8, devices=(0,), streams=1, host_threads=2)
+    try:
+        failed, err = r.run_host(1, source_pnm([str(jpg)]), sink_pnm(str(tmp_path / "jpg_%d.pgm")))
+        assert failed == 0, err
+    finally:
+        r.close()
+    got = pnm_read(str(tmp_path / "jpg_0.pgm"))
+    exp = _oracle_out(oracle, opts, HostImage.from_array(pil.copy(), A.FMT_GRAY8))
+    assert_same(got, exp, "jpeg page vs oracle on PIL's decode")
+    png_page = HostImage.load(src)
+    png_out = _oracle_out(oracle, opts, png_page)
+    ratio = binarized_diff_ratio(np.array(got.to_pil().convert("L")),
+                                 np.array(png_out.to_pil().convert("L")))
+    assert ratio < 0.10, ratio
+
+
+def test_runner_jpeg_colour_and_mixed_sources(hip, oracle, tmp_path):
+    """A runner chunk mixing JPEG (4:2:0 and 4:4:4) and PNM pages of one
+    RGB24 geometry: every page through its own decoder, JPEG pages decoded on
+    the slot's stream into their input slots; outputs against the oracle on
+    PIL's decode."""
+    from PIL import Image
+    w, h = SMALL
+    opts = oracle.default_options()
+    paths, pages = [], []
+    for i in range(5):
+        g = synth_page_host(w, h, 90 + i)
+        rgb = np.stack([g, np.roll(g, 3, 1), np.maximum(g, 40)], 2)
+        if i == 2:
+            q = str(tmp_path / ("p%d.ppm" % i))
+            pnm_write(q, HostImage.from_array(rgb, A.FMT_RGB24))
+            px = rgb
+        else:
+            q = str(tmp_path / ("p%d.jpg" % i))
+            Image.fromarray(rgb).save(q, "JPEG", quality=92, subsampling=2 if i % 2 else 0)
+            px = np.asarray(Image.open(q))
+        paths.append(q)
+        pages.append(HostImage.from_array(px.copy(), A.FMT_RGB24))
+    r = Runner(opts, 3, w, h, A.FMT_RGB24, devices=(0,), streams=2, host_threads=3)
+    try:
+        failed, err = r.run_host(len(paths), source_pnm(paths), sink_pnm(str(tmp_path / "o%02d.ppm")))
+        assert failed == 0, err
+    finally:
+        r.close()
+    for i, p in enumerate(pages):
+        assert_same(pnm_read(str(tmp_path / ("o%02d.ppm" % i))), _oracle_out(oracle, opts, p),
+                    "page %d (%s)" % (i, paths[i]))
 
 
 def test_runner_two_outputs_pbm(hip, oracle, tmp_path):

@@ -1,0 +1,591 @@
+// jpeg.cpp — host half of the JPEG decode peer (see jpeg.h):
+// marker parsing and Huffman decoding into the packed coefficient layout the
+// device kernels (kernels_jpeg.hip) turn into pixels.
+//
+// Reference: the reference decodes JPEG inputs with FFmpeg (file.c:29-128,
+// the batch decode queue's swscale conversion in sheet_stages.c:99-122) and
+// with nvImageCodec on its GPU path (imageprocess/nvimgcodec.c:679-1007,
+// nvimgcodec_decode / _decode_file / _decode_batch).  Decoding follows ITU-T
+// T.81 (baseline and extended sequential Huffman, Annex F) with libjpeg's
+// conventions where T.81 leaves room: the colour transform from the JFIF /
+// Adobe markers or component ids (jdapimin.c default_decompress_parms),
+// component geometry (jdinput.c initial_setup, per_scan_setup).
+#include <cerrno>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "jpeg.h"
+#include "runtime.h"
+
+namespace uph {
+
+namespace {
+
+constexpr int kLook = 9;  // Huffman lookahead bits
+
+struct Huff {
+  bool present = false;
+  uint16_t look[1 << kLook];  // len << 8 | symbol, 0 = longer code
+  int32_t maxcode[18];        // largest code of each length, -1 if none
+  int32_t valptr[17];
+  int32_t mincode[17];
+  uint8_t vals[256];
+};
+
+bool build_huff(Huff* t, const uint8_t* bits /*16*/, const uint8_t* vals, int nvals) {
+  memset(t->look, 0, sizeof(t->look));
+  memcpy(t->vals, vals, (size_t)nvals);
+  int code = 0, k = 0;
+  for (int len = 1; len <= 16; len++) {
+    t->valptr[len] = k;
+    t->mincode[len] = code;
+    for (int i = 0; i < bits[len - 1]; i++, k++, code++) {
+      if (len <= kLook) {
+        const int shift = kLook - len;
+        for (int j = 0; j < (1 << shift); j++)
+          t->look[(code << shift) | j] = (uint16_t)(len << 8 | vals[k]);
+      }
+    }
+    t->maxcode[len] = bits[len - 1] ? code - 1 : -1;
+    if (code > (1 << len)) return false;  // over-subscribed
+    code <<= 1;
+  }
+  t->maxcode[17] = 0x7fffffff;
+  t->present = true;
+  return true;
+}
+
+// MSB-first bit reader over entropy-coded data: byte stuffing removed; at a
+// marker it feeds zero bits (libjpeg's behaviour for corrupt data) and stops.
+struct Bits {
+  const uint8_t* p;
+  const uint8_t* end;
+  uint64_t buf = 0;
+  int n = 0;
+  int fed = 0;  // zero bytes fed past a marker or the end of the data
+  bool marker = false;
+  // true when decoding consumed fed zeros: the data ended (or a marker came)
+  // inside the entropy-coded segment
+  bool underrun() const { return n < 8 * fed; }
+  void fill() {
+    while (n <= 56) {
+      uint32_t byte = 0;
+      if (marker || p >= end) fed++;
+      if (!marker && p < end) {
+        byte = *p;
+        if (byte == 0xFF) {
+          if (p + 1 < end && p[1] == 0x00) {
+            p += 2;
+          } else {
+            marker = true;  // leave p at the marker
+            fed++;
+            byte = 0;
+          }
+        } else {
+          p++;
+        }
+      }
+      buf |= (uint64_t)byte << (56 - n);
+      n += 8;
+    }
+  }
+  uint32_t get(int s) {  // s in 1..16
+    if (n < s) fill();
+    const uint32_t v = (uint32_t)(buf >> (64 - s));
+    buf <<= s;
+    n -= s;
+    return v;
+  }
+  int decode(const Huff& t) {
+    if (n < 16) fill();
+    const uint16_t e = t.look[buf >> (64 - kLook)];
+    if (e) {
+      const int len = e >> 8;
+      buf <<= len;
+      n -= len;
+      return e & 0xff;
+    }
+    for (int len = kLook + 1; len <= 16; len++) {
+      const int32_t code = (int32_t)(buf >> (64 - len));
+      if (code <= t.maxcode[len]) {
+        buf <<= len;
+        n -= len;
+        return t.vals[t.valptr[len] + code - t.mincode[len]];
+      }
+    }
+    return -1;  // no such code: corrupt data
+  }
+  void reset() {  // byte-align at a restart marker
+    buf = 0;
+    n = 0;
+    fed = 0;
+    marker = false;
+  }
+};
+
+inline int extend(uint32_t v, int s) {
+  return v < (1u << (s - 1)) ? (int)v - (1 << s) + 1 : (int)v;
+}
+
+uint16_t be16(const uint8_t* p) { return (uint16_t)(p[0] << 8 | p[1]); }
+
+struct Parser {
+  const uint8_t* d;
+  size_t n;
+  const char* name;
+  size_t pos = 0;
+  // frame
+  bool have_frame = false;
+  int sof = -1;
+  int w = 0, h = 0, nf = 0;
+  int cid[4] = {}, hs[4] = {}, vs[4] = {}, tq[4] = {};
+  uint16_t qt[4][64];  // zigzag order
+  bool have_qt[4] = {};
+  Huff dc[4], ac[4];
+  int restart = 0;
+  bool jfif = false, adobe = false;
+  int adobe_transform = -1;
+};
+
+bool ffail(const Parser& P, const char* what) {
+  return fail("jpeg: %s: %s", P.name, what);
+}
+
+// Reads the next marker code at P.pos (skipping fill bytes); -1 at the end.
+int next_marker(Parser& P) {
+  while (P.pos < P.n && P.d[P.pos] != 0xFF) P.pos++;  // tolerate garbage between segments
+  while (P.pos < P.n && P.d[P.pos] == 0xFF) P.pos++;
+  if (P.pos >= P.n) return -1;
+  return P.d[P.pos++];
+}
+
+bool segment(Parser& P, const uint8_t** body, int* len) {
+  if (P.pos + 2 > P.n) return ffail(P, "truncated segment");
+  const int L = be16(P.d + P.pos);
+  if (L < 2 || P.pos + (size_t)L > P.n) return ffail(P, "bad segment length");
+  *body = P.d + P.pos + 2;
+  *len = L - 2;
+  P.pos += (size_t)L;
+  return true;
+}
+
+bool parse_sof(Parser& P, int code, const uint8_t* b, int len) {
+  if (P.have_frame) return ffail(P, "more than one frame");
+  if (code != 0xC0 && code != 0xC1) {
+    if (code == 0xC2 || code == 0xC6 || code == 0xCA || code == 0xCE)
+      return ffail(P, "progressive JPEG is not supported");
+    if (code >= 0xC9) return ffail(P, "arithmetic-coded JPEG is not supported");
+    return ffail(P, "lossless / hierarchical JPEG is not supported");
+  }
+  if (len < 6) return ffail(P, "bad SOF");
+  if (b[0] != 8) return ffail(P, "only 8-bit samples are supported");
+  P.h = be16(b + 1);
+  P.w = be16(b + 3);
+  P.nf = b[5];
+  if (P.h == 0) return ffail(P, "height defined by DNL is not supported");
+  if (P.w == 0) return ffail(P, "zero width");
+  if (P.nf != 1 && P.nf != 3) return ffail(P, "only 1- and 3-component images are supported");
+  if (len < 6 + 3 * P.nf) return ffail(P, "bad SOF");
+  for (int i = 0; i < P.nf; i++) {
+    P.cid[i] = b[6 + 3 * i];
+    P.hs[i] = b[7 + 3 * i] >> 4;
+    P.vs[i] = b[7 + 3 * i] & 15;
+    P.tq[i] = b[8 + 3 * i];
+    if (P.hs[i] < 1 || P.hs[i] > 4 || P.vs[i] < 1 || P.vs[i] > 4 || P.tq[i] > 3)
+      return ffail(P, "bad component parameters");
+  }
+  P.sof = code;
+  P.have_frame = true;
+  return true;
+}
+
+bool parse_dqt(Parser& P, const uint8_t* b, int len) {
+  int i = 0;
+  while (i < len) {
+    const int pq = b[i] >> 4, t = b[i] & 15;
+    i++;
+    if (t > 3 || pq > 1 || i + 64 * (pq + 1) > len) return ffail(P, "bad DQT");
+    for (int k = 0; k < 64; k++) P.qt[t][k] = pq ? be16(b + i + 2 * k) : b[i + k];
+    i += 64 * (pq + 1);
+    P.have_qt[t] = true;
+  }
+  return true;
+}
+
+bool parse_dht(Parser& P, const uint8_t* b, int len) {
+  int i = 0;
+  while (i < len) {
+    if (i + 17 > len) return ffail(P, "bad DHT");
+    const int tc = b[i] >> 4, th = b[i] & 15;
+    if (tc > 1 || th > 3) return ffail(P, "bad DHT");
+    int nv = 0;
+    for (int k = 0; k < 16; k++) nv += b[i + 1 + k];
+    if (nv > 256 || i + 17 + nv > len) return ffail(P, "bad DHT");
+    if (!build_huff(tc ? &P.ac[th] : &P.dc[th], b + i + 1, b + i + 17, nv))
+      return ffail(P, "bad Huffman table");
+    i += 17 + nv;
+  }
+  return true;
+}
+
+// Geometry of the frame (jdinput.c initial_setup) into the header.
+void frame_geometry(const Parser& P, JpegHeader* H) {
+  H->width = P.w;
+  H->height = P.h;
+  H->ncomp = P.nf;
+  H->hmax = H->vmax = 1;
+  for (int i = 0; i < P.nf; i++) {
+    H->hmax = H->hmax > P.hs[i] ? H->hmax : P.hs[i];
+    H->vmax = H->vmax > P.vs[i] ? H->vmax : P.vs[i];
+  }
+  const int mcux = (P.w + 8 * H->hmax - 1) / (8 * H->hmax);
+  const int mcuy = (P.h + 8 * H->vmax - 1) / (8 * H->vmax);
+  int64_t off = 0;
+  for (int i = 0; i < P.nf; i++) {
+    JpegComp& c = H->comp[i];
+    c.h = P.nf == 1 ? 1 : P.hs[i];
+    c.v = P.nf == 1 ? 1 : P.vs[i];
+    const int hm = P.nf == 1 ? 1 : H->hmax, vm = P.nf == 1 ? 1 : H->vmax;
+    c.dw = (int32_t)(((int64_t)P.w * c.h + hm - 1) / hm);
+    c.dh = (int32_t)(((int64_t)P.h * c.v + vm - 1) / vm);
+    const int wib = (c.dw + 7) / 8, hib = (c.dh + 7) / 8;
+    c.bw = P.nf == 1 ? wib : (mcux * c.h > wib ? mcux * c.h : wib);
+    c.bh = P.nf == 1 ? hib : (mcuy * c.v > hib ? mcuy * c.v : hib);
+    c.pitch = c.bw * 8;
+    c.plane_off = off;
+    off += (int64_t)c.pitch * c.bh * 8;
+    for (int k = 0; k < 64; k++) c.qzz[k] = P.qt[P.tq[i]][k];
+  }
+  H->scratch_bytes = P.nf == 1 ? 0 : off;
+}
+
+bool decode_scan(Parser& P, const uint8_t* b, int len, JpegDecoded* out) {
+  JpegHeader& H = out->h;
+  if (!P.have_frame) return ffail(P, "SOS before SOF");
+  if (len < 1) return ffail(P, "bad SOS");
+  const int ns = b[0];
+  if (ns < 1 || ns > 4 || len < 4 + 2 * ns) return ffail(P, "bad SOS");
+  if (H.nscans >= kJpegMaxScans) return ffail(P, "too many scans");
+  JpegScan& S = H.scan[H.nscans];
+  int tdc[4], tac[4];
+  for (int i = 0; i < ns; i++) {
+    const int id = b[1 + 2 * i];
+    int c = -1;
+    for (int k = 0; k < P.nf; k++)
+      if (P.cid[k] == id) c = k;
+    if (c < 0) return ffail(P, "scan names an unknown component");
+    S.comp[i] = c;
+    tdc[i] = b[2 + 2 * i] >> 4;
+    tac[i] = b[2 + 2 * i] & 15;
+    if (tdc[i] > 3 || tac[i] > 3 || !P.dc[tdc[i]].present || !P.ac[tac[i]].present)
+      return ffail(P, "scan uses a missing Huffman table");
+    if (!P.have_qt[P.tq[c]]) return ffail(P, "component uses a missing quantisation table");
+  }
+  const int ss = b[1 + 2 * ns], se = b[2 + 2 * ns], ahal = b[3 + 2 * ns];
+  if (ss != 0 || se != 63 || ahal != 0) return ffail(P, "not a sequential scan");
+  if (H.nscans == 0) frame_geometry(P, &H);
+  S.ncomp = ns;
+  if (ns == 1) {  // non-interleaved: one block per MCU over the component's real blocks
+    const JpegComp& c = H.comp[S.comp[0]];
+    S.mcus_x = (c.dw + 7) / 8;
+    S.mcus_y = (c.dh + 7) / 8;
+    S.blocks_per_mcu = 1;
+  } else {
+    S.mcus_x = (P.w + 8 * H.hmax - 1) / (8 * H.hmax);
+    S.mcus_y = (P.h + 8 * H.vmax - 1) / (8 * H.vmax);
+    S.blocks_per_mcu = 0;
+    for (int i = 0; i < ns; i++) S.blocks_per_mcu += H.comp[S.comp[i]].h * H.comp[S.comp[i]].v;
+    if (S.blocks_per_mcu > 10) return ffail(P, "more than 10 blocks per MCU");
+  }
+  S.first_block = H.nblocks;
+  S.first_group = (int32_t)H.ngroups;
+  const int64_t nb = (int64_t)S.mcus_x * S.mcus_y * S.blocks_per_mcu;
+  out->counts.reserve((size_t)(H.nblocks + nb));
+  // per block of an MCU: its component (for the Huffman tables and predictor)
+  int bcomp[10];
+  {
+    int k = 0;
+    for (int i = 0; i < ns; i++) {
+      const int nbl = ns == 1 ? 1 : H.comp[S.comp[i]].h * H.comp[S.comp[i]].v;
+      for (int j = 0; j < nbl; j++) bcomp[k++] = i;
+    }
+  }
+  Bits bits{P.d + P.pos, P.d + P.n};
+  int pred[4] = {0, 0, 0, 0};
+  int16_t blk[64];
+  int64_t mcu = 0;
+  const int64_t nmcu = (int64_t)S.mcus_x * S.mcus_y;
+  for (int my = 0; my < S.mcus_y; my++) {
+    out->groups.push_back((uint32_t)out->coefs.size());
+    if (out->coefs.size() > 0xF0000000u) return ffail(P, "image too large");
+    for (int mx = 0; mx < S.mcus_x; mx++, mcu++) {
+      if (P.restart && mcu > 0 && mcu % P.restart == 0) {
+        // restart marker: byte-align, skip RSTn, reset the predictors
+        if (bits.underrun()) return ffail(P, "truncated or corrupt entropy-coded data");
+        const uint8_t* q = bits.p;
+        while (q + 1 < bits.end && !(q[0] == 0xFF && q[1] >= 0xD0 && q[1] <= 0xD7)) q++;
+        if (q + 1 >= bits.end) return ffail(P, "missing restart marker");
+        bits.p = q + 2;
+        bits.reset();
+        pred[0] = pred[1] = pred[2] = pred[3] = 0;
+      }
+      for (int k = 0; k < S.blocks_per_mcu; k++) {
+        const int i = bcomp[k];
+        memset(blk, 0, sizeof(blk));
+        const int t = bits.decode(P.dc[tdc[i]]);
+        if (t < 0 || t > 11) return ffail(P, "corrupt entropy-coded data (DC)");
+        const int diff = t ? extend(bits.get(t), t) : 0;
+        pred[i] += diff;
+        blk[0] = (int16_t)pred[i];
+        int last = blk[0] ? 0 : -1;
+        for (int kk = 1; kk < 64;) {
+          const int rs = bits.decode(P.ac[tac[i]]);
+          if (rs < 0) return ffail(P, "corrupt entropy-coded data (AC)");
+          const int r = rs >> 4, s = rs & 15;
+          if (s) {
+            kk += r;
+            if (kk > 63 || s > 10) return ffail(P, "corrupt entropy-coded data (AC run)");
+            blk[kk] = (int16_t)extend(bits.get(s), s);
+            last = kk;
+            kk++;
+          } else if (r == 15) {
+            kk += 16;
+          } else {
+            break;  // EOB
+          }
+        }
+        const int cnt = last + 1;
+        out->counts.push_back((uint8_t)cnt);
+        out->coefs.insert(out->coefs.end(), blk, blk + cnt);
+      }
+    }
+  }
+  (void)nmcu;
+  if (bits.underrun()) return ffail(P, "truncated or corrupt entropy-coded data");
+  H.nblocks += nb;
+  H.ngroups += S.mcus_y;
+  H.nscans++;
+  // continue parsing after the entropy-coded segment: at the marker the bit
+  // reader stopped on (or scan forward to the next non-RST marker)
+  size_t q = (size_t)(bits.p - P.d);
+  while (q + 1 < P.n && !(P.d[q] == 0xFF && P.d[q + 1] != 0x00 &&
+                          !(P.d[q + 1] >= 0xD0 && P.d[q + 1] <= 0xD7)))
+    q++;
+  P.pos = q;
+  return true;
+}
+
+// marker loop; full = false stops after the frame header (probe)
+bool parse(Parser& P, bool full, JpegDecoded* out) {
+  if (P.n < 4 || P.d[0] != 0xFF || P.d[1] != 0xD8) return ffail(P, "not a JPEG file");
+  P.pos = 2;
+  for (;;) {
+    const int m = next_marker(P);
+    if (m < 0) {
+      if (full && out->h.nscans > 0) break;  // missing EOI: tolerated, as libjpeg
+      return ffail(P, "unexpected end of file");
+    }
+    if (m == 0xD9) break;                              // EOI
+    if ((m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;  // stray RSTn / TEM
+    const uint8_t* b;
+    int len;
+    if (!segment(P, &b, &len)) return false;
+    if (m >= 0xC0 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+      if (!parse_sof(P, m, b, len)) return false;
+      if (!full) return true;
+    } else if (m == 0xC4) {
+      if (!parse_dht(P, b, len)) return false;
+    } else if (m == 0xCC) {
+      return ffail(P, "arithmetic-coded JPEG is not supported");
+    } else if (m == 0xDB) {
+      if (!parse_dqt(P, b, len)) return false;
+    } else if (m == 0xDD) {
+      if (len < 2) return ffail(P, "bad DRI");
+      P.restart = be16(b);
+    } else if (m == 0xDA) {
+      if (!full) return ffail(P, "SOS before SOF");
+      if (!decode_scan(P, b, len, out)) return false;
+    } else if (m == 0xE0) {
+      if (len >= 5 && !memcmp(b, "JFIF", 5)) P.jfif = true;
+    } else if (m == 0xEE) {
+      if (len >= 12 && !memcmp(b, "Adobe", 5)) {
+        P.adobe = true;
+        P.adobe_transform = b[11];
+      }
+    }
+    // other APPn, COM, DHP, EXP: skipped
+  }
+  if (!P.have_frame) return ffail(P, "no frame header");
+  return true;
+}
+
+// jdapimin.c default_decompress_parms: the colour space of a 3-component file
+int color_of(const Parser& P) {
+  if (P.nf == 1) return 0;
+  if (P.jfif) return 1;
+  if (P.adobe) return P.adobe_transform == 0 ? 2 : 1;
+  if (P.cid[0] == 'R' && P.cid[1] == 'G' && P.cid[2] == 'B') return 2;
+  return 1;
+}
+
+bool read_file(const char* path, std::vector<uint8_t>* buf) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return fail("jpeg: cannot open %s: %s", path, strerror(errno));
+  bool ok = fseek(f, 0, SEEK_END) == 0;
+  const long sz = ok ? ftell(f) : -1;
+  ok = ok && sz >= 0 && sz < (1l << 31) && fseek(f, 0, SEEK_SET) == 0;
+  if (ok) {
+    buf->resize((size_t)sz);
+    ok = fread(buf->data(), 1, (size_t)sz, f) == (size_t)sz;
+  }
+  fclose(f);
+  return ok || fail("jpeg: cannot read %s", path);
+}
+
+int64_t align16(int64_t v) { return (v + 15) & ~(int64_t)15; }
+
+}  // namespace
+
+bool jpeg_probe_mem(const uint8_t* d, size_t n, const char* name, UphipPnmInfo* info) {
+  Parser P{d, n, name};
+  if (!parse(P, false, nullptr)) return false;
+  info->width = P.w;
+  info->height = P.h;
+  info->format = P.nf == 1 ? UPHIP_FMT_GRAY8 : UPHIP_FMT_RGB24;
+  return true;
+}
+
+bool jpeg_entropy_decode(const uint8_t* d, size_t n, const char* name, JpegDecoded* out) {
+  try {
+    *out = JpegDecoded();
+    Parser P{d, n, name};
+    if (!parse(P, true, out)) return false;
+    if (out->h.nscans == 0) return ffail(P, "no scan");
+    out->h.color = color_of(P);
+    // every component must be covered by a scan
+    bool seen[3] = {false, false, false};
+    for (int s = 0; s < out->h.nscans; s++)
+      for (int i = 0; i < out->h.scan[s].ncomp; i++) seen[out->h.scan[s].comp[i]] = true;
+    for (int i = 0; i < P.nf; i++)
+      if (!seen[i]) return ffail(P, "a component is missing from the scans");
+    out->groups.push_back((uint32_t)out->coefs.size());
+    JpegHeader& H = out->h;
+    H.counts_off = align16((int64_t)sizeof(JpegHeader));
+    H.groups_off = align16(H.counts_off + H.nblocks);
+    H.coefs_off = align16(H.groups_off + 4 * (H.ngroups + 1));
+    H.total_bytes = align16(H.coefs_off + 2 * (int64_t)out->coefs.size());
+    return true;
+  } catch (const std::bad_alloc&) {
+    return fail("jpeg: %s: out of memory", name);
+  }
+}
+
+void jpeg_pack(const JpegDecoded& j, uint8_t* dst) {
+  const JpegHeader& H = j.h;
+  memset(dst, 0, (size_t)H.total_bytes);
+  memcpy(dst, &H, sizeof(H));
+  memcpy(dst + H.counts_off, j.counts.data(), j.counts.size());
+  memcpy(dst + H.groups_off, j.groups.data(), 4 * j.groups.size());
+  memcpy(dst + H.coefs_off, j.coefs.data(), 2 * j.coefs.size());
+}
+
+bool jpeg_read_file(const char* path, std::vector<uint8_t>* buf) { return read_file(path, buf); }
+
+}  // namespace uph
+
+namespace uph {
+
+// Entropy-decode on the host, upload, decode on the current device/stream
+// into device memory (synchronous).
+bool jpeg_decode_to_device(const uint8_t* data, size_t size, const char* name, uint8_t* ddst,
+                           int64_t pitch, UphipPnmInfo* info) {
+  JpegDecoded j;
+  if (!jpeg_entropy_decode(data, size, name, &j)) return false;
+  const JpegHeader& H = j.h;
+  const int fmt = H.ncomp == 1 ? UPHIP_FMT_GRAY8 : UPHIP_FMT_RGB24;
+  if (info) {
+    if (info->width > 0 && (info->width != H.width || info->height != H.height || info->format != fmt))
+      return fail("jpeg: %s is %dx%d format %d, expected %dx%d format %d", name, H.width, H.height,
+                  fmt, info->width, info->height, info->format);
+    info->width = H.width;
+    info->height = H.height;
+    info->format = fmt;
+  }
+  if (pitch < (int64_t)H.width * (H.ncomp == 1 ? 1 : 3)) return fail("jpeg: pitch too small");
+  std::vector<uint8_t> packed((size_t)H.total_bytes);
+  jpeg_pack(j, packed.data());
+  hipStream_t st = current_stream();
+  uint8_t* dp = (uint8_t*)scratch(0, (size_t)H.total_bytes);
+  uint8_t* ds = H.scratch_bytes ? (uint8_t*)scratch(1, (size_t)H.scratch_bytes) : nullptr;
+  if (!dp || (H.scratch_bytes && !ds)) return false;
+  return UPH_HIP(hipMemcpyAsync(dp, packed.data(), packed.size(), hipMemcpyHostToDevice, st)) &&
+         jpeg_launch(H, dp, ds, ddst, pitch, st) && UPH_HIP(hipStreamSynchronize(st));
+}
+
+}  // namespace uph
+
+using namespace uph;
+
+extern "C" {
+
+int uphip_jpeg_probe(const char* path, UphipPnmInfo* info) {
+  if (!path || !info) return fail("jpeg_probe: null argument"), -1;
+  // the frame header is near the start; read what there is up to 1 MiB
+  FILE* f = fopen(path, "rb");
+  if (!f) return fail("jpeg: cannot open %s: %s", path, strerror(errno)), -1;
+  std::vector<uint8_t> buf(1 << 20);
+  buf.resize(fread(buf.data(), 1, buf.size(), f));
+  fclose(f);
+  if (jpeg_probe_mem(buf.data(), buf.size(), path, info)) return 0;
+  // a header past the first MiB (large APPn segments): the whole file
+  uphip_clear_error();
+  if (!jpeg_read_file(path, &buf)) return -1;
+  return jpeg_probe_mem(buf.data(), buf.size(), path, info) ? 0 : -1;
+}
+
+int64_t uphip_jpeg_entropy_decode(const void* data, size_t size, void* packed, int64_t capacity) {
+  if (!data) return fail("jpeg_entropy_decode: null argument"), -1;
+  JpegDecoded j;
+  if (!jpeg_entropy_decode((const uint8_t*)data, size, "<memory>", &j)) return -1;
+  if (packed && capacity >= j.h.total_bytes) jpeg_pack(j, (uint8_t*)packed);
+  return j.h.total_bytes;
+}
+
+int uphip_jpeg_decode(const void* data, size_t size, void* device_dst, int64_t pitch,
+                      UphipPnmInfo* info) {
+  if (!data || !device_dst) return fail("jpeg_decode: null argument"), -1;
+  if (!runtime_ready()) return fail("jpeg_decode: no HIP device"), -1;
+  return jpeg_decode_to_device((const uint8_t*)data, size, "<memory>", (uint8_t*)device_dst, pitch,
+                               info)
+             ? 0
+             : -1;
+}
+
+int uphip_jpeg_read(const char* path, void* dst, int64_t linesize, const UphipPnmInfo* expect) {
+  if (!path || !dst) return fail("jpeg_read: null argument"), -1;
+  if (!runtime_ready()) return fail("jpeg_read: no HIP device (JPEG decodes on the device)"), -1;
+  std::vector<uint8_t> file;
+  if (!jpeg_read_file(path, &file)) return -1;
+  UphipPnmInfo info{0, 0, 0};
+  if (!jpeg_probe_mem(file.data(), file.size(), path, &info)) return -1;
+  if (expect && (expect->width != info.width || expect->height != info.height ||
+                 expect->format != info.format))
+    return fail("jpeg: %s is %dx%d format %d, expected %dx%d format %d", path, info.width,
+                info.height, info.format, expect->width, expect->height, expect->format),
+           -1;
+  const int64_t rb = row_bytes(info.width, info.format);
+  if (linesize < rb) return fail("jpeg_read: linesize too small"), -1;
+  const int64_t dpitch = (rb + 255) & ~(int64_t)255;
+  uint8_t* dd = (uint8_t*)scratch(2, (size_t)(dpitch * info.height));
+  if (!dd || !jpeg_decode_to_device(file.data(), file.size(), path, dd, dpitch, &info)) return -1;
+  return UPH_HIP(hipMemcpy2D(dst, (size_t)linesize, dd, (size_t)dpitch, (size_t)rb,
+                             (size_t)info.height, hipMemcpyDeviceToHost))
+             ? 0
+             : -1;
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+// jpeg.h — the JPEG decode peer: the layout shared by the
+// host entropy decoder (jpeg.cpp) and the device kernels (kernels_jpeg.hip).
+//
+// The reference decodes JPEG pages through FFmpeg on the CPU path
+// (file.c:29-128 loadImage; the batch decode queue converts YUV frames to
+// RGB24 with swscale, sheet_stages.c:99-122) and through nvImageCodec on the
+// GPU path (imageprocess/nvimgcodec.c:679-1007).  Here the sequential part --
+// marker parsing and Huffman decoding -- runs on the host, and the data-
+// parallel part -- dequantisation, the inverse DCT, chroma upsampling and
+// YCbCr->RGB -- runs on the device, straight into a page buffer (a batch's
+// input slot in the runner).
+//
+// What is decoded: baseline and extended-sequential Huffman JPEG, 8-bit, one
+// component (-> GRAY8) or three (YCbCr -> RGB24, or RGB when the file says
+// so), sampling factors 1 or 2, restart intervals, any number of sequential
+// scans.  Progressive, arithmetic-coded, 12-bit, lossless and CMYK files are
+// refused with an error.  Pixel arithmetic follows libjpeg's defaults
+// (jidctint.c islow IDCT, jdsample.c fancy upsampling, jdcolor.c
+// ycc_rgb_convert) -- checked against PIL's libjpeg-turbo; FFmpeg's decoder
+// (the reference's) has its own IDCT and swscale conversion: parity with it
+// is unpinned.
+//
+// Packed layout (one contiguous buffer, uploaded as is):
+//   JpegHeader | counts (u8 per block, decode order) | group offsets (u32 per
+//   group + 1, int16 units into coefs) | coefs (int16, each block's zigzag
+//   prefix up to its last non-zero coefficient, pre-multiplied by nothing:
+//   the device dequantises)
+// A group is one MCU row of one scan (the unit the device prefix-sums).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "unpaper_hip.h"
+
+namespace uph {
+
+constexpr int kJpegMaxScans = 8;
+
+struct JpegComp {
+  int32_t h, v;          // sampling factors
+  int32_t bw, bh;        // blocks allocated in the component plane (MCU-padded)
+  int32_t dw, dh;        // downsampled width/height in samples (libjpeg's downsampled_*)
+  int64_t plane_off;     // byte offset of the plane in the device scratch (colour)
+  int32_t pitch;         // plane pitch = bw * 8
+  uint16_t qzz[64];      // quantisation table in zigzag order
+};
+
+struct JpegScan {
+  int32_t ncomp;          // components in the scan (1 = non-interleaved)
+  int32_t comp[4];        // their indices
+  int32_t mcus_x, mcus_y; // MCUs (or, non-interleaved, blocks) across / down
+  int32_t blocks_per_mcu;
+  int64_t first_block;    // index of the scan's first block in decode order
+  int32_t first_group;    // index of the scan's first group (MCU row)
+};
+
+struct JpegHeader {
+  int32_t width, height;
+  int32_t ncomp;          // 1 or 3
+  int32_t color;          // 0 gray, 1 YCbCr -> RGB, 2 RGB (no transform)
+  int32_t hmax, vmax;
+  JpegComp comp[3];
+  int32_t nscans;
+  JpegScan scan[kJpegMaxScans];
+  int64_t nblocks, ngroups;
+  int64_t counts_off, groups_off, coefs_off, total_bytes;  // within the packed buffer
+  int64_t scratch_bytes;  // device planes needed (colour; 0 for gray)
+};
+
+// jpeg_natural_order: zigzag index -> natural (row-major) index
+constexpr uint8_t kJpegNatural[64] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+    12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+    35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+// Host half: a decoded file's coefficients before packing.
+struct JpegDecoded {
+  JpegHeader h{};
+  std::vector<uint8_t> counts;    // per block: length of the zigzag prefix kept
+  std::vector<uint32_t> groups;   // per group (MCU row of a scan) + 1: coefficient offset
+  std::vector<int16_t> coefs;
+};
+
+// Marker parse + Huffman decode of a whole file image (thread-safe; errors
+// through fail()).  Sets the packed offsets (h.*_off, h.total_bytes).
+bool jpeg_entropy_decode(const uint8_t* data, size_t size, const char* name, JpegDecoded* out);
+// Writes the packed layout (h.total_bytes bytes) to dst.
+void jpeg_pack(const JpegDecoded& j, uint8_t* dst);
+// Device half: the packed image `dpacked` (device memory) into dst (rows dpitch
+// apart) on stream st; scratch holds h.scratch_bytes (colour planes).
+bool jpeg_launch(const JpegHeader& h, const uint8_t* dpacked, uint8_t* scratch, uint8_t* dst,
+                 int64_t dpitch, hipStream_t st);
+bool jpeg_read_file(const char* path, std::vector<uint8_t>* buf);
+// the pixel format a decoded header yields (GRAY8 or RGB24)
+inline int jpeg_format(const JpegHeader& h) { return h.ncomp == 1 ? UPHIP_FMT_GRAY8 : UPHIP_FMT_RGB24; }
+
+}  // namespace uph

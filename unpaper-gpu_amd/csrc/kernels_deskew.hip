@@ -21,9 +21,12 @@
 // with the step) and bands too wide for LDS (very large angle ranges) are
 // flagged and walked by k_rot_line, a direct per-line restatement.
 #include <climits>
+#include <mutex>
+#include <vector>
 #include <cmath>
 
 #include "filters.h"
+#include "libm_glibc.h"
 
 namespace uph {
 
@@ -697,6 +700,20 @@ float combine_edge_rotations(const float* rotation, int count, float deviation_r
   for (int i = 0; i < count; i++) total += pw(rotation[i] - average, 2);
   float deviation = sqrtf(total);
   return deviation <= deviation_rad ? average : 0.0f;
+}
+
+const uint32_t* glibc_pow2_table(int* n) {
+  static std::vector<uint32_t> table;
+  static bool ok = false;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    static float (*volatile pw)(float, float) = powf;  // the process's glibc, not a fold
+    glibc::build_pow2_table(pw, table);
+    ok = true;
+    for (uint32_t v : table) ok = ok && v != 0xffffffffu;
+  });
+  *n = (int)table.size();
+  return ok ? table.data() : nullptr;
 }
 
 }  // namespace uph

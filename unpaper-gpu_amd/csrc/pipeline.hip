@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "filters.h"
+#include "libm_glibc.h"
 #include "runtime.h"
 
 namespace uph {
@@ -220,8 +221,10 @@ struct RotSelectArgs {
   UphipRectangle dummy;
 };
 
-// detect_edge_rotation's argmax + detect_rotation_cpu's combination (exact via
-// the host-computed table for <= 2 edges) -> RotateArgs for deskew
+// detect_edge_rotation's argmax + detect_rotation_cpu's combination -> RotateArgs
+// for deskew.  <= 2 edges: the host-computed table (host libm); > 2 edges:
+// deskew.c:219-240 and :260-261 on the device with glibc's sinf/cosf/powf
+// restated bit for bit (libm_glibc.h).  `only`
 // only (may be null): other sheets get an inactive RotateArgs and keep their ctl.
 // One wave per sheet: the lanes scan the angles in strides, then a wave
 // reduction keeps the largest peak and, among equal ones, the first angle --
@@ -230,7 +233,8 @@ struct RotSelectArgs {
 __global__ void __launch_bounds__(64) k_rot_select(SheetCtl* ctl, const int32_t* peaks,
                                                    const RotTable* table, const RotCombo* combo,
                                                    RotSelectArgs a, RotateArgs* out, int count,
-                                                   const int32_t* only) {
+                                                   const int32_t* only, const uint32_t* pow2,
+                                                   int npow2) {
   const int s = blockIdx.x, lane = threadIdx.x;
   if (s >= count) return;
   if (only && !only[s]) {
@@ -268,19 +272,20 @@ __global__ void __launch_bounds__(64) k_rot_select(SheetCtl* ctl, const int32_t*
     if (a.nedges == 2) key = idx[0] * a.nangles + idx[1];
     r = combo[key];
   } else {
-    // > 2 edges: device arithmetic (sin/cos/pow may differ from glibc by 1 ulp)
+    // > 2 edges: the reference's float expressions in its order, IEEE division
+    // and square root, glibc's powf(d, 2) and sinf/cosf (libm_glibc.h)
     float rot[4], total = 0.0f;
     for (int e = 0; e < a.nedges; e++) {
       const float v = table->angle[idx[e]];
       rot[e] = a.negate[e] ? -v : v;
       total += rot[e];
     }
-    const float avg = total / a.nedges;
+    const float avg = __fdiv_rn(total, (float)a.nedges);
     float t2 = 0.0f;
-    for (int e = 0; e < a.nedges; e++) t2 += (rot[e] - avg) * (rot[e] - avg);
-    r.result = sqrtf(t2) <= a.deviation_rad ? avg : 0.0f;
-    r.sinv = sinf(-r.result);
-    r.cosv = cosf(-r.result);
+    for (int e = 0; e < a.nedges; e++) t2 += glibc::pow2(rot[e] - avg, pow2, npow2);
+    r.result = __fsqrt_rn(t2) <= a.deviation_rad ? avg : 0.0f;
+    r.sinv = glibc::sinf(-r.result);
+    r.cosv = glibc::cosf(-r.result);
   }
   if (i < UPHIP_MAX_PAGES) c.rotation[i] = active ? r.result : 0.0f;
   RotateArgs ra;
@@ -434,6 +439,8 @@ struct UphipBatch {
   RotTable table{};
   RotTable* dtable = nullptr;
   RotCombo* dcombo = nullptr;
+  uint32_t* dpow2 = nullptr;           // > 2 edges: glibc powf(x, 2) exceptions (libm_glibc.h)
+  int npow2 = 0;
   int max_scan = 0;
   float max_angle = 0.0f;  // largest |angle| of the scan table (rotation bound)
   int32_t* peaks = nullptr;
@@ -800,6 +807,12 @@ static bool allocate(UphipBatch* b) {
     }
     b->dcombo = dalloc<RotCombo>(b, ncombo);
     UPH_HIP(hipMemcpy(b->dcombo, combo.data(), sizeof(RotCombo) * ncombo, hipMemcpyHostToDevice));
+    if (nedges > 2) {
+      const uint32_t* t = glibc_pow2_table(&b->npow2);
+      if (!t) return fail("batch: this libm's powf(x, 2) is not reproducible on the device");
+      b->dpow2 = dalloc<uint32_t>(b, imax(b->npow2, 1));
+      UPH_HIP(hipMemcpy(b->dpow2, t, sizeof(uint32_t) * b->npow2, hipMemcpyHostToDevice));
+    }
     b->peaks = dalloc<int32_t>(b, (size_t)cap * UPHIP_MAX_PAGES * 4 * (na > 0 ? na : 1));
     int ms = o.deskew_parameters.deskewScanSize;
     if (ms == -1 || ms > 10000) ms = 10000;
@@ -1110,13 +1123,16 @@ static void border_all(UphipBatch* b, int count, bool rows_ready) {
 // the sheet unchanged and nothing writes the sheet between the decode and
 // the filters (sheet_stages.c:187-325: pre-mirror, -shift, -masks,
 // -stretch/size, -wipes, -border all off).
-static bool decode_fused(const UphipBatch* b, const uint8_t* src, int64_t spitch) {
+static bool decode_fused(const UphipBatch* b, const uint8_t* src, int64_t spitch,
+                         int64_t sstride) {
   const UphipOptions& o = b->o;
   const uint32_t dis = o.disable;
   if (b->work_fmt != F_GRAY8 || b->geo.page_format != F_GRAY8 || b->n_in != 1) return false;
   if (b->rp_w != b->sheet_w || b->rp_h != b->sheet_h || o.pre_rotate != 0) return false;
   if (b->sheet_w != b->W || b->sheet_h != b->H) return false;  // stretch / page size
-  if (((uintptr_t)src & 15) || (spitch & 15)) return false;
+  // 16-byte vector loads at src + s*sstride + y*spitch (a row's last vector
+  // may read up to 15 bytes past the row within its pitch)
+  if (((uintptr_t)src & 15) || (spitch & 15) || (sstride & 15)) return false;
   if (o.pre_mirror.horizontal || o.pre_mirror.vertical) return false;
   if (o.pre_shift.horizontal != 0 || o.pre_shift.vertical != 0 || o.pre_mask_count > 0) return false;
   if (!(dis & UPHIP_NO_WIPE) && o.pre_wipes.count > 0) return false;
@@ -1142,7 +1158,7 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
   int32_t w = b->sheet_w, h = b->sheet_h;
   Planes S0 = planes_of(b, w, h);
   const bool covered = n == 1 && b->rp_w == w && b->rp_h == h;
-  const bool fused = decode_fused(b, src, spitch);
+  const bool fused = decode_fused(b, src, spitch, sstride);
   // what the fused decode hands on
   const bool black_on = !(dis & UPHIP_NO_BLACKFILTER) && b->bgeo.nbars > 0;
   const bool vsum_ready = fused && black_on && b->bgeo.vregion.x1 >= b->bgeo.vregion.x0;
@@ -1311,7 +1327,7 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
       ra.mask_index = i;
       hipLaunchKernelGGL(k_rot_select, dim3(count), dim3(64), 0, b->st, b->ctl,
                          b->peaks, b->dtable, b->dcombo, ra, b->rot_args + (int64_t)i * b->cap,
-                         count, only);
+                         count, only, b->dpow2, b->npow2);
     };
     const bool linear = o.interpolate_type == UPHIP_INTERP_LINEAR &&
                         (P.fmt == F_GRAY8 || P.fmt == F_RGB24);
@@ -1672,11 +1688,14 @@ int uphip_batch_download_async(UphipBatch* b, void* host, int64_t linesize, int6
   };
   if (linesize == sp && sheet_stride == sp * b->out_h && ss == sheet_stride) {
     // host staging laid out like the planes: runs of sheets in the same plane
-    // go as one linear DMA copy (2D copies run far below the link rate)
+    // go as one linear DMA copy (2D copies run far below the link rate); the
+    // last sheet of a run ends at its last row, so a caller's buffer need not
+    // pad its final sheet to a whole stride
+    const int64_t extent = (int64_t)(b->out_h - 1) * sp + rb;
     for (int s = 0; s < n;) {
       int e = s + 1;
       while (e < n && (b->out || (cur[e] & 1) == (cur[s] & 1))) e++;
-      if (!UPH_HIP(hipMemcpyAsync(h + s * sheet_stride, src_of(s), (size_t)((e - s) * ss),
+      if (!UPH_HIP(hipMemcpyAsync(h + s * sheet_stride, src_of(s), (size_t)((e - s - 1) * ss + extent),
                                   hipMemcpyDeviceToHost, b->st)))
         return -1;
       s = e;

@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <vector>
 
 #include "runtime.h"
@@ -35,6 +36,7 @@ namespace {
 constexpr uint8_t kSig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
 constexpr int64_t kMaxSide = 1 << 20;    // as the PNM reader
 constexpr int64_t kMaxRaster = 1ll << 34;
+constexpr uint64_t kMaxIdat = 2ull * kMaxRaster;  // stored deflate blocks stay far below
 
 uint32_t be32(const uint8_t* p) {
   return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
@@ -63,6 +65,14 @@ bool parse(FILE* f, Png* p, bool full, const char* path) {
   if (fread(sig, 1, 8, f) != 8 || memcmp(sig, kSig, 8) != 0) return fail("png: %s: not a PNG file", path);
   bool have_ihdr = false, have_iend = false;
   std::vector<uint8_t> buf;
+  // chunk lengths are checked against what the file holds before anything is
+  // sized from them (a few crafted bytes must not allocate gigabytes)
+  long file_size = -1;
+  {
+    const long at = ftell(f);
+    if (at >= 0 && fseek(f, 0, SEEK_END) == 0) file_size = ftell(f);
+    if (at < 0 || fseek(f, at, SEEK_SET) != 0) return fail("png: %s: cannot seek", path);
+  }
   for (;;) {
     uint8_t hd[8];
     if (fread(hd, 1, 8, f) != 8) break;
@@ -72,6 +82,13 @@ bool parse(FILE* f, Png* p, bool full, const char* path) {
     const bool want = type == 0x49484452u /*IHDR*/ || type == 0x504C5445u /*PLTE*/ ||
                       type == 0x74524E53u /*tRNS*/ || (full && type == 0x49444154u /*IDAT*/);
     if (!have_ihdr && type != 0x49484452u) return fail("png: %s: first chunk is not IHDR", path);
+    if (file_size >= 0 && (long)len + 4 > file_size - ftell(f))
+      return fail("png: %s: truncated chunk", path);
+    if ((type == 0x49484452u && len != 13) || (type == 0x504C5445u && len > 768) ||
+        (type == 0x74524E53u && len > 256))
+      return fail("png: %s: bad chunk length", path);
+    if (type == 0x49444154u && p->idat.size() + len > kMaxIdat)
+      return fail("png: %s: compressed data larger than any valid raster", path);
     if (want) {
       uint8_t* dst;
       if (type == 0x49444154u) {
@@ -311,11 +328,14 @@ bool decode(Png& p, uint8_t* out, int64_t linesize, const char* path) {
   return in.finish() || fail("png: %s: corrupt image data (stream end, checksum)", path);
 }
 
-bool is_png(FILE* f) {
+// the file's signature: 1 PNG, 2 JPEG (SOI + a marker), 0 anything else (PNM)
+int sniff(FILE* f) {
   uint8_t sig[8];
-  const bool yes = fread(sig, 1, 8, f) == 8 && memcmp(sig, kSig, 8) == 0;
+  const size_t n = fread(sig, 1, 8, f);
   rewind(f);
-  return yes;
+  if (n == 8 && memcmp(sig, kSig, 8) == 0) return 1;
+  if (n >= 3 && sig[0] == 0xFF && sig[1] == 0xD8 && sig[2] == 0xFF) return 2;
+  return 0;
 }
 
 }  // namespace
@@ -330,7 +350,12 @@ int uphip_png_probe(const char* path, UphipPnmInfo* info) {
   FILE* f = fopen(path, "rb");
   if (!f) return fail("png: cannot open %s: %s", path, strerror(errno)), -1;
   Png p;
-  const bool ok = parse(f, &p, false, path);
+  bool ok;
+  try {
+    ok = parse(f, &p, false, path);
+  } catch (const std::bad_alloc&) {
+    ok = fail("png: %s: out of memory", path);
+  }
   fclose(f);
   if (!ok) return -1;
   info->width = (int32_t)p.w;
@@ -344,7 +369,12 @@ int uphip_png_read(const char* path, void* dst, int64_t linesize, const UphipPnm
   FILE* f = fopen(path, "rb");
   if (!f) return fail("png: cannot open %s: %s", path, strerror(errno)), -1;
   Png p;
-  const bool ok = parse(f, &p, true, path);
+  bool ok;
+  try {
+    ok = parse(f, &p, true, path);
+  } catch (const std::bad_alloc&) {
+    ok = fail("png: %s: out of memory", path);
+  }
   fclose(f);
   if (!ok) return -1;
   if (expect && (expect->width != p.w || expect->height != p.h || expect->format != p.fmt))
@@ -352,27 +382,36 @@ int uphip_png_read(const char* path, void* dst, int64_t linesize, const UphipPnm
                 (long long)p.h, p.fmt, expect->width, expect->height, expect->format),
            -1;
   if (linesize < row_bytes((int32_t)p.w, p.fmt)) return fail("png_read: linesize too small"), -1;
-  return decode(p, (uint8_t*)dst, linesize, path) ? 0 : -1;
+  try {
+    return decode(p, (uint8_t*)dst, linesize, path) ? 0 : -1;
+  } catch (const std::bad_alloc&) {
+    return fail("png: %s: out of memory", path), -1;
+  }
 }
 
-// loadImage's peer over the two host codecs: the file's signature picks PNG
+// loadImage's peer over the codecs: the file's signature picks PNG, JPEG
+// (entropy-decoded on the host, pixels made on the current device: jpeg.cpp)
 // or PNM.
 int uphip_image_probe(const char* path, UphipPnmInfo* info) {
   if (!path || !info) return fail("image_probe: null argument"), -1;
   FILE* f = fopen(path, "rb");
   if (!f) return fail("image: cannot open %s: %s", path, strerror(errno)), -1;
-  const bool png = is_png(f);
+  const int kind = sniff(f);
   fclose(f);
-  return png ? uphip_png_probe(path, info) : uphip_pnm_probe(path, info);
+  return kind == 1 ? uphip_png_probe(path, info)
+       : kind == 2 ? uphip_jpeg_probe(path, info)
+                   : uphip_pnm_probe(path, info);
 }
 
 int uphip_image_read(const char* path, void* dst, int64_t linesize, const UphipPnmInfo* expect) {
   if (!path || !dst) return fail("image_read: null argument"), -1;
   FILE* f = fopen(path, "rb");
   if (!f) return fail("image: cannot open %s: %s", path, strerror(errno)), -1;
-  const bool png = is_png(f);
+  const int kind = sniff(f);
   fclose(f);
-  return png ? uphip_png_read(path, dst, linesize, expect) : uphip_pnm_read(path, dst, linesize, expect);
+  return kind == 1 ? uphip_png_read(path, dst, linesize, expect)
+       : kind == 2 ? uphip_jpeg_read(path, dst, linesize, expect)
+                   : uphip_pnm_read(path, dst, linesize, expect);
 }
 
 }  // extern "C"

@@ -34,6 +34,7 @@
 #include <thread>
 #include <vector>
 
+#include "jpeg.h"
 #include "runtime.h"
 
 using Clock = std::chrono::steady_clock;
@@ -142,7 +143,11 @@ struct HostRegistration {
   size_t bytes = 0;
   bool tried = false;
   bool ok = false;
+  std::mutex mu;  // a source or sink may be shared by runners on other threads
+  // Registers [p, p + n) once; n is the extent the runner reads or writes,
+  // not a whole number of strides (the caller's last page need not be padded).
   bool ensure(const void* p, size_t n) {
+    std::lock_guard<std::mutex> lk(mu);
     if (tried) return ok;
     tried = true;
     ok = hipHostRegister(const_cast<void*>(p), n, hipHostRegisterDefault) == hipSuccess;
@@ -314,7 +319,22 @@ void uphip_sink_destroy(UphipSink* k) { delete k; }
 // ---------------------------------------------------------------------------
 namespace {
 
+// A JPEG page of a chunk: entropy-decoded by a load task into pinned memory
+// (jpeg.h packed layout); the device thread uploads it and decodes it on the
+// slot's stream straight into the batch's input slot before the run.
+struct JpegPage {
+  uint8_t* host = nullptr;  // pinned, grown on demand
+  size_t cap = 0;
+  bool on = false;          // this chunk's page is a JPEG waiting for the device
+  JpegHeader h{};
+};
+
 struct Slot {
+  std::vector<JpegPage> jpg;  // per page of the chunk (sheet * input_count + page)
+  uint8_t* djpg = nullptr;    // device copies of the chunk's packed JPEG pages
+  size_t djpg_cap = 0;
+  uint8_t* dscr = nullptr;    // colour planes (one page at a time on the stream)
+  size_t dscr_cap = 0;
   UphipBatch* b = nullptr;
   uint8_t* hin = nullptr;   // pinned input staging (count * input_count pages)
   uint8_t* hout = nullptr;  // pinned output staging (count sheets)
@@ -411,12 +431,93 @@ void store_sheet(UphipRunner* r, const UphipSink* k, int64_t job, const uint8_t*
   }
 }
 
-bool load_page(UphipRunner* r, const UphipSource* s, int64_t job, int32_t j, uint8_t* dst) {
+bool is_jpeg_file(const std::string& path) {
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) return false;
+  uint8_t sig[3];
+  const bool yes = fread(sig, 1, 3, f) == 3 && sig[0] == 0xFF && sig[1] == 0xD8 && sig[2] == 0xFF;
+  fclose(f);
+  return yes;
+}
+
+// The host half of a JPEG page into the slot's pinned buffer `jp`.
+bool jpeg_load(UphipRunner* r, const std::string& path, JpegPage* jp) {
+  std::vector<uint8_t> file;
+  JpegDecoded d;
+  if (!jpeg_read_file(path.c_str(), &file) ||
+      !jpeg_entropy_decode(file.data(), file.size(), path.c_str(), &d))
+    return false;
+  if (d.h.width != r->geo.page_width || d.h.height != r->geo.page_height ||
+      jpeg_format(d.h) != r->geo.page_format)
+    return fail("jpeg: %s is %dx%d format %d, expected %dx%d format %d", path.c_str(), d.h.width,
+                d.h.height, jpeg_format(d.h), r->geo.page_width, r->geo.page_height,
+                r->geo.page_format);
+  const size_t need = (size_t)d.h.total_bytes;
+  if (jp->cap < need) {
+    if (jp->host) hipHostFree(jp->host);
+    jp->host = nullptr;
+    jp->cap = 0;
+    if (!UPH_HIP(hipHostMalloc((void**)&jp->host, need + need / 4, hipHostMallocDefault))) return false;
+    jp->cap = need + need / 4;
+  }
+  jpeg_pack(d, jp->host);
+  jp->h = d.h;
+  jp->on = true;
+  return true;
+}
+
+bool load_page(UphipRunner* r, const UphipSource* s, int64_t job, int32_t j, uint8_t* dst,
+               JpegPage* jp) {
   const UphipPnmInfo geo{r->geo.page_width, r->geo.page_height, r->geo.page_format};
   const int64_t idx = job * r->opts.input_count + j;
   if (s->load) return s->load(s->user, job, j, dst, r->in_pitch) == 0;
   if (s->base) return mem_load(s, idx, dst, r->in_pitch, geo) == 0;
+  if (idx >= 0 && idx < (int64_t)s->paths.size() && is_jpeg_file(s->paths[(size_t)idx]))
+    return jpeg_load(r, s->paths[(size_t)idx], jp);
   return pnm_load(s, idx, dst, r->in_pitch, geo) == 0;
+}
+
+// Queue the chunk's JPEG pages on the slot's stream: upload each packed page,
+// then decode it into its input slot (after the staging upload, before the run).
+bool jpeg_submit(Slot* sl, int npages) {
+  size_t total = 0, scr = 0;
+  for (int p = 0; p < npages; p++) {
+    const JpegPage& jp = sl->jpg[(size_t)p];
+    if (!jp.on) continue;
+    total += (size_t)jp.h.total_bytes;
+    scr = std::max(scr, (size_t)jp.h.scratch_bytes);
+  }
+  if (!total) return true;
+  // the slot's stream is idle here (the slot was free): old buffers can go
+  if (sl->djpg_cap < total) {
+    if (sl->djpg) hipFree(sl->djpg);
+    sl->djpg = nullptr;
+    sl->djpg_cap = 0;
+    if (!UPH_HIP(hipMalloc((void**)&sl->djpg, total + total / 4))) return false;
+    sl->djpg_cap = total + total / 4;
+  }
+  if (scr && sl->dscr_cap < scr) {
+    if (sl->dscr) hipFree(sl->dscr);
+    sl->dscr = nullptr;
+    sl->dscr_cap = 0;
+    if (!UPH_HIP(hipMalloc((void**)&sl->dscr, scr))) return false;
+    sl->dscr_cap = scr;
+  }
+  hipStream_t st = (hipStream_t)uphip_batch_stream(sl->b);
+  size_t off = 0;
+  for (int p = 0; p < npages; p++) {
+    JpegPage& jp = sl->jpg[(size_t)p];
+    if (!jp.on) continue;
+    int64_t pitch = 0;
+    uint8_t* dst = (uint8_t*)uphip_batch_input_ptr(sl->b, p, &pitch);
+    if (!dst ||
+        !UPH_HIP(hipMemcpyAsync(sl->djpg + off, jp.host, (size_t)jp.h.total_bytes,
+                                hipMemcpyHostToDevice, st)) ||
+        !jpeg_launch(jp.h, sl->djpg + off, sl->dscr, dst, pitch, st))
+      return false;
+    off += (size_t)jp.h.total_bytes;
+  }
+  return true;
 }
 
 // per-sheet device status after a finished run: a failing wait names the
@@ -491,10 +592,16 @@ UphipRunner* uphip_runner_create(const UphipOptions* options, const UphipBatchGe
       uphip_batch_device_bytes(b, &bb);
       r->batch_bytes = bb;
       if (config->batches_per_device <= 0) {
+        // per slot: the batch, plus the dense input chunk a direct memory
+        // source is copied into (allocated at the first host run)
+        int64_t ip = 0;
+        uphip_batch_input_ptr(b, 0, &ip);
+        const int64_t din = ip * r->geo.page_height * r->geo.capacity *
+                            (options->input_count > 0 ? options->input_count : 1);
         size_t fr = 0, tot = 0;
         int n = 1;
         if (hipMemGetInfo(&fr, &tot) == hipSuccess && bb > 0)
-          n = 1 + (int)std::min<int64_t>((int64_t)(fr / 2) / bb, 15);
+          n = 1 + (int)std::min<int64_t>((int64_t)(fr / 2) / (bb + din), 15);
         r->cfg.batches_per_device = n;
       }
       dc.slots.resize((size_t)r->cfg.batches_per_device);
@@ -546,6 +653,10 @@ void uphip_runner_destroy(UphipRunner* r) {
       if (sl.hin) hipHostFree(sl.hin);
       if (sl.hout) hipHostFree(sl.hout);
       if (sl.din) hipFree(sl.din);
+      if (sl.djpg) hipFree(sl.djpg);
+      if (sl.dscr) hipFree(sl.dscr);
+      for (JpegPage& jp : sl.jpg)
+        if (jp.host) hipHostFree(jp.host);
     }
   }
   delete r;
@@ -658,11 +769,20 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
   // reads in place (uphip_batch_run_device takes any pitch); a memory sink
   // laid out like the batch's output rows receives the D2H copy itself.
   const int oc = r->opts.output_count < 1 ? 1 : r->opts.output_count;
+  // The direct source needs pages the batch can read in place: rows at least
+  // a row long and pages that do not overlap (page_stride 0, a repeated page,
+  // or overlapping pages take the staged path, which copies page by page).
+  const int64_t in_row = row_bytes(r->geo.page_width, r->geo.page_format);
+  const int64_t in_extent = (int64_t)(r->geo.page_height - 1) * src->linesize + in_row;
   const bool dsrc = src->base && !src->load && src->npages >= njobs * nin && njobs > 0 &&
-                    src->reg.ensure(src->base, (size_t)(src->npages * src->page_stride));
+                    src->linesize >= in_row && src->page_stride >= in_extent &&
+                    src->reg.ensure(src->base, (size_t)((src->npages - 1) * src->page_stride + in_extent));
+  const int64_t out_extent =
+      (int64_t)(r->out_h - 1) * r->out_linesize + row_bytes(r->out_w, r->out_fmt);
   const bool dsnk = sink->base && !sink->store && oc == 1 && sink->nsheets >= njobs && njobs > 0 &&
                     sink->linesize == r->out_linesize && sink->sheet_stride == r->out_sheet_stride &&
-                    sink->reg.ensure(sink->base, (size_t)(sink->nsheets * sink->sheet_stride));
+                    sink->reg.ensure(sink->base,
+                                     (size_t)((sink->nsheets - 1) * sink->sheet_stride + out_extent));
   if (dsrc) {
     const size_t need = (size_t)(src->page_stride * S * nin);
     const int caller_dev = uphip_get_device();
@@ -744,7 +864,7 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
             sl->count = (int32_t)std::min<int64_t>(S, njobs - first);
             sl->failed.assign((size_t)sl->count, 0);
             if (dsrc) {  // one DMA copy from the caller's pages, then the run
-              const size_t bytes = (size_t)(sl->count * nin * src->page_stride);
+              const size_t bytes = (size_t)((sl->count * nin - 1) * src->page_stride + in_extent);
               hipStream_t bst = (hipStream_t)uphip_batch_stream(sl->b);
               if (!UPH_HIP(hipMemcpyAsync(sl->din, src->base + first * nin * src->page_stride, bytes,
                                           hipMemcpyHostToDevice, bst)) ||
@@ -762,6 +882,8 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
               progress = true;
               continue;
             }
+            if (sl->jpg.size() < (size_t)(sl->count * nin)) sl->jpg.resize((size_t)(sl->count * nin));
+            for (JpegPage& jp : sl->jpg) jp.on = false;
             pend[k] = sl->count;
             state[k] = LOADING;
             phase[k] = LOADING;
@@ -770,7 +892,7 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
                 const auto a = Clock::now();
                 for (int j = 0; j < nin; j++) {
                   uint8_t* dst = sl->hin + ((int64_t)s * nin + j) * r->in_page_stride;
-                  if (!load_page(r, src, first + s, j, dst)) {
+                  if (!load_page(r, src, first + s, j, dst, &sl->jpg[(size_t)(s * nin + j)])) {
                     sl->failed[(size_t)s] |= 4;
                     uphip_clear_error();
                     // the slot still runs: a blank (white) page, cheap and
@@ -787,7 +909,7 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
           }
           if (st == LOADED && phase[k] == LOADING) {
             if (uphip_batch_upload_async(sl->b, sl->count, sl->hin, r->in_pitch, r->in_page_stride) != 0 ||
-                uphip_batch_run(sl->b, sl->count) != 0) {
+                !jpeg_submit(sl, sl->count * nin) || uphip_batch_run(sl->b, sl->count) != 0) {
               note("run failed");
               for (int s = 0; s < sl->count; s++) sl->failed[(size_t)s] |= 1;
               phase[k] = STORING;  // accounted (all failed) on the next pass
