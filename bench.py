@@ -103,7 +103,8 @@ def parse():
                     help="0 = the host share: OMP_NUM_THREADS, else os.cpu_count()")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-host-io", action="store_true", help="skip figures 2 and 3")
-    ap.add_argument("--no-latency", action="store_true", help="skip the C2 single-page latency")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the C2 single-page latency and the C4 single-sheet runs")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the C4 object of the default line (16 RGB24 sheets, verified)")
     ap.add_argument("--host-batch", type=int, default=32, help="sheets per batch, host-fed runs")
@@ -446,22 +447,34 @@ def run_c4(args, L, d, devices, firsts, n_gpus, version, valid, nsheets=0, steps
         checked, bad = verify_resident(r, devices[:1], firsts, nsheets, bsz,
                                        load_hashes("c4_hashes.json", "sheets"))
     r.close()
-    # one sheet alone on an idle GPU: latency, and the rotate launch
-    lat, rot, lat_stages = [], [], {}
-    b1 = Batch(opts, 1, C4_W, C4_H, A.FMT_RGB24, timing=True)
-    try:
-        for rep in range(4):
-            t1 = time.perf_counter()
-            b1.run_device(1, pages.ptr, pitch, stride)
-            b1.wait()
-            t2 = time.perf_counter()
-            st = dict(b1.stage_times())
-            if rep:
-                lat.append((t2 - t1) * 1e3)
-                rot.append(st.get(ROOFLINE_STAGE, 0.0))
-                lat_stages = st
-    finally:
-        b1.close()
+    # one sheet alone on an idle GPU: latency and the rotate launch (sheet 0,
+    # no band), then every sheet once alone: the odd sheets carry the dark
+    # band the blackfilter floods, and the heaviest one sets a batch's step
+    lat, rot, lat_stages, per_sheet, heavy = [], [], {}, [], (None, -1.0, {})
+    if not args.no_latency:
+        b1 = Batch(opts, 1, C4_W, C4_H, A.FMT_RGB24, timing=True)
+        try:
+            for rep in range(4):
+                t1 = time.perf_counter()
+                b1.run_device(1, pages.ptr, pitch, stride)
+                b1.wait()
+                t2 = time.perf_counter()
+                st = dict(b1.stage_times())
+                if rep:
+                    lat.append((t2 - t1) * 1e3)
+                    rot.append(st.get(ROOFLINE_STAGE, 0.0))
+                    lat_stages = st
+            for sheet in range(nsheets):
+                t1 = time.perf_counter()
+                b1.run_device(1, pages.ptr + sheet * stride, pitch, stride)
+                b1.wait()
+                ms = (time.perf_counter() - t1) * 1e3
+                st = dict(b1.stage_times())
+                per_sheet.append(round(ms, 2))
+                if ms > heavy[1]:
+                    heavy = (sheet, ms, st)
+        finally:
+            b1.close()
     pages.close()
     alg_sheet = 10 * C4_W * C4_H * 3
     rot_alg = 2 * C4_W * C4_H * 3
@@ -474,8 +487,14 @@ def run_c4(args, L, d, devices, firsts, n_gpus, version, valid, nsheets=0, steps
             "steps": steps, "warmup": warmup,
             "ms_per_step": round(elapsed / steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "latency_ms": round(statistics.median(lat), 2),
+            "latency_ms": round(statistics.median(lat), 2) if lat else None,
+            "latency_of": "sheet 0 alone (no dark band)",
             "latency_stages_ms": {k: round(v, 3) for k, v in lat_stages.items()},
+            "latency_band_ms": round(heavy[1], 2) if heavy[0] is not None else None,
+            "latency_band_of": "the slowest sheet alone (sheet %s; odd sheets carry a 40-px dark "
+                               "band the blackfilter floods)" % heavy[0],
+            "latency_band_stages_ms": {k: round(v, 3) for k, v in heavy[2].items()},
+            "latency_per_sheet_ms": per_sheet,
             "config": {"workload": "%d synthetic RGB24 9920x7016 double-page sheets per GPU, "
                                    "layout double, interpolate linear, border 60" % nsheets,
                        "sheets_per_batch": bsz, "streams": streams},

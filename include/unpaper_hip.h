@@ -590,6 +590,15 @@ int uphip_runner_output_info(UphipRunner *runner, int32_t *width, int32_t *heigh
                              int32_t *format, int64_t *linesize);
 UphipBatch *uphip_runner_batch(UphipRunner *runner, int32_t device_index,
                                int32_t slot);
+/* Host placement of device `device_index` (the peer of the reference's
+ * per-device pools and stream-bound workers, image_pipeline.c:226-376,
+ * batch_worker.c:174-253): the NUMA node of the GPU (sysfs via its PCI bus
+ * id; -1 when unknown), the CPUs of that node the device thread and its
+ * load/store pool are bound to (0 = not bound), and that pool's threads.
+ * Pinned staging is allocated by a thread on the node, with the device
+ * current (hipHostMalloc places it nearest the device). */
+int uphip_runner_placement(UphipRunner *runner, int32_t device_index, int32_t *numa_node,
+                           int32_t *ncpus, int32_t *pool_threads);
 
 /* Stage timing (off by default): when on, every run records a HIP event at
  * each stage boundary on the batch stream, kept until

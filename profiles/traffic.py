@@ -51,7 +51,25 @@ def pick(d, sub):
     return max(d[k] for k in ks)  # the full-plane variant
 
 
+def merge_c4(path, out):
+    with open(path) as f:
+        c4 = json.load(f)
+    try:
+        with open(out) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        doc = {}
+    doc["c4"] = c4
+    with open(out, "w") as f:
+        json.dump(doc, f, indent=1)
+    print("c4 merged into", out)
+
+
 def main():
+    if sys.argv[1] == "--merge-c4":
+        merge_c4(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else
+                 os.path.join(os.path.dirname(__file__), "traffic.json"))
+        return
     fdir, wdir, kern, stage, alg, pages, run_pages = sys.argv[1:8]
     out = sys.argv[8] if len(sys.argv) > 8 else os.path.join(os.path.dirname(__file__), "traffic.json")
     alg, pages, run_pages = int(alg), int(pages), int(run_pages)
@@ -85,6 +103,14 @@ def main():
     doc["pipeline_pages_in_run"] = run_pages
     print("pipeline: fetch x2 %.1f MB + write %.1f MB = %.1f MB per page" %
           (2 * pf / run_pages / 1e6, pw / run_pages / 1e6, (2 * pf + pw) / run_pages / 1e6))
+    # keys other tools own (the C4 rotate's "c4", tools/traffic_c4.sh) survive
+    try:
+        with open(out) as f:
+            old = json.load(f)
+        for k, v in old.items():
+            doc.setdefault(k, v)
+    except (OSError, ValueError):
+        pass
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)
     print("%s: fetch %.1f MB (x2 %.1f) + write %.1f MB = %.1f MB/launch vs alg %.1f MB (%.3fx)" %

@@ -130,6 +130,37 @@ def test_runner_memory_source_overlapping_pages(hip, oracle, stride_kind):
         assert_same(HostImage(w, h, exp.format, out[i]), exp, "%s page %d" % (stride_kind, i))
 
 
+def test_runner_numa_placement(hip):
+    """VERDICT r03 item 7: each device's thread and load/store pool are bound
+    to the CPUs of the GPU's NUMA node (sysfs via the PCI bus id), and the
+    pool threads split the host threads between devices."""
+    w, h = SMALL
+    opts = A.Options()
+    hip.lib.uphip_options_init(C.byref(opts))
+    r = Runner(opts, 2, w, h, A.FMT_GRAY8, devices=(0, 0), streams=1, host_threads=5)
+    try:
+        pl = [r.placement(i) for i in range(2)]
+    finally:
+        r.close()
+    assert sorted(p[2] for p in pl) == [2, 3]
+    bus = ctypes_bus_id(hip.lib, 0)
+    node_file = "/sys/bus/pci/devices/%s/numa_node" % bus.lower()
+    node = int(open(node_file).read()) if os.path.exists(node_file) else -1
+    for n, ncpu, _ in pl:
+        if node >= 0:
+            assert n == node and ncpu > 0, (pl, node)
+        else:
+            assert n == -1 and ncpu == 0, (pl, node)
+
+
+def ctypes_bus_id(lib, dev):
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    buf = ctypes.create_string_buffer(64)
+    assert hip.hipDeviceGetPCIBusId(buf, 63, dev) == 0
+    return buf.value.decode()
+
+
 def test_runner_pnm_files(hip, oracle, tmp_path):
     """Decode queue -> device -> encode queue: PGM in, PGM out."""
     w, h = SMALL

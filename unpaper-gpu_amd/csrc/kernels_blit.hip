@@ -1935,7 +1935,7 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
   // 8*(lane%16).  One wave's LDS operations complete in order, so its reads
   // see its writes without a fence.
   __builtin_amdgcn_wave_barrier();
-  for (int k0 = 0; k0 < kRows; k0 += 4) {
+  for (int k0 = 0; k0 < kRows && !UPH_DIAG_BITS(diag, 8192); k0 += 4) {
     const int rr = k0 + (lane >> 4);
     const int32_t y = yw + rr, x = xo;
     if (rr < kRows && y < P.H && x < P.W) {
@@ -1962,10 +1962,27 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
     csum_flush();
   }
   };
-  if constexpr (!LOOP) {  // one tile per block, XCD-aware order
-    int txi, tyi, s;
-    xcd_block_m(m_gxy, m_gx, &txi, &tyi, &s);
-    tile(txi, tyi, s);
+  if constexpr (!LOOP) {
+    if (loop_count > 0) {
+      // persistent: a 1-D grid of G blocks (G a multiple of 8) walks all
+      // loop_count tiles; XCD x = block & 7 takes the x-th contiguous chunk of
+      // the tile order (as xcd_block_m), its G / 8 blocks sweep the chunk
+      // together, so neighbouring tiles share that XCD's L2
+      const int q = loop_count >> 3, rr = loop_count & 7, xcd = blockIdx.x & 7;
+      const int first = xcd * q + (xcd < rr ? xcd : rr), cnt = q + (xcd < rr ? 1 : 0);
+      for (int j = blockIdx.x >> 3; j < cnt; j += (int)(gridDim.x >> 3)) {
+        const int t = first + j;
+        const int s = div_by_magic(t, m_gxy);
+        const int rem = t - s * tgx * tgy;
+        const int tyi = div_by_magic(rem, m_gx);
+        tile(rem - tyi * tgx, tyi, s);
+        __syncthreads();  // the next tile restages the LDS window
+      }
+    } else {  // one tile per block, XCD-aware order
+      int txi, tyi, s;
+      xcd_block_m(m_gxy, m_gx, &txi, &tyi, &s);
+      tile(txi, tyi, s);
+    }
   } else {
   // Persistent form for the large-window class, usually empty: the lanes of
   // every wave test 64 sheets at once (the same ballot in every wave), and
@@ -2006,6 +2023,7 @@ bool launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateAr
   const dim3 grid((src.P.W + kRotTW - 1) / kRotTW, (src.P.H + kRotTH - 1) / kRotTH, count);
   const dim3 ggrid((src.P.W + kRotTW - 1) / kRotTW, (src.P.H + kRotGH - 1) / kRotGH, count);
   if (interp == UPHIP_INTERP_CUBIC && src.P.fmt == F_GRAY8) {
+    if (diag_double() & 4096) colsum = nullptr;  // tuning build: time without the column sums
     const int rows = rotate_window_rows(max_abs_angle);
     auto lds_of = [](int r) {
       return (sizeof(float) * kRFS + sizeof(uint64_t)) * (size_t)r + kRFH * kRFW;
@@ -2018,7 +2036,15 @@ bool launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateAr
         !(diag_double() & 256)) {
       const dim3 fgrid((src.P.W + kRFW - 1) / kRFW, (src.P.H + kRFH - 1) / kRFH, count);
       const uint32_t mgxy = div_magic(fgrid.x * fgrid.y), mgx = div_magic(fgrid.x);
-      const int dd = diag_double() & (512 | 1024 | 2048);
+      const int dd = diag_double() & (512 | 1024 | 2048 | 8192);
+      if (diag_double() & 16384) {  // tuning A/B: persistent blocks over all tiles
+        const int ntiles = (int)(fgrid.x * fgrid.y * fgrid.z);
+        const int G = 8 * (int)std::min<int64_t>((ntiles + 7) / 8, 128 * (diag_double() & 32768 ? 2 : 1));
+        UPH_LAUNCH_DIAG(2, k_rotate_cubic_g8f<false>, dim3(G), dim3(kRFT), lds_of(rows), st, src, dst,
+                        args, rows, 0, dd, mgxy, mgx, ntiles, (int)fgrid.x, (int)fgrid.y, colsum,
+                        cs_stride);
+        return colsum != nullptr;
+      }
       if (rows > rows4) {
         // sheets whose angle fits the small window at four tiles per CU, then
         // the others at the scan range's window (three per CU); every sheet

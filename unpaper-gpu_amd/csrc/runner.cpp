@@ -19,6 +19,8 @@
 // with K slots per device in flight, so the host work of one slot overlaps the
 // device work of the others.
 #include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <atomic>
@@ -51,7 +53,12 @@ double secs(Clock::time_point a, Clock::time_point b) {
 // deadlock.
 class HostPool {
  public:
-  explicit HostPool(int n) {
+  // aff: the CPUs the workers run on (a device's NUMA node), or null
+  explicit HostPool(int n, const cpu_set_t* aff = nullptr) {
+    if (aff) {
+      aff_ = *aff;
+      pinned_ = true;
+    }
     for (int i = 0; i < n; i++) th_.emplace_back([this] { loop(); });
   }
   ~HostPool() {
@@ -62,6 +69,7 @@ class HostPool {
     cv_.notify_all();
     for (auto& t : th_) t.join();
   }
+  int size() const { return (int)th_.size(); }
   // fire-and-forget task (the caller tracks completion itself)
   void submit(std::function<void()> f) {
     {
@@ -106,6 +114,7 @@ class HostPool {
 
  private:
   void loop() {
+    if (pinned_) pthread_setaffinity_np(pthread_self(), sizeof(aff_), &aff_);
     for (;;) {
       std::function<void()> t;
       {
@@ -123,7 +132,50 @@ class HostPool {
   std::mutex mu_;
   std::condition_variable cv_;
   bool stop_ = false;
+  cpu_set_t aff_;
+  bool pinned_ = false;
 };
+
+// The CPUs of a device's NUMA node (sysfs via its PCI bus id), within the
+// CPUs this process may use.  False when the node is unknown (no NUMA, a
+// virtual device) or shares no CPU with the process.
+bool device_node_cpus(int device, int* node, cpu_set_t* cpus) {
+  *node = -1;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  for (char* c = bus; *c; c++) *c = (char)tolower((unsigned char)*c);
+  char path[256];
+  snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+  FILE* f = fopen(path, "r");
+  if (!f) return false;
+  const bool got = fscanf(f, "%d", node) == 1;
+  fclose(f);
+  if (!got || *node < 0) return false;
+  snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", *node);
+  f = fopen(path, "r");
+  if (!f) return false;
+  char list[4096] = {0};
+  const bool read = fgets(list, sizeof(list), f) != nullptr;
+  fclose(f);
+  if (!read) return false;
+  cpu_set_t allowed;
+  CPU_ZERO(cpus);
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return false;
+  for (char* p = list; *p && *p != '\n';) {  // "a-b,c,d-e"
+    char* e;
+    const long a = strtol(p, &e, 10);
+    long b = a;
+    if (e == p) break;
+    if (*e == '-') b = strtol(e + 1, &e, 10);
+    for (long c = a; c <= b && c < CPU_SETSIZE; c++)
+      if (c >= 0 && CPU_ISSET(c, &allowed)) CPU_SET(c, cpus);
+    p = *e == ',' ? e + 1 : e;
+  }
+  return CPU_COUNT(cpus) > 0;
+}
 
 }  // namespace
 }  // namespace uph
@@ -349,6 +401,18 @@ struct Slot {
 struct DeviceCtx {
   int device = 0;
   std::vector<Slot> slots;
+  // placement (image_pipeline.c:226-376 sizes pools per device; here each
+  // device also gets its node's CPUs): the device thread and this device's
+  // load/store pool run on the CPUs of the GPU's NUMA node; pinned staging
+  // comes from hipHostMalloc, which places it on the node nearest the
+  // current device
+  int numa = -1;
+  bool pinned = false;
+  cpu_set_t cpus;
+  HostPool* pool = nullptr;
+  void bind() const {
+    if (pinned) pthread_setaffinity_np(pthread_self(), sizeof(cpus), &cpus);
+  }
   // per-run results
   int64_t done = 0, failed = 0;
   double busy_s = 0;
@@ -363,7 +427,6 @@ struct UphipRunner {
   UphipRunnerConfig cfg;
   std::vector<int> devices;
   std::vector<DeviceCtx> dev;
-  HostPool* pool = nullptr;
   int32_t out_w = 0, out_h = 0, out_fmt = 0;
   int64_t in_pitch = 0, in_page_stride = 0;   // batch input slot layout (= staging layout)
   int64_t out_linesize = 0, out_sheet_stride = 0;
@@ -638,14 +701,25 @@ UphipRunner* uphip_runner_create(const UphipOptions* options, const UphipBatchGe
       r->out_linesize = op;
   }
   r->out_sheet_stride = r->out_linesize * r->out_h;
-  const int ht = config->host_threads > 0 ? config->host_threads : 4 * (int)r->devices.size();
-  r->pool = new HostPool(ht);
+  // load/store pools: one per device, its share of the host threads, on the
+  // device's NUMA node (the decode/encode queues' workers, lib/decode_queue.c)
+  const int nd = (int)r->devices.size();
+  const int ht = config->host_threads > 0 ? config->host_threads : 4 * nd;
+  for (int i = 0; i < nd; i++) {
+    DeviceCtx& dc = r->dev[(size_t)i];
+    dc.pinned = device_node_cpus(dc.device, &dc.numa, &dc.cpus);
+    const int share = std::max(1, ht / nd + (i < ht % nd ? 1 : 0));
+    dc.pool = new HostPool(share, dc.pinned ? &dc.cpus : nullptr);
+  }
   return r;
 }
 
 void uphip_runner_destroy(UphipRunner* r) {
   if (!r) return;
-  delete r->pool;
+  for (DeviceCtx& dc : r->dev) {
+    delete dc.pool;
+    dc.pool = nullptr;
+  }
   for (DeviceCtx& dc : r->dev) {
     uphip_set_device(dc.device);
     for (Slot& sl : dc.slots) {
@@ -671,6 +745,17 @@ int uphip_runner_layout(UphipRunner* r, int32_t* batches_per_device, int32_t* ca
   return 0;
 }
 
+int uphip_runner_placement(UphipRunner* r, int32_t device_index, int32_t* numa_node,
+                           int32_t* ncpus, int32_t* pool_threads) {
+  if (!r || device_index < 0 || device_index >= (int)r->dev.size())
+    return fail("runner_placement: bad device index"), -1;
+  const DeviceCtx& dc = r->dev[(size_t)device_index];
+  if (numa_node) *numa_node = dc.pinned ? dc.numa : -1;
+  if (ncpus) *ncpus = dc.pinned ? CPU_COUNT(&dc.cpus) : 0;
+  if (pool_threads) *pool_threads = dc.pool ? dc.pool->size() : 0;
+  return 0;
+}
+
 UphipBatch* uphip_runner_batch(UphipRunner* r, int32_t device_index, int32_t slot) {
   if (!r || device_index < 0 || device_index >= (int)r->dev.size() || slot < 0 ||
       slot >= (int)r->dev[(size_t)device_index].slots.size())
@@ -689,6 +774,7 @@ int uphip_runner_run_device(UphipRunner* r, const UphipDevicePages* shards, int3
       dc.done = dc.failed = 0;
       dc.error.clear();
       const auto a = Clock::now();
+      dc.bind();
       uphip_set_device(dc.device);
       const UphipDevicePages& sh = shards[i];
       const int64_t nin = r->opts.input_count;
@@ -741,17 +827,28 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
   const int S = r->geo.capacity;
   const int nin = r->opts.input_count;
   if (!r->staged) {  // pinned staging per slot, laid out like the batch's input slots
-    const int caller_dev = uphip_get_device();
-    bool ok = true;
-    for (DeviceCtx& dc : r->dev) {
-      uphip_set_device(dc.device);
-      for (Slot& sl : dc.slots) {
-        ok = ok && UPH_HIP(hipHostMalloc((void**)&sl.hin, (size_t)(r->in_page_stride * S * nin),
-                                         hipHostMallocDefault));
-        ok = ok && UPH_HIP(hipHostMalloc((void**)&sl.hout, (size_t)(r->out_sheet_stride * S),
-                                         hipHostMallocDefault));
-      }
+    // each device's staging from a thread on its node (hipHostMalloc places
+    // pinned memory on the node nearest the current device; the thread's
+    // binding makes any first-touch local too)
+    std::atomic<bool> ok{true};
+    {
+      std::vector<std::thread> th;
+      for (DeviceCtx& dc : r->dev)
+        th.emplace_back([&, pdc = &dc] {
+          pdc->bind();
+          uphip_set_device(pdc->device);
+          for (Slot& sl : pdc->slots) {
+            if (!UPH_HIP(hipHostMalloc((void**)&sl.hin, (size_t)(r->in_page_stride * S * nin),
+                                       hipHostMallocDefault)) ||
+                !UPH_HIP(hipHostMalloc((void**)&sl.hout, (size_t)(r->out_sheet_stride * S),
+                                       hipHostMallocDefault)))
+              ok = false;
+          }
+          if (!ok) uphip_clear_error();  // reported below from this thread
+        });
+      for (auto& t : th) t.join();
     }
+    if (!ok) fail("runner: pinned staging allocation failed");
     if (!ok) {  // all or nothing: a later call allocates afresh
       for (DeviceCtx& dc : r->dev)
         for (Slot& sl : dc.slots) {
@@ -760,7 +857,6 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
           sl.hin = sl.hout = nullptr;
         }
     }
-    uphip_set_device(caller_dev);
     if (!ok) return -1;
     r->staged = true;
   }
@@ -821,6 +917,7 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
       DeviceCtx& dc = r->dev[i];
       dc.done = dc.failed = 0;
       dc.error.clear();
+      dc.bind();
       uphip_set_device(dc.device);
       auto note = [&dc](const char* what) {
         if (dc.error.empty()) dc.error = uphip_last_error() ? uphip_last_error() : what;
@@ -888,7 +985,7 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
             state[k] = LOADING;
             phase[k] = LOADING;
             for (int s = 0; s < sl->count; s++) {
-              r->pool->submit([&, sl, k, s, first] {
+              dc.pool->submit([&, sl, k, s, first] {
                 const auto a = Clock::now();
                 for (int j = 0; j < nin; j++) {
                   uint8_t* dst = sl->hin + ((int64_t)s * nin + j) * r->in_page_stride;
@@ -967,7 +1064,7 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
             state[k] = STORING;
             for (int s = 0; s < sl->count; s++) {
               if (sl->failed[(size_t)s]) continue;
-              r->pool->submit([&, sl, k, s] {
+              dc.pool->submit([&, sl, k, s] {
                 const auto a = Clock::now();
                 bool good = true;
                 store_sheet(r, sink, sl->first + s, sl->hout + (int64_t)s * r->out_sheet_stride, &good);

@@ -52,7 +52,7 @@ EXPORTED = [
     "uphip_runner_run_device", "uphip_runner_run_host", "uphip_runner_get_stats",
     "uphip_runner_output_info", "uphip_runner_batch", "uphip_runner_layout", "uphip_batch_device_bytes", "uphip_host_alloc", "uphip_host_free",
     "uphip_check_libm", "uphip_jpeg_probe", "uphip_jpeg_read", "uphip_jpeg_decode",
-    "uphip_jpeg_entropy_decode",
+    "uphip_jpeg_entropy_decode", "uphip_runner_placement",
 ]
 
 
@@ -189,6 +189,8 @@ def load_library(path=LIB_PATH):
         "uphip_memcpy_htod": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
         "uphip_memcpy_dtoh": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
         "uphip_check_libm": (C.c_int, [C.c_uint32, C.POINTER(C.c_uint64)]),
+        "uphip_runner_placement": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int32),
+                                             C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
         "uphip_jpeg_probe": (C.c_int, [C.c_char_p, C.POINTER(A.PnmInfo)]),
         "uphip_jpeg_read": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int64, C.POINTER(A.PnmInfo)]),
         "uphip_jpeg_decode": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64,

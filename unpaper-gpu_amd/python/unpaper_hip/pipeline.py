@@ -212,6 +212,14 @@ class Runner:
         self.lib.uphip_runner_get_stats(self.handle, C.byref(s))
         return s
 
+    def placement(self, device_index):
+        """(NUMA node or -1, CPUs bound to or 0, load/store pool threads)."""
+        node, ncpu, pool = C.c_int32(), C.c_int32(), C.c_int32()
+        if self.lib.uphip_runner_placement(self.handle, device_index, C.byref(node),
+                                           C.byref(ncpu), C.byref(pool)) != 0:
+            _check(self.lib)
+        return node.value, ncpu.value, pool.value
+
     def close(self):
         if self.handle:
             self.lib.uphip_runner_destroy(self.handle)
