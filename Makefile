@@ -31,6 +31,11 @@ ifeq ($(DIAG),1)
 OBJDIR     := $(PKG)/build_diag
 LIBDIR     := $(PKG)/lib_diag
 DIAGFLAGS  := -DUPHIP_DIAG
+else ifneq ($(VARIANT),)
+# A/B builds: make lib VARIANT=name VFLAGS="-D..." -> lib_name/ (tuning only)
+OBJDIR     := $(PKG)/build_$(VARIANT)
+LIBDIR     := $(PKG)/lib_$(VARIANT)
+DIAGFLAGS  := $(VFLAGS)
 else
 OBJDIR     := $(PKG)/build
 LIBDIR     := $(PKG)/lib

@@ -6,6 +6,7 @@
 // a whole byte = 8 pixels).  Rows start 256-byte aligned, so the interior of a
 // row is written with 16-byte stores.
 #include <climits>
+#include <type_traits>
 
 #include "interp.h"
 #include "kernels.h"
@@ -1593,8 +1594,36 @@ __device__ __forceinline__ uint32_t row_off(int32_t y, int64_t pitch) {
   return (uint32_t)y * (uint32_t)pitch;
 }
 
+#ifndef UPH_ROT_MINB
+#define UPH_ROT_MINB 8
+#endif
+// 1: one block barrier per in-mask tile (staging): every wave finds the
+// window bounds itself, and the column sums are flushed by the last wave to
+// finish (an LDS arrival counter) instead of after a second barrier.  Measured
+// slower (1.11 vs 1.08 ms a 64-sheet launch: the corners' VALU in every wave
+// costs more than the barriers), kept off.
+#ifndef UPH_ROT_V2
+#define UPH_ROT_V2 0
+#endif
+#ifndef UPH_ROT_FULL
+#define UPH_ROT_FULL 1  // the branch-free row loop for full tiles
+#endif
+#ifdef UPHIP_DIAG
+// tuning build: per-phase shader clocks of wave 0 of every in-mask tile
+// (UPHIP_DIAG_DOUBLE bit 65536), summed; [7] counts the tiles
+// (spread over 1024 slots by block so the counters do not contend)
+__device__ unsigned long long g_rot_phase[1024 * 8];
+#define UPH_ROT_T(k)                                                         \
+  if (UPH_DIAG_BITS(diag, 65536) && threadIdx.x == 0) {                     \
+    const unsigned long long tn = wall_clock64();                            \
+    atomicAdd(&g_rot_phase[8 * (blockIdx.x & 1023) + (k)], tn - tprev);      \
+    tprev = tn;                                                              \
+  }
+#else
+#define UPH_ROT_T(k)
+#endif
 template <bool LOOP>
-__global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, PlaneRef dst,
+__global__ void __launch_bounds__(kRFT, UPH_ROT_MINB) k_rotate_cubic_g8f(PlaneRef src, PlaneRef dst,
                                                                const RotateArgs* args,
                                                                int max_rows, int cls_rows,
                                                                int diag,
@@ -1610,8 +1639,12 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
   // scan need not read the rotated plane again; per tile summed in LDS, then
   // one atomic per column
   __shared__ uint32_t csum_s[kRFW];
+  __shared__ int32_t done_s;  // waves whose column sums are in csum_s (UPH_ROT_V2)
   // one tile (txi, tyi) of sheet s; every return is block-uniform
   auto tile = [&](int txi, int tyi, int s) {
+#ifdef UPHIP_DIAG
+  unsigned long long tprev = wall_clock64();
+#endif
   // the plane selectors and the arguments are loaded together (one round trip)
   const uint8_t* sbase = plane_ptr(src, s);
   uint8_t* dbase = plane_ptr(dst, s);
@@ -1639,10 +1672,19 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
     if (threadIdx.x < kRFW && tx0 + (int)threadIdx.x < P.W)
       atomicAdd(colsum + s * cs_stride + tx0 + threadIdx.x, csum_s[threadIdx.x]);
   };
+#if UPH_ROT_V2
+  const bool inside = cu0 <= cu1 && cv0 <= cv1;  // uniform
+  if (colsum) {
+    if (threadIdx.x < kRFW) csum_s[threadIdx.x] = 0;
+    if (threadIdx.x == 0) done_s = 0;
+    if (!inside) __syncthreads();  // in-mask tiles: the staging barrier orders it
+  }
+#else
   if (colsum) {
     if (threadIdx.x < kRFW) csum_s[threadIdx.x] = 0;
     __syncthreads();
   }
+#endif
   if (!(cu0 <= cu1 && cv0 <= cv1)) {
     // no pixel of the tile inside the mask: copied unchanged (deskew.c:268-286)
     const int cb = 8 * (threadIdx.x & 15);
@@ -1672,6 +1714,7 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
     }
     return;
   }
+  UPH_ROT_T(0)
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // Source window of the tile's in-mask pixels (their 4x4 taps included).
@@ -1681,6 +1724,28 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
   // per-tile constant: wave 0 evaluates the four corners in lanes (c = lane
   // & 3), reduces them across the quad and posts the bounds in LDS, instead
   // of every wave running the float chain of all four corners.
+#if UPH_ROT_V2
+  // every wave: the corners in lanes (c = lane & 3), reduced across the quad;
+  // lane 0's quad holds the bounds (no LDS round trip, no barrier)
+  int32_t bx0, by0, bw, bh;
+  {
+    const int c = lane & 3;
+    const int32_t u = c & 1 ? cu1 : cu0, v = c & 2 ? cv1 : cv0;
+    const float X = scx + (u - tcx) * a.cosval + (v - tcy) * a.sinval;
+    const float Y = scy + (v - tcy) * a.cosval - (u - tcx) * a.sinval;
+    float mnx = fminf(X, dpp_f<0xB1>(X)), mxx = fmaxf(X, dpp_f<0xB1>(X));
+    float mny = fminf(Y, dpp_f<0xB1>(Y)), mxy = fmaxf(Y, dpp_f<0xB1>(Y));
+    mnx = fminf(mnx, dpp_f<0x4E>(mnx));
+    mxx = fmaxf(mxx, dpp_f<0x4E>(mxx));
+    mny = fminf(mny, dpp_f<0x4E>(mny));
+    mxy = fmaxf(mxy, dpp_f<0x4E>(mxy));
+    bx0 = __builtin_amdgcn_readfirstlane((int32_t)floorf(mnx)) - 1;
+    by0 = __builtin_amdgcn_readfirstlane((int32_t)floorf(mny)) - 1;
+    bw = __builtin_amdgcn_readfirstlane((int32_t)floorf(mxx)) + 3 - bx0 + 1;
+    bh = __builtin_amdgcn_readfirstlane((int32_t)floorf(mxy)) + 3 - by0 + 1;
+  }
+  UPH_ROT_T(1)
+#else
   if (wu == 0) {
     const int c = lane & 3;
     const int32_t u = c & 1 ? cu1 : cu0, v = c & 2 ? cv1 : cv0;
@@ -1698,10 +1763,12 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
     }
   }
   __syncthreads();
+  UPH_ROT_T(1)
   const int32_t bx0 = __builtin_amdgcn_readfirstlane(win_s[0]) - 1;
   const int32_t by0 = __builtin_amdgcn_readfirstlane(win_s[1]) - 1;
   const int32_t bw = __builtin_amdgcn_readfirstlane(win_s[2]) + 3 - bx0 + 1;
   const int32_t bh = __builtin_amdgcn_readfirstlane(win_s[3]) + 3 - by0 + 1;
+#endif
   const int32_t xa = bx0 >= 0 ? (bx0 & ~3) : -((-bx0 + 3) & ~3);  // window start, dword aligned
   const int nd = (bx0 - xa + bw + 3) >> 2;                         // source dwords per row
   const bool staged = bw > 0 && bh > 0 && 4 * nd <= kRFS && bh <= max_rows;
@@ -1786,6 +1853,7 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
     }
   }
   __syncthreads();
+  UPH_ROT_T(2)
   const int32_t xA = tx0 + lane, xB = xA + 64;
   const bool hasA = xA < P.W, hasB = xB < P.W;
   // per-lane terms of the source coordinates (constant down the column):
@@ -1866,21 +1934,28 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
   // LDS byte address of window (row 0, column 0) minus the 4x4 tap offset,
   // so a pixel's first tap sits at wbase + 4 (iy kRFS + ix)
   const uint32_t wbase = lds0 - 4u * (uint32_t)((1 + by0) * kRFS + 1 + xa);
+  UPH_ROT_T(3)
+  // Full tiles (every pixel inside the mask and the image, the window staged
+  // and starting inside the image) take a copy of the row loop without the
+  // per-pixel mask tests and their exec-mask branches.
+  uint32_t fsA = 0, fsB = 0;  // full tiles: this wave's column sums
+  auto row_loop = [&](auto full_tag) {
+  constexpr bool FULL = decltype(full_tag)::value;
 #pragma unroll
   for (int k = 0; k < kRows; k++) {
     const int32_t y = yw + k;
     const int32_t v = y - a.mask.y0;
-    const bool rowin = (v >= 0) & (v < sh) & (y < P.H);
+    const bool rowin = FULL || ((v >= 0) & (v < sh) & (y < P.H));
     const float cv = v - tcy;
     const float VS = cv * a.sinval, VC = scy + cv * a.cosval;
-    const bool inA = rowin & colA, inB = rowin & colB;
+    const bool inA = FULL || (rowin & colA), inB = FULL || (rowin & colB);
     uint32_t oA = 255, oB = 255;
-    const bool white = staged && ((white_rows >> k) & 1u);
-    if (!white && staged) {
+    const bool white = (FULL || staged) && ((white_rows >> k) & 1u);
+    if (!white && (FULL || staged)) {
       const float sxA = axA + VS, syA = VC - bsA, sxB = axB + VS, syB = VC - bsB;
       const int ixA = (int)sxA, iyA = (int)syA, ixB = (int)sxB, iyB = (int)syB;  // truncation
       float fxA, fyA, fxB, fyB;
-      if (posc) {
+      if (FULL || posc) {
         fxA = __builtin_amdgcn_fractf(sxA);
         fyA = __builtin_amdgcn_fractf(syA);
         fxB = __builtin_amdgcn_fractf(sxB);
@@ -1913,10 +1988,24 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
       oA = (uint32_t)o.x;  // integer-valued in [0, 255]
       oB = (uint32_t)o.y;
     }
-    if (!staged) break;  // uniform: the rows go through the loop below
-    if (inA) obuf[k * kRFW + lane] = (uint8_t)oA;
-    if (inB) obuf[k * kRFW + 64 + lane] = (uint8_t)oB;
+    if (!FULL && !staged) break;  // uniform: the rows go through the loop below
+    if (FULL) {  // every pixel in the mask: no per-lane branches
+      obuf[k * kRFW + lane] = (uint8_t)oA;
+      obuf[k * kRFW + 64 + lane] = (uint8_t)oB;
+      fsA += oA;  // the column sums from registers (no re-read of obuf)
+      fsB += oB;
+    } else {
+      if (inA) obuf[k * kRFW + lane] = (uint8_t)oA;
+      if (inB) obuf[k * kRFW + 64 + lane] = (uint8_t)oB;
+    }
   }
+  };
+  const bool full =
+      UPH_ROT_FULL && !partial && staged && posc && tx0 + kRFW <= P.W && ty0 + kRFH <= P.H;
+  if (full)
+    row_loop(std::true_type{});
+  else
+    row_loop(std::false_type{});
   if (!staged) {
     // window too large for LDS (large angles): taps from the frame (kept out
     // of the unrolled loop above)
@@ -1931,10 +2020,22 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
       if (rowin & colB) obuf[k * kRFW + 64 + lane] = interp_bicubic(S, axB + VS, VC - bsB).r;
     }
   }
+  UPH_ROT_T(4)
   // the wave's rows as 8-byte stores: lane -> row k0 + lane/16, bytes
   // 8*(lane%16).  One wave's LDS operations complete in order, so its reads
   // see its writes without a fence.
   __builtin_amdgcn_wave_barrier();
+  if (full && !UPH_DIAG_BITS(diag, 8192)) {
+    // inside the image: no bounds tests
+#pragma unroll
+    for (int k0 = 0; k0 < kRows; k0 += 4) {
+      const int rr = k0 + (lane >> 4);
+      if (rr < kRows) {
+        const uint64_t q = *reinterpret_cast<const uint64_t*>(obuf + rr * kRFW + cb);
+        *reinterpret_cast<uint64_t*>(dbase + row_off(yw + rr, P.pitch) + xo) = q;
+      }
+    }
+  } else
   for (int k0 = 0; k0 < kRows && !UPH_DIAG_BITS(diag, 8192); k0 += 4) {
     const int rr = k0 + (lane >> 4);
     const int32_t y = yw + rr, x = xo;
@@ -1948,41 +2049,52 @@ __global__ void __launch_bounds__(kRFT, 8) k_rotate_cubic_g8f(PlaneRef src, Plan
       }
     }
   }
+  UPH_ROT_T(5)
   if (colsum) {
     // this wave's rows of columns lane and 64 + lane, then the tile's
-    uint32_t sA = 0, sB = 0;
+    uint32_t sA = fsA, sB = fsB;
+    if (!full) {
 #pragma unroll
-    for (int k = 0; k < kRows; k++) {
-      if (yw + k >= P.H) break;
-      sA += obuf[k * kRFW + lane];
-      sB += obuf[k * kRFW + 64 + lane];
+      for (int k = 0; k < kRows; k++) {
+        if (yw + k >= P.H) break;
+        sA += obuf[k * kRFW + lane];
+        sB += obuf[k * kRFW + 64 + lane];
+      }
     }
+#if UPH_ROT_V2
+    // the wave's sums into the tile's, then the last wave to arrive adds the
+    // tile's into the sheet's (release/acquire on the arrival counter orders
+    // every wave's LDS adds before the last wave's reads)
+    __hip_atomic_fetch_add(&csum_s[lane], sA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(&csum_s[64 + lane], sB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    int prev = 0;
+    if (lane == 0)
+      prev = __hip_atomic_fetch_add(&done_s, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    prev = __shfl(prev, 0, 64);
+    if (prev == kRFWaves - 1) {
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      uint32_t* cs = colsum + s * cs_stride + tx0;
+      const uint32_t vA = __hip_atomic_load(&csum_s[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const uint32_t vB = __hip_atomic_load(&csum_s[64 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (tx0 + lane < P.W) atomicAdd(cs + lane, vA);
+      if (tx0 + 64 + lane < P.W) atomicAdd(cs + 64 + lane, vB);
+    }
+#else
     atomicAdd(&csum_s[lane], sA);
     atomicAdd(&csum_s[64 + lane], sB);
     csum_flush();
+#endif
   }
+  UPH_ROT_T(6)
+#ifdef UPHIP_DIAG
+  if (UPH_DIAG_BITS(diag, 65536) && threadIdx.x == 0)
+    atomicAdd(&g_rot_phase[8 * (blockIdx.x & 1023) + 7], 1ull);
+#endif
   };
-  if constexpr (!LOOP) {
-    if (loop_count > 0) {
-      // persistent: a 1-D grid of G blocks (G a multiple of 8) walks all
-      // loop_count tiles; XCD x = block & 7 takes the x-th contiguous chunk of
-      // the tile order (as xcd_block_m), its G / 8 blocks sweep the chunk
-      // together, so neighbouring tiles share that XCD's L2
-      const int q = loop_count >> 3, rr = loop_count & 7, xcd = blockIdx.x & 7;
-      const int first = xcd * q + (xcd < rr ? xcd : rr), cnt = q + (xcd < rr ? 1 : 0);
-      for (int j = blockIdx.x >> 3; j < cnt; j += (int)(gridDim.x >> 3)) {
-        const int t = first + j;
-        const int s = div_by_magic(t, m_gxy);
-        const int rem = t - s * tgx * tgy;
-        const int tyi = div_by_magic(rem, m_gx);
-        tile(rem - tyi * tgx, tyi, s);
-        __syncthreads();  // the next tile restages the LDS window
-      }
-    } else {  // one tile per block, XCD-aware order
-      int txi, tyi, s;
-      xcd_block_m(m_gxy, m_gx, &txi, &tyi, &s);
-      tile(txi, tyi, s);
-    }
+  if constexpr (!LOOP) {  // one tile per block, XCD-aware order
+    int txi, tyi, s;
+    xcd_block_m(m_gxy, m_gx, &txi, &tyi, &s);
+    tile(txi, tyi, s);
   } else {
   // Persistent form for the large-window class, usually empty: the lanes of
   // every wave test 64 sheets at once (the same ballot in every wave), and
@@ -2036,15 +2148,26 @@ bool launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateAr
         !(diag_double() & 256)) {
       const dim3 fgrid((src.P.W + kRFW - 1) / kRFW, (src.P.H + kRFH - 1) / kRFH, count);
       const uint32_t mgxy = div_magic(fgrid.x * fgrid.y), mgx = div_magic(fgrid.x);
-      const int dd = diag_double() & (512 | 1024 | 2048 | 8192);
-      if (diag_double() & 16384) {  // tuning A/B: persistent blocks over all tiles
-        const int ntiles = (int)(fgrid.x * fgrid.y * fgrid.z);
-        const int G = 8 * (int)std::min<int64_t>((ntiles + 7) / 8, 128 * (diag_double() & 32768 ? 2 : 1));
-        UPH_LAUNCH_DIAG(2, k_rotate_cubic_g8f<false>, dim3(G), dim3(kRFT), lds_of(rows), st, src, dst,
-                        args, rows, 0, dd, mgxy, mgx, ntiles, (int)fgrid.x, (int)fgrid.y, colsum,
-                        cs_stride);
-        return colsum != nullptr;
-      }
+      const int dd = diag_double() & (512 | 1024 | 2048 | 8192 | 65536);
+#ifdef UPHIP_DIAG
+      struct PhasePrint {  // after the launches below: the per-tile phase clocks
+        hipStream_t st;
+        ~PhasePrint() {
+          if (!(diag_double() & 65536)) return;
+          static unsigned long long hh[1024 * 8], z[1024 * 8];
+          unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+          hipStreamSynchronize(st);
+          hipMemcpyFromSymbol(hh, HIP_SYMBOL(g_rot_phase), sizeof(hh));
+          hipMemcpyToSymbol(HIP_SYMBOL(g_rot_phase), z, sizeof(z));
+          for (int i = 0; i < 1024 * 8; i++) h[i & 7] += hh[i];
+          if (!h[7]) return;
+          fprintf(stderr, "rotate phases (10 ns ticks/tile, %llu tiles): args %.0f corners %.0f staging %.0f "
+                  "flags %.0f compute %.0f stores %.0f colsum %.0f\n", h[7], (double)h[0] / h[7],
+                  (double)h[1] / h[7], (double)h[2] / h[7], (double)h[3] / h[7],
+                  (double)h[4] / h[7], (double)h[5] / h[7], (double)h[6] / h[7]);
+        }
+      } phase_print{st};
+#endif
       if (rows > rows4) {
         // sheets whose angle fits the small window at four tiles per CU, then
         // the others at the scan range's window (three per CU); every sheet
