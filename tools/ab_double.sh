@@ -3,7 +3,8 @@
 # launches a kernel twice when its UPHIP_DIAG_DOUBLE bit is set
 # (UPH_LAUNCH_DIAG); the drop in pages/s against 0 is what the kernel costs the
 # pipeline.  Bits: 1 rotation band, 16 rotation points, 128 rotation final +
-# line walk, 2 rotate.  usage: BITS="0 1 16 128" tools/ab_double.sh
+# line walk, 2 rotate, 4 moves, 8 copy, 32 gray cells, 64 blur counts,
+# 131072 noise classify, 262144 GRAY8 decode.  usage: BITS="0 1 16 128" tools/ab_double.sh
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out

@@ -1461,7 +1461,10 @@ __global__ void __launch_bounds__(kThreads) k_rotate_cubic_g8(PlaneRef src, Plan
 // separate multiply or add in the reference's order, as in cubic2.
 // ---------------------------------------------------------------------------
 constexpr int kRFW = 128;   // output columns per tile (2 per lane)
-constexpr int kRFH = 48;    // output rows per tile (6 per wave)
+#ifndef UPH_ROT_TALL
+#define UPH_ROT_TALL 0
+#endif
+constexpr int kRFH = UPH_ROT_TALL ? 96 : 48;  // output rows per tile (6 or 12 per wave)
 constexpr int kRFS = 144;   // staged row stride in floats (>= 141-float window rows at 5 deg)
 constexpr int kRFT = 512;   // threads per tile: 8 waves, kRFH / 8 consecutive rows each
 constexpr int kRFWaves = kRFT / 64;
@@ -1886,16 +1889,18 @@ __global__ void __launch_bounds__(kRFT, UPH_ROT_MINB) k_rotate_cubic_g8f(PlaneRe
   const int32_t xo = tx0 + cb;
   const bool partial = !(cu0 == u0 && cu1 == u1 && cv0 == v0 && cv1 == v1);
   if (partial) {
-    uint64_t q[2] = {0, 0};
+    constexpr int kQ = (kRows + 3) / 4;
+    uint64_t q[kQ];
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int h = 0; h < kQ; h++) {
+      q[h] = 0;
       const int rr = 4 * h + (lane >> 4);
       const int32_t y = imin(yw + rr, P.H - 1);
       const int32_t x = imin(xo, (int32_t)P.pitch - 8);  // rows are 256-byte pitched
       if (rr < kRows) q[h] = *reinterpret_cast<const uint64_t*>(sbase + row_off(y, P.pitch) + x);
     }
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int h = 0; h < kQ; h++) {
       const int rr = 4 * h + (lane >> 4);
       if (rr < kRows) *reinterpret_cast<uint64_t*>(obuf + rr * kRFW + cb) = q[h];
     }
@@ -1910,20 +1915,23 @@ __global__ void __launch_bounds__(kRFT, UPH_ROT_MINB) k_rotate_cubic_g8f(PlaneRe
     // r0 + j, r0 + j + 8, ... of the row's tap band, over the whole window
     // width (a row's taps span all but the ~(kRFH sin) columns of the
     // window's slant, so a column restriction would rarely change a flag)
-    const int k = lane >> 3, j = lane & 7;
-    bool hit = false;
-    if (k < kRows) {
-      const float cv = (yw + k - a.mask.y0) - tcy;
-      const float VC = scy + cv * a.cosval;
-      const int32_t yl = (int)(VC - bsL), yr = (int)(VC - bsR);
-      const int32_t r0 = imax(imin(yl, yr) - 1 - by0, 0);
-      const int32_t r1 = imin(imax(yl, yr) + 2 - by0, bh - 1);
-      for (int r = r0 + j; r <= r1; r += 8) hit |= nw[r] != 0;
-    }
-    const uint64_t m = __ballot(hit);
 #pragma unroll
-    for (int q = 0; q < kRows; q++)
-      if (((m >> (8 * q)) & 0xFFull) == 0) white_rows |= 1u << q;
+    for (int g = 0; g < kRows; g += 8) {
+      const int k = g + (lane >> 3), j = lane & 7;
+      bool hit = false;
+      if (k < kRows) {
+        const float cv = (yw + k - a.mask.y0) - tcy;
+        const float VC = scy + cv * a.cosval;
+        const int32_t yl = (int)(VC - bsL), yr = (int)(VC - bsR);
+        const int32_t r0 = imax(imin(yl, yr) - 1 - by0, 0);
+        const int32_t r1 = imin(imax(yl, yr) + 2 - by0, bh - 1);
+        for (int r = r0 + j; r <= r1; r += 8) hit |= nw[r] != 0;
+      }
+      const uint64_t m = __ballot(hit);
+#pragma unroll
+      for (int q = 0; q < 8 && g + q < kRows; q++)
+        if (((m >> (8 * q)) & 0xFFull) == 0) white_rows |= 1u << (g + q);
+    }
     if (UPH_DIAG_BITS(diag, 2048)) white_rows = 0;
     if (UPH_DIAG_BITS(diag, 512)) white_rows = ~0u;
   }
@@ -2142,10 +2150,15 @@ bool launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateAr
     };
     // the most window rows that still let four tiles (32 waves) share a CU's
     // 160 KB of LDS (16 + 512 B of static LDS per tile); windows of up to ~2.4 deg
-    const int rows4 = (int)((40 * 1024 - 16 - 4 * kRFW - kRFH * kRFW) /
+    // (TALL: two tiles, 16 waves, per CU)
+    const int rows4 = (int)(((UPH_ROT_TALL ? 80 : 40) * 1024 - 16 - 4 * kRFW - kRFH * kRFW) /
                             (sizeof(float) * kRFS + sizeof(uint64_t)));
-    if (lds_of(rows) <= 56 * 1024 && src.P.pitch * (int64_t)src.P.H < (1ll << 31) &&
-        !(diag_double() & 256)) {
+    if (UPH_ROT_TALL) {
+      allow_dynamic_lds((const void*)k_rotate_cubic_g8f<false>, 120 * 1024);
+      allow_dynamic_lds((const void*)k_rotate_cubic_g8f<true>, 120 * 1024);
+    }
+    if (lds_of(rows) <= (UPH_ROT_TALL ? 120 : 56) * 1024 &&
+        src.P.pitch * (int64_t)src.P.H < (1ll << 31) && !(diag_double() & 256)) {
       const dim3 fgrid((src.P.W + kRFW - 1) / kRFW, (src.P.H + kRFH - 1) / kRFH, count);
       const uint32_t mgxy = div_magic(fgrid.x * fgrid.y), mgx = div_magic(fgrid.x);
       const int dd = diag_double() & (512 | 1024 | 2048 | 8192 | 65536);

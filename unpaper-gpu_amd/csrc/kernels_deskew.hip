@@ -93,8 +93,10 @@ __device__ __forceinline__ LineSetup line_setup(const Rect& mask, const RotGeom&
 //   flag   [nlines]             1 = walk the line directly (k_rot_line)
 //   state  [nlines][4]          band result after kDepth steps: accumulated,
 //                               last step's blackness, peak, valid
+//   list   [nlines]             the flagged lines (k_rot_line's work list)
+//   nlist  [1]                  their count (zeroed before k_rot_points)
 struct RotScratch {
-  int32_t *cols, *ends, *part, *flag, *state;
+  int32_t *cols, *ends, *part, *flag, *state, *list, *nlist;
 };
 
 __host__ __device__ static inline int rot_slices(int max_scan) { return (max_scan + kSliceRows - 1) / kSliceRows; }
@@ -108,6 +110,8 @@ __host__ __device__ static inline RotScratch rot_scratch(int32_t* base, int nlin
   r.part = r.ends + 2 * (int64_t)nlines;
   r.flag = r.part + (int64_t)nlines * ns * kDepth;
   r.state = r.flag + nlines;
+  r.list = r.state + 4 * (int64_t)nlines;
+  r.nlist = r.list + nlines;
   return r;
 }
 
@@ -120,7 +124,7 @@ size_t rotation_lines_bytes(int count, int nedges, int nangles, int max_scan) {
   const int64_t ms = max_scan > 0 ? max_scan : 1;
   const int64_t ns = (ms + kSliceRows - 1) / kSliceRows;
   return sizeof(int32_t) * (size_t)(nlines * ms + 2 * nlines + nlines * ns * kDepth + nlines +
-                                    4 * nlines);
+                                    4 * nlines + nlines + 1);
 }
 
 // ---- k_rot_points: the points of every left/right line --------------------
@@ -159,6 +163,8 @@ __global__ void __launch_bounds__(256) k_rot_points(RotGeom g, const RotTable* t
       R.ends[2 * t + 1] = 0;
       R.flag[t] = 1;
       R.state[4 * t + 3] = 0;
+      // a top/bottom edge of an active sheet: walked directly
+      if (!(mask_active && !mask_active[s])) R.list[atomicAdd(R.nlist, 1)] = t;
     }
     return;
   }
@@ -443,7 +449,10 @@ __global__ void __launch_bounds__(256) k_rot_final(RotGeom g, const RotTable* ta
     return;
   }
   if (!band_range(R, (s * g.nedges + e) * na, na, sxh, band_cap, &bx0, &bw)) {
-    if (lane == 0) R.flag[t] = 1;
+    if (lane == 0) {
+      R.flag[t] = 1;
+      R.list[atomicAdd(R.nlist, 1)] = t;
+    }
     return;
   }
   const int ns = rot_slices(max_scan), nsl = (LS.scan + kSliceRows - 1) / kSliceRows;
@@ -478,6 +487,7 @@ __global__ void __launch_bounds__(256) k_rot_final(RotGeom g, const RotTable* ta
       R.state[4 * t + 2] = md > 0 ? md : 0;
       R.state[4 * t + 3] = 1;
       R.flag[t] = 1;
+      R.list[atomicAdd(R.nlist, 1)] = t;
     }
     return;
   }
@@ -507,12 +517,14 @@ __global__ void __launch_bounds__(256) k_rot_line(PlaneRef img, RotGeom g, const
                                                   int mask_index, int32_t* peaks, int count,
                                                   int max_scan, RotScratch R) {
   const int na = table->nangles;
-  const int nlines = count * g.nedges * na;
-  // grid-strided over the lines: only flagged ones are walked, so an empty
-  // fallback costs one flag read per line
-  for (int t = blockIdx.x; t < nlines; t += gridDim.x) {
+  (void)count;
+  // grid-strided over the work list of flagged lines (k_rot_points,
+  // k_rot_final append them): an empty list costs one load per block
+  const int n = __builtin_amdgcn_readfirstlane(*R.nlist);
+  for (int q = blockIdx.x; q < n; q += gridDim.x) {
+    const int t = __builtin_amdgcn_readfirstlane(R.list[q]);
     const int a = t % na, e = (t / na) % g.nedges, s = t / (na * g.nedges);
-    if (!R.flag[t] || (mask_active && !mask_active[s])) continue;
+    if (mask_active && !mask_active[s]) continue;
     walk_line<FMT>(img, g, table, masks, mask_index, peaks, a, e, s, t, max_scan, R);
     __syncthreads();  // the block's LDS is reused by its next line
   }
@@ -651,6 +663,7 @@ void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable
   if (g.nedges <= 0 || nangles <= 0) return;
   const int nlines = count * g.nedges * nangles;
   const RotScratch R = rot_scratch(lines, nlines, max_scan);
+  if (hipMemsetAsync(R.nlist, 0, sizeof(int32_t), st) != hipSuccess) return;  // the launches below report
   UPH_LAUNCH_DIAG(16, k_rot_points, dim3((nlines + 3) / 4), dim3(256), 0, st, g, table, masks,
                   mask_active, count, max_scan, R);
   switch (img.P.fmt) {

@@ -1151,7 +1151,7 @@ void launch_decode_gray(const uint8_t* src, int64_t spitch, int64_t sstride, con
                         int64_t vsum_stride, int32_t vx0, int32_t vx1, int count, hipStream_t st) {
   const int32_t nwr = (dst.P.W + 31) >> 5;
   const int64_t words = (int64_t)nwr * dst.P.H;
-  hipLaunchKernelGGL(k_decode_gray, dim3((unsigned)((words + 255) / 256), count), dim3(256), 0, st,
+  UPH_LAUNCH_DIAG(262144, k_decode_gray, dim3((unsigned)((words + 255) / 256), count), dim3(256), 0, st,
                      src, spitch, sstride, dst, white, bits, bits_stride, nwr, 1.0f / (float)nwr);
   if (vsum && vx0 <= vx1)
     hipLaunchKernelGGL(k_stripe_sums,
@@ -2160,7 +2160,7 @@ static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr
     hipLaunchKernelGGL(k_noise_bits, dim3((unsigned)((words + 255) / 256), count), dim3(256), 0, st,
                        img, g, bits, bstride, nwr, 1.0f / (float)nwr, active);
   }
-  hipLaunchKernelGGL(k_noise_classify<FMT>, grid, dim3(256), 0, st, img, gd, scr, ss, active, ctl,
+  UPH_LAUNCH_DIAG(131072, k_noise_classify<FMT>, grid, dim3(256), 0, st, img, gd, scr, ss, active, ctl,
                      bits, bstride);
   hipLaunchKernelGGL(k_noise_apply<FMT>, dim3(64, count), dim3(256), 0, st, img, g, scr, ss,
                      active, ctl);
