@@ -56,8 +56,8 @@ sys.path.insert(0, os.path.join(ROOT, "unpaper-gpu_amd", "python"))
 # serves the process; torch is only used for torch.distributed (gloo).
 from unpaper_hip import ctypes_abi as A  # noqa: E402
 from unpaper_hip.device import load_library, UnpaperHipError  # noqa: E402
-from unpaper_hip.pipeline import (Batch, DeviceBuffer, Runner, sink_memory, sink_pnm,  # noqa: E402
-                                  source_memory)
+from unpaper_hip.pipeline import (Batch, DeviceBuffer, Runner, sink_discard,  # noqa: E402
+                                  sink_memory, sink_pnm, source_memory, source_pnm)
 from unpaper_hip.workloads import A4_H, A4_W, C4_H, C4_W, c4_options  # noqa: E402
 
 METRIC = "pages/sec + Mpixel/s, 1000-page GRAY8 A4@300dpi batch, 1/2/4/8 GPU"
@@ -88,9 +88,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c3", choices=("c3", "c4"),
+    ap.add_argument("--config", default="c3", choices=("c3", "c4", "jpeg"),
                     help="c3: BASELINE configs[2] (the metric); c4: configs[3], RGB24 600dpi "
-                         "double-page sheets, layout double, bilinear, border wipe")
+                         "double-page sheets, layout double, bilinear, border wipe; jpeg: the "
+                         "JPEG decode peer (SURVEY f3) feeding the runner from JPEG files")
     ap.add_argument("--pages", type=int, default=0,
                     help="pages (c3) / sheets (c4) per GPU (default 1000 / 16)")
     ap.add_argument("--batch", type=int, default=0, help="sheets per batch (default 64 / 4)")
@@ -408,6 +409,78 @@ def host_threads_share():
         return os.cpu_count() or 1
 
 
+def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid):
+    """The JPEG decode peer in the runner: synthetic A4 GRAY8
+    pages saved by PIL as JPEG quality 95 (tmpfs), read by a runner file
+    source (host Huffman decode on the load pool into pinned memory, IDCT on
+    the device into the batch's input slots), the default pipeline, sheets
+    discarded.  PCIe- and host-inclusive: a figure of its own, never `value`
+    of the C3 line.  Two pages' outputs are checked against the oracle on
+    PIL's decode of the same files."""
+    from PIL import Image
+    from concurrent.futures import ThreadPoolExecutor
+    n = args.pages or 128
+    threads = host_threads_share()
+    tmpdir = tempfile.mkdtemp(prefix="uphip_jpeg_",
+                              dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    try:
+        # 16 distinct pages, reused round robin (the decode cost does not
+        # depend on the name)
+        def make(i):
+            g = np.empty((H, W), np.uint8)
+            L.uphip_synth_page_host(g.ctypes.data, W, W, H, firsts[0] + i)
+            path = os.path.join(tmpdir, "p%02d.jpg" % i)
+            Image.fromarray(g).save(path, "JPEG", quality=95)
+            return path
+        with ThreadPoolExecutor(min(16, threads)) as ex:
+            uniq = list(ex.map(make, range(16)))
+        paths = [uniq[i % 16] for i in range(n)]
+        mb = sum(os.path.getsize(p) for p in uniq) / 16 / 1e6
+        opts = A.Options()
+        L.uphip_options_init(C.byref(opts))
+        r = Runner(opts, 32, W, H, A.FMT_GRAY8, devices=devices[:1], streams=8,
+                   host_threads=threads)
+        try:
+            outs = os.path.join(tmpdir, "o%02d.pgm")
+            for rep in range(2):  # one warm-up pass (pinned buffers grow once)
+                t0 = time.perf_counter()
+                failed, err = r.run_host(n, source_pnm(paths), sink_pnm(outs, 16) if rep == 0 else
+                                         sink_discard())
+                t = time.perf_counter() - t0
+                if failed:
+                    raise UnpaperHipError("jpeg run: %d failed: %s" % (failed, err))
+            st = r.stats()
+        finally:
+            r.close()
+        checked = 0
+        if not args.no_verify:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            from oracle_py import Oracle
+            from unpaper_hip.hostimage import HostImage
+            from unpaper_hip.pipeline import pnm_read
+            oracle = Oracle()
+            oo = oracle.default_options()
+            for i in range(2):
+                px = np.asarray(Image.open(uniq[i]))
+                sheet, fmt, _ = oracle.process_sheet(oo, [HostImage.from_array(px.copy(),
+                                                                                A.FMT_GRAY8)])
+                exp = oracle.convert_for_save(sheet, fmt)
+                got = pnm_read(outs % i)
+                if not np.array_equal(got.payload(), exp.payload()):
+                    raise SystemExit("bench.py: JPEG page %d differs from the oracle" % i)
+                checked += 1
+    finally:
+        shutil.rmtree(tmpdir, ignore_errors=True)
+    return {"metric": "pages/s, A4 GRAY8 JPEG files through the runner (JPEG decode peer)",
+            "value": round(n / t, 2), "unit": "pages/s", "n_gpus": 1, "higher_is_better": True,
+            "dtype": "u8", "data": "synthetic (PIL JPEG quality 95, %.2f MB a page)" % mb,
+            "host_threads": threads, "load_s": round(st.load_s, 3),
+            "config": {"pages": n, "sheets_per_batch": 32, "streams": 8,
+                       "source": "JPEG files in tmpfs (16 distinct, round robin)",
+                       "sink": "discarded"},
+            "verified": checked, "library": version, "valid": valid}
+
+
 def run_c4(args, L, d, devices, firsts, n_gpus, version, valid, nsheets=0, steps=0, warmup=-1,
            batch=0):
     """BASELINE configs[3]: RGB24 600dpi double-page sheets, layout double,
@@ -538,6 +611,11 @@ def main():
     devices, firsts, n_gpus = shard_plan(d.world, d.rank, d.local_rank, args.gpus, ndev, npages)
     if args.config == "c4":
         line = run_c4(args, L, d, devices, firsts, n_gpus, version, valid)
+        if d.rank == 0:
+            print(json.dumps(line), flush=True)
+        return
+    if args.config == "jpeg":
+        line = run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid)
         if d.rank == 0:
             print(json.dumps(line), flush=True)
         return

@@ -10,6 +10,7 @@
 // conventions where T.81 leaves room: the colour transform from the JFIF /
 // Adobe markers or component ids (jdapimin.c default_decompress_parms),
 // component geometry (jdinput.c initial_setup, per_scan_setup).
+#include <algorithm>
 #include <cerrno>
 #include <cstdint>
 #include <cstdio>
@@ -25,11 +26,15 @@ namespace uph {
 
 namespace {
 
-constexpr int kLook = 9;  // Huffman lookahead bits
+constexpr int kLook = 10;  // Huffman lookahead bits
 
 struct Huff {
   bool present = false;
   uint16_t look[1 << kLook];  // len << 8 | symbol, 0 = longer code
+  // AC tables: a whole coefficient per lookahead when its code and magnitude
+  // bits fit: bits 0-4 bits consumed, 5-8 run, 9 end-of-block, 16-31 value
+  // (0 = take the general path)
+  uint32_t fast[1 << kLook];
   int32_t maxcode[18];        // largest code of each length, -1 if none
   int32_t valptr[17];
   int32_t mincode[17];
@@ -56,6 +61,19 @@ bool build_huff(Huff* t, const uint8_t* bits /*16*/, const uint8_t* vals, int nv
   }
   t->maxcode[17] = 0x7fffffff;
   t->present = true;
+  for (int p = 0; p < (1 << kLook); p++) {
+    const uint16_t e = t->look[p];
+    t->fast[p] = 0;
+    if (!e) continue;
+    const int len = e >> 8, rs = e & 0xff, r = rs >> 4, sz = rs & 15;
+    if (rs == 0) {  // end of block
+      t->fast[p] = (uint32_t)len | 1u << 9;
+    } else if (sz && len + sz <= kLook) {
+      const uint32_t m = ((uint32_t)p >> (kLook - len - sz)) & ((1u << sz) - 1u);
+      const int v = m < (1u << (sz - 1)) ? (int)m - (1 << sz) + 1 : (int)m;
+      t->fast[p] = (uint32_t)(len + sz) | (uint32_t)r << 5 | (uint32_t)(uint16_t)(int16_t)v << 16;
+    }
+  }
   return true;
 }
 
@@ -72,6 +90,23 @@ struct Bits {
   // inside the entropy-coded segment
   bool underrun() const { return n < 8 * fed; }
   void fill() {
+    // fast path: the next 8 bytes hold no 0xFF (no stuffing, no marker): as
+    // many whole bytes as fit in one go
+    if (!marker && p + 8 <= end) {
+      uint64_t w;
+      memcpy(&w, p, 8);
+      w = __builtin_bswap64(w);
+      const uint64_t nw = ~w;
+      if (!((nw - 0x0101010101010101ull) & ~nw & 0x8080808080808080ull)) {
+        const int take = (63 - n) >> 3;  // n + 8 take <= 63
+        if (take > 0) {
+          buf |= (w >> (64 - 8 * take)) << (64 - n - 8 * take);
+          p += take;
+          n += 8 * take;
+        }
+        return;
+      }
+    }
     while (n <= 56) {
       uint32_t byte = 0;
       if (marker || p >= end) fed++;
@@ -316,12 +351,19 @@ bool decode_scan(Parser& P, const uint8_t* b, int len, JpegDecoded* out) {
   }
   Bits bits{P.d + P.pos, P.d + P.n};
   int pred[4] = {0, 0, 0, 0};
-  int16_t blk[64];
+  // counts sized up front; coefficients written in place at `pos` (a block
+  // clears its 64 slots first, so the prefix up to its last non-zero is exact)
+  const size_t cbase = out->counts.size();
+  out->counts.resize(cbase + (size_t)nb);
+  uint8_t* counts = out->counts.data() + cbase;
+  size_t pos = out->coefs.size();
+  out->coefs.resize(pos + (size_t)std::max<int64_t>(nb * 8, 1 << 16));
+  int64_t bi = 0;
   int64_t mcu = 0;
   const int64_t nmcu = (int64_t)S.mcus_x * S.mcus_y;
   for (int my = 0; my < S.mcus_y; my++) {
-    out->groups.push_back((uint32_t)out->coefs.size());
-    if (out->coefs.size() > 0xF0000000u) return ffail(P, "image too large");
+    out->groups.push_back((uint32_t)pos);
+    if (pos > 0xF0000000u) return ffail(P, "image too large");
     for (int mx = 0; mx < S.mcus_x; mx++, mcu++) {
       if (P.restart && mcu > 0 && mcu % P.restart == 0) {
         // restart marker: byte-align, skip RSTn, reset the predictors
@@ -333,37 +375,53 @@ bool decode_scan(Parser& P, const uint8_t* b, int len, JpegDecoded* out) {
         bits.reset();
         pred[0] = pred[1] = pred[2] = pred[3] = 0;
       }
+      if (pos + 64 * 10 > out->coefs.size()) out->coefs.resize(out->coefs.size() * 2);
       for (int k = 0; k < S.blocks_per_mcu; k++) {
         const int i = bcomp[k];
-        memset(blk, 0, sizeof(blk));
+        int16_t* o = out->coefs.data() + pos;
+        memset(o, 0, 64 * sizeof(int16_t));  // runs of zeros need no stores
         const int t = bits.decode(P.dc[tdc[i]]);
         if (t < 0 || t > 11) return ffail(P, "corrupt entropy-coded data (DC)");
         const int diff = t ? extend(bits.get(t), t) : 0;
         pred[i] += diff;
-        blk[0] = (int16_t)pred[i];
-        int last = blk[0] ? 0 : -1;
+        o[0] = (int16_t)pred[i];
+        int last = o[0] ? 0 : -1;
+        const Huff& ac = P.ac[tac[i]];
         for (int kk = 1; kk < 64;) {
-          const int rs = bits.decode(P.ac[tac[i]]);
-          if (rs < 0) return ffail(P, "corrupt entropy-coded data (AC)");
-          const int r = rs >> 4, s = rs & 15;
-          if (s) {
+          if (bits.n < 16) bits.fill();
+          const uint32_t f = ac.fast[bits.buf >> (64 - kLook)];
+          if (f) {
+            const int used = f & 31;
+            bits.buf <<= used;
+            bits.n -= used;
+            if (f & (1u << 9)) break;  // EOB
+            const int r = (f >> 5) & 15;
             kk += r;
-            if (kk > 63 || s > 10) return ffail(P, "corrupt entropy-coded data (AC run)");
-            blk[kk] = (int16_t)extend(bits.get(s), s);
-            last = kk;
-            kk++;
+            if (kk > 63) return ffail(P, "corrupt entropy-coded data (AC run)");
+            o[kk] = (int16_t)(f >> 16);
+            last = kk++;
+            continue;
+          }
+          const int rs = bits.decode(ac);
+          if (rs < 0) return ffail(P, "corrupt entropy-coded data (AC)");
+          const int r = rs >> 4, sz = rs & 15;
+          if (sz) {
+            kk += r;
+            if (kk > 63 || sz > 10) return ffail(P, "corrupt entropy-coded data (AC run)");
+            o[kk] = (int16_t)extend(bits.get(sz), sz);
+            last = kk++;
           } else if (r == 15) {
             kk += 16;
           } else {
             break;  // EOB
           }
         }
-        const int cnt = last + 1;
-        out->counts.push_back((uint8_t)cnt);
-        out->coefs.insert(out->coefs.end(), blk, blk + cnt);
+        counts[bi++] = (uint8_t)(last + 1);
+        pos += (size_t)(last + 1);
       }
     }
   }
+  out->coefs.resize(pos);
   (void)nmcu;
   if (bits.underrun()) return ffail(P, "truncated or corrupt entropy-coded data");
   H.nblocks += nb;

@@ -1996,6 +1996,22 @@ __global__ void __launch_bounds__(kRFT, UPH_ROT_MINB) k_rotate_cubic_g8f(PlaneRe
       oA = (uint32_t)o.x;  // integer-valued in [0, 255]
       oB = (uint32_t)o.y;
     }
+#ifdef UPHIP_DIAG
+    if (UPH_DIAG_BITS(diag, 131072)) {  // tuning: +32 SALU a row (is the scalar unit a limit?)
+      int32_t z = k;
+      asm volatile(
+          "s_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\t"
+          "s_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\t"
+          "s_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\t"
+          "s_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\t"
+          "s_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\t"
+          "s_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\t"
+          "s_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\t"
+          "s_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 1"
+          : "+s"(z));
+      if (z == -1) oA = 0;
+    }
+#endif
     if (!FULL && !staged) break;  // uniform: the rows go through the loop below
     if (FULL) {  // every pixel in the mask: no per-lane branches
       obuf[k * kRFW + lane] = (uint8_t)oA;
@@ -2161,7 +2177,7 @@ bool launch_rotate_mask(const PlaneRef& src, const PlaneRef& dst, const RotateAr
         src.P.pitch * (int64_t)src.P.H < (1ll << 31) && !(diag_double() & 256)) {
       const dim3 fgrid((src.P.W + kRFW - 1) / kRFW, (src.P.H + kRFH - 1) / kRFH, count);
       const uint32_t mgxy = div_magic(fgrid.x * fgrid.y), mgx = div_magic(fgrid.x);
-      const int dd = diag_double() & (512 | 1024 | 2048 | 8192 | 65536);
+      const int dd = diag_double() & (512 | 1024 | 2048 | 8192 | 65536 | 131072);
 #ifdef UPHIP_DIAG
       struct PhasePrint {  // after the launches below: the per-tile phase clocks
         hipStream_t st;
