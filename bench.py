@@ -187,22 +187,20 @@ def load_hashes(name, key):
         return {}
 
 
-def resident_chunks(nchunks, streams):
-    """(batch k, chunk c) pairs whose outputs are resident after a pass: chunk c
-    runs on batch c % streams, so batch k ends with the last chunk of its class."""
-    return [(k, k + ((nchunks - 1 - k) // streams) * streams)
-            for k in range(min(streams, nchunks))]
-
-
 def verify_resident(runner, devices, firsts, npages, bsz, hashes):
-    """Hash every resident output page that has a committed oracle hash."""
-    nchunks = (npages + bsz - 1) // bsz
+    """Hash every resident output page that has a committed oracle hash: each
+    batch holds the outputs of the last chunk it ran (uphip_runner_slot_chunk;
+    the runner hands chunks to whichever batch is idle)."""
     checked = bad = 0
     for i in range(len(devices)):
-        for k, c in resident_chunks(nchunks, runner.streams):
+        for k in range(runner.streams):
+            ch = runner.slot_chunk(i, k)
+            if ch is None:
+                continue
+            first, n = ch
             b = runner.batch(i, k)
-            for s in range(min(bsz, npages - c * bsz)):
-                g = str(firsts[i] + c * bsz + s)
+            for s in range(n):
+                g = str(firsts[i] + first + s)
                 if g not in hashes:
                     continue
                 out = b.output(s)

@@ -573,8 +573,10 @@ UphipRunner *uphip_runner_create(const UphipOptions *options,
 void uphip_runner_destroy(UphipRunner *runner);
 /* Device-resident shards: device i processes shards[i] in place, `passes`
  * times back to back without draining between passes (benchmark steps);
- * chunk c of the shard runs on batch c % batches_per_device, whose outputs
- * stay resident (uphip_runner_batch).  Returns the number of failed jobs. */
+ * each chunk runs on a batch whose stream is idle (the first chunks on
+ * batches 0, 1, ... in order, later ones on whichever finishes first), and
+ * each batch's last chunk stays resident (uphip_runner_batch,
+ * uphip_runner_slot_chunk).  Returns the number of failed jobs. */
 int uphip_runner_run_device(UphipRunner *runner, const UphipDevicePages *shards,
                             int32_t passes);
 /* Host-fed run of jobs [0, njobs): source -> pinned staging -> device ->
@@ -590,6 +592,11 @@ int uphip_runner_output_info(UphipRunner *runner, int32_t *width, int32_t *heigh
                              int32_t *format, int64_t *linesize);
 UphipBatch *uphip_runner_batch(UphipRunner *runner, int32_t device_index,
                                int32_t slot);
+/* The chunk batch `slot` of device `device_index` ran last (its outputs are
+ * resident): first job (index into the device's shard or the host-fed job
+ * range) and sheet count; -1 when the batch has run none. */
+int64_t uphip_runner_slot_chunk(UphipRunner *runner, int32_t device_index, int32_t slot,
+                                int32_t *count);
 /* Host placement of device `device_index` (the peer of the reference's
  * per-device pools and stream-bound workers, image_pipeline.c:226-376,
  * batch_worker.c:174-253): the NUMA node of the GPU (sysfs via its PCI bus

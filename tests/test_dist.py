@@ -72,19 +72,6 @@ def test_single_process_device_fanout_plan():
         bench.shard_plan(1, 0, 0, 4, 2, 1000)
 
 
-@pytest.mark.parametrize("nchunks,streams", [(16, 16), (16, 4), (4, 16), (5, 2), (1, 1)])
-def test_resident_chunks(nchunks, streams):
-    """The chunk whose outputs each batch still holds after a pass (the bench
-    verifies exactly these pages)."""
-    sys.path.insert(0, ROOT)
-    import bench
-    got = bench.resident_chunks(nchunks, streams)
-    last = {}
-    for c in range(nchunks):
-        last[c % streams] = c
-    assert got == sorted(last.items())
-
-
 def test_diag_guard():
     sys.path.insert(0, ROOT)
     import bench

@@ -394,9 +394,13 @@ def test_runner_two_threads_one_device(hip, oracle):
         assert failed == 0, err
         st = r.stats()
         assert st.jobs_per_device[0] == 2 * n and st.jobs_per_device[1] == 2 * n
-        # chunk 0 (sheets 0..3) ran last on batch 0, chunk 1 (4..5) on batch 1
+        # each batch holds the chunk it ran last (chunks go to idle batches):
+        # between them the two batches of a thread hold chunk 0 (sheets 0..3)
+        # and chunk 1 (4..5)
         for i, first in enumerate((100, 200)):
-            for k, (c0, cnt) in enumerate(((0, 4), (4, 2))):
+            held = sorted(r.slot_chunk(i, k) + (k,) for k in range(2))
+            assert [h[:2] for h in held] == [(0, 4), (4, 2)], held
+            for c0, cnt, k in held:
                 b = r.batch(i, k)
                 for s in range(cnt):
                     exp = _oracle_out(oracle, opts, _pages(1, first + c0 + s, w, h)[0])

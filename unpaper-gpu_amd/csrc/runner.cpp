@@ -395,6 +395,8 @@ struct Slot {
   bool direct_out = false;  // this chunk's D2H went straight into the sink
   int64_t first = 0;        // first job of the chunk in flight
   int32_t count = 0;
+  int64_t last_first = -1;  // the chunk whose outputs the batch holds (uphip_runner_slot_chunk)
+  int32_t last_count = 0;
   std::vector<char> failed;  // per sheet of the chunk
 };
 
@@ -756,6 +758,16 @@ int uphip_runner_placement(UphipRunner* r, int32_t device_index, int32_t* numa_n
   return 0;
 }
 
+int64_t uphip_runner_slot_chunk(UphipRunner* r, int32_t device_index, int32_t slot,
+                                int32_t* count) {
+  if (!r || device_index < 0 || device_index >= (int)r->dev.size() || slot < 0 ||
+      slot >= (int)r->dev[(size_t)device_index].slots.size())
+    return fail("runner_slot_chunk: bad arguments"), -1;
+  const Slot& sl = r->dev[(size_t)device_index].slots[(size_t)slot];
+  if (count) *count = sl.last_first >= 0 ? sl.last_count : 0;
+  return sl.last_first;
+}
+
 UphipBatch* uphip_runner_batch(UphipRunner* r, int32_t device_index, int32_t slot) {
   if (!r || device_index < 0 || device_index >= (int)r->dev.size() || slot < 0 ||
       slot >= (int)r->dev[(size_t)device_index].slots.size())
@@ -778,12 +790,27 @@ int uphip_runner_run_device(UphipRunner* r, const UphipDevicePages* shards, int3
       uphip_set_device(dc.device);
       const UphipDevicePages& sh = shards[i];
       const int64_t nin = r->opts.input_count;
-      int k = 0;
-      std::vector<int32_t> used(dc.slots.size(), 0);
-      for (int32_t pass = 0; pass < passes; pass++, k = 0)
-      for (int64_t first = 0; first < sh.count; first += S, k++) {
+      const size_t ns = dc.slots.size();
+      std::vector<int32_t> used(ns, 0);
+      // Each chunk goes to a slot whose stream is idle (the first batches to
+      // the slots in order, then to whichever finishes first), so a slow
+      // chunk -- a sheet whose blackfilter replay runs long -- delays only its
+      // own slot: a fixed chunk -> slot mapping would queue every later chunk
+      // of that slot, pass after pass, behind it.
+      size_t next_fresh = 0;
+      auto idle_slot = [&]() -> size_t {
+        if (next_fresh < ns) return next_fresh++;
+        for (;;) {
+          for (size_t s = 0; s < ns; s++)
+            if (uphip_batch_query(dc.slots[s].b) != 0) return s;  // idle, or failed (run reports)
+          std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+      };
+      for (int32_t pass = 0; pass < passes; pass++)
+      for (int64_t first = 0; first < sh.count; first += S) {
         const int32_t n = (int32_t)std::min<int64_t>(S, sh.count - first);
-        Slot& sl = dc.slots[(size_t)k % dc.slots.size()];
+        const size_t k = idle_slot();
+        Slot& sl = dc.slots[k];
         if (uphip_batch_run_device(sl.b, n, (const uint8_t*)sh.pages + first * nin * sh.page_stride,
                                    sh.pitch, sh.page_stride) != 0) {
           if (dc.error.empty()) dc.error = uphip_last_error() ? uphip_last_error() : "run failed";
@@ -791,7 +818,9 @@ int uphip_runner_run_device(UphipRunner* r, const UphipDevicePages* shards, int3
           dc.failed += n;
           continue;
         }
-        used[(size_t)k % dc.slots.size()] = n;
+        used[k] = n;
+        sl.last_first = first;
+        sl.last_count = n;
         dc.done += n;
       }
       for (size_t s = 0; s < dc.slots.size(); s++) {
@@ -960,6 +989,8 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
             sl->first = first;
             sl->count = (int32_t)std::min<int64_t>(S, njobs - first);
             sl->failed.assign((size_t)sl->count, 0);
+            sl->last_first = first;
+            sl->last_count = sl->count;
             if (dsrc) {  // one DMA copy from the caller's pages, then the run
               const size_t bytes = (size_t)((sl->count * nin - 1) * src->page_stride + in_extent);
               hipStream_t bst = (hipStream_t)uphip_batch_stream(sl->b);

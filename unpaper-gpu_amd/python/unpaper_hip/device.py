@@ -52,7 +52,7 @@ EXPORTED = [
     "uphip_runner_run_device", "uphip_runner_run_host", "uphip_runner_get_stats",
     "uphip_runner_output_info", "uphip_runner_batch", "uphip_runner_layout", "uphip_batch_device_bytes", "uphip_host_alloc", "uphip_host_free",
     "uphip_check_libm", "uphip_jpeg_probe", "uphip_jpeg_read", "uphip_jpeg_decode",
-    "uphip_jpeg_entropy_decode", "uphip_runner_placement",
+    "uphip_jpeg_entropy_decode", "uphip_runner_placement", "uphip_runner_slot_chunk",
 ]
 
 
@@ -178,6 +178,8 @@ def load_library(path=LIB_PATH):
                                                C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                                C.POINTER(C.c_int64)]),
         "uphip_runner_batch": (C.c_void_p, [C.c_void_p, C.c_int32, C.c_int32]),
+        "uphip_runner_slot_chunk": (C.c_int64, [C.c_void_p, C.c_int32, C.c_int32,
+                                                C.POINTER(C.c_int32)]),
         "uphip_host_alloc": (C.c_void_p, [C.c_size_t]),
         "uphip_host_free": (None, [C.c_void_p]),
         "uphip_synth_sheets_rgb": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int32,

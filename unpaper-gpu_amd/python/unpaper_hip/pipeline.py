@@ -192,6 +192,13 @@ class Runner:
         b.close = lambda: None
         return b
 
+    def slot_chunk(self, device_index, slot):
+        """(first job, sheet count) of the chunk batch `slot` ran last (its
+        outputs are resident), or None when it has run none."""
+        n = C.c_int32(0)
+        first = self.lib.uphip_runner_slot_chunk(self.handle, device_index, slot, C.byref(n))
+        return None if first < 0 else (first, n.value)
+
     def run_device(self, shards, passes=1):
         """shards: one (device_ptr, pitch, page_stride, count) per device.
         Returns (failed jobs, the library's error message or None)."""
