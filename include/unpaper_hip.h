@@ -227,6 +227,14 @@ void uphip_noisefilter(UphipImage image, uint64_t intensity,
 void uphip_grayfilter(UphipImage image, UphipGrayfilterParameters params);
 float uphip_detect_rotation(UphipImage image, UphipRectangle mask,
                             const UphipDeskewParameters params);
+/* The peaks uphip_detect_rotation chooses from: detect_edge_rotation_peak
+ * (deskew.c:48-146) of every enabled edge (left, top, right, bottom, in that
+ * order) x every angle of detect_edge_rotation's loop (deskew.c:153-174, 0,
+ * -step, +step, ...) into peaks[edge * nangles + angle].  Returns the count
+ * written, or -1 (error, or more than `capacity`).  Not a backend entry. */
+int32_t uphip_detect_rotation_peaks(UphipImage image, UphipRectangle mask,
+                                    const UphipDeskewParameters params, int32_t *peaks,
+                                    int32_t capacity);
 void uphip_deskew(UphipImage source, UphipRectangle mask, float radians,
                   UphipInterpolation interpolate_type);
 

@@ -1084,6 +1084,25 @@ static float edge_rotation(OImage im, UphipRectangle mask,
   return detected;
 }
 
+int o_rotation_peaks(OImage im, UphipRectangle mask, const UphipDeskewParameters *pr,
+                     int32_t *out, int capacity) {
+  /* every peak detect_edge_rotation compares (deskew.c:153-174), edges in
+   * detect_rotation_cpu's order (deskew.c:181-218) */
+  const UphipDelta shifts[4] = {{1, 0}, {0, 1}, {-1, 0}, {0, -1}};
+  const bool on[4] = {pr->scan_edges.left, pr->scan_edges.top, pr->scan_edges.right,
+                      pr->scan_edges.bottom};
+  int n = 0;
+  for (int k = 0; k < 4; k++) {
+    if (!on[k]) continue;
+    for (float r = 0.0; r <= pr->deskewScanRangeRad;
+         r = (r >= 0.0) ? -(r + pr->deskewScanStepRad) : -r) {
+      if (n >= capacity) return -1;
+      out[n++] = edge_rotation_peak(im, mask, pr, shifts[k], tanf(r));
+    }
+  }
+  return n;
+}
+
 float o_detect_rotation(OImage im, UphipRectangle mask,
                         const UphipDeskewParameters *pr) {
   /* detect_rotation_cpu, deskew.c:181-241 */

@@ -67,6 +67,9 @@ void o_blurfilter(OImage image, UphipBlurfilterParameters params,
                   uint8_t abs_white_threshold);
 void o_noisefilter(OImage image, uint64_t intensity, uint8_t min_white_level);
 void o_grayfilter(OImage image, UphipGrayfilterParameters params);
+/* the per-(edge, angle) peaks o_detect_rotation chooses from; -1 past capacity */
+int o_rotation_peaks(OImage image, UphipRectangle mask, const UphipDeskewParameters *params,
+                     int32_t *out, int capacity);
 float o_detect_rotation(OImage image, UphipRectangle mask,
                         const UphipDeskewParameters *params);
 void o_deskew(OImage source, UphipRectangle mask, float radians, int32_t interp);

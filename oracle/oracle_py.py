@@ -73,6 +73,8 @@ class Oracle:
             "o_noisefilter": (None, [img, C.c_uint64, C.c_uint8]),
             "o_grayfilter": (None, [img, A.GrayfilterParameters]),
             "o_detect_rotation": (C.c_float, [img, A.Rectangle, C.POINTER(A.DeskewParameters)]),
+            "o_rotation_peaks": (C.c_int, [img, A.Rectangle, C.POINTER(A.DeskewParameters),
+                                           C.c_void_p, C.c_int]),
             "o_deskew": (None, [img, A.Rectangle, C.c_float, C.c_int32]),
             "o_center_mask": (None, [img, A.Point, A.Rectangle]),
             "o_process_sheet": (C.c_int, [C.POINTER(A.Options), C.POINTER(OImage), pimg,
@@ -186,6 +188,12 @@ class Oracle:
 
     def detect_rotation(self, h, mask, params):
         return self.lib.o_detect_rotation(self.wrap(h), mask, C.byref(params))
+
+    def rotation_peaks(self, h, mask, params):
+        out = np.zeros(4 * 1024, np.int32)
+        n = self.lib.o_rotation_peaks(self.wrap(h), mask, C.byref(params), out.ctypes.data, out.size)
+        assert n >= 0
+        return out[:n].copy()
 
     def deskew(self, h, mask, radians, interp):
         self.lib.o_deskew(self.wrap(h), mask, radians, interp)

@@ -374,3 +374,40 @@ def test_detect_rotation_fallbacks(hip, oracle, fmt, case):
     r1 = hip.detect_rotation(hip.upload(h), mask, p)
     r2 = oracle.detect_rotation(h, mask, p)
     assert np.float32(r1).tobytes() == np.float32(r2).tobytes()
+
+
+@pytest.mark.parametrize("fmt", [A.FMT_GRAY8, A.FMT_RGB24])
+@pytest.mark.parametrize("case", ["page", "left_edge", "wide_margin", "wide_range", "scan_all",
+                                  "all_edges", "small_step"])
+def test_rotation_peaks_every_line(hip, oracle, fmt, case):
+    """Every (edge, angle) peak of detect_edge_rotation_peak (deskew.c:48-146),
+    not only the chosen angle: the band path (segments of the float
+    recurrence, u16 slice sums), the direct walks (content > 128 steps in,
+    top/bottom edges, bands too wide, lines through X = 0 with many binade
+    segments) against the oracle, element for element."""
+    w, h, margin, deg = 1200, 900, 90, 1.7
+    mask = (0, 0, w - 1, h - 1)  # left lines start at X in [0, 1): they cross X = 0
+    kw = dict(size=1500, dev=10.0)
+    if case == "page":
+        w, h, deg, mask, kw = 800, 600, 0.6, (60, 0, 739, 599), dict(size=400)
+    elif case == "wide_margin":
+        margin = 330
+    elif case == "wide_range":
+        kw = dict(rng=40.0, step=2.0, dev=90.0, size=1500)
+    elif case == "scan_all":
+        kw = dict(size=-1, dev=10.0)
+    elif case == "all_edges":
+        kw = dict(size=700, dev=10.0, edges=(True, True, True, True))
+    elif case == "small_step":
+        kw = dict(rng=2.0, step=0.01, dev=10.0, size=1500)
+    img = make_image(w, h, fmt, seed=21, margin=margin)
+    oracle.deskew(img, A.rect(0, 0, w - 1, h - 1), float(np.float32(deg * math.pi / 180)),
+                  A.INTERP_LINEAR)
+    p = deskew_params(oracle, **kw)
+    got = hip.detect_rotation_peaks(hip.upload(img), A.rect(*mask), p)
+    exp = oracle.rotation_peaks(img, A.rect(*mask), p)
+    assert got.shape == exp.shape
+    # scan size -1 makes maxBlackness negative (255 * -1 * depth): every line
+    # stops at once and every peak is 0 in the reference too
+    assert exp.any() or case == "scan_all"
+    assert np.array_equal(got, exp), np.flatnonzero(got != exp)[:20]

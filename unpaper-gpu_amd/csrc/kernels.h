@@ -81,13 +81,22 @@ void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* 
 //    the sheet's resulting plane (moved, or the current one when the move is
 //    the identity) at rows[s * rows_stride + y] -- detect_border's row sums
 //    (masks.c:410-449), no other pass over the plane.
+//  * dry: count only (rows), write nothing (not with masks).
 struct MoveExtra {
   const MaskArgs* masks;
   uint32_t* rows;
   int64_t rows_stride;
   int32_t rx0, rx1;
   uint8_t thr;
+  bool dry;
 };
+// center_mask (center[s]) then apply_masks (masks[s], one mask) and
+// align_mask (align[s]) as one pass from src into dst (every byte of every
+// sheet written): what launch_move_rect + launch_move_rect_fused with masks
+// produce through an intermediate plane.  False (nothing launched) unless
+// the plane is GRAY8 and pitch * H < 2^31.
+bool launch_move_chain(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* center,
+                       const MaskArgs* masks, const MoveArgs* align, int count, hipStream_t st);
 // Returns false (nothing launched) unless the plane is GRAY8.
 bool launch_move_rect_fused(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* args,
                             const MoveExtra& x, int count, hipStream_t st);

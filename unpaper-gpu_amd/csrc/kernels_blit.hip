@@ -625,6 +625,8 @@ template <int MODE>
 __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneRef dst,
                                                             const MoveArgs* args, MoveExtra X) {
   constexpr bool kMask = (MODE & 1) != 0, kRows = (MODE & 2) != 0;
+  constexpr bool kDry = (MODE & 4) != 0;  // count only: nothing is written
+  static_assert(!(kDry && kMask), "a dry pass counts; it does not mask");
   const int s = blockIdx.z;
   const MoveArgs a = args[s];
   if (!kMask && !kRows && !a.active) return;
@@ -808,7 +810,7 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
             default: out = shift_bytes16<3>(w, r); break;
           }
         }
-        *reinterpret_cast<uint4*>(drow + x0) = out;
+        if (!kDry) *reinterpret_cast<uint4*>(drow + x0) = out;
         if (kRows && reg[k]) acc[ky] += dark16(out, reg[k], kadd);
       }
     }
@@ -868,7 +870,7 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
       o[d] = (sw4[d] & m0) | (mw4[d] & m2) | (bg4 & mb) | (mcol4 & mc);
     }
     const uint4 ov = make_uint4(o[0], o[1], o[2], o[3]);
-    *reinterpret_cast<uint4*>(dbase + (int64_t)y * P.pitch + x0) = ov;
+    if (!kDry) *reinterpret_cast<uint4*>(dbase + (int64_t)y * P.pitch + x0) = ov;
     if (kRows) {
       const uint32_t rg = cols16(x0, X.rx0, X.rx1);
       if (rg) atomicAdd(&rowcnt[y - yb], dark16(ov, rg, kadd));
@@ -899,13 +901,233 @@ bool launch_move_rect_fused(const PlaneRef& src, const PlaneRef& dst, const Move
   if (src.P.fmt != F_GRAY8) return false;
   const int64_t blocks = (src.P.H + kMoveBlockRows - 1) / kMoveBlockRows;
   const dim3 grid((unsigned)(blocks < 1 ? 1 : blocks), 1, count);
-  const int mode = (x.masks ? 1 : 0) | (x.rows ? 2 : 0);
+  const int mode = (x.masks ? 1 : 0) | (x.rows ? 2 : 0) | (x.dry ? 4 : 0);
+  if (x.dry && x.masks) return false;
   switch (mode) {
+    case 6: UPH_LAUNCH_DIAG(4, k_move_rect_g16<6>, grid, dim3(kThreads), 0, st, src, dst, args, x); break;
     case 1: UPH_LAUNCH_DIAG(4, k_move_rect_g16<1>, grid, dim3(kThreads), 0, st, src, dst, args, x); break;
     case 2: UPH_LAUNCH_DIAG(4, k_move_rect_g16<2>, grid, dim3(kThreads), 0, st, src, dst, args, x); break;
     case 3: UPH_LAUNCH_DIAG(4, k_move_rect_g16<3>, grid, dim3(kThreads), 0, st, src, dst, args, x); break;
     default: UPH_LAUNCH_DIAG(4, k_move_rect_g16<0>, grid, dim3(kThreads), 0, st, src, dst, args, x); break;
   }
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// center_mask, then apply_masks + align_mask (sheet_stages.c:415-499,
+// masks.c:222-322) as ONE gather from the uncentred plane R, so that the
+// centred plane C is never written: O(x, y) follows the align move's class
+// rule back to C, C's centring rule back to R, and ends at a pixel of R or a
+// constant (a background or the mask colour).  The classes are
+// k_move_rect_g16's, stage by stage (move_class), so O is byte for byte what
+// the two passes produce.  The border scan between the two moves reads only
+// C's dark counts per row, which a dry centring pass (k_move_rect_g16 with
+// kDry) counts from R without writing C.
+//
+// Columns: every stage's class changes only at a few columns (the move's
+// five, the mask's two, and the first move's five seen through both possible
+// outcomes of the second), so a row is a few intervals with one source
+// offset or constant each.  A block (kMoveBlockRows rows of one sheet)
+// finds the breakpoints, evaluates each (row, interval) once into LDS, and
+// its lanes then write 16-byte vectors: one constant, or two aligned loads of
+// R realigned by the interval's offset; vectors holding a breakpoint go byte
+// by byte.
+// ---------------------------------------------------------------------------
+// k_move_rect_g16's class of (x, y) under move `a` (0 keep, 1 background,
+// 2 moved: (x, y) become its source, 3 mask colour)
+__device__ __forceinline__ int move_class(const MoveArgs& a, int32_t W, int32_t H, bool kmask,
+                                          const Rect& mk, int32_t& x, int32_t& y) {
+  const bool inmk = y >= mk.y0 && y <= mk.y1 && x >= mk.x0 && x <= mk.x1;
+  if (!a.active) return kmask && !inmk ? 3 : 0;  // the identity: masked in place
+  const Rect A = clip(a.area, W, H);
+  const int32_t aw = A.x1 - A.x0 + 1, ah = A.y1 - A.y0 + 1;
+  const int32_t sw = iabs(a.area.x0 - a.area.x1) + 1, sh = iabs(a.area.y0 - a.area.y1) + 1;
+  const int32_t u = x - a.tx, v = y - a.ty;
+  const bool trow = v >= 0 && v < sh, mrow = trow && v < ah;
+  const bool arow = y >= A.y0 && y <= A.y1;
+  const bool c1 = u >= 0 && u < sw, c2 = u < aw, c4 = x >= A.x0 && x <= A.x1;
+  int cls = (trow && c1) ? ((mrow && c2) ? 2 : 1) : ((arow && c4) ? 1 : 0);
+  if (kmask && cls == 0 && !inmk) cls = 3;
+  if (cls == 2) {
+    x = A.x0 + u;
+    y = A.y0 + v;
+  }
+  return cls;
+}
+
+constexpr int kChainBp = 17;  // 7 of the align move and mask + 2 x 5 of the centring
+struct ChainSheet {
+  MoveArgs m1, m2;
+  Rect mk;
+  bool kmask;
+  uint8_t mcol, bg1, bg2;
+};
+// The source of O(x, y): {-1, byte offset of the R pixel from (x, y)} or
+// {constant, 0}
+__device__ __forceinline__ int2 chain_cell(const ChainSheet& c, int32_t W, int32_t H,
+                                           int64_t pitch, int32_t x, int32_t y) {
+  int32_t sx = x, sy = y;
+  const int c2 = move_class(c.m2, W, H, c.kmask, c.mk, sx, sy);
+  if (c2 == 1) return make_int2(c.bg2, 0);
+  if (c2 == 3) return make_int2(c.mcol, 0);
+  const int c1 = move_class(c.m1, W, H, false, c.mk, sx, sy);
+  if (c1 == 1) return make_int2(c.bg1, 0);
+  return make_int2(-1, (int32_t)((int64_t)(sy - y) * pitch + (sx - x)));
+}
+
+__global__ void __launch_bounds__(kThreads) k_move_chain_g16(PlaneRef src, PlaneRef dst,
+                                                             const MoveArgs* center,
+                                                             const MaskArgs* masks,
+                                                             const MoveArgs* align) {
+  const int s = blockIdx.z;
+  const Planes& P = src.P;
+  const int32_t W = P.W, H = P.H;
+  const int64_t pitch = P.pitch;
+  const uint8_t* sbase = plane_ptr(src, s);
+  uint8_t* dbase = plane_ptr(dst, s);
+  const int32_t yb = blockIdx.x * kMoveBlockRows;
+  const int nrows = imin(kMoveBlockRows, H - yb);
+  ChainSheet c;
+  c.m1 = center[s];
+  c.m2 = align[s];
+  const MaskArgs& ma = masks[s];
+  c.kmask = ma.n > 0;
+  c.mk = c.kmask ? normalize(ma.m[0]) : Rect{INT_MIN / 2, INT_MIN / 2, INT_MAX / 2, INT_MAX / 2};
+  c.mcol = gray_of(Px{ma.color[0], ma.color[1], ma.color[2]});
+  c.bg1 = gray_of(Px{c.m1.bg[0], c.m1.bg[1], c.m1.bg[2]});
+  c.bg2 = gray_of(Px{c.m2.bg[0], c.m2.bg[1], c.m2.bg[2]});
+  __shared__ int32_t bp[kChainBp];
+  __shared__ int32_t nbp_s;
+  __shared__ int2 cell[kMoveBlockRows][kChainBp + 1];
+  if (threadIdx.x == 0) {
+    // the columns where some stage's class can change (first column of the
+    // new interval), sorted, unique, inside (0, W)
+    int32_t b[kChainBp];
+    int n = 0;
+    auto add = [&](int32_t v) {
+      if (v > 0 && v < W) b[n++] = v;
+    };
+    const MoveArgs& m2 = c.m2;
+    int32_t d2 = 0;
+    if (m2.active) {
+      const Rect A = clip(m2.area, W, H);
+      const int32_t sw = iabs(m2.area.x0 - m2.area.x1) + 1;
+      add(m2.tx);
+      add(m2.tx + (A.x1 - A.x0 + 1));
+      add(m2.tx + sw);
+      add(A.x0);
+      add(A.x1 + 1);
+      d2 = A.x0 - m2.tx;
+    }
+    if (c.kmask) {
+      add(c.mk.x0);
+      add(c.mk.x1 + 1);
+    }
+    if (c.m1.active) {
+      const MoveArgs& m1 = c.m1;
+      const Rect A = clip(m1.area, W, H);
+      const int32_t sw = iabs(m1.area.x0 - m1.area.x1) + 1;
+      const int32_t q[5] = {m1.tx, m1.tx + (A.x1 - A.x0 + 1), m1.tx + sw, A.x0, A.x1 + 1};
+      for (int k = 0; k < 5; k++) {
+        add(q[k]);                  // seen through a kept column of the align move
+        if (m2.active) add(q[k] - d2);  // through a moved one
+      }
+    }
+    for (int i = 1; i < n; i++)  // insertion sort
+      for (int k = i; k > 0 && b[k - 1] > b[k]; k--) {
+        const int32_t t = b[k];
+        b[k] = b[k - 1];
+        b[k - 1] = t;
+      }
+    int m = 0;
+    for (int i = 0; i < n; i++)
+      if (m == 0 || b[i] != bp[m - 1]) bp[m++] = b[i];
+    nbp_s = m;
+  }
+  __syncthreads();
+  const int nbp = nbp_s;
+  // every (row, interval) of the block: interval i starts at column 0 or bp[i-1]
+  for (int t = threadIdx.x; t < nrows * (nbp + 1); t += blockDim.x) {
+    const int r = t / (nbp + 1), i = t - r * (nbp + 1);
+    cell[r][i] = chain_cell(c, W, H, pitch, i == 0 ? 0 : bp[i - 1], yb + r);
+  }
+  __syncthreads();
+  auto interval = [&](int32_t x) {
+    int i = 0;
+    for (int k = 0; k < nbp; k++) i += bp[k] <= x;
+    return i;
+  };
+  const int lane = threadIdx.x & 63;
+  const int32_t nv = (W + 15) >> 4;
+  const int r0 = (threadIdx.x >> 6) * kMoveRows;  // the wave's rows of the block
+  // uniform vectors: lanes along the row, the wave's kMoveRows rows
+  for (int32_t vi = lane; vi < nv; vi += 64) {
+    const int32_t x0 = 16 * vi;
+    const int il = interval(x0);
+    if (x0 + 16 > W || il != interval(x0 + 15)) continue;  // byte path below
+    for (int k = 0; k < kMoveRows; k++) {
+      const int r = r0 + k;
+      if (r >= nrows) break;
+      const int32_t y = yb + r;
+      const int2 ce = cell[r][il];
+      uint4 out;
+      if (ce.x >= 0) {
+        const uint32_t v4 = (uint32_t)ce.x * 0x01010101u;
+        out = make_uint4(v4, v4, v4, v4);
+      } else {
+        // R bytes x0 + off .. + 15 of this row's offset: two aligned vectors
+        // realigned by (off mod 16), the same for every vector of the interval
+        const uint8_t* p = sbase + (int64_t)y * pitch + x0 + ce.y;
+        const int r16 = (int)((uintptr_t)p & 15u);
+        const uint4* q = reinterpret_cast<const uint4*>(p - r16);
+        const uint4 lo = q[0];
+        const uint4 hi = r16 ? q[1] : lo;
+        const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        const int qd = r16 >> 2, rb = r16 & 3;
+        uint32_t d[5];
+#pragma unroll
+        for (int j = 0; j < 5; j++)
+          d[j] = qd == 0 ? w[j] : qd == 1 ? w[j + 1] : qd == 2 ? w[j + 2] : w[j + 3];
+        out = make_uint4(__builtin_amdgcn_alignbyte(d[1], d[0], rb),
+                         __builtin_amdgcn_alignbyte(d[2], d[1], rb),
+                         __builtin_amdgcn_alignbyte(d[3], d[2], rb),
+                         __builtin_amdgcn_alignbyte(d[4], d[3], rb));
+      }
+      *reinterpret_cast<uint4*>(dbase + (int64_t)y * pitch + x0) = out;
+    }
+  }
+  // vectors holding a breakpoint, and the row's partial last vector: byte by
+  // byte, a lane per (row, vector); columns >= W are written as 0
+  int32_t dv[kChainBp + 1];
+  int nd = 0;
+  for (int k = 0; k < nbp; k++) {
+    const int32_t v = bp[k] >> 4;
+    if ((bp[k] & 15) && (nd == 0 || dv[nd - 1] != v)) dv[nd++] = v;
+  }
+  if ((W & 15) && (nd == 0 || dv[nd - 1] != (W >> 4))) dv[nd++] = W >> 4;
+  for (int t = threadIdx.x; t < nrows * nd; t += blockDim.x) {
+    const int r = t / nd, x0 = 16 * dv[t - r * nd];
+    const int32_t y = yb + r;
+    const uint8_t* srow = sbase + (int64_t)y * pitch;
+    uint32_t o[4] = {0u, 0u, 0u, 0u};
+    for (int j = 0; j < 16; j++) {
+      const int32_t x = x0 + j;
+      if (x >= W) break;
+      const int2 ce = cell[r][interval(x)];
+      const uint32_t v = ce.x >= 0 ? (uint32_t)ce.x : srow[x + ce.y];
+      o[j >> 2] |= v << (8 * (j & 3));
+    }
+    *reinterpret_cast<uint4*>(dbase + (int64_t)y * pitch + x0) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+bool launch_move_chain(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* center,
+                       const MaskArgs* masks, const MoveArgs* align, int count, hipStream_t st) {
+  if (src.P.fmt != F_GRAY8 || src.P.pitch * (int64_t)src.P.H >= (1ll << 31) || src.P.H < 1)
+    return false;
+  const int64_t blocks = (src.P.H + kMoveBlockRows - 1) / kMoveBlockRows;
+  UPH_LAUNCH_DIAG(4, k_move_chain_g16, dim3((unsigned)blocks, 1, count), dim3(kThreads), 0, st,
+                  src, dst, center, masks, align);
   return true;
 }
 
@@ -1642,7 +1864,9 @@ __global__ void __launch_bounds__(kRFT, UPH_ROT_MINB) k_rotate_cubic_g8f(PlaneRe
   // scan need not read the rotated plane again; per tile summed in LDS, then
   // one atomic per column
   __shared__ uint32_t csum_s[kRFW];
-  __shared__ int32_t done_s;  // waves whose column sums are in csum_s (UPH_ROT_V2)
+#if UPH_ROT_V2
+  __shared__ int32_t done_s;  // waves whose column sums are in csum_s
+#endif
   // one tile (txi, tyi) of sheet s; every return is block-uniform
   auto tile = [&](int txi, int tyi, int s) {
 #ifdef UPHIP_DIAG

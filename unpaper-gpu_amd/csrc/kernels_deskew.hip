@@ -10,7 +10,8 @@
 // (int)X_i differs.  So all angles and the first kDepth steps read one band
 // of columns beside the mask edge.  The fast path is
 //   k_rot_points  the float recurrence X += -m of every line (deskew.c:
-//                 107-112) in closed form per binade -> column lists;
+//                 107-112) in closed form per binade -> a few segments per
+//                 line (point i of a segment: X = T + (i - i0) d, exact);
 //   k_rot_band_g  one workgroup per 128-row slice of a (sheet, edge): the
 //                 slice's band is staged in LDS as per-column prefix sums of
 //                 the blackness, then every angle x kDepth steps is summed
@@ -86,33 +87,58 @@ __device__ __forceinline__ LineSetup line_setup(const Rect& mask, const RotGeom&
   return L;
 }
 
-// Scratch layout of one launch (all int32):
-//   cols   [nlines][max_scan]   column of point i of each left/right line
+// Scratch layout of one launch:
+//   segs   [nlines][kLineSegs]  int4 {i0, n, T, d}: points i0 .. i0+n of a
+//                               left/right line have column (int)(T + (i-i0) d)
+//                               (T, d floats, the sum exact: it is the
+//                               recurrence's float X_i)
+//   nseg   [nlines]             segments of the line (0: none, walked directly)
 //   ends   [nlines][2]          first and last column of the line
-//   part   [nlines][nslices][kDepth]  band slice sums
+//   part   [nlines][nslices][kDepth]  band slice sums, u16 (<= 128 * 255)
 //   flag   [nlines]             1 = walk the line directly (k_rot_line)
 //   state  [nlines][4]          band result after kDepth steps: accumulated,
 //                               last step's blackness, peak, valid
 //   list   [nlines]             the flagged lines (k_rot_line's work list)
 //   nlist  [1]                  their count (zeroed before k_rot_points)
+constexpr int kLineSegs = 32;  // a line with more (it passes near X = 0) is walked directly
 struct RotScratch {
-  int32_t *cols, *ends, *part, *flag, *state, *list, *nlist;
+  int4* segs;
+  int32_t *nseg, *ends;
+  uint16_t* part;
+  int32_t *flag, *state, *list, *nlist;
 };
 
 __host__ __device__ static inline int rot_slices(int max_scan) { return (max_scan + kSliceRows - 1) / kSliceRows; }
 
+// int32 words of each array (part: u16 pairs; kDepth is even)
 __host__ __device__ static inline RotScratch rot_scratch(int32_t* base, int nlines, int max_scan) {
   RotScratch r;
   const int64_t ms = max_scan > 0 ? max_scan : 1;
   const int64_t ns = (ms + kSliceRows - 1) / kSliceRows;
-  r.cols = base;
-  r.ends = r.cols + (int64_t)nlines * ms;
-  r.part = r.ends + 2 * (int64_t)nlines;
-  r.flag = r.part + (int64_t)nlines * ns * kDepth;
+  r.segs = reinterpret_cast<int4*>(base);
+  r.nseg = base + (int64_t)nlines * kLineSegs * 4;
+  r.ends = r.nseg + nlines;
+  r.part = reinterpret_cast<uint16_t*>(r.ends + 2 * (int64_t)nlines);
+  r.flag = r.ends + 2 * (int64_t)nlines + (int64_t)nlines * ns * (kDepth / 2);
   r.state = r.flag + nlines;
   r.list = r.state + 4 * (int64_t)nlines;
   r.nlist = r.list + nlines;
   return r;
+}
+
+// column of point i of a left/right line from its segments (sorted by i0,
+// covering 0 .. scan-1): exact, see k_rot_points
+__device__ __forceinline__ int32_t seg_col(const int4* sg, int nsg, int i) {
+  float T = 0.0f, d = 0.0f;
+  int b = 0;
+  for (int q = 0; q < nsg; q++) {
+    const int4 v = sg[q];
+    if (v.x > i) break;
+    T = __int_as_float(v.z);
+    d = __int_as_float(v.w);
+    b = v.x;
+  }
+  return (int)fmaf((float)(i - b), d, T);
 }
 
 const int32_t* rotation_line_flags(const int32_t* lines, int nlines, int max_scan) {
@@ -123,8 +149,8 @@ size_t rotation_lines_bytes(int count, int nedges, int nangles, int max_scan) {
   const int64_t nlines = (int64_t)count * nedges * nangles;
   const int64_t ms = max_scan > 0 ? max_scan : 1;
   const int64_t ns = (ms + kSliceRows - 1) / kSliceRows;
-  return sizeof(int32_t) * (size_t)(nlines * ms + 2 * nlines + nlines * ns * kDepth + nlines +
-                                    4 * nlines + nlines + 1);
+  return sizeof(int32_t) * (size_t)(nlines * kLineSegs * 4 + nlines + 2 * nlines +
+                                    nlines * ns * (kDepth / 2) + nlines + 4 * nlines + nlines + 1);
 }
 
 // ---- k_rot_points: the points of every left/right line --------------------
@@ -134,126 +160,96 @@ size_t rotation_lines_bytes(int count, int nedges, int nangles, int max_scan) {
 // increment d every step (for a tie, s/u a half-integer, the even multiple
 // wins, constant from an even X_i/u on), so X_i = T + k*d exactly for a whole
 // run of steps, whose length follows from integer arithmetic in units of u.
-// Lane 0 of a wave splits its line into such segments, with one explicit
-// float step at each binade change, odd-tie start or X = 0; all 64 lanes then
-// write the points in parallel.  Beyond kMaxSegs segments lane 0 replays the
-// rest of the recurrence itself.
-constexpr int kMaxSegs = 64;
-struct PointSeg {
-  int32_t i0, n;     // points i0 .. i0 + n
-  double T, du;      // |X_i0| and the increment d (exact doubles)
-  float sign;
-};
-
+// A thread per line splits it into such segments, with one explicit float
+// step at each binade change, odd-tie start or X = 0, and stores them (the
+// band and the direct walk evaluate a point's column from them: T, d and
+// every T + k d are floats, so fmaf(k, d, T) is exact).  A line with more
+// than kLineSegs segments (one passing near X = 0) is walked directly.
 __global__ void __launch_bounds__(256) k_rot_points(RotGeom g, const RotTable* table,
                                                     const Rect* masks, const int32_t* mask_active,
-                                                    int count, int max_scan, RotScratch R) {
+                                                    int count, RotScratch R) {
   const int na = table->nangles;
   const int nlines = count * g.nedges * na;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int t = blockIdx.x * 4 + w;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nlines) return;
-  __shared__ PointSeg segs[4][kMaxSegs];
-  __shared__ int32_t nseg_s[4], last_s[4];
   const int a = t % na, e = (t / na) % g.nedges, s = t / (na * g.nedges);
-  const bool live = !(mask_active && !mask_active[s]) && g.edge_shift[e][1] == 0;
-  if (!live) {
-    if (lane == 0) {
-      R.ends[2 * t] = 0;
-      R.ends[2 * t + 1] = 0;
-      R.flag[t] = 1;
-      R.state[4 * t + 3] = 0;
-      // a top/bottom edge of an active sheet: walked directly
-      if (!(mask_active && !mask_active[s])) R.list[atomicAdd(R.nlist, 1)] = t;
-    }
+  const bool act = !(mask_active && !mask_active[s]);
+  R.state[4 * t + 3] = 0;
+  if (!act || g.edge_shift[e][1] != 0) {
+    R.ends[2 * t] = 0;
+    R.ends[2 * t + 1] = 0;
+    R.nseg[t] = 0;
+    R.flag[t] = 1;
+    if (act) R.list[atomicAdd(R.nlist, 1)] = t;  // a top/bottom edge: walked directly
     return;
   }
   const LineSetup L = line_setup(masks[s], g, g.edge_shift[e][0], 0, table->slope[a]);
   const int scan = L.scan;
-  int32_t* cols = R.cols + (int64_t)t * max_scan;
-  if (lane == 0) {
-    int ns = 0, last = 0;
-    float X = L.X;
-    const float st = L.stepX;
-    int i = 0;
-    while (scan > 0) {
-      if (ns >= kMaxSegs) {
-        // the literal recurrence for the remaining points
-        for (int k = i; k < scan; k++) {
-          cols[k] = last = (int)X;
-          X += st;
-        }
+  int4* sg = R.segs + (int64_t)t * kLineSegs;
+  int ns = 0, last = 0;
+  bool over = false;
+  float X = L.X;
+  const float st = L.stepX;
+  int i = 0;
+  while (scan > 0) {
+    if (ns >= kLineSegs) {
+      over = true;
+      break;
+    }
+    const float sign = X > 0.0f ? 1.0f : -1.0f;
+    const double T = (double)fabsf(X), sig = (double)st * (double)sign;
+    int64_t nn = 0;
+    double du = 0.0;
+    if (X != 0.0f) {
+      int E;
+      frexpf(fabsf(X), &E);  // |X| = m * 2^E, m in [0.5, 1)
+      if (E < -100) {        // u would leave the float range: walk directly
+        over = true;
         break;
       }
-      const float sign = X > 0.0f ? 1.0f : -1.0f;
-      const double T = (double)fabsf(X), sig = (double)st * (double)sign;
-      int64_t nn = 0;
-      double du = 0.0;
-      if (X != 0.0f) {
-        int E;
-        frexpf(fabsf(X), &E);  // |X| = m * 2^E, m in [0.5, 1)
-        const double lo = ldexp(1.0, E - 1), hi = ldexp(1.0, E), u = ldexp(1.0, E - 24);
-        const double q = sig / u;  // exact: u is a power of two
-        const double fqd = floor(q);
-        const int64_t fq = (int64_t)fqd;
-        // A tie (q = fq + 1/2) rounds to the even multiple of u: from an even
-        // |X|/u the increment is then always the even one of fq, fq + 1; from
-        // an odd one, one explicit step first.
-        const bool tie = q - fqd == 0.5;
-        if (!tie || !(((int64_t)(T / u)) & 1)) {
-          const int64_t dq = tie ? (fq & 1 ? fq + 1 : fq) : (int64_t)floor(q + 0.5);
-          const int64_t H = (int64_t)((hi - T) / u), G = (int64_t)((T - lo) / u);
-          const int64_t rem = scan - 1 - i;  // steps still to take
-          // steps k = 1.. whose exact sum X_{k-1} + s stays in [lo, hi)
-          if (dq > 0) {
-            const int64_t c = H - fq - 1;
-            nn = c >= 0 ? c / dq + 1 : 0;
-          } else if (dq < 0) {
-            const int64_t c = G + fq;
-            nn = c >= 0 ? c / (-dq) + 1 : 0;
-          } else {
-            nn = (q >= 0.0 || G >= 1) ? rem : 0;
-          }
-          if (nn > rem) nn = rem;
-          du = (double)dq * u;
+      const double lo = ldexp(1.0, E - 1), hi = ldexp(1.0, E), u = ldexp(1.0, E - 24);
+      const double q = sig / u;  // exact: u is a power of two
+      const double fqd = floor(q);
+      const int64_t fq = (int64_t)fqd;
+      // A tie (q = fq + 1/2) rounds to the even multiple of u: from an even
+      // |X|/u the increment is then always the even one of fq, fq + 1; from
+      // an odd one, one explicit step first.
+      const bool tie = q - fqd == 0.5;
+      if (!tie || !(((int64_t)(T / u)) & 1)) {
+        const int64_t dq = tie ? (fq & 1 ? fq + 1 : fq) : (int64_t)floor(q + 0.5);
+        const int64_t H = (int64_t)((hi - T) / u), G = (int64_t)((T - lo) / u);
+        const int64_t rem = scan - 1 - i;  // steps still to take
+        // steps k = 1.. whose exact sum X_{k-1} + s stays in [lo, hi)
+        if (dq > 0) {
+          const int64_t c = H - fq - 1;
+          nn = c >= 0 ? c / dq + 1 : 0;
+        } else if (dq < 0) {
+          const int64_t c = G + fq;
+          nn = c >= 0 ? c / (-dq) + 1 : 0;
+        } else {
+          nn = (q >= 0.0 || G >= 1) ? rem : 0;
         }
+        if (nn > rem) nn = rem;
+        du = (double)dq * u;  // s rounded to u: a float (s itself, or < 2^24 units of u)
       }
-      segs[w][ns++] = PointSeg{i, (int32_t)nn, T, du, sign};
-      i += (int)nn;
-      if (i >= scan - 1) {
-        last = (int)((double)sign * (T + (double)nn * du));
-        break;
-      }
-      // one explicit step (binade change, tie or zero)
-      X = sign * (float)(T + (double)nn * du) + st;
-      i++;
     }
-    nseg_s[w] = ns;
-    last_s[w] = last;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  const int ns = nseg_s[w];
-  if (ns > 0) {
-    for (int q = 0; q < ns; q++) {
-      const PointSeg sg = segs[w][q];
-      for (int k = lane; k <= sg.n; k += 64)
-        cols[sg.i0 + k] = (int)((double)sg.sign * (sg.T + (double)k * sg.du));
+    const float Ts = sign * (float)T, ds = sign * (float)du;
+    sg[ns++] = make_int4(i, (int32_t)nn, __float_as_int(Ts), __float_as_int(ds));
+    i += (int)nn;
+    if (i >= scan - 1) {
+      last = (int)fmaf((float)nn, ds, Ts);
+      break;
     }
+    // one explicit step (binade change, tie or zero)
+    X = sign * (float)(T + (double)nn * du) + st;
+    i++;
   }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  if (lane == 0) {
-    int first = 0, last = 0;
-    if (scan > 0) {
-      first = (int)L.X;  // point 0 is the start value itself
-      last = last_s[w];
-    }
-    R.ends[2 * t] = first;
-    R.ends[2 * t + 1] = last;
-    R.flag[t] = 0;
-    R.state[4 * t + 3] = 0;
-  }
+  const int first = scan > 0 ? (int)L.X : 0;  // point 0 is the start value itself
+  R.ends[2 * t] = first;
+  R.ends[2 * t + 1] = over ? first : last;
+  R.nseg[t] = over ? 0 : ns;
+  R.flag[t] = over;
+  if (over) R.list[atomicAdd(R.nlist, 1)] = t;
 }
 
 // Band of one (sheet, edge): columns [bx0, bx0 + bw) cover every point of
@@ -305,7 +301,7 @@ __global__ void __launch_bounds__(kBandThreads, 4)
   const int32_t ylo = imax(nm.y0, 0), yhi = imin(nm.y1, g.H - 1);
   const int32_t ystart = (int32_t)LS.Y;  // exact: integer start, +1.0 per point
   const uint8_t* base = plane_ptr(img, s);
-  const int rows = i1 - i0, n = rows * bw;
+  const int rows = i1 - i0;
   // blackness 255-max(rgb) of in-mask, in-image pixels (0 elsewhere,
   // get_pixel's white); a wave per row, lanes along it (no index division),
   // unconditional clamped loads masked arithmetically, all of a row's in
@@ -377,11 +373,34 @@ __global__ void __launch_bounds__(kBandThreads, 4)
   const int32_t o0 = sxh * lane - bx0, o1 = sxh * (lane + 64) - bx0;
   const int ns = rot_slices(max_scan);
   for (int a = w; a < na; a += nw) {
-    const int t = tbase + a;
-    const int32_t* cols = R.cols + (int64_t)t * max_scan + i0;
-    // the slice's columns, two rows per lane; run starts by ballot
-    const int32_t cA = lane < rows ? cols[lane] : 0;
-    const int32_t cB = lane + 64 < rows ? cols[lane + 64] : 0;
+    const int t = __builtin_amdgcn_readfirstlane(tbase + a);
+    // the slice's columns, two rows per lane (from the line's segments that
+    // overlap the slice); run starts by ballot
+    int32_t cA = 0, cB = 0;
+    {
+      const int4* sg = R.segs + (int64_t)t * kLineSegs;
+      const int nsg = __builtin_amdgcn_readfirstlane(R.nseg[t]);
+      const int iA = i0 + lane, iB = i0 + 64 + lane;
+      float TA = 0.0f, dA = 0.0f, TB = 0.0f, dB = 0.0f;
+      int bA = 0, bB = 0;
+      for (int q = 0; q < nsg; q++) {
+        const int4 v = sg[q];
+        if (v.x >= i1) break;          // starts after the slice
+        if (v.x + v.y < i0) continue;  // ends before it
+        if (iA >= v.x) {
+          TA = __int_as_float(v.z);
+          dA = __int_as_float(v.w);
+          bA = v.x;
+        }
+        if (iB >= v.x) {
+          TB = __int_as_float(v.z);
+          dB = __int_as_float(v.w);
+          bB = v.x;
+        }
+      }
+      if (lane < rows) cA = (int)fmaf((float)(iA - bA), dA, TA);
+      if (lane + 64 < rows) cB = (int)fmaf((float)(iB - bB), dB, TB);
+    }
     const int32_t upA = __shfl_up(cA, 1, 64), upB = __shfl_up(cB, 1, 64);
     const int32_t lastA = __builtin_amdgcn_readlane(cA, 63);
     const bool stA = lane < rows && (lane == 0 || upA != cA);
@@ -418,9 +437,9 @@ __global__ void __launch_bounds__(kBandThreads, 4)
       rs = re;
       x = nx;
     }
-    int32_t* P = R.part + ((int64_t)t * ns + sl) * kDepth;
-    P[lane] = acc0;
-    P[lane + 64] = acc1;
+    uint16_t* P = R.part + ((int64_t)t * ns + sl) * kDepth;
+    P[lane] = (uint16_t)acc0;
+    P[lane + 64] = (uint16_t)acc1;
   }
 }
 
@@ -458,9 +477,10 @@ __global__ void __launch_bounds__(256) k_rot_final(RotGeom g, const RotTable* ta
   const int ns = rot_slices(max_scan), nsl = (LS.scan + kSliceRows - 1) / kSliceRows;
   int B[2] = {0, 0};
   for (int q = 0; q < nsl; q++) {
-    const int32_t* P = R.part + ((int64_t)t * ns + q) * kDepth;
-    B[0] += P[2 * lane];
-    B[1] += P[2 * lane + 1];
+    // steps 2 lane (low half) and 2 lane + 1 (high half) of slice q
+    const uint32_t v = reinterpret_cast<const uint32_t*>(R.part + ((int64_t)t * ns + q) * kDepth)[lane];
+    B[0] += (int)(v & 0xFFFFu);
+    B[1] += (int)(v >> 16);
   }
   // steps 2*lane, 2*lane+1 (deskew.c:114-146)
   const int maxAbs = (int)(255 * g.scan_size * g.scan_depth);
@@ -553,10 +573,12 @@ __device__ void walk_line(PlaneRef img, const RotGeom& g, const RotTable* table,
   // a left/right line continues from the band's state after kDepth steps,
   // with the point lists k_rot_points built; others start from scratch
   const bool resume = R.state[4 * t + 3] != 0;
-  if (syv == 0) {
+  const int nsg = syv == 0 ? R.nseg[t] : 0;
+  if (nsg > 0) {
     const int32_t ystart = (int32_t)LS.Y;  // rows: Ystart + i exactly
+    const int4* sg = R.segs + (int64_t)t * kLineSegs;
     for (int i = threadIdx.x; i < scan; i += blockDim.x) {
-      px[i] = R.cols[(int64_t)t * max_scan + i];
+      px[i] = seg_col(sg, nsg, i);
       py[i] = ystart + i;
     }
   } else if (threadIdx.x == 0) {
@@ -664,8 +686,8 @@ void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable
   const int nlines = count * g.nedges * nangles;
   const RotScratch R = rot_scratch(lines, nlines, max_scan);
   if (hipMemsetAsync(R.nlist, 0, sizeof(int32_t), st) != hipSuccess) return;  // the launches below report
-  UPH_LAUNCH_DIAG(16, k_rot_points, dim3((nlines + 3) / 4), dim3(256), 0, st, g, table, masks,
-                  mask_active, count, max_scan, R);
+  UPH_LAUNCH_DIAG(16, k_rot_points, dim3((nlines + 255) / 256), dim3(256), 0, st, g, table, masks,
+                  mask_active, count, R);
   switch (img.P.fmt) {
     case F_GRAY8:
       launch_rot_t<F_GRAY8>(img, g, table, masks, mask_active, mask_index, peaks, count, st,

@@ -20,6 +20,68 @@ static bool ready(const UphipImage& im, const char* op) {
 
 static PlaneRef ref1(const UphipFrame* f) { return fixed_ref(frame_planes(f), 0); }
 
+// The peaks of every enabled edge (left, top, right, bottom) x angle
+// (detect_edge_rotation_peak, deskew.c:48-146, for each angle of
+// detect_edge_rotation's loop, deskew.c:153-174) into hp[edge * na + angle].
+static bool rotation_peaks(const UphipImage& image, UphipRectangle mask,
+                           const UphipDeskewParameters& params, RotTable& table, bool (&on)[4],
+                           std::vector<int32_t>& hp) {
+  if (rotation_angles(params, &table) < 0)
+    return fail("detect_rotation: more than %d angles", kMaxAngles);
+  const int na = table.nangles;
+  RotGeom g;
+  g.W = image.frame->width;
+  g.H = image.frame->height;
+  g.nedges = 0;
+  const UphipEdges& E = params.scan_edges;
+  const int shifts[4][2] = {{1, 0}, {0, 1}, {-1, 0}, {0, -1}};  // left, top, right, bottom
+  on[0] = E.left;
+  on[1] = E.top;
+  on[2] = E.right;
+  on[3] = E.bottom;
+  for (int k = 0; k < 4; k++)
+    if (on[k]) {
+      g.edge_shift[g.nedges][0] = shifts[k][0];
+      g.edge_shift[g.nedges][1] = shifts[k][1];
+      g.nedges++;
+    }
+  g.scan_size = params.deskewScanSize;
+  g.scan_depth = params.deskewScanDepth;
+  g.max_masks = 1;
+  hipStream_t st = current_stream();
+  RotTable* dt = (RotTable*)scratch(4, sizeof(RotTable));
+  Rect* dm = (Rect*)scratch(5, sizeof(Rect));
+  int32_t* peaks = (int32_t*)scratch(6, sizeof(int32_t) * 4 * (size_t)(na > 0 ? na : 1));
+  if (!dt || !dm || !peaks) return false;
+  Rect m = to_rect(mask);
+  UPH_HIP(hipMemcpyAsync(dt, &table, sizeof(RotTable), hipMemcpyHostToDevice, st));
+  UPH_HIP(hipMemcpyAsync(dm, &m, sizeof(Rect), hipMemcpyHostToDevice, st));
+  const int32_t mw = iabs(m.x0 - m.x1) + 1, mh = iabs(m.y0 - m.y1) + 1;
+  int max_scan = params.deskewScanSize == -1 ? imax(mw, mh) : params.deskewScanSize;
+  max_scan = imin(imin(max_scan, 10000), imax(mw, mh));
+  int32_t* lines = (int32_t*)scratch(7, rotation_lines_bytes(1, g.nedges, na, max_scan));
+  if (!lines) return false;
+  float max_angle = 0.0f;
+  for (int i = 0; i < na; i++) max_angle = fmaxf(max_angle, fabsf(table.angle[i]));
+  launch_rotation_peaks(ref1(image.frame), g, dt, dm, nullptr, 0, peaks, 1, st, na, max_scan,
+                        lines, max_angle);
+  hp.assign(4 * (size_t)(na > 0 ? na : 1), 0);
+  UPH_HIP(hipMemcpyAsync(hp.data(), peaks, sizeof(int32_t) * g.nedges * na,
+                         hipMemcpyDeviceToHost, st));
+#ifdef UPHIP_DIAG
+  if (getenv("UPHIP_DIAG_ROTATION")) {  // tuning build only: lines left to the direct walk
+    std::vector<int32_t> fl((size_t)g.nedges * na);
+    UPH_HIP(hipMemcpyAsync(fl.data(), rotation_line_flags(lines, g.nedges * na, max_scan),
+                           sizeof(int32_t) * fl.size(), hipMemcpyDeviceToHost, st));
+    UPH_HIP(hipStreamSynchronize(st));
+    int nf = 0;
+    for (int32_t f : fl) nf += f != 0;
+    fprintf(stderr, "uphip: detect_rotation %d of %d lines walked directly\n", nf, (int)fl.size());
+  }
+#endif
+  return UPH_HIP(hipStreamSynchronize(st));
+}
+
 extern "C" {
 
 void uphip_grayfilter(UphipImage image0, UphipGrayfilterParameters params) {
@@ -123,61 +185,11 @@ float uphip_detect_rotation(UphipImage image0, UphipRectangle mask,
   if (!ready(image0, "detect_rotation")) return 0.0f;
   MonoProxy mp(image0, false, "detect_rotation");  // 1-bit frames: GRAY8 proxy (mono_proxy.h)
   if (!mp.ok()) return 0.0f;
-  const UphipImage image = mp.image();
   static thread_local RotTable table;
-  if (rotation_angles(params, &table) < 0) {
-    fail("detect_rotation: more than %d angles", kMaxAngles);
-    return 0.0f;
-  }
+  bool on[4];
+  std::vector<int32_t> hp;
+  if (!rotation_peaks(mp.image(), mask, params, table, on, hp)) return 0.0f;
   const int na = table.nangles;
-  RotGeom g;
-  g.W = image.frame->width;
-  g.H = image.frame->height;
-  g.nedges = 0;
-  const UphipEdges& E = params.scan_edges;
-  const int shifts[4][2] = {{1, 0}, {0, 1}, {-1, 0}, {0, -1}};  // left, top, right, bottom
-  const bool on[4] = {E.left, E.top, E.right, E.bottom};
-  for (int k = 0; k < 4; k++)
-    if (on[k]) {
-      g.edge_shift[g.nedges][0] = shifts[k][0];
-      g.edge_shift[g.nedges][1] = shifts[k][1];
-      g.nedges++;
-    }
-  g.scan_size = params.deskewScanSize;
-  g.scan_depth = params.deskewScanDepth;
-  g.max_masks = 1;
-  hipStream_t st = current_stream();
-  RotTable* dt = (RotTable*)scratch(4, sizeof(RotTable));
-  Rect* dm = (Rect*)scratch(5, sizeof(Rect));
-  int32_t* peaks = (int32_t*)scratch(6, sizeof(int32_t) * 4 * (size_t)(na > 0 ? na : 1));
-  if (!dt || !dm || !peaks) return 0.0f;
-  Rect m = to_rect(mask);
-  UPH_HIP(hipMemcpyAsync(dt, &table, sizeof(RotTable), hipMemcpyHostToDevice, st));
-  UPH_HIP(hipMemcpyAsync(dm, &m, sizeof(Rect), hipMemcpyHostToDevice, st));
-  const int32_t mw = iabs(m.x0 - m.x1) + 1, mh = iabs(m.y0 - m.y1) + 1;
-  int max_scan = params.deskewScanSize == -1 ? imax(mw, mh) : params.deskewScanSize;
-  max_scan = imin(imin(max_scan, 10000), imax(mw, mh));
-  int32_t* lines = (int32_t*)scratch(7, rotation_lines_bytes(1, g.nedges, na, max_scan));
-  if (!lines) return 0.0f;
-  float max_angle = 0.0f;
-  for (int i = 0; i < na; i++) max_angle = fmaxf(max_angle, fabsf(table.angle[i]));
-  launch_rotation_peaks(ref1(image.frame), g, dt, dm, nullptr, 0, peaks, 1, st, na, max_scan,
-                        lines, max_angle);
-  std::vector<int32_t> hp(4 * (size_t)(na > 0 ? na : 1));
-  UPH_HIP(hipMemcpyAsync(hp.data(), peaks, sizeof(int32_t) * g.nedges * na,
-                         hipMemcpyDeviceToHost, st));
-#ifdef UPHIP_DIAG
-  if (getenv("UPHIP_DIAG_ROTATION")) {  // tuning build only: lines left to the direct walk
-    std::vector<int32_t> fl((size_t)g.nedges * na);
-    UPH_HIP(hipMemcpyAsync(fl.data(), rotation_line_flags(lines, g.nedges * na, max_scan),
-                           sizeof(int32_t) * fl.size(), hipMemcpyDeviceToHost, st));
-    UPH_HIP(hipStreamSynchronize(st));
-    int nf = 0;
-    for (int32_t f : fl) nf += f != 0;
-    fprintf(stderr, "uphip: detect_rotation %d of %d lines walked directly\n", nf, (int)fl.size());
-  }
-#endif
-  if (!UPH_HIP(hipStreamSynchronize(st))) return 0.0f;
   float rot[4];
   int count = 0, e = 0;
   for (int k = 0; k < 4; k++) {
@@ -196,6 +208,24 @@ float uphip_detect_rotation(UphipImage image0, UphipRectangle mask,
     e++;
   }
   return combine_edge_rotations(rot, count, params.deskewScanDeviationRad);
+}
+
+int32_t uphip_detect_rotation_peaks(UphipImage image0, UphipRectangle mask,
+                                    const UphipDeskewParameters params, int32_t* peaks,
+                                    int32_t capacity) {
+  // the per-line peaks behind uphip_detect_rotation (deskew.c:48-146)
+  if (!peaks || capacity < 0) return fail("detect_rotation_peaks: bad arguments"), -1;
+  if (!ready(image0, "detect_rotation_peaks")) return -1;
+  MonoProxy mp(image0, false, "detect_rotation_peaks");
+  if (!mp.ok()) return -1;
+  static thread_local RotTable table;
+  bool on[4];
+  std::vector<int32_t> hp;
+  if (!rotation_peaks(mp.image(), mask, params, table, on, hp)) return -1;
+  const int n = (on[0] + on[1] + on[2] + on[3]) * table.nangles;
+  if (n > capacity) return fail("detect_rotation_peaks: %d peaks, capacity %d", n, capacity), -1;
+  for (int i = 0; i < n; i++) peaks[i] = hp[(size_t)i];
+  return n;
 }
 
 }  // extern "C"

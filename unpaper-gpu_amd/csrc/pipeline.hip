@@ -1029,9 +1029,25 @@ static bool border_rows_from_center(const UphipBatch* b) {
   return true;
 }
 
+// The centring move, the border scan and the masked align move chained
+// (launch_move_chain): the centring only counts (a dry pass, C is never
+// written) and the align move gathers straight from the uncentred plane.
+// Needs border_rows_from_center, one page (one centring move), the align move
+// on, and 32-bit plane offsets.
+#ifndef UPH_CHAIN_MOVES
+#define UPH_CHAIN_MOVES 1  // 0: the two moves as separate passes (A/B builds)
+#endif
+static bool chain_center_align(const UphipBatch* b) {
+  if (!UPH_CHAIN_MOVES || !border_rows_from_center(b) || b->points.size() != 1) return false;
+  if (b->o.disable & UPHIP_NO_BORDER_ALIGN) return false;
+  return b->pitch * (int64_t)b->H < (1ll << 31) && UPHIP_MAX_PAGES >= 2;
+}
+
 // rows_ready: the vertical scan's row sums are already in b->sums
-// (border_rows_from_center)
-static void border_all(UphipBatch* b, int count, bool rows_ready) {
+// (border_rows_from_center).  center: the chained centring move's arguments
+// (chain_center_align), whose plane was never written.
+static void border_all(UphipBatch* b, int count, bool rows_ready,
+                       const MoveArgs* center = nullptr) {
   const UphipBorderScanParameters& p = b->o.border_scan_parameters;
   const int nout = (int)b->outside.size();
   const int32_t W = b->W, H = b->H;
@@ -1099,6 +1115,13 @@ static void border_all(UphipBatch* b, int count, bool rows_ready) {
   // identity)
   const bool align = !(b->o.disable & UPHIP_NO_BORDER_ALIGN);
   const bool fold = align && nout == 1 && P.fmt == F_GRAY8;
+  if (center) {
+    // every sheet's output written to the other plane: flip them all
+    launch_move_chain(cur_ref(P, b->ctl), other_ref(P, b->ctl), center, b->border_mask_args,
+                      b->move_args, count, b->st);
+    flip_all(b, count);
+    return;
+  }
   if (!fold)
     launch_apply_masks_thr(cur_ref(P, b->ctl), b->border_mask_args, count,
                            b->o.abs_black_threshold, b->st);
@@ -1376,13 +1399,15 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
   }
   // ---- post (sheet_stages.c:415-534) -------------------------------------
   const bool rows_fused = border_rows_from_center(b);
+  const bool chain = chain_center_align(b);
+  MoveArgs* const center_mv = chain ? b->move_args + b->cap : nullptr;  // align uses [0, cap)
   if (!(dis & UPHIP_NO_MASK_CENTER)) {
     if (!(dis & UPHIP_NO_MASK_SCAN)) {
       detect_masks_all(b, 1, count, center_sums_ready);
       mark(b, "masks_center");
     }
     for (size_t i = 0; i < b->points.size(); i++) {
-      MoveArgs* mv = b->move_args;  // reuse the first cap entries
+      MoveArgs* mv = chain ? center_mv : b->move_args;  // reuse the first cap entries
       hipLaunchKernelGGL(k_center_args, dim3((count + 255) / 256), dim3(256), 0, b->st, b->ctl,
                          (int)i, b->W, b->H, o.sheet_background, mv, count);
       if (rows_fused && i + 1 == b->points.size()) {
@@ -1394,11 +1419,12 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
         x.rx0 = oc.x0;
         x.rx1 = oc.x1;
         x.thr = o.abs_black_threshold;
+        x.dry = chain;  // chained: count C's rows from R, write nothing
         launch_move_rect_fused(cur_ref(P, b->ctl), other_ref(P, b->ctl), mv, x, count, b->st);
       } else {
         launch_move_rect(cur_ref(P, b->ctl), other_ref(P, b->ctl), mv, count, b->st);
       }
-      launch_flip_if_active(b->ctl, &mv->active, sizeof(MoveArgs), count, b->st);
+      if (!chain) launch_flip_if_active(b->ctl, &mv->active, sizeof(MoveArgs), count, b->st);
     }
     mark(b, "center");
   }
@@ -1413,7 +1439,7 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
   }
   if (!(dis & UPHIP_NO_BORDER)) border_uniform(b, P, o.border, count);
   if (!(dis & UPHIP_NO_BORDER_SCAN) && !b->outside.empty()) {
-    border_all(b, count, rows_fused);
+    border_all(b, count, rows_fused, center_mv);
     mark(b, "border");
   }
   if (!(dis & UPHIP_NO_WIPE)) wipes_uniform(b, P, o.post_wipes, count);

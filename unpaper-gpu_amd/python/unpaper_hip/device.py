@@ -53,6 +53,7 @@ EXPORTED = [
     "uphip_runner_output_info", "uphip_runner_batch", "uphip_runner_layout", "uphip_batch_device_bytes", "uphip_host_alloc", "uphip_host_free",
     "uphip_check_libm", "uphip_jpeg_probe", "uphip_jpeg_read", "uphip_jpeg_decode",
     "uphip_jpeg_entropy_decode", "uphip_runner_placement", "uphip_runner_slot_chunk",
+    "uphip_detect_rotation_peaks",
 ]
 
 
@@ -106,6 +107,8 @@ def load_library(path=LIB_PATH):
         "uphip_noisefilter": (None, [Image, C.c_uint64, C.c_uint8]),
         "uphip_grayfilter": (None, [Image, A.GrayfilterParameters]),
         "uphip_detect_rotation": (C.c_float, [Image, A.Rectangle, A.DeskewParameters]),
+        "uphip_detect_rotation_peaks": (C.c_int32, [Image, A.Rectangle, A.DeskewParameters,
+                                                    C.c_void_p, C.c_int32]),
         "uphip_deskew": (None, [Image, A.Rectangle, C.c_float, C.c_int]),
         "uphip_try_init": (C.c_int, []),
         "uphip_init_status_string": (C.c_char_p, [C.c_int]),
@@ -356,6 +359,15 @@ class Backend:
 
     def grayfilter(self, d, params):
         self.lib.uphip_grayfilter(d.img, params); self._done()
+
+    def detect_rotation_peaks(self, d, mask, params):
+        """Per (edge, angle) peaks (uphip_detect_rotation_peaks) as an int32 array."""
+        out = np.zeros(4 * 1024, np.int32)
+        n = self.lib.uphip_detect_rotation_peaks(d.img, mask, params, out.ctypes.data, out.size)
+        self._done()
+        if n < 0:
+            raise UnpaperHipError("detect_rotation_peaks failed")
+        return out[:n].copy()
 
     def detect_rotation(self, d, mask, params):
         r = self.lib.uphip_detect_rotation(d.img, mask, params); self._done()
