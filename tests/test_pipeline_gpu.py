@@ -531,3 +531,33 @@ def test_rotate_window_classes_batch(hip, oracle):
             large += need > 59
             small += need <= 59
     assert large >= 20 and small >= 20, (large, small)
+
+
+def _blank_band(w, h, page, top, bottom):
+    """Synthetic page `page` with rows [0, top) and [h - bottom, h) made white:
+    the border scan from that edge finds its first dark band only past them."""
+    g = synth_page_host(w, h, page).copy()
+    g[:top] = 255
+    if bottom:
+        g[-bottom:] = 255
+    return HostImage.from_array(g, A.FMT_GRAY8, abs_black_threshold=170)
+
+
+@pytest.mark.parametrize("margins", [(0, 0), (400, 0), (0, 450), (420, 430), (700, 10)])
+@pytest.mark.parametrize("align", ["center", "top", "bottom_right"])
+def test_chained_center_border_align(hip, oracle, margins, align):
+    """The centring move, the border scan and the masked align move chained
+    (pipeline.hip chain_center_align, kernels_blit.hip k_move_chain_g16):
+    the scan first counts only the rows within 320 of each edge; pages whose
+    margin is wider (the top, the bottom or both blanked past 320 rows) make
+    it count the middle rows and scan again.  Whole sheets against the
+    oracle, which centres, scans and aligns in three steps."""
+    opts = oracle.default_options()
+    if align == "top":
+        opts.mask_alignment_parameters.alignment = A.Edges(False, True, False, False)
+    elif align == "bottom_right":
+        opts.mask_alignment_parameters.alignment = A.Edges(False, False, True, True)
+        opts.mask_alignment_parameters.margin = A.Delta(7, 11)
+    w, h = 1240, 1754  # A4 at 150 dpi: > 2 x 320 + 64 rows
+    sheets = [[_blank_band(w, h, p, *margins)] for p in (2, 7)]
+    check(oracle, opts, sheets, "margins %r align %s" % (margins, align))

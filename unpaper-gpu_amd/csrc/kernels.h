@@ -81,7 +81,9 @@ void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* 
 //    the sheet's resulting plane (moved, or the current one when the move is
 //    the identity) at rows[s * rows_stride + y] -- detect_border's row sums
 //    (masks.c:410-449), no other pass over the plane.
-//  * dry: count only (rows), write nothing (not with masks).
+//  * dry: count only (rows), write nothing (not with masks); a dry pass may
+//    cover only the rows [ya0, ya1) and [yb0, yb1) (empty ranges: all rows),
+//    and only the sheets s with only[s] != 0 (only == nullptr: all).
 struct MoveExtra {
   const MaskArgs* masks;
   uint32_t* rows;
@@ -89,6 +91,8 @@ struct MoveExtra {
   int32_t rx0, rx1;
   uint8_t thr;
   bool dry;
+  int32_t ya0, ya1, yb0, yb1;
+  const int32_t* only;
 };
 // center_mask (center[s]) then apply_masks (masks[s], one mask) and
 // align_mask (align[s]) as one pass from src into dst (every byte of every

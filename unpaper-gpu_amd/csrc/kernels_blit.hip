@@ -628,6 +628,7 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
   constexpr bool kDry = (MODE & 4) != 0;  // count only: nothing is written
   static_assert(!(kDry && kMask), "a dry pass counts; it does not mask");
   const int s = blockIdx.z;
+  if (X.only && !X.only[s]) return;
   const MoveArgs a = args[s];
   if (!kMask && !kRows && !a.active) return;
   const Planes& P = src.P;
@@ -635,9 +636,17 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
   uint8_t* dbase = plane_ptr(dst, s);
   const int lane = threadIdx.x & 63;
   const int32_t nv = (P.W + 15) >> 4;                  // vectors per row (inside the pitch)
-  const int32_t yb = blockIdx.x * kMoveBlockRows;       // the block's first row
+  // the block's rows: blocks cover the row ranges [ya0, ya1) then [yb0, yb1)
+  // (all rows by default), kMoveBlockRows each
+  const bool ranged = X.ya1 > X.ya0 || X.yb1 > X.yb0;
+  const int32_t ra0 = ranged ? X.ya0 : 0, ra1 = ranged ? X.ya1 : P.H;
+  const int32_t nba = ra1 > ra0 ? (ra1 - ra0 + kMoveBlockRows - 1) / kMoveBlockRows : 0;
+  const bool second = (int32_t)blockIdx.x >= nba;
+  const int32_t yb = second ? X.yb0 + ((int32_t)blockIdx.x - nba) * kMoveBlockRows
+                            : ra0 + (int32_t)blockIdx.x * kMoveBlockRows;  // the block's first row
+  const int32_t yend = imin(second ? X.yb1 : ra1, P.H);  // first row past the block's range
   const int32_t y0 = yb + (threadIdx.x >> 6) * kMoveRows;
-  const int32_t y1 = imin(y0 + kMoveRows, P.H);
+  const int32_t y1 = imin(y0 + kMoveRows, yend);
   // folded apply_masks (one mask, masks.c:306-322 semantics: normalized,
   // pixels outside it <- colour)
   Rect mk{INT_MIN / 2, INT_MIN / 2, INT_MAX / 2, INT_MAX / 2};
@@ -667,7 +676,7 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
     }
     __syncthreads();
     const int32_t y = yb + (int32_t)threadIdx.x;
-    if (threadIdx.x < kMoveBlockRows && y < P.H) X.rows[(int64_t)s * X.rows_stride + y] = rowcnt[threadIdx.x];
+    if (threadIdx.x < kMoveBlockRows && y < yend) X.rows[(int64_t)s * X.rows_stride + y] = rowcnt[threadIdx.x];
   };
   if (!a.active) {
     // the identity move: mask the current plane in place and/or count it
@@ -823,7 +832,7 @@ __global__ void __launch_bounds__(kThreads) k_move_rect_g16(PlaneRef src, PlaneR
   // and wave.
   const int tid = threadIdx.x;
   const int32_t yr = yb + (nd ? tid / nd : 0);
-  if (tid < nd * kMoveBlockRows && yr < P.H) {
+  if (tid < nd * kMoveBlockRows && yr < yend) {
     const int di = tid - (tid / nd) * nd;
     int32_t vi = dvs[0];
 #pragma unroll
@@ -899,7 +908,13 @@ void launch_move_rect(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* 
 bool launch_move_rect_fused(const PlaneRef& src, const PlaneRef& dst, const MoveArgs* args,
                             const MoveExtra& x, int count, hipStream_t st) {
   if (src.P.fmt != F_GRAY8) return false;
-  const int64_t blocks = (src.P.H + kMoveBlockRows - 1) / kMoveBlockRows;
+  int64_t blocks = (src.P.H + kMoveBlockRows - 1) / kMoveBlockRows;
+  if (x.ya1 > x.ya0 || x.yb1 > x.yb0) {  // row ranges (see k_move_rect_g16)
+    if (!x.dry) return false;             // only a counting pass may skip rows
+    blocks = (x.ya1 > x.ya0 ? (x.ya1 - x.ya0 + kMoveBlockRows - 1) / kMoveBlockRows : 0) +
+             (x.yb1 > x.yb0 ? (x.yb1 - x.yb0 + kMoveBlockRows - 1) / kMoveBlockRows : 0);
+    if (blocks == 0) return true;
+  }
   const dim3 grid((unsigned)(blocks < 1 ? 1 : blocks), 1, count);
   const int mode = (x.masks ? 1 : 0) | (x.rows ? 2 : 0) | (x.dry ? 4 : 0);
   if (x.dry && x.masks) return false;
@@ -1061,39 +1076,55 @@ __global__ void __launch_bounds__(kThreads) k_move_chain_g16(PlaneRef src, Plane
   const int32_t nv = (W + 15) >> 4;
   const int r0 = (threadIdx.x >> 6) * kMoveRows;  // the wave's rows of the block
   // uniform vectors: lanes along the row, the wave's kMoveRows rows
+  constexpr int kG = 4;  // rows whose loads are in flight together
   for (int32_t vi = lane; vi < nv; vi += 64) {
     const int32_t x0 = 16 * vi;
     const int il = interval(x0);
     if (x0 + 16 > W || il != interval(x0 + 15)) continue;  // byte path below
-    for (int k = 0; k < kMoveRows; k++) {
-      const int r = r0 + k;
-      if (r >= nrows) break;
-      const int32_t y = yb + r;
-      const int2 ce = cell[r][il];
-      uint4 out;
-      if (ce.x >= 0) {
-        const uint32_t v4 = (uint32_t)ce.x * 0x01010101u;
-        out = make_uint4(v4, v4, v4, v4);
-      } else {
-        // R bytes x0 + off .. + 15 of this row's offset: two aligned vectors
-        // realigned by (off mod 16), the same for every vector of the interval
-        const uint8_t* p = sbase + (int64_t)y * pitch + x0 + ce.y;
-        const int r16 = (int)((uintptr_t)p & 15u);
-        const uint4* q = reinterpret_cast<const uint4*>(p - r16);
-        const uint4 lo = q[0];
-        const uint4 hi = r16 ? q[1] : lo;
-        const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        const int qd = r16 >> 2, rb = r16 & 3;
-        uint32_t d[5];
 #pragma unroll
-        for (int j = 0; j < 5; j++)
-          d[j] = qd == 0 ? w[j] : qd == 1 ? w[j + 1] : qd == 2 ? w[j + 2] : w[j + 3];
-        out = make_uint4(__builtin_amdgcn_alignbyte(d[1], d[0], rb),
-                         __builtin_amdgcn_alignbyte(d[2], d[1], rb),
-                         __builtin_amdgcn_alignbyte(d[3], d[2], rb),
-                         __builtin_amdgcn_alignbyte(d[4], d[3], rb));
+    for (int k0 = 0; k0 < kMoveRows; k0 += kG) {
+      int2 ce[kG];
+      int r16[kG];
+      uint4 lo[kG], hi[kG];
+#pragma unroll
+      for (int j = 0; j < kG; j++) {
+        // R bytes x0 + off .. + 15 of the row's cell: two aligned vectors
+        // realigned by (off mod 16), the same for every vector of the interval
+        const int r = r0 + k0 + j;
+        ce[j] = r < nrows ? cell[r][il] : make_int2(0, 0);
+        r16[j] = 0;
+        lo[j] = hi[j] = make_uint4(0u, 0u, 0u, 0u);
+        if (r < nrows && ce[j].x < 0) {
+          const uint8_t* p = sbase + (int64_t)(yb + r) * pitch + x0 + ce[j].y;
+          r16[j] = (int)((uintptr_t)p & 15u);
+          const uint4* q = reinterpret_cast<const uint4*>(p - r16[j]);
+          lo[j] = q[0];
+          if (r16[j]) hi[j] = q[1];
+        }
       }
-      *reinterpret_cast<uint4*>(dbase + (int64_t)y * pitch + x0) = out;
+#pragma unroll
+      for (int j = 0; j < kG; j++) {
+        const int r = r0 + k0 + j;
+        if (r >= nrows) break;
+        uint4 out;
+        if (ce[j].x >= 0) {
+          const uint32_t v4 = (uint32_t)ce[j].x * 0x01010101u;
+          out = make_uint4(v4, v4, v4, v4);
+        } else {
+          const uint32_t w[8] = {lo[j].x, lo[j].y, lo[j].z, lo[j].w,
+                                 hi[j].x, hi[j].y, hi[j].z, hi[j].w};
+          const int qd = r16[j] >> 2, rb = r16[j] & 3;
+          uint32_t d[5];
+#pragma unroll
+          for (int m = 0; m < 5; m++)
+            d[m] = qd == 0 ? w[m] : qd == 1 ? w[m + 1] : qd == 2 ? w[m + 2] : w[m + 3];
+          out = make_uint4(__builtin_amdgcn_alignbyte(d[1], d[0], rb),
+                           __builtin_amdgcn_alignbyte(d[2], d[1], rb),
+                           __builtin_amdgcn_alignbyte(d[3], d[2], rb),
+                           __builtin_amdgcn_alignbyte(d[4], d[3], rb));
+        }
+        *reinterpret_cast<uint4*>(dbase + (int64_t)(yb + r) * pitch + x0) = out;
+      }
     }
   }
   // vectors holding a breakpoint, and the row's partial last vector: byte by

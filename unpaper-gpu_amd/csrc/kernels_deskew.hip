@@ -378,26 +378,21 @@ __global__ void __launch_bounds__(kBandThreads, 4)
     // overlap the slice); run starts by ballot
     int32_t cA = 0, cB = 0;
     {
-      const int4* sg = R.segs + (int64_t)t * kLineSegs;
+      // lane q holds segment q (all loads in flight at once); each lane then
+      // picks the last segment starting at or before its rows
       const int nsg = __builtin_amdgcn_readfirstlane(R.nseg[t]);
+      const int4 mine = lane < nsg ? R.segs[(int64_t)t * kLineSegs + lane] : make_int4(INT_MAX, 0, 0, 0);
       const int iA = i0 + lane, iB = i0 + 64 + lane;
-      float TA = 0.0f, dA = 0.0f, TB = 0.0f, dB = 0.0f;
-      int bA = 0, bB = 0;
-      for (int q = 0; q < nsg; q++) {
-        const int4 v = sg[q];
-        if (v.x >= i1) break;          // starts after the slice
-        if (v.x + v.y < i0) continue;  // ends before it
-        if (iA >= v.x) {
-          TA = __int_as_float(v.z);
-          dA = __int_as_float(v.w);
-          bA = v.x;
-        }
-        if (iB >= v.x) {
-          TB = __int_as_float(v.z);
-          dB = __int_as_float(v.w);
-          bB = v.x;
-        }
+      int qA = 0, qB = 0;
+      for (int q = 1; q < nsg; q++) {
+        const int s0 = __builtin_amdgcn_readlane(mine.x, q);
+        if (s0 >= i1) break;  // uniform: starts after the slice
+        qA = iA >= s0 ? q : qA;
+        qB = iB >= s0 ? q : qB;
       }
+      const int bA = __shfl(mine.x, qA, 64), bB = __shfl(mine.x, qB, 64);
+      const float TA = __int_as_float(__shfl(mine.z, qA, 64)), dA = __int_as_float(__shfl(mine.w, qA, 64));
+      const float TB = __int_as_float(__shfl(mine.z, qB, 64)), dB = __int_as_float(__shfl(mine.w, qB, 64));
       if (lane < rows) cA = (int)fmaf((float)(iA - bA), dA, TA);
       if (lane + 64 < rows) cB = (int)fmaf((float)(iB - bB), dB, TB);
     }
@@ -574,11 +569,13 @@ __device__ void walk_line(PlaneRef img, const RotGeom& g, const RotTable* table,
   // with the point lists k_rot_points built; others start from scratch
   const bool resume = R.state[4 * t + 3] != 0;
   const int nsg = syv == 0 ? R.nseg[t] : 0;
+  __shared__ int4 segs_s[kLineSegs];
   if (nsg > 0) {
+    if ((int)threadIdx.x < nsg) segs_s[threadIdx.x] = R.segs[(int64_t)t * kLineSegs + threadIdx.x];
+    __syncthreads();
     const int32_t ystart = (int32_t)LS.Y;  // rows: Ystart + i exactly
-    const int4* sg = R.segs + (int64_t)t * kLineSegs;
     for (int i = threadIdx.x; i < scan; i += blockDim.x) {
-      px[i] = seg_col(sg, nsg, i);
+      px[i] = seg_col(segs_s, nsg, i);
       py[i] = ystart + i;
     }
   } else if (threadIdx.x == 0) {

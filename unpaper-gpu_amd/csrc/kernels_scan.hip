@@ -378,11 +378,17 @@ void launch_edge_scan(const EdgeArgs* args, int jobs_per_sheet, const uint32_t* 
 // result = k*|step| for the first k with count >= threshold while
 // k*|step| < max_step, else 0.
 // ---------------------------------------------------------------------------
+// Counted rows may have a gap [gap0, gap1) (gap0 >= gap1: none): a band
+// reaching into it before any band hits marks the sheet in need[] (the caller
+// counts the gap and scans that sheet again); only (optional): the sheets to
+// scan.
 __global__ void __launch_bounds__(256) k_border_scan(const BorderEdgeArgs* args,
                                                      const uint32_t* sums, int64_t sums_stride,
-                                                     int32_t* results) {
+                                                     int32_t* results, int32_t gap0, int32_t gap1,
+                                                     int32_t* need, const int32_t* only) {
   const int s = blockIdx.y;
   const int job = blockIdx.x;
+  if (only && !only[s]) return;
   const int64_t slot = (int64_t)s * gridDim.x + job;
   const BorderEdgeArgs a = args[slot];
   if (!a.active) return;
@@ -405,27 +411,39 @@ __global__ void __launch_bounds__(256) k_border_scan(const BorderEdgeArgs* args,
     return;
   }
   const int32_t kmax = (a.max_step + ast - 1) / ast;  // k*|step| < max_step
+  // found: 2 k for the first hit, 2 k + 1 when band k reaches the gap first
   for (int32_t kb = 0; kb < kmax; kb += blockDim.x) {
     const int32_t k = kb + (int32_t)threadIdx.x;
     if (k < kmax) {
       const int32_t lo = a.lo + k * a.step, hi = a.hi + k * a.step;
-      uint32_t c = 0;
-      for (int32_t p = imax(lo, 0); p <= imin(hi, n - 1); p++) c += lds[p];
-      if (c >= (uint32_t)a.threshold) atomicMin(&found, k);
+      const int32_t p0 = imax(lo, 0), p1 = imin(hi, n - 1);
+      if (p0 <= p1 && p0 < gap1 && p1 >= gap0) {
+        atomicMin(&found, 2 * k + 1);
+      } else {
+        uint32_t c = 0;
+        for (int32_t p = p0; p <= p1; p++) c += lds[p];
+        if (c >= (uint32_t)a.threshold) atomicMin(&found, 2 * k);
+      }
     }
     __syncthreads();
     if (found != INT_MAX) break;
   }
-  if (threadIdx.x == 0) results[slot] = found == INT_MAX ? 0 : found * ast;
+  if (threadIdx.x == 0) {
+    const bool gap = found != INT_MAX && (found & 1);
+    if (gap) need[s] = 1;
+    results[slot] = found == INT_MAX || gap ? 0 : (found >> 1) * ast;
+  }
 }
 
 void launch_border_scan(const BorderEdgeArgs* args, int jobs_per_sheet, const uint32_t* sums,
                         int64_t sums_stride, int32_t* results, int count, hipStream_t st,
-                        int32_t max_extent) {
+                        int32_t max_extent, int32_t gap0, int32_t gap1, int32_t* need,
+                        const int32_t* only) {
   if (jobs_per_sheet <= 0 || count <= 0) return;
+  if (gap0 < gap1 && !need) return;  // a gap needs somewhere to report
   hipLaunchKernelGGL(k_border_scan, dim3(jobs_per_sheet, count), dim3(256),
                      axis_lds(max_extent, (const void*)k_border_scan), st, args, sums, sums_stride,
-                     results);
+                     results, gap0, gap1, need, only);
 }
 
 }  // namespace uph

@@ -453,6 +453,7 @@ struct UphipBatch {
   uint32_t* nbits = nullptr;           // GRAY8 noisefilter dark bit-plane (k_decode_gray)
   int64_t nbits_stride = 0;            // words per sheet
   MoveArgs* move_args = nullptr;      // cap * MAX_PAGES
+  int32_t* border_need = nullptr;     // cap: the chained border scan needs the middle rows
   MaskArgs* border_mask_args = nullptr;
   int32_t* edge_res = nullptr;        // cap * npoints * 4
   int32_t* border_res = nullptr;      // cap * nout * 4
@@ -768,6 +769,7 @@ static bool allocate(UphipBatch* b) {
   b->edge_res = dalloc<int32_t>(b, (size_t)cap * imax(np, 1) * 4);
   b->border_res = dalloc<int32_t>(b, (size_t)cap * imax(nout, 1) * 4);
   b->move_args = dalloc<MoveArgs>(b, (size_t)cap * UPHIP_MAX_PAGES);
+  b->border_need = dalloc<int32_t>(b, cap);
   b->border_mask_args = dalloc<MaskArgs>(b, cap);
   b->rot_args = dalloc<RotateArgs>(b, (size_t)cap * UPHIP_MAX_PAGES);
   b->rot_indep = dalloc<int32_t>(b, cap);
@@ -1043,6 +1045,25 @@ static bool chain_center_align(const UphipBatch* b) {
   return b->pitch * (int64_t)b->H < (1ll << 31) && UPHIP_MAX_PAGES >= 2;
 }
 
+// The chained border scan first counts only the rows within
+// kBorderEdgeRows of the top and bottom (the scan from each edge stops at the
+// first dark band, normally within the margin); sheets whose scan reaches
+// the middle rows get them counted and are scanned again.
+constexpr int32_t kBorderEdgeRows = 320;  // a multiple of the move's block rows
+static bool border_edge_rows_only(const UphipBatch* b) { return b->H > 2 * kBorderEdgeRows + 64; }
+// The centring move's counting pass (border_rows_from_center): C's dark
+// pixels per row over outside rect 0's columns into border_all's row sums.
+static MoveExtra center_count_args(const UphipBatch* b) {
+  const Rect oc = clip(b->outside[0], b->W, b->H);
+  MoveExtra x{};
+  x.rows = b->sums + imax(b->W, b->H);  // border_all's vertical offset, outside rect 0
+  x.rows_stride = b->sums_stride;
+  x.rx0 = oc.x0;
+  x.rx1 = oc.x1;
+  x.thr = b->o.abs_black_threshold;
+  return x;
+}
+
 // rows_ready: the vertical scan's row sums are already in b->sums
 // (border_rows_from_center).  center: the chained centring move's arguments
 // (chain_center_align), whose plane was never written.
@@ -1088,8 +1109,24 @@ static void border_all(UphipBatch* b, int count, bool rows_ready,
   BorderEdgeArgs* de =
       (BorderEdgeArgs*)upload_cached(b, all.data(), sizeof(BorderEdgeArgs) * all.size());
   UPH_HIP(hipMemsetAsync(b->border_res, 0, sizeof(int32_t) * count * nout * 4, b->st));
-  launch_border_scan(de, nout * 4, b->sums, b->sums_stride, b->border_res, count, b->st,
-                     imax(W, H));
+  if (center && border_edge_rows_only(b)) {
+    // rows [kBorderEdgeRows, H - kBorderEdgeRows) not counted yet: scan, count
+    // them for the sheets that reach them, scan those again
+    UPH_HIP(hipMemsetAsync(b->border_need, 0, sizeof(int32_t) * count, b->st));
+    launch_border_scan(de, nout * 4, b->sums, b->sums_stride, b->border_res, count, b->st,
+                       imax(W, H), kBorderEdgeRows, H - kBorderEdgeRows, b->border_need);
+    MoveExtra x = center_count_args(b);
+    x.dry = true;
+    x.ya0 = kBorderEdgeRows;
+    x.ya1 = H - kBorderEdgeRows;
+    x.only = b->border_need;
+    launch_move_rect_fused(cur_ref(P, b->ctl), other_ref(P, b->ctl), center, x, count, b->st);
+    launch_border_scan(de, nout * 4, b->sums, b->sums_stride, b->border_res, count, b->st,
+                       imax(W, H), 0, 0, nullptr, b->border_need);
+  } else {
+    launch_border_scan(de, nout * 4, b->sums, b->sums_stride, b->border_res, count, b->st,
+                       imax(W, H));
+  }
   BorderAssembleArgs ba;
   memset(&ba, 0, sizeof(ba));
   ba.W = W;
@@ -1412,14 +1449,14 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
                          (int)i, b->W, b->H, o.sheet_background, mv, count);
       if (rows_fused && i + 1 == b->points.size()) {
         // the last move also counts the border scan's dark pixels per row
-        const Rect oc = clip(b->outside[0], b->W, b->H);
-        MoveExtra x{};
-        x.rows = b->sums + imax(b->W, b->H);  // border_all's vertical offset, outside rect 0
-        x.rows_stride = b->sums_stride;
-        x.rx0 = oc.x0;
-        x.rx1 = oc.x1;
-        x.thr = o.abs_black_threshold;
+        MoveExtra x = center_count_args(b);
         x.dry = chain;  // chained: count C's rows from R, write nothing
+        if (chain && border_edge_rows_only(b)) {  // the rows near the edges first
+          x.ya0 = 0;
+          x.ya1 = kBorderEdgeRows;
+          x.yb0 = b->H - kBorderEdgeRows;
+          x.yb1 = b->H;
+        }
         launch_move_rect_fused(cur_ref(P, b->ctl), other_ref(P, b->ctl), mv, x, count, b->st);
       } else {
         launch_move_rect(cur_ref(P, b->ctl), other_ref(P, b->ctl), mv, count, b->st);

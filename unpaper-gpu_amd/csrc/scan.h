@@ -50,8 +50,12 @@ void launch_axis_reduce(const PlaneRef& ref, const AxisArgs* args, int axis, int
 void launch_edge_scan(const EdgeArgs* args, int jobs_per_sheet, const uint32_t* sums,
                       int64_t sums_stride, int32_t* results, int count, hipStream_t st,
                       int32_t max_extent);
+// Rows [gap0, gap1) of the sums not counted (gap0 >= gap1: none): a sheet
+// whose scan reaches them before a hit gets need[s] = 1 and result 0, to be
+// scanned again once they are.  only (optional): the sheets to scan.
 void launch_border_scan(const BorderEdgeArgs* args, int jobs_per_sheet, const uint32_t* sums,
                         int64_t sums_stride, int32_t* results, int count, hipStream_t st,
-                        int32_t max_extent);
+                        int32_t max_extent, int32_t gap0 = 0, int32_t gap1 = 0,
+                        int32_t* need = nullptr, const int32_t* only = nullptr);
 
 }  // namespace uph
