@@ -1012,7 +1012,8 @@ __global__ void __launch_bounds__(kThreads) k_move_chain_g16(PlaneRef src, Plane
   c.bg1 = gray_of(Px{c.m1.bg[0], c.m1.bg[1], c.m1.bg[2]});
   c.bg2 = gray_of(Px{c.m2.bg[0], c.m2.bg[1], c.m2.bg[2]});
   __shared__ int32_t bp[kChainBp];
-  __shared__ int32_t nbp_s;
+  __shared__ int32_t nbp_s, nd_s;
+  __shared__ int32_t dv[kChainBp + 1];  // vectors holding a breakpoint (+ the row's partial one)
   __shared__ int2 cell[kMoveBlockRows][kChainBp + 1];
   if (threadIdx.x == 0) {
     // the columns where some stage's class can change (first column of the
@@ -1058,6 +1059,14 @@ __global__ void __launch_bounds__(kThreads) k_move_chain_g16(PlaneRef src, Plane
     for (int i = 0; i < n; i++)
       if (m == 0 || b[i] != bp[m - 1]) bp[m++] = b[i];
     nbp_s = m;
+    int nd = 0;
+    for (int k = 0; k < m; k++) {
+      const int32_t v = bp[k] >> 4;
+      if ((bp[k] & 15) && (nd == 0 || dv[nd - 1] != v)) dv[nd++] = v;
+    }
+    if ((W & 15) && (nd == 0 || dv[nd - 1] != (W >> 4))) dv[nd++] = W >> 4;
+    nd_s = nd;
+    for (int k = m; k < kChainBp; k++) bp[k] = INT_MAX;  // the register copy's padding
   }
   __syncthreads();
   const int nbp = nbp_s;
@@ -1067,9 +1076,13 @@ __global__ void __launch_bounds__(kThreads) k_move_chain_g16(PlaneRef src, Plane
     cell[r][i] = chain_cell(c, W, H, pitch, i == 0 ? 0 : bp[i - 1], yb + r);
   }
   __syncthreads();
+  int32_t bpr[kChainBp];  // the breakpoints in registers (INT_MAX past nbp)
+#pragma unroll
+  for (int k = 0; k < kChainBp; k++) bpr[k] = bp[k];
   auto interval = [&](int32_t x) {
     int i = 0;
-    for (int k = 0; k < nbp; k++) i += bp[k] <= x;
+#pragma unroll
+    for (int k = 0; k < kChainBp; k++) i += bpr[k] <= x;
     return i;
   };
   const int lane = threadIdx.x & 63;
@@ -1113,42 +1126,77 @@ __global__ void __launch_bounds__(kThreads) k_move_chain_g16(PlaneRef src, Plane
         } else {
           const uint32_t w[8] = {lo[j].x, lo[j].y, lo[j].z, lo[j].w,
                                  hi[j].x, hi[j].y, hi[j].z, hi[j].w};
-          const int qd = r16[j] >> 2, rb = r16[j] & 3;
-          uint32_t d[5];
+          const int ru = __builtin_amdgcn_readfirstlane(r16[j]);
+          if (__builtin_amdgcn_ballot_w64(r16[j] != ru) == 0) {
+            // the wave's vectors share one realignment (one cell, usually):
+            // a uniform dword select, as k_move_rect_g16 does
+            const int rb = ru & 3;
+            switch (ru >> 2) {
+              case 0: out = shift_bytes16<0>(w, rb); break;
+              case 1: out = shift_bytes16<1>(w, rb); break;
+              case 2: out = shift_bytes16<2>(w, rb); break;
+              default: out = shift_bytes16<3>(w, rb); break;
+            }
+          } else {
+            const int qd = r16[j] >> 2, rb = r16[j] & 3;
+            uint32_t d[5];
 #pragma unroll
-          for (int m = 0; m < 5; m++)
-            d[m] = qd == 0 ? w[m] : qd == 1 ? w[m + 1] : qd == 2 ? w[m + 2] : w[m + 3];
-          out = make_uint4(__builtin_amdgcn_alignbyte(d[1], d[0], rb),
-                           __builtin_amdgcn_alignbyte(d[2], d[1], rb),
-                           __builtin_amdgcn_alignbyte(d[3], d[2], rb),
-                           __builtin_amdgcn_alignbyte(d[4], d[3], rb));
+            for (int m = 0; m < 5; m++)
+              d[m] = qd == 0 ? w[m] : qd == 1 ? w[m + 1] : qd == 2 ? w[m + 2] : w[m + 3];
+            out = make_uint4(__builtin_amdgcn_alignbyte(d[1], d[0], rb),
+                             __builtin_amdgcn_alignbyte(d[2], d[1], rb),
+                             __builtin_amdgcn_alignbyte(d[3], d[2], rb),
+                             __builtin_amdgcn_alignbyte(d[4], d[3], rb));
+          }
         }
         *reinterpret_cast<uint4*>(dbase + (int64_t)(yb + r) * pitch + x0) = out;
       }
     }
   }
-  // vectors holding a breakpoint, and the row's partial last vector: byte by
-  // byte, a lane per (row, vector); columns >= W are written as 0
-  int32_t dv[kChainBp + 1];
-  int nd = 0;
-  for (int k = 0; k < nbp; k++) {
-    const int32_t v = bp[k] >> 4;
-    if ((bp[k] & 15) && (nd == 0 || dv[nd - 1] != v)) dv[nd++] = v;
-  }
-  if ((W & 15) && (nd == 0 || dv[nd - 1] != (W >> 4))) dv[nd++] = W >> 4;
+  // vectors holding a breakpoint, and the row's partial last vector: a lane
+  // per (row, vector), interval by interval, byte by byte; columns >= W are
+  // written as 0
+  const int nd = nd_s;
   for (int t = threadIdx.x; t < nrows * nd; t += blockDim.x) {
     const int r = t / nd, x0 = 16 * dv[t - r * nd];
     const int32_t y = yb + r;
     const uint8_t* srow = sbase + (int64_t)y * pitch;
-    uint32_t o[4] = {0u, 0u, 0u, 0u};
-    for (int j = 0; j < 16; j++) {
-      const int32_t x = x0 + j;
-      if (x >= W) break;
-      const int2 ce = cell[r][interval(x)];
-      const uint32_t v = ce.x >= 0 ? (uint32_t)ce.x : srow[x + ce.y];
-      o[j >> 2] |= v << (8 * (j & 3));
+    uint64_t o0 = 0, o1 = 0;
+    const int il = interval(x0), ih = interval(imin(x0 + 15, W - 1));
+    if (ih - il <= 3) {
+      // the (at most three) breakpoints inside the vector; every byte's
+      // source is independent of the others, so all 16 loads are in flight
+      int32_t bk[3];
+#pragma unroll
+      for (int m = 0; m < 3; m++) bk[m] = il + m < ih ? bp[il + m] : INT_MAX;
+      uint32_t v[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int32_t x = x0 + j;
+        const int i = il + (bk[0] <= x) + (bk[1] <= x) + (bk[2] <= x);
+        const int2 ce = cell[r][i];
+        v[j] = x >= W ? 0u : ce.x >= 0 ? (uint32_t)ce.x : (uint32_t)srow[x + ce.y];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        o0 |= (uint64_t)v[j] << (8 * j);
+        o1 |= (uint64_t)v[8 + j] << (8 * j);
+      }
+    } else {
+      for (int i = il; i <= ih; i++) {
+        const int32_t s0 = imax(i == 0 ? 0 : bp[i - 1], x0);
+        const int32_t s1 = imin(imin(i < nbp ? bp[i] : W, W), x0 + 16);
+        const int2 ce = cell[r][i];
+        for (int32_t x = s0; x < s1; x++) {
+          const uint64_t v = ce.x >= 0 ? (uint64_t)ce.x : (uint64_t)srow[x + ce.y];
+          const int j = x - x0;
+          if (j < 8) o0 |= v << (8 * j);
+          else o1 |= v << (8 * (j - 8));
+        }
+      }
     }
-    *reinterpret_cast<uint4*>(dbase + (int64_t)y * pitch + x0) = make_uint4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<uint4*>(dbase + (int64_t)y * pitch + x0) =
+        make_uint4((uint32_t)o0, (uint32_t)(o0 >> 32), (uint32_t)o1, (uint32_t)(o1 >> 32));
   }
 }
 

@@ -383,18 +383,30 @@ __global__ void __launch_bounds__(kBandThreads, 4)
       const int nsg = __builtin_amdgcn_readfirstlane(R.nseg[t]);
       const int4 mine = lane < nsg ? R.segs[(int64_t)t * kLineSegs + lane] : make_int4(INT_MAX, 0, 0, 0);
       const int iA = i0 + lane, iB = i0 + 64 + lane;
-      int qA = 0, qB = 0;
-      for (int q = 1; q < nsg; q++) {
-        const int s0 = __builtin_amdgcn_readlane(mine.x, q);
-        if (s0 >= i1) break;  // uniform: starts after the slice
-        qA = iA >= s0 ? q : qA;
-        qB = iB >= s0 ? q : qB;
+      // the segment holding row i0 (uniform), and whether it holds the slice
+      int q0 = 0;
+      while (q0 + 1 < nsg && __builtin_amdgcn_readlane(mine.x, q0 + 1) <= i0) q0++;
+      const int nxt = q0 + 1 < nsg ? __builtin_amdgcn_readlane(mine.x, q0 + 1) : INT_MAX;
+      if (nxt >= i1) {  // one segment: its values are wave-uniform
+        const int b = __builtin_amdgcn_readlane(mine.x, q0);
+        const float T = __int_as_float(__builtin_amdgcn_readlane(mine.z, q0));
+        const float d = __int_as_float(__builtin_amdgcn_readlane(mine.w, q0));
+        if (lane < rows) cA = (int)fmaf((float)(iA - b), d, T);
+        if (lane + 64 < rows) cB = (int)fmaf((float)(iB - b), d, T);
+      } else {
+        int qA = q0, qB = q0;
+        for (int q = q0 + 1; q < nsg; q++) {
+          const int s0 = __builtin_amdgcn_readlane(mine.x, q);
+          if (s0 >= i1) break;  // uniform: starts after the slice
+          qA = iA >= s0 ? q : qA;
+          qB = iB >= s0 ? q : qB;
+        }
+        const int bA = __shfl(mine.x, qA, 64), bB = __shfl(mine.x, qB, 64);
+        const float TA = __int_as_float(__shfl(mine.z, qA, 64)), dA = __int_as_float(__shfl(mine.w, qA, 64));
+        const float TB = __int_as_float(__shfl(mine.z, qB, 64)), dB = __int_as_float(__shfl(mine.w, qB, 64));
+        if (lane < rows) cA = (int)fmaf((float)(iA - bA), dA, TA);
+        if (lane + 64 < rows) cB = (int)fmaf((float)(iB - bB), dB, TB);
       }
-      const int bA = __shfl(mine.x, qA, 64), bB = __shfl(mine.x, qB, 64);
-      const float TA = __int_as_float(__shfl(mine.z, qA, 64)), dA = __int_as_float(__shfl(mine.w, qA, 64));
-      const float TB = __int_as_float(__shfl(mine.z, qB, 64)), dB = __int_as_float(__shfl(mine.w, qB, 64));
-      if (lane < rows) cA = (int)fmaf((float)(iA - bA), dA, TA);
-      if (lane + 64 < rows) cB = (int)fmaf((float)(iB - bB), dB, TB);
     }
     const int32_t upA = __shfl_up(cA, 1, 64), upB = __shfl_up(cB, 1, 64);
     const int32_t lastA = __builtin_amdgcn_readlane(cA, 63);
@@ -471,6 +483,7 @@ __global__ void __launch_bounds__(256) k_rot_final(RotGeom g, const RotTable* ta
   }
   const int ns = rot_slices(max_scan), nsl = (LS.scan + kSliceRows - 1) / kSliceRows;
   int B[2] = {0, 0};
+#pragma unroll 4
   for (int q = 0; q < nsl; q++) {
     // steps 2 lane (low half) and 2 lane + 1 (high half) of slice q
     const uint32_t v = reinterpret_cast<const uint32_t*>(R.part + ((int64_t)t * ns + q) * kDepth)[lane];
