@@ -1014,6 +1014,7 @@ __global__ void __launch_bounds__(kThreads) k_move_chain_g16(PlaneRef src, Plane
   __shared__ int32_t bp[kChainBp];
   __shared__ int32_t nbp_s, nd_s;
   __shared__ int32_t dv[kChainBp + 1];  // vectors holding a breakpoint (+ the row's partial one)
+  __shared__ uint8_t live[kChainBp], imap[kChainBp + 1];
   __shared__ int2 cell[kMoveBlockRows][kChainBp + 1];
   if (threadIdx.x == 0) {
     // the columns where some stage's class can change (first column of the
@@ -1059,6 +1060,36 @@ __global__ void __launch_bounds__(kThreads) k_move_chain_g16(PlaneRef src, Plane
     for (int i = 0; i < n; i++)
       if (m == 0 || b[i] != bp[m - 1]) bp[m++] = b[i];
     nbp_s = m;
+  }
+  __syncthreads();
+  int nbp = nbp_s;
+  // every (row, interval) of the block: interval i starts at column 0 or bp[i-1]
+  for (int t = threadIdx.x; t < nrows * (nbp + 1); t += blockDim.x) {
+    const int r = t / (nbp + 1), i = t - r * (nbp + 1);
+    cell[r][i] = chain_cell(c, W, H, pitch, i == 0 ? 0 : bp[i - 1], yb + r);
+  }
+  __syncthreads();
+  // a breakpoint whose two intervals have the same source in every row of
+  // the block changes nothing here: dropped (fewer byte-path vectors)
+  if ((int)threadIdx.x < nbp) {
+    const int k = threadIdx.x;
+    bool same = true;
+    for (int r = 0; r < nrows; r++) {
+      const int2 a = cell[r][k], b = cell[r][k + 1];
+      same = same && a.x == b.x && a.y == b.y;
+    }
+    live[k] = !same;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int m = 0;
+    imap[0] = 0;
+    for (int k = 0; k < nbp; k++)
+      if (live[k]) {
+        bp[m++] = bp[k];  // in place: m <= k
+        imap[m] = (uint8_t)(k + 1);
+      }
+    nbp_s = m;
     int nd = 0;
     for (int k = 0; k < m; k++) {
       const int32_t v = bp[k] >> 4;
@@ -1069,13 +1100,7 @@ __global__ void __launch_bounds__(kThreads) k_move_chain_g16(PlaneRef src, Plane
     for (int k = m; k < kChainBp; k++) bp[k] = INT_MAX;  // the register copy's padding
   }
   __syncthreads();
-  const int nbp = nbp_s;
-  // every (row, interval) of the block: interval i starts at column 0 or bp[i-1]
-  for (int t = threadIdx.x; t < nrows * (nbp + 1); t += blockDim.x) {
-    const int r = t / (nbp + 1), i = t - r * (nbp + 1);
-    cell[r][i] = chain_cell(c, W, H, pitch, i == 0 ? 0 : bp[i - 1], yb + r);
-  }
-  __syncthreads();
+  nbp = nbp_s;
   int32_t bpr[kChainBp];  // the breakpoints in registers (INT_MAX past nbp)
 #pragma unroll
   for (int k = 0; k < kChainBp; k++) bpr[k] = bp[k];
@@ -1104,7 +1129,7 @@ __global__ void __launch_bounds__(kThreads) k_move_chain_g16(PlaneRef src, Plane
         // R bytes x0 + off .. + 15 of the row's cell: two aligned vectors
         // realigned by (off mod 16), the same for every vector of the interval
         const int r = r0 + k0 + j;
-        ce[j] = r < nrows ? cell[r][il] : make_int2(0, 0);
+        ce[j] = r < nrows ? cell[r][imap[il]] : make_int2(0, 0);
         r16[j] = 0;
         lo[j] = hi[j] = make_uint4(0u, 0u, 0u, 0u);
         if (r < nrows && ce[j].x < 0) {
@@ -1174,7 +1199,7 @@ __global__ void __launch_bounds__(kThreads) k_move_chain_g16(PlaneRef src, Plane
       for (int j = 0; j < 16; j++) {
         const int32_t x = x0 + j;
         const int i = il + (bk[0] <= x) + (bk[1] <= x) + (bk[2] <= x);
-        const int2 ce = cell[r][i];
+        const int2 ce = cell[r][imap[i]];
         v[j] = x >= W ? 0u : ce.x >= 0 ? (uint32_t)ce.x : (uint32_t)srow[x + ce.y];
       }
 #pragma unroll
@@ -1186,7 +1211,7 @@ __global__ void __launch_bounds__(kThreads) k_move_chain_g16(PlaneRef src, Plane
       for (int i = il; i <= ih; i++) {
         const int32_t s0 = imax(i == 0 ? 0 : bp[i - 1], x0);
         const int32_t s1 = imin(imin(i < nbp ? bp[i] : W, W), x0 + 16);
-        const int2 ce = cell[r][i];
+        const int2 ce = cell[r][imap[i]];
         for (int32_t x = s0; x < s1; x++) {
           const uint64_t v = ce.x >= 0 ? (uint64_t)ce.x : (uint64_t)srow[x + ce.y];
           const int j = x - x0;
@@ -1912,6 +1937,9 @@ __device__ __forceinline__ uint32_t row_off(int32_t y, int64_t pitch) {
 #ifndef UPH_ROT_FULL
 #define UPH_ROT_FULL 1  // the branch-free row loop for full tiles
 #endif
+#ifndef UPH_ROT_UNIFORM
+#define UPH_ROT_UNIFORM 0  // 1: skip wave rows of uniform 4x4 windows (A/B: see DESIGN §5)
+#endif
 #ifdef UPHIP_DIAG
 // tuning build: per-phase shader clocks of wave 0 of every in-mask tile
 // (UPHIP_DIAG_DOUBLE bit 65536), summed; [7] counts the tiles
@@ -2281,6 +2309,23 @@ __global__ void __launch_bounds__(kRFT, UPH_ROT_MINB) k_rotate_cubic_g8f(PlaneRe
       const uint32_t ta[4] = {pA, pA + 8 * kRFS, pB, pB + 8 * kRFS};
       f2 t[4][4];
       lds_taps16(ta, t);
+#if UPH_ROT_UNIFORM
+      // A/B variant: a wave row whose every pixel has a
+      // uniform 4x4 window (all taps equal: every difference is 0, so each
+      // cubic_scale returns its b) skips the arithmetic
+      lds_wait_pair<0>(t[3]);
+      bool uni = true;
+#pragma unroll
+      for (int pp = 0; pp < 4; pp++)
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          uni = uni && t[pp][j].x == t[pp & 2][0].x && t[pp][j].y == t[pp & 2][0].x;
+      if (__builtin_amdgcn_ballot_w64(!uni) == 0) {
+        oA = (uint32_t)t[0][0].x;
+        oB = (uint32_t)t[2][0].x;
+      } else
+#endif
+      {
       // rows (0,1) and (2,3) of A once its eight tap pairs are in, then of B
       const f2 FA = splat2(fxA), HA = splat2(0.5f * fxA);
       const f2 FB = splat2(fxB), HB = splat2(0.5f * fxB);
@@ -2298,6 +2343,7 @@ __global__ void __launch_bounds__(kRFT, UPH_ROT_MINB) k_rotate_cubic_g8f(PlaneRe
                           f2{c[0].y, c[2].y}, f2{c[1].x, c[3].x}, f2{c[1].y, c[3].y});
       oA = (uint32_t)o.x;  // integer-valued in [0, 255]
       oB = (uint32_t)o.y;
+      }
     }
 #ifdef UPHIP_DIAG
     if (UPH_DIAG_BITS(diag, 131072)) {  // tuning: +32 SALU a row (is the scalar unit a limit?)
