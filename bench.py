@@ -86,8 +86,8 @@ ROOFLINE_KERNEL = {"c3": "k_rotate_cubic_g8f",
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=("c3", "c4", "jpeg"),
                     help="c3: BASELINE configs[2] (the metric); c4: configs[3], RGB24 600dpi "
                          "double-page sheets, layout double, bilinear, border wipe; jpeg: the "
