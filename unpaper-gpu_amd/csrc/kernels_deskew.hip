@@ -106,6 +106,7 @@ struct RotScratch {
   int32_t *nseg, *ends;
   uint16_t* part;
   int32_t *flag, *state, *list, *nlist;
+  int32_t *blo, *bhi;  // per (sheet, edge): the least / greatest column of its lines' ends
 };
 
 __host__ __device__ static inline int rot_slices(int max_scan) { return (max_scan + kSliceRows - 1) / kSliceRows; }
@@ -123,6 +124,8 @@ __host__ __device__ static inline RotScratch rot_scratch(int32_t* base, int nlin
   r.state = r.flag + nlines;
   r.list = r.state + 4 * (int64_t)nlines;
   r.nlist = r.list + nlines;
+  r.blo = r.nlist + 1;           // indexed by sheet * nedges + edge (< nlines)
+  r.bhi = r.blo + nlines;
   return r;
 }
 
@@ -150,7 +153,8 @@ size_t rotation_lines_bytes(int count, int nedges, int nangles, int max_scan) {
   const int64_t ms = max_scan > 0 ? max_scan : 1;
   const int64_t ns = (ms + kSliceRows - 1) / kSliceRows;
   return sizeof(int32_t) * (size_t)(nlines * kLineSegs * 4 + nlines + 2 * nlines +
-                                    nlines * ns * (kDepth / 2) + nlines + 4 * nlines + nlines + 1);
+                                    nlines * ns * (kDepth / 2) + nlines + 4 * nlines + nlines + 1 +
+                                    2 * nlines);
 }
 
 // ---- k_rot_points: the points of every left/right line --------------------
@@ -171,6 +175,14 @@ __global__ void __launch_bounds__(256) k_rot_points(RotGeom g, const RotTable* t
   const int na = table->nangles;
   const int nlines = count * g.nedges * na;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  // the block's (sheet, edge) column ranges, reduced in LDS first (the lines
+  // of one pair are consecutive: <= 256 pairs a block)
+  __shared__ int32_t slo[256], shi[256];
+  const int se_base = (int)(blockIdx.x * blockDim.x) / na;
+  slo[threadIdx.x] = INT_MAX;
+  shi[threadIdx.x] = INT_MIN;
+  __syncthreads();
+  [&] {  // one line (returns leave the lambda; every thread reaches the barrier below)
   if (t >= nlines) return;
   const int a = t % na, e = (t / na) % g.nedges, s = t / (na * g.nedges);
   const bool act = !(mask_active && !mask_active[s]);
@@ -208,24 +220,30 @@ __global__ void __launch_bounds__(256) k_rot_points(RotGeom g, const RotTable* t
         break;
       }
       const double lo = ldexp(1.0, E - 1), hi = ldexp(1.0, E), u = ldexp(1.0, E - 24);
-      const double q = sig / u;  // exact: u is a power of two
+      // divisions by u are exact scalings (u is a power of two)
+      const double q = ldexp(sig, 24 - E);
       const double fqd = floor(q);
       const int64_t fq = (int64_t)fqd;
       // A tie (q = fq + 1/2) rounds to the even multiple of u: from an even
       // |X|/u the increment is then always the even one of fq, fq + 1; from
       // an odd one, one explicit step first.
       const bool tie = q - fqd == 0.5;
-      if (!tie || !(((int64_t)(T / u)) & 1)) {
+      if (!tie || !(((int64_t)ldexp(T, 24 - E)) & 1)) {
         const int64_t dq = tie ? (fq & 1 ? fq + 1 : fq) : (int64_t)floor(q + 0.5);
-        const int64_t H = (int64_t)((hi - T) / u), G = (int64_t)((T - lo) / u);
+        // units of u left to the binade's ends: < 2^24
+        const int64_t H = (int64_t)ldexp(hi - T, 24 - E), G = (int64_t)ldexp(T - lo, 24 - E);
         const int64_t rem = scan - 1 - i;  // steps still to take
+        // c / d for 0 <= c < 2^24, d >= 1 in 32 bits (c / d = 0 when d > c)
+        auto div24 = [](int64_t c, int64_t d) -> int64_t {
+          return d > c ? 0 : (int64_t)((uint32_t)c / (uint32_t)d);
+        };
         // steps k = 1.. whose exact sum X_{k-1} + s stays in [lo, hi)
         if (dq > 0) {
           const int64_t c = H - fq - 1;
-          nn = c >= 0 ? c / dq + 1 : 0;
+          nn = c >= 0 ? div24(c, dq) + 1 : 0;
         } else if (dq < 0) {
           const int64_t c = G + fq;
-          nn = c >= 0 ? c / (-dq) + 1 : 0;
+          nn = c >= 0 ? div24(c, -dq) + 1 : 0;
         } else {
           nn = (q >= 0.0 || G >= 1) ? rem : 0;
         }
@@ -247,26 +265,34 @@ __global__ void __launch_bounds__(256) k_rot_points(RotGeom g, const RotTable* t
   const int first = scan > 0 ? (int)L.X : 0;  // point 0 is the start value itself
   R.ends[2 * t] = first;
   R.ends[2 * t + 1] = over ? first : last;
+  // the (sheet, edge)'s column range over all its lines (band_range)
+  const int se = t / na, lo = over ? first : imin(first, last), hi = over ? first : imax(first, last);
+  atomicMin(&slo[se - se_base], lo);
+  atomicMax(&shi[se - se_base], hi);
   R.nseg[t] = over ? 0 : ns;
   R.flag[t] = over;
   if (over) R.list[atomicAdd(R.nlist, 1)] = t;
+  }();
+  __syncthreads();
+  const int tl = imin(nlines, (int)((blockIdx.x + 1) * blockDim.x)) - 1;
+  const int ng = tl >= 0 ? tl / na - se_base + 1 : 0;
+  if ((int)threadIdx.x < ng && slo[threadIdx.x] <= shi[threadIdx.x]) {
+    atomicMin(&R.blo[se_base + threadIdx.x], slo[threadIdx.x]);
+    atomicMax(&R.bhi[se_base + threadIdx.x], shi[threadIdx.x]);
+  }
 }
 
 // Band of one (sheet, edge): columns [bx0, bx0 + bw) cover every point of
 // every angle for steps 0..kDepth-1.  Returns false when it does not fit.
 __device__ __forceinline__ bool band_range(const RotScratch& R, int tbase, int na, int sxh,
                                            int band_cap, int32_t* bx0, int32_t* bw) {
-  int32_t lo = INT_MAX, hi = INT_MIN;
-  for (int a = 0; a < na; a++) {
-    const int32_t f = R.ends[2 * (tbase + a)], l = R.ends[2 * (tbase + a) + 1];
-    lo = imin(lo, imin(f, l));
-    hi = imax(hi, imax(f, l));
-  }
+  const int se = tbase / na;
+  int32_t lo = R.blo[se], hi = R.bhi[se];
   if (sxh > 0) hi += kDepth - 1;
   else lo -= kDepth - 1;
   *bx0 = lo;
   *bw = hi - lo + 1;
-  return *bw <= band_cap;
+  return *bw <= band_cap && lo <= hi;
 }
 
 // ---- k_rot_band: slice sums of every angle x kDepth steps -----------------
@@ -539,8 +565,9 @@ __device__ void walk_line(PlaneRef img, const RotGeom& g, const RotTable* table,
                           int mask_index, int32_t* peaks, int a, int e, int s, int t,
                           int max_scan, const RotScratch& R);
 
+constexpr int kWalkThreads = 1024;  // 16 waves share a walked line's points
 template <int FMT>
-__global__ void __launch_bounds__(256) k_rot_line(PlaneRef img, RotGeom g, const RotTable* table,
+__global__ void __launch_bounds__(kWalkThreads) k_rot_line(PlaneRef img, RotGeom g, const RotTable* table,
                                                   const Rect* masks, const int32_t* mask_active,
                                                   int mask_index, int32_t* peaks, int count,
                                                   int max_scan, RotScratch R) {
@@ -570,7 +597,8 @@ __device__ void walk_line(PlaneRef img, const RotGeom& g, const RotTable* table,
   const int scan = LS.scan, maxDepth = LS.maxDepth;
   const int maxAbs = (int)(255 * g.scan_size * g.scan_depth);
   extern __shared__ int32_t pts[];  // [scan] x, then [scan] y
-  __shared__ int32_t part[4][64];
+  constexpr int kWaves = kWalkThreads / 64;
+  __shared__ int32_t part[kWaves][64];
   __shared__ int32_t done_flag, result;
   if (scan <= 0) {
     if (threadIdx.x == 0) *out = 0;
@@ -623,7 +651,7 @@ __device__ void walk_line(PlaneRef img, const RotGeom& g, const RotTable* table,
     // unconditional clamped loads, masked arithmetically (get_pixel's white
     // off the mask/image), so the unrolled loads overlap
 #pragma unroll 8
-    for (int i = w; i < scan; i += 4) {
+    for (int i = w; i < scan; i += kWaves) {
       const int32_t x = px[i] + sxh * dep, y = py[i] + syv * dep;
       const bool ok = (x >= nm.x0) & (x <= nm.x1) & (y >= nm.y0) & (y <= nm.y1) & (x >= 0) &
                       (y >= 0) & (x < g.W) & (y < g.H);
@@ -633,7 +661,9 @@ __device__ void walk_line(PlaneRef img, const RotGeom& g, const RotTable* table,
     part[w][lane] = acc;
     __syncthreads();
     if (w == 0) {
-      const int B = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+      int B = 0;
+#pragma unroll
+      for (int k = 0; k < kWaves; k++) B += part[k][lane];
       int tot;
       const int before = carry_acc + iwave_prefix_excl(B, &tot);
       const bool exec = before < maxAbs && dep < maxDepth;
@@ -684,7 +714,7 @@ static void launch_rot_t(const PlaneRef& img, const RotGeom& g, const RotTable* 
                   mask_active, mask_index, peaks, count, max_scan, R, band_cap);
   const size_t lds = sizeof(int32_t) * 2 * (size_t)(max_scan > 0 ? max_scan : 1);
   allow_dynamic_lds((const void*)k_rot_line<FMT>, lds);
-  UPH_LAUNCH_DIAG(128, k_rot_line<FMT>, dim3(imin(nlines, 1024)), dim3(256), lds, st, img, g,
+  UPH_LAUNCH_DIAG(128, k_rot_line<FMT>, dim3(imin(nlines, 1024)), dim3(kWalkThreads), lds, st, img, g,
                   table, masks, mask_active, mask_index, peaks, count, max_scan, R);
 }
 
@@ -695,7 +725,11 @@ void launch_rotation_peaks(const PlaneRef& img, const RotGeom& g, const RotTable
   if (g.nedges <= 0 || nangles <= 0) return;
   const int nlines = count * g.nedges * nangles;
   const RotScratch R = rot_scratch(lines, nlines, max_scan);
-  if (hipMemsetAsync(R.nlist, 0, sizeof(int32_t), st) != hipSuccess) return;  // the launches below report
+  // the launches below report a failure; column ranges start empty (0x7F.. / 0x80..)
+  if (hipMemsetAsync(R.nlist, 0, sizeof(int32_t), st) != hipSuccess ||
+      hipMemsetAsync(R.blo, 0x7F, sizeof(int32_t) * nlines, st) != hipSuccess ||
+      hipMemsetAsync(R.bhi, 0x80, sizeof(int32_t) * nlines, st) != hipSuccess)
+    return;
   UPH_LAUNCH_DIAG(16, k_rot_points, dim3((nlines + 255) / 256), dim3(256), 0, st, g, table, masks,
                   mask_active, count, R);
   switch (img.P.fmt) {
