@@ -971,6 +971,12 @@ __device__ __forceinline__ int move_class(const MoveArgs& a, int32_t W, int32_t 
 }
 
 constexpr int kChainBp = 17;  // 7 of the align move and mask + 2 x 5 of the centring
+#ifndef UPH_CHAIN_WAVES
+#define UPH_CHAIN_WAVES 4
+#endif
+constexpr int kChainThreads = 64 * UPH_CHAIN_WAVES;
+constexpr int kChainRows = kMoveRows * UPH_CHAIN_WAVES;  // rows per block (kMoveRows a wave)
+static_assert(kChainThreads >= kChainBp, "a thread per breakpoint");
 struct ChainSheet {
   MoveArgs m1, m2;
   Rect mk;
@@ -990,7 +996,7 @@ __device__ __forceinline__ int2 chain_cell(const ChainSheet& c, int32_t W, int32
   return make_int2(-1, (int32_t)((int64_t)(sy - y) * pitch + (sx - x)));
 }
 
-__global__ void __launch_bounds__(kThreads) k_move_chain_g16(PlaneRef src, PlaneRef dst,
+__global__ void __launch_bounds__(kChainThreads) k_move_chain_g16(PlaneRef src, PlaneRef dst,
                                                              const MoveArgs* center,
                                                              const MaskArgs* masks,
                                                              const MoveArgs* align) {
@@ -1000,8 +1006,8 @@ __global__ void __launch_bounds__(kThreads) k_move_chain_g16(PlaneRef src, Plane
   const int64_t pitch = P.pitch;
   const uint8_t* sbase = plane_ptr(src, s);
   uint8_t* dbase = plane_ptr(dst, s);
-  const int32_t yb = blockIdx.x * kMoveBlockRows;
-  const int nrows = imin(kMoveBlockRows, H - yb);
+  const int32_t yb = blockIdx.x * kChainRows;
+  const int nrows = imin(kChainRows, H - yb);
   ChainSheet c;
   c.m1 = center[s];
   c.m2 = align[s];
@@ -1015,7 +1021,7 @@ __global__ void __launch_bounds__(kThreads) k_move_chain_g16(PlaneRef src, Plane
   __shared__ int32_t nbp_s, nd_s;
   __shared__ int32_t dv[kChainBp + 1];  // vectors holding a breakpoint (+ the row's partial one)
   __shared__ uint8_t live[kChainBp], imap[kChainBp + 1];
-  __shared__ int2 cell[kMoveBlockRows][kChainBp + 1];
+  __shared__ int2 cell[kChainRows][kChainBp + 1];
   if (threadIdx.x == 0) {
     // the columns where some stage's class can change (first column of the
     // new interval), sorted, unique, inside (0, W)
@@ -1229,8 +1235,8 @@ bool launch_move_chain(const PlaneRef& src, const PlaneRef& dst, const MoveArgs*
                        const MaskArgs* masks, const MoveArgs* align, int count, hipStream_t st) {
   if (src.P.fmt != F_GRAY8 || src.P.pitch * (int64_t)src.P.H >= (1ll << 31) || src.P.H < 1)
     return false;
-  const int64_t blocks = (src.P.H + kMoveBlockRows - 1) / kMoveBlockRows;
-  UPH_LAUNCH_DIAG(4, k_move_chain_g16, dim3((unsigned)blocks, 1, count), dim3(kThreads), 0, st,
+  const int64_t blocks = (src.P.H + kChainRows - 1) / kChainRows;
+  UPH_LAUNCH_DIAG(4, k_move_chain_g16, dim3((unsigned)blocks, 1, count), dim3(kChainThreads), 0, st,
                   src, dst, center, masks, align);
   return true;
 }
