@@ -177,6 +177,64 @@ static void jpeg(const char *fixtures) {
   }
 }
 
+/* crafted JPEG headers: an over-subscribed Huffman table must
+ * be refused before it indexes the lookahead table, and a frame claiming far
+ * more blocks than the file holds must fail without sizing anything from it */
+static size_t put16(uint8_t *p, size_t i, int v) {
+  p[i] = (uint8_t)(v >> 8);
+  p[i + 1] = (uint8_t)v;
+  return i + 2;
+}
+
+static void jpeg_crafted(void) {
+  static uint8_t f[4096];
+  for (int variant = 0; variant < 3; variant++) {
+    size_t i = 0;
+    f[i++] = 0xFF, f[i++] = 0xD8;
+    if (variant < 2) { /* DHT with bits[0] = 3 or 255 (at most 2 codes of length 1) */
+      const int n1 = variant == 0 ? 3 : 255;
+      f[i++] = 0xFF, f[i++] = 0xC4;
+      i = put16(f, i, 2 + 17 + n1);
+      f[i++] = 0x00;
+      f[i++] = (uint8_t)n1;
+      for (int k = 1; k < 16; k++) f[i++] = 0;
+      for (int k = 0; k < n1; k++) f[i++] = (uint8_t)k;
+    } else { /* 65535 x 65535 x 3 components with a few bytes of data */
+      f[i++] = 0xFF, f[i++] = 0xDB;
+      i = put16(f, i, 2 + 65);
+      f[i++] = 0x00;
+      for (int k = 0; k < 64; k++) f[i++] = 1;
+      f[i++] = 0xFF, f[i++] = 0xC0;
+      i = put16(f, i, 2 + 6 + 9);
+      f[i++] = 8;
+      i = put16(f, i, 65535);
+      i = put16(f, i, 65535);
+      f[i++] = 3;
+      for (int c = 0; c < 3; c++) f[i++] = (uint8_t)(c + 1), f[i++] = 0x11, f[i++] = 0;
+      for (int ac = 0; ac < 2; ac++) { /* one 1-bit code each: DC cat 0, AC EOB */
+        f[i++] = 0xFF, f[i++] = 0xC4;
+        i = put16(f, i, 2 + 17 + 1);
+        f[i++] = (uint8_t)(ac << 4);
+        f[i++] = 1;
+        for (int k = 1; k < 16; k++) f[i++] = 0;
+        f[i++] = 0;
+      }
+      f[i++] = 0xFF, f[i++] = 0xDA;
+      i = put16(f, i, 2 + 1 + 6 + 3);
+      f[i++] = 3;
+      for (int c = 0; c < 3; c++) f[i++] = (uint8_t)(c + 1), f[i++] = 0x00;
+      f[i++] = 0, f[i++] = 63, f[i++] = 0;
+      for (int k = 0; k < 32; k++) f[i++] = 0x00;
+    }
+    f[i++] = 0xFF, f[i++] = 0xD9;
+    if (uphip_jpeg_entropy_decode(f, i, NULL, 0) >= 0) {
+      fprintf(stderr, "crafted jpeg %d accepted\n", variant);
+      g_fail++;
+    }
+    uphip_clear_error();
+  }
+}
+
 int main(int argc, char **argv) {
   const char *dir = argc > 1 ? argv[1] : "/tmp";
   UphipOptions o;
@@ -198,6 +256,7 @@ int main(int argc, char **argv) {
   codec(dir);
   png(dir, argc > 2 ? argv[2] : "tests/golden/reference");
   jpeg(argc > 2 ? argv[2] : "tests/golden/reference");
+  jpeg_crafted();
   printf("sanitize: %d failures\n", g_fail);
   return g_fail ? 1 : 0;
 }

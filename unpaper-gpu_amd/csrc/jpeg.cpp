@@ -49,6 +49,9 @@ bool build_huff(Huff* t, const uint8_t* bits /*16*/, const uint8_t* vals, int nv
     t->valptr[len] = k;
     t->mincode[len] = code;
     for (int i = 0; i < bits[len - 1]; i++, k++, code++) {
+      // an over-subscribed table (more codes of this length than 2^len)
+      // is refused before its codes index the lookahead table
+      if (code >= (1 << len)) return false;
       if (len <= kLook) {
         const int shift = kLook - len;
         for (int j = 0; j < (1 << shift); j++)
@@ -56,7 +59,6 @@ bool build_huff(Huff* t, const uint8_t* bits /*16*/, const uint8_t* vals, int nv
       }
     }
     t->maxcode[len] = bits[len - 1] ? code - 1 : -1;
-    if (code > (1 << len)) return false;  // over-subscribed
     code <<= 1;
   }
   t->maxcode[17] = 0x7fffffff;
@@ -180,6 +182,7 @@ struct Parser {
   int cid[4] = {}, hs[4] = {}, vs[4] = {}, tq[4] = {};
   uint16_t qt[4][64];  // zigzag order
   bool have_qt[4] = {};
+  bool latched[4] = {};
   Huff dc[4], ac[4];
   int restart = 0;
   bool jfif = false, adobe = false;
@@ -293,7 +296,6 @@ void frame_geometry(const Parser& P, JpegHeader* H) {
     c.pitch = c.bw * 8;
     c.plane_off = off;
     off += (int64_t)c.pitch * c.bh * 8;
-    for (int k = 0; k < 64; k++) c.qzz[k] = P.qt[P.tq[i]][k];
   }
   H->scratch_bytes = P.nf == 1 ? 0 : off;
 }
@@ -323,6 +325,15 @@ bool decode_scan(Parser& P, const uint8_t* b, int len, JpegDecoded* out) {
   const int ss = b[1 + 2 * ns], se = b[2 + 2 * ns], ahal = b[3 + 2 * ns];
   if (ss != 0 || se != 63 || ahal != 0) return ffail(P, "not a sequential scan");
   if (H.nscans == 0) frame_geometry(P, &H);
+  // libjpeg latches a component's quantisation table when the component
+  // first appears in a scan (jdinput.c latch_quant_tables): a DQT between
+  // scans applies to the components that appear later
+  for (int i = 0; i < ns; i++) {
+    const int c = S.comp[i];
+    if (P.latched[c]) continue;
+    for (int k = 0; k < 64; k++) H.comp[c].qzz[k] = P.qt[P.tq[c]][k];
+    P.latched[c] = true;
+  }
   S.ncomp = ns;
   if (ns == 1) {  // non-interleaved: one block per MCU over the component's real blocks
     const JpegComp& c = H.comp[S.comp[0]];
@@ -339,6 +350,10 @@ bool decode_scan(Parser& P, const uint8_t* b, int len, JpegDecoded* out) {
   S.first_block = H.nblocks;
   S.first_group = (int32_t)H.ngroups;
   const int64_t nb = (int64_t)S.mcus_x * S.mcus_y * S.blocks_per_mcu;
+  // every block takes at least two bits (a DC and an AC code): a frame header
+  // claiming more blocks than the file's remaining bytes can hold is refused
+  // before anything is sized from it
+  if (nb > 4 * (int64_t)(P.n - P.pos) + 64) return ffail(P, "frame larger than the file's data");
   out->counts.reserve((size_t)(H.nblocks + nb));
   // per block of an MCU: its component (for the Huffman tables and predictor)
   int bcomp[10];
@@ -362,6 +377,9 @@ bool decode_scan(Parser& P, const uint8_t* b, int len, JpegDecoded* out) {
   int64_t mcu = 0;
   const int64_t nmcu = (int64_t)S.mcus_x * S.mcus_y;
   for (int my = 0; my < S.mcus_y; my++) {
+    // the data ran out (zero bits fed past its end or a marker): stop now
+    // rather than decode the rest of the frame from zeros
+    if (bits.underrun()) return ffail(P, "truncated or corrupt entropy-coded data");
     out->groups.push_back((uint32_t)pos);
     if (pos > 0xF0000000u) return ffail(P, "image too large");
     for (int mx = 0; mx < S.mcus_x; mx++, mcu++) {

@@ -96,6 +96,8 @@ void jpeg_pack(const JpegDecoded& j, uint8_t* dst);
 bool jpeg_launch(const JpegHeader& h, const uint8_t* dpacked, uint8_t* scratch, uint8_t* dst,
                  int64_t dpitch, hipStream_t st);
 bool jpeg_read_file(const char* path, std::vector<uint8_t>* buf);
+// The frame header alone (geometry, pixel format), no entropy decoding.
+bool jpeg_probe_mem(const uint8_t* d, size_t n, const char* name, UphipPnmInfo* info);
 // the pixel format a decoded header yields (GRAY8 or RGB24)
 inline int jpeg_format(const JpegHeader& h) { return h.ncomp == 1 ? UPHIP_FMT_GRAY8 : UPHIP_FMT_RGB24; }
 

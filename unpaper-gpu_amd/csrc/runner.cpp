@@ -506,17 +506,22 @@ bool is_jpeg_file(const std::string& path) {
 }
 
 // The host half of a JPEG page into the slot's pinned buffer `jp`.
-bool jpeg_load(UphipRunner* r, const std::string& path, JpegPage* jp) {
+bool jpeg_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp) {
   std::vector<uint8_t> file;
-  JpegDecoded d;
-  if (!jpeg_read_file(path.c_str(), &file) ||
-      !jpeg_entropy_decode(file.data(), file.size(), path.c_str(), &d))
-    return false;
-  if (d.h.width != r->geo.page_width || d.h.height != r->geo.page_height ||
-      jpeg_format(d.h) != r->geo.page_format)
-    return fail("jpeg: %s is %dx%d format %d, expected %dx%d format %d", path.c_str(), d.h.width,
-                d.h.height, jpeg_format(d.h), r->geo.page_width, r->geo.page_height,
+  if (!jpeg_read_file(path.c_str(), &file)) return false;
+  // the frame header first: a file of the wrong geometry (or a crafted one
+  // claiming a huge frame) is refused before anything is sized from it
+  UphipPnmInfo info{0, 0, 0};
+  if (!jpeg_probe_mem(file.data(), file.size(), path.c_str(), &info)) return false;
+  if (info.width != r->geo.page_width || info.height != r->geo.page_height ||
+      info.format != r->geo.page_format)
+    return fail("jpeg: %s is %dx%d format %d, expected %dx%d format %d", path.c_str(), info.width,
+                info.height, info.format, r->geo.page_width, r->geo.page_height,
                 r->geo.page_format);
+  JpegDecoded d;
+  if (!jpeg_entropy_decode(file.data(), file.size(), path.c_str(), &d)) return false;
+  // pinned memory for this device (the pool thread may have another current)
+  if (uphip_set_device(device) != 0) return false;
   const size_t need = (size_t)d.h.total_bytes;
   if (jp->cap < need) {
     if (jp->host) hipHostFree(jp->host);
@@ -531,14 +536,14 @@ bool jpeg_load(UphipRunner* r, const std::string& path, JpegPage* jp) {
   return true;
 }
 
-bool load_page(UphipRunner* r, const UphipSource* s, int64_t job, int32_t j, uint8_t* dst,
-               JpegPage* jp) {
+bool load_page(UphipRunner* r, int device, const UphipSource* s, int64_t job, int32_t j,
+               uint8_t* dst, JpegPage* jp) {
   const UphipPnmInfo geo{r->geo.page_width, r->geo.page_height, r->geo.page_format};
   const int64_t idx = job * r->opts.input_count + j;
   if (s->load) return s->load(s->user, job, j, dst, r->in_pitch) == 0;
   if (s->base) return mem_load(s, idx, dst, r->in_pitch, geo) == 0;
   if (idx >= 0 && idx < (int64_t)s->paths.size() && is_jpeg_file(s->paths[(size_t)idx]))
-    return jpeg_load(r, s->paths[(size_t)idx], jp);
+    return jpeg_load(r, device, s->paths[(size_t)idx], jp);
   return pnm_load(s, idx, dst, r->in_pitch, geo) == 0;
 }
 
@@ -1020,7 +1025,7 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
                 const auto a = Clock::now();
                 for (int j = 0; j < nin; j++) {
                   uint8_t* dst = sl->hin + ((int64_t)s * nin + j) * r->in_page_stride;
-                  if (!load_page(r, src, first + s, j, dst, &sl->jpg[(size_t)(s * nin + j)])) {
+                  if (!load_page(r, dc.device, src, first + s, j, dst, &sl->jpg[(size_t)(s * nin + j)])) {
                     sl->failed[(size_t)s] |= 4;
                     uphip_clear_error();
                     // the slot still runs: a blank (white) page, cheap and
