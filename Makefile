@@ -87,9 +87,9 @@ $(LIB): $(HIP_OBJS) $(CPP_OBJS) $(C_OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread -lz
 
-$(ORACLE_LIB): oracle/oracle.c oracle/oracle.h include/unpaper_hip.h
+$(ORACLE_LIB): oracle/oracle.c oracle/jpeg_enc.c oracle/oracle.h include/unpaper_hip.h
 	@mkdir -p oracle/_build
-	$(CC) $(CFLAGS_O) -shared -o $@ oracle/oracle.c -lm
+	$(CC) $(CFLAGS_O) -shared -o $@ oracle/oracle.c oracle/jpeg_enc.c -lm
 
 # A plain C program: the reference's own callers are C (sheet_stages.c).
 $(CTEST): tests/c/backend_ops.c tests/c/pages.h include/unpaper_hip.h oracle/oracle.h $(LIB) $(ORACLE_LIB)

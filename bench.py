@@ -57,7 +57,8 @@ sys.path.insert(0, os.path.join(ROOT, "unpaper-gpu_amd", "python"))
 from unpaper_hip import ctypes_abi as A  # noqa: E402
 from unpaper_hip.device import load_library, UnpaperHipError  # noqa: E402
 from unpaper_hip.pipeline import (Batch, DeviceBuffer, Runner, sink_discard,  # noqa: E402
-                                  sink_memory, sink_pnm, source_memory, source_pnm)
+                                  sink_jpeg, sink_memory, sink_pnm, source_memory,
+                                  source_pnm)
 from unpaper_hip.workloads import A4_H, A4_W, C4_H, C4_W, c4_options  # noqa: E402
 
 METRIC = "pages/sec + Mpixel/s, 1000-page GRAY8 A4@300dpi batch, 1/2/4/8 GPU"
@@ -342,6 +343,7 @@ def host_io(opts, dev0, host_in, npages, args, threads):
         out["h2d_d2h"] = {"value": round(npages / t, 2), "unit": "pages/s",
                           "load_s": round(st.load_s, 3), "store_s": round(st.store_s, 3),
                           "verified": len(sample)}
+        keep = [np.ascontiguousarray(host_out[p][:, :W]) for p in sample[:2]]
         del host_out, snk
         tmpdir = tempfile.mkdtemp(prefix="uphip_bench_",
                                   dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
@@ -357,6 +359,33 @@ def host_io(opts, dev0, host_in, npages, args, threads):
             out["pnm_write"] = {"value": round(npages / t, 2), "unit": "pages/s",
                                 "load_s": round(st.load_s, 3), "store_s": round(st.store_s, 3),
                                 "files": "PGM (P5) into tmpfs, 64 names reused"}
+            # the GPU JPEG output branch (sheet_stages.c:554-581): pages encoded
+            # on the device after their batch, only the files cross PCIe
+            snk = sink_jpeg(os.path.join(tmpdir, "out_%04lld.jpg"), 64, 85, 0)
+            for rep in range(2):
+                t0 = time.perf_counter()
+                failed, err = r.run_host(npages, src, snk)
+                t = time.perf_counter() - t0
+                if failed:
+                    raise UnpaperHipError("JPEG run: %d failed: %s" % (failed, err))
+            st = r.stats()
+            # files equal libjpeg-turbo's (PIL) encode of the oracle-verified sheets
+            import io
+            from PIL import Image
+            same = 0
+            for i, sheet in enumerate(keep):
+                b = io.BytesIO()
+                Image.fromarray(sheet).save(b, "JPEG", quality=85)
+                with open(os.path.join(tmpdir, "out_%04d.jpg" % sample[i]), "rb") as f:
+                    same += f.read() == b.getvalue()
+            if same != len(keep):
+                raise SystemExit("bench.py: JPEG files differ from PIL's encode of the sheets")
+            kb = os.path.getsize(os.path.join(tmpdir, "out_0000.jpg")) / 1e3
+            out["jpeg_write"] = {"value": round(npages / t, 2), "unit": "pages/s",
+                                 "load_s": round(st.load_s, 3), "store_s": round(st.store_s, 3),
+                                 "files": "JPEG q85 (GPU encode) into tmpfs, 64 names reused, "
+                                          "%.0f kB a page" % kb,
+                                 "verified": same}
         finally:
             shutil.rmtree(tmpdir, ignore_errors=True)
         out["config"] = {"sheets_per_batch": args.host_batch, "streams": args.host_streams,

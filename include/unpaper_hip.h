@@ -447,6 +447,24 @@ int uphip_batch_download_async(UphipBatch *batch, void *host, int64_t linesize,
                                int64_t sheet_stride);
 int uphip_batch_query(UphipBatch *batch);
 void *uphip_batch_stream(UphipBatch *batch);
+/* The GPU JPEG output branch for a whole batch (encode_queue_submit_gpu,
+ * lib/encode_queue.c:860-990, per sheet in the reference): queued on the
+ * batch stream after uphip_batch_run*, it encodes every output page of the
+ * last run (count * output_count pages; page j of a sheet is its j-th
+ * output_count-th, side by side as the PNM sinks split it) from the finished
+ * working sheet -- GRAY8 sheets as one component, RGB24 ones as YCbCr --
+ * and packs the files one after another in device memory, then copies their
+ * sizes to the host.  After the stream is idle (uphip_batch_query() == 1):
+ *   jpeg_sizes:           sizes[i] of page i (-1: larger than the batch's
+ *                         encode buffers, re-encode it with uphip_jpeg_encode
+ *                         from uphip_batch_jpeg_page); returns the packed total
+ *   jpeg_download_async:  the packed files into host memory (total bytes)
+ *   jpeg_page:            device pointer / pitch / size of output page i. */
+int uphip_batch_encode_jpeg_async(UphipBatch *batch, int32_t quality, int32_t sampling);
+int64_t uphip_batch_jpeg_sizes(UphipBatch *batch, int64_t *sizes, int32_t max_pages);
+int uphip_batch_jpeg_download_async(UphipBatch *batch, void *host, int64_t capacity);
+int uphip_batch_jpeg_page(UphipBatch *batch, int32_t page, const void **device_src,
+                          int64_t *pitch, int32_t *width, int32_t *height, int32_t *format);
 /* Row pitch of the output sheets on the device: host staging with this
  * linesize (and pitch * height per sheet) downloads as linear DMA copies. */
 int uphip_batch_output_pitch(UphipBatch *batch, int64_t *pitch);
@@ -500,6 +518,26 @@ int uphip_jpeg_decode(const void *data, size_t size, void *device_dst, int64_t p
  * Returns its size in bytes, or -1. */
 int64_t uphip_jpeg_entropy_decode(const void *data, size_t size, void *packed,
                                   int64_t capacity);
+/* JPEG encode peer of nvimgcodec_encode / nvimgcodec_encode_jpeg
+ * (imageprocess/nvimgcodec.c:1007-1148), the GPU output branch of
+ * sheet_stage_output (src/core/sheet_stages.c:554-581): a device image
+ * (GRAY8 -> one component, RGB24 -> YCbCr with `sampling`; rows `pitch`
+ * bytes apart) encoded on the current device/stream as a baseline JPEG file
+ * with the Annex K tables scaled by `quality` (1..100, 0 = 85, the
+ * reference's default: lib/options.h:42, nvimgcodec.c:451).  The bytes equal
+ * libjpeg-turbo's for the same quality and sampling (PIL's encoder;
+ * nvImageCodec's own output is unpinned).  Returns the file size; the bytes
+ * are copied to `out` (host memory) only when `capacity` suffices (out =
+ * NULL sizes a buffer).  Synchronous; -1 on error. */
+#define UPHIP_JPEG_DEFAULT_QUALITY 85
+typedef enum {
+  UPHIP_JPEG_444 = 0, /* nvImageCodec's default (no chroma subsampling) */
+  UPHIP_JPEG_422 = 1,
+  UPHIP_JPEG_420 = 2, /* libjpeg's default */
+} UphipJpegSampling;
+int64_t uphip_jpeg_encode(const void *device_src, int64_t pitch, int32_t width,
+                          int32_t height, int32_t format, int32_t quality,
+                          int32_t sampling, void *out, int64_t capacity);
 /* Any codec, picked by the file's signature (PNG, JPEG or PNM). */
 int uphip_image_probe(const char *path, UphipPnmInfo *info);
 int uphip_image_read(const char *path, void *dst, int64_t linesize,
@@ -573,6 +611,11 @@ UphipSink *uphip_sink_memory(void *base, int64_t linesize, int64_t sheet_stride,
  * when wrap > 0) */
 UphipSink *uphip_sink_pnm(const char *pattern, int64_t wrap);
 UphipSink *uphip_sink_discard(void);
+/* JPEG files (the GPU encode branch): pages encoded on the device right after
+ * their batch (uphip_batch_encode_jpeg_async), only the files cross PCIe;
+ * names as uphip_sink_pnm.  quality 0 = 85. */
+UphipSink *uphip_sink_jpeg(const char *pattern, int64_t wrap, int32_t quality,
+                           int32_t sampling);
 void uphip_sink_destroy(UphipSink *sink);
 
 UphipRunner *uphip_runner_create(const UphipOptions *options,

@@ -107,6 +107,16 @@ void o_stats_reset(void);
 
 /* options_init defaults (lib/options.c:23-173 + cli_options.c thresholds) */
 void o_options_init(UphipOptions *o);
+
+/* jpeg_enc.c — the JPEG encode of the GPU output branch (nvimgcodec.c:
+ * 1007-1212), restated as libjpeg-turbo's baseline encoder (pinned to PIL's
+ * libjpeg-turbo; nvImageCodec itself is unpinned).  fmt GRAY8 -> 1 component,
+ * RGB24 -> YCbCr with sampling 0 = 4:4:4, 1 = 4:2:2, 2 = 4:2:0. */
+int64_t o_jpeg_encode(const uint8_t *src, int64_t linesize, int w, int h, int fmt,
+                      int quality, int sampling, uint8_t *out, int64_t cap);
+int64_t o_jpeg_header(int w, int h, int ncomp, int sampling, int quality, uint8_t *out,
+                      int64_t cap);
+void o_jpeg_quant_tables(int quality, uint16_t qtab[2][64]);
 size_t oracle_abi_sizeof(const char *name);
 
 #ifdef __cplusplus

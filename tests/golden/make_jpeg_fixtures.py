@@ -1,6 +1,6 @@
 """Small JPEG fixtures for the host decoder's sanitizer run (tests/c/sanitize_main.c):
 PIL-encoded files of the kinds the decoder takes (gray, 4:2:0 with restart
-markers, 4:4:4 with optimised tables) and one it refuses (progressive).
+markers, 4:4:4 with optimised tables, progressive).
 Run from the repository root: python tests/golden/make_jpeg_fixtures.py"""
 import os
 

@@ -3,7 +3,8 @@
 Parity anchors:
 - pixels: PIL's libjpeg-turbo (libjpeg's default islow IDCT, fancy
   upsampling, ycc_rgb_convert), byte for byte, for gray, 4:4:4, 4:2:2 and
-  4:2:0 files, odd sizes, restart intervals, optimised Huffman tables.  The
+  4:2:0 files, odd sizes, restart intervals, optimised Huffman tables,
+  baseline and progressive (spectral selection, successive approximation).  The
   reference decodes with FFmpeg (file.c:29-128) or nvImageCodec
   (nvimgcodec.c:679-1007): parity with those decoders is unpinned.
 - the reference's own acceptance test (tests/unpaper_tests.py:921-955):
@@ -61,6 +62,15 @@ CASES = [
     ("RGB", 5, 9, dict(quality=90, subsampling=2)),      # downsampled width <= 2: box
     ("RGB", 300, 200, dict(quality=85, subsampling=2, restart_marker_blocks=3)),
     ("RGB", 257, 129, dict(quality=100, subsampling=0)),
+    # progressive (SOF2): spectral selection + successive approximation
+    # scans, end-of-band runs (libjpeg's jpeg_simple_progression script)
+    ("L", 333, 257, dict(quality=95, progressive=True)),
+    ("L", 70, 50, dict(quality=30, progressive=True, optimize=True)),
+    ("RGB", 71, 53, dict(quality=90, subsampling=2, progressive=True)),
+    ("RGB", 77, 41, dict(quality=90, subsampling=1, progressive=True)),
+    ("RGB", 257, 129, dict(quality=100, subsampling=0, progressive=True)),
+    ("RGB", 300, 200, dict(quality=85, subsampling=2, progressive=True,
+                           restart_marker_blocks=3)),
 ]
 
 
@@ -103,11 +113,12 @@ def test_probe(lib, tmp_path):
         assert info.format == fmt
 
 
-@pytest.mark.parametrize("what,kw", [("progressive", dict(progressive=True)),
+@pytest.mark.parametrize("what,kw", [("truncated_progressive", dict(progressive=True)),
                                      ("truncated", None), ("garbage", None)])
 def test_refused_files(lib, what, kw):
-    if what == "progressive":
+    if what == "truncated_progressive":
         data = make_jpeg(64, 64, "RGB", quality=90, **kw)
+        data = data[:len(data) * 2 // 3]
     elif what == "truncated":
         data = make_jpeg(64, 64, "L", quality=90)[:40]
     else:

@@ -187,6 +187,10 @@ struct Parser {
   int restart = 0;
   bool jfif = false, adobe = false;
   int adobe_transform = -1;
+  // progressive (SOF2): every component's coefficients, zigzag order, over
+  // its MCU-padded blocks (bw x bh), refined scan after scan
+  bool progressive = false;
+  std::vector<int16_t> pc[3];
 };
 
 bool ffail(const Parser& P, const char* what) {
@@ -213,12 +217,11 @@ bool segment(Parser& P, const uint8_t** body, int* len) {
 
 bool parse_sof(Parser& P, int code, const uint8_t* b, int len) {
   if (P.have_frame) return ffail(P, "more than one frame");
-  if (code != 0xC0 && code != 0xC1) {
-    if (code == 0xC2 || code == 0xC6 || code == 0xCA || code == 0xCE)
-      return ffail(P, "progressive JPEG is not supported");
+  if (code != 0xC0 && code != 0xC1 && code != 0xC2) {
     if (code >= 0xC9) return ffail(P, "arithmetic-coded JPEG is not supported");
     return ffail(P, "lossless / hierarchical JPEG is not supported");
   }
+  P.progressive = code == 0xC2;
   if (len < 6) return ffail(P, "bad SOF");
   if (b[0] != 8) return ffail(P, "only 8-bit samples are supported");
   P.h = be16(b + 1);
@@ -455,6 +458,229 @@ bool decode_scan(Parser& P, const uint8_t* b, int len, JpegDecoded* out) {
   return true;
 }
 
+// Progressive scans (T.81 G.1.2; libjpeg jdphuff.c decode_mcu_DC_first /
+// _DC_refine / _AC_first / _AC_refine): DC scans interleaved or not, AC
+// scans of one component, spectral selection Ss..Se, successive
+// approximation Ah/Al, end-of-band runs.  Coefficients accumulate in P.pc.
+bool decode_prog_scan(Parser& P, const uint8_t* b, int len, JpegDecoded* out) {
+  JpegHeader& H = out->h;
+  if (!P.have_frame) return ffail(P, "SOS before SOF");
+  if (len < 1) return ffail(P, "bad SOS");
+  const int ns = b[0];
+  if (ns < 1 || ns > 4 || len < 4 + 2 * ns) return ffail(P, "bad SOS");
+  int comp[4], tdc[4], tac[4];
+  const int ss = b[1 + 2 * ns], se = b[2 + 2 * ns], ah = b[3 + 2 * ns] >> 4, al = b[3 + 2 * ns] & 15;
+  // jdphuff.c start_pass_phuff_decoder's checks
+  if (ss == 0 ? se != 0 : (se < ss || se > 63 || ns != 1)) return ffail(P, "bad progressive scan");
+  if ((ah != 0 && ah != al + 1) || al > 13) return ffail(P, "bad successive approximation");
+  if (H.nscans == 0 && P.pc[0].empty()) {
+    frame_geometry(P, &H);
+    int64_t nb = 0;
+    for (int c = 0; c < P.nf; c++) nb += (int64_t)H.comp[c].bw * H.comp[c].bh;
+    // the DC scan codes each block in at least one bit
+    if (nb > 8 * (int64_t)(P.n - P.pos) + 64 || nb > (1 << 24))
+      return ffail(P, "frame larger than the file's data");
+    for (int c = 0; c < P.nf; c++) P.pc[c].assign((size_t)H.comp[c].bw * H.comp[c].bh * 64, 0);
+  }
+  for (int i = 0; i < ns; i++) {
+    const int id = b[1 + 2 * i];
+    int c = -1;
+    for (int k = 0; k < P.nf; k++)
+      if (P.cid[k] == id) c = k;
+    if (c < 0) return ffail(P, "scan names an unknown component");
+    comp[i] = c;
+    tdc[i] = b[2 + 2 * i] >> 4;
+    tac[i] = b[2 + 2 * i] & 15;
+    if (ss == 0 && ah == 0 && (tdc[i] > 3 || !P.dc[tdc[i]].present))
+      return ffail(P, "scan uses a missing Huffman table");
+    if (ss > 0 && (tac[i] > 3 || !P.ac[tac[i]].present))
+      return ffail(P, "scan uses a missing Huffman table");
+    if (!P.have_qt[P.tq[c]]) return ffail(P, "component uses a missing quantisation table");
+    if (!P.latched[c]) {
+      for (int k = 0; k < 64; k++) H.comp[c].qzz[k] = P.qt[P.tq[c]][k];
+      P.latched[c] = true;
+    }
+  }
+  // MCU geometry: interleaved (DC scans of several components) over the
+  // frame's MCUs, else one block per MCU over the component's real blocks
+  int mcus_x, mcus_y;
+  if (ns == 1) {
+    const JpegComp& c = H.comp[comp[0]];
+    mcus_x = (c.dw + 7) / 8;
+    mcus_y = (c.dh + 7) / 8;
+  } else {
+    mcus_x = (P.w + 8 * H.hmax - 1) / (8 * H.hmax);
+    mcus_y = (P.h + 8 * H.vmax - 1) / (8 * H.vmax);
+  }
+  Bits bits{P.d + P.pos, P.d + P.n};
+  int pred[4] = {0, 0, 0, 0};
+  int eobrun = 0;
+  const int p1 = 1 << al, m1 = -(1 << al);
+  int64_t mcu = 0;
+  for (int my = 0; my < mcus_y; my++) {
+    if (bits.underrun()) return ffail(P, "truncated or corrupt entropy-coded data");
+    for (int mx = 0; mx < mcus_x; mx++, mcu++) {
+      if (P.restart && mcu > 0 && mcu % P.restart == 0) {
+        if (bits.underrun()) return ffail(P, "truncated or corrupt entropy-coded data");
+        const uint8_t* q = bits.p;
+        while (q + 1 < bits.end && !(q[0] == 0xFF && q[1] >= 0xD0 && q[1] <= 0xD7)) q++;
+        if (q + 1 >= bits.end) return ffail(P, "missing restart marker");
+        bits.p = q + 2;
+        bits.reset();
+        pred[0] = pred[1] = pred[2] = pred[3] = 0;
+        eobrun = 0;
+      }
+      for (int i = 0; i < ns; i++) {
+        const JpegComp& C = H.comp[comp[i]];
+        const int nbx = ns == 1 ? 1 : C.h, nby = ns == 1 ? 1 : C.v;
+        for (int by = 0; by < nby; by++)
+          for (int bx = 0; bx < nbx; bx++) {
+            const int64_t gx = (int64_t)mx * nbx + bx, gy = (int64_t)my * nby + by;
+            int16_t* blk = P.pc[comp[i]].data() + (gy * C.bw + gx) * 64;
+            if (ss == 0) {
+              if (ah == 0) {  // DC first
+                const int t = bits.decode(P.dc[tdc[i]]);
+                if (t < 0 || t > 11) return ffail(P, "corrupt entropy-coded data (DC)");
+                pred[i] += t ? extend(bits.get(t), t) : 0;
+                blk[0] = (int16_t)(pred[i] * (1 << al));
+              } else if (bits.get(1)) {  // DC refine
+                blk[0] = (int16_t)(blk[0] | p1);
+              }
+              continue;
+            }
+            const Huff& ac = P.ac[tac[i]];
+            int k = ss;
+            if (ah == 0) {  // AC first
+              if (eobrun > 0) {
+                eobrun--;
+                continue;
+              }
+              for (; k <= se; k++) {
+                const int rs = bits.decode(ac);
+                if (rs < 0) return ffail(P, "corrupt entropy-coded data (AC)");
+                const int r = rs >> 4, sz = rs & 15;
+                if (sz) {
+                  k += r;
+                  if (k > se || sz > 10) return ffail(P, "corrupt entropy-coded data (AC run)");
+                  blk[k] = (int16_t)(extend(bits.get(sz), sz) * (1 << al));
+                } else if (r == 15) {
+                  k += 15;
+                } else {
+                  eobrun = (1 << r) - 1;
+                  if (r) eobrun += (int)bits.get(r);
+                  break;
+                }
+              }
+              continue;
+            }
+            // AC refine
+            auto refine = [&](int16_t* coef) {
+              if (bits.get(1) && (*coef & p1) == 0) *coef = (int16_t)(*coef + (*coef >= 0 ? p1 : m1));
+            };
+            if (eobrun == 0) {
+              for (; k <= se; k++) {
+                const int rs = bits.decode(ac);
+                if (rs < 0) return ffail(P, "corrupt entropy-coded data (AC)");
+                int r = rs >> 4;
+                int sv = 0;
+                if (rs & 15) {
+                  if ((rs & 15) != 1) return ffail(P, "corrupt entropy-coded data (AC refine)");
+                  sv = bits.get(1) ? p1 : m1;
+                } else if (r != 15) {
+                  eobrun = 1 << r;
+                  if (r) eobrun += (int)bits.get(r);
+                  break;
+                }
+                do {
+                  int16_t* coef = blk + k;
+                  if (*coef != 0) {
+                    refine(coef);
+                  } else {
+                    if (--r < 0) break;  // the zero the new coefficient goes to
+                  }
+                  k++;
+                } while (k <= se);
+                if (sv) {
+                  if (k > se) return ffail(P, "corrupt entropy-coded data (AC refine)");
+                  blk[k] = (int16_t)sv;
+                }
+              }
+            }
+            if (eobrun > 0) {
+              for (; k <= se; k++)
+                if (blk[k] != 0) refine(blk + k);
+              eobrun--;
+            }
+          }
+      }
+    }
+  }
+  if (bits.underrun()) return ffail(P, "truncated or corrupt entropy-coded data");
+  size_t q = (size_t)(bits.p - P.d);
+  while (q + 1 < P.n && !(P.d[q] == 0xFF && P.d[q + 1] != 0x00 &&
+                          !(P.d[q + 1] >= 0xD0 && P.d[q + 1] <= 0xD7)))
+    q++;
+  P.pos = q;
+  return true;
+}
+
+// The finished progressive coefficients as one sequential scan (interleaved
+// over the frame's MCUs for colour, the real blocks for gray) in the packed
+// layout the device decodes.
+bool flatten_progressive(Parser& P, JpegDecoded* out) {
+  JpegHeader& H = out->h;
+  if (P.pc[0].empty()) return ffail(P, "no scan");
+  for (int c = 0; c < P.nf; c++)
+    if (!P.latched[c]) return ffail(P, "a component is missing from the scans");
+  JpegScan& S = H.scan[0];
+  S.ncomp = P.nf;
+  for (int i = 0; i < P.nf; i++) S.comp[i] = i;
+  if (P.nf == 1) {
+    S.mcus_x = (H.comp[0].dw + 7) / 8;
+    S.mcus_y = (H.comp[0].dh + 7) / 8;
+    S.blocks_per_mcu = 1;
+  } else {
+    S.mcus_x = (P.w + 8 * H.hmax - 1) / (8 * H.hmax);
+    S.mcus_y = (P.h + 8 * H.vmax - 1) / (8 * H.vmax);
+    S.blocks_per_mcu = 0;
+    for (int i = 0; i < P.nf; i++) S.blocks_per_mcu += H.comp[i].h * H.comp[i].v;
+    if (S.blocks_per_mcu > 10) return ffail(P, "more than 10 blocks per MCU");
+  }
+  S.first_block = 0;
+  S.first_group = 0;
+  const int64_t nb = (int64_t)S.mcus_x * S.mcus_y * S.blocks_per_mcu;
+  out->counts.resize((size_t)nb);
+  out->coefs.clear();
+  out->groups.clear();
+  int64_t bi = 0;
+  auto put = [&](const int16_t* blk) {
+    int last = 63;
+    while (last >= 0 && blk[last] == 0) last--;
+    out->counts[(size_t)bi++] = (uint8_t)(last + 1);
+    out->coefs.insert(out->coefs.end(), blk, blk + last + 1);
+  };
+  for (int my = 0; my < S.mcus_y; my++) {
+    out->groups.push_back((uint32_t)out->coefs.size());
+    if (out->coefs.size() > 0xF0000000u) return ffail(P, "image too large");
+    for (int mx = 0; mx < S.mcus_x; mx++) {
+      if (P.nf == 1) {
+        put(P.pc[0].data() + ((int64_t)my * H.comp[0].bw + mx) * 64);
+        continue;
+      }
+      for (int c = 0; c < P.nf; c++) {
+        const JpegComp& C = H.comp[c];
+        for (int by = 0; by < C.v; by++)
+          for (int bx = 0; bx < C.h; bx++)
+            put(P.pc[c].data() + (((int64_t)my * C.v + by) * C.bw + (int64_t)mx * C.h + bx) * 64);
+      }
+    }
+  }
+  H.nblocks = nb;
+  H.ngroups = S.mcus_y;
+  H.nscans = 1;
+  return true;
+}
+
 // marker loop; full = false stops after the frame header (probe)
 bool parse(Parser& P, bool full, JpegDecoded* out) {
   if (P.n < 4 || P.d[0] != 0xFF || P.d[1] != 0xD8) return ffail(P, "not a JPEG file");
@@ -462,7 +688,7 @@ bool parse(Parser& P, bool full, JpegDecoded* out) {
   for (;;) {
     const int m = next_marker(P);
     if (m < 0) {
-      if (full && out->h.nscans > 0) break;  // missing EOI: tolerated, as libjpeg
+      if (full && (out->h.nscans > 0 || !P.pc[0].empty())) break;  // missing EOI: tolerated, as libjpeg
       return ffail(P, "unexpected end of file");
     }
     if (m == 0xD9) break;                              // EOI
@@ -484,7 +710,8 @@ bool parse(Parser& P, bool full, JpegDecoded* out) {
       P.restart = be16(b);
     } else if (m == 0xDA) {
       if (!full) return ffail(P, "SOS before SOF");
-      if (!decode_scan(P, b, len, out)) return false;
+      if (!(P.progressive ? decode_prog_scan(P, b, len, out) : decode_scan(P, b, len, out)))
+        return false;
     } else if (m == 0xE0) {
       if (len >= 5 && !memcmp(b, "JFIF", 5)) P.jfif = true;
     } else if (m == 0xEE) {
@@ -540,6 +767,7 @@ bool jpeg_entropy_decode(const uint8_t* d, size_t n, const char* name, JpegDecod
     *out = JpegDecoded();
     Parser P{d, n, name};
     if (!parse(P, true, out)) return false;
+    if (P.progressive && !flatten_progressive(P, out)) return false;
     if (out->h.nscans == 0) return ffail(P, "no scan");
     out->h.color = color_of(P);
     // every component must be covered by a scan

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "filters.h"
+#include "jpeg_enc.h"
 #include "libm_glibc.h"
 #include "runtime.h"
 
@@ -60,6 +61,18 @@ __global__ void k_ctl_init(SheetCtl* ctl, int count, int32_t npoints, UphipPoint
 __global__ void k_status_fold(const SheetCtl* ctl, int count, int32_t* sticky) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s < count && ctl[s].status) atomicOr(sticky, ctl[s].status);
+}
+
+// The encode sources of a batch's output pages: page i = output page i % oc
+// of sheet i / oc, in the plane that holds the sheet (jpeg_enc.h)
+__global__ void k_jenc_sources(const SheetCtl* ctl, const uint8_t* p0, const uint8_t* p1,
+                               int64_t pitch, int64_t stride, int oc, int64_t page_bytes,
+                               JencImage* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int s = i / oc, j = i - s * oc;
+  const uint8_t* base = (ctl[s].cur & 1) ? p1 : p0;
+  out[i] = JencImage{base + (int64_t)s * stride + (int64_t)j * page_bytes, pitch};
 }
 
 __global__ void k_flip_all(SheetCtl* ctl, int count) {
@@ -469,6 +482,9 @@ struct UphipBatch {
   // run 0's i-th block)
   std::vector<void*> cache;
   size_t cache_pos = 0;
+  // GPU JPEG output branch (uphip_batch_encode_jpeg_async)
+  JencContext* jenc = nullptr;
+  int jenc_pages = 0;
 };
 
 namespace {
@@ -1568,6 +1584,7 @@ void uphip_batch_destroy(UphipBatch* b) {
   for (auto& r : b->runs)
     for (auto& m : r) hipEventDestroy(m.second);
   for (void* p : b->allocs) hipFree(p);
+  delete b->jenc;
   if (b->st) hipStreamDestroy(b->st);
   delete b;
 }
@@ -1769,6 +1786,74 @@ int uphip_batch_download_async(UphipBatch* b, void* host, int64_t linesize, int6
     if (!UPH_HIP(hipMemcpy2DAsync(h + s * sheet_stride, linesize, src_of(s), sp, rb, b->out_h,
                                   hipMemcpyDeviceToHost, b->st)))
       return -1;
+  return 0;
+}
+
+// ---- GPU JPEG output branch (sheet_stages.c:554-581) -----------------------
+int uphip_batch_encode_jpeg_async(UphipBatch* b, int32_t quality, int32_t sampling) {
+  if (!b || b->last_count <= 0) return fail("batch_encode_jpeg: nothing to encode"), -1;
+  if (quality == 0) quality = UPHIP_JPEG_DEFAULT_QUALITY;
+  hipSetDevice(b->device);
+  const int oc = b->o.output_count < 1 ? 1 : b->o.output_count;
+  const int n = b->last_count * oc;
+  const int bpp = b->work_fmt == F_GRAY8 ? 1 : 3;
+  const int32_t pw = b->out_w / oc;
+  // bit stream per page: the page's pixel bytes (+64 KiB); pages that do not
+  // fit (noise at high quality) come back as -1 for a single re-encode
+  const int64_t page = (int64_t)pw * b->out_h * bpp + (64 << 10);
+  if (!b->jenc) b->jenc = new JencContext();
+  JencContext& c = *b->jenc;
+  if (!c.setup(pw, b->out_h, b->work_fmt == F_GRAY8 ? UPHIP_FMT_GRAY8 : UPHIP_FMT_RGB24, sampling,
+               quality, n, page / 4, page * n, b->st))
+    return -1;
+  hipLaunchKernelGGL(k_jenc_sources, dim3((n + 255) / 256), dim3(256), 0, b->st, b->ctl,
+                     b->planes[0], b->planes[1], b->pitch, b->plane_stride, oc,
+                     (int64_t)pw * bpp, c.B.images, n);
+  if (!c.encode_async(b->st)) return -1;
+  b->jenc_pages = n;
+  return 0;
+}
+
+int64_t uphip_batch_jpeg_sizes(UphipBatch* b, int64_t* sizes, int32_t max_pages) {
+  if (!b || !b->jenc || b->jenc_pages <= 0) return fail("batch_jpeg_sizes: no encode"), -1;
+  if (uphip_batch_query(b) != 1) return fail("batch_jpeg_sizes: the encode has not finished"), -1;
+  int64_t total = 0;
+  for (int i = 0; i < b->jenc_pages; i++) {
+    const int64_t s = b->jenc->host_sizes[i];
+    if (sizes && i < max_pages) sizes[i] = s < 0 ? -1 : s;
+    if (s > 0) total += s;
+  }
+  return total;
+}
+
+int uphip_batch_jpeg_download_async(UphipBatch* b, void* host, int64_t capacity) {
+  const int64_t total = uphip_batch_jpeg_sizes(b, nullptr, 0);
+  if (total < 0) return -1;
+  if (!host || capacity < total) return fail("batch_jpeg_download: buffer too small"), -1;
+  if (total == 0) return 0;
+  hipSetDevice(b->device);
+  return UPH_HIP(hipMemcpyAsync(host, b->jenc->out, (size_t)total, hipMemcpyDeviceToHost, b->st))
+             ? 0
+             : -1;
+}
+
+int uphip_batch_jpeg_page(UphipBatch* b, int32_t page, const void** device_src, int64_t* pitch,
+                          int32_t* width, int32_t* height, int32_t* format) {
+  const int oc = b && b->o.output_count > 1 ? b->o.output_count : 1;
+  if (!b || page < 0 || page >= b->last_count * oc) return fail("batch_jpeg_page: bad page"), -1;
+  hipSetDevice(b->device);
+  if (!UPH_HIP(hipStreamSynchronize(b->st))) return -1;
+  const int s = page / oc, j = page % oc;
+  int32_t cur = 0;
+  if (!UPH_HIP(hipMemcpy(&cur, &b->ctl[s].cur, 4, hipMemcpyDeviceToHost))) return -1;
+  const int bpp = b->work_fmt == F_GRAY8 ? 1 : 3;
+  const int32_t pw = b->out_w / oc;
+  if (device_src)
+    *device_src = b->planes[cur & 1] + (int64_t)s * b->plane_stride + (int64_t)j * pw * bpp;
+  if (pitch) *pitch = b->pitch;
+  if (width) *width = pw;
+  if (height) *height = b->out_h;
+  if (format) *format = b->work_fmt == F_GRAY8 ? UPHIP_FMT_GRAY8 : UPHIP_FMT_RGB24;
   return 0;
 }
 

@@ -233,6 +233,9 @@ struct UphipSink {
   int64_t linesize = 0, sheet_stride = 0, nsheets = 0;
   std::string pattern;
   int64_t wrap = 0;
+  // JPEG files encoded on the device (uphip_sink_jpeg)
+  bool jpeg = false;
+  int32_t quality = UPHIP_JPEG_DEFAULT_QUALITY, sampling = UPHIP_JPEG_444;
   HostRegistration reg;
 };
 
@@ -360,6 +363,23 @@ UphipSink* uphip_sink_pnm(const char* pattern, int64_t wrap) {
   return k;
 }
 
+UphipSink* uphip_sink_jpeg(const char* pattern, int64_t wrap, int32_t quality, int32_t sampling) {
+  if (!pattern) return fail("sink_jpeg: null pattern"), nullptr;
+  if (quality == 0) quality = UPHIP_JPEG_DEFAULT_QUALITY;
+  if (quality < 1 || quality > 100) return fail("sink_jpeg: quality %d outside 1..100", quality), nullptr;
+  if (sampling < UPHIP_JPEG_444 || sampling > UPHIP_JPEG_420)
+    return fail("sink_jpeg: unknown sampling %d", sampling), nullptr;
+  std::string fmt;
+  if (!output_pattern(pattern, &fmt)) return nullptr;
+  UphipSink* k = new UphipSink();
+  k->pattern = fmt;
+  k->wrap = wrap;
+  k->jpeg = true;
+  k->quality = quality;
+  k->sampling = sampling;
+  return k;
+}
+
 UphipSink* uphip_sink_discard(void) { return new UphipSink(); }
 
 void uphip_sink_destroy(UphipSink* k) { delete k; }
@@ -398,6 +418,10 @@ struct Slot {
   int64_t last_first = -1;  // the chunk whose outputs the batch holds (uphip_runner_slot_chunk)
   int32_t last_count = 0;
   std::vector<char> failed;  // per sheet of the chunk
+  // JPEG sink: the chunk's packed files (pinned) and each page's size / offset
+  uint8_t* hjpg = nullptr;
+  size_t hjpg_cap = 0;
+  std::vector<int64_t> jsize, joff;
 };
 
 struct DeviceCtx {
@@ -493,6 +517,55 @@ void store_sheet(UphipRunner* r, const UphipSink* k, int64_t job, const uint8_t*
       ls = prb;
     }
     if (uphip_pnm_write(path, src, ls, pw, r->out_h, r->out_fmt) != 0) *ok = false;
+  }
+}
+
+std::string sink_path(const UphipSink* k, int64_t idx) {
+  if (k->wrap > 0) idx %= k->wrap;
+  char path[4096];
+  // the pattern holds at most one ll integer conversion (output_pattern)
+#pragma GCC diagnostic push
+#pragma GCC diagnostic ignored "-Wformat-nonliteral"
+  snprintf(path, sizeof(path), k->pattern.c_str(), (long long)idx);
+#pragma GCC diagnostic pop
+  return path;
+}
+
+bool write_file(const std::string& path, const uint8_t* p, size_t n) {
+  FILE* f = fopen(path.c_str(), "wb");
+  if (!f) return fail("sink_jpeg: cannot create %s", path.c_str());
+  const bool ok = fwrite(p, 1, n, f) == n;
+  return (fclose(f) == 0 && ok) || fail("sink_jpeg: cannot write %s", path.c_str());
+}
+
+// The JPEG pages of sheet s of a slot's chunk into their files: from the
+// chunk's packed download, or -- a page the batch's encode buffers could not
+// hold -- encoded again on its own, on the device, from the batch's sheet.
+void store_jpeg_sheet(UphipRunner* r, const UphipSink* k, int device, UphipBatch* b, int64_t job,
+                      int s, const uint8_t* packed, const std::vector<int64_t>& size,
+                      const std::vector<int64_t>& off, bool* ok) {
+  const int oc = r->opts.output_count < 1 ? 1 : r->opts.output_count;
+  for (int j = 0; j < oc; j++) {
+    const int i = s * oc + j;
+    const std::string path = sink_path(k, job * oc + j);
+    if (size[(size_t)i] > 0) {
+      if (!write_file(path, packed + off[(size_t)i], (size_t)size[(size_t)i])) *ok = false;
+      continue;
+    }
+    const void* src = nullptr;
+    int64_t pitch = 0;
+    int32_t w = 0, h = 0, fmt = 0;
+    if (uphip_set_device(device) != 0 ||
+        uphip_batch_jpeg_page(b, i, &src, &pitch, &w, &h, &fmt) != 0) {
+      *ok = false;
+      continue;
+    }
+    const int64_t n = uphip_jpeg_encode(src, pitch, w, h, fmt, k->quality, k->sampling, nullptr, 0);
+    std::vector<uint8_t> file(n > 0 ? (size_t)n : 0);
+    if (n <= 0 ||
+        uphip_jpeg_encode(src, pitch, w, h, fmt, k->quality, k->sampling, file.data(), n) != n ||
+        !write_file(path, file.data(), file.size()))
+      *ok = false;
   }
 }
 
@@ -736,6 +809,7 @@ void uphip_runner_destroy(UphipRunner* r) {
       if (sl.din) hipFree(sl.din);
       if (sl.djpg) hipFree(sl.djpg);
       if (sl.dscr) hipFree(sl.dscr);
+      if (sl.hjpg) hipHostFree(sl.hjpg);
       for (JpegPage& jp : sl.jpg)
         if (jp.host) hipHostFree(jp.host);
     }
@@ -1002,7 +1076,9 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
               if (!UPH_HIP(hipMemcpyAsync(sl->din, src->base + first * nin * src->page_stride, bytes,
                                           hipMemcpyHostToDevice, bst)) ||
                   uphip_batch_run_device(sl->b, sl->count, sl->din, src->linesize,
-                                         src->page_stride) != 0) {
+                                         src->page_stride) != 0 ||
+                  (sink->jpeg &&
+                   uphip_batch_encode_jpeg_async(sl->b, sink->quality, sink->sampling) != 0)) {
                 note("run failed");
                 for (int s = 0; s < sl->count; s++) sl->failed[(size_t)s] |= 1;
                 phase[k] = STORING;
@@ -1042,7 +1118,9 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
           }
           if (st == LOADED && phase[k] == LOADING) {
             if (uphip_batch_upload_async(sl->b, sl->count, sl->hin, r->in_pitch, r->in_page_stride) != 0 ||
-                !jpeg_submit(sl, sl->count * nin) || uphip_batch_run(sl->b, sl->count) != 0) {
+                !jpeg_submit(sl, sl->count * nin) || uphip_batch_run(sl->b, sl->count) != 0 ||
+                (sink->jpeg &&
+                 uphip_batch_encode_jpeg_async(sl->b, sink->quality, sink->sampling) != 0)) {
               note("run failed");
               for (int s = 0; s < sl->count; s++) sl->failed[(size_t)s] |= 1;
               phase[k] = STORING;  // accounted (all failed) on the next pass
@@ -1071,7 +1149,33 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
             for (int s = 0; s < sl->count; s++) clean &= !sl->failed[(size_t)s];
             sl->direct_out = dsnk && clean;
             uint8_t* dst = sl->direct_out ? sink->base + sl->first * sink->sheet_stride : sl->hout;
-            if (uphip_batch_download_async(sl->b, dst, r->out_linesize, r->out_sheet_stride) != 0) {
+            bool queued;
+            if (sink->jpeg) {
+              // only the encoded files come back: sizes (already on the
+              // host), then one copy of the packed files
+              const int npg = sl->count * oc;
+              sl->jsize.assign((size_t)npg, -1);
+              sl->joff.assign((size_t)npg, 0);
+              const int64_t total = uphip_batch_jpeg_sizes(sl->b, sl->jsize.data(), npg);
+              int64_t o = 0;
+              for (int i = 0; i < npg; i++) {
+                sl->joff[(size_t)i] = o;
+                if (sl->jsize[(size_t)i] > 0) o += sl->jsize[(size_t)i];
+              }
+              queued = total >= 0;
+              if (queued && sl->hjpg_cap < (size_t)total) {
+                if (sl->hjpg) hipHostFree(sl->hjpg);
+                sl->hjpg = nullptr;
+                sl->hjpg_cap = 0;
+                const size_t cap = (size_t)total + (size_t)total / 2 + 4096;
+                queued = UPH_HIP(hipHostMalloc((void**)&sl->hjpg, cap, hipHostMallocDefault));
+                if (queued) sl->hjpg_cap = cap;
+              }
+              queued = queued && uphip_batch_jpeg_download_async(sl->b, sl->hjpg, (int64_t)sl->hjpg_cap) == 0;
+            } else {
+              queued = uphip_batch_download_async(sl->b, dst, r->out_linesize, r->out_sheet_stride) == 0;
+            }
+            if (!queued) {
               note("download failed");
               for (int s = 0; s < sl->count; s++) sl->failed[(size_t)s] |= 1;
               inflight.erase(inflight.begin() + (long)q);
@@ -1103,7 +1207,11 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
               dc.pool->submit([&, sl, k, s] {
                 const auto a = Clock::now();
                 bool good = true;
-                store_sheet(r, sink, sl->first + s, sl->hout + (int64_t)s * r->out_sheet_stride, &good);
+                if (sink->jpeg)
+                  store_jpeg_sheet(r, sink, dc.device, sl->b, sl->first + s, s, sl->hjpg, sl->jsize,
+                                   sl->joff, &good);
+                else
+                  store_sheet(r, sink, sl->first + s, sl->hout + (int64_t)s * r->out_sheet_stride, &good);
                 if (!good) {
                   sl->failed[(size_t)s] |= 2;
                   uphip_clear_error();

@@ -53,6 +53,8 @@ EXPORTED = [
     "uphip_runner_output_info", "uphip_runner_batch", "uphip_runner_layout", "uphip_batch_device_bytes", "uphip_host_alloc", "uphip_host_free",
     "uphip_check_libm", "uphip_jpeg_probe", "uphip_jpeg_read", "uphip_jpeg_decode",
     "uphip_jpeg_entropy_decode", "uphip_runner_placement", "uphip_runner_slot_chunk",
+    "uphip_jpeg_encode", "uphip_batch_encode_jpeg_async", "uphip_batch_jpeg_sizes",
+    "uphip_batch_jpeg_download_async", "uphip_batch_jpeg_page", "uphip_sink_jpeg",
     "uphip_detect_rotation_peaks",
 ]
 
@@ -202,6 +204,15 @@ def load_library(path=LIB_PATH):
                                         C.POINTER(A.PnmInfo)]),
         "uphip_jpeg_entropy_decode": (C.c_int64, [C.c_void_p, C.c_size_t, C.c_void_p,
                                                   C.c_int64]),
+        "uphip_jpeg_encode": (C.c_int64, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                          C.c_int32, C.c_int32, C.c_void_p, C.c_int64]),
+        "uphip_batch_encode_jpeg_async": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+        "uphip_batch_jpeg_sizes": (C.c_int64, [C.c_void_p, C.POINTER(C.c_int64), C.c_int32]),
+        "uphip_batch_jpeg_download_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
+        "uphip_batch_jpeg_page": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p),
+                                            C.POINTER(C.c_int64), C.POINTER(C.c_int32),
+                                            C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+        "uphip_sink_jpeg": (C.c_void_p, [C.c_char_p, C.c_int64, C.c_int32, C.c_int32]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(L, name):

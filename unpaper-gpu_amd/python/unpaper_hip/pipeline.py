@@ -98,6 +98,44 @@ class Batch:
             raise UnpaperHipError("batch_get_output failed")
         return out
 
+    def encode_jpeg(self, quality=0, sampling=0):
+        """Queue the GPU JPEG output branch on the last run's pages
+        (uphip_batch_encode_jpeg_async)."""
+        if self.lib.uphip_batch_encode_jpeg_async(self.handle, quality, sampling) != 0:
+            _check(self.lib)
+            raise UnpaperHipError("batch_encode_jpeg failed")
+
+    def jpeg_files(self, pages):
+        """The encoded files of the last encode_jpeg (None for a page the
+        batch's buffers could not hold: uphip_batch_jpeg_page + jpeg_encode)."""
+        L = self.lib
+        self.wait()
+        sizes = (C.c_int64 * pages)()
+        total = L.uphip_batch_jpeg_sizes(self.handle, sizes, pages)
+        _check(L)
+        buf = np.zeros(max(total, 1), np.uint8)
+        if total > 0 and L.uphip_batch_jpeg_download_async(self.handle, buf.ctypes.data, total) != 0:
+            _check(L)
+        self.wait()
+        out, off = [], 0
+        for i in range(pages):
+            n = sizes[i]
+            if n > 0:
+                out.append(buf[off:off + n].tobytes())
+                off += n
+            else:
+                out.append(None)
+        return out
+
+    def jpeg_page(self, page):
+        """(device pointer, pitch, width, height, format) of output page `page`."""
+        src, pitch = C.c_void_p(), C.c_int64()
+        w, h, f = C.c_int32(), C.c_int32(), C.c_int32()
+        if self.lib.uphip_batch_jpeg_page(self.handle, page, C.byref(src), C.byref(pitch),
+                                          C.byref(w), C.byref(h), C.byref(f)) != 0:
+            _check(self.lib)
+        return src.value, pitch.value, w.value, h.value, f.value
+
     def report(self, sheet):
         r = A.SheetReport()
         self.lib.uphip_batch_get_report(self.handle, sheet, C.byref(r))
@@ -293,6 +331,31 @@ def sink_pnm(pattern, wrap=0):
     h = L.uphip_sink_pnm(pattern.encode(), wrap)
     _check(L)
     return _Handle(h, L.uphip_sink_destroy)
+
+
+def sink_jpeg(pattern, wrap=0, quality=0, sampling=0):
+    """JPEG files encoded on the device (uphip_sink_jpeg; quality 0 = 85,
+    sampling 0 = 4:4:4, 1 = 4:2:2, 2 = 4:2:0 for RGB24 sheets)."""
+    L = load_library()
+    h = L.uphip_sink_jpeg(pattern.encode(), wrap, quality, sampling)
+    _check(L)
+    return _Handle(h, L.uphip_sink_destroy)
+
+
+def jpeg_encode(device_ptr, pitch, width, height, fmt, quality=0, sampling=0):
+    """uphip_jpeg_encode: one device image -> JPEG file bytes."""
+    L = load_library()
+    n = L.uphip_jpeg_encode(device_ptr, pitch, width, height, fmt, quality, sampling, None, 0)
+    _check(L)
+    if n <= 0:
+        raise UnpaperHipError("jpeg_encode failed")
+    buf = np.zeros(n, np.uint8)
+    m = L.uphip_jpeg_encode(device_ptr, pitch, width, height, fmt, quality, sampling,
+                            buf.ctypes.data, n)
+    _check(L)
+    if m != n:
+        raise UnpaperHipError("jpeg_encode: size changed between calls")
+    return buf.tobytes()
 
 
 def sink_discard():
