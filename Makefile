@@ -63,8 +63,8 @@ LLVMCC     := /opt/rocm/lib/llvm/bin/clang
 SANFLAGS   := -fsanitize=address,undefined -fno-sanitize-recover=undefined \
               -fno-omit-frame-pointer -g -O1
 
-.PHONY: all lib oracle ctest adapter sanitize libm_check clean
-all: lib oracle ctest libm_check
+.PHONY: all lib oracle ctest adapter sanitize libm_check jdec_emul clean
+all: lib oracle ctest libm_check jdec_emul
 
 lib: $(LIB)
 oracle: $(ORACLE_LIB)
@@ -132,6 +132,14 @@ $(SANITIZE): tests/c/sanitize_main.c oracle/oracle.c oracle/oracle.h $(CSRC)/pnm
 	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
 	  -Iinclude -I$(CSRC) -c $(CSRC)/runtime.hip -o tests/c/_build/san/runtime.o
 	$(HIPCC) $(SANFLAGS) tests/c/_build/san/*.o -o $@ -lm -lz
+
+# the device Huffman decoder's phases replayed on the CPU (test infrastructure)
+JDEC_EMUL  := tests/c/_build/libjdec_emul.so
+jdec_emul: $(JDEC_EMUL)
+$(JDEC_EMUL): tests/c/jdec_emul.cpp $(CSRC)/jpeg_huff_core.h $(CSRC)/jpeg.h $(LIB)
+	@mkdir -p tests/c/_build
+	$(HIPCC) --cuda-host-only -x hip -O2 -std=c++17 -fPIC -shared -Wall -Iinclude -I$(CSRC) $< -o $@ \
+	  -L$(PKG)/lib -lunpaper_hip -Wl,-rpath,'$$ORIGIN/../../../$(PKG)/lib'
 
 sanitize: $(SANITIZE)
 	ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=print_stacktrace=1 $(SANITIZE) $(CURDIR)/tests/c/_build/san $(CURDIR)/tests/golden/reference

@@ -188,7 +188,12 @@ def upsample(h, c, P):
 
 def decode(lib, data: bytes):
     """Pixels (H, W) uint8 or (H, W, 3) uint8 as the device path makes them."""
-    h, P, _ = planes(entropy_decode(lib, data))
+    return decode_packed(entropy_decode(lib, data))
+
+
+def decode_packed(buf):
+    """Pixels from a packed coefficient image (jpeg.h layout)."""
+    h, P, _ = planes(buf)
     if h.ncomp == 1:
         return P[0][:h.height, :h.width].copy()
     c0, c1, c2 = (upsample(h, c, P[c]) for c in range(3))

@@ -88,6 +88,71 @@ def test_host_decoder_with_reference_arithmetic_matches_pil(lib, mode, w, h, kw)
     assert np.array_equal(got, exp), np.count_nonzero(got != exp)
 
 
+def _emulator():
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "_build",
+                        "libjdec_emul.so")
+    if not os.path.exists(path):
+        import subprocess
+        subprocess.check_call(["make", "-s", "jdec_emul"],
+                              cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    E = C.CDLL(path)
+    E.jdec_emulate.restype = C.c_int64
+    E.jdec_emulate.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64,
+                               C.POINTER(C.c_int32)]
+    return E
+
+
+def emulate(data):
+    E = _emulator()
+    passes = C.c_int32()
+    n = E.jdec_emulate(data, len(data), None, 0, C.byref(passes))
+    if n < 0:
+        return n, None, passes.value
+    buf = np.zeros(n, np.uint8)
+    assert E.jdec_emulate(data, len(data), buf.ctypes.data, n, C.byref(passes)) == n
+    return n, buf, passes.value
+
+
+SEQ_CASES = [c for c in CASES if not c[3].get("progressive")] + [
+    ("L", 2480, 400, dict(quality=95)),     # many subsequences, no restarts
+    ("RGB", 640, 480, dict(quality=75, subsampling=2, restart_marker_rows=1)),
+    ("RGB", 333, 211, dict(quality=50, subsampling=1, optimize=True)),
+    ("L", 1, 1, dict(quality=90)),
+    ("L", 8, 8, dict(quality=100)),
+]
+
+
+@pytest.mark.parametrize("mode,w,h,kw", SEQ_CASES)
+def test_device_huffman_decoder_emulated_matches_pil(lib, mode, w, h, kw):
+    """The device entropy decoder's phases (kernels_jpeg_huff.hip) replayed on
+    the CPU (tests/c/jdec_emul.cpp, same code) give PIL's pixels; the
+    subsequence synchronisation converges within its passes."""
+    data = make_jpeg(w, h, mode, seed=w + 1, **kw)
+    n, buf, passes = emulate(data)
+    assert n > 0, n
+    got = jpeg_ref.decode_packed(buf)
+    exp = pil_decode(data)
+    assert np.array_equal(got, exp), np.count_nonzero(got != exp)
+    hdr, _, (counts, groups, off) = jpeg_ref.planes(buf)
+    per = hdr.scan[0].mcus_x * hdr.scan[0].blocks_per_mcu
+    for g in range(hdr.ngroups):
+        assert groups[g] == off[g * per]
+    assert groups[-1] == counts.sum()
+    assert passes >= 1, "no convergence within the sync passes (serial settle)"
+
+
+def test_device_huffman_decoder_emulated_refusals(lib):
+    """Progressive files stay with the host decoder (-2); corrupt data is
+    reported, never silently decoded."""
+    assert emulate(make_jpeg(64, 48, "RGB", quality=90, progressive=True))[0] == -2
+    data = bytearray(make_jpeg(120, 90, "L", quality=90))
+    sos = data.index(b"\xff\xda")
+    for k in range(sos + 20, len(data) - 2, 7):
+        data[k] ^= 0xA5
+    n, _, _ = emulate(bytes(data))
+    assert n < 0
+
+
 def test_packed_layout_group_offsets(lib):
     """The per-MCU-row offsets the device prefix-sums from agree with the
     running count of coefficients (jpeg.h)."""
@@ -171,3 +236,51 @@ def test_device_decode_a4_gray_and_rgb(hip):
         buf.close()
         got = host[:, :2480 * bpp].reshape(exp.shape)
         assert np.array_equal(got, exp), (mode, np.count_nonzero(got != exp))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,w,h,kw", SEQ_CASES)
+def test_device_huffman_decode_matches_pil(hip, tmp_path, mode, w, h, kw):
+    """One-scan sequential files take the device Huffman decoder
+    (kernels_jpeg_huff.hip): pixels equal PIL's."""
+    data = make_jpeg(w, h, mode, seed=w + 1, **kw)
+    exp = pil_decode(data)
+    L = hip.lib
+    from unpaper_hip.pipeline import DeviceBuffer
+    bpp = 1 if mode == "L" else 3
+    pitch = (w * bpp + 255) // 256 * 256
+    buf = DeviceBuffer(pitch * h)
+    try:
+        info = A.PnmInfo()
+        assert L.uphip_jpeg_decode(data, len(data), buf.ptr, pitch, C.byref(info)) == 0, \
+            L.uphip_last_error()
+        host = np.empty((h, pitch), np.uint8)
+        assert L.uphip_memcpy_dtoh(host.ctypes.data, buf.ptr, host.nbytes) == 0
+    finally:
+        buf.close()
+    got = host[:, :w * bpp].reshape(exp.shape)
+    assert np.array_equal(got, exp), np.count_nonzero(got != exp)
+
+
+@pytest.mark.gpu
+def test_device_huffman_decode_corrupt_data_fails_loudly(hip):
+    """Bit errors in the entropy-coded data: the device decoder reports them
+    (uphip_jpeg_decode returns -1 with a message), it never returns pixels
+    silently -- unless the damaged stream still decodes (then it must equal
+    PIL's decode of the same bytes)."""
+    from unpaper_hip.pipeline import DeviceBuffer
+    L = hip.lib
+    data = bytearray(make_jpeg(120, 90, "L", quality=90))
+    sos = data.index(b"\xff\xda")
+    for k in range(sos + 20, len(data) - 2, 7):
+        data[k] ^= 0xA5
+    buf = DeviceBuffer(256 * 90)
+    try:
+        info = A.PnmInfo()
+        rc = L.uphip_jpeg_decode(bytes(data), len(data), buf.ptr, 256, C.byref(info))
+        assert rc == -1
+        assert L.uphip_last_error() is not None
+        L.uphip_clear_error()
+    finally:
+        buf.close()
+

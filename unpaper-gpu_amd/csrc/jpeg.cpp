@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <vector>
 
@@ -191,6 +192,11 @@ struct Parser {
   // its MCU-padded blocks (bw x bh), refined scan after scan
   bool progressive = false;
   std::vector<int16_t> pc[3];
+  // device entropy decoding (jpeg_stream_prepare): the one scan's data is
+  // copied, not decoded; a file that needs more (progressive, more scans)
+  // sets not_device
+  JdecStreamHost* stream = nullptr;
+  bool not_device = false;
 };
 
 bool ffail(const Parser& P, const char* what) {
@@ -681,6 +687,131 @@ bool flatten_progressive(Parser& P, JpegDecoded* out) {
   return true;
 }
 
+// The one scan of a sequential file for the device decoder: scan header,
+// geometry, decode tables, and the entropy-coded data with the byte stuffing
+// and the restart markers removed (each restart segment starts on a byte).
+bool stream_scan(Parser& P, const uint8_t* b, int len) {
+  JdecStreamHost& S = *P.stream;
+  JdecHeader& D = S.hd;
+  JpegHeader& H = D.h;
+  if (!P.have_frame) return ffail(P, "SOS before SOF");
+  if (H.nscans > 0) return P.not_device = true, false;  // several scans: host decoder
+  if (len < 1) return ffail(P, "bad SOS");
+  const int ns = b[0];
+  if (ns < 1 || ns > 4 || len < 4 + 2 * ns) return ffail(P, "bad SOS");
+  if (ns != P.nf) return P.not_device = true, false;  // one scan per component
+  JpegScan& Sc = H.scan[0];
+  for (int i = 0; i < ns; i++) {
+    const int id = b[1 + 2 * i];
+    int c = -1;
+    for (int k = 0; k < P.nf; k++)
+      if (P.cid[k] == id) c = k;
+    if (c < 0) return ffail(P, "scan names an unknown component");
+    Sc.comp[i] = c;
+    D.tdc[i] = b[2 + 2 * i] >> 4;
+    D.tac[i] = b[2 + 2 * i] & 15;
+    if (D.tdc[i] > 3 || D.tac[i] > 3 || !P.dc[D.tdc[i]].present || !P.ac[D.tac[i]].present)
+      return ffail(P, "scan uses a missing Huffman table");
+    if (!P.have_qt[P.tq[c]]) return ffail(P, "component uses a missing quantisation table");
+  }
+  if (b[1 + 2 * ns] != 0 || b[2 + 2 * ns] != 63 || b[3 + 2 * ns] != 0)
+    return ffail(P, "not a sequential scan");
+  frame_geometry(P, &H);
+  for (int i = 0; i < ns; i++)
+    for (int k = 0; k < 64; k++) H.comp[Sc.comp[i]].qzz[k] = P.qt[P.tq[Sc.comp[i]]][k];
+  Sc.ncomp = ns;
+  if (ns == 1) {
+    Sc.mcus_x = (H.comp[Sc.comp[0]].dw + 7) / 8;
+    Sc.mcus_y = (H.comp[Sc.comp[0]].dh + 7) / 8;
+    Sc.blocks_per_mcu = 1;
+    D.bcomp[0] = 0;
+  } else {
+    Sc.mcus_x = (P.w + 8 * H.hmax - 1) / (8 * H.hmax);
+    Sc.mcus_y = (P.h + 8 * H.vmax - 1) / (8 * H.vmax);
+    int nb = 0;
+    for (int i = 0; i < ns; i++) nb += H.comp[Sc.comp[i]].h * H.comp[Sc.comp[i]].v;
+    if (nb > 10) return ffail(P, "more than 10 blocks per MCU");
+    Sc.blocks_per_mcu = 0;
+    for (int i = 0; i < ns; i++)
+      for (int j = 0; j < H.comp[Sc.comp[i]].h * H.comp[Sc.comp[i]].v; j++)
+        D.bcomp[Sc.blocks_per_mcu++] = i;
+  }
+  Sc.first_block = 0;
+  Sc.first_group = 0;
+  H.nblocks = (int64_t)Sc.mcus_x * Sc.mcus_y * Sc.blocks_per_mcu;
+  H.ngroups = Sc.mcus_y;
+  H.nscans = 1;
+  // each block takes at least two bits
+  if (H.nblocks > 4 * (int64_t)(P.n - P.pos) + 64) return ffail(P, "frame larger than the file's data");
+  for (int t = 0; t < 4; t++) {
+    const Huff* src[2] = {&P.dc[t], &P.ac[t]};
+    JdecTable* dst[2] = {&D.dc[t], &D.ac[t]};
+    for (int k = 0; k < 2; k++) {
+      if (!src[k]->present) continue;
+      memcpy(dst[k]->look, src[k]->look, sizeof(dst[k]->look));
+      for (int l = 0; l < 18; l++) dst[k]->maxcode[l] = src[k]->maxcode[l];
+      for (int l = 1; l <= 16; l++) dst[k]->valoff[l] = src[k]->valptr[l] - src[k]->mincode[l];
+      memcpy(dst[k]->vals, src[k]->vals, 256);
+    }
+  }
+  D.restart = P.restart;
+  // unstuff: 0xFF 0x00 -> 0xFF, RSTn -> a new segment, fill bytes skipped,
+  // any other marker ends the data
+  std::vector<uint8_t>& out = S.data;
+  out.clear();
+  out.reserve(P.n - P.pos + 16);
+  S.seg.assign(1, 0);
+  const uint8_t* p = P.d + P.pos;
+  const uint8_t* end = P.d + P.n;
+  while (p < end) {
+    const uint8_t* ff = (const uint8_t*)memchr(p, 0xFF, (size_t)(end - p));
+    if (!ff) {
+      out.insert(out.end(), p, end);
+      p = end;
+      break;
+    }
+    out.insert(out.end(), p, ff);
+    p = ff;
+    if (p + 1 >= end) break;
+    const uint8_t m = p[1];
+    if (m == 0x00) {
+      out.push_back(0xFF);
+      p += 2;
+    } else if (m == 0xFF) {
+      p += 1;  // fill byte
+    } else if (m >= 0xD0 && m <= 0xD7) {
+      S.seg.push_back((int64_t)out.size() * 8);
+      p += 2;
+    } else {
+      break;  // EOI or another marker
+    }
+  }
+  P.pos = (size_t)(p - P.d);
+  const int64_t nbits = (int64_t)out.size() * 8;
+  S.seg.push_back(nbits);
+  D.nseg = (int32_t)S.seg.size() - 1;
+  D.nbits = nbits;
+  const int64_t nmcu = (int64_t)Sc.mcus_x * Sc.mcus_y;
+  if (P.restart) {
+    if ((int64_t)D.nseg != (nmcu + P.restart - 1) / P.restart)
+      return ffail(P, "restart markers do not match the restart interval");
+  } else if (D.nseg != 1) {
+    return ffail(P, "restart marker without a restart interval");
+  }
+  S.segsub.assign((size_t)D.nseg + 1, 0);
+  int64_t nsub = 0;
+  for (int g = 0; g < D.nseg; g++) {
+    S.segsub[(size_t)g] = (int32_t)nsub;
+    const int64_t bits = S.seg[(size_t)g + 1] - S.seg[(size_t)g];
+    nsub += std::max<int64_t>(1, (bits + kJdecSubBits - 1) / kJdecSubBits);
+    if (nsub > 0x7fffffff) return ffail(P, "image too large");
+  }
+  S.segsub[(size_t)D.nseg] = (int32_t)nsub;
+  D.nsub = nsub;
+  out.resize(out.size() + 16, 0);  // slack for the device's word reads
+  return true;
+}
+
 // marker loop; full = false stops after the frame header (probe)
 bool parse(Parser& P, bool full, JpegDecoded* out) {
   if (P.n < 4 || P.d[0] != 0xFF || P.d[1] != 0xD8) return ffail(P, "not a JPEG file");
@@ -688,7 +819,8 @@ bool parse(Parser& P, bool full, JpegDecoded* out) {
   for (;;) {
     const int m = next_marker(P);
     if (m < 0) {
-      if (full && (out->h.nscans > 0 || !P.pc[0].empty())) break;  // missing EOI: tolerated, as libjpeg
+      const bool any = P.stream ? P.stream->hd.h.nscans > 0 : (out->h.nscans > 0 || !P.pc[0].empty());
+      if (full && any) break;  // missing EOI: tolerated, as libjpeg
       return ffail(P, "unexpected end of file");
     }
     if (m == 0xD9) break;                              // EOI
@@ -710,8 +842,12 @@ bool parse(Parser& P, bool full, JpegDecoded* out) {
       P.restart = be16(b);
     } else if (m == 0xDA) {
       if (!full) return ffail(P, "SOS before SOF");
-      if (!(P.progressive ? decode_prog_scan(P, b, len, out) : decode_scan(P, b, len, out)))
+      if (P.stream) {
+        if (P.progressive) return P.not_device = true, false;
+        if (!stream_scan(P, b, len)) return false;
+      } else if (!(P.progressive ? decode_prog_scan(P, b, len, out) : decode_scan(P, b, len, out))) {
         return false;
+      }
     } else if (m == 0xE0) {
       if (len >= 5 && !memcmp(b, "JFIF", 5)) P.jfif = true;
     } else if (m == 0xEE) {
@@ -788,6 +924,39 @@ bool jpeg_entropy_decode(const uint8_t* d, size_t n, const char* name, JpegDecod
   }
 }
 
+int jpeg_stream_prepare(const uint8_t* d, size_t n, const char* name, JdecStreamHost* out) {
+  try {
+    out->hd = JdecHeader{};
+    std::unique_ptr<Parser> P(new Parser{d, n, name});
+    P->stream = out;
+    if (!parse(*P, true, nullptr)) return P->not_device ? 0 : -1;
+    if (out->hd.h.nscans == 0) return ffail(*P, "no scan"), -1;
+    JdecHeader& D = out->hd;
+    JpegHeader& H = D.h;
+    H.color = color_of(*P);
+    // the packed layout the device writes (upper bound: 64 coefficients a block)
+    H.counts_off = align16((int64_t)sizeof(JpegHeader));
+    H.groups_off = align16(H.counts_off + H.nblocks);
+    H.coefs_off = align16(H.groups_off + 4 * (H.ngroups + 1));
+    H.total_bytes = align16(H.coefs_off + 2 * 64 * H.nblocks);
+    D.seg_off = align16((int64_t)sizeof(JdecHeader));
+    D.segsub_off = align16(D.seg_off + 8 * (int64_t)out->seg.size());
+    D.data_off = align16(D.segsub_off + 4 * (int64_t)out->segsub.size());
+    D.total_bytes = align16(D.data_off + (int64_t)out->data.size());
+    return 1;
+  } catch (const std::bad_alloc&) {
+    return fail("jpeg: %s: out of memory", name), -1;
+  }
+}
+
+void jpeg_stream_pack(const JdecStreamHost& s, uint8_t* dst) {
+  const JdecHeader& D = s.hd;
+  memcpy(dst, &D, sizeof(D));
+  memcpy(dst + D.seg_off, s.seg.data(), 8 * s.seg.size());
+  memcpy(dst + D.segsub_off, s.segsub.data(), 4 * s.segsub.size());
+  memcpy(dst + D.data_off, s.data.data(), s.data.size());
+}
+
 void jpeg_pack(const JpegDecoded& j, uint8_t* dst) {
   const JpegHeader& H = j.h;
   memset(dst, 0, (size_t)H.total_bytes);
@@ -807,9 +976,13 @@ namespace uph {
 // into device memory (synchronous).
 bool jpeg_decode_to_device(const uint8_t* data, size_t size, const char* name, uint8_t* ddst,
                            int64_t pitch, UphipPnmInfo* info) {
+  // one-scan sequential files: Huffman decoding on the device too
+  JdecStreamHost S;
+  const int dev = jpeg_stream_prepare(data, size, name, &S);
+  if (dev < 0) return false;
   JpegDecoded j;
-  if (!jpeg_entropy_decode(data, size, name, &j)) return false;
-  const JpegHeader& H = j.h;
+  if (!dev && !jpeg_entropy_decode(data, size, name, &j)) return false;
+  const JpegHeader& H = dev ? S.hd.h : j.h;
   const int fmt = H.ncomp == 1 ? UPHIP_FMT_GRAY8 : UPHIP_FMT_RGB24;
   if (info) {
     if (info->width > 0 && (info->width != H.width || info->height != H.height || info->format != fmt))
@@ -820,14 +993,31 @@ bool jpeg_decode_to_device(const uint8_t* data, size_t size, const char* name, u
     info->format = fmt;
   }
   if (pitch < (int64_t)H.width * (H.ncomp == 1 ? 1 : 3)) return fail("jpeg: pitch too small");
-  std::vector<uint8_t> packed((size_t)H.total_bytes);
-  jpeg_pack(j, packed.data());
   hipStream_t st = current_stream();
   uint8_t* dp = (uint8_t*)scratch(0, (size_t)H.total_bytes);
   uint8_t* ds = H.scratch_bytes ? (uint8_t*)scratch(1, (size_t)H.scratch_bytes) : nullptr;
   if (!dp || (H.scratch_bytes && !ds)) return false;
-  return UPH_HIP(hipMemcpyAsync(dp, packed.data(), packed.size(), hipMemcpyHostToDevice, st)) &&
-         jpeg_launch(H, dp, ds, ddst, pitch, st) && UPH_HIP(hipStreamSynchronize(st));
+  if (!dev) {
+    std::vector<uint8_t> packed((size_t)H.total_bytes);
+    jpeg_pack(j, packed.data());
+    return UPH_HIP(hipMemcpyAsync(dp, packed.data(), packed.size(), hipMemcpyHostToDevice, st)) &&
+           jpeg_launch(H, dp, ds, ddst, pitch, st) && UPH_HIP(hipStreamSynchronize(st));
+  }
+  std::vector<uint8_t> up((size_t)S.hd.total_bytes);
+  jpeg_stream_pack(S, up.data());
+  uint8_t* dstream = (uint8_t*)scratch(3, up.size());
+  uint8_t* dscr = (uint8_t*)scratch(4, jdec_scratch_bytes(S.hd));
+  int32_t* dstatus = (int32_t*)scratch(5, 4);
+  int32_t status = 0;
+  if (!dstream || !dscr || !dstatus ||
+      !UPH_HIP(hipMemsetAsync(dstatus, 0, 4, st)) ||
+      !UPH_HIP(hipMemcpyAsync(dstream, up.data(), up.size(), hipMemcpyHostToDevice, st)) ||
+      !jdec_launch(S.hd, dstream, dp, dscr, dstatus, st) || !jpeg_launch(H, dp, ds, ddst, pitch, st) ||
+      !UPH_HIP(hipMemcpyAsync(&status, dstatus, 4, hipMemcpyDeviceToHost, st)) ||
+      !UPH_HIP(hipStreamSynchronize(st)))
+    return false;
+  if (status) return fail("jpeg: %s: corrupt entropy-coded data (device decode, 0x%x)", name, status);
+  return true;
 }
 
 }  // namespace uph

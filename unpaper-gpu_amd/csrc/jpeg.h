@@ -78,6 +78,67 @@ constexpr uint8_t kJpegNatural[64] = {
     35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
     58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
+// ---------------------------------------------------------------------------
+// Device entropy decoding (kernels_jpeg_huff.hip).  For a sequential file
+// with one scan the host only parses the markers and copies the entropy-coded
+// data with the byte stuffing and restart markers removed; the device decodes
+// the Huffman codes itself, in parallel over fixed-size subsequences of the
+// bit stream that synchronise by iteration (a decoder started at an arbitrary
+// bit falls into step with the true code boundaries after a few codes, and
+// the iteration carries each subsequence's exact exit state to the next until
+// none changes), then writes the packed layout above for the IDCT kernel.
+// Progressive and multi-scan files keep the host entropy decoder.
+// ---------------------------------------------------------------------------
+constexpr int kJdecSubBits = 8192;  // subsequence length (1 KiB of data)
+constexpr int kJdecLook = 10;        // lookahead bits of the decode tables (jpeg.cpp kLook)
+
+struct JdecTable {
+  uint16_t look[1 << kJdecLook];     // len << 8 | symbol, 0 = a longer code
+  int32_t maxcode[18];               // largest code of each length, -1 if none; [17] sentinel
+  int32_t valoff[17];                // vals index of code c of length l: c + valoff[l]
+  uint8_t vals[256];
+};
+
+// The uploaded stream: JdecHeader | segment start bits (int64, nseg + 1) |
+// segment subsequence prefix (int32, nseg + 1) | data (unstuffed, 16 zero
+// bytes of slack).  h describes the frame, its one scan and the offsets of
+// the packed layout the device writes (upper bound of 64 coefficients a block).
+struct JdecHeader {
+  JpegHeader h;
+  int32_t restart;        // MCUs per restart interval (0: none)
+  int32_t nseg;           // restart segments (>= 1)
+  int64_t nsub;           // subsequences
+  int64_t nbits;          // data bits
+  int32_t tdc[4], tac[4]; // table slots of the scan's components
+  int32_t bcomp[10];      // scan component of each block of an MCU
+  JdecTable dc[4], ac[4];
+  int64_t seg_off, segsub_off, data_off, total_bytes;
+};
+
+struct JdecStreamHost {
+  JdecHeader hd{};
+  std::vector<int64_t> seg;     // segment start bits, + the end
+  std::vector<int32_t> segsub;  // subsequences before each segment, + the total
+  std::vector<uint8_t> data;
+};
+
+// Marker parse + unstuffing for the device decoder.  Returns 1 when the file
+// is a one-scan sequential JPEG (out filled), 0 when it needs the host
+// entropy decoder (progressive or several scans; no error set), -1 on error.
+int jpeg_stream_prepare(const uint8_t* data, size_t size, const char* name, JdecStreamHost* out);
+// Writes the uploaded layout (hd.total_bytes bytes).
+void jpeg_stream_pack(const JdecStreamHost& s, uint8_t* dst);
+// Device scratch of the decode phases for one image.
+size_t jdec_scratch_bytes(const JdecHeader& hd);
+// One image: the stream at `dstream` (device copy of jpeg_stream_pack's
+// bytes), its header `hd`, into the packed coefficient layout at `dpacked`
+// (hd.h.total_bytes), using `scratch` (jdec_scratch_bytes), on stream st;
+// jpeg_launch then turns the packed layout into pixels.
+// A corrupt stream (an invalid code, a coefficient past 63, segments or
+// blocks that do not add up) sets *dstatus (device int32) non-zero.
+bool jdec_launch(const JdecHeader& hd, const uint8_t* dstream, uint8_t* dpacked, uint8_t* scratch,
+                 int32_t* dstatus, hipStream_t st);
+
 // Host half: a decoded file's coefficients before packing.
 struct JpegDecoded {
   JpegHeader h{};

@@ -398,6 +398,8 @@ struct JpegPage {
   uint8_t* host = nullptr;  // pinned, grown on demand
   size_t cap = 0;
   bool on = false;          // this chunk's page is a JPEG waiting for the device
+  bool dev = false;         // Huffman-decoded on the device (host holds a JdecHeader stream)
+  size_t bytes = 0;         // bytes to upload
   JpegHeader h{};
 };
 
@@ -407,6 +409,13 @@ struct Slot {
   size_t djpg_cap = 0;
   uint8_t* dscr = nullptr;    // colour planes (one page at a time on the stream)
   size_t dscr_cap = 0;
+  uint8_t* djpk = nullptr;    // packed coefficients of a device-decoded page (one at a time)
+  size_t djpk_cap = 0;
+  uint8_t* djsc = nullptr;    // device Huffman scratch (one page at a time)
+  size_t djsc_cap = 0;
+  int32_t* djst = nullptr;    // per page: device Huffman status
+  int djst_cap = 0;
+  bool jdev = false;          // the chunk has device-decoded pages (statuses to read)
   UphipBatch* b = nullptr;
   uint8_t* hin = nullptr;   // pinned input staging (count * input_count pages)
   uint8_t* hout = nullptr;  // pinned output staging (count sheets)
@@ -591,11 +600,17 @@ bool jpeg_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp
     return fail("jpeg: %s is %dx%d format %d, expected %dx%d format %d", path.c_str(), info.width,
                 info.height, info.format, r->geo.page_width, r->geo.page_height,
                 r->geo.page_format);
+  // a one-scan sequential file goes to the device as its unstuffed entropy
+  // data (Huffman decoding there too); progressive / multi-scan files are
+  // entropy-decoded here
+  JdecStreamHost S;
+  const int dev = jpeg_stream_prepare(file.data(), file.size(), path.c_str(), &S);
+  if (dev < 0) return false;
   JpegDecoded d;
-  if (!jpeg_entropy_decode(file.data(), file.size(), path.c_str(), &d)) return false;
+  if (!dev && !jpeg_entropy_decode(file.data(), file.size(), path.c_str(), &d)) return false;
   // pinned memory for this device (the pool thread may have another current)
   if (uphip_set_device(device) != 0) return false;
-  const size_t need = (size_t)d.h.total_bytes;
+  const size_t need = (size_t)(dev ? S.hd.total_bytes : d.h.total_bytes);
   if (jp->cap < need) {
     if (jp->host) hipHostFree(jp->host);
     jp->host = nullptr;
@@ -603,8 +618,13 @@ bool jpeg_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp
     if (!UPH_HIP(hipHostMalloc((void**)&jp->host, need + need / 4, hipHostMallocDefault))) return false;
     jp->cap = need + need / 4;
   }
-  jpeg_pack(d, jp->host);
-  jp->h = d.h;
+  if (dev)
+    jpeg_stream_pack(S, jp->host);
+  else
+    jpeg_pack(d, jp->host);
+  jp->h = dev ? S.hd.h : d.h;
+  jp->dev = dev == 1;
+  jp->bytes = need;
   jp->on = true;
   return true;
 }
@@ -623,14 +643,38 @@ bool load_page(UphipRunner* r, int device, const UphipSource* s, int64_t job, in
 // Queue the chunk's JPEG pages on the slot's stream: upload each packed page,
 // then decode it into its input slot (after the staging upload, before the run).
 bool jpeg_submit(Slot* sl, int npages) {
-  size_t total = 0, scr = 0;
+  size_t total = 0, scr = 0, pk = 0, hs = 0;
+  sl->jdev = false;
   for (int p = 0; p < npages; p++) {
     const JpegPage& jp = sl->jpg[(size_t)p];
     if (!jp.on) continue;
-    total += (size_t)jp.h.total_bytes;
+    total += jp.bytes;
     scr = std::max(scr, (size_t)jp.h.scratch_bytes);
+    if (jp.dev) {
+      sl->jdev = true;
+      pk = std::max(pk, (size_t)jp.h.total_bytes);
+      hs = std::max(hs, jdec_scratch_bytes(*(const JdecHeader*)jp.host));
+    }
   }
   if (!total) return true;
+  auto grow = [](auto** p, size_t* cap, size_t need) -> bool {
+    if (*cap >= need) return true;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (!UPH_HIP(hipMalloc((void**)p, need))) return false;
+    *cap = need;
+    return true;
+  };
+  if (sl->jdev) {
+    size_t stcap = (size_t)sl->djst_cap;
+    if (!grow(&sl->djpk, &sl->djpk_cap, pk) || !grow(&sl->djsc, &sl->djsc_cap, hs) ||
+        !grow(&sl->djst, &stcap, 4 * (size_t)npages))
+      return false;
+    sl->djst_cap = (int)(stcap / 4);
+    if (!UPH_HIP(hipMemsetAsync(sl->djst, 0, 4 * (size_t)npages, (hipStream_t)uphip_batch_stream(sl->b))))
+      return false;
+  }
   // the slot's stream is idle here (the slot was free): old buffers can go
   if (sl->djpg_cap < total) {
     if (sl->djpg) hipFree(sl->djpg);
@@ -653,12 +697,17 @@ bool jpeg_submit(Slot* sl, int npages) {
     if (!jp.on) continue;
     int64_t pitch = 0;
     uint8_t* dst = (uint8_t*)uphip_batch_input_ptr(sl->b, p, &pitch);
-    if (!dst ||
-        !UPH_HIP(hipMemcpyAsync(sl->djpg + off, jp.host, (size_t)jp.h.total_bytes,
-                                hipMemcpyHostToDevice, st)) ||
-        !jpeg_launch(jp.h, sl->djpg + off, sl->dscr, dst, pitch, st))
+    if (!dst || !UPH_HIP(hipMemcpyAsync(sl->djpg + off, jp.host, jp.bytes, hipMemcpyHostToDevice, st)))
       return false;
-    off += (size_t)jp.h.total_bytes;
+    if (jp.dev) {  // Huffman decoding into the slot's packed buffer, then pixels
+      if (!jdec_launch(*(const JdecHeader*)jp.host, sl->djpg + off, sl->djpk, sl->djsc, sl->djst + p,
+                       st) ||
+          !jpeg_launch(jp.h, sl->djpk, sl->dscr, dst, pitch, st))
+        return false;
+    } else if (!jpeg_launch(jp.h, sl->djpg + off, sl->dscr, dst, pitch, st)) {
+      return false;
+    }
+    off += jp.bytes;
   }
   return true;
 }
@@ -809,6 +858,9 @@ void uphip_runner_destroy(UphipRunner* r) {
       if (sl.din) hipFree(sl.din);
       if (sl.djpg) hipFree(sl.djpg);
       if (sl.dscr) hipFree(sl.dscr);
+      if (sl.djpk) hipFree(sl.djpk);
+      if (sl.djsc) hipFree(sl.djsc);
+      if (sl.djst) hipFree(sl.djst);
       if (sl.hjpg) hipHostFree(sl.hjpg);
       for (JpegPage& jp : sl.jpg)
         if (jp.host) hipHostFree(jp.host);
@@ -1066,6 +1118,7 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
               continue;
             }
             sl->first = first;
+            sl->jdev = false;
             sl->count = (int32_t)std::min<int64_t>(S, njobs - first);
             sl->failed.assign((size_t)sl->count, 0);
             sl->last_first = first;
@@ -1143,6 +1196,16 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
             std::vector<char> pre = sl->failed;
             collect_failures(*sl);  // the stream is idle: a status read only
             for (size_t s = 0; s < pre.size(); s++) sl->failed[s] |= pre[s];
+            if (sl->jdev) {  // pages whose entropy-coded data the device found corrupt
+              std::vector<int32_t> jst((size_t)(sl->count * nin), 0);
+              if (!UPH_HIP(hipMemcpy(jst.data(), sl->djst, 4 * jst.size(), hipMemcpyDeviceToHost)))
+                jst.assign(jst.size(), 1);
+              for (size_t q = 0; q < jst.size(); q++)
+                if (jst[q]) {
+                  sl->failed[q / (size_t)nin] |= 4;
+                  if (dc.error.empty()) dc.error = "corrupt JPEG entropy-coded data (device decode)";
+                }
+            }
             // straight into a memory sink unless a sheet failed (its slot in
             // the sink stays untouched, as with the store tasks)
             bool clean = true;
