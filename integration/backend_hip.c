@@ -20,6 +20,8 @@
 #include "backend_hip.h"
 
 #include <stddef.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "unpaper_hip.h"
@@ -287,3 +289,30 @@ void deskew_hip(Image source, Rectangle mask, float radians, Interpolation inter
                (UphipInterpolation)interpolate_type);
   wrote(source);
 }
+
+/* The GPU output branch (sheet_stages.c:554-581 -> encode_queue_submit_gpu,
+ * lib/encode_queue.c:860-990): the sheet's device copy encoded as a JPEG
+ * file, the peer of nvimgcodec_encode_to_file (nvimgcodec.c:1164-1200).
+ * quality 0 = 85 (lib/options.h:42).  GRAY8 sheets give one component,
+ * RGB24 sheets YCbCr 4:4:4. */
+bool backend_hip_encode_to_file(Image *image, int quality, const char *filename) {
+  const UphipImage d = dev(*image);
+  const void *src = uphip_image_device_ptr(d);
+  const int64_t pitch = uphip_image_device_pitch(d);
+  const UphipRectangleSize sz = uphip_size_of_image(d);
+  const UphipPixelFormat fmt = uphip_image_format(d);
+  if (!src || (fmt != UPHIP_FMT_GRAY8 && fmt != UPHIP_FMT_RGB24)) return false;
+  const int64_t n = uphip_jpeg_encode(src, pitch, sz.width, sz.height, fmt, quality,
+                                      UPHIP_JPEG_444, NULL, 0);
+  if (n <= 0) return false;
+  uint8_t *buf = malloc((size_t)n);
+  if (!buf) return false;
+  bool ok = uphip_jpeg_encode(src, pitch, sz.width, sz.height, fmt, quality, UPHIP_JPEG_444,
+                              buf, n) == n;
+  FILE *f = ok ? fopen(filename, "wb") : NULL;
+  ok = f && fwrite(buf, 1, (size_t)n, f) == (size_t)n;
+  if (f && fclose(f) != 0) ok = false;
+  free(buf);
+  return ok;
+}
+

@@ -48,3 +48,5 @@ void backend_hip_mark_cpu_dirty(Image *image);
 void backend_hip_mark_gpu_dirty(Image *image);
 /* Free the device copy a frame's state owns (from the state's free). */
 void backend_hip_release(HipState *st);
+/* nvimgcodec_encode_to_file's peer for the GPU output branch (JPEG). */
+bool backend_hip_encode_to_file(Image *image, int quality, const char *filename);

@@ -16,6 +16,7 @@
  * check equal, 2 = no HIP device.
  */
 #include <stdio.h>
+#include <unistd.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -311,6 +312,25 @@ static void run_format(int fmt, const UphipOptions *o) {
     o_deskew(h, um, rad, UPHIP_INTERP_CUBIC);
     deskew_hip(im, CP(Rectangle, um), rad, INTERP_CUBIC);
     compare("deskew", h, &im);
+  }
+  if (fmt == UPHIP_FMT_GRAY8 || fmt == UPHIP_FMT_RGB24) {
+    /* the GPU output branch (nvimgcodec_encode_to_file's peer): the file
+     * equals the oracle's encode of the same (compared) pixels */
+    char path[128];
+    snprintf(path, sizeof path, "/tmp/adapter_ops_%d_%d.jpg", (int)getpid(), fmt);
+    const bool ok = backend_hip_encode_to_file(&im, 85, path);
+    api_error("encode_to_file");
+    const int64_t cap = (int64_t)h.width * h.height * 8 + 65536;
+    uint8_t *exp = malloc((size_t)cap), *got = malloc((size_t)cap);
+    const int64_t ne = o_jpeg_encode(h.data, h.linesize, h.width, h.height, fmt, 85, 0, exp, cap);
+    FILE *f = ok ? fopen(path, "rb") : NULL;
+    const int64_t ng = f ? (int64_t)fread(got, 1, (size_t)cap, f) : -1;
+    if (f) fclose(f);
+    remove(path);
+    check_int("encode_to_file", fmt, ne, ng, "file size");
+    check_int("encode_to_file", fmt, 0, ng == ne ? memcmp(exp, got, (size_t)ne) != 0 : 1, "bytes");
+    free(exp);
+    free(got);
   }
   o_free_image(&h);
   free_img(&im);
