@@ -399,7 +399,9 @@ int uphip_batch_output_info(UphipBatch *batch, int32_t *width, int32_t *height,
  * pitch in bytes.  Caller may write input pages there directly (device-side
  * decode / pre-staged inputs). */
 void *uphip_batch_input_ptr(UphipBatch *batch, int32_t slot, int64_t *pitch);
-/* Host → device copy of one page (async on the batch stream). */
+/* Host → device copy of one page (async on the batch stream: `host` must
+ * stay valid until the stream has passed the copy, i.e. until
+ * uphip_batch_wait or uphip_batch_query() == 1). */
 int uphip_batch_set_input(UphipBatch *batch, int32_t slot, const void *host,
                           int64_t linesize);
 /* Run the pipeline on sheets [0, count) whose pages sit in the batch's input

@@ -241,7 +241,7 @@ def test_batch_encode_overflow_reencodes(hip, oracle):
     buffers) gives PIL's bytes."""
     from unpaper_hip.pipeline import Batch, jpeg_encode
     from unpaper_hip.hostimage import HostImage
-    w, h = 200, 160
+    w, h = 640, 480  # ~6 Mbit of codes against a 3 Mbit buffer (pixels + 64 KiB)
     opts = oracle.default_options()
     opts.disable = A.NO_PROCESSING
     rng = np.random.default_rng(5)

@@ -68,6 +68,10 @@ class Batch:
     def set_input(self, sheet, page_index, h: HostImage):
         slot = sheet * self.options.input_count + page_index
         arr = np.ascontiguousarray(h.data)
+        # the copy is asynchronous on the batch stream: the source must live
+        # until the stream has passed it (released by wait())
+        self._inputs = getattr(self, "_inputs", {})
+        self._inputs[slot] = arr
         if self.lib.uphip_batch_set_input(self.handle, slot, arr.ctypes.data, arr.shape[1]) != 0:
             _check(self.lib)
 
@@ -85,6 +89,7 @@ class Batch:
 
     def wait(self):
         rc = self.lib.uphip_batch_wait(self.handle)
+        self._inputs = {}
         _check(self.lib)
         if rc != 0:
             raise UnpaperHipError("batch_wait failed")
