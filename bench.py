@@ -446,7 +446,7 @@ def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid):
     PIL's decode of the same files."""
     from PIL import Image
     from concurrent.futures import ThreadPoolExecutor
-    n = args.pages or 128
+    n = args.pages or 512
     threads = host_threads_share()
     tmpdir = tempfile.mkdtemp(prefix="uphip_jpeg_",
                               dir="/dev/shm" if os.path.isdir("/dev/shm") else None)

@@ -31,17 +31,25 @@ int64_t jdec_emulate(const uint8_t* file, size_t n, uint8_t* out, int64_t cap, i
   jpeg_stream_pack(S, stream.data());
   const JdecHeader& hd = S.hd;
   std::vector<uint8_t> scratch(jdec_scratch_bytes(hd) + 256);
-  const Ctx c = ctx_of(stream.data());
-  const JdecScratch X = carve(scratch.data(), hd.nsub);
-  const JdecTable* dct[3];
-  const JdecTable* act[3];
+  const JdecScratch X = carve(scratch.data(), hd.nsub, hd.nmac);
   JdecTable dtab[3], atab[3];
+  int8_t bcomp[12] = {};
   for (int i = 0; i < hd.h.scan[0].ncomp; i++) {
     dtab[i] = hd.dc[hd.tdc[i]];
     atab[i] = hd.ac[hd.tac[i]];
   }
-  (void)dct;
-  (void)act;
+  for (int i = 0; i < 10; i++) bcomp[i] = (int8_t)hd.bcomp[i];
+  const uint8_t* base = stream.data();
+  Dec d;
+  d.dct = dtab;
+  d.act = atab;
+  d.bcomp = bcomp;
+  d.bpm = hd.h.scan[0].blocks_per_mcu;
+  d.nseg = hd.nseg;
+  d.seg = (const int64_t*)(base + hd.seg_off);
+  d.segsub = (const int32_t*)(base + hd.segsub_off);
+  d.segmac = (const int32_t*)(base + hd.segmac_off);
+  d.data = (const uint32_t*)(base + hd.data_off);
   int32_t status = 0;
   // k_jdec_sync
   memset(X.changed, 0, 4 * (kSyncPasses + 2));
@@ -50,7 +58,7 @@ int64_t jdec_emulate(const uint8_t* file, size_t n, uint8_t* out, int64_t cap, i
     for (int p = 1; p < pass; p++)
       if (X.changed[p] == 0) skip = true;
     if (skip) continue;
-    for (int64_t i = 0; i < hd.nsub; i++) sync_sub(c, dtab, atab, X, i, pass);
+    for (int64_t m = 0; m < hd.nmac; m++) sync_macro(d, X, m, pass);
   }
   // k_jdec_settle
   *passes = 0;
@@ -62,23 +70,15 @@ int64_t jdec_emulate(const uint8_t* file, size_t n, uint8_t* out, int64_t cap, i
       conv = true;
     }
   if (!conv) {
-    const int fb = kSyncPasses & 1;
-    JdecState prev{0, 0};
-    for (int64_t i = 0; i < hd.nsub; i++) {
-      const Sub s = sub_of(c, i);
-      const JdecState st = s.first ? JdecState{s.start, 0} : prev;
-      prev = run_to(c, dtab, atab, st, s.stop, s.seg_end);
-      X.xpos[fb][i] = prev.pos;
-      X.xbk[fb][i] = prev.bk;
-    }
-    *X.final_buf = fb;
+    settle_serial(d, X, kSyncPasses & 1);
+    *X.final_buf = kSyncPasses & 1;
   }
   // k_jdec_count
   for (int64_t i = 0; i < hd.nsub; i++) {
     int32_t nb = 0, dc[3] = {0, 0, 0}, diff = 0;
     int64_t nc = 0;
     const bool ok = walk_owned(
-        c, dtab, atab, X, i, [&](int, int zz, int val, int) { if (zz == 0) diff = val; },
+        d, X, i, [&](int, int zz, int val, int) { if (zz == 0) diff = val; },
         [&](int b, int last) {
           nb++;
           nc += last + 1;
@@ -107,8 +107,8 @@ int64_t jdec_emulate(const uint8_t* file, size_t n, uint8_t* out, int64_t cap, i
     const int bpm = hd.h.scan[0].blocks_per_mcu;
     std::vector<int32_t> pre(X.dcpre, X.dcpre + 3 * hd.nsub);
     for (int64_t i = 0; i < hd.nsub; i++) {
-      const int g = seg_of(c, i);
-      const int64_t f = c.segsub[g];
+      const int g = seg_search(d.segsub, d.nseg, i);
+      const int64_t f = d.segsub[g];
       if (i == f && hd.restart && X.blkoff[i] != (int64_t)g * hd.restart * bpm) status |= 2;
       for (int k = 0; k < 3; k++) X.dcpre[3 * i + k] = pre[3 * i + k] - pre[3 * f + k];
     }
@@ -124,7 +124,7 @@ int64_t jdec_emulate(const uint8_t* file, size_t n, uint8_t* out, int64_t cap, i
     int64_t blk = X.blkoff[i], co = X.coefoff[i];
     int pred[3] = {X.dcpre[3 * i], X.dcpre[3 * i + 1], X.dcpre[3 * i + 2]};
     const bool ok = walk_owned(
-        c, dtab, atab, X, i,
+        d, X, i,
         [&](int cb, int zz, int val, int last) {
           if (blk >= hd.h.nblocks) return;
           if (zz == 0) {

@@ -799,15 +799,21 @@ bool stream_scan(Parser& P, const uint8_t* b, int len) {
     return ffail(P, "restart marker without a restart interval");
   }
   S.segsub.assign((size_t)D.nseg + 1, 0);
-  int64_t nsub = 0;
+  S.segmac.assign((size_t)D.nseg + 1, 0);
+  int64_t nsub = 0, nmac = 0;
   for (int g = 0; g < D.nseg; g++) {
     S.segsub[(size_t)g] = (int32_t)nsub;
+    S.segmac[(size_t)g] = (int32_t)nmac;
     const int64_t bits = S.seg[(size_t)g + 1] - S.seg[(size_t)g];
-    nsub += std::max<int64_t>(1, (bits + kJdecSubBits - 1) / kJdecSubBits);
+    const int64_t k = std::max<int64_t>(1, (bits + kJdecSubBits - 1) / kJdecSubBits);
+    nsub += k;
+    nmac += (k + kJdecMacro - 1) / kJdecMacro;
     if (nsub > 0x7fffffff) return ffail(P, "image too large");
   }
   S.segsub[(size_t)D.nseg] = (int32_t)nsub;
+  S.segmac[(size_t)D.nseg] = (int32_t)nmac;
   D.nsub = nsub;
+  D.nmac = nmac;
   out.resize(out.size() + 16, 0);  // slack for the device's word reads
   return true;
 }
@@ -941,7 +947,8 @@ int jpeg_stream_prepare(const uint8_t* d, size_t n, const char* name, JdecStream
     H.total_bytes = align16(H.coefs_off + 2 * 64 * H.nblocks);
     D.seg_off = align16((int64_t)sizeof(JdecHeader));
     D.segsub_off = align16(D.seg_off + 8 * (int64_t)out->seg.size());
-    D.data_off = align16(D.segsub_off + 4 * (int64_t)out->segsub.size());
+    D.segmac_off = align16(D.segsub_off + 4 * (int64_t)out->segsub.size());
+    D.data_off = align16(D.segmac_off + 4 * (int64_t)out->segmac.size());
     D.total_bytes = align16(D.data_off + (int64_t)out->data.size());
     return 1;
   } catch (const std::bad_alloc&) {
@@ -954,6 +961,7 @@ void jpeg_stream_pack(const JdecStreamHost& s, uint8_t* dst) {
   memcpy(dst, &D, sizeof(D));
   memcpy(dst + D.seg_off, s.seg.data(), 8 * s.seg.size());
   memcpy(dst + D.segsub_off, s.segsub.data(), 4 * s.segsub.size());
+  memcpy(dst + D.segmac_off, s.segmac.data(), 4 * s.segmac.size());
   memcpy(dst + D.data_off, s.data.data(), s.data.size());
 }
 
@@ -1006,7 +1014,7 @@ bool jpeg_decode_to_device(const uint8_t* data, size_t size, const char* name, u
   std::vector<uint8_t> up((size_t)S.hd.total_bytes);
   jpeg_stream_pack(S, up.data());
   uint8_t* dstream = (uint8_t*)scratch(3, up.size());
-  uint8_t* dscr = (uint8_t*)scratch(4, jdec_scratch_bytes(S.hd));
+  uint8_t* dscr = (uint8_t*)scratch(4, jdec_scratch_bytes(S.hd) + sizeof(JdecJob));
   int32_t* dstatus = (int32_t*)scratch(5, 4);
   int32_t status = 0;
   if (!dstream || !dscr || !dstatus ||

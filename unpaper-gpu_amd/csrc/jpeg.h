@@ -89,7 +89,8 @@ constexpr uint8_t kJpegNatural[64] = {
 // none changes), then writes the packed layout above for the IDCT kernel.
 // Progressive and multi-scan files keep the host entropy decoder.
 // ---------------------------------------------------------------------------
-constexpr int kJdecSubBits = 8192;  // subsequence length (1 KiB of data)
+constexpr int kJdecSubBits = 1024;   // subsequence length (the count / write passes' unit)
+constexpr int kJdecMacro = 8;        // subsequences a synchronisation pass decodes in a row
 constexpr int kJdecLook = 10;        // lookahead bits of the decode tables (jpeg.cpp kLook)
 
 struct JdecTable {
@@ -100,25 +101,36 @@ struct JdecTable {
 };
 
 // The uploaded stream: JdecHeader | segment start bits (int64, nseg + 1) |
-// segment subsequence prefix (int32, nseg + 1) | data (unstuffed, 16 zero
-// bytes of slack).  h describes the frame, its one scan and the offsets of
+// segment subsequence prefix (int32, nseg + 1) | segment macro prefix
+// (int32, nseg + 1; a macro = kJdecMacro subsequences of one segment) | data
+// (unstuffed, 16 zero bytes of slack).  h describes the frame, its one scan and the offsets of
 // the packed layout the device writes (upper bound of 64 coefficients a block).
 struct JdecHeader {
   JpegHeader h;
   int32_t restart;        // MCUs per restart interval (0: none)
   int32_t nseg;           // restart segments (>= 1)
   int64_t nsub;           // subsequences
+  int64_t nmac;           // macros
   int64_t nbits;          // data bits
   int32_t tdc[4], tac[4]; // table slots of the scan's components
   int32_t bcomp[10];      // scan component of each block of an MCU
   JdecTable dc[4], ac[4];
-  int64_t seg_off, segsub_off, data_off, total_bytes;
+  int64_t seg_off, segsub_off, segmac_off, data_off, total_bytes;
+};
+
+// One image of a batched device decode (kernels read job blockIdx.y).
+struct JdecJob {
+  const uint8_t* stream;  // device copy of the uploaded stream
+  uint8_t* packed;        // packed coefficient layout (JdecHeader::h.total_bytes)
+  uint8_t* scratch;       // jdec_scratch_bytes
+  int32_t* status;        // non-zero: corrupt data
 };
 
 struct JdecStreamHost {
   JdecHeader hd{};
   std::vector<int64_t> seg;     // segment start bits, + the end
   std::vector<int32_t> segsub;  // subsequences before each segment, + the total
+  std::vector<int32_t> segmac;  // macros before each segment, + the total
   std::vector<uint8_t> data;
 };
 
@@ -128,7 +140,8 @@ struct JdecStreamHost {
 int jpeg_stream_prepare(const uint8_t* data, size_t size, const char* name, JdecStreamHost* out);
 // Writes the uploaded layout (hd.total_bytes bytes).
 void jpeg_stream_pack(const JdecStreamHost& s, uint8_t* dst);
-// Device scratch of the decode phases for one image.
+// Device scratch of the decode phases for one image (jdec_launch needs
+// sizeof(JdecJob) more).
 size_t jdec_scratch_bytes(const JdecHeader& hd);
 // One image: the stream at `dstream` (device copy of jpeg_stream_pack's
 // bytes), its header `hd`, into the packed coefficient layout at `dpacked`
@@ -138,6 +151,10 @@ size_t jdec_scratch_bytes(const JdecHeader& hd);
 // blocks that do not add up) sets *dstatus (device int32) non-zero.
 bool jdec_launch(const JdecHeader& hd, const uint8_t* dstream, uint8_t* dpacked, uint8_t* scratch,
                  int32_t* dstatus, hipStream_t st);
+// Several images in one set of launches: jobs[n] in device memory (statuses
+// zeroed by the caller); max_nsub / max_nmac over the images.
+bool jdec_launch_batch(const JdecJob* djobs, int n, int64_t max_nsub, int64_t max_nmac,
+                       hipStream_t st);
 
 // Host half: a decoded file's coefficients before packing.
 struct JpegDecoded {

@@ -8,10 +8,12 @@
 // The stream is cut into subsequences of kJdecSubBits bits (restart segments
 // are cut separately; a segment's first subsequence starts in a known state).
 // A decoder state is (bit position, block of the MCU, next zigzag index).
-//   k_jdec_sync  pass 0: every subsequence decodes from its first bit as if a
-//                block started there, up to the first code boundary at or past
-//                its end: its exit state.  Pass t > 0: every subsequence
-//                starts from the exit its predecessor had in pass t-1.  A
+//   k_jdec_sync  pass 0: every macro (kJdecMacro subsequences) decodes from
+//                its first bit as if a block started there, recording the
+//                state at the first code boundary at or past the end of each
+//                of its subsequences (their exits).  Pass t > 0: every macro
+//                starts from the exit its predecessor had in pass t-1 (only
+//                macros whose entry changed decode again).  A
 //                decoder that starts off the true code boundaries falls into
 //                step after a few codes (Huffman codes self-synchronise, and
 //                an end of block realigns the block state), so exits stop
@@ -23,14 +25,16 @@
 //                the passes launched) the exact exits by one lane walking the
 //                subsequences in order -- correct for any stream, slow only
 //                for pathological ones.
-//   k_jdec_count a subsequence owns the blocks whose DC code starts in it:
+//   k_jdec_count a subsequence (one lane each, kJdecMacro x the sync passes'
+//                parallelism) owns the blocks whose DC code starts in it:
 //                their number, coefficient count, DC difference sums
 //   k_jdec_scan  per image: block / coefficient offsets, DC predictors
 //                (restarting at each segment), consistency checks
 //   k_jdec_emit  decode again, write counts, zigzag prefixes (absolute DCs),
 //                MCU-row offsets
-// Codes come from a 10-bit lookahead table (lengths 11..16 by the canonical
-// maxcode walk); one 32-bit peek serves a code and its magnitude bits.
+// Codes come from a 10-bit lookahead table in LDS (lengths 11..16 by the
+// canonical maxcode walk); one 32-bit peek serves a code and its magnitude
+// bits.  Every kernel takes all the images of a chunk (grid.y = image).
 #include "jpeg.h"
 #include "jpeg_huff_core.h"
 #include "runtime.h"
@@ -40,12 +44,14 @@ namespace uph {
 using namespace jdec;
 
 namespace {
-// the decode tables of the scan's components in LDS
+
+// the image's decode tables and block map in LDS
 struct TabLds {
   JdecTable dc[3], ac[3];
+  int8_t bcomp[12];
 };
 
-__device__ void load_tables(const JdecHeader& H, TabLds* t) {
+__device__ Dec load_dec(const JdecHeader& H, TabLds* t) {
   const int ns = H.h.scan[0].ncomp;
   for (int i = 0; i < ns; i++) {
     const uint32_t* s0 = (const uint32_t*)&H.dc[H.tdc[i]];
@@ -57,75 +63,96 @@ __device__ void load_tables(const JdecHeader& H, TabLds* t) {
       d1[j] = s1[j];
     }
   }
+  if (threadIdx.x < 10) t->bcomp[threadIdx.x] = (int8_t)H.bcomp[threadIdx.x];
   __syncthreads();
+  const uint8_t* base = (const uint8_t*)&H;
+  Dec d;
+  d.dct = t->dc;
+  d.act = t->ac;
+  d.bcomp = t->bcomp;
+  d.bpm = H.h.scan[0].blocks_per_mcu;
+  d.nseg = H.nseg;
+  d.seg = (const int64_t*)(base + H.seg_off);
+  d.segsub = (const int32_t*)(base + H.segsub_off);
+  d.segmac = (const int32_t*)(base + H.segmac_off);
+  d.data = (const uint32_t*)(base + H.data_off);
+  return d;
+}
+
+__device__ __forceinline__ JdecScratch scratch_of(const JdecJob& J, const JdecHeader& H) {
+  return carve(J.scratch, H.nsub, H.nmac);
 }
 
 }  // namespace
 
-// Sync pass `pass` (0: from the subsequence starts).  Grid: ceil(nsub/256).
-__global__ void __launch_bounds__(256) k_jdec_sync(const uint8_t* stream, uint8_t* scratch, int pass) {
-  const Ctx c = ctx_of(stream);
-  const JdecHeader& H = *c.hd;
-  const JdecScratch S = carve(scratch, H.nsub);
-  if (pass > 0)
-    for (int p = 1; p < pass; p++)
-      if (S.changed[p] == 0) return;  // converged earlier
+// Clears the pass flags of every image.  Grid: (1, images).
+__global__ void k_jdec_init(const JdecJob* jobs) {
+  const JdecJob J = jobs[blockIdx.y];
+  const JdecHeader& H = *(const JdecHeader*)J.stream;
+  const JdecScratch S = scratch_of(J, H);
+  if (threadIdx.x < kSyncPasses + 2) S.changed[threadIdx.x] = 0;
+}
+
+// Sync pass `pass` (0: from the macro starts).  Grid: (macros / 256, images).
+__global__ void __launch_bounds__(256) k_jdec_sync(const JdecJob* jobs, int pass) {
+  const JdecJob J = jobs[blockIdx.y];
+  const JdecHeader& H = *(const JdecHeader*)J.stream;
+  if ((int64_t)blockIdx.x * blockDim.x >= H.nmac) return;
+  const JdecScratch S = scratch_of(J, H);
+  for (int p = 1; p < pass; p++)
+    if (S.changed[p] == 0) return;  // converged earlier
   __shared__ TabLds tl;
-  load_tables(H, &tl);
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= H.nsub) return;
-  sync_sub(c, tl.dc, tl.ac, S, i, pass);
+  const Dec d = load_dec(H, &tl);
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m < H.nmac) sync_macro(d, S, m, pass);
 }
 
 // Which buffer holds the exact exits; without convergence, one lane walks the
-// subsequences in order (exact for any stream).  Grid: 1 block.
-__global__ void __launch_bounds__(256) k_jdec_settle(const uint8_t* stream, uint8_t* scratch) {
-  const Ctx c = ctx_of(stream);
-  const JdecHeader& H = *c.hd;
-  const JdecScratch S = carve(scratch, H.nsub);
+// stream in order.  Grid: (1, images).
+__global__ void __launch_bounds__(256) k_jdec_settle(const JdecJob* jobs) {
+  const JdecJob J = jobs[blockIdx.y];
+  const JdecHeader& H = *(const JdecHeader*)J.stream;
+  const JdecScratch S = scratch_of(J, H);
   __shared__ TabLds tl;
-  load_tables(H, &tl);
+  const Dec d = load_dec(H, &tl);
   if (threadIdx.x != 0) return;
   for (int p = 1; p <= kSyncPasses; p++)
     if (S.changed[p] == 0) {
       *S.final_buf = p & 1;
       return;
     }
-  const int fb = kSyncPasses & 1;
-  JdecState prev{0, 0};
-  for (int64_t i = 0; i < H.nsub; i++) {
-    const Sub s = sub_of(c, i);
-    const JdecState st = s.first ? JdecState{s.start, 0} : prev;
-    prev = run_to(c, tl.dc, tl.ac, st, s.stop, s.seg_end);
-    S.xpos[fb][i] = prev.pos;
-    S.xbk[fb][i] = prev.bk;
-  }
-  *S.final_buf = fb;
+  settle_serial(d, S, kSyncPasses & 1);
+  *S.final_buf = kSyncPasses & 1;
 }
 
 // Owned blocks, coefficients and DC difference sums per subsequence.
-__global__ void __launch_bounds__(256) k_jdec_count(const uint8_t* stream, uint8_t* scratch,
-                                                    int32_t* status) {
-  const Ctx c = ctx_of(stream);
-  const JdecHeader& H = *c.hd;
-  const JdecScratch S = carve(scratch, H.nsub);
+__global__ void __launch_bounds__(256) k_jdec_count(const JdecJob* jobs) {
+  const JdecJob J = jobs[blockIdx.y];
+  const JdecHeader& H = *(const JdecHeader*)J.stream;
+  if ((int64_t)blockIdx.x * blockDim.x >= H.nsub) return;
+  const JdecScratch S = scratch_of(J, H);
   __shared__ TabLds tl;
-  load_tables(H, &tl);
+  const Dec d = load_dec(H, &tl);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= H.nsub) return;
-  int32_t nb = 0, dc[3] = {0, 0, 0}, diff = 0;
+  int32_t nb = 0, dc0 = 0, dc1 = 0, dc2 = 0, diff = 0;
   int64_t nc = 0;
   const bool ok = walk_owned(
-      c, tl.dc, tl.ac, S, i, [&](int, int zz, int val, int) { if (zz == 0) diff = val; },
+      d, S, i, [&](int, int zz, int val, int) { if (zz == 0) diff = val; },
       [&](int b, int last) {
         nb++;
         nc += last + 1;
-        dc[H.bcomp[b]] += diff;
+        const int c = d.bcomp[b];
+        dc0 += c == 0 ? diff : 0;
+        dc1 += c == 1 ? diff : 0;
+        dc2 += c == 2 ? diff : 0;
       });
-  if (!ok) atomicOr(status, 1);
+  if (!ok) atomicOr(J.status, 1);
   S.nblk[i] = nb;
   S.ncoef[i] = nc;
-  for (int k = 0; k < 3; k++) S.dcsum[3 * i + k] = dc[k];
+  S.dcsum[3 * i] = dc0;
+  S.dcsum[3 * i + 1] = dc1;
+  S.dcsum[3 * i + 2] = dc2;
 }
 
 namespace {
@@ -153,16 +180,17 @@ __device__ T scan_block(T v, T* excl, T* lds) {
 
 }  // namespace
 
-// Offsets and DC predictors (grid: 1 block of 1024).
-__global__ void __launch_bounds__(1024) k_jdec_scan(const uint8_t* stream, uint8_t* scratch,
-                                                    uint8_t* packed, int32_t* status) {
+// Offsets and DC predictors.  Grid: (1, images), 1024 threads.
+__global__ void __launch_bounds__(1024) k_jdec_scan(const JdecJob* jobs) {
   __shared__ long long lds[16];
-  const Ctx c = ctx_of(stream);
-  const JdecHeader& H = *c.hd;
-  const JdecScratch S = carve(scratch, H.nsub);
+  const JdecJob J = jobs[blockIdx.y];
+  const JdecHeader& H = *(const JdecHeader*)J.stream;
+  const JdecScratch S = scratch_of(J, H);
+  const uint8_t* base = J.stream;
+  const int32_t* segsub = (const int32_t*)(base + H.segsub_off);
   long long cb = 0, cc = 0, cd[3] = {0, 0, 0};
-  for (int64_t base = 0; base < H.nsub; base += 1024) {
-    const int64_t i = base + threadIdx.x;
+  for (int64_t b0 = 0; b0 < H.nsub; b0 += 1024) {
+    const int64_t i = b0 + threadIdx.x;
     const bool live = i < H.nsub;
     long long ex;
     const long long tb = scan_block<long long>(live ? S.nblk[i] : 0, &ex, lds);
@@ -182,51 +210,49 @@ __global__ void __launch_bounds__(1024) k_jdec_scan(const uint8_t* stream, uint8
   // restart intervals
   const int bpm = H.h.scan[0].blocks_per_mcu;
   for (int64_t i = threadIdx.x; i < H.nsub; i += 1024) {
-    const int g = seg_of(c, i);
-    const int64_t f = c.segsub[g];
-    if (i == f && H.restart && S.blkoff[i] != (int64_t)g * H.restart * bpm) atomicOr(status, 2);
+    const int g = seg_search(segsub, H.nseg, i);
+    const int64_t f = segsub[g];
+    if (i == f && H.restart && S.blkoff[i] != (int64_t)g * H.restart * bpm) atomicOr(J.status, 2);
     if (i != f)
       for (int k = 0; k < 3; k++) S.dcpre[3 * i + k] -= S.dcpre[3 * f + k];
   }
   __syncthreads();
   if (H.nseg > 1)
-    for (int64_t i = threadIdx.x; i < H.nsub; i += 1024) {
-      const int64_t f = c.segsub[seg_of(c, i)];
-      if (i == f)
+    for (int64_t i = threadIdx.x; i < H.nsub; i += 1024)
+      if (i == segsub[seg_search(segsub, H.nseg, i)])
         for (int k = 0; k < 3; k++) S.dcpre[3 * i + k] = 0;
-    }
   if (threadIdx.x == 0) {
-    if (cb != H.h.nblocks) atomicOr(status, 4);
-    ((uint32_t*)(packed + H.h.groups_off))[H.h.ngroups] = (uint32_t)cc;
-    if (cc > 0xF0000000ll) atomicOr(status, 8);
+    if (cb != H.h.nblocks) atomicOr(J.status, 4);
+    ((uint32_t*)(J.packed + H.h.groups_off))[H.h.ngroups] = (uint32_t)cc;
+    if (cc > 0xF0000000ll) atomicOr(J.status, 8);
   }
 }
 
 // Writes counts, zigzag prefixes (absolute DCs) and MCU-row offsets.
-__global__ void __launch_bounds__(256) k_jdec_emit(const uint8_t* stream, uint8_t* scratch,
-                                                   uint8_t* packed, int32_t* status) {
-  const Ctx c = ctx_of(stream);
-  const JdecHeader& H = *c.hd;
-  const JdecScratch S = carve(scratch, H.nsub);
+__global__ void __launch_bounds__(256) k_jdec_emit(const JdecJob* jobs) {
+  const JdecJob J = jobs[blockIdx.y];
+  const JdecHeader& H = *(const JdecHeader*)J.stream;
+  if ((int64_t)blockIdx.x * blockDim.x >= H.nsub) return;
+  const JdecScratch S = scratch_of(J, H);
   __shared__ TabLds tl;
-  load_tables(H, &tl);
+  const Dec d = load_dec(H, &tl);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= H.nsub) return;
-  uint8_t* counts = packed + H.h.counts_off;
-  uint32_t* groups = (uint32_t*)(packed + H.h.groups_off);
-  int16_t* coefs = (int16_t*)(packed + H.h.coefs_off);
+  uint8_t* counts = J.packed + H.h.counts_off;
+  uint32_t* groups = (uint32_t*)(J.packed + H.h.groups_off);
+  int16_t* coefs = (int16_t*)(J.packed + H.h.coefs_off);
   int64_t blk = S.blkoff[i], co = S.coefoff[i];
-  int pred[3] = {S.dcpre[3 * i], S.dcpre[3 * i + 1], S.dcpre[3 * i + 2]};
+  int p0 = S.dcpre[3 * i], p1 = S.dcpre[3 * i + 1], p2 = S.dcpre[3 * i + 2];
   const int64_t row_blocks = (int64_t)H.h.scan[0].mcus_x * H.h.scan[0].blocks_per_mcu;
   const int64_t nblocks = H.h.nblocks;
   const bool ok = walk_owned(
-      c, tl.dc, tl.ac, S, i,
+      d, S, i,
       [&](int cb, int zz, int val, int last) {
         if (blk >= nblocks) return;
         if (zz == 0) {
           if (blk % row_blocks == 0) groups[blk / row_blocks] = (uint32_t)co;
-          int& p = pred[H.bcomp[cb]];
-          p += val;
+          const int c = d.bcomp[cb];
+          const int p = (c == 0 ? (p0 += val) : c == 1 ? (p1 += val) : (p2 += val));
           coefs[co] = (int16_t)p;
           return;
         }
@@ -238,29 +264,38 @@ __global__ void __launch_bounds__(256) k_jdec_emit(const uint8_t* stream, uint8_
         blk++;
         co += last + 1;
       });
-  if (!ok) atomicOr(status, 16);
+  if (!ok) atomicOr(J.status, 16);
 }
 
 size_t jdec_scratch_bytes(const JdecHeader& hd) {
-  const size_t n = (size_t)(hd.nsub > 0 ? hd.nsub : 1);
-  return a256(8 * n) * 2 + a256(4 * n) * 2 + a256(n) * 2 + a256(4 * (kSyncPasses + 2)) +
-         a256(4 * n) + a256(8 * n) + a256(12 * n) + a256(8 * n) * 2 + a256(12 * n);
+  return scratch_bytes(hd.nsub > 0 ? hd.nsub : 1, hd.nmac > 0 ? hd.nmac : 1);
 }
 
+bool jdec_launch_batch(const JdecJob* djobs, int n, int64_t max_nsub, int64_t max_nmac,
+                       hipStream_t st) {
+  if (n <= 0 || n > 65535 || max_nsub <= 0 || max_nmac <= 0 || max_nsub > 0x7fffffffll)
+    return fail("jpeg: bad device decode batch");
+  const dim3 gm((unsigned)((max_nmac + 255) / 256), (unsigned)n);
+  const dim3 gs((unsigned)((max_nsub + 255) / 256), (unsigned)n);
+  hipLaunchKernelGGL(k_jdec_init, dim3(1, (unsigned)n), dim3(64), 0, st, djobs);
+  for (int p = 0; p <= kSyncPasses; p++)
+    hipLaunchKernelGGL(k_jdec_sync, gm, dim3(256), 0, st, djobs, p);
+  hipLaunchKernelGGL(k_jdec_settle, dim3(1, (unsigned)n), dim3(256), 0, st, djobs);
+  hipLaunchKernelGGL(k_jdec_count, gs, dim3(256), 0, st, djobs);
+  hipLaunchKernelGGL(k_jdec_scan, dim3(1, (unsigned)n), dim3(1024), 0, st, djobs);
+  hipLaunchKernelGGL(k_jdec_emit, gs, dim3(256), 0, st, djobs);
+  return UPH_HIP(hipGetLastError());
+}
+
+// One image; the job record goes to the end of its scratch.
 bool jdec_launch(const JdecHeader& hd, const uint8_t* dstream, uint8_t* dpacked, uint8_t* scratch,
                  int32_t* dstatus, hipStream_t st) {
-  if (hd.nsub <= 0 || hd.nsub > 0x7fffffffll) return fail("jpeg: bad subsequence count");
   if (hd.h.nscans != 1) return fail("jpeg: device decode takes one scan");
-  const JdecScratch S = carve(scratch, hd.nsub);
-  if (!UPH_HIP(hipMemsetAsync(S.changed, 0, 4 * (kSyncPasses + 2), st))) return false;
-  const dim3 grid((unsigned)((hd.nsub + 255) / 256));
-  for (int p = 0; p <= kSyncPasses; p++)
-    hipLaunchKernelGGL(k_jdec_sync, grid, dim3(256), 0, st, dstream, scratch, p);
-  hipLaunchKernelGGL(k_jdec_settle, dim3(1), dim3(256), 0, st, dstream, scratch);
-  hipLaunchKernelGGL(k_jdec_count, grid, dim3(256), 0, st, dstream, scratch, dstatus);
-  hipLaunchKernelGGL(k_jdec_scan, dim3(1), dim3(1024), 0, st, dstream, scratch, dpacked, dstatus);
-  hipLaunchKernelGGL(k_jdec_emit, grid, dim3(256), 0, st, dstream, scratch, dpacked, dstatus);
-  return UPH_HIP(hipGetLastError());
+  JdecJob* dj = (JdecJob*)(scratch + jdec_scratch_bytes(hd));
+  const JdecJob j{dstream, dpacked, scratch, dstatus};
+  return UPH_HIP(hipMemcpyAsync(dj, &j, sizeof(j), hipMemcpyHostToDevice, st)) &&
+         UPH_HIP(hipStreamSynchronize(st)) &&  // the job record is on this frame
+         jdec_launch_batch(dj, 1, hd.nsub, hd.nmac, st);
 }
 
 }  // namespace uph

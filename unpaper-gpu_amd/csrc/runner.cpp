@@ -409,12 +409,15 @@ struct Slot {
   size_t djpg_cap = 0;
   uint8_t* dscr = nullptr;    // colour planes (one page at a time on the stream)
   size_t dscr_cap = 0;
-  uint8_t* djpk = nullptr;    // packed coefficients of a device-decoded page (one at a time)
+  uint8_t* djpk = nullptr;    // packed coefficients of the device-decoded pages
   size_t djpk_cap = 0;
-  uint8_t* djsc = nullptr;    // device Huffman scratch (one page at a time)
+  uint8_t* djsc = nullptr;    // their device Huffman scratch
   size_t djsc_cap = 0;
   int32_t* djst = nullptr;    // per page: device Huffman status
-  int djst_cap = 0;
+  size_t djst_cap = 0;
+  JdecJob* djob = nullptr;    // the decode jobs (device) and their pinned source
+  JdecJob* hjob = nullptr;
+  size_t djob_cap = 0;
   bool jdev = false;          // the chunk has device-decoded pages (statuses to read)
   UphipBatch* b = nullptr;
   uint8_t* hin = nullptr;   // pinned input staging (count * input_count pages)
@@ -644,6 +647,8 @@ bool load_page(UphipRunner* r, int device, const UphipSource* s, int64_t job, in
 // then decode it into its input slot (after the staging upload, before the run).
 bool jpeg_submit(Slot* sl, int npages) {
   size_t total = 0, scr = 0, pk = 0, hs = 0;
+  int ndev = 0;
+  int64_t max_nsub = 0, max_nmac = 0;
   sl->jdev = false;
   for (int p = 0; p < npages; p++) {
     const JpegPage& jp = sl->jpg[(size_t)p];
@@ -651,62 +656,82 @@ bool jpeg_submit(Slot* sl, int npages) {
     total += jp.bytes;
     scr = std::max(scr, (size_t)jp.h.scratch_bytes);
     if (jp.dev) {
-      sl->jdev = true;
-      pk = std::max(pk, (size_t)jp.h.total_bytes);
-      hs = std::max(hs, jdec_scratch_bytes(*(const JdecHeader*)jp.host));
+      const JdecHeader& hd = *(const JdecHeader*)jp.host;
+      ndev++;
+      pk += ((size_t)jp.h.total_bytes + 255) & ~(size_t)255;
+      hs += (jdec_scratch_bytes(hd) + 255) & ~(size_t)255;
+      max_nsub = std::max<int64_t>(max_nsub, hd.nsub);
+      max_nmac = std::max<int64_t>(max_nmac, hd.nmac);
     }
   }
   if (!total) return true;
+  // the slot's stream is idle here (the slot was free): old buffers can go
   auto grow = [](auto** p, size_t* cap, size_t need) -> bool {
     if (*cap >= need) return true;
     if (*p) hipFree(*p);
     *p = nullptr;
     *cap = 0;
-    if (!UPH_HIP(hipMalloc((void**)p, need))) return false;
-    *cap = need;
+    if (!UPH_HIP(hipMalloc((void**)p, need + need / 4))) return false;
+    *cap = need + need / 4;
     return true;
   };
-  if (sl->jdev) {
-    size_t stcap = (size_t)sl->djst_cap;
-    if (!grow(&sl->djpk, &sl->djpk_cap, pk) || !grow(&sl->djsc, &sl->djsc_cap, hs) ||
-        !grow(&sl->djst, &stcap, 4 * (size_t)npages))
-      return false;
-    sl->djst_cap = (int)(stcap / 4);
-    if (!UPH_HIP(hipMemsetAsync(sl->djst, 0, 4 * (size_t)npages, (hipStream_t)uphip_batch_stream(sl->b))))
-      return false;
-  }
-  // the slot's stream is idle here (the slot was free): old buffers can go
-  if (sl->djpg_cap < total) {
-    if (sl->djpg) hipFree(sl->djpg);
-    sl->djpg = nullptr;
-    sl->djpg_cap = 0;
-    if (!UPH_HIP(hipMalloc((void**)&sl->djpg, total + total / 4))) return false;
-    sl->djpg_cap = total + total / 4;
-  }
-  if (scr && sl->dscr_cap < scr) {
-    if (sl->dscr) hipFree(sl->dscr);
-    sl->dscr = nullptr;
-    sl->dscr_cap = 0;
-    if (!UPH_HIP(hipMalloc((void**)&sl->dscr, scr))) return false;
-    sl->dscr_cap = scr;
-  }
+  if (!grow(&sl->djpg, &sl->djpg_cap, total) || (scr && !grow(&sl->dscr, &sl->dscr_cap, scr)))
+    return false;
   hipStream_t st = (hipStream_t)uphip_batch_stream(sl->b);
-  size_t off = 0;
+  if (ndev) {
+    sl->jdev = true;
+    if (!grow(&sl->djpk, &sl->djpk_cap, pk) || !grow(&sl->djsc, &sl->djsc_cap, hs) ||
+        !grow(&sl->djst, &sl->djst_cap, 4 * (size_t)npages))
+      return false;
+    if (sl->djob_cap < (size_t)npages) {
+      if (sl->djob) hipFree(sl->djob);
+      if (sl->hjob) hipHostFree(sl->hjob);
+      sl->djob = nullptr;
+      sl->hjob = nullptr;
+      sl->djob_cap = 0;
+      if (!UPH_HIP(hipMalloc((void**)&sl->djob, sizeof(JdecJob) * (size_t)npages)) ||
+          !UPH_HIP(hipHostMalloc((void**)&sl->hjob, sizeof(JdecJob) * (size_t)npages,
+                                 hipHostMallocDefault)))
+        return false;
+      sl->djob_cap = (size_t)npages;
+    }
+    if (!UPH_HIP(hipMemsetAsync(sl->djst, 0, 4 * (size_t)npages, st))) return false;
+  }
+  // upload every page; the device-decoded ones as one batch of jobs
+  size_t off = 0, poff = 0, soff = 0;
+  int nj = 0;
+  std::vector<int> jpage;
+  for (int p = 0; p < npages; p++) {
+    JpegPage& jp = sl->jpg[(size_t)p];
+    if (!jp.on) continue;
+    if (!UPH_HIP(hipMemcpyAsync(sl->djpg + off, jp.host, jp.bytes, hipMemcpyHostToDevice, st)))
+      return false;
+    if (jp.dev) {
+      const JdecHeader& hd = *(const JdecHeader*)jp.host;
+      sl->hjob[nj] = JdecJob{sl->djpg + off, sl->djpk + poff, sl->djsc + soff, sl->djst + p};
+      jpage.push_back(p);
+      nj++;
+      poff += ((size_t)jp.h.total_bytes + 255) & ~(size_t)255;
+      soff += (jdec_scratch_bytes(hd) + 255) & ~(size_t)255;
+    }
+    off += jp.bytes;
+  }
+  if (nj) {
+    if (!UPH_HIP(hipMemcpyAsync(sl->djob, sl->hjob, sizeof(JdecJob) * (size_t)nj,
+                                hipMemcpyHostToDevice, st)) ||
+        !jdec_launch_batch(sl->djob, nj, max_nsub, max_nmac, st))
+      return false;
+  }
+  // pixels: each page from its packed coefficients into its input slot
+  off = 0;
+  int k = 0;
   for (int p = 0; p < npages; p++) {
     JpegPage& jp = sl->jpg[(size_t)p];
     if (!jp.on) continue;
     int64_t pitch = 0;
     uint8_t* dst = (uint8_t*)uphip_batch_input_ptr(sl->b, p, &pitch);
-    if (!dst || !UPH_HIP(hipMemcpyAsync(sl->djpg + off, jp.host, jp.bytes, hipMemcpyHostToDevice, st)))
-      return false;
-    if (jp.dev) {  // Huffman decoding into the slot's packed buffer, then pixels
-      if (!jdec_launch(*(const JdecHeader*)jp.host, sl->djpg + off, sl->djpk, sl->djsc, sl->djst + p,
-                       st) ||
-          !jpeg_launch(jp.h, sl->djpk, sl->dscr, dst, pitch, st))
-        return false;
-    } else if (!jpeg_launch(jp.h, sl->djpg + off, sl->dscr, dst, pitch, st)) {
-      return false;
-    }
+    const uint8_t* packed = jp.dev ? sl->hjob[k++].packed : sl->djpg + off;
+    if (!dst || !jpeg_launch(jp.h, packed, sl->dscr, dst, pitch, st)) return false;
     off += jp.bytes;
   }
   return true;
@@ -861,6 +886,8 @@ void uphip_runner_destroy(UphipRunner* r) {
       if (sl.djpk) hipFree(sl.djpk);
       if (sl.djsc) hipFree(sl.djsc);
       if (sl.djst) hipFree(sl.djst);
+      if (sl.djob) hipFree(sl.djob);
+      if (sl.hjob) hipHostFree(sl.hjob);
       if (sl.hjpg) hipHostFree(sl.hjpg);
       for (JpegPage& jp : sl.jpg)
         if (jp.host) hipHostFree(jp.host);
