@@ -32,21 +32,18 @@ int64_t jdec_emulate(const uint8_t* file, size_t n, uint8_t* out, int64_t cap, i
   const JdecHeader& hd = S.hd;
   std::vector<uint8_t> scratch(jdec_scratch_bytes(hd) + 256);
   const JdecScratch X = carve(scratch.data(), hd.nsub, hd.nmac);
-  JdecTable dtab[3], atab[3];
-  int8_t bcomp[12] = {};
+  JdecTable tab[6];
   for (int i = 0; i < hd.h.scan[0].ncomp; i++) {
-    dtab[i] = hd.dc[hd.tdc[i]];
-    atab[i] = hd.ac[hd.tac[i]];
+    tab[i] = hd.dc[hd.tdc[i]];
+    tab[3 + i] = hd.ac[hd.tac[i]];
   }
-  for (int i = 0; i < 10; i++) bcomp[i] = (int8_t)hd.bcomp[i];
   const uint8_t* base = stream.data();
   Dec d;
-  d.dct = dtab;
-  d.act = atab;
-  d.bcomp = bcomp;
+  d.tab = tab;
   d.bpm = hd.h.scan[0].blocks_per_mcu;
+  d.bmap = block_map(hd.bcomp, d.bpm);
   d.nseg = hd.nseg;
-  d.seg = (const int64_t*)(base + hd.seg_off);
+  d.seg = (const int32_t*)(base + hd.seg_off);
   d.segsub = (const int32_t*)(base + hd.segsub_off);
   d.segmac = (const int32_t*)(base + hd.segmac_off);
   d.data = (const uint32_t*)(base + hd.data_off);
@@ -72,22 +69,6 @@ int64_t jdec_emulate(const uint8_t* file, size_t n, uint8_t* out, int64_t cap, i
   if (!conv) {
     settle_serial(d, X, kSyncPasses & 1);
     *X.final_buf = kSyncPasses & 1;
-  }
-  // k_jdec_count
-  for (int64_t i = 0; i < hd.nsub; i++) {
-    int32_t nb = 0, dc[3] = {0, 0, 0}, diff = 0;
-    int64_t nc = 0;
-    const bool ok = walk_owned(
-        d, X, i, [&](int, int zz, int val, int) { if (zz == 0) diff = val; },
-        [&](int b, int last) {
-          nb++;
-          nc += last + 1;
-          dc[hd.bcomp[b]] += diff;
-        });
-    if (!ok) status |= 1;
-    X.nblk[i] = nb;
-    X.ncoef[i] = nc;
-    for (int k = 0; k < 3; k++) X.dcsum[3 * i + k] = dc[k];
   }
   // k_jdec_scan
   std::vector<uint8_t> packed((size_t)hd.h.total_bytes, 0);
@@ -115,7 +96,7 @@ int64_t jdec_emulate(const uint8_t* file, size_t n, uint8_t* out, int64_t cap, i
     if (cb != hd.h.nblocks) status |= 4;
     ((uint32_t*)(packed.data() + hd.h.groups_off))[hd.h.ngroups] = (uint32_t)cc;
   }
-  // k_jdec_emit
+  // k_jdec_zero: the vector above starts zeroed; k_jdec_emit
   uint8_t* counts = packed.data() + hd.h.counts_off;
   uint32_t* groups = (uint32_t*)(packed.data() + hd.h.groups_off);
   int16_t* coefs = (int16_t*)(packed.data() + hd.h.coefs_off);
@@ -123,22 +104,21 @@ int64_t jdec_emulate(const uint8_t* file, size_t n, uint8_t* out, int64_t cap, i
   for (int64_t i = 0; i < hd.nsub; i++) {
     int64_t blk = X.blkoff[i], co = X.coefoff[i];
     int pred[3] = {X.dcpre[3 * i], X.dcpre[3 * i + 1], X.dcpre[3 * i + 2]};
+    int64_t next_row = (blk + row_blocks - 1) / row_blocks * row_blocks;
     const bool ok = walk_owned(
         d, X, i,
-        [&](int cb, int zz, int val, int last) {
+        [&](int c, int zz, int val) {
           if (blk >= hd.h.nblocks) return;
           if (zz == 0) {
-            if (blk % row_blocks == 0) groups[blk / row_blocks] = (uint32_t)co;
-            int& p = pred[hd.bcomp[cb]];
-            p += val;
-            coefs[co] = (int16_t)p;
-            return;
+            if (blk == next_row) groups[blk / row_blocks] = (uint32_t)co;
+            pred[c] += val;
+            val = pred[c];
           }
-          for (int z = last + 1; z < zz; z++) coefs[co + z] = 0;
           coefs[co + zz] = (int16_t)val;
         },
-        [&](int, int last) {
+        [&](int last) {
           if (blk < hd.h.nblocks) counts[blk] = (uint8_t)(last + 1);
+          next_row += blk == next_row ? row_blocks : 0;
           blk++;
           co += last + 1;
         });

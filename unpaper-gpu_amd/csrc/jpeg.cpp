@@ -780,15 +780,17 @@ bool stream_scan(Parser& P, const uint8_t* b, int len) {
     } else if (m == 0xFF) {
       p += 1;  // fill byte
     } else if (m >= 0xD0 && m <= 0xD7) {
-      S.seg.push_back((int64_t)out.size() * 8);
+      if (out.size() >= kJdecMaxBytes) return P.not_device = true, false;  // host decoder
+      S.seg.push_back((int32_t)out.size() * 8);
       p += 2;
     } else {
       break;  // EOI or another marker
     }
   }
   P.pos = (size_t)(p - P.d);
+  if (out.size() >= kJdecMaxBytes) return P.not_device = true, false;  // host decoder
   const int64_t nbits = (int64_t)out.size() * 8;
-  S.seg.push_back(nbits);
+  S.seg.push_back((int32_t)nbits);
   D.nseg = (int32_t)S.seg.size() - 1;
   D.nbits = nbits;
   const int64_t nmcu = (int64_t)Sc.mcus_x * Sc.mcus_y;
@@ -814,7 +816,7 @@ bool stream_scan(Parser& P, const uint8_t* b, int len) {
   S.segmac[(size_t)D.nseg] = (int32_t)nmac;
   D.nsub = nsub;
   D.nmac = nmac;
-  out.resize(out.size() + 16, 0);  // slack for the device's word reads
+  out.resize(out.size() + 48, 0);  // slack for the device's read-ahead (jpeg_huff_core.h)
   return true;
 }
 
@@ -946,7 +948,7 @@ int jpeg_stream_prepare(const uint8_t* d, size_t n, const char* name, JdecStream
     H.coefs_off = align16(H.groups_off + 4 * (H.ngroups + 1));
     H.total_bytes = align16(H.coefs_off + 2 * 64 * H.nblocks);
     D.seg_off = align16((int64_t)sizeof(JdecHeader));
-    D.segsub_off = align16(D.seg_off + 8 * (int64_t)out->seg.size());
+    D.segsub_off = align16(D.seg_off + 4 * (int64_t)out->seg.size());
     D.segmac_off = align16(D.segsub_off + 4 * (int64_t)out->segsub.size());
     D.data_off = align16(D.segmac_off + 4 * (int64_t)out->segmac.size());
     D.total_bytes = align16(D.data_off + (int64_t)out->data.size());
@@ -959,7 +961,7 @@ int jpeg_stream_prepare(const uint8_t* d, size_t n, const char* name, JdecStream
 void jpeg_stream_pack(const JdecStreamHost& s, uint8_t* dst) {
   const JdecHeader& D = s.hd;
   memcpy(dst, &D, sizeof(D));
-  memcpy(dst + D.seg_off, s.seg.data(), 8 * s.seg.size());
+  memcpy(dst + D.seg_off, s.seg.data(), 4 * s.seg.size());
   memcpy(dst + D.segsub_off, s.segsub.data(), 4 * s.segsub.size());
   memcpy(dst + D.segmac_off, s.segmac.data(), 4 * s.segmac.size());
   memcpy(dst + D.data_off, s.data.data(), s.data.size());

@@ -92,6 +92,8 @@ constexpr uint8_t kJpegNatural[64] = {
 constexpr int kJdecSubBits = 1024;   // subsequence length (the count / write passes' unit)
 constexpr int kJdecMacro = 8;        // subsequences a synchronisation pass decodes in a row
 constexpr int kJdecLook = 10;        // lookahead bits of the decode tables (jpeg.cpp kLook)
+// entropy-coded bytes the device decoder takes (bit positions are int32)
+constexpr size_t kJdecMaxBytes = (size_t)1 << 27;
 
 struct JdecTable {
   uint16_t look[1 << kJdecLook];     // len << 8 | symbol, 0 = a longer code
@@ -100,10 +102,10 @@ struct JdecTable {
   uint8_t vals[256];
 };
 
-// The uploaded stream: JdecHeader | segment start bits (int64, nseg + 1) |
+// The uploaded stream: JdecHeader | segment start bits (int32, nseg + 1) |
 // segment subsequence prefix (int32, nseg + 1) | segment macro prefix
 // (int32, nseg + 1; a macro = kJdecMacro subsequences of one segment) | data
-// (unstuffed, 16 zero bytes of slack).  h describes the frame, its one scan and the offsets of
+// (unstuffed, 48 zero bytes of slack).  h describes the frame, its one scan and the offsets of
 // the packed layout the device writes (upper bound of 64 coefficients a block).
 struct JdecHeader {
   JpegHeader h;
@@ -128,7 +130,7 @@ struct JdecJob {
 
 struct JdecStreamHost {
   JdecHeader hd{};
-  std::vector<int64_t> seg;     // segment start bits, + the end
+  std::vector<int32_t> seg;     // segment start bits, + the end
   std::vector<int32_t> segsub;  // subsequences before each segment, + the total
   std::vector<int32_t> segmac;  // macros before each segment, + the total
   std::vector<uint8_t> data;

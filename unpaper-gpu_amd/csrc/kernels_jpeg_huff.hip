@@ -25,13 +25,17 @@
 //                the passes launched) the exact exits by one lane walking the
 //                subsequences in order -- correct for any stream, slow only
 //                for pathological ones.
-//   k_jdec_count a subsequence (one lane each, kJdecMacro x the sync passes'
-//                parallelism) owns the blocks whose DC code starts in it:
-//                their number, coefficient count, DC difference sums
+//                A macro also counts, per subsequence, the blocks whose DC
+//                code starts in its bits (their number, coefficients, DC
+//                difference sums): the counts of a macro's last decode are
+//                those of its exact entry.
 //   k_jdec_scan  per image: block / coefficient offsets, DC predictors
 //                (restarting at each segment), consistency checks
-//   k_jdec_emit  decode again, write counts, zigzag prefixes (absolute DCs),
-//                MCU-row offsets
+//   k_jdec_zero  clears the coefficient prefixes
+//   k_jdec_emit  per subsequence (one lane each, kJdecMacro x the sync
+//                passes' parallelism): decode again from its exact entry,
+//                write counts, non-zero coefficients (absolute DCs), MCU-row
+//                offsets
 // Codes come from a 10-bit lookahead table in LDS (lengths 11..16 by the
 // canonical maxcode walk); one 32-bit peek serves a code and its magnitude
 // bits.  Every kernel takes all the images of a chunk (grid.y = image).
@@ -45,10 +49,10 @@ using namespace jdec;
 
 namespace {
 
-// the image's decode tables and block map in LDS
+// the image's decode tables in LDS: DC tables of the scan components, then
+// their AC tables
 struct TabLds {
-  JdecTable dc[3], ac[3];
-  int8_t bcomp[12];
+  JdecTable t[6];
 };
 
 __device__ Dec load_dec(const JdecHeader& H, TabLds* t) {
@@ -56,26 +60,24 @@ __device__ Dec load_dec(const JdecHeader& H, TabLds* t) {
   for (int i = 0; i < ns; i++) {
     const uint32_t* s0 = (const uint32_t*)&H.dc[H.tdc[i]];
     const uint32_t* s1 = (const uint32_t*)&H.ac[H.tac[i]];
-    uint32_t* d0 = (uint32_t*)&t->dc[i];
-    uint32_t* d1 = (uint32_t*)&t->ac[i];
+    uint32_t* d0 = (uint32_t*)&t->t[i];
+    uint32_t* d1 = (uint32_t*)&t->t[3 + i];
     for (int j = threadIdx.x; j < (int)(sizeof(JdecTable) / 4); j += blockDim.x) {
       d0[j] = s0[j];
       d1[j] = s1[j];
     }
   }
-  if (threadIdx.x < 10) t->bcomp[threadIdx.x] = (int8_t)H.bcomp[threadIdx.x];
   __syncthreads();
   const uint8_t* base = (const uint8_t*)&H;
   Dec d;
-  d.dct = t->dc;
-  d.act = t->ac;
-  d.bcomp = t->bcomp;
+  d.tab = (const JD_LDS JdecTable*)t->t;
   d.bpm = H.h.scan[0].blocks_per_mcu;
+  d.bmap = block_map(H.bcomp, d.bpm);
   d.nseg = H.nseg;
-  d.seg = (const int64_t*)(base + H.seg_off);
-  d.segsub = (const int32_t*)(base + H.segsub_off);
-  d.segmac = (const int32_t*)(base + H.segmac_off);
-  d.data = (const uint32_t*)(base + H.data_off);
+  d.seg = (const JD_GLB int32_t*)(base + H.seg_off);
+  d.segsub = (const JD_GLB int32_t*)(base + H.segsub_off);
+  d.segmac = (const JD_GLB int32_t*)(base + H.segmac_off);
+  d.data = (const JD_GLB uint32_t*)(base + H.data_off);
   return d;
 }
 
@@ -125,36 +127,6 @@ __global__ void __launch_bounds__(256) k_jdec_settle(const JdecJob* jobs) {
   *S.final_buf = kSyncPasses & 1;
 }
 
-// Owned blocks, coefficients and DC difference sums per subsequence.
-__global__ void __launch_bounds__(256) k_jdec_count(const JdecJob* jobs) {
-  const JdecJob J = jobs[blockIdx.y];
-  const JdecHeader& H = *(const JdecHeader*)J.stream;
-  if ((int64_t)blockIdx.x * blockDim.x >= H.nsub) return;
-  const JdecScratch S = scratch_of(J, H);
-  __shared__ TabLds tl;
-  const Dec d = load_dec(H, &tl);
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= H.nsub) return;
-  int32_t nb = 0, dc0 = 0, dc1 = 0, dc2 = 0, diff = 0;
-  int64_t nc = 0;
-  const bool ok = walk_owned(
-      d, S, i, [&](int, int zz, int val, int) { if (zz == 0) diff = val; },
-      [&](int b, int last) {
-        nb++;
-        nc += last + 1;
-        const int c = d.bcomp[b];
-        dc0 += c == 0 ? diff : 0;
-        dc1 += c == 1 ? diff : 0;
-        dc2 += c == 2 ? diff : 0;
-      });
-  if (!ok) atomicOr(J.status, 1);
-  S.nblk[i] = nb;
-  S.ncoef[i] = nc;
-  S.dcsum[3 * i] = dc0;
-  S.dcsum[3 * i + 1] = dc1;
-  S.dcsum[3 * i + 2] = dc2;
-}
-
 namespace {
 
 template <class T>
@@ -187,7 +159,7 @@ __global__ void __launch_bounds__(1024) k_jdec_scan(const JdecJob* jobs) {
   const JdecHeader& H = *(const JdecHeader*)J.stream;
   const JdecScratch S = scratch_of(J, H);
   const uint8_t* base = J.stream;
-  const int32_t* segsub = (const int32_t*)(base + H.segsub_off);
+  const JD_GLB int32_t* segsub = (const JD_GLB int32_t*)(base + H.segsub_off);
   long long cb = 0, cc = 0, cd[3] = {0, 0, 0};
   for (int64_t b0 = 0; b0 < H.nsub; b0 += 1024) {
     const int64_t i = b0 + threadIdx.x;
@@ -228,7 +200,23 @@ __global__ void __launch_bounds__(1024) k_jdec_scan(const JdecJob* jobs) {
   }
 }
 
-// Writes counts, zigzag prefixes (absolute DCs) and MCU-row offsets.
+// Zeroes each image's coefficient prefixes (the write pass stores only the
+// non-zero coefficients).  Grid: (blocks, images).
+__global__ void __launch_bounds__(256) k_jdec_zero(const JdecJob* jobs) {
+  const JdecJob J = jobs[blockIdx.y];
+  const JdecHeader& H = *(const JdecHeader*)J.stream;
+  const int64_t ncoef = *(const uint32_t*)(J.packed + H.h.groups_off + 4 * H.h.ngroups);
+  const int64_t cap = (H.h.total_bytes - H.h.coefs_off) >> 4;
+  int64_t n16 = (2 * ncoef + 15) >> 4;  // coefs_off is 16-aligned
+  n16 = n16 < cap ? n16 : cap;          // (a corrupt total is caught by the scan)
+  uint4* dst = (uint4*)(J.packed + H.h.coefs_off);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = make_uint4(0, 0, 0, 0);
+}
+
+// Writes counts, zigzag prefixes (absolute DCs; the zeros are in place) and
+// MCU-row offsets.
 __global__ void __launch_bounds__(256) k_jdec_emit(const JdecJob* jobs) {
   const JdecJob J = jobs[blockIdx.y];
   const JdecHeader& H = *(const JdecHeader*)J.stream;
@@ -238,29 +226,31 @@ __global__ void __launch_bounds__(256) k_jdec_emit(const JdecJob* jobs) {
   const Dec d = load_dec(H, &tl);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= H.nsub) return;
-  uint8_t* counts = J.packed + H.h.counts_off;
-  uint32_t* groups = (uint32_t*)(J.packed + H.h.groups_off);
-  int16_t* coefs = (int16_t*)(J.packed + H.h.coefs_off);
+  JD_GLB uint8_t* counts = (JD_GLB uint8_t*)(J.packed + H.h.counts_off);
+  JD_GLB uint32_t* groups = (JD_GLB uint32_t*)(J.packed + H.h.groups_off);
+  JD_GLB int16_t* coefs = (JD_GLB int16_t*)(J.packed + H.h.coefs_off);
   int64_t blk = S.blkoff[i], co = S.coefoff[i];
   int p0 = S.dcpre[3 * i], p1 = S.dcpre[3 * i + 1], p2 = S.dcpre[3 * i + 2];
   const int64_t row_blocks = (int64_t)H.h.scan[0].mcus_x * H.h.scan[0].blocks_per_mcu;
   const int64_t nblocks = H.h.nblocks;
+  int64_t next_row = (blk + row_blocks - 1) / row_blocks * row_blocks;  // next row start
   const bool ok = walk_owned(
       d, S, i,
-      [&](int cb, int zz, int val, int last) {
+      [&](int c, int zz, int val) {
         if (blk >= nblocks) return;
+        int v = val;
         if (zz == 0) {
-          if (blk % row_blocks == 0) groups[blk / row_blocks] = (uint32_t)co;
-          const int c = d.bcomp[cb];
-          const int p = (c == 0 ? (p0 += val) : c == 1 ? (p1 += val) : (p2 += val));
-          coefs[co] = (int16_t)p;
-          return;
+          if (blk == next_row) groups[blk / row_blocks] = (uint32_t)co;
+          p0 += c == 0 ? val : 0;
+          p1 += c == 1 ? val : 0;
+          p2 += c == 2 ? val : 0;
+          v = c == 0 ? p0 : c == 1 ? p1 : p2;
         }
-        for (int z = last + 1; z < zz; z++) coefs[co + z] = 0;  // the run's zeros
-        coefs[co + zz] = (int16_t)val;
+        coefs[co + zz] = (int16_t)v;
       },
-      [&](int, int last) {
+      [&](int last) {
         if (blk < nblocks) counts[blk] = (uint8_t)(last + 1);
+        next_row += blk == next_row ? row_blocks : 0;
         blk++;
         co += last + 1;
       });
@@ -281,8 +271,8 @@ bool jdec_launch_batch(const JdecJob* djobs, int n, int64_t max_nsub, int64_t ma
   for (int p = 0; p <= kSyncPasses; p++)
     hipLaunchKernelGGL(k_jdec_sync, gm, dim3(256), 0, st, djobs, p);
   hipLaunchKernelGGL(k_jdec_settle, dim3(1, (unsigned)n), dim3(256), 0, st, djobs);
-  hipLaunchKernelGGL(k_jdec_count, gs, dim3(256), 0, st, djobs);
   hipLaunchKernelGGL(k_jdec_scan, dim3(1, (unsigned)n), dim3(1024), 0, st, djobs);
+  hipLaunchKernelGGL(k_jdec_zero, dim3(256, (unsigned)n), dim3(256), 0, st, djobs);
   hipLaunchKernelGGL(k_jdec_emit, gs, dim3(256), 0, st, djobs);
   return UPH_HIP(hipGetLastError());
 }
