@@ -439,9 +439,10 @@ def host_threads_share():
 def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid):
     """The JPEG decode peer in the runner: synthetic A4 GRAY8
     pages saved by PIL as JPEG quality 95 (tmpfs), read by a runner file
-    source (host Huffman decode on the load pool into pinned memory, IDCT on
-    the device into the batch's input slots), the default pipeline, sheets
-    discarded.  PCIe- and host-inclusive: a figure of its own, never `value`
+    source (marker parse + unstuffing on the load pool into pinned memory;
+    Huffman decode of every page of a chunk in one set of launches, then the
+    IDCT into the batch's input slots, on the device), the default pipeline,
+    sheets discarded.  PCIe- and host-inclusive: a figure of its own, never `value`
     of the C3 line.  Two pages' outputs are checked against the oracle on
     PIL's decode of the same files."""
     from PIL import Image

@@ -592,7 +592,10 @@ bool is_jpeg_file(const std::string& path) {
 
 // The host half of a JPEG page into the slot's pinned buffer `jp`.
 bool jpeg_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp) {
-  std::vector<uint8_t> file;
+  // per pool thread, kept across pages: fresh multi-MB buffers per page would
+  // page-fault (and contend on the address space) on every load
+  thread_local std::vector<uint8_t> file;
+  thread_local JdecStreamHost S;
   if (!jpeg_read_file(path.c_str(), &file)) return false;
   // the frame header first: a file of the wrong geometry (or a crafted one
   // claiming a huge frame) is refused before anything is sized from it
@@ -606,7 +609,6 @@ bool jpeg_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp
   // a one-scan sequential file goes to the device as its unstuffed entropy
   // data (Huffman decoding there too); progressive / multi-scan files are
   // entropy-decoded here
-  JdecStreamHost S;
   const int dev = jpeg_stream_prepare(file.data(), file.size(), path.c_str(), &S);
   if (dev < 0) return false;
   JpegDecoded d;
@@ -641,6 +643,34 @@ bool load_page(UphipRunner* r, int device, const UphipSource* s, int64_t job, in
   if (idx >= 0 && idx < (int64_t)s->paths.size() && is_jpeg_file(s->paths[(size_t)idx]))
     return jpeg_load(r, device, s->paths[(size_t)idx], jp);
   return pnm_load(s, idx, dst, r->in_pitch, geo) == 0;
+}
+
+// Queue the H2D copy of the slot's staged pages, skipping the JPEG pages (their
+// decode writes the batch's input slots itself, after this copy): runs of
+// other pages go as one copy each (the staging is laid out like the slots).
+bool upload_staging(UphipRunner* r, Slot* sl, int npages) {
+  bool any = false;
+  for (int p = 0; p < npages; p++) any |= sl->jpg[(size_t)p].on;
+  if (!any)
+    return uphip_batch_upload_async(sl->b, sl->count, sl->hin, r->in_pitch, r->in_page_stride) == 0;
+  hipStream_t st = (hipStream_t)uphip_batch_stream(sl->b);
+  for (int p = 0; p < npages;) {
+    if (sl->jpg[(size_t)p].on) {
+      p++;
+      continue;
+    }
+    int e = p;
+    while (e < npages && !sl->jpg[(size_t)e].on) e++;
+    int64_t pitch = 0;
+    uint8_t* dst = (uint8_t*)uphip_batch_input_ptr(sl->b, p, &pitch);
+    if (!dst || pitch != r->in_pitch ||
+        !UPH_HIP(hipMemcpyAsync(dst, sl->hin + (int64_t)p * r->in_page_stride,
+                                (size_t)((int64_t)(e - p) * r->in_page_stride),
+                                hipMemcpyHostToDevice, st)))
+      return false;
+    p = e;
+  }
+  return true;
 }
 
 // Queue the chunk's JPEG pages on the slot's stream: upload each packed page,
@@ -1197,8 +1227,8 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
             progress = true;
           }
           if (st == LOADED && phase[k] == LOADING) {
-            if (uphip_batch_upload_async(sl->b, sl->count, sl->hin, r->in_pitch, r->in_page_stride) != 0 ||
-                !jpeg_submit(sl, sl->count * nin) || uphip_batch_run(sl->b, sl->count) != 0 ||
+            if (!upload_staging(r, sl, sl->count * nin) || !jpeg_submit(sl, sl->count * nin) ||
+                uphip_batch_run(sl->b, sl->count) != 0 ||
                 (sink->jpeg &&
                  uphip_batch_encode_jpeg_async(sl->b, sink->quality, sink->sampling) != 0)) {
               note("run failed");
