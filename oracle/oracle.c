@@ -551,6 +551,16 @@ static bool fill_start(OImage im, UphipPoint p, FillFrame *f, UphipPixel color,
   f->p = p;
   for (int k = 0; k < 4; k++)
     f->dist[k] = fill_line(im, p, DIR_DX[k], DIR_DY[k], color, mmin, mmax, intensity);
+#ifdef ORACLE_FRAME_LOG
+  { /* development aid (tools/dbg/black_frames.sh): one line per frame */
+    static FILE *log;
+    if (!log && getenv("ORACLE_FRAME_LOG")) log = fopen(getenv("ORACLE_FRAME_LOG"), "w");
+    if (log)
+      fprintf(log, "%d %d %llu %llu %llu %llu\n", p.x, p.y, (unsigned long long)f->dist[0],
+              (unsigned long long)f->dist[1], (unsigned long long)f->dist[2],
+              (unsigned long long)f->dist[3]);
+  }
+#endif
   f->dir = 0;
   f->d = 0;
   f->sub = 0;
