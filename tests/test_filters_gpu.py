@@ -169,6 +169,18 @@ def test_blurfilter_pages(hip, oracle, fmt, size, params):
          lambda o: oracle.blurfilter(o, p, 229))
 
 
+@pytest.mark.parametrize("fmt", [A.FMT_GRAY8, A.FMT_RGB24])
+@pytest.mark.parametrize("width", [1320, 2000, 3960, 4480, 4520])
+def test_blurfilter_wide_rows(hip, oracle, fmt, width):
+    # rows of 33 .. 112 blocks take the chunked scalar resolver (C4's 99),
+    # 113 the generic one
+    h = make_image(width, 300, fmt, seed=7, specks=600)
+    for params in (((40, 30), (15, 20), 0.05), ((40, 40), (40, 10), 0.3)):
+        p = A.BlurfilterParameters(A.RectangleSize(*params[0]), A.Delta(*params[1]), params[2])
+        both(hip, oracle, h.copy(), lambda d: hip.blurfilter(d, p, 229),
+             lambda o: oracle.blurfilter(o, p, 229))
+
+
 # ---------------------------------------------------------------- blackfilter
 def black_params(oracle, size=(20, 20), step=(5, 5), depth=(500, 500), thr=242, intensity=20,
                  direction=(True, True), exclusions=()):

@@ -700,6 +700,127 @@ __device__ __forceinline__ uint64_t blur_row_fixed(uint32_t& Av, uint32_t rowv, 
   return wipes;
 }
 
+// Rows of 33 .. 112 blocks.  Within a row the recurrence only READS A as it
+// was before the row (an entry entering the window, A[k+4] at block k, has
+// not been written in this row yet), so the scalar window reads the row's
+// A and counts from their lanes and writes nothing back per block; the row's
+// final A is then made lane-parallel from its counts and wipe bits (the last
+// write of each entry, below), a handful of vector operations a row.
+// 16 blocks KC+1 .. KC+16 of a row: their counts and the A entries entering
+// the window read from lanes known at compile time up front, then a chain of
+// scalar operations per block.  Blocks past bpr run too (their wipe bits are
+// masked off; the row's state is rebuilt from the bits, not from the window).
+__device__ __forceinline__ uint32_t lane_c(const Lanes2& v, int l) {
+  return l < 64 ? lane_get(v.v0, l) : lane_get(v.v1, l - 64);
+}
+template <int OP, int KC>
+__device__ __forceinline__ void blur_chunk_ro(const Lanes2& Aold, const Lanes2& rowv, int32_t bpr,
+                                              uint32_t total, int32_t tmax, uint32_t (&W)[5],
+                                              uint64_t& w0, uint64_t& w1) {
+  if (KC + 1 > bpr) return;
+  uint32_t e[16], nx[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int k = KC + 1 + i;
+    e[i] = k < 128 ? lane_c(rowv, k) : 0u;
+    nx[i] = k + 4 < 128 ? lane_c(Aold, k + 4) : 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int k = KC + 1 + i;
+    uint32_t mx;
+    bool w;
+    if (OP == 0) {
+      W[4] = e[i];
+      mx = umax(W[0], umax(W[2], W[4]));
+      w = (int32_t)mx <= tmax;
+      W[2] = w ? total : W[2];
+    } else if (OP == 1) {
+      W[2] = e[i];
+      mx = umax(umax(W[0], W[1]), umax(W[2], W[3]));
+      w = (int32_t)mx <= tmax;
+      W[3] = w ? total : W[3];
+    } else {
+      W[3] = e[i];
+      mx = umax(umax(W[1], W[2]), umax(W[3], W[4]));
+      w = (int32_t)mx <= tmax;
+      W[1] = w ? total : W[1];
+    }
+    if (k <= 64) w0 |= w ? 1ull << (k - 1) : 0ull;
+    else if (k <= 128) w1 |= w ? 1ull << (k - 65) : 0ull;
+    W[0] = W[1];
+    W[1] = W[2];
+    W[2] = W[3];
+    W[3] = W[4];
+    W[4] = nx[i];
+  }
+}
+template <int OP>
+__device__ __forceinline__ void blur_row_ro(const Lanes2& Aold, const Lanes2& rowv, int32_t bpr,
+                                            uint32_t total, int32_t tmax, uint64_t (&wipes)[2]) {
+  constexpr int ON = OP == 0 ? 2 : OP == 1 ? 0 : 1;
+  uint32_t W[5];
+#pragma unroll
+  for (int j = 0; j < 5; j++) W[j] = lane_get(Aold.v0, j);
+  W[ON] = lane_get(rowv.v0, 0);  // next[0] = A[on]
+  uint64_t w0 = 0, w1 = 0;  // bit k-1: block k
+  blur_chunk_ro<OP, 0>(Aold, rowv, bpr, total, tmax, W, w0, w1);
+  blur_chunk_ro<OP, 16>(Aold, rowv, bpr, total, tmax, W, w0, w1);
+  blur_chunk_ro<OP, 32>(Aold, rowv, bpr, total, tmax, W, w0, w1);
+  blur_chunk_ro<OP, 48>(Aold, rowv, bpr, total, tmax, W, w0, w1);
+  blur_chunk_ro<OP, 64>(Aold, rowv, bpr, total, tmax, W, w0, w1);
+  blur_chunk_ro<OP, 80>(Aold, rowv, bpr, total, tmax, W, w0, w1);
+  blur_chunk_ro<OP, 96>(Aold, rowv, bpr, total, tmax, W, w0, w1);
+  wipes[0] = bpr >= 64 ? w0 : w0 & ((1ull << bpr) - 1);
+  wipes[1] = bpr <= 64 ? 0 : bpr >= 128 ? w1 : w1 & ((1ull << (bpr - 64)) - 1);
+}
+// The row's final A, entry j per lane (j = lane, 64 + lane): the last write
+// of entry j during the row of type OP (next[0] first, then per block k the
+// count write and the wipe write):
+//   OP 0: count A[k+3] = row[k], wipe A[k+1] = total, next[0] at A[2]
+//   OP 1: count A[k+1] = row[k], wipe A[k+2] = total, next[0] at A[0]
+//   OP 2: count A[k+2] = row[k], wipe A[k]   = total, next[0] at A[1]
+template <int OP>
+__device__ __forceinline__ Lanes2 blur_row_state(const Lanes2& Aold, const Lanes2& rowv,
+                                                 int32_t bpr, uint32_t total,
+                                                 const uint64_t (&wipes)[2]) {
+  constexpr int S = OP == 0 ? 3 : OP == 1 ? 1 : 2;  // count shift: A[j] = row[j - S]
+  constexpr int ON = OP == 0 ? 2 : OP == 1 ? 0 : 1;
+  const int lane = threadIdx.x & 63;
+  const uint32_t r0 = lane_get(rowv.v0, 0);
+  auto wbit = [&](int32_t k) -> bool {  // block k wiped
+    if (k < 1 || k > bpr) return false;
+    const uint64_t m = k <= 64 ? wipes[0] : wipes[1];
+    return (m >> ((k - 1) & 63)) & 1;
+  };
+  auto entry = [&](int32_t j, uint32_t old, uint32_t shifted) -> uint32_t {
+    // shifted = row[j - S] (valid for j >= S)
+    if (OP == 0) {
+      if (j >= 2 && j <= bpr + 1 && wbit(j - 1)) return total;
+      if (j >= 4 && j <= bpr + 3) return shifted;
+      return j == ON ? r0 : old;
+    } else if (OP == 1) {
+      if (j >= 2 && j <= bpr + 1) return shifted;
+      if (j == bpr + 2 && wbit(bpr)) return total;
+      return j == ON ? r0 : old;
+    } else {
+      if (j >= 1 && j <= bpr && wbit(j)) return total;
+      if (j >= 3 && j <= bpr + 2) return shifted;
+      return j == ON ? r0 : old;
+    }
+  };
+  // row[j - S] for j = lane and j = 64 + lane
+  const int src0 = (lane - S) & 63;
+  const uint32_t a0 = (uint32_t)__shfl((int)rowv.v0, src0, 64);
+  const uint32_t b0 = (uint32_t)__shfl((int)rowv.v1, src0, 64);
+  const uint32_t sh0 = a0;                      // lane >= S: row[lane - S] (v0)
+  const uint32_t sh1 = lane >= S ? b0 : a0;     // row[64 + lane - S]: v1 or the top of v0
+  Lanes2 r;
+  r.v0 = entry(lane, Aold.v0, sh0);
+  r.v1 = entry(64 + lane, Aold.v1, sh1);
+  return r;
+}
+
 template <int BPR>
 __device__ __forceinline__ void blur_rows_fixed(uint32_t Av, const uint32_t* counts, uint8_t* wipe,
                                                 int32_t T, uint32_t total, int32_t tmax) {
@@ -717,6 +838,10 @@ __device__ __forceinline__ void blur_rows_fixed(uint32_t Av, const uint32_t* cou
   }
 }
 
+// CHUNKED: rows of 33 .. 112 blocks (blur_row_ro + blur_row_state); otherwise the fixed
+// row lengths 12 .. 32 and the generic sliding window.  Separate kernels keep
+// the chunked path's scalar registers free of the fixed rows' pressure.
+template <bool CHUNKED>
 __global__ void __launch_bounds__(64) k_blur_resolve_w(BlurGeom g, uint8_t* scratch,
                                                        int64_t sstride, const int32_t* active) {
   const int s = blockIdx.x;
@@ -751,7 +876,7 @@ __global__ void __launch_bounds__(64) k_blur_resolve_w(BlurGeom g, uint8_t* scra
   }
   tmax = __builtin_amdgcn_readfirstlane(tmax);
   // row lengths of 150-400 dpi pages at the default 100-pixel blocks
-  switch (bpr) {
+  if (!CHUNKED) switch (bpr) {
 #define UPH_BLUR_FIXED(n) \
   case n:                 \
     blur_rows_fixed<n>(Av, counts, wipe, g.T, total, tmax); \
@@ -779,9 +904,24 @@ __global__ void __launch_bounds__(64) k_blur_resolve_w(BlurGeom g, uint8_t* scra
     if (t + 1 < g.T) rowv = row_of(t + 1);
     const int op = t % 3;
     uint64_t wipes[2];
-    if (op == 0) blur_row<0>(A2, cur, bpr, total, tmax, wipes);
-    else if (op == 1) blur_row<1>(A2, cur, bpr, total, tmax, wipes);
-    else blur_row<2>(A2, cur, bpr, total, tmax, wipes);
+    if (CHUNKED) {
+      if (op == 0) {
+        blur_row_ro<0>(A2, cur, bpr, total, tmax, wipes);
+        A2 = blur_row_state<0>(A2, cur, bpr, total, wipes);
+      } else if (op == 1) {
+        blur_row_ro<1>(A2, cur, bpr, total, tmax, wipes);
+        A2 = blur_row_state<1>(A2, cur, bpr, total, wipes);
+      } else {
+        blur_row_ro<2>(A2, cur, bpr, total, tmax, wipes);
+        A2 = blur_row_state<2>(A2, cur, bpr, total, wipes);
+      }
+    } else if (op == 0) {
+      blur_row<0>(A2, cur, bpr, total, tmax, wipes);
+    } else if (op == 1) {
+      blur_row<1>(A2, cur, bpr, total, tmax, wipes);
+    } else {
+      blur_row<2>(A2, cur, bpr, total, tmax, wipes);
+    }
     if (lane < bpr) wipe[t * bpr + lane] = (uint8_t)((wipes[0] >> lane) & 1);
     if (64 + lane < bpr) wipe[t * bpr + 64 + lane] = (uint8_t)((wipes[1] >> lane) & 1);
   }
@@ -819,8 +959,10 @@ static void launch_blur_t(const PlaneRef& img, const BlurGeom& g, uint8_t* scr, 
   const size_t lds = sizeof(uint64_t) * ((size_t)g.nrect + 3 * (size_t)(g.bpr + 2));
   const bool scalar = g.bpr >= 1 && g.bpr + 8 <= kBlurLanesMax && (int64_t)g.sw * g.sh < (1ll << 31);
   if (diag_skip() & 8) {
+  } else if (scalar && g.bpr > 32 && g.bpr <= 112) {
+    hipLaunchKernelGGL(k_blur_resolve_w<true>, dim3(count), dim3(64), 0, st, g, scr, ss, active);
   } else if (scalar) {
-    hipLaunchKernelGGL(k_blur_resolve_w, dim3(count), dim3(64), 0, st, g, scr, ss, active);
+    hipLaunchKernelGGL(k_blur_resolve_w<false>, dim3(count), dim3(64), 0, st, g, scr, ss, active);
   } else {
     hipLaunchKernelGGL(k_blur_resolve, dim3(count), dim3(256), lds, st, g, scr, ss, active);
   }
