@@ -1043,7 +1043,9 @@ size_t noise_scratch_bytes(const NoiseGeom& g) {
   // lists + a global sort buffer for the rare > 8192-trigger sequential case;
   // the GRAY8 dark bit-plane shares the sort buffer's space (it is read by
   // k_noise_classify only, before k_noise_resolve may sort)
-  const size_t sort = 4 * pow2_at_least((size_t)g.capacity);
+  // (and k_noise_group's keys / roots / last, 3 x 16384 words)
+  size_t sort = 4 * pow2_at_least((size_t)g.capacity);
+  if (sort < 12 * 16384) sort = 12 * 16384;
   const size_t bits = 4 * (size_t)noise_bit_words(g) * (size_t)g.H;
   return noise_list_bytes(g) + (sort > bits ? sort : bits);
 }
@@ -2111,7 +2113,173 @@ __device__ void noise_resolve_components(const uint32_t* keys, uint32_t* aux, in
 }
 
 constexpr int kCompCap = 16384;  // triggers the component replay keeps in LDS
+static_assert(kCompCap == 16384, "noise_scratch_bytes reserves 3 x 16384 words for k_noise_group");
 constexpr int kResolveThreads = 1024;
+
+// The component replay in two kernels for intensity N <= 4 and at most
+// kCompCap triggers: k_noise_group (a block per sheet) orders the triggers
+// in raster order by a counting sort over row buckets (then insertion sort
+// within a bucket), links those within 2N-1 by union-find and writes, per
+// trigger in raster order, its key, its component's root (the component's
+// first trigger) and, for a root, its component's last trigger;
+// k_noise_replay (many blocks per sheet) gives each component to one
+// thread, which replays its triggers in raster order.  The replay's
+// scattered box reads then spread over the chip instead of one CU's address
+// path.  The group kernel writes a flag (word 2 of the sheet's list header):
+// 1 when the two kernels handle the sheet, 0 when k_noise_resolve must.
+constexpr int kNoiseBuckets = 4096;
+constexpr int kGroupBucketMax = 256;  // longer buckets: k_noise_resolve's sort
+// keys, parents, bucket starts, the scan's wave sums, a flag (all dynamic:
+// allow_dynamic_lds raises the dynamic limit to the whole 160 KiB)
+constexpr size_t kGroupLds = sizeof(uint32_t) * (2 * (size_t)kCompCap + kNoiseBuckets + 1 + 16 + 1);
+
+__device__ __forceinline__ int noise_bucket_shift(int32_t H) {
+  int b = 0;
+  while (((H - 1) >> b) >= kNoiseBuckets) b++;
+  return b;
+}
+
+__global__ void __launch_bounds__(1024) k_noise_group(NoiseGeom g, uint8_t* scratch, int64_t sstride,
+                                                      const int32_t* active, SheetCtl* ctl,
+                                                      uint32_t* sortbuf, int64_t sort_stride) {
+  const int s = blockIdx.x;
+  if (active && !active[s]) return;
+  NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
+  uint32_t* flag = NP.nclear + 2;
+  const uint32_t n = *NP.nseq;
+  const int N = g.intensity;
+  const int tid = threadIdx.x;
+  if (n == 0 || n > (uint32_t)kCompCap || N > 4) {
+    if (tid == 0) *flag = n == 0 ? 1u : 0u;
+    return;
+  }
+  uint32_t* gk = sortbuf + s * sort_stride;  // keys [0, C), roots [C, 2C), last [2C, 3C)
+  extern __shared__ uint32_t glds[];
+  uint32_t* keys = glds;
+  uint32_t* par = glds + kCompCap;
+  uint32_t* bc = glds + 2 * kCompCap;  // bucket starts (nb + 1)
+  uint32_t* wsum = bc + kNoiseBuckets + 1;
+  uint32_t& too_long = wsum[16];
+  const int b = noise_bucket_shift(g.H);
+  const int nb = ((g.H - 1) >> b) + 1;
+  const int R = 2 * N - 1;
+  if (tid == 0) too_long = 0u;
+  for (int i = tid; i <= nb; i += 1024) bc[i] = 0;
+  __syncthreads();
+  for (int i = tid; i < (int)n; i += 1024) atomicAdd(&bc[(NP.seq[i] >> 16) >> b], 1u);
+  __syncthreads();
+  // exclusive scan of the nb counts: 4 consecutive buckets a thread
+  {
+    const int b0 = 4 * tid;
+    uint32_t c[4], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      c[k] = b0 + k < nb ? bc[b0 + k] : 0u;
+      sum += c[k];
+    }
+    if (c[0] > kGroupBucketMax || c[1] > kGroupBucketMax || c[2] > kGroupBucketMax ||
+        c[3] > kGroupBucketMax)
+      too_long = 1u;
+    // block exclusive scan of `sum`
+    uint32_t incl = sum;
+    const int lane = tid & 63, wv = tid >> 6;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = (uint32_t)__shfl_up((int)incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (int k = 0; k < wv; k++) before += wsum[k];
+    uint32_t run = before + incl - sum;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (b0 + k < nb) {
+        bc[b0 + k] = run;
+        par[b0 + k] = run;  // scatter cursors
+      }
+      run += c[k];
+    }
+    if (tid == 0) bc[nb] = n;
+  }
+  __syncthreads();
+  if (too_long) {  // a dense stretch of triggers: the general resolver's sort
+    if (tid == 0) *flag = 0u;
+    return;
+  }
+  for (int i = tid; i < (int)n; i += 1024) {
+    const uint32_t key = NP.seq[i];
+    keys[atomicAdd(&par[(key >> 16) >> b], 1u)] = key;
+  }
+  __syncthreads();
+  for (int k = tid; k < nb; k += 1024) {  // raster order inside each bucket
+    const int lo = (int)bc[k], hi = (int)bc[k + 1];
+    for (int i = lo + 1; i < hi; i++) {
+      const uint32_t v = keys[i];
+      int j = i - 1;
+      while (j >= lo && keys[j] > v) {
+        keys[j + 1] = keys[j];
+        j--;
+      }
+      keys[j + 1] = v;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < (int)n; i += 1024) par[i] = (uint32_t)i;
+  __syncthreads();
+  // link every trigger to the earlier ones within R (rows y-R .. y)
+  for (int i = tid; i < (int)n; i += 1024) {
+    const uint32_t key = keys[i];
+    const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
+    for (int j = (int)bc[imax(y - R, 0) >> b]; j < i; j++) {
+      const uint32_t kj = keys[j];
+      const int32_t xj = (int32_t)(kj & 0xFFFF), yj = (int32_t)(kj >> 16);
+      if (yj >= y - R && xj >= x - R && xj <= x + R) uf_union(par, (uint32_t)i, (uint32_t)j);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < (int)n; i += 1024) {
+    gk[i] = keys[i];
+    gk[kCompCap + i] = uf_find(par, (uint32_t)i);
+  }
+  __syncthreads();
+  for (int i = tid; i < (int)n; i += 1024) keys[i] = 0u;
+  __syncthreads();
+  for (int i = tid; i < (int)n; i += 1024) atomicMax(&keys[gk[kCompCap + i]], (uint32_t)i);
+  __syncthreads();
+  for (int i = tid; i < (int)n; i += 1024) gk[2 * kCompCap + i] = keys[i];
+  if (tid == 0) *flag = 1u;
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(256) k_noise_replay(PlaneRef img, NoiseGeom g, uint8_t* scratch,
+                                                      int64_t sstride, const int32_t* active,
+                                                      const uint32_t* sortbuf, int64_t sort_stride) {
+  const int s = blockIdx.y;
+  if (active && !active[s]) return;
+  NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
+  const uint32_t n = *NP.nseq;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (NP.nclear[2] != 1u || i >= (int)n) return;
+  const uint32_t* gk = sortbuf + s * sort_stride;
+  if (gk[kCompCap + i] != (uint32_t)i) return;  // not a component's first trigger
+  const int last = (int)gk[2 * kCompCap + i];
+  Mask81 rowp[5], colp[5];
+#pragma unroll
+  for (int L = 1; L <= 4; L++) {
+    rowp[L] = ring_part(L, true);
+    colp[L] = ring_part(L, false);
+  }
+  uint8_t* base = plane_ptr(img, s);
+  for (int j = i; j <= last; j++) {
+    if (gk[kCompCap + j] != (uint32_t)i) continue;
+    const uint32_t key = gk[j];
+    __threadfence_block();  // this thread's earlier clears are visible to its loads
+    replay_trigger4<FMT>((int32_t)(key & 0xFFFF), (int32_t)(key >> 16), g.intensity, g, base,
+                         img.P.pitch, rowp, colp);
+  }
+}
 
 template <int FMT>
 __global__ void __launch_bounds__(kResolveThreads) k_noise_resolve(PlaneRef img, NoiseGeom g, uint8_t* scratch,
@@ -2125,7 +2293,7 @@ __global__ void __launch_bounds__(kResolveThreads) k_noise_resolve(PlaneRef img,
 #ifdef UPHIP_DIAG
   if ((g.diag & 8) && threadIdx.x == 0) printf("uphip noise: sheet %d seq %u clear %u\n", s, n, *NP.nclear);
 #endif
-  if (n == 0) return;
+  if (n == 0 || NP.nclear[2] == 1u) return;  // done by k_noise_group + k_noise_replay
   if (n > (uint32_t)g.capacity) {
     if (threadIdx.x == 0 && ctl) atomicOr(&ctl[s].status, STATUS_NOISE_OVERFLOW);
     return;
@@ -2308,8 +2476,15 @@ static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr
                      active, ctl);
   constexpr size_t kResolveLds = 2 * sizeof(uint32_t) * kCompCap;  // 128 KiB
   allow_dynamic_lds((const void*)k_noise_resolve<FMT>, kResolveLds);
-  if (!(diag_skip() & 2)) hipLaunchKernelGGL(k_noise_resolve<FMT>, dim3(count), dim3(kResolveThreads), kResolveLds, st, img, gd, scr, ss, active,
-                     ctl, sortbuf, sort_stride);
+  allow_dynamic_lds((const void*)k_noise_group, kGroupLds);
+  if (!(diag_skip() & 2)) {
+    hipLaunchKernelGGL(k_noise_group, dim3(count), dim3(1024), kGroupLds, st, g, scr, ss, active, ctl,
+                       sortbuf, sort_stride);
+    hipLaunchKernelGGL(k_noise_replay<FMT>, dim3(kCompCap / 256, count), dim3(256), 0, st, img, g,
+                       scr, ss, active, sortbuf, sort_stride);
+    hipLaunchKernelGGL(k_noise_resolve<FMT>, dim3(count), dim3(kResolveThreads), kResolveLds, st, img,
+                       gd, scr, ss, active, ctl, sortbuf, sort_stride);
+  }
 }
 
 void launch_noisefilter(const PlaneRef& img, const NoiseGeom& g, void* scratch,
