@@ -479,7 +479,6 @@ __device__ __forceinline__ void fill_cross(const Sheet& S, int32_t px, int32_t p
   if (S.I == 0) {  // the counter is 0 after the first position, whatever it holds
 #pragma unroll
     for (int d = 0; d < 4; d++) dist[d] = 0;
-    paint_cross(S, px, py, dist);  // the start
     return;
   }
   BSTAT({ const uint64_t tw = wall_clock64(); __builtin_amdgcn_s_waitcnt(0); bs->t_wait0 += wall_clock64() - tw; })
@@ -526,9 +525,9 @@ __device__ __forceinline__ void fill_cross(const Sheet& S, int32_t px, int32_t p
   }
 #pragma unroll
   for (int d = 0; d < 4; d++) dist[d] = uni(stop[d] - 1);
-  BSTAT(const uint64_t tp = wall_clock64();)
-  paint_cross(S, px, py, dist);
-  BSTAT(bs->t_paint += wall_clock64() - tp;)
+  // the paints are issued by the caller after the frame's first check
+  // evaluation: a wait for the check windows' loads would otherwise wait for
+  // every paint atomic issued after them (one vector memory counter)
 }
 
 // Neighbour checks (flood_fill_around_line, fill.c:54-74): the checks of line
@@ -650,6 +649,11 @@ __device__ __forceinline__ bool flood(const Sheet& S, int32_t sx, int32_t sy, Fr
       BSTAT(const uint64_t t1 = wall_clock64(); bs->check_trips++;)
       int32_t nxt;
       c = uni(check_eval(S, wc, top, cs, 0, 0, p1, &resume, &nxt));
+      // the cross's paints touch none of its checks: issued now, before any
+      // later load (this wave's memory operations stay in order)
+      BSTAT(const uint64_t tp = wall_clock64();)
+      paint_cross(S, nx, ny, top.dist);
+      BSTAT(bs->t_paint += wall_clock64() - tp;)
       if (c == INT_MAX) c = uni(check_scan(S, top, cs, nxt, &resume, bs));
       BSTAT(bs->t_check += wall_clock64() - t1;)
       sp++;
