@@ -63,8 +63,8 @@ LLVMCC     := /opt/rocm/lib/llvm/bin/clang
 SANFLAGS   := -fsanitize=address,undefined -fno-sanitize-recover=undefined \
               -fno-omit-frame-pointer -g -O1
 
-.PHONY: all lib oracle ctest adapter sanitize libm_check jdec_emul clean
-all: lib oracle ctest libm_check jdec_emul
+.PHONY: all lib oracle ctest adapter sanitize libm_check jdec_emul j2k_emul clean
+all: lib oracle ctest libm_check jdec_emul j2k_emul
 
 lib: $(LIB)
 oracle: $(ORACLE_LIB)
@@ -117,7 +117,7 @@ $(LIBM_CHECK): tests/c/libm_check.cpp $(CSRC)/libm_glibc.h
 # One compiler (ROCm clang) for every object so that one sanitizer runtime
 # serves the program; the HIP sources are compiled for the host only.
 $(SANITIZE): tests/c/sanitize_main.c oracle/oracle.c oracle/oracle.h $(CSRC)/pnm.cpp $(CSRC)/png.cpp \
-             $(CSRC)/jpeg.cpp tests/c/san_stubs.cpp $(CSRC)/runtime.hip $(HDRS)
+             $(CSRC)/jpeg.cpp $(CSRC)/j2k.cpp tests/c/san_stubs.cpp $(CSRC)/runtime.hip $(HDRS)
 	@mkdir -p tests/c/_build/san
 	$(LLVMCC) $(SANFLAGS) -std=gnu11 -ffp-contract=off -c oracle/oracle.c -o tests/c/_build/san/oracle.o
 	$(LLVMCC) $(SANFLAGS) -std=gnu11 -Iinclude -c tests/c/sanitize_main.c -o tests/c/_build/san/main.o
@@ -127,6 +127,8 @@ $(SANITIZE): tests/c/sanitize_main.c oracle/oracle.c oracle/oracle.h $(CSRC)/pnm
 	  -Iinclude -I$(CSRC) -c $(CSRC)/png.cpp -o tests/c/_build/san/png.o
 	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
 	  -Iinclude -I$(CSRC) -c $(CSRC)/jpeg.cpp -o tests/c/_build/san/jpeg.o
+	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
+	  -Iinclude -I$(CSRC) -c $(CSRC)/j2k.cpp -o tests/c/_build/san/j2k.o
 	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
 	  -Iinclude -I$(CSRC) -c tests/c/san_stubs.cpp -o tests/c/_build/san/san_stubs.o
 	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
@@ -139,6 +141,14 @@ jdec_emul: $(JDEC_EMUL)
 $(JDEC_EMUL): tests/c/jdec_emul.cpp $(CSRC)/jpeg_huff_core.h $(CSRC)/jpeg.h $(LIB)
 	@mkdir -p tests/c/_build
 	$(HIPCC) --cuda-host-only -x hip -O2 -std=c++17 -fPIC -shared -Wall -Iinclude -I$(CSRC) $< -o $@ \
+	  -L$(PKG)/lib -lunpaper_hip -Wl,-rpath,'$$ORIGIN/../../../$(PKG)/lib'
+
+# the JPEG 2000 decode's device half replayed on the CPU (test infrastructure)
+J2K_EMUL   := tests/c/_build/libj2k_emul.so
+j2k_emul: $(J2K_EMUL)
+$(J2K_EMUL): tests/c/j2k_emul.cpp $(CSRC)/j2k_dwt.h $(CSRC)/j2k.h $(LIB)
+	@mkdir -p tests/c/_build
+	$(HIPCC) --cuda-host-only -x hip -O2 -std=c++17 -fPIC -shared -ffp-contract=off -Wall -Iinclude -I$(CSRC) $< -o $@ \
 	  -L$(PKG)/lib -lunpaper_hip -Wl,-rpath,'$$ORIGIN/../../../$(PKG)/lib'
 
 sanitize: $(SANITIZE)

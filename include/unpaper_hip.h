@@ -540,7 +540,39 @@ typedef enum {
 int64_t uphip_jpeg_encode(const void *device_src, int64_t pitch, int32_t width,
                           int32_t height, int32_t format, int32_t quality,
                           int32_t sampling, void *out, int64_t capacity);
-/* Any codec, picked by the file's signature (PNG, JPEG or PNM). */
+/* JPEG 2000 peer of the JP2 half of nvImageCodec (imageprocess/nvimgcodec.c
+ * NVIMGCODEC_FORMAT_JPEG2000 decode, lib/decode_queue.c:53-71 is_jp2_file
+ * routing .jp2/.j2k/.j2c to it; nvimgcodec_encode_jp2 with
+ * nvimgcodec_default_jp2_lossless_params, lib/encode_queue.c:883-962).
+ * Decode: JP2 files or raw codestreams, 8-bit unsigned, 1 or 3 components
+ * (-> GRAY8 / RGB24), no subsampling, code-block style 0, any tiling,
+ * precincts, progression order, layers, 5/3 or 9/7 (csrc/j2k.h).  Packet
+ * headers and the EBCOT code-block decoder run on the host; the inverse
+ * wavelet and component transforms, the DC shift and the store on the
+ * current device.  Pixels equal OpenJPEG's (PIL's decoder) for reversible
+ * and irreversible files.  uphip_jp2_read returns host pixels,
+ * uphip_jp2_decode writes device memory (rows `pitch` apart; info: in =
+ * expected geometry when width > 0, out = geometry).  Both synchronise. */
+int uphip_jp2_probe(const char *path, UphipPnmInfo *info);
+int uphip_jp2_read(const char *path, void *dst, int64_t linesize,
+                   const UphipPnmInfo *expect);
+int uphip_jp2_decode(const void *data, size_t size, void *device_dst, int64_t pitch,
+                     UphipPnmInfo *info);
+/* The host half alone (no device needed): the coefficient planes
+ * (csrc/j2k.h layout; int32 for 5/3 files, float for 9/7) written to `coef`
+ * when `capacity` suffices; info = geometry.  Returns their size in bytes,
+ * or -1. */
+int64_t uphip_jp2_entropy_decode(const void *data, size_t size, void *coef, int64_t capacity,
+                                 UphipPnmInfo *info);
+/* Lossless JP2 encode of a device image (GRAY8 or RGB24, rows `pitch`
+ * apart): forward RCT and 5/3 wavelet on the current device, code-blocks
+ * coded on the host; one tile, one layer, LRCP, 64x64 code-blocks, up to 5
+ * decomposition levels.  Returns the file size; the bytes are copied to
+ * `out` only when `capacity` suffices (out = NULL sizes a buffer).
+ * Synchronous; -1 on error. */
+int64_t uphip_jp2_encode(const void *device_src, int64_t pitch, int32_t width,
+                         int32_t height, int32_t format, void *out, int64_t capacity);
+/* Any codec, picked by the file's signature (PNG, JPEG, JPEG 2000 or PNM). */
 int uphip_image_probe(const char *path, UphipPnmInfo *info);
 int uphip_image_read(const char *path, void *dst, int64_t linesize,
                      const UphipPnmInfo *expect);
@@ -618,6 +650,10 @@ UphipSink *uphip_sink_discard(void);
  * names as uphip_sink_pnm.  quality 0 = 85. */
 UphipSink *uphip_sink_jpeg(const char *pattern, int64_t wrap, int32_t quality,
                            int32_t sampling);
+/* Lossless JPEG 2000 files (uphip_jp2_encode of each output page, from the
+ * batch's device planes, on the store tasks): the .jp2 output branch of
+ * lib/encode_queue.c:883-962 (nvimgcodec_default_jp2_lossless_params). */
+UphipSink *uphip_sink_jp2(const char *pattern, int64_t wrap);
 void uphip_sink_destroy(UphipSink *sink);
 
 UphipRunner *uphip_runner_create(const UphipOptions *options,

@@ -1,5 +1,6 @@
 // Sanitizer build only (make sanitize): the host codecs are linked without the
-// device kernels, so the JPEG device halves are stubs that report no device.
+// device kernels, so the JPEG and JPEG 2000 device halves are stubs that report no device.
+#include "j2k.h"
 #include "jpeg.h"
 #include "runtime.h"
 
@@ -11,4 +12,13 @@ size_t jdec_scratch_bytes(const JdecHeader&) { return 0; }
 bool jdec_launch(const JdecHeader&, const uint8_t*, uint8_t*, uint8_t*, int32_t*, hipStream_t) {
   return fail("jpeg: no device in the sanitizer build");
 }
+namespace j2k {
+size_t decode_tmp_bytes(const Image&) { return 0; }
+bool decode_launch(const Image&, uint32_t*, uint8_t*, int64_t, void*, hipStream_t) {
+  return fail("jp2: no device in the sanitizer build");
+}
+bool encode_launch(const Image&, const uint8_t*, int64_t, uint32_t*, hipStream_t) {
+  return fail("jp2: no device in the sanitizer build");
+}
+}  // namespace j2k
 }  // namespace uph

@@ -176,6 +176,48 @@ static void jpeg(const char *fixtures) {
   }
 }
 
+/* the JPEG 2000 host half (j2k.cpp: boxes, markers, packet headers, tag
+ * trees, the MQ decoder and the coding passes) on the committed fixtures
+ * (tests/golden/j2k) and cut / bit-flipped copies: the fixtures must decode,
+ * nothing may crash */
+static void j2k(const char *fixtures) {
+  static const char *good[] = {"gray.jp2",         "rgb_mct.jp2",      "rgb_nomct.jp2",
+                               "tiled_rpcl.j2k",   "offset_tiles.jp2", "lossy_layers.jp2",
+                               "lossy_rgb.jp2",    "plt.jp2"};
+  static uint8_t raw[1 << 16], tmp[1 << 16];
+  char path[512];
+  unsigned seed = 12345;
+  for (size_t i = 0; i < sizeof good / sizeof *good; i++) {
+    snprintf(path, sizeof path, "%s/../j2k/%s", fixtures, good[i]);
+    FILE *f = fopen(path, "rb");
+    if (!f) {
+      fprintf(stderr, "j2k fixture %s missing\n", path);
+      g_fail++;
+      continue;
+    }
+    const size_t n = fread(raw, 1, sizeof raw, f);
+    fclose(f);
+    UphipPnmInfo info;
+    const int64_t need = uphip_jp2_entropy_decode(raw, n, NULL, 0, &info);
+    if (need <= 0) {
+      fprintf(stderr, "j2k %s: %s\n", path, uphip_last_error());
+      g_fail++;
+    }
+    uphip_clear_error();
+    for (size_t cut = 0; cut < n; cut += n / 29 + 1) {
+      uphip_jp2_entropy_decode(raw, cut, NULL, 0, &info); /* must not crash */
+      uphip_clear_error();
+      for (int k = 0; k < 3; k++) {
+        memcpy(tmp, raw, n);
+        seed = seed * 1103515245u + 12345u;
+        tmp[(cut + (seed >> 8)) % n] ^= (uint8_t)(1 + (seed >> 24) % 255);
+        uphip_jp2_entropy_decode(tmp, n, NULL, 0, &info);
+        uphip_clear_error();
+      }
+    }
+  }
+}
+
 /* crafted JPEG headers: an over-subscribed Huffman table must
  * be refused before it indexes the lookahead table, and a frame claiming far
  * more blocks than the file holds must fail without sizing anything from it */
@@ -256,6 +298,7 @@ int main(int argc, char **argv) {
   png(dir, argc > 2 ? argv[2] : "tests/golden/reference");
   jpeg(argc > 2 ? argv[2] : "tests/golden/reference");
   jpeg_crafted();
+  j2k(argc > 2 ? argv[2] : "tests/golden/reference");
   printf("sanitize: %d failures\n", g_fail);
   return g_fail ? 1 : 0;
 }

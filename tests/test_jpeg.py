@@ -107,6 +107,8 @@ def emulate(data):
     passes = C.c_int32()
     n = E.jdec_emulate(data, len(data), None, 0, C.byref(passes))
     if n < 0:
+        from unpaper_hip.device import load_library
+        load_library().uphip_clear_error()  # errors stick per thread until cleared
         return n, None, passes.value
     buf = np.zeros(n, np.uint8)
     assert E.jdec_emulate(data, len(data), buf.ctypes.data, n, C.byref(passes)) == n

@@ -1,0 +1,195 @@
+// kernels_j2k.hip — the device half of JPEG 2000 (j2k.h): inverse wavelet
+// transforms per resolution level (rows, then columns, as OpenJPEG's
+// dwt.c and the standard's 2D_SR), the inverse component transform, the DC
+// level shift and the store into the destination image; for the lossless
+// encoder the DC shift, the forward RCT and the forward 5/3 transform
+// (columns, then rows, per level).  A lane per row or column: the lines of
+// a level are independent, and the columns' lanes read one row of the plane
+// together (coalesced); `tmp` holds each lane's interleaved line.
+#include <algorithm>
+#include <type_traits>
+
+#include "j2k.h"
+#include "j2k_dwt.h"
+#include "runtime.h"
+
+namespace uph {
+namespace j2k {
+
+namespace {
+
+template <class T>
+__global__ void __launch_bounds__(256) k_j2k_rows(T* plane, int stride, int rw, int rh, int cas,
+                                                  T* tmp) {
+  const int y = blockIdx.x * 256 + threadIdx.x;
+  if (y >= rh) return;
+  T* row = plane + (int64_t)y * stride;
+  T* t = tmp + (int64_t)y * rw;
+  interleave(row, 1, rw, cas, t, 1);
+  if constexpr (std::is_integral<T>::value) idwt53_line((int32_t*)t, rw, cas, 1);
+  else idwt97_line((float*)t, rw, cas, 1);
+  for (int i = 0; i < rw; i++) row[i] = t[i];
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_j2k_cols(T* plane, int stride, int rw, int rh, int cas,
+                                                  T* tmp) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  if (x >= rw) return;
+  interleave(plane + x, stride, rh, cas, tmp + x, rw);
+  if constexpr (std::is_integral<T>::value) idwt53_line((int32_t*)(tmp + x), rh, cas, rw);
+  else idwt97_line((float*)(tmp + x), rh, cas, rw);
+  for (int i = 0; i < rh; i++) plane[(int64_t)i * stride + x] = tmp[(int64_t)i * rw + x];
+}
+
+// one tile into the image: inverse MCT, DC shift, clamp, store
+template <bool REV>
+__global__ void __launch_bounds__(256) k_j2k_out(const uint32_t* coef, Tile t, int ncomp,
+                                                 int32_t ox, int32_t oy, uint8_t* dst,
+                                                 int64_t pitch) {
+  const int w = t.x1 - t.x0, h = t.y1 - t.y0;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)w * h) return;
+  const int x = (int)(i % w), y = (int)(i / w);
+  uint8_t* d = dst + (int64_t)(t.y0 + y - oy) * pitch;
+  const int X = t.x0 + x - ox;
+  auto at = [&](int c) { return coef[t.tc[c].off + (int64_t)y * t.tc[c].stride + x]; };
+  if (ncomp == 1) {
+    if (REV) d[X] = clamp8((int32_t)at(0) + 128);
+    else d[X] = clamp8(round_half_even(__uint_as_float(at(0))) + 128);
+    return;
+  }
+  uint8_t r, g, b;
+  if (REV) {
+    const int32_t y0 = (int32_t)at(0), y1 = (int32_t)at(1), y2 = (int32_t)at(2);
+    if (t.mct) {
+      rct_inverse(y0, y1, y2, &r, &g, &b);
+    } else {
+      r = clamp8(y0 + 128);
+      g = clamp8(y1 + 128);
+      b = clamp8(y2 + 128);
+    }
+  } else {
+    const float y0 = __uint_as_float(at(0)), y1 = __uint_as_float(at(1)), y2 = __uint_as_float(at(2));
+    if (t.mct) {
+      ict_inverse(y0, y1, y2, &r, &g, &b);
+    } else {
+      r = clamp8(round_half_even(y0) + 128);
+      g = clamp8(round_half_even(y1) + 128);
+      b = clamp8(round_half_even(y2) + 128);
+    }
+  }
+  d[3 * X] = r;
+  d[3 * X + 1] = g;
+  d[3 * X + 2] = b;
+}
+
+// encoder: image -> DC-shifted (and RCT-transformed) integer planes
+__global__ void __launch_bounds__(256) k_j2k_in(const uint8_t* src, int64_t pitch, int w, int h,
+                                                int ncomp, uint32_t* coef) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)w * h) return;
+  const int x = (int)(i % w), y = (int)(i / w);
+  const uint8_t* s = src + (int64_t)y * pitch;
+  const int64_t n = (int64_t)w * h;
+  if (ncomp == 1) {
+    coef[i] = (uint32_t)((int32_t)s[x] - 128);
+    return;
+  }
+  const int32_t R = (int32_t)s[3 * x] - 128, G = (int32_t)s[3 * x + 1] - 128,
+                B = (int32_t)s[3 * x + 2] - 128;
+  coef[i] = (uint32_t)((R + 2 * G + B) >> 2);  // RCT (G.2.1)
+  coef[n + i] = (uint32_t)(B - G);
+  coef[2 * n + i] = (uint32_t)(R - G);
+}
+
+__global__ void __launch_bounds__(256) k_j2k_fcols(int32_t* plane, int stride, int rw, int rh,
+                                                   int cas, int32_t* tmp) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  if (x >= rw) return;
+  for (int i = 0; i < rh; i++) tmp[(int64_t)i * rw + x] = plane[(int64_t)i * stride + x];
+  fdwt53_line(tmp + x, rh, cas, rw);
+  deinterleave(tmp + x, rw, rh, cas, plane + x, stride);
+}
+__global__ void __launch_bounds__(256) k_j2k_frows(int32_t* plane, int stride, int rw, int rh,
+                                                   int cas, int32_t* tmp) {
+  const int y = blockIdx.x * 256 + threadIdx.x;
+  if (y >= rh) return;
+  int32_t* row = plane + (int64_t)y * stride;
+  int32_t* t = tmp + (int64_t)y * rw;
+  for (int i = 0; i < rw; i++) t[i] = row[i];
+  fdwt53_line(t, rw, cas, 1);
+  deinterleave(t, 1, rw, cas, row, 1);
+}
+
+unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+}  // namespace
+
+size_t decode_tmp_bytes(const Image& img) {
+  int64_t tmp_elems = 1;
+  for (const Tile& t : img.tiles)
+    tmp_elems = std::max<int64_t>(tmp_elems, (int64_t)(t.x1 - t.x0) * (t.y1 - t.y0));
+  return (size_t)tmp_elems * 4;
+}
+
+bool decode_launch(const Image& img, uint32_t* dcoef, uint8_t* dst, int64_t pitch, void* vtmp,
+                   hipStream_t st) {
+  uint32_t* tmp = (uint32_t*)vtmp;
+  if (!tmp) return fail("jp2: no line buffer");
+  for (const Tile& t : img.tiles) {
+    for (int c = 0; c < img.ncomp; c++) {
+      const TileComp& tc = t.tc[c];
+      for (int r = 1; r <= tc.nlevels; r++) {
+        const int rw = tc.rx1[r] - tc.rx0[r], rh = tc.ry1[r] - tc.ry0[r];
+        if (rw <= 0 || rh <= 0) continue;
+        uint32_t* plane = dcoef + tc.off;
+        if (img.reversible) {
+          hipLaunchKernelGGL(k_j2k_rows<int32_t>, dim3(blocks(rh)), dim3(256), 0, st,
+                             (int32_t*)plane, tc.stride, rw, rh, tc.rx0[r] & 1, (int32_t*)tmp);
+          hipLaunchKernelGGL(k_j2k_cols<int32_t>, dim3(blocks(rw)), dim3(256), 0, st,
+                             (int32_t*)plane, tc.stride, rw, rh, tc.ry0[r] & 1, (int32_t*)tmp);
+        } else {
+          hipLaunchKernelGGL(k_j2k_rows<float>, dim3(blocks(rh)), dim3(256), 0, st, (float*)plane,
+                             tc.stride, rw, rh, tc.rx0[r] & 1, (float*)tmp);
+          hipLaunchKernelGGL(k_j2k_cols<float>, dim3(blocks(rw)), dim3(256), 0, st, (float*)plane,
+                             tc.stride, rw, rh, tc.ry0[r] & 1, (float*)tmp);
+        }
+      }
+    }
+    const int64_t npx = (int64_t)(t.x1 - t.x0) * (t.y1 - t.y0);
+    if (img.reversible)
+      hipLaunchKernelGGL(k_j2k_out<true>, dim3(blocks(npx)), dim3(256), 0, st, dcoef, t, img.ncomp,
+                         img.x0, img.y0, dst, pitch);
+    else
+      hipLaunchKernelGGL(k_j2k_out<false>, dim3(blocks(npx)), dim3(256), 0, st, dcoef, t, img.ncomp,
+                         img.x0, img.y0, dst, pitch);
+  }
+  return UPH_HIP(hipGetLastError());
+}
+
+bool encode_launch(const Image& img, const uint8_t* src, int64_t pitch, uint32_t* dcoef,
+                   hipStream_t st) {
+  const Tile& t = img.tiles[0];
+  const int w = t.x1 - t.x0, h = t.y1 - t.y0;
+  int32_t* tmp = (int32_t*)scratch(7, (size_t)w * h * 4);
+  if (!tmp) return false;
+  hipLaunchKernelGGL(k_j2k_in, dim3(blocks((int64_t)w * h)), dim3(256), 0, st, src, pitch, w, h,
+                     img.ncomp, dcoef);
+  for (int c = 0; c < img.ncomp; c++) {
+    const TileComp& tc = t.tc[c];
+    int32_t* plane = (int32_t*)(dcoef + tc.off);
+    for (int r = tc.nlevels; r >= 1; r--) {
+      const int rw = tc.rx1[r] - tc.rx0[r], rh = tc.ry1[r] - tc.ry0[r];
+      if (rw <= 0 || rh <= 0) continue;
+      hipLaunchKernelGGL(k_j2k_fcols, dim3(blocks(rw)), dim3(256), 0, st, plane, tc.stride, rw, rh,
+                         tc.ry0[r] & 1, tmp);
+      hipLaunchKernelGGL(k_j2k_frows, dim3(blocks(rh)), dim3(256), 0, st, plane, tc.stride, rw, rh,
+                         tc.rx0[r] & 1, tmp);
+    }
+  }
+  return UPH_HIP(hipGetLastError());
+}
+
+}  // namespace j2k
+}  // namespace uph

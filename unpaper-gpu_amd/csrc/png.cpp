@@ -328,13 +328,18 @@ bool decode(Png& p, uint8_t* out, int64_t linesize, const char* path) {
   return in.finish() || fail("png: %s: corrupt image data (stream end, checksum)", path);
 }
 
-// the file's signature: 1 PNG, 2 JPEG (SOI + a marker), 0 anything else (PNM)
+// the file's signature: 1 PNG, 2 JPEG (SOI + a marker), 3 JPEG 2000 (the JP2
+// signature box or SOC + SIZ), 0 anything else (PNM)
 int sniff(FILE* f) {
-  uint8_t sig[8];
-  const size_t n = fread(sig, 1, 8, f);
+  uint8_t sig[12];
+  const size_t n = fread(sig, 1, 12, f);
   rewind(f);
-  if (n == 8 && memcmp(sig, kSig, 8) == 0) return 1;
+  static const uint8_t kJp2[12] = {0, 0, 0, 12, 0x6A, 0x50, 0x20, 0x20, 0x0D, 0x0A, 0x87, 0x0A};
+  if (n >= 8 && memcmp(sig, kSig, 8) == 0) return 1;
   if (n >= 3 && sig[0] == 0xFF && sig[1] == 0xD8 && sig[2] == 0xFF) return 2;
+  if ((n == 12 && memcmp(sig, kJp2, 12) == 0) ||
+      (n >= 4 && sig[0] == 0xFF && sig[1] == 0x4F && sig[2] == 0xFF && sig[3] == 0x51))
+    return 3;
   return 0;
 }
 
@@ -390,8 +395,8 @@ int uphip_png_read(const char* path, void* dst, int64_t linesize, const UphipPnm
 }
 
 // loadImage's peer over the codecs: the file's signature picks PNG, JPEG
-// (entropy-decoded on the host, pixels made on the current device: jpeg.cpp)
-// or PNM.
+// (entropy-decoded on the host, pixels made on the current device: jpeg.cpp),
+// JPEG 2000 (j2k.cpp, likewise split) or PNM.
 int uphip_image_probe(const char* path, UphipPnmInfo* info) {
   if (!path || !info) return fail("image_probe: null argument"), -1;
   FILE* f = fopen(path, "rb");
@@ -400,6 +405,7 @@ int uphip_image_probe(const char* path, UphipPnmInfo* info) {
   fclose(f);
   return kind == 1 ? uphip_png_probe(path, info)
        : kind == 2 ? uphip_jpeg_probe(path, info)
+       : kind == 3 ? uphip_jp2_probe(path, info)
                    : uphip_pnm_probe(path, info);
 }
 
@@ -411,6 +417,7 @@ int uphip_image_read(const char* path, void* dst, int64_t linesize, const UphipP
   fclose(f);
   return kind == 1 ? uphip_png_read(path, dst, linesize, expect)
        : kind == 2 ? uphip_jpeg_read(path, dst, linesize, expect)
+       : kind == 3 ? uphip_jp2_read(path, dst, linesize, expect)
                    : uphip_pnm_read(path, dst, linesize, expect);
 }
 

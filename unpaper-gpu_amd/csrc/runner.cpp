@@ -36,6 +36,7 @@
 #include <thread>
 #include <vector>
 
+#include "j2k.h"
 #include "jpeg.h"
 #include "runtime.h"
 
@@ -236,6 +237,9 @@ struct UphipSink {
   // JPEG files encoded on the device (uphip_sink_jpeg)
   bool jpeg = false;
   int32_t quality = UPHIP_JPEG_DEFAULT_QUALITY, sampling = UPHIP_JPEG_444;
+  // lossless JPEG 2000 files (uphip_sink_jp2): transforms on the device from
+  // the batch's output planes, code-blocks on the store tasks
+  bool jp2 = false;
   HostRegistration reg;
 };
 
@@ -380,6 +384,17 @@ UphipSink* uphip_sink_jpeg(const char* pattern, int64_t wrap, int32_t quality, i
   return k;
 }
 
+UphipSink* uphip_sink_jp2(const char* pattern, int64_t wrap) {
+  if (!pattern) return fail("sink_jp2: null pattern"), nullptr;
+  std::string fmt;
+  if (!output_pattern(pattern, &fmt)) return nullptr;
+  UphipSink* k = new UphipSink();
+  k->pattern = fmt;
+  k->wrap = wrap;
+  k->jp2 = true;
+  return k;
+}
+
 UphipSink* uphip_sink_discard(void) { return new UphipSink(); }
 
 void uphip_sink_destroy(UphipSink* k) { delete k; }
@@ -401,6 +416,10 @@ struct JpegPage {
   bool dev = false;         // Huffman-decoded on the device (host holds a JdecHeader stream)
   size_t bytes = 0;         // bytes to upload
   JpegHeader h{};
+  // a JPEG 2000 page instead: host holds its coefficient planes (j2k.h), the
+  // device runs the inverse transforms into the input slot
+  bool j2k = false;
+  j2k::Image img;
 };
 
 struct Slot {
@@ -581,6 +600,34 @@ void store_jpeg_sheet(UphipRunner* r, const UphipSink* k, int device, UphipBatch
   }
 }
 
+// The pages of sheet s as lossless JPEG 2000 files, each encoded from the
+// batch's output plane (uphip_jp2_encode on this task's own stream).
+void store_jp2_sheet(UphipRunner* r, const UphipSink* k, int device, UphipBatch* b, int64_t job,
+                     int s, bool* ok) {
+  thread_local std::vector<uint8_t> file;
+  const int oc = r->opts.output_count < 1 ? 1 : r->opts.output_count;
+  for (int j = 0; j < oc; j++) {
+    const int i = s * oc + j;
+    const std::string path = sink_path(k, job * oc + j);
+    const void* src = nullptr;
+    int64_t pitch = 0;
+    int32_t w = 0, h = 0, fmt = 0;
+    if (uphip_set_device(device) != 0 ||
+        uphip_batch_jpeg_page(b, i, &src, &pitch, &w, &h, &fmt) != 0) {
+      *ok = false;
+      continue;
+    }
+    const size_t guess = (size_t)w * h * (fmt == UPHIP_FMT_GRAY8 ? 1 : 3) / 2 + 65536;
+    if (file.size() < guess) file.resize(guess);
+    int64_t n = uphip_jp2_encode(src, pitch, w, h, fmt, file.data(), (int64_t)file.size());
+    if (n > (int64_t)file.size()) {
+      file.resize((size_t)n);
+      n = uphip_jp2_encode(src, pitch, w, h, fmt, file.data(), n);
+    }
+    if (n <= 0 || !write_file(path, file.data(), (size_t)n)) *ok = false;
+  }
+}
+
 bool is_jpeg_file(const std::string& path) {
   FILE* f = fopen(path.c_str(), "rb");
   if (!f) return false;
@@ -629,6 +676,49 @@ bool jpeg_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp
     jpeg_pack(d, jp->host);
   jp->h = dev ? S.hd.h : d.h;
   jp->dev = dev == 1;
+  jp->j2k = false;
+  jp->bytes = need;
+  jp->on = true;
+  return true;
+}
+
+bool is_j2k_file(const std::string& path) {
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) return false;
+  uint8_t sig[12];
+  const size_t n = fread(sig, 1, 12, f);
+  fclose(f);
+  return j2k::is_j2k(sig, n);
+}
+
+// The host half of a JPEG 2000 page (packet headers, code-blocks) into the
+// slot's pinned buffer `jp` as coefficient planes.
+bool j2k_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp) {
+  thread_local std::vector<uint8_t> file;
+  thread_local std::vector<uint32_t> coef;
+  if (!jpeg_read_file(path.c_str(), &file)) return false;
+  UphipPnmInfo info{0, 0, 0};
+  if (!j2k::probe(file.data(), file.size(), path.c_str(), &info)) return false;
+  if (info.width != r->geo.page_width || info.height != r->geo.page_height ||
+      info.format != r->geo.page_format)
+    return fail("jp2: %s is %dx%d format %d, expected %dx%d format %d", path.c_str(), info.width,
+                info.height, info.format, r->geo.page_width, r->geo.page_height,
+                r->geo.page_format);
+  if (!j2k::decode_host(file.data(), file.size(), path.c_str(), &jp->img, &coef)) return false;
+  if (uphip_set_device(device) != 0) return false;
+  const size_t need = coef.size() * 4;
+  if (jp->cap < need) {
+    if (jp->host) hipHostFree(jp->host);
+    jp->host = nullptr;
+    jp->cap = 0;
+    if (!UPH_HIP(hipHostMalloc((void**)&jp->host, need + need / 4, hipHostMallocDefault))) return false;
+    jp->cap = need + need / 4;
+  }
+  memcpy(jp->host, coef.data(), need);
+  jp->h = JpegHeader{};
+  jp->h.scratch_bytes = (int64_t)j2k::decode_tmp_bytes(jp->img);  // the line buffer
+  jp->j2k = true;
+  jp->dev = false;
   jp->bytes = need;
   jp->on = true;
   return true;
@@ -640,8 +730,11 @@ bool load_page(UphipRunner* r, int device, const UphipSource* s, int64_t job, in
   const int64_t idx = job * r->opts.input_count + j;
   if (s->load) return s->load(s->user, job, j, dst, r->in_pitch) == 0;
   if (s->base) return mem_load(s, idx, dst, r->in_pitch, geo) == 0;
-  if (idx >= 0 && idx < (int64_t)s->paths.size() && is_jpeg_file(s->paths[(size_t)idx]))
-    return jpeg_load(r, device, s->paths[(size_t)idx], jp);
+  if (idx >= 0 && idx < (int64_t)s->paths.size()) {
+    const std::string& path = s->paths[(size_t)idx];
+    if (is_jpeg_file(path)) return jpeg_load(r, device, path, jp);
+    if (is_j2k_file(path)) return j2k_load(r, device, path, jp);
+  }
   return pnm_load(s, idx, dst, r->in_pitch, geo) == 0;
 }
 
@@ -673,8 +766,11 @@ bool upload_staging(UphipRunner* r, Slot* sl, int npages) {
   return true;
 }
 
-// Queue the chunk's JPEG pages on the slot's stream: upload each packed page,
-// then decode it into its input slot (after the staging upload, before the run).
+// Queue the chunk's JPEG and JPEG 2000 pages on the slot's stream: upload each
+// packed page (JPEG 2000: its coefficient planes), then decode it into its
+// input slot (after the staging upload, before the run).
+size_t up256(size_t n) { return (n + 255) & ~(size_t)255; }
+
 bool jpeg_submit(Slot* sl, int npages) {
   size_t total = 0, scr = 0, pk = 0, hs = 0;
   int ndev = 0;
@@ -683,7 +779,7 @@ bool jpeg_submit(Slot* sl, int npages) {
   for (int p = 0; p < npages; p++) {
     const JpegPage& jp = sl->jpg[(size_t)p];
     if (!jp.on) continue;
-    total += jp.bytes;
+    total += up256(jp.bytes);  // page starts aligned (JPEG 2000 planes are int32)
     scr = std::max(scr, (size_t)jp.h.scratch_bytes);
     if (jp.dev) {
       const JdecHeader& hd = *(const JdecHeader*)jp.host;
@@ -744,7 +840,7 @@ bool jpeg_submit(Slot* sl, int npages) {
       poff += ((size_t)jp.h.total_bytes + 255) & ~(size_t)255;
       soff += (jdec_scratch_bytes(hd) + 255) & ~(size_t)255;
     }
-    off += jp.bytes;
+    off += up256(jp.bytes);
   }
   if (nj) {
     if (!UPH_HIP(hipMemcpyAsync(sl->djob, sl->hjob, sizeof(JdecJob) * (size_t)nj,
@@ -760,9 +856,15 @@ bool jpeg_submit(Slot* sl, int npages) {
     if (!jp.on) continue;
     int64_t pitch = 0;
     uint8_t* dst = (uint8_t*)uphip_batch_input_ptr(sl->b, p, &pitch);
+    if (jp.j2k) {
+      if (!dst || !j2k::decode_launch(jp.img, (uint32_t*)(sl->djpg + off), dst, pitch, sl->dscr, st))
+        return false;
+      off += up256(jp.bytes);
+      continue;
+    }
     const uint8_t* packed = jp.dev ? sl->hjob[k++].packed : sl->djpg + off;
     if (!dst || !jpeg_launch(jp.h, packed, sl->dscr, dst, pitch, st)) return false;
-    off += jp.bytes;
+    off += up256(jp.bytes);
   }
   return true;
 }
@@ -1292,6 +1394,8 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
                 if (queued) sl->hjpg_cap = cap;
               }
               queued = queued && uphip_batch_jpeg_download_async(sl->b, sl->hjpg, (int64_t)sl->hjpg_cap) == 0;
+            } else if (sink->jp2) {
+              queued = true;  // the store tasks encode from the batch's planes
             } else {
               queued = uphip_batch_download_async(sl->b, dst, r->out_linesize, r->out_sheet_stride) == 0;
             }
@@ -1330,6 +1434,8 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
                 if (sink->jpeg)
                   store_jpeg_sheet(r, sink, dc.device, sl->b, sl->first + s, s, sl->hjpg, sl->jsize,
                                    sl->joff, &good);
+                else if (sink->jp2)
+                  store_jp2_sheet(r, sink, dc.device, sl->b, sl->first + s, s, &good);
                 else
                   store_sheet(r, sink, sl->first + s, sl->hout + (int64_t)s * r->out_sheet_stride, &good);
                 if (!good) {

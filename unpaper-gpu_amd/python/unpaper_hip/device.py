@@ -55,7 +55,8 @@ EXPORTED = [
     "uphip_jpeg_entropy_decode", "uphip_runner_placement", "uphip_runner_slot_chunk",
     "uphip_jpeg_encode", "uphip_batch_encode_jpeg_async", "uphip_batch_jpeg_sizes",
     "uphip_batch_jpeg_download_async", "uphip_batch_jpeg_page", "uphip_sink_jpeg",
-    "uphip_detect_rotation_peaks",
+    "uphip_detect_rotation_peaks", "uphip_jp2_probe", "uphip_jp2_read", "uphip_jp2_decode",
+    "uphip_jp2_encode", "uphip_sink_jp2", "uphip_jp2_entropy_decode",
 ]
 
 
@@ -213,6 +214,15 @@ def load_library(path=LIB_PATH):
                                             C.POINTER(C.c_int64), C.POINTER(C.c_int32),
                                             C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
         "uphip_sink_jpeg": (C.c_void_p, [C.c_char_p, C.c_int64, C.c_int32, C.c_int32]),
+        "uphip_jp2_probe": (C.c_int, [C.c_char_p, C.POINTER(A.PnmInfo)]),
+        "uphip_jp2_read": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int64, C.POINTER(A.PnmInfo)]),
+        "uphip_jp2_decode": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64,
+                                       C.POINTER(A.PnmInfo)]),
+        "uphip_jp2_encode": (C.c_int64, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                         C.c_void_p, C.c_int64]),
+        "uphip_sink_jp2": (C.c_void_p, [C.c_char_p, C.c_int64]),
+        "uphip_jp2_entropy_decode": (C.c_int64, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64,
+                                                 C.POINTER(A.PnmInfo)]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(L, name):

@@ -363,6 +363,31 @@ def jpeg_encode(device_ptr, pitch, width, height, fmt, quality=0, sampling=0):
     return buf.tobytes()
 
 
+def sink_jp2(pattern, wrap=0):
+    """Lossless JPEG 2000 files (uphip_sink_jp2: transforms on the device,
+    code-blocks on the store tasks)."""
+    L = load_library()
+    h = L.uphip_sink_jp2(pattern.encode(), wrap)
+    _check(L)
+    return _Handle(h, L.uphip_sink_destroy)
+
+
+def jp2_encode(device_ptr, pitch, width, height, fmt):
+    """uphip_jp2_encode: one device image -> lossless JP2 file bytes."""
+    L = load_library()
+    cap = width * height * (1 if fmt == 0 else 3) // 2 + 65536
+    buf = np.zeros(cap, np.uint8)
+    n = L.uphip_jp2_encode(device_ptr, pitch, width, height, fmt, buf.ctypes.data, cap)
+    _check(L)
+    if n > cap:
+        buf = np.zeros(n, np.uint8)
+        n = L.uphip_jp2_encode(device_ptr, pitch, width, height, fmt, buf.ctypes.data, n)
+        _check(L)
+    if n <= 0:
+        raise UnpaperHipError("jp2_encode failed")
+    return buf[:n].tobytes()
+
+
 def sink_discard():
     L = load_library()
     return _Handle(L.uphip_sink_discard(), L.uphip_sink_destroy)
