@@ -2115,6 +2115,10 @@ __device__ void noise_resolve_components(const uint32_t* keys, uint32_t* aux, in
 constexpr int kCompCap = 16384;  // triggers the component replay keeps in LDS
 static_assert(kCompCap == 16384, "noise_scratch_bytes reserves 3 x 16384 words for k_noise_group");
 constexpr int kResolveThreads = 1024;
+#ifndef UPH_REPLAY_BLOCKS
+#define UPH_REPLAY_BLOCKS 4
+#endif
+constexpr int kReplayBlocks = UPH_REPLAY_BLOCKS;  // k_noise_replay blocks per sheet
 
 // The component replay in two kernels for intensity N <= 4 and at most
 // kCompCap triggers: k_noise_group (a block per sheet) orders the triggers
@@ -2260,11 +2264,8 @@ __global__ void __launch_bounds__(256) k_noise_replay(PlaneRef img, NoiseGeom g,
   if (active && !active[s]) return;
   NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
   const uint32_t n = *NP.nseq;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (NP.nclear[2] != 1u || i >= (int)n) return;
+  if (NP.nclear[2] != 1u || blockIdx.x * blockDim.x >= n) return;
   const uint32_t* gk = sortbuf + s * sort_stride;
-  if (gk[kCompCap + i] != (uint32_t)i) return;  // not a component's first trigger
-  const int last = (int)gk[2 * kCompCap + i];
   Mask81 rowp[5], colp[5];
 #pragma unroll
   for (int L = 1; L <= 4; L++) {
@@ -2272,12 +2273,18 @@ __global__ void __launch_bounds__(256) k_noise_replay(PlaneRef img, NoiseGeom g,
     colp[L] = ring_part(L, false);
   }
   uint8_t* base = plane_ptr(img, s);
-  for (int j = i; j <= last; j++) {
-    if (gk[kCompCap + j] != (uint32_t)i) continue;
-    const uint32_t key = gk[j];
-    __threadfence_block();  // this thread's earlier clears are visible to its loads
-    replay_trigger4<FMT>((int32_t)(key & 0xFFFF), (int32_t)(key >> 16), g.intensity, g, base,
-                         img.P.pitch, rowp, colp);
+  // a few blocks per sheet walk its triggers (sheets hold far fewer triggers
+  // than kCompCap: a grid sized for the cap was mostly blocks that exit)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)n; i += gridDim.x * blockDim.x) {
+    if (gk[kCompCap + i] != (uint32_t)i) continue;  // not a component's first trigger
+    const int last = (int)gk[2 * kCompCap + i];
+    for (int j = i; j <= last; j++) {
+      if (gk[kCompCap + j] != (uint32_t)i) continue;
+      const uint32_t key = gk[j];
+      __threadfence_block();  // this thread's earlier clears are visible to its loads
+      replay_trigger4<FMT>((int32_t)(key & 0xFFFF), (int32_t)(key >> 16), g.intensity, g, base,
+                           img.P.pitch, rowp, colp);
+    }
   }
 }
 
@@ -2480,7 +2487,7 @@ static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr
   if (!(diag_skip() & 2)) {
     hipLaunchKernelGGL(k_noise_group, dim3(count), dim3(1024), kGroupLds, st, g, scr, ss, active, ctl,
                        sortbuf, sort_stride);
-    hipLaunchKernelGGL(k_noise_replay<FMT>, dim3(kCompCap / 256, count), dim3(256), 0, st, img, g,
+    hipLaunchKernelGGL(k_noise_replay<FMT>, dim3(kReplayBlocks, count), dim3(256), 0, st, img, g,
                        scr, ss, active, sortbuf, sort_stride);
     hipLaunchKernelGGL(k_noise_resolve<FMT>, dim3(count), dim3(kResolveThreads), kResolveLds, st, img,
                        gd, scr, ss, active, ctl, sortbuf, sort_stride);
