@@ -146,7 +146,7 @@ $(JDEC_EMUL): tests/c/jdec_emul.cpp $(CSRC)/jpeg_huff_core.h $(CSRC)/jpeg.h $(LI
 # the JPEG 2000 decode's device half replayed on the CPU (test infrastructure)
 J2K_EMUL   := tests/c/_build/libj2k_emul.so
 j2k_emul: $(J2K_EMUL)
-$(J2K_EMUL): tests/c/j2k_emul.cpp $(CSRC)/j2k_dwt.h $(CSRC)/j2k.h $(LIB)
+$(J2K_EMUL): tests/c/j2k_emul.cpp $(CSRC)/j2k_dwt.h $(CSRC)/j2k.h $(CSRC)/j2k_t1.h $(CSRC)/j2k_t1_lane.h $(LIB)
 	@mkdir -p tests/c/_build
 	$(HIPCC) --cuda-host-only -x hip -O2 -std=c++17 -fPIC -shared -ffp-contract=off -Wall -Iinclude -I$(CSRC) $< -o $@ \
 	  -L$(PKG)/lib -lunpaper_hip -Wl,-rpath,'$$ORIGIN/../../../$(PKG)/lib'

@@ -7,11 +7,13 @@
 // forward transforms replayed, then j2k::encode_host).  Built by
 // `make j2k_emul`.
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
 #include "j2k.h"
 #include "j2k_dwt.h"
+#include "j2k_t1_lane.h"
 
 using namespace uph::j2k;
 
@@ -20,10 +22,65 @@ extern "C" {
 // Decodes `file` into out (rows of width * ncomp bytes); returns the byte
 // count (written when cap suffices) or -1 (uphip_last_error); info3 =
 // {width, height, ncomp}.
+static int64_t finish(const Image& img, std::vector<uint32_t>& coef, uint8_t* out, int64_t cap,
+                      int32_t* info3);
+
 int64_t j2k_emulate(const uint8_t* file, size_t n, uint8_t* out, int64_t cap, int32_t* info3) {
   Image img;
   std::vector<uint32_t> coef;
   if (!decode_host(file, n, "<emul>", &img, &coef)) return -1;
+  return finish(img, coef, out, cap, info3);
+}
+
+// The same with the code-blocks through the device decoder's lane code
+// (j2k_t1_lane.h, LS = 1): every job of a 64-job group decoded with the
+// group's width, height and pass count as the kernel's lanes are.
+int64_t j2k_emulate_t1lane(const uint8_t* file, size_t n, uint8_t* out, int64_t cap,
+                           int32_t* info3) {
+  Image img;
+  T1Batch tb;
+  if (!decode_host(file, n, "<emul>", &img, nullptr, &tb)) return -1;
+  std::vector<uint32_t> coef((size_t)img.coef_elems, 0u);
+  MqState qe[47];
+  for (int i = 0; i < 47; i++) qe[i] = kMq[i];
+  uint8_t zct[kZcTable];
+  zc_table(zct);
+  const int njobs = (int)tb.jobs.size();
+  std::vector<uint16_t> fl;
+  std::vector<uint32_t> val;
+  uint8_t cx[kNumCtx];
+  for (int g0 = 0; g0 < njobs; g0 += 64) {
+    int Wg = 0, Hg = 0, P = 0;
+    for (int j = g0; j < njobs && j < g0 + 64; j++) {
+      Wg = std::max(Wg, (int)tb.jobs[(size_t)j].w);
+      Hg = std::max(Hg, (int)tb.jobs[(size_t)j].h);
+      P = std::max(P, (int)tb.jobs[(size_t)j].npasses);
+    }
+    for (int j = g0; j < njobs && j < g0 + 64; j++) {
+      const T1Job& job = tb.jobs[(size_t)j];
+      fl.assign((size_t)((Hg + 3) / 4 + 2) * (Wg + 2), 0xABCD);  // the lane code zeroes them
+      val.assign((size_t)Hg * Wg, 0x5A5A5A5A);
+      T1Lane<1> L;
+      L.WS = Wg + 2;
+      L.Wg = Wg;
+      L.fl = fl.data();
+      L.val = val.data();
+      L.cx = cx;
+      L.qe = qe;
+      L.zct = zct;
+      L.w = job.w;
+      L.h = job.h;
+      L.orient = job.orient;
+      t1_decode_lane(L, true, tb.data.data() + job.data, job.numbps, job.npasses, (Hg + 3) / 4, P,
+                     [](bool b) { return b; });
+      t1_store_lane(L, true, job, coef.data(), Hg);
+    }
+  }
+  return finish(img, coef, out, cap, info3);
+}
+
+static int64_t finish(const Image& img, std::vector<uint32_t>& coef, uint8_t* out, int64_t cap,
+                      int32_t* info3) {
   info3[0] = img.width;
   info3[1] = img.height;
   info3[2] = img.ncomp;

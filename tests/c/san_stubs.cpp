@@ -14,6 +14,10 @@ bool jdec_launch(const JdecHeader&, const uint8_t*, uint8_t*, uint8_t*, int32_t*
 }
 namespace j2k {
 size_t decode_tmp_bytes(const Image&) { return 0; }
+size_t t1_slot_bytes(int, int) { return 0; }
+bool t1_launch(const T1Job*, int, const uint8_t*, uint32_t*, void*, int, int, int, hipStream_t) {
+  return fail("jp2: no device in the sanitizer build");
+}
 bool decode_launch(const Image&, uint32_t*, uint8_t*, int64_t, void*, hipStream_t) {
   return fail("jp2: no device in the sanitizer build");
 }

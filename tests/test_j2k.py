@@ -8,7 +8,9 @@ parity is pinned to OpenJPEG 2.5 (PIL's JPEG 2000 codec), the decoder
 nvImageCodec's CPU JPEG 2000 plugin also wraps:
 
 - CPU: the decoder's host half + the device half replayed on the CPU
-  (tests/c/j2k_emul.cpp, same line functions) equals PIL's decode byte for
+  (tests/c/j2k_emul.cpp: the device code-block decoder's lane code,
+  j2k_t1_lane.h, in 64-block groups, and the same line functions; also the
+  host code-block coder of j2k_t1.h) equals PIL's decode byte for
   byte on committed fixtures (tests/golden/j2k, tests/golden/make_j2k_fixtures.py)
   and a seeded matrix of encoder options (tiles, offsets, precincts,
   progression orders, code-block sizes, quality layers, 5/3 and 9/7, RCT/ICT);
@@ -40,6 +42,8 @@ def _emul():
     E = C.CDLL(EMUL)
     E.j2k_emulate.restype = C.c_int64
     E.j2k_emulate.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64, C.c_void_p]
+    E.j2k_emulate_t1lane.restype = C.c_int64
+    E.j2k_emulate_t1lane.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64, C.c_void_p]
     E.j2k_emulate_encode.restype = C.c_int64
     E.j2k_emulate_encode.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                      C.c_int64]
@@ -54,14 +58,18 @@ def _err():
     return e.decode() if e else None
 
 
-def emulate_decode(data):
+def emulate_decode(data, lane=False):
+    """The host half, then the code-blocks through j2k_t1.h's coder (or, with
+    lane, the device decoder's lane code in 64-block groups) and the device
+    half's line functions."""
     E = _emul()
+    fn = E.j2k_emulate_t1lane if lane else E.j2k_emulate
     info = (C.c_int32 * 3)()
-    n = E.j2k_emulate(data, len(data), None, 0, info)
+    n = fn(data, len(data), None, 0, info)
     if n < 0:
         raise ValueError(_err())
     out = np.zeros(n, np.uint8)
-    assert E.j2k_emulate(data, len(data), out.ctypes.data, n, info) == n
+    assert fn(data, len(data), out.ctypes.data, n, info) == n
     w, h, c = info
     return out.reshape(h, w, c) if c > 1 else out.reshape(h, w)
 
@@ -128,10 +136,11 @@ OPTIONS = [
 
 @pytest.mark.parametrize("name", sorted(os.path.basename(p) for p in
                                         glob.glob(os.path.join(FIXTURES, "*.j*"))))
-def test_fixtures_decode_as_openjpeg(name):
+@pytest.mark.parametrize("lane", [False, True])
+def test_fixtures_decode_as_openjpeg(name, lane):
     data = open(os.path.join(FIXTURES, name), "rb").read()
     exp = np.load(os.path.join(FIXTURES, name.rsplit(".", 1)[0] + ".npy"))
-    got = emulate_decode(data)
+    got = emulate_decode(data, lane)
     assert got.shape == exp.shape and (got == exp).all(), name
 
 
@@ -146,9 +155,10 @@ def test_decode_matches_openjpeg(opt, rgb, mct):
             continue
         a = page(w, h, opt * 7 + w, rgb)
         data = pil_save(a, **kw)
-        got = emulate_decode(data)
         exp = pil_decode(data)
-        assert got.shape == exp.shape and (got == exp).all(), (kw, w, h)
+        for lane in (False, True):
+            got = emulate_decode(data, lane)
+            assert got.shape == exp.shape and (got == exp).all(), (kw, w, h, lane)
         if not kw.get("irreversible") and "quality_layers" not in kw:
             assert (got == a).all()  # lossless
 

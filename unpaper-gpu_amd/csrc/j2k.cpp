@@ -14,6 +14,7 @@
 #include <string>
 
 #include "j2k_t1.h"
+#include "j2k_t1_lane.h"
 #include "runtime.h"
 
 namespace uph {
@@ -756,7 +757,7 @@ bool probe(const uint8_t* d, size_t n, const char* name, UphipPnmInfo* info) {
 }
 
 bool decode_host(const uint8_t* d, size_t n, const char* name, Image* img,
-                 std::vector<uint32_t>* coef) {
+                 std::vector<uint32_t>* coef, T1Batch* t1) {
   try {
     std::unique_ptr<Stream> Sp(new Stream);
     Stream& S = *Sp;
@@ -788,7 +789,13 @@ bool decode_host(const uint8_t* d, size_t n, const char* name, Image* img,
       }
     }
     img->coef_elems = total;
-    coef->assign((size_t)total, 0u);
+    if (t1) {
+      t1->jobs.clear();
+      t1->data.clear();
+      t1->maxw = t1->maxh = 0;
+    } else {
+      coef->assign((size_t)total, 0u);
+    }
     std::vector<uint8_t> flags;
     std::vector<int32_t> vals;
     std::vector<uint8_t> buf;
@@ -806,7 +813,7 @@ bool decode_host(const uint8_t* d, size_t n, const char* name, Image* img,
       // Tier 1 into the planes
       for (int c = 0; c < z.C; c++) {
         const TileComp& tc = T.tc[c];
-        uint32_t* plane = coef->data() + tc.off;
+        uint32_t* plane = t1 ? nullptr : coef->data() + tc.off;
         for (auto& R : st[(size_t)c].res)
           for (int b = 0; b < R.nbands; b++) {
             Band& B = R.band[b];
@@ -815,6 +822,30 @@ bool decode_host(const uint8_t* d, size_t n, const char* name, Image* img,
               const int w = cb.x1 - cb.x0, h = cb.y1 - cb.y0;
               if (w <= 0 || h <= 0) continue;
               if (cb.numbps <= 0 || cb.numbps > 30) return jfail(name, "bad code-block bit-planes");
+              if (t1) {  // for the device decoder
+                T1Job job;
+                job.data = (uint32_t)t1->data.size();
+                job.len = (uint32_t)cb.data.size();
+                job.out = tc.off + (int64_t)(B.py + cb.y0 - B.y0) * tc.stride + (B.px + cb.x0 - B.x0);
+                job.stride = tc.stride;
+                job.w = (uint16_t)w;
+                job.h = (uint16_t)h;
+                job.orient = (uint8_t)B.orient;
+                job.numbps = (uint8_t)cb.numbps;
+                // passes past plane 1 decode nothing
+                job.npasses = (uint8_t)std::min(cb.npasses, 3 * cb.numbps - 2);
+                job.pad = 0;
+                job.halfstep = img->reversible ? 0.0f : 0.5f * B.step;
+                t1->jobs.push_back(job);
+                t1->data.insert(t1->data.end(), cb.data.begin(), cb.data.end());
+                t1->data.push_back(0xFF);
+                t1->data.push_back(0xFF);
+                while (t1->data.size() & 3) t1->data.push_back(0);
+                t1->maxw = std::max(t1->maxw, w);
+                t1->maxh = std::max(t1->maxh, h);
+                if (t1->data.size() > 0xFFFFFFF0u) return jfail(name, "code-block data too large");
+                continue;
+              }
               flags.assign((size_t)(w + 2) * (h + 2), 0);
               vals.assign((size_t)w * h, 0);
               buf.assign(cb.data.begin(), cb.data.end());
@@ -845,6 +876,12 @@ bool decode_host(const uint8_t* d, size_t n, const char* name, Image* img,
           }
       }
     }
+    if (t1)  // alike blocks share a wave: by width, height, then passes
+      std::stable_sort(t1->jobs.begin(), t1->jobs.end(), [](const T1Job& x, const T1Job& y) {
+        if (x.w != y.w) return x.w > y.w;
+        if (x.h != y.h) return x.h > y.h;
+        return x.npasses > y.npasses;
+      });
     return true;
   } catch (const std::bad_alloc&) {
     return fail("jp2: %s: out of memory", name);
@@ -1202,11 +1239,13 @@ using namespace uph;
 
 namespace {
 
+constexpr int kT1MaxSlots = 1024;  // k_j2k_t1 workgroups (scratch slots) of one launch
+
 bool j2k_decode_to_device(const uint8_t* data, size_t size, const char* name, uint8_t* ddst,
                           int64_t pitch, UphipPnmInfo* info) {
   j2k::Image img;
-  std::vector<uint32_t> coef;
-  if (!j2k::decode_host(data, size, name, &img, &coef)) return false;
+  j2k::T1Batch tb;
+  if (!j2k::decode_host(data, size, name, &img, nullptr, &tb)) return false;
   const int fmt = img.ncomp == 1 ? UPHIP_FMT_GRAY8 : UPHIP_FMT_RGB24;
   if (info) {
     if (info->width > 0 && (info->width != img.width || info->height != img.height || info->format != fmt))
@@ -1217,11 +1256,22 @@ bool j2k_decode_to_device(const uint8_t* data, size_t size, const char* name, ui
     info->format = fmt;
   }
   if (pitch < (int64_t)img.width * img.ncomp) return fail("jp2: pitch too small");
+  // code-block jobs and codewords up, coefficients decoded on the device
   hipStream_t st = current_stream();
-  uint32_t* dc = (uint32_t*)scratch(6, coef.size() * 4 + 4);
+  const int njobs = (int)tb.jobs.size();
+  const size_t jb = (sizeof(j2k::T1Job) * (size_t)njobs + 255) & ~(size_t)255;
+  const int nslots = std::min((njobs + 63) / 64, kT1MaxSlots);
+  uint8_t* dup = (uint8_t*)scratch(3, jb + tb.data.size() + 4);
+  uint32_t* dc = (uint32_t*)scratch(6, (size_t)img.coef_elems * 4 + 4);
   void* tmp = scratch(7, j2k::decode_tmp_bytes(img));
-  return dc && tmp &&
-         UPH_HIP(hipMemcpyAsync(dc, coef.data(), coef.size() * 4, hipMemcpyHostToDevice, st)) &&
+  void* t1s = scratch(4, (size_t)std::max(nslots, 1) * j2k::t1_slot_bytes(tb.maxw, tb.maxh));
+  return dup && dc && tmp && t1s &&
+         (njobs == 0 || UPH_HIP(hipMemcpyAsync(dup, tb.jobs.data(), sizeof(j2k::T1Job) * (size_t)njobs,
+                                               hipMemcpyHostToDevice, st))) &&
+         (tb.data.empty() || UPH_HIP(hipMemcpyAsync(dup + jb, tb.data.data(), tb.data.size(),
+                                                    hipMemcpyHostToDevice, st))) &&
+         UPH_HIP(hipMemsetAsync(dc, 0, (size_t)img.coef_elems * 4, st)) &&
+         j2k::t1_launch((const j2k::T1Job*)dup, njobs, dup + jb, dc, t1s, nslots, tb.maxw, tb.maxh, st) &&
          j2k::decode_launch(img, dc, ddst, pitch, tmp, st) && UPH_HIP(hipStreamSynchronize(st));
 }
 

@@ -61,8 +61,20 @@ struct Image {
 // decoder does not take: precision other than 8 unsigned, subsampled
 // components, 2 or 4+ components, code-block styles other than 0, region of
 // interest, progression order changes, packed packet headers.
+struct T1Job;
+// The code-blocks of a file for the device decoder (k_j2k_t1): jobs sorted
+// by shape and pass count, their codewords back to back (each followed by
+// 0xFF 0xFF, offsets 4-byte aligned).
+struct T1Batch {
+  std::vector<T1Job> jobs;
+  std::vector<uint8_t> data;
+  int maxw = 0, maxh = 0;
+};
+// With `t1`, the code-blocks are not decoded here: they are appended to *t1
+// (coef is then not touched and may be null); the device decodes them into a
+// zeroed coefficient buffer (t1_launch) before decode_launch.
 bool decode_host(const uint8_t* data, size_t size, const char* name, Image* img,
-                 std::vector<uint32_t>* coef);
+                 std::vector<uint32_t>* coef, T1Batch* t1 = nullptr);
 // Geometry only (width, height, GRAY8 / RGB24).
 bool probe(const uint8_t* data, size_t size, const char* name, UphipPnmInfo* info);
 // Whether the bytes start a JP2 file or a J2K codestream.
@@ -75,6 +87,15 @@ bool is_j2k(const uint8_t* data, size_t size);
 size_t decode_tmp_bytes(const Image& img);
 bool decode_launch(const Image& img, uint32_t* dcoef, uint8_t* dst, int64_t pitch, void* tmp,
                    hipStream_t st);
+
+// The device code-block decoder: one wave (a workgroup of 64) per 64 jobs,
+// `nslots` workgroups walking the groups, each with a scratch slot of
+// t1_slot_bytes(maxw, maxh) bytes; writes every sample of every job's block
+// into dcoef (samples of blocks without passes stay as they are: zero them
+// first).
+size_t t1_slot_bytes(int maxw, int maxh);
+bool t1_launch(const T1Job* djobs, int njobs, const uint8_t* ddata, uint32_t* dcoef, void* dscr,
+               int nslots, int maxw, int maxh, hipStream_t st);
 
 // Lossless encode: the device transforms `src` (GRAY8 or RGB24) into the
 // coefficient planes (`dcoef`, laid out as decode_host's for the encoder's

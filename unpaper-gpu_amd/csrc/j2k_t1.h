@@ -12,8 +12,13 @@
 // the quantisation step.
 #pragma once
 
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
+
+#ifndef J2K_HD
+#define J2K_HD __host__ __device__
+#endif
 
 namespace uph {
 namespace j2k {
@@ -215,7 +220,7 @@ constexpr uint8_t kSig = 1, kNeg = 2, kVisit = 4, kRefined = 8;
 
 // Zero-coding context (Table D.1) from the significant neighbours; orient 0
 // LL, 1 HL, 2 LH, 3 HH.
-inline int zc_ctx(int orient, int h, int v, int d) {
+J2K_HD inline int zc_ctx(int orient, int h, int v, int d) {
   if (orient == 1) {
     const int t = h;
     h = v;

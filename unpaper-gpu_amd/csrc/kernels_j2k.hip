@@ -11,6 +11,7 @@
 
 #include "j2k.h"
 #include "j2k_dwt.h"
+#include "j2k_t1_lane.h"
 #include "runtime.h"
 
 namespace uph {
@@ -124,7 +125,70 @@ __global__ void __launch_bounds__(256) k_j2k_frows(int32_t* plane, int stride, i
 
 unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
 
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// EBCOT code-block decode, a lane per block (j2k_t1_lane.h): the MQ tables
+// and the context bytes in LDS, flags and values in the block's scratch slot
+// laid out lane-minor (coalesced), the decoded block into the coefficients.
+__global__ void __launch_bounds__(64) k_j2k_t1(const T1Job* jobs, int njobs, const uint8_t* data,
+                                               uint32_t* coef, uint8_t* scr, int64_t slot_bytes,
+                                               int64_t val_off) {
+  __shared__ MqState qe[47];
+  __shared__ uint8_t zct[kZcTable];
+  __shared__ uint8_t cxs[kNumCtx * 64];
+  const int lane = threadIdx.x;
+  if (lane < 47) qe[lane] = kMq[lane];
+  for (int i = lane; i < kZcTable; i += 64) {
+    const int r = i % 45;
+    zct[i] = (uint8_t)zc_ctx(i / 45, r / 15, (r / 5) % 3, r % 5);
+  }
+  __syncthreads();
+  const int ngroups = (njobs + 63) >> 6;
+  uint8_t* slot = scr + (int64_t)blockIdx.x * slot_bytes;
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int j = g * 64 + lane;
+    const bool active = j < njobs;
+    T1Job job{};
+    if (active) job = jobs[j];
+    const int Wg = wave_max(job.w), Hg = wave_max(job.h), P = wave_max(job.npasses);
+    T1Lane<64> L;
+    L.WS = Wg + 2;
+    L.Wg = Wg;
+    L.fl = reinterpret_cast<uint16_t*>(slot) + lane;
+    L.val = reinterpret_cast<uint32_t*>(slot + val_off) + lane;
+    L.cx = cxs + lane;
+    L.qe = qe;
+    L.zct = zct;
+    L.w = job.w;
+    L.h = job.h;
+    L.orient = job.orient;
+    t1_decode_lane(L, active, data + job.data, job.numbps, job.npasses, (Hg + 3) >> 2, P,
+                   [](bool b) { return __ballot(b) != 0; });
+    t1_store_lane(L, active, job, coef, Hg);
+  }
+}
+
 }  // namespace
+
+size_t t1_slot_bytes(int maxw, int maxh) {
+  const size_t flags = (((size_t)((maxh + 3) / 4 + 2) * (size_t)(maxw + 2) * 64 * 2) + 255) & ~(size_t)255;
+  return flags + (size_t)maxw * (size_t)maxh * 64 * 4;
+}
+
+bool t1_launch(const T1Job* djobs, int njobs, const uint8_t* ddata, uint32_t* dcoef, void* dscr,
+               int nslots, int maxw, int maxh, hipStream_t st) {
+  if (njobs <= 0) return true;
+  const int64_t slot = (int64_t)t1_slot_bytes(maxw, maxh);
+  const int64_t val_off =
+      (int64_t)((((size_t)((maxh + 3) / 4 + 2) * (size_t)(maxw + 2) * 64 * 2) + 255) & ~(size_t)255);
+  hipLaunchKernelGGL(k_j2k_t1, dim3((unsigned)nslots), dim3(64), 0, st, djobs, njobs, ddata, dcoef,
+                     (uint8_t*)dscr, slot, val_off);
+  return UPH_HIP(hipGetLastError());
+}
 
 size_t decode_tmp_bytes(const Image& img) {
   int64_t tmp_elems = 1;

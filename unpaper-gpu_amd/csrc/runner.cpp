@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "j2k.h"
+#include "j2k_t1_lane.h"
 #include "jpeg.h"
 #include "runtime.h"
 
@@ -416,16 +417,29 @@ struct JpegPage {
   bool dev = false;         // Huffman-decoded on the device (host holds a JdecHeader stream)
   size_t bytes = 0;         // bytes to upload
   JpegHeader h{};
-  // a JPEG 2000 page instead: host holds its coefficient planes (j2k.h), the
-  // device runs the inverse transforms into the input slot
+  // a JPEG 2000 page instead: host holds its code-block jobs (j2k_t1_lane.h;
+  // offsets relative to the page) then their codewords; the device decodes
+  // the code-blocks of all the chunk's JPEG 2000 pages in one launch, then
+  // runs each page's inverse transforms into its input slot
   bool j2k = false;
   j2k::Image img;
+  int32_t njobs = 0;
+  size_t jobs_bytes = 0;  // 256-aligned
+  int maxw = 0, maxh = 0;
 };
 
 struct Slot {
   std::vector<JpegPage> jpg;  // per page of the chunk (sheet * input_count + page)
   uint8_t* djpg = nullptr;    // device copies of the chunk's packed JPEG pages
   size_t djpg_cap = 0;
+  j2k::T1Job* hj2j = nullptr; // the chunk's JPEG 2000 jobs, offsets made chunk-wide (pinned)
+  size_t hj2j_cap = 0;
+  j2k::T1Job* dj2j = nullptr; // their device copy
+  size_t dj2j_cap = 0;
+  uint32_t* dj2c = nullptr;   // the JPEG 2000 pages' coefficient planes
+  size_t dj2c_cap = 0;
+  uint8_t* dj2t = nullptr;    // k_j2k_t1 scratch slots
+  size_t dj2t_cap = 0;
   uint8_t* dscr = nullptr;    // colour planes (one page at a time on the stream)
   size_t dscr_cap = 0;
   uint8_t* djpk = nullptr;    // packed coefficients of the device-decoded pages
@@ -691,11 +705,11 @@ bool is_j2k_file(const std::string& path) {
   return j2k::is_j2k(sig, n);
 }
 
-// The host half of a JPEG 2000 page (packet headers, code-blocks) into the
-// slot's pinned buffer `jp` as coefficient planes.
+// The host half of a JPEG 2000 page (headers, packet headers) into the
+// slot's pinned buffer `jp`: its code-block jobs, then their codewords.
 bool j2k_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp) {
   thread_local std::vector<uint8_t> file;
-  thread_local std::vector<uint32_t> coef;
+  thread_local j2k::T1Batch tb;
   if (!jpeg_read_file(path.c_str(), &file)) return false;
   UphipPnmInfo info{0, 0, 0};
   if (!j2k::probe(file.data(), file.size(), path.c_str(), &info)) return false;
@@ -704,9 +718,13 @@ bool j2k_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp)
     return fail("jp2: %s is %dx%d format %d, expected %dx%d format %d", path.c_str(), info.width,
                 info.height, info.format, r->geo.page_width, r->geo.page_height,
                 r->geo.page_format);
-  if (!j2k::decode_host(file.data(), file.size(), path.c_str(), &jp->img, &coef)) return false;
+  if (!j2k::decode_host(file.data(), file.size(), path.c_str(), &jp->img, nullptr, &tb)) return false;
   if (uphip_set_device(device) != 0) return false;
-  const size_t need = coef.size() * 4;
+  jp->njobs = (int32_t)tb.jobs.size();
+  jp->jobs_bytes = (sizeof(j2k::T1Job) * tb.jobs.size() + 255) & ~(size_t)255;
+  jp->maxw = tb.maxw;
+  jp->maxh = tb.maxh;
+  const size_t need = jp->jobs_bytes + tb.data.size();
   if (jp->cap < need) {
     if (jp->host) hipHostFree(jp->host);
     jp->host = nullptr;
@@ -714,7 +732,8 @@ bool j2k_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp)
     if (!UPH_HIP(hipHostMalloc((void**)&jp->host, need + need / 4, hipHostMallocDefault))) return false;
     jp->cap = need + need / 4;
   }
-  memcpy(jp->host, coef.data(), need);
+  memcpy(jp->host, tb.jobs.data(), sizeof(j2k::T1Job) * tb.jobs.size());
+  memcpy(jp->host + jp->jobs_bytes, tb.data.data(), tb.data.size());
   jp->h = JpegHeader{};
   jp->h.scratch_bytes = (int64_t)j2k::decode_tmp_bytes(jp->img);  // the line buffer
   jp->j2k = true;
@@ -848,17 +867,71 @@ bool jpeg_submit(Slot* sl, int npages) {
         !jdec_launch_batch(sl->djob, nj, max_nsub, max_nmac, st))
       return false;
   }
+  // JPEG 2000 pages: every code-block of the chunk in one launch (offsets
+  // made chunk-wide), into one coefficient buffer
+  {
+    int64_t nj = 0, coefs = 0;
+    int maxw = 0, maxh = 0;
+    for (int p = 0; p < npages; p++) {
+      const JpegPage& jp = sl->jpg[(size_t)p];
+      if (!jp.on || !jp.j2k) continue;
+      nj += jp.njobs;
+      coefs += jp.img.coef_elems;
+      maxw = std::max(maxw, jp.maxw);
+      maxh = std::max(maxh, jp.maxh);
+    }
+    if (coefs > 0) {
+      const int nslots = (int)std::min<int64_t>((nj + 63) / 64, 1024);
+      if (!grow(&sl->dj2c, &sl->dj2c_cap, (size_t)coefs * 4) ||
+          !grow(&sl->dj2t, &sl->dj2t_cap, (size_t)std::max(nslots, 1) * j2k::t1_slot_bytes(maxw, maxh)) ||
+          !grow(&sl->dj2j, &sl->dj2j_cap, sizeof(j2k::T1Job) * (size_t)std::max<int64_t>(nj, 1)))
+        return false;
+      if (sl->hj2j_cap < (size_t)nj) {
+        if (sl->hj2j) hipHostFree(sl->hj2j);
+        sl->hj2j = nullptr;
+        sl->hj2j_cap = 0;
+        if (!UPH_HIP(hipHostMalloc((void**)&sl->hj2j, sizeof(j2k::T1Job) * (size_t)nj + 256,
+                                   hipHostMallocDefault)))
+          return false;
+        sl->hj2j_cap = (size_t)nj;
+      }
+      size_t o = 0;
+      int64_t q = 0, cb = 0;
+      for (int p = 0; p < npages; p++) {
+        const JpegPage& jp = sl->jpg[(size_t)p];
+        if (!jp.on) continue;
+        if (jp.j2k) {
+          const j2k::T1Job* pj = reinterpret_cast<const j2k::T1Job*>(jp.host);
+          for (int i = 0; i < jp.njobs; i++) {
+            j2k::T1Job t = pj[i];
+            t.data += (uint32_t)(o + jp.jobs_bytes);
+            t.out += cb;
+            sl->hj2j[q++] = t;
+          }
+          cb += jp.img.coef_elems;
+        }
+        o += up256(jp.bytes);
+      }
+      if (o > 0xFFFFFFF0u) return fail("jp2: chunk too large for 32-bit codeword offsets");
+      if (!UPH_HIP(hipMemcpyAsync(sl->dj2j, sl->hj2j, sizeof(j2k::T1Job) * (size_t)nj,
+                                  hipMemcpyHostToDevice, st)) ||
+          !UPH_HIP(hipMemsetAsync(sl->dj2c, 0, (size_t)coefs * 4, st)) ||
+          !j2k::t1_launch(sl->dj2j, (int)nj, sl->djpg, sl->dj2c, sl->dj2t, nslots, maxw, maxh, st))
+        return false;
+    }
+  }
   // pixels: each page from its packed coefficients into its input slot
   off = 0;
   int k = 0;
+  int64_t cb = 0;
   for (int p = 0; p < npages; p++) {
     JpegPage& jp = sl->jpg[(size_t)p];
     if (!jp.on) continue;
     int64_t pitch = 0;
     uint8_t* dst = (uint8_t*)uphip_batch_input_ptr(sl->b, p, &pitch);
     if (jp.j2k) {
-      if (!dst || !j2k::decode_launch(jp.img, (uint32_t*)(sl->djpg + off), dst, pitch, sl->dscr, st))
-        return false;
+      if (!dst || !j2k::decode_launch(jp.img, sl->dj2c + cb, dst, pitch, sl->dscr, st)) return false;
+      cb += jp.img.coef_elems;
       off += up256(jp.bytes);
       continue;
     }
@@ -1021,6 +1094,10 @@ void uphip_runner_destroy(UphipRunner* r) {
       if (sl.djob) hipFree(sl.djob);
       if (sl.hjob) hipHostFree(sl.hjob);
       if (sl.hjpg) hipHostFree(sl.hjpg);
+      if (sl.hj2j) hipHostFree(sl.hj2j);
+      if (sl.dj2j) hipFree(sl.dj2j);
+      if (sl.dj2c) hipFree(sl.dj2c);
+      if (sl.dj2t) hipFree(sl.dj2t);
       for (JpegPage& jp : sl.jpg)
         if (jp.host) hipHostFree(jp.host);
     }
