@@ -89,7 +89,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c3", choices=("c3", "c4", "jpeg"),
+    ap.add_argument("--config", default="c3", choices=("c3", "c4", "jpeg", "jp2"),
                     help="c3: BASELINE configs[2] (the metric); c4: configs[3], RGB24 600dpi "
                          "double-page sheets, layout double, bilinear, border wipe; jpeg: the "
                          "JPEG decode peer (SURVEY f3) feeding the runner from JPEG files")
@@ -441,7 +441,7 @@ def host_threads_share():
         return os.cpu_count() or 1
 
 
-def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid):
+def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid, codec="jpeg"):
     """The JPEG decode peer in the runner: synthetic A4 GRAY8
     pages saved by PIL as JPEG quality 95 (tmpfs), read by a runner file
     source (marker parse + unstuffing on the load pool into pinned memory;
@@ -449,7 +449,10 @@ def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid):
     IDCT into the batch's input slots, on the device), the default pipeline,
     sheets discarded.  PCIe- and host-inclusive: a figure of its own, never `value`
     of the C3 line.  Two pages' outputs are checked against the oracle on
-    PIL's decode of the same files."""
+    PIL's decode of the same files.  codec "jp2": the same pages saved
+    losslessly as JPEG 2000 (OpenJPEG's defaults), headers and packet headers
+    parsed on the load pool, every code-block of a chunk decoded on the
+    device in one launch, then the wavelet into the input slots."""
     from PIL import Image
     from concurrent.futures import ThreadPoolExecutor
     n = args.pages or 512
@@ -462,8 +465,12 @@ def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid):
         def make(i):
             g = np.empty((H, W), np.uint8)
             L.uphip_synth_page_host(g.ctypes.data, W, W, H, firsts[0] + i)
-            path = os.path.join(tmpdir, "p%02d.jpg" % i)
-            Image.fromarray(g).save(path, "JPEG", quality=95)
+            if codec == "jp2":
+                path = os.path.join(tmpdir, "p%02d.jp2" % i)
+                Image.fromarray(g).save(path, "JPEG2000")
+            else:
+                path = os.path.join(tmpdir, "p%02d.jpg" % i)
+                Image.fromarray(g).save(path, "JPEG", quality=95)
             return path
         with ThreadPoolExecutor(min(16, threads)) as ex:
             uniq = list(ex.map(make, range(16)))
@@ -481,7 +488,7 @@ def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid):
                                          sink_discard())
                 t = time.perf_counter() - t0
                 if failed:
-                    raise UnpaperHipError("jpeg run: %d failed: %s" % (failed, err))
+                    raise UnpaperHipError("%s run: %d failed: %s" % (codec, failed, err))
             st = r.stats()
         finally:
             r.close()
@@ -500,16 +507,19 @@ def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid):
                 exp = oracle.convert_for_save(sheet, fmt)
                 got = pnm_read(outs % i)
                 if not np.array_equal(got.payload(), exp.payload()):
-                    raise SystemExit("bench.py: JPEG page %d differs from the oracle" % i)
+                    raise SystemExit("bench.py: %s page %d differs from the oracle" % (codec, i))
                 checked += 1
     finally:
         shutil.rmtree(tmpdir, ignore_errors=True)
-    return {"metric": "pages/s, A4 GRAY8 JPEG files through the runner (JPEG decode peer)",
+    what = ("JPEG 2000 files through the runner (JPEG 2000 decode peer)" if codec == "jp2" else
+            "JPEG files through the runner (JPEG decode peer)")
+    made = "PIL JPEG 2000 lossless" if codec == "jp2" else "PIL JPEG quality 95"
+    return {"metric": "pages/s, A4 GRAY8 " + what,
             "value": round(n / t, 2), "unit": "pages/s", "n_gpus": 1, "higher_is_better": True,
-            "dtype": "u8", "data": "synthetic (PIL JPEG quality 95, %.2f MB a page)" % mb,
+            "dtype": "u8", "data": "synthetic (%s, %.2f MB a page)" % (made, mb),
             "host_threads": threads, "load_s": round(st.load_s, 3),
             "config": {"pages": n, "sheets_per_batch": 32, "streams": 8,
-                       "source": "JPEG files in tmpfs (16 distinct, round robin)",
+                       "source": "%s files in tmpfs (16 distinct, round robin)" % codec.upper(),
                        "sink": "discarded"},
             "verified": checked, "library": version, "valid": valid}
 
@@ -647,8 +657,8 @@ def main():
         if d.rank == 0:
             print(json.dumps(line), flush=True)
         return
-    if args.config == "jpeg":
-        line = run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid)
+    if args.config in ("jpeg", "jp2"):
+        line = run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid, args.config)
         if d.rank == 0:
             print(json.dumps(line), flush=True)
         return

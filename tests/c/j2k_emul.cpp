@@ -23,7 +23,7 @@ extern "C" {
 // count (written when cap suffices) or -1 (uphip_last_error); info3 =
 // {width, height, ncomp}.
 static int64_t finish(const Image& img, std::vector<uint32_t>& coef, uint8_t* out, int64_t cap,
-                      int32_t* info3);
+                      int32_t* info3, bool pairs = false);
 
 int64_t j2k_emulate(const uint8_t* file, size_t n, uint8_t* out, int64_t cap, int32_t* info3) {
   Image img;
@@ -76,11 +76,42 @@ int64_t j2k_emulate_t1lane(const uint8_t* file, size_t n, uint8_t* out, int64_t 
       t1_store_lane(L, true, job, coef.data(), Hg);
     }
   }
-  return finish(img, coef, out, cap, info3);
+  return finish(img, coef, out, cap, info3, true);
 }
 
+// the inverse pair kernels (k_j2k_irow / k_j2k_icol) on the CPU
+extern "C++" {
+template <class T, int CAS>
+static void pair_level(T* plane, T* tmp, int stride, int rw, int rh) {
+  for (int y = 0; y < rh; y++)
+    for (int t = 0; 2 * t < rw; t++) {
+      T o0, o1;
+      idwt_pair<T, CAS>(plane + (int64_t)y * stride, 1, rw, t, &o0, &o1);
+      tmp[(int64_t)y * stride + 2 * t] = o0;
+      if (2 * t + 1 < rw) tmp[(int64_t)y * stride + 2 * t + 1] = o1;
+    }
+}
+template <class T, int CAS>
+static void pair_cols(T* tmp, T* plane, int stride, int rw, int rh) {
+  for (int x = 0; x < rw; x++)
+    for (int t = 0; 2 * t < rh; t++) {
+      T o0, o1;
+      idwt_pair<T, CAS>(tmp + x, stride, rh, t, &o0, &o1);
+      plane[(int64_t)(2 * t) * stride + x] = o0;
+      if (2 * t + 1 < rh) plane[(int64_t)(2 * t + 1) * stride + x] = o1;
+    }
+}
+template <class T>
+static void pair_2d(T* plane, T* tmp, int stride, int rw, int rh, int cx, int cy) {
+  if (cx) pair_level<T, 1>(plane, tmp, stride, rw, rh);
+  else pair_level<T, 0>(plane, tmp, stride, rw, rh);
+  if (cy) pair_cols<T, 1>(tmp, plane, stride, rw, rh);
+  else pair_cols<T, 0>(tmp, plane, stride, rw, rh);
+}
+}  // extern "C++"
+
 static int64_t finish(const Image& img, std::vector<uint32_t>& coef, uint8_t* out, int64_t cap,
-                      int32_t* info3) {
+                      int32_t* info3, bool pairs) {
   info3[0] = img.width;
   info3[1] = img.height;
   info3[2] = img.ncomp;
@@ -96,6 +127,12 @@ static int64_t finish(const Image& img, std::vector<uint32_t>& coef, uint8_t* ou
         uint32_t* plane = coef.data() + tc.off;
         tmp.assign((size_t)rw * rh, 0u);
         const int cx = tc.rx0[r] & 1, cy = tc.ry0[r] & 1;
+        if (pairs) {  // as the device does
+          std::vector<uint32_t> t2((size_t)tc.stride * rh);
+          if (img.reversible) pair_2d((int32_t*)plane, (int32_t*)t2.data(), tc.stride, rw, rh, cx, cy);
+          else pair_2d((float*)plane, (float*)t2.data(), tc.stride, rw, rh, cx, cy);
+          continue;
+        }
         for (int y = 0; y < rh; y++) {  // k_j2k_rows
           uint32_t* row = plane + (int64_t)y * tc.stride;
           uint32_t* tl = tmp.data() + (int64_t)y * rw;
@@ -142,6 +179,62 @@ static int64_t finish(const Image& img, std::vector<uint32_t>& coef, uint8_t* ou
   return bytes;
 }
 
+// The pair-at-a-time lifting (j2k_dwt.h, the device kernels' form) against
+// the sequential in-place lifting for every line length 1..nmax, both
+// parities, 5/3 both ways and 9/7 inverse, on seeded data; returns the
+// number of mismatching samples.
+int64_t j2k_dwt_check(int nmax, uint32_t seed) {
+  int64_t bad = 0;
+  uint32_t rs = seed;
+  auto rnd = [&]() { rs = rs * 1664525u + 1013904223u; return rs >> 8; };
+  for (int n = 1; n <= nmax; n++)
+    for (int cas = 0; cas < 2; cas++) {
+      std::vector<int32_t> a(n), nat(n), m(n);
+      std::vector<float> fa(n), fnat(n);
+      for (int i = 0; i < n; i++) {
+        a[i] = (int32_t)(rnd() % 2001) - 1000;
+        fa[i] = (float)((int32_t)(rnd() % 20001) - 10000) * 0.037f;
+      }
+      // inverse 5/3 and 9/7: Mallat -> natural
+      std::vector<int32_t> ref(n);
+      std::vector<float> fref(n);
+      interleave(a.data(), 1, n, cas, ref.data(), 1);
+      idwt53_line(ref.data(), n, cas, 1);
+      interleave(fa.data(), 1, n, cas, fref.data(), 1);
+      idwt97_line(fref.data(), n, cas, 1);
+      for (int t = 0; 2 * t < n; t++) {
+        int32_t o0 = 0, o1 = 0;
+        float f0 = 0, f1 = 0;
+        if (cas) {
+          idwt_pair<int32_t, 1>(a.data(), 1, n, t, &o0, &o1);
+          idwt_pair<float, 1>(fa.data(), 1, n, t, &f0, &f1);
+        } else {
+          idwt_pair<int32_t, 0>(a.data(), 1, n, t, &o0, &o1);
+          idwt_pair<float, 0>(fa.data(), 1, n, t, &f0, &f1);
+        }
+        bad += o0 != ref[2 * t];
+        bad += memcmp(&f0, &fref[2 * t], 4) != 0;
+        if (2 * t + 1 < n) {
+          bad += o1 != ref[2 * t + 1];
+          bad += memcmp(&f1, &fref[2 * t + 1], 4) != 0;
+        }
+      }
+      // forward 5/3: natural -> Mallat
+      std::vector<int32_t> fw(a);
+      fdwt53_line(fw.data(), n, cas, 1);
+      std::vector<int32_t> fm(n);
+      deinterleave(fw.data(), 1, n, cas, fm.data(), 1);
+      for (int t = 0; 2 * t < n; t++) {
+        int32_t o0 = 0, o1 = 0;
+        if (cas) fdwt53_pair<1>(a.data(), 1, n, t, &o0, &o1);
+        else fdwt53_pair<0>(a.data(), 1, n, t, &o0, &o1);
+        bad += o0 != fm[mallat_index(2 * t, n, cas)];
+        if (2 * t + 1 < n) bad += o1 != fm[mallat_index(2 * t + 1, n, cas)];
+      }
+    }
+  return bad;
+}
+
 // Encodes `src` (rows of w * ncomp bytes) as the device path would; returns
 // the file size (written when cap suffices) or -1.
 int64_t j2k_emulate_encode(const uint8_t* src, int32_t w, int32_t h, int32_t ncomp, uint8_t* out,
@@ -168,18 +261,25 @@ int64_t j2k_emulate_encode(const uint8_t* src, int32_t w, int32_t h, int32_t nco
     int32_t* plane = (int32_t*)(coef.data() + tc.off);
     for (int r = tc.nlevels; r >= 1; r--) {
       const int rw = tc.rx1[r] - tc.rx0[r], rh = tc.ry1[r] - tc.ry0[r];
-      for (int x = 0; x < rw; x++) {  // k_j2k_fcols
-        for (int i = 0; i < rh; i++) tmp[(size_t)i * rw + x] = plane[(int64_t)i * tc.stride + x];
-        fdwt53_line(tmp.data() + x, rh, tc.ry0[r] & 1, rw);
-        deinterleave(tmp.data() + x, rw, rh, tc.ry0[r] & 1, plane + x, tc.stride);
-      }
-      for (int y = 0; y < rh; y++) {  // k_j2k_frows
-        int32_t* row = plane + (int64_t)y * tc.stride;
-        int32_t* tl = tmp.data() + (int64_t)y * rw;
-        memcpy(tl, row, 4 * (size_t)rw);
-        fdwt53_line(tl, rw, tc.rx0[r] & 1, 1);
-        deinterleave(tl, 1, rw, tc.rx0[r] & 1, row, 1);
-      }
+      std::vector<int32_t> t2((size_t)tc.stride * rh);
+      const int cx = tc.rx0[r] & 1, cy = tc.ry0[r] & 1;
+      for (int x = 0; x < rw; x++)  // k_j2k_fcol: plane -> t2
+        for (int t = 0; 2 * t < rh; t++) {
+          int32_t o0, o1;
+          if (cy) fdwt53_pair<1>(plane + x, tc.stride, rh, t, &o0, &o1);
+          else fdwt53_pair<0>(plane + x, tc.stride, rh, t, &o0, &o1);
+          t2[(size_t)mallat_index(2 * t, rh, cy) * tc.stride + x] = o0;
+          if (2 * t + 1 < rh) t2[(size_t)mallat_index(2 * t + 1, rh, cy) * tc.stride + x] = o1;
+        }
+      for (int y = 0; y < rh; y++)  // k_j2k_frow: t2 -> plane
+        for (int t = 0; 2 * t < rw; t++) {
+          int32_t o0, o1;
+          const int32_t* line = t2.data() + (size_t)y * tc.stride;
+          if (cx) fdwt53_pair<1>(line, 1, rw, t, &o0, &o1);
+          else fdwt53_pair<0>(line, 1, rw, t, &o0, &o1);
+          plane[(int64_t)y * tc.stride + mallat_index(2 * t, rw, cx)] = o0;
+          if (2 * t + 1 < rw) plane[(int64_t)y * tc.stride + mallat_index(2 * t + 1, rw, cx)] = o1;
+        }
     }
   }
   std::vector<uint8_t> file;

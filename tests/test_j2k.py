@@ -163,6 +163,18 @@ def test_decode_matches_openjpeg(opt, rgb, mct):
             assert (got == a).all()  # lossless
 
 
+def test_pair_lifting_equals_sequential_lifting():
+    """The device kernels lift one output pair a thread over a window of the
+    line's symmetric extension (j2k_dwt.h idwt_pair / fdwt53_pair); against
+    the in-place sequential lifting for every length 1..200 and both
+    parities: 5/3 both ways, 9/7 inverse, bit for bit."""
+    E = _emul()
+    E.j2k_dwt_check.restype = C.c_int64
+    E.j2k_dwt_check.argtypes = [C.c_int, C.c_uint32]
+    for seed in (1, 7, 1234):
+        assert E.j2k_dwt_check(200, seed) == 0
+
+
 def test_decode_refuses_what_it_does_not_take(tmp_path):
     a16 = (np.arange(24 * 20, dtype=np.uint16).reshape(20, 24) * 97)
     data16 = pil_save(a16)  # 16-bit precision

@@ -876,6 +876,7 @@ bool decode_host(const uint8_t* d, size_t n, const char* name, Image* img,
           }
       }
     }
+    if (t1) t1->data.insert(t1->data.end(), 16, 0);  // the decoder's read-ahead
     if (t1)  // alike blocks share a wave: by width, height, then passes
       std::stable_sort(t1->jobs.begin(), t1->jobs.end(), [](const T1Job& x, const T1Job& y) {
         if (x.w != y.w) return x.w > y.w;

@@ -64,7 +64,7 @@ struct Image {
 struct T1Job;
 // The code-blocks of a file for the device decoder (k_j2k_t1): jobs sorted
 // by shape and pass count, their codewords back to back (each followed by
-// 0xFF 0xFF, offsets 4-byte aligned).
+// 0xFF 0xFF, offsets 4-byte aligned, 16 bytes of read-ahead at the end).
 struct T1Batch {
   std::vector<T1Job> jobs;
   std::vector<uint8_t> data;

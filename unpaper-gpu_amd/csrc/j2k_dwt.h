@@ -95,6 +95,108 @@ J2K_HD inline void deinterleave(const T* src, int64_t ts, int n, int cas, T* dst
   }
 }
 
+// ---------------------------------------------------------------------------
+// The same transforms one output pair at a time, for a thread per pair: the
+// lifting steps recomputed over a window of the line's whole-sample
+// symmetric (periodic) extension, which equals the in-place sequential
+// lifting above value for value (each lifted value of the extension is the
+// value at its mirrored position; the float steps keep the operands and
+// their order).  Line i of n samples: the Mallat layout (lows [0, sn),
+// highs [sn, n); elements s apart) on the inverse's input and the forward's
+// output, natural order (elements ds apart) on the other side.
+
+J2K_HD inline int mirror_ext(int i, int n) {  // n >= 2
+  const int P = 2 * (n - 1);
+  i %= P;
+  if (i < 0) i += P;
+  return i >= n ? P - i : i;
+}
+// natural position i (0 <= i < n) of a Mallat line
+J2K_HD inline int mallat_index(int i, int n, int cas) {
+  const int sn = (n + 1 - cas) / 2;
+  return ((i + cas) & 1) == 0 ? (i - cas) / 2 : sn + (i - (1 - cas)) / 2;
+}
+
+// Inverse: natural-order samples 2t and 2t + 1 (when < n) of a Mallat line.
+template <class T, int CAS>
+J2K_HD inline void idwt_pair(const T* src, int64_t s, int n, int t, T* o0, T* o1) {
+  const int b = 2 * t;
+  constexpr bool kInt = T(1) / T(2) == T(0);  // 5/3 (int32) or 9/7 (float)
+  if (n == 1) {  // a single sample: a high one is halved (OpenJPEG dwt.c)
+    const T x = src[0];
+    if constexpr (kInt) *o0 = CAS ? x / 2 : x;
+    else *o0 = CAS ? x * 0.5f : x;
+    return;
+  }
+  auto ld = [&](int j) -> T { return src[(int64_t)mallat_index(mirror_ext(b + j, n), n, CAS) * s]; };
+  // low positions: ((j + CAS) & 1) == 0
+  if constexpr (kInt) {  // 5/3: window b-2 .. b+3
+    T w[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) w[j] = ld(j - 2);
+    T s1[6];
+#pragma unroll
+    for (int j = 1; j < 5; j++)
+      s1[j] = ((j - 2 + CAS) & 1) == 0 ? w[j] - ((w[j - 1] + w[j + 1] + 2) >> 2) : w[j];
+    T out[2];
+#pragma unroll
+    for (int j = 2; j < 4; j++)
+      out[j - 2] = ((j - 2 + CAS) & 1) == 0 ? s1[j] : w[j] + ((s1[j - 1] + s1[j + 1]) >> 1);
+    *o0 = out[0];
+    if (b + 1 < n) *o1 = out[1];
+  } else {  // 9/7 float: window b-4 .. b+5
+    const float kA = -1.586134342059924f, kB = -0.052980118572961f;
+    const float kG = 0.882911075530934f, kD = 0.443506852043971f;
+    const float kK = 1.230174104914001f, kInvK = 13318.0f / 16384.0f;
+    float a[10];
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+      const float x = ld(j - 4);
+      a[j] = ((j - 4 + CAS) & 1) == 0 ? x * kK : x * kInvK;
+    }
+    float c[10];
+#pragma unroll
+    for (int j = 1; j < 9; j++)  // delta on the lows
+      c[j] = ((j - 4 + CAS) & 1) == 0 ? a[j] - kD * (a[j - 1] + a[j + 1]) : a[j];
+#pragma unroll
+    for (int j = 2; j < 8; j++)  // gamma on the highs
+      a[j] = ((j - 4 + CAS) & 1) != 0 ? c[j] - kG * (c[j - 1] + c[j + 1]) : c[j];
+#pragma unroll
+    for (int j = 3; j < 7; j++)  // beta on the lows
+      c[j] = ((j - 4 + CAS) & 1) == 0 ? a[j] - kB * (a[j - 1] + a[j + 1]) : a[j];
+#pragma unroll
+    for (int j = 4; j < 6; j++)  // alpha on the highs
+      a[j] = ((j - 4 + CAS) & 1) != 0 ? c[j] - kA * (c[j - 1] + c[j + 1]) : c[j];
+    *o0 = (T)a[4];
+    if (b + 1 < n) *o1 = (T)a[5];
+  }
+}
+
+// Forward 5/3: natural-order samples 2t and 2t + 1 (when < n) lifted, for
+// their Mallat positions.
+template <int CAS>
+J2K_HD inline void fdwt53_pair(const int32_t* src, int64_t ds, int n, int t, int32_t* o0,
+                               int32_t* o1) {
+  const int b = 2 * t;
+  if (n == 1) {
+    *o0 = CAS ? src[0] * 2 : src[0];
+    return;
+  }
+  int32_t w[6];
+#pragma unroll
+  for (int j = 0; j < 6; j++) w[j] = src[(int64_t)mirror_ext(b + j - 2, n) * ds];
+  int32_t h1[6];
+#pragma unroll
+  for (int j = 1; j < 5; j++)  // highs: predict
+    h1[j] = ((j - 2 + CAS) & 1) != 0 ? w[j] - ((w[j - 1] + w[j + 1]) >> 1) : w[j];
+  int32_t out[2];
+#pragma unroll
+  for (int j = 2; j < 4; j++)  // lows: update
+    out[j - 2] = ((j - 2 + CAS) & 1) == 0 ? h1[j] + ((h1[j - 1] + h1[j + 1] + 2) >> 2) : h1[j];
+  *o0 = out[0];
+  if (b + 1 < n) *o1 = out[1];
+}
+
 // The inverse component transforms and the DC level shift of one pixel
 // (G.2: RCT for reversible, ICT for irreversible data; 8-bit output)
 J2K_HD inline uint8_t clamp8(int32_t v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }

@@ -73,8 +73,12 @@ struct T1Lane {
   // this lane's block
   int w, h, orient;
   int pm;  // lowest plane whose refinement pass was decoded (1 << 30: none)
-  // MQ decoder
-  const uint8_t* bp;
+  // MQ decoder; the codeword is read through a 12-byte window of aligned
+  // words (w0 at q, w1, w2), the word 8 bytes ahead loaded when the window
+  // moves, long before its bytes are needed
+  const uint32_t* q;  // 4-byte aligned
+  uint32_t w0, w1, w2;
+  int bi;             // offset of the current byte (BP) from q: 0 .. 3
   uint32_t a, c;
   int ct;
 
@@ -90,25 +94,44 @@ struct T1Lane {
 #endif
   }
 
+  // bytes BP and BP + 1 (bi + 1 <= 4 < 8)
+  J2K_HD uint32_t byte_at(int i) const {
+    const uint64_t v = ((uint64_t)w1 << 32) | w0;
+    return (uint32_t)(v >> (8 * i)) & 0xFFu;
+  }
+  J2K_HD void advance() {  // BP++
+    if (++bi == 4) {
+      bi = 0;
+      q++;
+      w0 = w1;
+      w1 = w2;
+      w2 = q[2];
+    }
+  }
   J2K_HD void bytein() {
-    if (bp[0] == 0xFF) {
-      if (bp[1] > 0x8F) {
+    if (byte_at(bi) == 0xFF) {
+      if (byte_at(bi + 1) > 0x8F) {
         c += 0xFF00;
         ct = 8;
       } else {
-        bp++;
-        c += (uint32_t)bp[0] << 9;
+        advance();
+        c += byte_at(bi) << 9;
         ct = 7;
       }
     } else {
-      bp++;
-      c += (uint32_t)bp[0] << 8;
+      advance();
+      c += byte_at(bi) << 8;
       ct = 8;
     }
   }
+  // data: 4-byte aligned, readable 12 bytes past the codeword's FF FF
   J2K_HD void mq_init(const uint8_t* data) {
-    bp = data;
-    c = (uint32_t)bp[0] << 16;
+    q = reinterpret_cast<const uint32_t*>(data);
+    w0 = q[0];
+    w1 = q[1];
+    w2 = q[2];
+    bi = 0;
+    c = byte_at(0) << 16;
     bytein();
     c <<= 7;
     ct -= 7;

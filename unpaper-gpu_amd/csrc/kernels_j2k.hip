@@ -3,9 +3,10 @@
 // dwt.c and the standard's 2D_SR), the inverse component transform, the DC
 // level shift and the store into the destination image; for the lossless
 // encoder the DC shift, the forward RCT and the forward 5/3 transform
-// (columns, then rows, per level).  A lane per row or column: the lines of
-// a level are independent, and the columns' lanes read one row of the plane
-// together (coalesced); `tmp` holds each lane's interleaved line.
+// (columns, then rows, per level).  A thread per output pair of a line: the
+// lifting recomputed over a small window of the line (j2k_dwt.h), each pass
+// from one buffer into the other (plane and tmp, the same row stride), the
+// column passes' threads along the rows (coalesced).
 #include <algorithm>
 #include <type_traits>
 
@@ -19,28 +20,33 @@ namespace j2k {
 
 namespace {
 
-template <class T>
-__global__ void __launch_bounds__(256) k_j2k_rows(T* plane, int stride, int rw, int rh, int cas,
-                                                  T* tmp) {
-  const int y = blockIdx.x * 256 + threadIdx.x;
-  if (y >= rh) return;
-  T* row = plane + (int64_t)y * stride;
-  T* t = tmp + (int64_t)y * rw;
-  interleave(row, 1, rw, cas, t, 1);
-  if constexpr (std::is_integral<T>::value) idwt53_line((int32_t*)t, rw, cas, 1);
-  else idwt97_line((float*)t, rw, cas, 1);
-  for (int i = 0; i < rw; i++) row[i] = t[i];
+// Inverse wavelet of one level, a thread per output pair (j2k_dwt.h
+// idwt_pair): rows of the plane (Mallat in x) into tmp in natural order, then
+// columns of tmp (Mallat in y) back into the plane; a column pass's threads
+// span 64 columns, so every load and store of a row segment is coalesced.
+template <class T, int CAS>
+__global__ void __launch_bounds__(256) k_j2k_irow(const T* __restrict__ src, T* __restrict__ dst,
+                                                  int stride, int rw, int rh) {
+  const int y = blockIdx.y;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (2 * t >= rw) return;
+  const T* line = src + (int64_t)y * stride;
+  T o0, o1;
+  idwt_pair<T, CAS>(line, 1, rw, t, &o0, &o1);
+  T* d = dst + (int64_t)y * stride + 2 * t;
+  d[0] = o0;
+  if (2 * t + 1 < rw) d[1] = o1;
 }
-
-template <class T>
-__global__ void __launch_bounds__(256) k_j2k_cols(T* plane, int stride, int rw, int rh, int cas,
-                                                  T* tmp) {
-  const int x = blockIdx.x * 256 + threadIdx.x;
-  if (x >= rw) return;
-  interleave(plane + x, stride, rh, cas, tmp + x, rw);
-  if constexpr (std::is_integral<T>::value) idwt53_line((int32_t*)(tmp + x), rh, cas, rw);
-  else idwt97_line((float*)(tmp + x), rh, cas, rw);
-  for (int i = 0; i < rh; i++) plane[(int64_t)i * stride + x] = tmp[(int64_t)i * rw + x];
+template <class T, int CAS>
+__global__ void __launch_bounds__(256) k_j2k_icol(const T* __restrict__ src, T* __restrict__ dst,
+                                                  int stride, int rw, int rh) {
+  const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int t = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (x >= rw || 2 * t >= rh) return;
+  T o0, o1;
+  idwt_pair<T, CAS>(src + x, stride, rh, t, &o0, &o1);
+  dst[(int64_t)(2 * t) * stride + x] = o0;
+  if (2 * t + 1 < rh) dst[(int64_t)(2 * t + 1) * stride + x] = o1;
 }
 
 // one tile into the image: inverse MCT, DC shift, clamp, store
@@ -104,23 +110,33 @@ __global__ void __launch_bounds__(256) k_j2k_in(const uint8_t* src, int64_t pitc
   coef[2 * n + i] = (uint32_t)(R - G);
 }
 
-__global__ void __launch_bounds__(256) k_j2k_fcols(int32_t* plane, int stride, int rw, int rh,
-                                                   int cas, int32_t* tmp) {
-  const int x = blockIdx.x * 256 + threadIdx.x;
-  if (x >= rw) return;
-  for (int i = 0; i < rh; i++) tmp[(int64_t)i * rw + x] = plane[(int64_t)i * stride + x];
-  fdwt53_line(tmp + x, rh, cas, rw);
-  deinterleave(tmp + x, rw, rh, cas, plane + x, stride);
+// Forward 5/3 of one level (encoder), a thread per input pair: columns of
+// the plane (natural) into tmp (Mallat in y), then rows of tmp (natural in
+// x) back into the plane (Mallat in x).
+template <int CAS>
+__global__ void __launch_bounds__(256) k_j2k_fcol(const int32_t* __restrict__ src,
+                                                  int32_t* __restrict__ dst, int stride, int rw,
+                                                  int rh) {
+  const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int t = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (x >= rw || 2 * t >= rh) return;
+  int32_t o0, o1;
+  fdwt53_pair<CAS>(src + x, stride, rh, t, &o0, &o1);
+  dst[(int64_t)mallat_index(2 * t, rh, CAS) * stride + x] = o0;
+  if (2 * t + 1 < rh) dst[(int64_t)mallat_index(2 * t + 1, rh, CAS) * stride + x] = o1;
 }
-__global__ void __launch_bounds__(256) k_j2k_frows(int32_t* plane, int stride, int rw, int rh,
-                                                   int cas, int32_t* tmp) {
-  const int y = blockIdx.x * 256 + threadIdx.x;
-  if (y >= rh) return;
-  int32_t* row = plane + (int64_t)y * stride;
-  int32_t* t = tmp + (int64_t)y * rw;
-  for (int i = 0; i < rw; i++) t[i] = row[i];
-  fdwt53_line(t, rw, cas, 1);
-  deinterleave(t, 1, rw, cas, row, 1);
+template <int CAS>
+__global__ void __launch_bounds__(256) k_j2k_frow(const int32_t* __restrict__ src,
+                                                  int32_t* __restrict__ dst, int stride, int rw,
+                                                  int rh) {
+  const int y = blockIdx.y;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (2 * t >= rw) return;
+  int32_t o0, o1;
+  fdwt53_pair<CAS>(src + (int64_t)y * stride, 1, rw, t, &o0, &o1);
+  int32_t* d = dst + (int64_t)y * stride;
+  d[mallat_index(2 * t, rw, CAS)] = o0;
+  if (2 * t + 1 < rw) d[mallat_index(2 * t + 1, rw, CAS)] = o1;
 }
 
 unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
@@ -208,16 +224,23 @@ bool decode_launch(const Image& img, uint32_t* dcoef, uint8_t* dst, int64_t pitc
         const int rw = tc.rx1[r] - tc.rx0[r], rh = tc.ry1[r] - tc.ry0[r];
         if (rw <= 0 || rh <= 0) continue;
         uint32_t* plane = dcoef + tc.off;
+        const dim3 rg((unsigned)((rw + 511) / 512), (unsigned)rh);
+        const dim3 cg((unsigned)((rw + 63) / 64), (unsigned)((rh + 7) / 8));
+        const int cx = tc.rx0[r] & 1, cy = tc.ry0[r] & 1;
         if (img.reversible) {
-          hipLaunchKernelGGL(k_j2k_rows<int32_t>, dim3(blocks(rh)), dim3(256), 0, st,
-                             (int32_t*)plane, tc.stride, rw, rh, tc.rx0[r] & 1, (int32_t*)tmp);
-          hipLaunchKernelGGL(k_j2k_cols<int32_t>, dim3(blocks(rw)), dim3(256), 0, st,
-                             (int32_t*)plane, tc.stride, rw, rh, tc.ry0[r] & 1, (int32_t*)tmp);
+          int32_t* pl = (int32_t*)plane;
+          int32_t* tp = (int32_t*)tmp;
+          if (cx) hipLaunchKernelGGL((k_j2k_irow<int32_t, 1>), rg, dim3(256), 0, st, pl, tp, tc.stride, rw, rh);
+          else hipLaunchKernelGGL((k_j2k_irow<int32_t, 0>), rg, dim3(256), 0, st, pl, tp, tc.stride, rw, rh);
+          if (cy) hipLaunchKernelGGL((k_j2k_icol<int32_t, 1>), cg, dim3(256), 0, st, tp, pl, tc.stride, rw, rh);
+          else hipLaunchKernelGGL((k_j2k_icol<int32_t, 0>), cg, dim3(256), 0, st, tp, pl, tc.stride, rw, rh);
         } else {
-          hipLaunchKernelGGL(k_j2k_rows<float>, dim3(blocks(rh)), dim3(256), 0, st, (float*)plane,
-                             tc.stride, rw, rh, tc.rx0[r] & 1, (float*)tmp);
-          hipLaunchKernelGGL(k_j2k_cols<float>, dim3(blocks(rw)), dim3(256), 0, st, (float*)plane,
-                             tc.stride, rw, rh, tc.ry0[r] & 1, (float*)tmp);
+          float* pl = (float*)plane;
+          float* tp = (float*)tmp;
+          if (cx) hipLaunchKernelGGL((k_j2k_irow<float, 1>), rg, dim3(256), 0, st, pl, tp, tc.stride, rw, rh);
+          else hipLaunchKernelGGL((k_j2k_irow<float, 0>), rg, dim3(256), 0, st, pl, tp, tc.stride, rw, rh);
+          if (cy) hipLaunchKernelGGL((k_j2k_icol<float, 1>), cg, dim3(256), 0, st, tp, pl, tc.stride, rw, rh);
+          else hipLaunchKernelGGL((k_j2k_icol<float, 0>), cg, dim3(256), 0, st, tp, pl, tc.stride, rw, rh);
         }
       }
     }
@@ -246,10 +269,12 @@ bool encode_launch(const Image& img, const uint8_t* src, int64_t pitch, uint32_t
     for (int r = tc.nlevels; r >= 1; r--) {
       const int rw = tc.rx1[r] - tc.rx0[r], rh = tc.ry1[r] - tc.ry0[r];
       if (rw <= 0 || rh <= 0) continue;
-      hipLaunchKernelGGL(k_j2k_fcols, dim3(blocks(rw)), dim3(256), 0, st, plane, tc.stride, rw, rh,
-                         tc.ry0[r] & 1, tmp);
-      hipLaunchKernelGGL(k_j2k_frows, dim3(blocks(rh)), dim3(256), 0, st, plane, tc.stride, rw, rh,
-                         tc.rx0[r] & 1, tmp);
+      const dim3 rg((unsigned)((rw + 511) / 512), (unsigned)rh);
+      const dim3 cg((unsigned)((rw + 63) / 64), (unsigned)((rh + 7) / 8));
+      if (tc.ry0[r] & 1) hipLaunchKernelGGL(k_j2k_fcol<1>, cg, dim3(256), 0, st, plane, tmp, tc.stride, rw, rh);
+      else hipLaunchKernelGGL(k_j2k_fcol<0>, cg, dim3(256), 0, st, plane, tmp, tc.stride, rw, rh);
+      if (tc.rx0[r] & 1) hipLaunchKernelGGL(k_j2k_frow<1>, rg, dim3(256), 0, st, tmp, plane, tc.stride, rw, rh);
+      else hipLaunchKernelGGL(k_j2k_frow<0>, rg, dim3(256), 0, st, tmp, plane, tc.stride, rw, rh);
     }
   }
   return UPH_HIP(hipGetLastError());
