@@ -235,13 +235,13 @@ int64_t j2k_dwt_check(int nmax, uint32_t seed) {
   return bad;
 }
 
-// Encodes `src` (rows of w * ncomp bytes) as the device path would; returns
-// the file size (written when cap suffices) or -1.
-int64_t j2k_emulate_encode(const uint8_t* src, int32_t w, int32_t h, int32_t ncomp, uint8_t* out,
-                           int64_t cap) {
-  Image img;
-  if (!encode_geometry(w, h, ncomp, &img)) return -1;
-  std::vector<uint32_t> coef((size_t)img.coef_elems);
+// The device's forward transforms on the CPU (k_j2k_in, k_j2k_fcol /
+// k_j2k_frow through the pair functions) into img's coefficient planes.
+static bool emul_forward(const uint8_t* src, int32_t w, int32_t h, int32_t ncomp, Image* img,
+                         std::vector<uint32_t>* coefp) {
+  if (!encode_geometry(w, h, ncomp, img)) return false;
+  std::vector<uint32_t>& coef = *coefp;
+  coef.assign((size_t)img->coef_elems, 0u);
   const int64_t n = (int64_t)w * h;
   for (int64_t i = 0; i < n; i++) {  // k_j2k_in
     const uint8_t* s = src + i * ncomp;
@@ -254,8 +254,7 @@ int64_t j2k_emulate_encode(const uint8_t* src, int32_t w, int32_t h, int32_t nco
     coef[(size_t)(n + i)] = (uint32_t)(B - G);
     coef[(size_t)(2 * n + i)] = (uint32_t)(R - G);
   }
-  std::vector<int32_t> tmp((size_t)n);
-  const Tile& t = img.tiles[0];
+  const Tile& t = img->tiles[0];
   for (int c = 0; c < ncomp; c++) {
     const TileComp& tc = t.tc[c];
     int32_t* plane = (int32_t*)(coef.data() + tc.off);
@@ -282,10 +281,102 @@ int64_t j2k_emulate_encode(const uint8_t* src, int32_t w, int32_t h, int32_t nco
         }
     }
   }
-  std::vector<uint8_t> file;
-  if (!encode_host(img, coef.data(), &file)) return -1;
+  return true;
+}
+
+static int64_t give(const std::vector<uint8_t>& file, uint8_t* out, int64_t cap) {
   if (out && cap >= (int64_t)file.size()) memcpy(out, file.data(), file.size());
   return (int64_t)file.size();
+}
+
+// Encodes `src` (rows of w * ncomp bytes) as the device path would, the
+// code-blocks coded by j2k_t1.h's host coder; returns the file size
+// (written when cap suffices) or -1.
+int64_t j2k_emulate_encode(const uint8_t* src, int32_t w, int32_t h, int32_t ncomp, uint8_t* out,
+                           int64_t cap) {
+  Image img;
+  std::vector<uint32_t> coef;
+  std::vector<uint8_t> file;
+  if (!emul_forward(src, w, h, ncomp, &img, &coef) || !encode_host(img, coef.data(), &file)) return -1;
+  return give(file, out, cap);
+}
+
+// The same with the code-blocks through the device encoder's lane code
+// (j2k_t1_lane.h, LS = 1) in 64-block groups, as k_j2k_t1enc runs them.
+int64_t j2k_emulate_encode_lane(const uint8_t* src, int32_t w, int32_t h, int32_t ncomp,
+                                uint8_t* out, int64_t cap) {
+  Image img;
+  std::vector<uint32_t> coef;
+  std::vector<T1EncJob> jobs;
+  size_t obytes = 0;
+  if (!emul_forward(src, w, h, ncomp, &img, &coef) || !encode_jobs(img, &jobs, &obytes)) return -1;
+  MqState qe[47];
+  for (int i = 0; i < 47; i++) qe[i] = kMq[i];
+  uint8_t zct[kZcTable];
+  zc_table(zct);
+  std::vector<uint8_t> odata(obytes + 16);
+  const int njobs = (int)jobs.size();
+  std::vector<uint32_t> off(njobs), len(njobs);
+  std::vector<uint8_t> nbv(njobs);
+  std::vector<uint16_t> fl;
+  std::vector<uint64_t> mg;
+  uint8_t cx[kNumCtx];
+  for (int g0 = 0; g0 < njobs; g0 += 64) {
+    const int g1 = std::min(njobs, g0 + 64);
+    int Wg = 0, Hg = 0, P = 0;
+    std::vector<int> nbs;
+    for (int j = g0; j < g1; j++) {
+      const T1EncJob& jb = jobs[(size_t)j];
+      uint32_t m = 0;
+      for (int y = 0; y < jb.h; y++)
+        for (int x = 0; x < jb.w; x++) {
+          const int32_t v = (int32_t)coef[(size_t)(jb.in + (int64_t)y * jb.stride + x)];
+          m |= (uint32_t)(v < 0 ? -v : v);
+        }
+      int nb = 0;
+      while (m) {
+        nb++;
+        m >>= 1;
+      }
+      nbs.push_back(nb);
+      Wg = std::max(Wg, (int)jb.w);
+      Hg = std::max(Hg, (int)jb.h);
+      P = std::max(P, nb > 0 ? 3 * nb - 2 : 0);
+    }
+    const int Sg = (Hg + 3) / 4;
+    for (int j = g0; j < g1; j++) {
+      const T1EncJob& jb = jobs[(size_t)j];
+      const int nb = nbs[(size_t)(j - g0)];
+      fl.assign((size_t)(Sg + 2) * (Wg + 2), 0);
+      mg.assign((size_t)Sg * Wg, 0);
+      T1EncLane<1> L;
+      L.WS = Wg + 2;
+      L.Wg = Wg;
+      L.fl = fl.data();
+      L.mg = mg.data();
+      for (int y = 0; y < jb.h; y++)
+        for (int x = 0; x < jb.w; x++) {
+          const int32_t v = (int32_t)coef[(size_t)(jb.in + (int64_t)y * jb.stride + x)];
+          const uint32_t a = (uint32_t)(v < 0 ? -v : v);
+          mg[(size_t)((y >> 2) * Wg + x)] |= (uint64_t)a << (16 * (y & 3));
+          if (v < 0) L.F(y >> 2, x) |= (uint16_t)(2u << (4 * (y & 3)));
+        }
+      L.cx = cx;
+      L.qe = qe;
+      L.zct = zct;
+      L.w = jb.w;
+      L.h = jb.h;
+      L.orient = jb.orient;
+      L.out = odata.data() + jb.out;
+      const int32_t n = t1_encode_lane(L, nb > 0, nb, Sg, P, [](bool b) { return b; });
+      off[(size_t)j] = jb.out;
+      len[(size_t)j] = (uint32_t)n;
+      nbv[(size_t)j] = (uint8_t)nb;
+    }
+  }
+  std::vector<uint8_t> file;
+  if (!encode_host_coded(img, off.data(), len.data(), nbv.data(), odata.data(), &file)) return -1;
+  return give(file, out, cap);
 }
 
 }  // extern "C"

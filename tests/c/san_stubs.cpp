@@ -15,6 +15,14 @@ bool jdec_launch(const JdecHeader&, const uint8_t*, uint8_t*, uint8_t*, int32_t*
 namespace j2k {
 size_t decode_tmp_bytes(const Image&) { return 0; }
 size_t t1_slot_bytes(int, int) { return 0; }
+size_t t1enc_slot_bytes(int, int) { return 0; }
+bool t1enc_launch(const T1EncJob*, int, const uint32_t*, uint8_t*, uint32_t*, uint8_t*, void*, int, int,
+                  int, hipStream_t) {
+  return fail("jp2: no device in the sanitizer build");
+}
+bool t1enc_pack(const T1EncJob*, int, const uint8_t*, const uint32_t*, uint32_t*, uint8_t*, hipStream_t) {
+  return fail("jp2: no device in the sanitizer build");
+}
 bool t1_launch(const T1Job*, int, const uint8_t*, uint32_t*, void*, int, int, int, hipStream_t) {
   return fail("jp2: no device in the sanitizer build");
 }

@@ -44,6 +44,9 @@ def _emul():
     E.j2k_emulate.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64, C.c_void_p]
     E.j2k_emulate_t1lane.restype = C.c_int64
     E.j2k_emulate_t1lane.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64, C.c_void_p]
+    E.j2k_emulate_encode_lane.restype = C.c_int64
+    E.j2k_emulate_encode_lane.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
+                                          C.c_int64]
     E.j2k_emulate_encode.restype = C.c_int64
     E.j2k_emulate_encode.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                      C.c_int64]
@@ -74,15 +77,19 @@ def emulate_decode(data, lane=False):
     return out.reshape(h, w, c) if c > 1 else out.reshape(h, w)
 
 
-def emulate_encode(a):
+def emulate_encode(a, lane=False):
+    """The device's forward transforms replayed, then the code-blocks through
+    j2k_t1.h's host coder (or, with lane, the device encoder's lane code in
+    64-block groups) and the host's packets."""
     E = _emul()
+    fn = E.j2k_emulate_encode_lane if lane else E.j2k_emulate_encode
     a = np.ascontiguousarray(a)
     h, w = a.shape[:2]
     c = 1 if a.ndim == 2 else 3
-    n = E.j2k_emulate_encode(a.ctypes.data, w, h, c, None, 0)
+    n = fn(a.ctypes.data, w, h, c, None, 0)
     assert n > 0, _err()
     out = np.zeros(n, np.uint8)
-    assert E.j2k_emulate_encode(a.ctypes.data, w, h, c, out.ctypes.data, n) == n
+    assert fn(a.ctypes.data, w, h, c, out.ctypes.data, n) == n
     return out.tobytes()
 
 
@@ -256,6 +263,7 @@ def test_encode_is_lossless_and_matches_openjpeg(w, h, rgb):
     a = page(w, h, w * 31 + h, rgb) if w > 8 and h > 8 else \
         np.random.default_rng(w + h).integers(0, 256, (h, w, 3) if rgb else (h, w)).astype(np.uint8)
     f = emulate_encode(a)
+    assert emulate_encode(a, lane=True) == f  # the device encoder's lane code
     assert f[:12] == b"\x00\x00\x00\x0cjP  \r\n\x87\n"
     assert (pil_decode(f) == a).all()
     assert (emulate_decode(f) == a).all()

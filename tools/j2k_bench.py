@@ -52,6 +52,21 @@ def main():
     print("jp2 %s A4 lossless: file %.2f MB, uphip_jp2_decode %.1f ms/page (host headers + device "
           "code-blocks/wavelet), host code-block decode %.0f ms/page" %
           ("RGB" if rgb else "gray", sum(len(f) for f in files) / n / 1e6, dt * 1e3, dh * 1e3), flush=True)
+    # encode: the decoded page back to a lossless file (device transforms and
+    # code-blocks, host packets); the file must equal PIL's packets
+    from unpaper_hip.pipeline import jp2_encode
+    fmt = A.FMT_RGB24 if rgb else A.FMT_GRAY8
+    f0 = jp2_encode(d.ptr, pitch, W, H, fmt)
+    back = np.asarray(Image.open(io.BytesIO(f0)))
+    assert (back == refs[-1]).all(), "encode does not round-trip"
+    body = lambda f: f[f.index(b"\xff\x93") + 2:]
+    same = body(f0) == body(files[-1])
+    t = time.perf_counter()
+    for _ in range(n):
+        jp2_encode(d.ptr, pitch, W, H, fmt)
+    de = (time.perf_counter() - t) / n
+    print("jp2 encode %.1f ms/page (%.2f MB), packets %s OpenJPEG's" %
+          (de * 1e3, len(f0) / 1e6, "equal to" if same else "DIFFERENT from"), flush=True)
     d.close()
 
 

@@ -1006,46 +1006,108 @@ bool encode_geometry(int32_t w, int32_t h, int32_t ncomp, Image* img) {
   return true;
 }
 
+namespace {
+
+// the encoder's coding parameters and code-block geometry, per component
+void encode_params(const Image& img, std::vector<TCState>* st) {
+  const Tile& T = img.tiles[0];
+  const int C = img.ncomp, NL = T.tc[0].nlevels;
+  Cod cod;
+  cod.scod = 0;
+  cod.prog = 0;
+  cod.layers = 1;
+  cod.mct = T.mct;
+  cod.nlevels = NL;
+  cod.cbw = cod.cbh = 6;
+  cod.cbsty = 0;
+  cod.reversible = 1;
+  st->assign((size_t)C, TCState());
+  for (int c = 0; c < C; c++) {
+    Qcd q;
+    q.guard = 2;
+    q.style = 0;
+    q.nexp = 3 * NL + 1;
+    for (int i = 0; i < q.nexp; i++) {
+      const int orient = i == 0 ? 0 : (i - 1) % 3 + 1;
+      const int gain = orient == 0 ? 0 : orient == 3 ? 2 : 1;
+      q.expn[i] = 8 + gain;  // OpenJPEG: exponent = precision + band gain, MCT or not
+      q.mant[i] = 0;
+    }
+    (*st)[(size_t)c].cod = cod;
+    (*st)[(size_t)c].qcd = q;
+    band_geometry(T.tc[c], cod, q, 8, &(*st)[(size_t)c]);
+  }
+}
+
+}  // namespace
+
+bool encode_jobs(const Image& img, std::vector<T1EncJob>* jobs, size_t* out_bytes) {
+  try {
+    std::vector<TCState> st;
+    encode_params(img, &st);
+    jobs->clear();
+    size_t o = 0;
+    for (int c = 0; c < img.ncomp; c++) {
+      const TileComp& tc = img.tiles[0].tc[c];
+      for (auto& R : st[(size_t)c].res)
+        for (int b = 0; b < R.nbands; b++) {
+          const Band& B = R.band[b];
+          for (const CBlk& cb : B.cb) {
+            const int bw = cb.x1 - cb.x0, bh = cb.y1 - cb.y0;
+            if (bw <= 0 || bh <= 0) continue;
+            T1EncJob j{};
+            j.in = tc.off + (int64_t)(B.py + cb.y0 - B.y0) * tc.stride + (B.px + cb.x0 - B.x0);
+            j.stride = tc.stride;
+            j.w = (uint16_t)bw;
+            j.h = (uint16_t)bh;
+            j.out = (uint32_t)o;
+            j.orient = (uint8_t)B.orient;
+            jobs->push_back(j);
+            o += (t1_enc_cap(bw, bh) + 15) & ~15u;
+            if (o > 0xFFFFFFF0u) return fail("jp2 encode: image too large");
+          }
+        }
+    }
+    *out_bytes = o;
+    return true;
+  } catch (const std::bad_alloc&) {
+    return fail("jp2 encode: out of memory");
+  }
+}
+
+namespace {
+bool encode_finish(const Image& img, const uint32_t* coef, const uint32_t* doff,
+                   const uint32_t* dlen, const uint8_t* dnb, const uint8_t* ddata,
+                   std::vector<uint8_t>* out);
+}  // namespace
+
 bool encode_host(const Image& img, const uint32_t* coef, std::vector<uint8_t>* out) {
+  return encode_finish(img, coef, nullptr, nullptr, nullptr, nullptr, out);
+}
+bool encode_host_coded(const Image& img, const uint32_t* off, const uint32_t* len,
+                       const uint8_t* nb, const uint8_t* data, std::vector<uint8_t>* out) {
+  return encode_finish(img, nullptr, off, len, nb, data, out);
+}
+
+namespace {
+// the code-blocks coded here (coef) or taken from the device (off / len / nb
+// / data, in encode_jobs' order), then packets, codestream and JP2 boxes
+bool encode_finish(const Image& img, const uint32_t* coef, const uint32_t* doff,
+                   const uint32_t* dlen, const uint8_t* dnb, const uint8_t* ddata,
+                   std::vector<uint8_t>* out) {
   try {
     const Tile& T = img.tiles[0];
     const int C = img.ncomp, NL = T.tc[0].nlevels;
     const int w = img.width, h = img.height;
-    // coding parameters as the decoder will read them
-    Cod cod;
-    cod.scod = 0;
-    cod.prog = 0;
-    cod.layers = 1;
-    cod.mct = T.mct;
-    cod.nlevels = NL;
-    cod.cbw = cod.cbh = 6;
-    cod.cbsty = 0;
-    cod.reversible = 1;
     const int ebase = 8;  // OpenJPEG: exponent = precision + band gain, MCT or not
-    std::vector<TCState> st((size_t)C);
+    std::vector<TCState> st;
+    encode_params(img, &st);
     // code every code-block; the magnitude bits set the guard bits
-    struct Coded {
-      std::vector<uint8_t> data;
-      int numbps, npasses;
-    };
-    std::vector<std::vector<Coded>> coded;  // per (c, r, band) code-blocks
     int guard = 2;
     std::vector<uint8_t> flags, buf;
     std::vector<int32_t> vals;
+    size_t bi = 0;  // block index in encode_jobs' order
     for (int c = 0; c < C; c++) {
-      Qcd q;
-      q.guard = 2;
-      q.style = 0;
-      q.nexp = 3 * NL + 1;
-      for (int i = 0; i < q.nexp; i++) {
-        const int orient = i == 0 ? 0 : (i - 1) % 3 + 1;
-        const int gain = orient == 0 ? 0 : orient == 3 ? 2 : 1;
-        q.expn[i] = ebase + gain;
-        q.mant[i] = 0;
-      }
-      st[(size_t)c].cod = cod;
-      st[(size_t)c].qcd = q;
-      band_geometry(T.tc[c], cod, q, 8, &st[(size_t)c]);
       const TileComp& tc = T.tc[c];
       for (int r = 0; r <= NL; r++) {
         Res& R = st[(size_t)c].res[(size_t)r];
@@ -1056,6 +1118,17 @@ bool encode_host(const Image& img, const uint32_t* coef, std::vector<uint8_t>* o
             cb.npasses = 0;
             cb.data.clear();
             if (bw <= 0 || bh <= 0) continue;
+            if (!coef) {  // coded on the device
+              const int nb = dnb[bi];
+              cb.numbps = nb;
+              if (nb > 0) {
+                cb.npasses = 3 * nb - 2;
+                cb.data.assign(ddata + doff[bi], ddata + doff[bi] + dlen[bi]);
+                while (guard + B.Mb - 2 < nb) guard++;
+              }
+              bi++;
+              continue;
+            }
             vals.resize((size_t)bw * bh);
             for (int y = 0; y < bh; y++) {
               const uint32_t* row = coef + tc.off + (int64_t)(B.py + cb.y0 - B.y0 + y) * tc.stride +
@@ -1232,6 +1305,7 @@ bool encode_host(const Image& img, const uint32_t* coef, std::vector<uint8_t>* o
     return fail("jp2 encode: out of memory");
   }
 }
+}  // namespace
 
 }  // namespace j2k
 }  // namespace uph
@@ -1360,15 +1434,50 @@ int64_t uphip_jp2_encode(const void* device_src, int64_t pitch, int32_t width, i
   if (pitch < (int64_t)width * ncomp) return fail("jp2_encode: pitch too small"), -1;
   j2k::Image img;
   if (!j2k::encode_geometry(width, height, ncomp, &img)) return -1;
+  std::vector<j2k::T1EncJob> jobs;
+  size_t obytes = 0;
+  if (!j2k::encode_jobs(img, &jobs, &obytes)) return -1;
+  const int njobs = (int)jobs.size();
+  int maxw = 1, maxh = 1;
+  for (const j2k::T1EncJob& j : jobs) {
+    maxw = std::max(maxw, (int)j.w);
+    maxh = std::max(maxh, (int)j.h);
+  }
+  // device: forward transforms, code-blocks, codewords packed; host: packets
   hipStream_t st = current_stream();
+  const int nslots = std::min((njobs + 63) / 64, kT1MaxSlots);
+  const size_t jb = (sizeof(j2k::T1EncJob) * (size_t)njobs + 255) & ~(size_t)255;
+  const size_t lb = ((size_t)njobs * 4 + 4 + 255) & ~(size_t)255;
   uint32_t* dc = (uint32_t*)scratch(6, (size_t)img.coef_elems * 4);
-  std::vector<uint32_t> coef((size_t)img.coef_elems);
-  if (!dc || !j2k::encode_launch(img, (const uint8_t*)device_src, pitch, dc, st) ||
-      !UPH_HIP(hipMemcpyAsync(coef.data(), dc, coef.size() * 4, hipMemcpyDeviceToHost, st)) ||
+  uint8_t* dj = (uint8_t*)scratch(3, jb);
+  void* t1s = scratch(4, (size_t)std::max(nslots, 1) * j2k::t1enc_slot_bytes(maxw, maxh));
+  uint8_t* dw = (uint8_t*)scratch(5, obytes + 2 * lb + (size_t)njobs + 16);
+  uint8_t* dpk = (uint8_t*)scratch(1, obytes + 16);
+  if (!dc || !dj || !t1s || !dw || !dpk) return -1;
+  uint32_t* dlen = (uint32_t*)(dw + obytes);
+  uint32_t* doff = (uint32_t*)(dw + obytes + lb);
+  uint8_t* dnb = dw + obytes + 2 * lb;
+  std::vector<uint32_t> off((size_t)njobs + 1), len((size_t)njobs);
+  std::vector<uint8_t> nb((size_t)njobs);
+  if (!j2k::encode_launch(img, (const uint8_t*)device_src, pitch, dc, st) ||
+      !UPH_HIP(hipMemcpyAsync(dj, jobs.data(), sizeof(j2k::T1EncJob) * (size_t)njobs,
+                              hipMemcpyHostToDevice, st)) ||
+      !j2k::t1enc_launch((const j2k::T1EncJob*)dj, njobs, dc, dw, dlen, dnb, t1s, nslots, maxw, maxh,
+                         st) ||
+      !j2k::t1enc_pack((const j2k::T1EncJob*)dj, njobs, dw, dlen, doff, dpk, st) ||
+      !UPH_HIP(hipMemcpyAsync(off.data(), doff, 4 * ((size_t)njobs + 1), hipMemcpyDeviceToHost, st)) ||
+      !UPH_HIP(hipMemcpyAsync(len.data(), dlen, 4 * (size_t)njobs, hipMemcpyDeviceToHost, st)) ||
+      !UPH_HIP(hipMemcpyAsync(nb.data(), dnb, (size_t)njobs, hipMemcpyDeviceToHost, st)) ||
       !UPH_HIP(hipStreamSynchronize(st)))
     return -1;
+  for (uint8_t v : nb)
+    if (v > 16) return fail("jp2_encode: coefficients beyond 16 bits"), -1;
+  std::vector<uint8_t> packed((size_t)off[(size_t)njobs] + 1);
+  if (off[(size_t)njobs] &&
+      !UPH_HIP(hipMemcpy(packed.data(), dpk, off[(size_t)njobs], hipMemcpyDeviceToHost)))
+    return -1;
   std::vector<uint8_t> file;
-  if (!j2k::encode_host(img, coef.data(), &file)) return -1;
+  if (!j2k::encode_host_coded(img, off.data(), len.data(), nb.data(), packed.data(), &file)) return -1;
   if (out && capacity >= (int64_t)file.size()) memcpy(out, file.data(), file.size());
   return (int64_t)file.size();
 }

@@ -104,6 +104,22 @@ bool encode_geometry(int32_t w, int32_t h, int32_t ncomp, Image* img);
 bool encode_launch(const Image& img, const uint8_t* src, int64_t pitch, uint32_t* dcoef,
                    hipStream_t st);
 bool encode_host(const Image& img, const uint32_t* coef, std::vector<uint8_t>* out);
+// The device-coded variant: the code-blocks in encode_jobs' order (their
+// codewords at data + off[i], len[i] bytes, nb[i] magnitude planes).
+struct T1EncJob;
+bool encode_jobs(const Image& img, std::vector<T1EncJob>* jobs, size_t* out_bytes);
+bool encode_host_coded(const Image& img, const uint32_t* off, const uint32_t* len,
+                       const uint8_t* nb, const uint8_t* data, std::vector<uint8_t>* out);
+// device code-block encoder: every job's codeword into its output region,
+// lengths and plane counts per job (coef: the forward transform's planes)
+size_t t1enc_slot_bytes(int maxw, int maxh);
+bool t1enc_launch(const T1EncJob* djobs, int njobs, const uint32_t* dcoef, uint8_t* dout,
+                  uint32_t* dlen, uint8_t* dnb, void* dscr, int nslots, int maxw, int maxh,
+                  hipStream_t st);
+// the codewords packed: doff[i] = exclusive prefix sum of dlen (doff[njobs]
+// = total), each job's bytes at dpacked + doff[i]
+bool t1enc_pack(const T1EncJob* djobs, int njobs, const uint8_t* dout, const uint32_t* dlen,
+                uint32_t* doff, uint8_t* dpacked, hipStream_t st);
 
 }  // namespace j2k
 }  // namespace uph

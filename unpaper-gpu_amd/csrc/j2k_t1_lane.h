@@ -61,6 +61,18 @@ J2K_HD inline uint32_t t1_six(uint32_t u, uint32_t m, uint32_t d, int sh) {
   return ((u >> (12 + sh)) & 1u) | (t1_sig4(m >> sh) << 1) | (((d >> sh) & 1u) << 5);
 }
 
+// The type and plane of pass k (cleanup at numbps first): type 0 SPP, 1 MRP,
+// 2 CUP; bpno in bpno_plus_one units (decoding stops below 1).
+J2K_HD inline void t1_pass(int k, int numbps, int* type, int* bpno) {
+  if (k == 0) {
+    *type = 2;
+    *bpno = numbps;
+  } else {
+    *type = (k - 1) % 3;
+    *bpno = numbps - 1 - (k - 1) / 3;
+  }
+}
+
 template <int LS>
 struct T1Lane {
   // wave-uniform geometry
@@ -283,16 +295,270 @@ template <int LS, class Any>
 J2K_HD void t1_decode_lane(T1Lane<LS>& L, bool active, const uint8_t* data, int numbps,
                            int npasses, int Sg, int maxpasses, Any any);
 
-// The type and plane of pass k (cleanup at numbps first): type 0 SPP, 1 MRP,
-// 2 CUP; bpno in bpno_plus_one units (decoding stops below 1).
-J2K_HD inline void t1_pass(int k, int numbps, int* type, int* bpno) {
-  if (k == 0) {
-    *type = 2;
-    *bpno = numbps;
-  } else {
-    *type = (k - 1) % 3;
-    *bpno = numbps - 1 - (k - 1) / 3;
+// ---------------------------------------------------------------------------
+// The encoder, a lane per code-block the same way (j2k_t1.h's enc_* passes):
+// the block's magnitudes as four 16-bit rows per stripe column (one 8-byte
+// word a column, lane-minor), the flags as above with every sample's sign
+// preset (a sign only counts once the sample is significant), the MQ
+// encoder's registers per lane and its bytes into the lane's output region.
+struct T1EncJob {
+  int64_t in;      // element offset of sample (0, 0) in the coefficient buffer (int32)
+  int32_t stride;  // plane row stride (elements)
+  uint16_t w, h;
+  uint32_t out;    // byte offset of the block's output region (t1_enc_cap bytes)
+  uint8_t orient, pad[3];
+};
+// output bytes a block may need: at most three decisions a sample a plane,
+// 16 planes, one byte per eight decisions, plus the flush
+J2K_HD inline uint32_t t1_enc_cap(int w, int h) { return (uint32_t)(w * h * 6 + 64); }
+
+template <int LS>
+struct T1EncLane {
+  int WS, Wg;
+  uint16_t* fl;          // flags, as T1Lane
+  const uint64_t* mg;    // magnitudes: word (s * Wg + col) * LS, row r in bits 16 r
+  uint8_t* cx;
+  const MqState* qe;
+  const uint8_t* zct;
+  int w, h, orient;
+  // MQ encoder (C.2): the last byte emitted is kept in `last` (its index n)
+  uint8_t* out;
+  int32_t n;
+  uint32_t last;
+  uint32_t a, c;
+  int ct;
+
+  J2K_HD uint16_t& F(int s, int col) const { return fl[(int64_t)((s + 1) * WS + col + 1) * LS]; }
+  J2K_HD uint64_t M4(int s, int col) const { return mg[(int64_t)(s * Wg + col) * LS]; }
+
+  J2K_HD void init() {
+    n = -1;
+    last = 0;
+    a = 0x8000;
+    c = 0;
+    ct = 12;
   }
+  J2K_HD void emit(uint32_t b) {
+    out[++n] = (uint8_t)b;
+    last = b;
+  }
+  J2K_HD void byteout() {
+    if (last == 0xFF) {
+      emit(c >> 20);
+      c &= 0xFFFFF;
+      ct = 7;
+    } else if (c < 0x8000000) {
+      emit(c >> 19);
+      c &= 0x7FFFF;
+      ct = 8;
+    } else {
+      last++;  // the carry into the byte already out
+      if (n >= 0) out[n] = (uint8_t)last;
+      if (last == 0xFF) {
+        c &= 0x7FFFFFF;
+        emit(c >> 20);
+        c &= 0xFFFFF;
+        ct = 7;
+      } else {
+        emit(c >> 19);
+        c &= 0x7FFFF;
+        ct = 8;
+      }
+    }
+  }
+  J2K_HD void renorm() {
+    do {
+      a <<= 1;
+      c <<= 1;
+      ct--;
+      if (ct == 0) byteout();
+    } while (a < 0x8000);
+  }
+  J2K_HD void enc(int k, int d) {
+    uint8_t& e = cx[k * LS];
+    const uint32_t ent = e;
+    const MqState s = qe[ent & 63u];
+    const uint32_t mps = ent >> 7;
+    a -= s.qe;
+    if ((uint32_t)d == mps) {  // CODEMPS
+      if ((a & 0x8000) == 0) {
+        if (a < s.qe) a = s.qe;
+        else c += s.qe;
+        e = (uint8_t)(s.nmps | (mps << 7));
+        renorm();
+      } else {
+        c += s.qe;
+      }
+    } else {  // CODELPS
+      if (a < s.qe) c += s.qe;
+      else a = s.qe;
+      e = (uint8_t)(s.nlps | ((s.sw ? 1u - mps : mps) << 7));
+      renorm();
+    }
+  }
+  // FLUSH (C.2.9); the codeword's length (a final 0xFF dropped)
+  J2K_HD int32_t flush() {
+    const uint32_t t = c + a;
+    c |= 0xFFFF;
+    if (c >= t) c -= 0x8000;
+    c <<= ct;
+    byteout();
+    c <<= ct;
+    byteout();
+    return last == 0xFF ? n : n + 1;
+  }
+  J2K_HD void reset_contexts() {
+    for (int k = 0; k < kNumCtx; k++) cx[k * LS] = 0;
+    cx[kCtxUni * LS] = 46;
+    cx[kCtxRl * LS] = 3;
+    cx[0] = 4;
+  }
+
+  J2K_HD void enc_sign(int r, uint32_t L6, uint32_t M6, uint32_t R6, uint32_t LN, uint32_t MN,
+                       uint32_t RN, uint32_t* Mc) {
+    auto contrib = [](uint32_t s6, uint32_t n6, int row) -> int {
+      return ((s6 >> row) & 1u) ? (((n6 >> row) & 1u) ? -1 : 1) : 0;
+    };
+    int H = contrib(L6, LN, r + 1) + contrib(R6, RN, r + 1);
+    int Vv = contrib(M6, MN, r) + contrib(M6, MN, r + 2);
+    H = H > 0 ? 1 : H < 0 ? -1 : 0;
+    Vv = Vv > 0 ? 1 : Vv < 0 ? -1 : 0;
+    int ctx, xr;
+    if (H == 0 && Vv == 0) {
+      ctx = kCtxSc;
+      xr = 0;
+    } else if (H == 0) {
+      ctx = kCtxSc + 1;
+      xr = Vv < 0;
+    } else {
+      xr = H < 0;
+      const int hv = H * Vv;
+      ctx = kCtxSc + (hv > 0 ? 4 : hv == 0 ? 3 : 2);
+    }
+    const int neg = (int)((*Mc >> (4 * r + 1)) & 1u);
+    enc(ctx, neg ^ xr);
+    *Mc |= 1u << (4 * r);
+  }
+
+  // one stripe column of pass `type` at magnitude plane p; m4 its magnitudes
+  J2K_HD void column(int type, int p, int s, uint64_t m4, uint32_t Ul, uint32_t Ml, uint32_t Dl,
+                     uint32_t Uc, uint32_t* Mc, uint32_t Dc, uint32_t Ur, uint32_t Mr, uint32_t Dr) {
+    const int rows = h - 4 * s < 4 ? h - 4 * s : 4;
+    const uint32_t L6 = t1_six(Ul, Ml, Dl, 0), R6 = t1_six(Ur, Mr, Dr, 0);
+    auto bit = [&](int r) -> int { return (int)((m4 >> (16 * r + p)) & 1u); };
+    auto nb = [&](uint32_t M6, int r) -> uint32_t {
+      return (((L6 | R6) >> r) & 7u) | ((M6 >> r) & 5u);
+    };
+    auto zc = [&](uint32_t M6, int r) -> int {
+      const int hh = (int)(((L6 >> (r + 1)) & 1u) + ((R6 >> (r + 1)) & 1u));
+      const int vv = (int)(((M6 >> r) & 1u) + ((M6 >> (r + 2)) & 1u));
+      const int dd = (int)(((L6 >> r) & 1u) + ((L6 >> (r + 2)) & 1u) + ((R6 >> r) & 1u) +
+                           ((R6 >> (r + 2)) & 1u));
+      return zct[orient * 45 + hh * 15 + vv * 5 + dd];
+    };
+    auto sig_at = [&](int r) {
+      enc_sign(r, L6, t1_six(Uc, *Mc, Dc, 0), R6, t1_six(Ul, Ml, Dl, 1), t1_six(Uc, *Mc, Dc, 1),
+               t1_six(Ur, Mr, Dr, 1), Mc);
+    };
+    if (type == 0) {  // significance propagation
+      for (int r = 0; r < rows; r++) {
+        if ((*Mc >> (4 * r)) & 1u) continue;
+        const uint32_t M6 = t1_six(Uc, *Mc, Dc, 0);
+        if (!nb(M6, r)) continue;
+        const int b = bit(r);
+        enc(zc(M6, r), b);
+        if (b) sig_at(r);
+        *Mc |= 4u << (4 * r);
+      }
+    } else if (type == 1) {  // magnitude refinement
+      for (int r = 0; r < rows; r++) {
+        if (((*Mc >> (4 * r)) & 5u) != 1u) continue;
+        const uint32_t M6 = t1_six(Uc, *Mc, Dc, 0);
+        const int ctx = ((*Mc >> (4 * r)) & 8u) ? kCtxMr + 2 : kCtxMr + (nb(M6, r) ? 1 : 0);
+        enc(ctx, bit(r));
+        *Mc |= 8u << (4 * r);
+      }
+    } else {  // cleanup
+      int r0 = 0;
+      bool done = false;
+      if (rows == 4 && (*Mc & 0x5555u) == 0u) {
+        const uint32_t M6 = t1_six(Uc, *Mc, Dc, 0);
+        if (!nb(M6, 0) && !nb(M6, 1) && !nb(M6, 2) && !nb(M6, 3)) {
+          int r = -1;
+          for (int k = 0; k < 4 && r < 0; k++)
+            if (bit(k)) r = k;
+          if (r < 0) {
+            enc(kCtxRl, 0);
+            done = true;
+          } else {
+            enc(kCtxRl, 1);
+            enc(kCtxUni, r >> 1);
+            enc(kCtxUni, r & 1);
+            sig_at(r);
+            r0 = r + 1;
+          }
+        }
+      }
+      if (!done)
+        for (int r = r0; r < rows; r++) {
+          if ((*Mc >> (4 * r)) & 5u) continue;
+          const uint32_t M6 = t1_six(Uc, *Mc, Dc, 0);
+          const int b = bit(r);
+          enc(zc(M6, r), b);
+          if (b) sig_at(r);
+        }
+      *Mc &= ~0x4444u;
+    }
+  }
+};
+
+// Encodes the lane's block (nb magnitude planes, every pass), lockstep over
+// the wave like t1_decode_lane; flags must hold the preset signs (and zero
+// elsewhere, the border included).  Returns the codeword's length.
+template <int LS, class Any>
+J2K_HD int32_t t1_encode_lane(T1EncLane<LS>& L, bool active, int nb, int Sg, int maxpasses,
+                              Any any) {
+  if (active) {
+    L.reset_contexts();
+    L.init();
+  }
+  for (int k = 0; k < maxpasses; k++) {
+    int type, p;
+    t1_pass(k, nb - 1, &type, &p);  // plane p in magnitude units
+    const bool on = active && k < 3 * nb - 2;
+    if (!any(on)) continue;
+    for (int s = 0; s < Sg; s++) {
+      uint32_t Ul = 0, Ml = 0, Dl = 0;
+      uint32_t Uc = L.F(s - 1, 0), Mc = L.F(s, 0), Dc = L.F(s + 1, 0);
+      uint32_t Ur = L.F(s - 1, 1), Mr = L.F(s, 1), Dr = L.F(s + 1, 1);
+      const bool srow = on && 4 * s < L.h;
+      uint64_t m4 = srow ? L.M4(s, 0) : 0, m4n = 0;
+      for (int col = 0; col < L.Wg; col++) {
+        uint32_t Un = 0, Mn = 0, Dn = 0;
+        if (col + 2 <= L.Wg) {
+          Un = L.F(s - 1, col + 2);
+          Mn = L.F(s, col + 2);
+          Dn = L.F(s + 1, col + 2);
+        }
+        if (srow && col + 1 < L.Wg) m4n = L.M4(s, col + 1);
+        if (srow && col < L.w) {
+          L.column(type, p, s, m4, Ul, Ml, Dl, Uc, &Mc, Dc, Ur, Mr, Dr);
+          L.F(s, col) = (uint16_t)Mc;
+        }
+        m4 = m4n;
+        Ul = Uc;
+        Uc = Ur;
+        Ur = Un;
+        Ml = Mc;
+        Mc = Mr;
+        Mr = Mn;
+        Dl = Dc;
+        Dc = Dr;
+        Dr = Dn;
+      }
+    }
+  }
+  return active ? L.flush() : 0;
 }
 
 template <int LS, class Any>

@@ -147,15 +147,319 @@ __device__ __forceinline__ int wave_max(int v) {
   return v;
 }
 
+// Flag rows of groups up to 64 blocks wide go through LDS: a ring of four
+// stripe rows (the stripes above, at and below the one being decoded, and
+// the next one arriving), each row the 64 lanes' words of Wg + 2 columns.
+// 0: flags straight from the slot (measured faster: 6 waves a SIMD hide the
+// slot's latency better than the ring's LDS lets one wave a SIMD hide
+// nothing; 209 vs 293 ms per 32-page launch)
+#ifndef UPH_T1_RING
+#define UPH_T1_RING 0
+#endif
+constexpr int kRingCols = UPH_T1_RING ? 66 : 0;
+constexpr int kRingRow = kRingCols * 64;  // uint16 words
+
+// one flag row between the scratch slot (global) and a ring row (LDS), as
+// 16-byte chunks across the lanes (the layouts are the same)
+__device__ __forceinline__ void t1_row_load(const uint16_t* g, int ws, uint4 (&r)[9]) {
+  const int n16 = ws * 8;  // 16-byte chunks in the row (ws * 64 words)
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int ch = i * 64 + threadIdx.x;
+    if (ch < n16) r[i] = reinterpret_cast<const uint4*>(g)[ch];
+  }
+}
+__device__ __forceinline__ void t1_row_put(uint16_t* l, int ws, const uint4 (&r)[9]) {
+  const int n16 = ws * 8;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int ch = i * 64 + threadIdx.x;
+    if (ch < n16) reinterpret_cast<uint4*>(l)[ch] = r[i];
+  }
+}
+__device__ __forceinline__ void t1_row_store(uint16_t* g, int ws, const uint16_t* l) {
+  const int n16 = ws * 8;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int ch = i * 64 + threadIdx.x;
+    if (ch < n16) reinterpret_cast<uint4*>(g)[ch] = reinterpret_cast<const uint4*>(l)[ch];
+  }
+}
+
+// t1_decode_lane with the flag rows in the LDS ring (groups with Wg <= 64):
+// each pass loads the first three rows, then per stripe prefetches the row
+// two below into registers, decodes the stripe from LDS, writes the stripe's
+// row back to the slot and puts the prefetched row in the freed ring row.
+// The rows cross lanes on their way (16-byte chunks), so the slot's writes
+// and the next pass's reads are ordered by the workgroup (one wave) barrier.
+__device__ __attribute__((noinline)) void t1_decode_ring(T1Lane<64>& L, bool active, const uint8_t* data, int numbps,
+                               int npasses, int Sg, int maxpasses, uint16_t* ring,
+                               uint16_t* gfl) {
+  const int lane = threadIdx.x;
+  const int WS = L.WS;
+  for (int i = lane; i < (Sg + 2) * WS * 8; i += 64) reinterpret_cast<uint4*>(gfl)[i] = make_uint4(0, 0, 0, 0);
+  L.pm = 1 << 30;
+  if (active) {
+    L.reset_contexts();
+    L.mq_init(data);
+  }
+  __syncthreads();
+  for (int k = 0; k < maxpasses; k++) {
+    int type, bpno;
+    t1_pass(k, numbps, &type, &bpno);
+    const bool on = active && k < npasses && bpno >= 1;
+    if (__ballot(on) == 0) continue;
+    if (on && type == 1) L.pm = bpno;
+    {
+      uint4 r[9];
+      for (int R = 0; R < 3 && R <= Sg + 1; R++) {
+        t1_row_load(gfl + (int64_t)R * WS * 64, WS, r);
+        t1_row_put(ring + R * kRingRow, WS, r);
+      }
+    }
+    for (int s = 0; s < Sg; s++) {
+      const int R = s + 1;
+      uint4 pre[9];
+      const bool more = R + 2 <= Sg + 1;
+      if (more) t1_row_load(gfl + (int64_t)(R + 2) * WS * 64, WS, pre);
+      const uint16_t* U = ring + ((R - 1) & 3) * kRingRow + lane;
+      uint16_t* M = ring + (R & 3) * kRingRow + lane;
+      const uint16_t* D = ring + ((R + 1) & 3) * kRingRow + lane;
+      uint32_t Ul = 0, Ml = 0, Dl = 0;
+      uint32_t Uc = U[64], Mc = M[64], Dc = D[64];
+      uint32_t Ur = U[128], Mr = M[128], Dr = D[128];
+      const bool srow = on && 4 * s < L.h;
+      for (int col = 0; col < L.Wg; col++) {
+        uint32_t Un = 0, Mn = 0, Dn = 0;
+        if (col + 2 <= L.Wg) {
+          Un = U[(col + 3) * 64];
+          Mn = M[(col + 3) * 64];
+          Dn = D[(col + 3) * 64];
+        }
+        if (srow && col < L.w) {
+          L.column(type, bpno, s, col, Ul, Ml, Dl, Uc, &Mc, Dc, Ur, Mr, Dr);
+          M[(col + 1) * 64] = (uint16_t)Mc;
+        }
+        Ul = Uc;
+        Uc = Ur;
+        Ur = Un;
+        Ml = Mc;
+        Mc = Mr;
+        Mr = Mn;
+        Dl = Dc;
+        Dc = Dr;
+        Dr = Dn;
+      }
+      __builtin_amdgcn_wave_barrier();  // this wave's LDS writes land in order before its reads
+      t1_row_store(gfl + (int64_t)R * WS * 64, WS, ring + (R & 3) * kRingRow);
+      if (more) t1_row_put(ring + ((R + 2) & 3) * kRingRow, WS, pre);
+    }
+    __syncthreads();  // the rows written back before the next pass reads them
+  }
+}
+
+// The encoder's passes with the flag rows in the LDS ring (as
+// t1_decode_ring); the magnitudes' stripe-column words from the slot,
+// prefetched a column ahead.
+__device__ __attribute__((noinline)) int32_t t1_encode_ring(T1EncLane<64>& L, bool active, int nb, int Sg, int maxpasses,
+                                  uint16_t* ring, uint16_t* gfl) {
+  const int lane = threadIdx.x;
+  const int WS = L.WS;
+  if (active) {
+    L.reset_contexts();
+    L.init();
+  }
+  __syncthreads();  // the slot's preset flags (other lanes' chunks below)
+  for (int k = 0; k < maxpasses; k++) {
+    int type, p;
+    t1_pass(k, nb - 1, &type, &p);
+    const bool on = active && k < 3 * nb - 2;
+    if (__ballot(on) == 0) continue;
+    {
+      uint4 r[9];
+      for (int R = 0; R < 3 && R <= Sg + 1; R++) {
+        t1_row_load(gfl + (int64_t)R * WS * 64, WS, r);
+        t1_row_put(ring + R * kRingRow, WS, r);
+      }
+    }
+    for (int s = 0; s < Sg; s++) {
+      const int R = s + 1;
+      uint4 pre[9];
+      const bool more = R + 2 <= Sg + 1;
+      if (more) t1_row_load(gfl + (int64_t)(R + 2) * WS * 64, WS, pre);
+      const uint16_t* U = ring + ((R - 1) & 3) * kRingRow + lane;
+      uint16_t* M = ring + (R & 3) * kRingRow + lane;
+      const uint16_t* D = ring + ((R + 1) & 3) * kRingRow + lane;
+      uint32_t Ul = 0, Ml = 0, Dl = 0;
+      uint32_t Uc = U[64], Mc = M[64], Dc = D[64];
+      uint32_t Ur = U[128], Mr = M[128], Dr = D[128];
+      const bool srow = on && 4 * s < L.h;
+      uint64_t m4 = L.M4(s, 0), m4n = 0;
+      for (int col = 0; col < L.Wg; col++) {
+        uint32_t Un = 0, Mn = 0, Dn = 0;
+        if (col + 2 <= L.Wg) {
+          Un = U[(col + 3) * 64];
+          Mn = M[(col + 3) * 64];
+          Dn = D[(col + 3) * 64];
+        }
+        if (col + 1 < L.Wg) m4n = L.M4(s, col + 1);
+        if (srow && col < L.w) {
+          L.column(type, p, s, m4, Ul, Ml, Dl, Uc, &Mc, Dc, Ur, Mr, Dr);
+          M[(col + 1) * 64] = (uint16_t)Mc;
+        }
+        m4 = m4n;
+        Ul = Uc;
+        Uc = Ur;
+        Ur = Un;
+        Ml = Mc;
+        Mc = Mr;
+        Mr = Mn;
+        Dl = Dc;
+        Dc = Dr;
+        Dr = Dn;
+      }
+      __builtin_amdgcn_wave_barrier();
+      t1_row_store(gfl + (int64_t)R * WS * 64, WS, ring + (R & 3) * kRingRow);
+      if (more) t1_row_put(ring + ((R + 2) & 3) * kRingRow, WS, pre);
+    }
+    __syncthreads();
+  }
+  return active ? L.flush() : 0;
+}
+
+// EBCOT code-block encode, a lane per block: the block's magnitudes and
+// preset signs into the slot (lane-minor), its plane count, then every pass
+// (flags through the LDS ring when the group is at most 64 wide); the
+// codeword into the job's output region.
+__global__ void __launch_bounds__(64) k_j2k_t1enc(const T1EncJob* jobs, int njobs,
+                                                  const uint32_t* coef, uint8_t* dout,
+                                                  uint32_t* dlen, uint8_t* dnb, uint8_t* scr,
+                                                  int64_t slot_bytes, int64_t mg_off) {
+  __shared__ MqState qe[47];
+  __shared__ uint8_t zct[kZcTable];
+  __shared__ uint8_t cxs[kNumCtx * 64];
+  __shared__ __attribute__((aligned(16))) uint16_t ring[UPH_T1_RING ? 4 * kRingRow : 8];
+  const int lane = threadIdx.x;
+  if (lane < 47) qe[lane] = kMq[lane];
+  for (int i = lane; i < kZcTable; i += 64) {
+    const int r = i % 45;
+    zct[i] = (uint8_t)zc_ctx(i / 45, r / 15, (r / 5) % 3, r % 5);
+  }
+  __syncthreads();
+  const int ngroups = (njobs + 63) >> 6;
+  uint8_t* slot = scr + (int64_t)blockIdx.x * slot_bytes;
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int j = g * 64 + lane;
+    const bool active = j < njobs;
+    T1EncJob job{};
+    if (active) job = jobs[j];
+    const int Wg = wave_max(job.w), Hg = wave_max(job.h);
+    const int Sg = (Hg + 3) >> 2, WS = Wg + 2;
+    uint16_t* fl = reinterpret_cast<uint16_t*>(slot) + lane;
+    uint64_t* mg = reinterpret_cast<uint64_t*>(slot + mg_off) + lane;
+    // magnitudes and signs, lane-minor; the plane count
+    uint32_t mor = 0;
+    for (int R = 0; R < Sg + 2; R++)
+      for (int col = -1; col <= Wg; col++) {
+        const int s = R - 1;
+        uint32_t f = 0;
+        uint64_t m4 = 0;
+        if (active && s >= 0 && s < Sg && col >= 0 && col < job.w) {
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int y = 4 * s + r;
+            if (y < job.h) {
+              const int32_t v = (int32_t)coef[job.in + (int64_t)y * job.stride + col];
+              const uint32_t a = (uint32_t)(v < 0 ? -v : v);
+              mor |= a;
+              m4 |= (uint64_t)(a & 0xFFFFu) << (16 * r);
+              if (v < 0) f |= 2u << (4 * r);
+            }
+          }
+        }
+        fl[(int64_t)(R * WS + col + 1) * 64] = (uint16_t)f;
+        if (s >= 0 && s < Sg && col >= 0 && col < Wg) mg[(int64_t)(s * Wg + col) * 64] = m4;
+      }
+    int nb = mor ? 32 - __builtin_clz(mor) : 0;
+    if (nb > 16) {  // beyond the 16-bit magnitude words (not from 8-bit samples): refused
+      if (active) dnb[j] = 0xFF;
+      nb = 0;
+    }
+    const int P = wave_max(nb > 0 ? 3 * nb - 2 : 0);
+    T1EncLane<64> L;
+    L.WS = WS;
+    L.Wg = Wg;
+    L.fl = fl;
+    L.mg = mg;
+    L.cx = cxs + lane;
+    L.qe = qe;
+    L.zct = zct;
+    L.w = job.w;
+    L.h = job.h;
+    L.orient = job.orient;
+    L.out = dout + job.out;
+    int32_t n;
+    if (WS <= kRingCols)
+      n = t1_encode_ring(L, active && nb > 0, nb, Sg, P, ring, reinterpret_cast<uint16_t*>(slot));
+    else
+      n = t1_encode_lane(L, active && nb > 0, nb, Sg, P, [](bool b) { return __ballot(b) != 0; });
+    if (active) {
+      dlen[j] = (uint32_t)n;
+      if (mor < 0x10000u) dnb[j] = (uint8_t)nb;
+    }
+    __syncthreads();  // the slot is rewritten by the next group
+  }
+}
+
+// exclusive prefix sum of the codeword lengths (one workgroup), total at [n]
+__global__ void __launch_bounds__(1024) k_j2k_scan(const uint32_t* len, uint32_t* off, int n) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += 1024) {
+    const int i = base + threadIdx.x;
+    const uint32_t v = i < n ? len[i] : 0u;
+    uint32_t incl = v;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = (uint32_t)__shfl_up((int)incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t before = carry;
+    for (int k = 0; k < wv; k++) before += wsum[k];
+    if (i < n) off[i] = before + incl - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = before + incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) off[n] = carry;
+}
+
+// each job's codeword to its packed offset, a wave a job
+__global__ void __launch_bounds__(256) k_j2k_gather(const T1EncJob* jobs, int njobs,
+                                                    const uint8_t* dout, const uint32_t* len,
+                                                    const uint32_t* off, uint8_t* packed) {
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= njobs) return;
+  const uint8_t* s = dout + jobs[j].out;
+  uint8_t* d = packed + off[j];
+  for (uint32_t i = threadIdx.x & 63; i < len[j]; i += 64) d[i] = s[i];
+}
+
 // EBCOT code-block decode, a lane per block (j2k_t1_lane.h): the MQ tables
-// and the context bytes in LDS, flags and values in the block's scratch slot
-// laid out lane-minor (coalesced), the decoded block into the coefficients.
+// and the context bytes in LDS, flags in the block's scratch slot laid out
+// lane-minor (coalesced; through the LDS ring for groups up to 64 wide),
+// magnitude bits there too, the decoded block into the coefficients.
 __global__ void __launch_bounds__(64) k_j2k_t1(const T1Job* jobs, int njobs, const uint8_t* data,
                                                uint32_t* coef, uint8_t* scr, int64_t slot_bytes,
                                                int64_t val_off) {
   __shared__ MqState qe[47];
   __shared__ uint8_t zct[kZcTable];
   __shared__ uint8_t cxs[kNumCtx * 64];
+  __shared__ __attribute__((aligned(16))) uint16_t ring[UPH_T1_RING ? 4 * kRingRow : 8];
   const int lane = threadIdx.x;
   if (lane < 47) qe[lane] = kMq[lane];
   for (int i = lane; i < kZcTable; i += 64) {
@@ -182,13 +486,44 @@ __global__ void __launch_bounds__(64) k_j2k_t1(const T1Job* jobs, int njobs, con
     L.w = job.w;
     L.h = job.h;
     L.orient = job.orient;
-    t1_decode_lane(L, active, data + job.data, job.numbps, job.npasses, (Hg + 3) >> 2, P,
-                   [](bool b) { return __ballot(b) != 0; });
+    if (Wg + 2 <= kRingCols)
+      t1_decode_ring(L, active, data + job.data, job.numbps, job.npasses, (Hg + 3) >> 2, P, ring,
+                     reinterpret_cast<uint16_t*>(slot));
+    else
+      t1_decode_lane(L, active, data + job.data, job.numbps, job.npasses, (Hg + 3) >> 2, P,
+                     [](bool b) { return __ballot(b) != 0; });
+    __syncthreads();  // flags written back (other lanes' chunks) before the store reads them
     t1_store_lane(L, active, job, coef, Hg);
   }
 }
 
 }  // namespace
+
+size_t t1enc_slot_bytes(int maxw, int maxh) {
+  const size_t flags = (((size_t)((maxh + 3) / 4 + 2) * (size_t)(maxw + 2) * 64 * 2) + 255) & ~(size_t)255;
+  return flags + (size_t)((maxh + 3) / 4) * (size_t)maxw * 64 * 8;
+}
+
+bool t1enc_launch(const T1EncJob* djobs, int njobs, const uint32_t* dcoef, uint8_t* dout,
+                  uint32_t* dlen, uint8_t* dnb, void* dscr, int nslots, int maxw, int maxh,
+                  hipStream_t st) {
+  if (njobs <= 0) return true;
+  const int64_t slot = (int64_t)t1enc_slot_bytes(maxw, maxh);
+  const int64_t mg_off =
+      (int64_t)((((size_t)((maxh + 3) / 4 + 2) * (size_t)(maxw + 2) * 64 * 2) + 255) & ~(size_t)255);
+  hipLaunchKernelGGL(k_j2k_t1enc, dim3((unsigned)nslots), dim3(64), 0, st, djobs, njobs, dcoef, dout,
+                     dlen, dnb, (uint8_t*)dscr, slot, mg_off);
+  return UPH_HIP(hipGetLastError());
+}
+
+bool t1enc_pack(const T1EncJob* djobs, int njobs, const uint8_t* dout, const uint32_t* dlen,
+                uint32_t* doff, uint8_t* dpacked, hipStream_t st) {
+  if (njobs <= 0) return true;
+  hipLaunchKernelGGL(k_j2k_scan, dim3(1), dim3(1024), 0, st, dlen, doff, njobs);
+  hipLaunchKernelGGL(k_j2k_gather, dim3((unsigned)((njobs + 3) / 4)), dim3(256), 0, st, djobs, njobs,
+                     dout, dlen, doff, dpacked);
+  return UPH_HIP(hipGetLastError());
+}
 
 size_t t1_slot_bytes(int maxw, int maxh) {
   const size_t flags = (((size_t)((maxh + 3) / 4 + 2) * (size_t)(maxw + 2) * 64 * 2) + 255) & ~(size_t)255;
