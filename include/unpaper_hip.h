@@ -547,9 +547,9 @@ int64_t uphip_jpeg_encode(const void *device_src, int64_t pitch, int32_t width,
  * Decode: JP2 files or raw codestreams, 8-bit unsigned, 1 or 3 components
  * (-> GRAY8 / RGB24), no subsampling, code-block style 0, any tiling,
  * precincts, progression order, layers, 5/3 or 9/7 (csrc/j2k.h).  Packet
- * headers and the EBCOT code-block decoder run on the host; the inverse
- * wavelet and component transforms, the DC shift and the store on the
- * current device.  Pixels equal OpenJPEG's (PIL's decoder) for reversible
+ * headers are read on the host; the EBCOT code-block decoder (a lane per
+ * block), the inverse wavelet and component transforms, the DC shift and
+ * the store run on the current device.  Pixels equal OpenJPEG's (PIL's decoder) for reversible
  * and irreversible files.  uphip_jp2_read returns host pixels,
  * uphip_jp2_decode writes device memory (rows `pitch` apart; info: in =
  * expected geometry when width > 0, out = geometry).  Both synchronise. */
@@ -558,16 +558,17 @@ int uphip_jp2_read(const char *path, void *dst, int64_t linesize,
                    const UphipPnmInfo *expect);
 int uphip_jp2_decode(const void *data, size_t size, void *device_dst, int64_t pitch,
                      UphipPnmInfo *info);
-/* The host half alone (no device needed): the coefficient planes
- * (csrc/j2k.h layout; int32 for 5/3 files, float for 9/7) written to `coef`
- * when `capacity` suffices; info = geometry.  Returns their size in bytes,
- * or -1. */
+/* A host decode of the coefficient planes (no device needed; the
+ * code-blocks through the host reference coder, csrc/j2k_t1.h): written to
+ * `coef` (csrc/j2k.h layout; int32 for 5/3 files, float for 9/7) when
+ * `capacity` suffices; info = geometry.  Returns their size in bytes, or
+ * -1.  Test and tooling entry; the decode paths above do not use it. */
 int64_t uphip_jp2_entropy_decode(const void *data, size_t size, void *coef, int64_t capacity,
                                  UphipPnmInfo *info);
 /* Lossless JP2 encode of a device image (GRAY8 or RGB24, rows `pitch`
- * apart): forward RCT and 5/3 wavelet on the current device, code-blocks
- * coded on the host; one tile, one layer, LRCP, 64x64 code-blocks, up to 5
- * decomposition levels.  Returns the file size; the bytes are copied to
+ * apart): forward RCT, 5/3 wavelet and the code-blocks on the current
+ * device, packets on the host; one tile, one layer, LRCP, 64x64
+ * code-blocks, up to 5 decomposition levels.  Returns the file size; the bytes are copied to
  * `out` only when `capacity` suffices (out = NULL sizes a buffer).
  * Synchronous; -1 on error. */
 int64_t uphip_jp2_encode(const void *device_src, int64_t pitch, int32_t width,

@@ -99,7 +99,9 @@ struct T1Lane {
   // a refinement bit into the sample's magnitude (the device's lanes OR
   // with a no-return atomic: nothing waits for it)
   J2K_HD void vor(int y, int x, uint32_t bits) const {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(UPH_T1_NOVAL)  // timing variant: no value traffic (wrong output)
+    (void)y, (void)x, (void)bits;
+#elif defined(__HIP_DEVICE_COMPILE__)
     __hip_atomic_fetch_or(&V(y, x), bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #else
     V(y, x) |= bits;
@@ -221,7 +223,9 @@ struct T1Lane {
     }
     const int neg = dec(ctx) ^ xr;
     *Mc |= (uint32_t)(1 | (neg << 1)) << (4 * r);
+#ifndef UPH_T1_NOVAL
     V(y, x) = one;
+#endif
   }
 
   // one stripe column of pass `type` at plane bpno (bpno_plus_one units)
