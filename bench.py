@@ -57,7 +57,7 @@ sys.path.insert(0, os.path.join(ROOT, "unpaper-gpu_amd", "python"))
 from unpaper_hip import ctypes_abi as A  # noqa: E402
 from unpaper_hip.device import load_library, UnpaperHipError  # noqa: E402
 from unpaper_hip.pipeline import (Batch, DeviceBuffer, Runner, sink_discard,  # noqa: E402
-                                  sink_jpeg, sink_memory, sink_pnm, source_memory,
+                                  sink_jp2, sink_jpeg, sink_memory, sink_pnm, source_memory,
                                   source_pnm)
 from unpaper_hip.workloads import A4_H, A4_W, C4_H, C4_W, c4_options  # noqa: E402
 
@@ -391,6 +391,34 @@ def host_io(opts, dev0, host_in, npages, args, threads):
                                  "files": "JPEG q85 (GPU encode) into tmpfs, 64 names reused, "
                                           "%.0f kB a page" % kb,
                                  "verified": same}
+            # the lossless JPEG 2000 output branch (encode_queue.c:883-962):
+            # transforms and code-blocks on the device per output page (the
+            # store tasks), packets on the host; files decode (PIL) to the
+            # oracle-verified sheets
+            nj = min(npages, 256)
+            snk = sink_jp2(os.path.join(tmpdir, "out_%04lld.jp2"), 64)
+            for rep in range(2):
+                t0 = time.perf_counter()
+                failed, err = r.run_host(nj, src, snk)
+                t = time.perf_counter() - t0
+                if failed:
+                    raise UnpaperHipError("JP2 run: %d failed: %s" % (failed, err))
+            st = r.stats()
+            failed, err = r.run_host(min(nj, 64), src, snk)  # file p holds page p again
+            if failed:
+                raise UnpaperHipError("JP2 check run: %d failed: %s" % (failed, err))
+            same = 0
+            for i, sheet in enumerate(keep):
+                back = np.asarray(Image.open(os.path.join(tmpdir, "out_%04d.jp2" % sample[i])))
+                same += bool(np.array_equal(back, sheet))
+            if same != len(keep):
+                raise SystemExit("bench.py: JP2 files do not decode to the sheets")
+            kb = os.path.getsize(os.path.join(tmpdir, "out_0000.jp2")) / 1e3
+            out["jp2_write"] = {"value": round(nj / t, 2), "unit": "pages/s",
+                                "load_s": round(st.load_s, 3), "store_s": round(st.store_s, 3),
+                                "files": "lossless JP2 (GPU transforms + code-blocks) into tmpfs, "
+                                         "%d pages, 64 names reused, %.0f kB a page" % (nj, kb),
+                                "verified": same}
         finally:
             shutil.rmtree(tmpdir, ignore_errors=True)
         out["config"] = {"sheets_per_batch": args.host_batch, "streams": args.host_streams,

@@ -151,13 +151,20 @@ struct T1Lane {
     ct -= 7;
     a = 0x8000;
   }
+  // RENORMD in chunks: the count of doublings that bring A to 0x8000 from
+  // its leading zeros, applied up to the next byte boundary at a time (the
+  // one-bit loop of C.3.3 would run up to 15 turns, and a wave takes every
+  // turn any lane needs)
   J2K_HD void renorm() {
-    do {
+    int n = __builtin_clz(a) - 16;
+    while (n > 0) {
       if (ct == 0) bytein();
-      a <<= 1;
-      c <<= 1;
-      ct--;
-    } while (a < 0x8000);
+      const int k = n < ct ? n : ct;
+      a <<= k;
+      c <<= k;
+      ct -= k;
+      n -= k;
+    }
   }
   // MqDecoder::decode with the context byte in memory
   J2K_HD int dec(int k) {
@@ -370,13 +377,17 @@ struct T1EncLane {
       }
     }
   }
+  // RENORME in chunks up to each byte-out, as the decoder's
   J2K_HD void renorm() {
-    do {
-      a <<= 1;
-      c <<= 1;
-      ct--;
+    int n = __builtin_clz(a) - 16;
+    while (n > 0) {
+      const int k = n < ct ? n : ct;
+      a <<= k;
+      c <<= k;
+      ct -= k;
+      n -= k;
       if (ct == 0) byteout();
-    } while (a < 0x8000);
+    }
   }
   J2K_HD void enc(int k, int d) {
     uint8_t& e = cx[k * LS];
