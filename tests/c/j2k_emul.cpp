@@ -368,7 +368,10 @@ int64_t j2k_emulate_encode_lane(const uint8_t* src, int32_t w, int32_t h, int32_
       L.h = jb.h;
       L.orient = jb.orient;
       L.out = odata.data() + jb.out;
+      L.cap = (int32_t)t1_enc_cap(jb.w, jb.h);
+      L.over = false;
       const int32_t n = t1_encode_lane(L, nb > 0, nb, Sg, P, [](bool b) { return b; });
+      if (L.over) return -1;
       off[(size_t)j] = jb.out;
       len[(size_t)j] = (uint32_t)n;
       nbv[(size_t)j] = (uint8_t)nb;

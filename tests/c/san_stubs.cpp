@@ -20,7 +20,8 @@ bool t1enc_launch(const T1EncJob*, int, const uint32_t*, uint8_t*, uint32_t*, ui
                   int, hipStream_t) {
   return fail("jp2: no device in the sanitizer build");
 }
-bool t1enc_pack(const T1EncJob*, int, const uint8_t*, const uint32_t*, uint32_t*, uint8_t*, hipStream_t) {
+bool t1enc_pack(const T1EncJob*, int, const uint8_t*, const uint32_t*, uint32_t*, uint8_t*, uint64_t, int32_t*,
+                bool, hipStream_t) {
   return fail("jp2: no device in the sanitizer build");
 }
 bool t1_launch(const T1Job*, int, const uint8_t*, uint32_t*, void*, int, int, int, hipStream_t) {
@@ -29,7 +30,7 @@ bool t1_launch(const T1Job*, int, const uint8_t*, uint32_t*, void*, int, int, in
 bool decode_launch(const Image&, uint32_t*, uint8_t*, int64_t, void*, hipStream_t) {
   return fail("jp2: no device in the sanitizer build");
 }
-bool encode_launch(const Image&, const uint8_t*, int64_t, uint32_t*, hipStream_t) {
+bool encode_launch(const Image&, const uint8_t*, int64_t, uint32_t*, void*, hipStream_t) {
   return fail("jp2: no device in the sanitizer build");
 }
 }  // namespace j2k

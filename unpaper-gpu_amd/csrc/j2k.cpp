@@ -1453,25 +1453,29 @@ int64_t uphip_jp2_encode(const void* device_src, int64_t pitch, int32_t width, i
   void* t1s = scratch(4, (size_t)std::max(nslots, 1) * j2k::t1enc_slot_bytes(maxw, maxh));
   uint8_t* dw = (uint8_t*)scratch(5, obytes + 2 * lb + (size_t)njobs + 16);
   uint8_t* dpk = (uint8_t*)scratch(1, obytes + 16);
-  if (!dc || !dj || !t1s || !dw || !dpk) return -1;
+  void* tmp = scratch(7, (size_t)img.coef_elems * 4);
+  if (!dc || !dj || !t1s || !dw || !dpk || !tmp) return -1;
   uint32_t* dlen = (uint32_t*)(dw + obytes);
   uint32_t* doff = (uint32_t*)(dw + obytes + lb);
   uint8_t* dnb = dw + obytes + 2 * lb;
   std::vector<uint32_t> off((size_t)njobs + 1), len((size_t)njobs);
   std::vector<uint8_t> nb((size_t)njobs);
-  if (!j2k::encode_launch(img, (const uint8_t*)device_src, pitch, dc, st) ||
+  if (!j2k::encode_launch(img, (const uint8_t*)device_src, pitch, dc, tmp, st) ||
       !UPH_HIP(hipMemcpyAsync(dj, jobs.data(), sizeof(j2k::T1EncJob) * (size_t)njobs,
                               hipMemcpyHostToDevice, st)) ||
       !j2k::t1enc_launch((const j2k::T1EncJob*)dj, njobs, dc, dw, dlen, dnb, t1s, nslots, maxw, maxh,
                          st) ||
-      !j2k::t1enc_pack((const j2k::T1EncJob*)dj, njobs, dw, dlen, doff, dpk, st) ||
+      !j2k::t1enc_pack((const j2k::T1EncJob*)dj, njobs, dw, dlen, doff, dpk, obytes, nullptr, false, st) ||
       !UPH_HIP(hipMemcpyAsync(off.data(), doff, 4 * ((size_t)njobs + 1), hipMemcpyDeviceToHost, st)) ||
       !UPH_HIP(hipMemcpyAsync(len.data(), dlen, 4 * (size_t)njobs, hipMemcpyDeviceToHost, st)) ||
       !UPH_HIP(hipMemcpyAsync(nb.data(), dnb, (size_t)njobs, hipMemcpyDeviceToHost, st)) ||
       !UPH_HIP(hipStreamSynchronize(st)))
     return -1;
   for (uint8_t v : nb)
-    if (v > 16) return fail("jp2_encode: coefficients beyond 16 bits"), -1;
+    if (v > 16)
+      return fail(v == 0xFE ? "jp2_encode: a code-block's codeword outgrew its region"
+                            : "jp2_encode: coefficients beyond 16 bits"),
+             -1;
   std::vector<uint8_t> packed((size_t)off[(size_t)njobs] + 1);
   if (off[(size_t)njobs] &&
       !UPH_HIP(hipMemcpy(packed.data(), dpk, off[(size_t)njobs], hipMemcpyDeviceToHost)))

@@ -101,7 +101,8 @@ bool t1_launch(const T1Job* djobs, int njobs, const uint8_t* ddata, uint32_t* dc
 // coefficient planes (`dcoef`, laid out as decode_host's for the encoder's
 // geometry), the host codes them.
 bool encode_geometry(int32_t w, int32_t h, int32_t ncomp, Image* img);
-bool encode_launch(const Image& img, const uint8_t* src, int64_t pitch, uint32_t* dcoef,
+// (tmp: coef_elems * 4 bytes of device line buffer)
+bool encode_launch(const Image& img, const uint8_t* src, int64_t pitch, uint32_t* dcoef, void* tmp,
                    hipStream_t st);
 bool encode_host(const Image& img, const uint32_t* coef, std::vector<uint8_t>* out);
 // The device-coded variant: the code-blocks in encode_jobs' order (their
@@ -117,9 +118,12 @@ bool t1enc_launch(const T1EncJob* djobs, int njobs, const uint32_t* dcoef, uint8
                   uint32_t* dlen, uint8_t* dnb, void* dscr, int nslots, int maxw, int maxh,
                   hipStream_t st);
 // the codewords packed: doff[i] = exclusive prefix sum of dlen (doff[njobs]
-// = total), each job's bytes at dpacked + doff[i]
+// = total; chained: the sums start at doff[0]'s value, the previous
+// sub-batch's total), each job's bytes at dpacked + doff[i]; a job past
+// `cap` packed bytes sets *derr instead
 bool t1enc_pack(const T1EncJob* djobs, int njobs, const uint8_t* dout, const uint32_t* dlen,
-                uint32_t* doff, uint8_t* dpacked, hipStream_t st);
+                uint32_t* doff, uint8_t* dpacked, uint64_t cap, int32_t* derr, bool chained,
+                hipStream_t st);
 
 }  // namespace j2k
 }  // namespace uph

@@ -319,9 +319,10 @@ struct T1EncJob {
   uint32_t out;    // byte offset of the block's output region (t1_enc_cap bytes)
   uint8_t orient, pad[3];
 };
-// output bytes a block may need: at most three decisions a sample a plane,
-// 16 planes, one byte per eight decisions, plus the flush
-J2K_HD inline uint32_t t1_enc_cap(int w, int h) { return (uint32_t)(w * h * 6 + 64); }
+// output bytes a block's region holds: two a sample (lossless 8-bit data
+// codes to ~1 byte a sample at worst, random noise) and the flush; a block
+// that needs more is reported (T1EncLane::over), not written past its region
+J2K_HD inline uint32_t t1_enc_cap(int w, int h) { return (uint32_t)(w * h * 2 + 256); }
 
 template <int LS>
 struct T1EncLane {
@@ -332,9 +333,11 @@ struct T1EncLane {
   const MqState* qe;
   const uint8_t* zct;
   int w, h, orient;
-  // MQ encoder (C.2): the last byte emitted is kept in `last` (its index n)
+  // MQ encoder (C.2): the last byte emitted is kept in `last` (its index n);
+  // bytes past `cap` are counted, not stored, and set `over`
   uint8_t* out;
-  int32_t n;
+  int32_t n, cap;
+  bool over;
   uint32_t last;
   uint32_t a, c;
   int ct;
@@ -344,13 +347,15 @@ struct T1EncLane {
 
   J2K_HD void init() {
     n = -1;
+    over = false;
     last = 0;
     a = 0x8000;
     c = 0;
     ct = 12;
   }
   J2K_HD void emit(uint32_t b) {
-    out[++n] = (uint8_t)b;
+    if (++n < cap) out[n] = (uint8_t)b;
+    else over = true;
     last = b;
   }
   J2K_HD void byteout() {
@@ -364,7 +369,7 @@ struct T1EncLane {
       ct = 8;
     } else {
       last++;  // the carry into the byte already out
-      if (n >= 0) out[n] = (uint8_t)last;
+      if (n >= 0 && n < cap) out[n] = (uint8_t)last;
       if (last == 0xFF) {
         c &= 0x7FFFFFF;
         emit(c >> 20);

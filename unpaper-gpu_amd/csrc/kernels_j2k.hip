@@ -398,24 +398,29 @@ __global__ void __launch_bounds__(64) k_j2k_t1enc(const T1EncJob* jobs, int njob
     L.h = job.h;
     L.orient = job.orient;
     L.out = dout + job.out;
+    L.cap = (int32_t)t1_enc_cap(job.w, job.h);
+    L.over = false;  // (init() runs only for blocks with planes)
     int32_t n;
     if (WS <= kRingCols)
       n = t1_encode_ring(L, active && nb > 0, nb, Sg, P, ring, reinterpret_cast<uint16_t*>(slot));
     else
       n = t1_encode_lane(L, active && nb > 0, nb, Sg, P, [](bool b) { return __ballot(b) != 0; });
     if (active) {
-      dlen[j] = (uint32_t)n;
-      if (mor < 0x10000u) dnb[j] = (uint8_t)nb;
+      dlen[j] = L.over ? 0u : (uint32_t)n;
+      if (mor < 0x10000u) dnb[j] = L.over ? 0xFE : (uint8_t)nb;  // > 16: refused by the host
     }
     __syncthreads();  // the slot is rewritten by the next group
   }
 }
 
-// exclusive prefix sum of the codeword lengths (one workgroup), total at [n]
-__global__ void __launch_bounds__(1024) k_j2k_scan(const uint32_t* len, uint32_t* off, int n) {
+// exclusive prefix sum of the codeword lengths (one workgroup), total at
+// [n]; with `base`, the sums start at *base (read before off[0] is written:
+// a chunk's sub-batches chain through it)
+__global__ void __launch_bounds__(1024) k_j2k_scan(const uint32_t* len, uint32_t* off, int n,
+                                                  const uint32_t* base) {
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t carry;
-  if (threadIdx.x == 0) carry = 0;
+  if (threadIdx.x == 0) carry = base ? *base : 0u;
   __syncthreads();
   for (int base = 0; base < n; base += 1024) {
     const int i = base + threadIdx.x;
@@ -438,12 +443,18 @@ __global__ void __launch_bounds__(1024) k_j2k_scan(const uint32_t* len, uint32_t
   if (threadIdx.x == 0) off[n] = carry;
 }
 
-// each job's codeword to its packed offset, a wave a job
+// each job's codeword to its packed offset, a wave a job; past `cap` bytes
+// of packed output the job is dropped and *err set
 __global__ void __launch_bounds__(256) k_j2k_gather(const T1EncJob* jobs, int njobs,
                                                     const uint8_t* dout, const uint32_t* len,
-                                                    const uint32_t* off, uint8_t* packed) {
+                                                    const uint32_t* off, uint8_t* packed,
+                                                    uint64_t cap, int32_t* err) {
   const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (j >= njobs) return;
+  if ((uint64_t)off[j] + len[j] > cap) {
+    if ((threadIdx.x & 63) == 0 && err) atomicOr(err, 1);
+    return;
+  }
   const uint8_t* s = dout + jobs[j].out;
   uint8_t* d = packed + off[j];
   for (uint32_t i = threadIdx.x & 63; i < len[j]; i += 64) d[i] = s[i];
@@ -517,11 +528,13 @@ bool t1enc_launch(const T1EncJob* djobs, int njobs, const uint32_t* dcoef, uint8
 }
 
 bool t1enc_pack(const T1EncJob* djobs, int njobs, const uint8_t* dout, const uint32_t* dlen,
-                uint32_t* doff, uint8_t* dpacked, hipStream_t st) {
+                uint32_t* doff, uint8_t* dpacked, uint64_t cap, int32_t* derr, bool chained,
+                hipStream_t st) {
   if (njobs <= 0) return true;
-  hipLaunchKernelGGL(k_j2k_scan, dim3(1), dim3(1024), 0, st, dlen, doff, njobs);
+  hipLaunchKernelGGL(k_j2k_scan, dim3(1), dim3(1024), 0, st, dlen, doff, njobs,
+                     chained ? (const uint32_t*)doff : (const uint32_t*)nullptr);
   hipLaunchKernelGGL(k_j2k_gather, dim3((unsigned)((njobs + 3) / 4)), dim3(256), 0, st, djobs, njobs,
-                     dout, dlen, doff, dpacked);
+                     dout, dlen, doff, dpacked, cap, derr);
   return UPH_HIP(hipGetLastError());
 }
 
@@ -591,11 +604,11 @@ bool decode_launch(const Image& img, uint32_t* dcoef, uint8_t* dst, int64_t pitc
 }
 
 bool encode_launch(const Image& img, const uint8_t* src, int64_t pitch, uint32_t* dcoef,
-                   hipStream_t st) {
+                   void* vtmp, hipStream_t st) {
   const Tile& t = img.tiles[0];
   const int w = t.x1 - t.x0, h = t.y1 - t.y0;
-  int32_t* tmp = (int32_t*)scratch(7, (size_t)w * h * 4);
-  if (!tmp) return false;
+  int32_t* tmp = (int32_t*)vtmp;
+  if (!tmp) return fail("jp2 encode: no line buffer");
   hipLaunchKernelGGL(k_j2k_in, dim3(blocks((int64_t)w * h)), dim3(256), 0, st, src, pitch, w, h,
                      img.ncomp, dcoef);
   for (int c = 0; c < img.ncomp; c++) {

@@ -467,6 +467,21 @@ struct Slot {
   uint8_t* hjpg = nullptr;
   size_t hjpg_cap = 0;
   std::vector<int64_t> jsize, joff;
+  // JPEG 2000 sink: the chunk's pages coded on the device (jp2_chunk_submit):
+  // one device arena (coefficients and code-block outputs of a sub-batch,
+  // the coder's slots, jobs, lengths, offsets, planes, packed codewords)
+  // and the pinned copies of the offsets / lengths / planes per job
+  uint8_t* dj2e = nullptr;
+  size_t dj2e_cap = 0;
+  uint8_t* hj2e = nullptr;
+  size_t hj2e_cap = 0;
+  j2k::Image j2img;
+  int32_t j2jobs = 0;         // code-blocks a page
+  uint32_t* hj2off = nullptr; // pinned views into hj2e (npages * j2jobs + 1, ...)
+  uint32_t* hj2len = nullptr;
+  uint8_t* hj2nb = nullptr;
+  int32_t* hj2err = nullptr;
+  const uint8_t* dj2pk = nullptr;  // packed codewords (device)
 };
 
 struct DeviceCtx {
@@ -614,31 +629,141 @@ void store_jpeg_sheet(UphipRunner* r, const UphipSink* k, int device, UphipBatch
   }
 }
 
-// The pages of sheet s as lossless JPEG 2000 files, each encoded from the
-// batch's output plane (uphip_jp2_encode on this task's own stream).
-void store_jp2_sheet(UphipRunner* r, const UphipSink* k, int device, UphipBatch* b, int64_t job,
-                     int s, bool* ok) {
-  thread_local std::vector<uint8_t> file;
+constexpr int kJ2kSubBatch = 16;  // pages coded per k_j2k_t1enc launch (bounds the arena)
+
+// The chunk's output pages as lossless JPEG 2000 code-blocks, queued on the
+// batch's stream once its run has finished: per sub-batch of pages the
+// forward transforms of each page, one code-block launch, the packing into
+// one buffer (offsets chained across sub-batches); then the offsets, lengths
+// and plane counts to pinned memory.  The store tasks copy each page's
+// packed bytes and write its packets and file.
+bool jp2_chunk_submit(UphipRunner* r, Slot* sl, int npg) {
+  if (npg <= 0) return true;
+  std::vector<const uint8_t*> src((size_t)npg);
+  int64_t pitch = 0;
+  int32_t w = 0, h = 0, fmt = 0;
+  for (int i = 0; i < npg; i++) {
+    const void* p = nullptr;
+    if (uphip_batch_jpeg_page(sl->b, i, &p, &pitch, &w, &h, &fmt) != 0) return false;
+    src[(size_t)i] = (const uint8_t*)p;
+  }
+  if (fmt != UPHIP_FMT_GRAY8 && fmt != UPHIP_FMT_RGB24) return fail("sink_jp2: GRAY8 or RGB24 sheets only");
+  j2k::Image& img = sl->j2img;
+  std::vector<j2k::T1EncJob> page;
+  size_t obytes = 0;
+  if (!j2k::encode_geometry(w, h, fmt == UPHIP_FMT_GRAY8 ? 1 : 3, &img) ||
+      !j2k::encode_jobs(img, &page, &obytes))
+    return false;
+  const int J = (int)page.size();
+  sl->j2jobs = J;
+  int maxw = 1, maxh = 1;
+  for (const j2k::T1EncJob& j : page) {
+    maxw = std::max(maxw, (int)j.w);
+    maxh = std::max(maxh, (int)j.h);
+  }
+  const int P = std::min(npg, kJ2kSubBatch);
+  const int nslots = std::min((P * J + 63) / 64, 1024);
+  auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
+  const size_t cb = al((size_t)P * img.coef_elems * 4), tb = al((size_t)img.coef_elems * 4);
+  const size_t ob = al((size_t)P * obytes), sb = al((size_t)nslots * j2k::t1enc_slot_bytes(maxw, maxh));
+  const size_t jb = al(sizeof(j2k::T1EncJob) * (size_t)P * J);
+  const size_t nj = (size_t)npg * J;
+  const size_t lb = al(4 * nj), fb = al(4 * (nj + 1)), nb = al(nj), eb = 256;
+  // packed codewords: the pages' raw bytes and a half more (lossless files
+  // of 8-bit pages stay below their samples); a chunk past it fails loudly
+  const uint64_t pk = (uint64_t)npg * ((uint64_t)img.coef_elems * 3 / 2 + 65536);
+  const size_t need = cb + tb + ob + sb + jb + lb + fb + nb + eb + al(pk);
+  auto grow = [](uint8_t** p, size_t* cap, size_t n, bool pinned) -> bool {
+    if (*cap >= n) return true;
+    if (*p) pinned ? hipHostFree(*p) : hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (!(pinned ? UPH_HIP(hipHostMalloc((void**)p, n, hipHostMallocDefault)) : UPH_HIP(hipMalloc((void**)p, n))))
+      return false;
+    *cap = n;
+    return true;
+  };
+  const size_t hjobs = al(sizeof(j2k::T1EncJob) * (size_t)P * J);
+  const size_t hneed = hjobs + 4 * (nj + 1) + 4 * nj + nj + 64;
+  if (!grow(&sl->dj2e, &sl->dj2e_cap, need, false) || !grow(&sl->hj2e, &sl->hj2e_cap, hneed, true))
+    return false;
+  uint8_t* a = sl->dj2e;
+  uint32_t* dcoef = (uint32_t*)a;
+  void* dtmp = a + cb;
+  uint8_t* dout = a + cb + tb;
+  void* dscr = a + cb + tb + ob;
+  j2k::T1EncJob* djobs = (j2k::T1EncJob*)(a + cb + tb + ob + sb);
+  uint32_t* dlen = (uint32_t*)(a + cb + tb + ob + sb + jb);
+  uint32_t* doff = (uint32_t*)(a + cb + tb + ob + sb + jb + lb);
+  uint8_t* dnb = a + cb + tb + ob + sb + jb + lb + fb;
+  int32_t* derr = (int32_t*)(a + cb + tb + ob + sb + jb + lb + fb + nb);
+  uint8_t* dpk = a + cb + tb + ob + sb + jb + lb + fb + nb + eb;
+  sl->dj2pk = dpk;
+  hipStream_t st = (hipStream_t)uphip_batch_stream(sl->b);
+  // the jobs of a sub-batch: page p's blocks with its coefficient and output
+  // offsets (the same for every sub-batch: staged once)
+  j2k::T1EncJob* sub = (j2k::T1EncJob*)sl->hj2e;  // pinned: the copy is asynchronous
+  for (int p = 0; p < P; p++)
+    for (int i = 0; i < J; i++) {
+      j2k::T1EncJob t = page[(size_t)i];
+      t.in += (int64_t)p * img.coef_elems;
+      t.out += (uint32_t)((size_t)p * obytes);
+      sub[(size_t)p * J + i] = t;
+    }
+  if (!UPH_HIP(hipMemcpyAsync(djobs, sub, sizeof(j2k::T1EncJob) * (size_t)P * J, hipMemcpyHostToDevice, st)) ||
+      !UPH_HIP(hipMemsetAsync(doff, 0, 4, st)) || !UPH_HIP(hipMemsetAsync(derr, 0, 4, st)))
+    return false;
+  for (int p0 = 0; p0 < npg; p0 += P) {
+    const int n = std::min(P, npg - p0);
+    for (int p = 0; p < n; p++)
+      if (!j2k::encode_launch(img, src[(size_t)(p0 + p)], pitch, dcoef + (size_t)p * img.coef_elems, dtmp, st))
+        return false;
+    const size_t j0 = (size_t)p0 * J;
+    if (!j2k::t1enc_launch(djobs, n * J, dcoef, dout, dlen + j0, dnb + j0, dscr, nslots, maxw, maxh, st) ||
+        !j2k::t1enc_pack(djobs, n * J, dout, dlen + j0, doff + j0, dpk, pk, derr, true, st))
+      return false;
+  }
+  sl->hj2off = (uint32_t*)(sl->hj2e + hjobs);
+  sl->hj2len = sl->hj2off + nj + 1;
+  sl->hj2nb = (uint8_t*)(sl->hj2len + nj);
+  sl->hj2err = (int32_t*)(((uintptr_t)(sl->hj2nb + nj) + 3) & ~(uintptr_t)3);
+  return UPH_HIP(hipMemcpyAsync(sl->hj2off, doff, 4 * (nj + 1), hipMemcpyDeviceToHost, st)) &&
+         UPH_HIP(hipMemcpyAsync(sl->hj2len, dlen, 4 * nj, hipMemcpyDeviceToHost, st)) &&
+         UPH_HIP(hipMemcpyAsync(sl->hj2nb, dnb, nj, hipMemcpyDeviceToHost, st)) &&
+         UPH_HIP(hipMemcpyAsync(sl->hj2err, derr, 4, hipMemcpyDeviceToHost, st));
+}
+
+// The pages of sheet s of a slot's chunk as JPEG 2000 files: each page's
+// packed codewords from the device, its packets and boxes here.
+void store_jp2_chunk_sheet(UphipRunner* r, const UphipSink* k, int device, const Slot* sl,
+                           int64_t job, int s, bool* ok) {
+  thread_local std::vector<uint8_t> data, file;
+  thread_local std::vector<uint32_t> off;
   const int oc = r->opts.output_count < 1 ? 1 : r->opts.output_count;
+  if (*sl->hj2err) {
+    *ok = fail("sink_jp2: code-blocks larger than the packing buffer");
+    return;
+  }
+  const int J = sl->j2jobs;
+  for (int j = 0; j < oc; j++)
+    for (int q = 0; q < J; q++)
+      if (sl->hj2nb[(size_t)(s * oc + j) * J + q] > 16) {
+        *ok = fail("sink_jp2: a code-block's codeword outgrew its region");
+        return;
+      }
   for (int j = 0; j < oc; j++) {
     const int i = s * oc + j;
-    const std::string path = sink_path(k, job * oc + j);
-    const void* src = nullptr;
-    int64_t pitch = 0;
-    int32_t w = 0, h = 0, fmt = 0;
+    const uint32_t* po = sl->hj2off + (size_t)i * J;
+    const uint32_t base = po[0], end = po[J];
+    data.resize((size_t)(end - base) + 1);
+    off.resize((size_t)J);
+    for (int q = 0; q < J; q++) off[(size_t)q] = po[q] - base;
     if (uphip_set_device(device) != 0 ||
-        uphip_batch_jpeg_page(b, i, &src, &pitch, &w, &h, &fmt) != 0) {
+        (end > base && !UPH_HIP(hipMemcpy(data.data(), sl->dj2pk + base, end - base, hipMemcpyDeviceToHost))) ||
+        !j2k::encode_host_coded(sl->j2img, off.data(), sl->hj2len + (size_t)i * J, sl->hj2nb + (size_t)i * J,
+                                data.data(), &file) ||
+        !write_file(sink_path(k, job * oc + j), file.data(), file.size()))
       *ok = false;
-      continue;
-    }
-    const size_t guess = (size_t)w * h * (fmt == UPHIP_FMT_GRAY8 ? 1 : 3) / 2 + 65536;
-    if (file.size() < guess) file.resize(guess);
-    int64_t n = uphip_jp2_encode(src, pitch, w, h, fmt, file.data(), (int64_t)file.size());
-    if (n > (int64_t)file.size()) {
-      file.resize((size_t)n);
-      n = uphip_jp2_encode(src, pitch, w, h, fmt, file.data(), n);
-    }
-    if (n <= 0 || !write_file(path, file.data(), (size_t)n)) *ok = false;
   }
 }
 
@@ -1098,6 +1223,8 @@ void uphip_runner_destroy(UphipRunner* r) {
       if (sl.dj2j) hipFree(sl.dj2j);
       if (sl.dj2c) hipFree(sl.dj2c);
       if (sl.dj2t) hipFree(sl.dj2t);
+      if (sl.dj2e) hipFree(sl.dj2e);
+      if (sl.hj2e) hipHostFree(sl.hj2e);
       for (JpegPage& jp : sl.jpg)
         if (jp.host) hipHostFree(jp.host);
     }
@@ -1472,7 +1599,8 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
               }
               queued = queued && uphip_batch_jpeg_download_async(sl->b, sl->hjpg, (int64_t)sl->hjpg_cap) == 0;
             } else if (sink->jp2) {
-              queued = true;  // the store tasks encode from the batch's planes
+              // the chunk's pages coded on the device; the store tasks write
+              queued = jp2_chunk_submit(r, sl, sl->count * oc);
             } else {
               queued = uphip_batch_download_async(sl->b, dst, r->out_linesize, r->out_sheet_stride) == 0;
             }
@@ -1512,7 +1640,7 @@ int uphip_runner_run_host(UphipRunner* r, int64_t njobs, UphipSource* src, Uphip
                   store_jpeg_sheet(r, sink, dc.device, sl->b, sl->first + s, s, sl->hjpg, sl->jsize,
                                    sl->joff, &good);
                 else if (sink->jp2)
-                  store_jp2_sheet(r, sink, dc.device, sl->b, sl->first + s, s, &good);
+                  store_jp2_chunk_sheet(r, sink, dc.device, sl, sl->first + s, s, &good);
                 else
                   store_sheet(r, sink, sl->first + s, sl->hout + (int64_t)s * r->out_sheet_stride, &good);
                 if (!good) {
