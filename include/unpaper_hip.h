@@ -579,6 +579,93 @@ int uphip_image_read(const char *path, void *dst, int64_t linesize,
                      const UphipPnmInfo *expect);
 
 /* ---------------------------------------------------------------------------
+ * PDF container (csrc/pdf.h) — the reference's pdf/pdf_reader.h and
+ * pdf/pdf_writer.h without MuPDF: a reader of scanned documents (one image
+ * per page: classic and stream cross-reference sections, object streams,
+ * incremental updates, a file scan when the xref is damaged) and an
+ * image-per-page writer.  Not provided: rendering of vector / text pages
+ * (pdf_render_page*), decryption (pdf_doc_authenticate), JBIG2 / CCITT
+ * decoding -- pages that need them fail with an error naming the cause.
+ * Functions returning int give 0 on success, -1 on error (uphip_last_error).
+ * ------------------------------------------------------------------------- */
+typedef struct UphipPdfDocument UphipPdfDocument;
+typedef struct UphipPdfWriter UphipPdfWriter;
+/* pdf_reader.h:19-28 */
+typedef enum {
+  UPHIP_PDF_IMAGE_UNKNOWN = 0,
+  UPHIP_PDF_IMAGE_JPEG = 1,
+  UPHIP_PDF_IMAGE_JP2 = 2,
+  UPHIP_PDF_IMAGE_JBIG2 = 3,
+  UPHIP_PDF_IMAGE_CCITT = 4,
+  UPHIP_PDF_IMAGE_PNG = 5,
+  UPHIP_PDF_IMAGE_RAW = 6,
+  UPHIP_PDF_IMAGE_FLATE = 7,
+} UphipPdfImageFormat;
+/* pdf_reader.h:31-44: the bytes as stored (a trailing DCT / JPX / JBIG2 /
+ * CCITT / Flate filter not applied, filters before it applied) */
+typedef struct {
+  uint8_t *data;
+  size_t size;
+  int32_t width, height;
+  int32_t components, bits_per_component;
+  int32_t format;   /* UphipPdfImageFormat */
+  int32_t is_mask;
+  uint8_t *jbig2_globals;
+  size_t jbig2_globals_size;
+} UphipPdfImage;
+/* pdf_reader.h:47-56: UTF-8 strings, NULL when absent */
+typedef struct {
+  char *title, *author, *subject, *keywords, *creator, *producer;
+  char *creation_date, *modification_date;
+} UphipPdfMetadata;
+/* pdf_reader.h:59-63 */
+typedef struct {
+  float width, height;  /* points, the page bounds after /Rotate */
+  int32_t rotation;     /* the page's /Rotate */
+} UphipPdfPageInfo;
+/* pdf_reader.c:72-214 (pdf_open, pdf_open_memory: the buffer must outlive
+ * the document, pdf_close) */
+UphipPdfDocument *uphip_pdf_open(const char *path);
+UphipPdfDocument *uphip_pdf_open_memory(const uint8_t *data, size_t size);
+void uphip_pdf_close(UphipPdfDocument *doc);
+int uphip_pdf_page_count(UphipPdfDocument *doc);      /* -1 on error */
+int uphip_pdf_needs_password(UphipPdfDocument *doc);  /* 1 = encrypted */
+int uphip_pdf_get_page_info(UphipPdfDocument *doc, int page, UphipPdfPageInfo *info);
+/* pdf_reader.c:290-433: the page's largest image XObject; free with
+ * uphip_pdf_free_image */
+int uphip_pdf_extract_page_image(UphipPdfDocument *doc, int page, UphipPdfImage *image);
+void uphip_pdf_free_image(UphipPdfImage *image);
+int uphip_pdf_get_metadata(UphipPdfDocument *doc, UphipPdfMetadata *meta);
+void uphip_pdf_free_metadata(UphipPdfMetadata *meta);
+const char *uphip_pdf_image_format_name(int32_t format);
+int uphip_pdf_is_pdf_file(const char *filename);  /* by extension, pdf_reader.c:60-70 */
+/* A page's pixels (pdf_pipeline_decode.c:278-320 without the render
+ * fallback): JPEG / JPEG 2000 images decode on the current device, Flate and
+ * raw 8-bit gray / RGB and 1-bit images on the host.  dpi > 0 applies the
+ * reference's size check (the image within 4 px of the page at `dpi`,
+ * pdf_pipeline_decode.c:69-111; a mismatch would need rendering and fails);
+ * dpi 0 takes the image as it is.  read: `expect` as uphip_image_read. */
+int uphip_pdf_page_probe(UphipPdfDocument *doc, int page, int32_t dpi, UphipPnmInfo *info);
+int uphip_pdf_read_page(UphipPdfDocument *doc, int page, int32_t dpi, void *dst,
+                        int64_t linesize, const UphipPnmInfo *expect);
+/* pdf_writer.h: pages are streamed to "<path>.part" as they are added and
+ * the file is renamed into place by close; abort removes it.  dpi <= 0 in
+ * create = 72; dpi 0 in add_page = the writer's.  Producer is "unpaper". */
+UphipPdfWriter *uphip_pdf_writer_create(const char *path, const UphipPdfMetadata *meta,
+                                        int32_t dpi);
+int uphip_pdf_writer_add_page_jpeg(UphipPdfWriter *writer, const uint8_t *data, size_t len,
+                                   int32_t width, int32_t height, int32_t dpi);
+int uphip_pdf_writer_add_page_jp2(UphipPdfWriter *writer, const uint8_t *data, size_t len,
+                                  int32_t width, int32_t height, int32_t dpi);
+/* format: 0 = GRAY8, 1 = RGB24 (PdfPixelFormat) */
+int uphip_pdf_writer_add_page_pixels(UphipPdfWriter *writer, const uint8_t *pixels,
+                                     int32_t width, int32_t height, int32_t stride,
+                                     int32_t format, int32_t dpi);
+int uphip_pdf_writer_page_count(UphipPdfWriter *writer);
+int uphip_pdf_writer_close(UphipPdfWriter *writer);  /* frees the writer */
+void uphip_pdf_writer_abort(UphipPdfWriter *writer); /* frees the writer */
+
+/* ---------------------------------------------------------------------------
  * Multi-device runner — the peer of lib/batch_worker.c (batch_process_parallel,
  * :273) + lib/threadpool.c + the decode/encode queues (lib/decode_queue.c,
  * lib/encode_queue.c) + the pinned per-stream staging of
@@ -655,6 +742,24 @@ UphipSink *uphip_sink_jpeg(const char *pattern, int64_t wrap, int32_t quality,
  * batch's device planes, on the store tasks): the .jp2 output branch of
  * lib/encode_queue.c:883-962 (nvimgcodec_default_jp2_lossless_params). */
 UphipSink *uphip_sink_jp2(const char *pattern, int64_t wrap);
+/* The PDF pipeline (pdf/pdf_pipeline_cpu_batch.c:381-496, 504-628):
+ * uphip_source_pdf reads page i of the document for input page i (JPEG /
+ * JPEG 2000 images through the device decode of the batch, Flate / raw on
+ * the load tasks; dpi as uphip_pdf_read_page).  uphip_sink_pdf writes
+ * every output page into one PDF: mode UPHIP_PDF_FAST = JPEG pages (the
+ * device encode of uphip_sink_jpeg, quality 0 = 85), UPHIP_PDF_HIGH =
+ * lossless JPEG 2000 pages (as uphip_sink_jp2); pages in output order,
+ * failed ones left out (pdf_page_accumulator.c:90-130); dpi sizes the
+ * pages (0 = 300, the reference's PDF_RENDER_DPI).  uphip_sink_finish
+ * completes the file (0 / -1); a PDF sink destroyed unfinished leaves no
+ * file. */
+#define UPHIP_PDF_FAST 0
+#define UPHIP_PDF_HIGH 1
+UphipSource *uphip_source_pdf(const char *path, int32_t dpi);
+int64_t uphip_source_page_count(UphipSource *source);
+UphipSink *uphip_sink_pdf(const char *path, const UphipPdfMetadata *meta, int32_t dpi,
+                          int32_t quality, int32_t mode);
+int uphip_sink_finish(UphipSink *sink);
 void uphip_sink_destroy(UphipSink *sink);
 
 UphipRunner *uphip_runner_create(const UphipOptions *options,

@@ -218,6 +218,105 @@ static void j2k(const char *fixtures) {
   }
 }
 
+/* the PDF reader on the fixtures (tests/golden/pdf), their truncations and
+ * byte flips: open, page info, image extraction, host pixel decode and the
+ * metadata must fail cleanly or succeed, never touch memory out of bounds;
+ * then a writer round trip */
+static void pdf_case(const UphipPdfDocument *unused, const uint8_t *p, size_t n) {
+  (void)unused;
+  UphipPdfDocument *d = uphip_pdf_open_memory(p, n);
+  if (!d) {
+    uphip_clear_error();
+    return;
+  }
+  const int np = uphip_pdf_page_count(d);
+  static uint8_t px[1 << 20];
+  for (int i = 0; i < np && i < 6; i++) {
+    UphipPdfPageInfo info;
+    UphipPdfImage im;
+    UphipPnmInfo g;
+    uphip_pdf_get_page_info(d, i, &info);
+    if (uphip_pdf_extract_page_image(d, i, &im) == 0) uphip_pdf_free_image(&im);
+    if (uphip_pdf_page_probe(d, i, 0, &g) == 0 && (g.format == UPHIP_FMT_GRAY8 || g.format == UPHIP_FMT_RGB24 ||
+                                                   g.format >= UPHIP_FMT_MONOWHITE)) {
+      const int64_t ls = g.format == UPHIP_FMT_RGB24 ? 3 * (int64_t)g.width
+                         : g.format == UPHIP_FMT_GRAY8 ? g.width : ((int64_t)g.width + 7) / 8;
+      if (ls * g.height <= (int64_t)sizeof px) {
+        UphipPdfImage im2;
+        if (uphip_pdf_extract_page_image(d, i, &im2) == 0) {
+          if (im2.format == UPHIP_PDF_IMAGE_FLATE || im2.format == UPHIP_PDF_IMAGE_RAW)
+            uphip_pdf_read_page(d, i, 0, px, ls, &g);
+          uphip_pdf_free_image(&im2);
+        }
+      }
+    }
+    uphip_clear_error();
+  }
+  UphipPdfMetadata m;
+  if (uphip_pdf_get_metadata(d, &m) == 0) uphip_pdf_free_metadata(&m);
+  uphip_pdf_close(d);
+  uphip_clear_error();
+}
+
+static void pdf(const char *dir, const char *fixtures) {
+  static const char *good[] = {"xrefstream_objstm.pdf", "incremental.pdf", "damaged_xref.pdf", "filters.pdf",
+                               "pil_multipage.pdf",     "jpx.pdf",         "encrypted.pdf",    "test_jbig2.pdf"};
+  static uint8_t raw[1 << 16], tmp[1 << 16];
+  char path[512];
+  unsigned seed = 777;
+  for (size_t i = 0; i < sizeof good / sizeof *good; i++) {
+    snprintf(path, sizeof path, "%s/../pdf/%s", fixtures, good[i]);
+    FILE *f = fopen(path, "rb");
+    if (!f) {
+      fprintf(stderr, "pdf fixture %s missing\n", path);
+      g_fail++;
+      continue;
+    }
+    const size_t n = fread(raw, 1, sizeof raw, f);
+    fclose(f);
+    UphipPdfDocument *d = uphip_pdf_open_memory(raw, n);
+    if (!d || (uphip_pdf_page_count(d) <= 0 && !uphip_pdf_needs_password(d))) {
+      fprintf(stderr, "pdf %s: %s\n", path, uphip_last_error());
+      g_fail++;
+    }
+    uphip_pdf_close(d);
+    uphip_clear_error();
+    pdf_case(NULL, raw, n);
+    for (size_t cut = 1; cut < n; cut += n / 23 + 1) {
+      pdf_case(NULL, raw, cut);
+      for (int k = 0; k < 3; k++) {
+        memcpy(tmp, raw, n);
+        seed = seed * 1103515245u + 12345u;
+        tmp[(cut + (seed >> 8)) % n] ^= (uint8_t)(1 + (seed >> 24) % 255);
+        pdf_case(NULL, tmp, n);
+      }
+    }
+  }
+  snprintf(path, sizeof path, "%s/san.pdf", dir);
+  UphipPdfMetadata meta = {0};
+  meta.title = (char *)"t\xc3\xa9st (1)";
+  UphipPdfWriter *w = uphip_pdf_writer_create(path, &meta, 200);
+  static uint8_t g[33 * 17];
+  for (size_t k = 0; k < sizeof g; k++) g[k] = (uint8_t)(k * 7);
+  if (!w || uphip_pdf_writer_add_page_pixels(w, g, 30, 17, 33, 0, 0) != 0 ||
+      uphip_pdf_writer_add_page_pixels(w, g, 11, 17, 33, 1, 0) != 0 || uphip_pdf_writer_close(w) != 0) {
+    fprintf(stderr, "pdf writer: %s\n", uphip_last_error());
+    g_fail++;
+    return;
+  }
+  UphipPdfDocument *d = uphip_pdf_open(path);
+  UphipPdfMetadata m;
+  if (!d || uphip_pdf_page_count(d) != 2 || uphip_pdf_get_metadata(d, &m) != 0 || !m.title ||
+      strcmp(m.title, meta.title) != 0) {
+    fprintf(stderr, "pdf writer round trip: %s\n", uphip_last_error());
+    g_fail++;
+  } else {
+    uphip_pdf_free_metadata(&m);
+  }
+  uphip_pdf_close(d);
+  remove(path);
+}
+
 /* crafted JPEG headers: an over-subscribed Huffman table must
  * be refused before it indexes the lookahead table, and a frame claiming far
  * more blocks than the file holds must fail without sizing anything from it */
@@ -299,6 +398,7 @@ int main(int argc, char **argv) {
   jpeg(argc > 2 ? argv[2] : "tests/golden/reference");
   jpeg_crafted();
   j2k(argc > 2 ? argv[2] : "tests/golden/reference");
+  pdf(dir, argc > 2 ? argv[2] : "tests/golden/reference");
   printf("sanitize: %d failures\n", g_fail);
   return g_fail ? 1 : 0;
 }

@@ -39,6 +39,7 @@
 #include "j2k.h"
 #include "j2k_t1_lane.h"
 #include "jpeg.h"
+#include "pdf.h"
 #include "runtime.h"
 
 using Clock = std::chrono::steady_clock;
@@ -225,6 +226,9 @@ struct UphipSource {
   const uint8_t* base = nullptr;
   int64_t linesize = 0, page_stride = 0, npages = 0;
   std::vector<std::string> paths;
+  // a PDF document: page i of it is input page i (uphip_source_pdf)
+  std::shared_ptr<uph::pdf::Document> pdf;
+  int32_t pdf_dpi = 0;
   HostRegistration reg;
 };
 
@@ -241,6 +245,10 @@ struct UphipSink {
   // lossless JPEG 2000 files (uphip_sink_jp2): transforms on the device from
   // the batch's output planes, code-blocks on the store tasks
   bool jp2 = false;
+  // one PDF of all the output pages (uphip_sink_pdf): the encoded pages go
+  // to the writer instead of files
+  std::unique_ptr<uph::pdf::Writer> pdfw;
+  int32_t pdf_dpi = 300;
   HostRegistration reg;
 };
 
@@ -338,6 +346,29 @@ UphipSource* uphip_source_pnm(const char* const* paths, int64_t npaths) {
   return s;
 }
 
+UphipSource* uphip_source_pdf(const char* path, int32_t dpi) {
+  if (!path) return fail("source_pdf: null path"), nullptr;
+  if (dpi < 0) return fail("source_pdf: dpi %d", dpi), nullptr;
+  std::vector<uint8_t> bytes;
+  if (!uph::jpeg_read_file(path, &bytes)) return nullptr;
+  auto doc = std::make_shared<uph::pdf::Document>();
+  if (!doc->open(std::move(bytes), path)) return nullptr;
+  if (doc->encrypted()) return fail("source_pdf: %s is encrypted (decryption is not supported)", path), nullptr;
+  if (doc->page_count() <= 0) return fail("source_pdf: %s has no pages", path), nullptr;
+  UphipSource* s = new UphipSource();
+  s->pdf = std::move(doc);
+  s->pdf_dpi = dpi;
+  return s;
+}
+
+int64_t uphip_source_page_count(UphipSource* s) {
+  if (!s) return fail("source_page_count: null source"), -1;
+  if (s->pdf) return s->pdf->page_count();
+  if (s->base) return s->npages;
+  if (!s->paths.empty()) return (int64_t)s->paths.size();
+  return fail("source_page_count: a callback source has no page count"), -1;
+}
+
 void uphip_source_destroy(UphipSource* s) { delete s; }
 
 UphipSink* uphip_sink_callback(UphipStoreFn store, void* user) {
@@ -397,6 +428,47 @@ UphipSink* uphip_sink_jp2(const char* pattern, int64_t wrap) {
 }
 
 UphipSink* uphip_sink_discard(void) { return new UphipSink(); }
+
+UphipSink* uphip_sink_pdf(const char* path, const UphipPdfMetadata* meta, int32_t dpi, int32_t quality,
+                          int32_t mode) {
+  if (!path) return fail("sink_pdf: null path"), nullptr;
+  if (mode != UPHIP_PDF_FAST && mode != UPHIP_PDF_HIGH) return fail("sink_pdf: unknown mode %d", mode), nullptr;
+  if (quality == 0) quality = UPHIP_JPEG_DEFAULT_QUALITY;
+  if (quality < 1 || quality > 100) return fail("sink_pdf: quality %d outside 1..100", quality), nullptr;
+  if (dpi < 0 || dpi > 1200) return fail("sink_pdf: dpi %d outside 0..1200", dpi), nullptr;
+  uph::pdf::Meta m;
+  if (meta) {
+    const char* f[8] = {meta->title,   meta->author,   meta->subject,       meta->keywords,
+                        meta->creator, meta->producer, meta->creation_date, meta->modification_date};
+    std::string* o[8] = {&m.title,   &m.author,   &m.subject,       &m.keywords,
+                         &m.creator, &m.producer, &m.creation_date, &m.modification_date};
+    for (int i = 0; i < 8; i++)
+      if (f[i]) {
+        *o[i] = f[i];
+        m.has[i] = true;
+      }
+  }
+  std::unique_ptr<uph::pdf::Writer> w(new uph::pdf::Writer());
+  if (!w->create(path, meta ? &m : nullptr, dpi ? dpi : 300)) return nullptr;
+  UphipSink* k = new UphipSink();
+  k->pdfw = std::move(w);
+  k->pdf_dpi = dpi ? dpi : 300;  // PDF_RENDER_DPI (pdf_pipeline_cpu_batch.c:41)
+  k->quality = quality;
+  k->sampling = UPHIP_JPEG_444;
+  if (mode == UPHIP_PDF_HIGH)
+    k->jp2 = true;
+  else
+    k->jpeg = true;
+  return k;
+}
+
+int uphip_sink_finish(UphipSink* k) {
+  if (!k) return fail("sink_finish: null sink"), -1;
+  if (!k->pdfw) return 0;
+  const bool ok = k->pdfw->close();
+  k->pdfw.reset();
+  return ok ? 0 : -1;
+}
 
 void uphip_sink_destroy(UphipSink* k) { delete k; }
 
@@ -598,6 +670,19 @@ bool write_file(const std::string& path, const uint8_t* p, size_t n) {
   return (fclose(f) == 0 && ok) || fail("sink_jpeg: cannot write %s", path.c_str());
 }
 
+// An encoded output page `idx` (job * output_count + page): its file, or its
+// page of the sink's PDF (the page accumulator's writes,
+// pdf_page_accumulator.c:44-62; here straight from the store task, the
+// writer orders the page tree).
+bool sink_write(const UphipSink* k, int64_t idx, const uint8_t* p, size_t n) {
+  if (!k->pdfw) return write_file(sink_path(k, idx), p, n);
+  UphipPnmInfo g{0, 0, 0};
+  if (k->jpeg ? !uph::jpeg_probe_mem(p, n, "output page", &g) : !uph::j2k::probe(p, n, "output page", &g))
+    return false;
+  return k->pdfw->add_page(idx, k->jpeg ? uph::pdf::kJpeg : uph::pdf::kJp2, p, n, g.width, g.height, 0, 0,
+                           k->pdf_dpi);
+}
+
 // The JPEG pages of sheet s of a slot's chunk into their files: from the
 // chunk's packed download, or -- a page the batch's encode buffers could not
 // hold -- encoded again on its own, on the device, from the batch's sheet.
@@ -607,9 +692,8 @@ void store_jpeg_sheet(UphipRunner* r, const UphipSink* k, int device, UphipBatch
   const int oc = r->opts.output_count < 1 ? 1 : r->opts.output_count;
   for (int j = 0; j < oc; j++) {
     const int i = s * oc + j;
-    const std::string path = sink_path(k, job * oc + j);
     if (size[(size_t)i] > 0) {
-      if (!write_file(path, packed + off[(size_t)i], (size_t)size[(size_t)i])) *ok = false;
+      if (!sink_write(k, job * oc + j, packed + off[(size_t)i], (size_t)size[(size_t)i])) *ok = false;
       continue;
     }
     const void* src = nullptr;
@@ -624,7 +708,7 @@ void store_jpeg_sheet(UphipRunner* r, const UphipSink* k, int device, UphipBatch
     std::vector<uint8_t> file(n > 0 ? (size_t)n : 0);
     if (n <= 0 ||
         uphip_jpeg_encode(src, pitch, w, h, fmt, k->quality, k->sampling, file.data(), n) != n ||
-        !write_file(path, file.data(), file.size()))
+        !sink_write(k, job * oc + j, file.data(), file.size()))
       *ok = false;
   }
 }
@@ -762,7 +846,7 @@ void store_jp2_chunk_sheet(UphipRunner* r, const UphipSink* k, int device, const
         (end > base && !UPH_HIP(hipMemcpy(data.data(), sl->dj2pk + base, end - base, hipMemcpyDeviceToHost))) ||
         !j2k::encode_host_coded(sl->j2img, off.data(), sl->hj2len + (size_t)i * J, sl->hj2nb + (size_t)i * J,
                                 data.data(), &file) ||
-        !write_file(sink_path(k, job * oc + j), file.data(), file.size()))
+        !sink_write(k, job * oc + j, file.data(), file.size()))
       *ok = false;
   }
 }
@@ -777,28 +861,25 @@ bool is_jpeg_file(const std::string& path) {
 }
 
 // The host half of a JPEG page into the slot's pinned buffer `jp`.
-bool jpeg_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp) {
-  // per pool thread, kept across pages: fresh multi-MB buffers per page would
-  // page-fault (and contend on the address space) on every load
-  thread_local std::vector<uint8_t> file;
+bool jpeg_load_mem(UphipRunner* r, int device, const uint8_t* data, size_t size, const char* name,
+                   JpegPage* jp) {
   thread_local JdecStreamHost S;
-  if (!jpeg_read_file(path.c_str(), &file)) return false;
   // the frame header first: a file of the wrong geometry (or a crafted one
   // claiming a huge frame) is refused before anything is sized from it
   UphipPnmInfo info{0, 0, 0};
-  if (!jpeg_probe_mem(file.data(), file.size(), path.c_str(), &info)) return false;
+  if (!jpeg_probe_mem(data, size, name, &info)) return false;
   if (info.width != r->geo.page_width || info.height != r->geo.page_height ||
       info.format != r->geo.page_format)
-    return fail("jpeg: %s is %dx%d format %d, expected %dx%d format %d", path.c_str(), info.width,
+    return fail("jpeg: %s is %dx%d format %d, expected %dx%d format %d", name, info.width,
                 info.height, info.format, r->geo.page_width, r->geo.page_height,
                 r->geo.page_format);
   // a one-scan sequential file goes to the device as its unstuffed entropy
   // data (Huffman decoding there too); progressive / multi-scan files are
   // entropy-decoded here
-  const int dev = jpeg_stream_prepare(file.data(), file.size(), path.c_str(), &S);
+  const int dev = jpeg_stream_prepare(data, size, name, &S);
   if (dev < 0) return false;
   JpegDecoded d;
-  if (!dev && !jpeg_entropy_decode(file.data(), file.size(), path.c_str(), &d)) return false;
+  if (!dev && !jpeg_entropy_decode(data, size, name, &d)) return false;
   // pinned memory for this device (the pool thread may have another current)
   if (uphip_set_device(device) != 0) return false;
   const size_t need = (size_t)(dev ? S.hd.total_bytes : d.h.total_bytes);
@@ -821,6 +902,14 @@ bool jpeg_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp
   return true;
 }
 
+bool jpeg_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp) {
+  // per pool thread, kept across pages: fresh multi-MB buffers per page would
+  // page-fault (and contend on the address space) on every load
+  thread_local std::vector<uint8_t> file;
+  if (!jpeg_read_file(path.c_str(), &file)) return false;
+  return jpeg_load_mem(r, device, file.data(), file.size(), path.c_str(), jp);
+}
+
 bool is_j2k_file(const std::string& path) {
   FILE* f = fopen(path.c_str(), "rb");
   if (!f) return false;
@@ -832,18 +921,17 @@ bool is_j2k_file(const std::string& path) {
 
 // The host half of a JPEG 2000 page (headers, packet headers) into the
 // slot's pinned buffer `jp`: its code-block jobs, then their codewords.
-bool j2k_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp) {
-  thread_local std::vector<uint8_t> file;
+bool j2k_load_mem(UphipRunner* r, int device, const uint8_t* data, size_t size, const char* name,
+                  JpegPage* jp) {
   thread_local j2k::T1Batch tb;
-  if (!jpeg_read_file(path.c_str(), &file)) return false;
   UphipPnmInfo info{0, 0, 0};
-  if (!j2k::probe(file.data(), file.size(), path.c_str(), &info)) return false;
+  if (!j2k::probe(data, size, name, &info)) return false;
   if (info.width != r->geo.page_width || info.height != r->geo.page_height ||
       info.format != r->geo.page_format)
-    return fail("jp2: %s is %dx%d format %d, expected %dx%d format %d", path.c_str(), info.width,
+    return fail("jp2: %s is %dx%d format %d, expected %dx%d format %d", name, info.width,
                 info.height, info.format, r->geo.page_width, r->geo.page_height,
                 r->geo.page_format);
-  if (!j2k::decode_host(file.data(), file.size(), path.c_str(), &jp->img, nullptr, &tb)) return false;
+  if (!j2k::decode_host(data, size, name, &jp->img, nullptr, &tb)) return false;
   if (uphip_set_device(device) != 0) return false;
   jp->njobs = (int32_t)tb.jobs.size();
   jp->jobs_bytes = (sizeof(j2k::T1Job) * tb.jobs.size() + 255) & ~(size_t)255;
@@ -868,12 +956,38 @@ bool j2k_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp)
   return true;
 }
 
+bool j2k_load(UphipRunner* r, int device, const std::string& path, JpegPage* jp) {
+  thread_local std::vector<uint8_t> file;
+  if (!jpeg_read_file(path.c_str(), &file)) return false;
+  return j2k_load_mem(r, device, file.data(), file.size(), path.c_str(), jp);
+}
+
+// Page `idx` of a PDF source (the decode queue of the PDF pipeline,
+// pdf_pipeline_cpu_batch.c:381-496): its image's JPEG / JPEG 2000 bytes to
+// the device decode like a file's, Flate / raw pixels decoded here.
+bool pdf_load(UphipRunner* r, int device, const UphipSource* s, int64_t idx, uint8_t* dst, JpegPage* jp) {
+  if (idx < 0 || idx >= s->pdf->page_count())
+    return fail("source_pdf: page %lld out of range (%d pages)", (long long)idx, s->pdf->page_count());
+  thread_local pdf::PageImage im;
+  UphipPnmInfo g{0, 0, 0};
+  if (!pdf::page_geometry(*s->pdf, (int)idx, s->pdf_dpi, &im, &g)) return false;
+  char name[64];
+  snprintf(name, sizeof(name), "pdf page %lld", (long long)idx);
+  if (im.format == pdf::kJpeg) return jpeg_load_mem(r, device, im.data.data(), im.data.size(), name, jp);
+  if (im.format == pdf::kJp2) return j2k_load_mem(r, device, im.data.data(), im.data.size(), name, jp);
+  if (g.width != r->geo.page_width || g.height != r->geo.page_height || g.format != r->geo.page_format)
+    return fail("pdf: %s is %dx%d format %d, expected %dx%d format %d", name, g.width, g.height, g.format,
+                r->geo.page_width, r->geo.page_height, r->geo.page_format);
+  return pdf::decode_pixels(im, dst, r->in_pitch, name);
+}
+
 bool load_page(UphipRunner* r, int device, const UphipSource* s, int64_t job, int32_t j,
                uint8_t* dst, JpegPage* jp) {
   const UphipPnmInfo geo{r->geo.page_width, r->geo.page_height, r->geo.page_format};
   const int64_t idx = job * r->opts.input_count + j;
   if (s->load) return s->load(s->user, job, j, dst, r->in_pitch) == 0;
   if (s->base) return mem_load(s, idx, dst, r->in_pitch, geo) == 0;
+  if (s->pdf) return pdf_load(r, device, s, idx, dst, jp);
   if (idx >= 0 && idx < (int64_t)s->paths.size()) {
     const std::string& path = s->paths[(size_t)idx];
     if (is_jpeg_file(path)) return jpeg_load(r, device, path, jp);

@@ -280,3 +280,21 @@ ABI_STRUCTS = {
     "UphipDeskewParameters": DeskewParameters, "UphipOptions": Options,
     "UphipSheetReport": SheetReport, "UphipBatchGeometry": BatchGeometry,
 }
+
+
+# PDF container (include/unpaper_hip.h, pdf/pdf_reader.h:31-63 peers)
+class PdfImage(C.Structure):
+    _fields_ = [("data", C.POINTER(C.c_uint8)), ("size", C.c_size_t),
+                ("width", C.c_int32), ("height", C.c_int32),
+                ("components", C.c_int32), ("bits_per_component", C.c_int32),
+                ("format", C.c_int32), ("is_mask", C.c_int32),
+                ("jbig2_globals", C.POINTER(C.c_uint8)), ("jbig2_globals_size", C.c_size_t)]
+
+
+class PdfMetadata(C.Structure):
+    _fields_ = [(n, C.c_char_p) for n in ("title", "author", "subject", "keywords", "creator",
+                                           "producer", "creation_date", "modification_date")]
+
+
+class PdfPageInfo(C.Structure):
+    _fields_ = [("width", C.c_float), ("height", C.c_float), ("rotation", C.c_int32)]

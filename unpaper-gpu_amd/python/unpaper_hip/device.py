@@ -57,6 +57,14 @@ EXPORTED = [
     "uphip_batch_jpeg_download_async", "uphip_batch_jpeg_page", "uphip_sink_jpeg",
     "uphip_detect_rotation_peaks", "uphip_jp2_probe", "uphip_jp2_read", "uphip_jp2_decode",
     "uphip_jp2_encode", "uphip_sink_jp2", "uphip_jp2_entropy_decode",
+    "uphip_pdf_open", "uphip_pdf_open_memory", "uphip_pdf_close", "uphip_pdf_page_count",
+    "uphip_pdf_needs_password", "uphip_pdf_get_page_info", "uphip_pdf_extract_page_image",
+    "uphip_pdf_free_image", "uphip_pdf_get_metadata", "uphip_pdf_free_metadata",
+    "uphip_pdf_image_format_name", "uphip_pdf_is_pdf_file", "uphip_pdf_page_probe",
+    "uphip_pdf_read_page", "uphip_pdf_writer_create", "uphip_pdf_writer_add_page_jpeg",
+    "uphip_pdf_writer_add_page_jp2", "uphip_pdf_writer_add_page_pixels",
+    "uphip_pdf_writer_page_count", "uphip_pdf_writer_close", "uphip_pdf_writer_abort",
+    "uphip_source_pdf", "uphip_source_page_count", "uphip_sink_pdf", "uphip_sink_finish",
 ]
 
 
@@ -223,6 +231,36 @@ def load_library(path=LIB_PATH):
         "uphip_sink_jp2": (C.c_void_p, [C.c_char_p, C.c_int64]),
         "uphip_jp2_entropy_decode": (C.c_int64, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64,
                                                  C.POINTER(A.PnmInfo)]),
+        "uphip_pdf_open": (C.c_void_p, [C.c_char_p]),
+        "uphip_pdf_open_memory": (C.c_void_p, [C.c_void_p, C.c_size_t]),
+        "uphip_pdf_close": (None, [C.c_void_p]),
+        "uphip_pdf_page_count": (C.c_int, [C.c_void_p]),
+        "uphip_pdf_needs_password": (C.c_int, [C.c_void_p]),
+        "uphip_pdf_get_page_info": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(A.PdfPageInfo)]),
+        "uphip_pdf_extract_page_image": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(A.PdfImage)]),
+        "uphip_pdf_free_image": (None, [C.POINTER(A.PdfImage)]),
+        "uphip_pdf_get_metadata": (C.c_int, [C.c_void_p, C.POINTER(A.PdfMetadata)]),
+        "uphip_pdf_free_metadata": (None, [C.POINTER(A.PdfMetadata)]),
+        "uphip_pdf_image_format_name": (C.c_char_p, [C.c_int32]),
+        "uphip_pdf_is_pdf_file": (C.c_int, [C.c_char_p]),
+        "uphip_pdf_page_probe": (C.c_int, [C.c_void_p, C.c_int, C.c_int32, C.POINTER(A.PnmInfo)]),
+        "uphip_pdf_read_page": (C.c_int, [C.c_void_p, C.c_int, C.c_int32, C.c_void_p, C.c_int64,
+                                          C.POINTER(A.PnmInfo)]),
+        "uphip_pdf_writer_create": (C.c_void_p, [C.c_char_p, C.POINTER(A.PdfMetadata), C.c_int32]),
+        "uphip_pdf_writer_add_page_jpeg": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t,
+                                                     C.c_int32, C.c_int32, C.c_int32]),
+        "uphip_pdf_writer_add_page_jp2": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t,
+                                                    C.c_int32, C.c_int32, C.c_int32]),
+        "uphip_pdf_writer_add_page_pixels": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
+                                                       C.c_int32, C.c_int32, C.c_int32]),
+        "uphip_pdf_writer_page_count": (C.c_int, [C.c_void_p]),
+        "uphip_pdf_writer_close": (C.c_int, [C.c_void_p]),
+        "uphip_pdf_writer_abort": (None, [C.c_void_p]),
+        "uphip_source_pdf": (C.c_void_p, [C.c_char_p, C.c_int32]),
+        "uphip_source_page_count": (C.c_int64, [C.c_void_p]),
+        "uphip_sink_pdf": (C.c_void_p, [C.c_char_p, C.POINTER(A.PdfMetadata), C.c_int32, C.c_int32,
+                                        C.c_int32]),
+        "uphip_sink_finish": (C.c_int, [C.c_void_p]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(L, name):

@@ -315,6 +315,24 @@ def source_pnm(paths):
     return _Handle(h, L.uphip_source_destroy, (arr,))
 
 
+def source_pdf(path, dpi=0):
+    """Page i of a PDF as input page i (uphip_source_pdf; dpi 0 = the page
+    images as they are, dpi > 0 = the reference's size check)."""
+    L = load_library()
+    h = L.uphip_source_pdf(path.encode(), dpi)
+    _check(L)
+    if not h:
+        raise UnpaperHipError("source_pdf failed")
+    return _Handle(h, L.uphip_source_destroy)
+
+
+def source_page_count(src):
+    L = load_library()
+    n = L.uphip_source_page_count(src.handle)
+    _check(L)
+    return n
+
+
 def source_callback(fn):
     """fn(job, page, dst_ptr, linesize) -> 0 on success (called from C threads)."""
     L = load_library()
@@ -386,6 +404,29 @@ def jp2_encode(device_ptr, pitch, width, height, fmt):
     if n <= 0:
         raise UnpaperHipError("jp2_encode failed")
     return buf[:n].tobytes()
+
+
+class _PdfSink(_Handle):
+    def finish(self):
+        """Completes the PDF (uphip_sink_finish)."""
+        L = load_library()
+        if self.handle and L.uphip_sink_finish(self.handle) != 0:
+            _check(L)
+            raise UnpaperHipError("sink_finish failed")
+
+
+def sink_pdf(path, meta=None, dpi=0, quality=0, mode=0):
+    """All output pages into one PDF (uphip_sink_pdf): mode 0 = JPEG pages
+    (fast), 1 = lossless JPEG 2000 pages (high); dpi 0 = 300.  Call
+    finish() after the run."""
+    from .pdf import _meta_struct
+    L = load_library()
+    m, keep = _meta_struct(meta)
+    h = L.uphip_sink_pdf(path.encode(), C.byref(m) if m is not None else None, dpi, quality, mode)
+    _check(L)
+    if not h:
+        raise UnpaperHipError("sink_pdf failed")
+    return _PdfSink(h, L.uphip_sink_destroy, (m, keep))
 
 
 def sink_discard():
