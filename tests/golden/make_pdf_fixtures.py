@@ -144,6 +144,155 @@ def jpeg_bytes(arr, **kw):
     return b.getvalue()
 
 
+# ---------------------------------------------------------------------------
+# JBIG2 generic-region encoder (T.88 6.2 with the E.2 MQ encoder), written
+# from the standard for these fixtures: templates 0-3, typical prediction,
+# adaptive template pixels; the decoder under test must give the bitmaps back
+# ---------------------------------------------------------------------------
+QE = [(0x5601, 1, 1, 1), (0x3401, 2, 6, 0), (0x1801, 3, 9, 0), (0x0AC1, 4, 12, 0), (0x0521, 5, 29, 0),
+      (0x0221, 38, 33, 0), (0x5601, 7, 6, 1), (0x5401, 8, 14, 0), (0x4801, 9, 14, 0), (0x3801, 10, 14, 0),
+      (0x3001, 11, 17, 0), (0x2401, 12, 18, 0), (0x1C01, 13, 20, 0), (0x1601, 29, 21, 0), (0x5601, 15, 14, 1),
+      (0x5401, 16, 14, 0), (0x5101, 17, 15, 0), (0x4801, 18, 16, 0), (0x3801, 19, 17, 0), (0x3401, 20, 18, 0),
+      (0x3001, 21, 19, 0), (0x2801, 22, 19, 0), (0x2401, 23, 20, 0), (0x2201, 24, 21, 0), (0x1C01, 25, 22, 0),
+      (0x1801, 26, 23, 0), (0x1601, 27, 24, 0), (0x1401, 28, 25, 0), (0x1201, 29, 26, 0), (0x1101, 30, 27, 0),
+      (0x0AC1, 31, 28, 0), (0x09C1, 32, 29, 0), (0x08A1, 33, 30, 0), (0x0521, 34, 31, 0), (0x0441, 35, 32, 0),
+      (0x02A1, 36, 33, 0), (0x0221, 37, 34, 0), (0x0141, 38, 35, 0), (0x0111, 39, 36, 0), (0x0085, 40, 37, 0),
+      (0x0049, 41, 38, 0), (0x0025, 42, 39, 0), (0x0015, 43, 40, 0), (0x0009, 44, 41, 0), (0x0005, 45, 42, 0),
+      (0x0001, 45, 43, 0), (0x5601, 46, 46, 0)]
+
+
+class MqEnc:
+    def __init__(self):
+        self.a, self.c, self.ct, self.b = 0x8000, 0, 12, None
+        self.out = bytearray()
+        self.idx, self.mps = {}, {}
+
+    def _byteout(self):
+        if self.b == 0xFF:
+            self._emit(self.c >> 20, 0xFFFFF, 7)
+        elif self.c < 0x8000000:
+            self._emit(self.c >> 19, 0x7FFFF, 8)
+        else:
+            self.b += 1
+            if self.b == 0xFF:
+                self.c &= 0x7FFFFFF
+                self._emit(self.c >> 20, 0xFFFFF, 7)
+            else:
+                self._emit(self.c >> 19, 0x7FFFF, 8)
+
+    def _emit(self, byte, mask, ct):
+        if self.b is not None:
+            self.out.append(self.b)
+        self.b = byte & 0xFF
+        self.c &= mask
+        self.ct = ct
+
+    def _renorm(self):
+        while True:
+            self.a = (self.a << 1) & 0xFFFFFFFF
+            self.c = (self.c << 1) & 0xFFFFFFFF
+            self.ct -= 1
+            if self.ct == 0:
+                self._byteout()
+            if self.a & 0x8000:
+                break
+
+    def encode(self, cx, d):
+        i, m = self.idx.get(cx, 0), self.mps.get(cx, 0)
+        qe, nmps, nlps, sw = QE[i]
+        self.a -= qe
+        if d == m:
+            if self.a & 0x8000:
+                self.c += qe
+                return
+            if self.a < qe:
+                self.a = qe
+            else:
+                self.c += qe
+            self.idx[cx] = nmps
+        else:
+            if self.a < qe:
+                self.c += qe
+            else:
+                self.a = qe
+            if sw:
+                self.mps[cx] = 1 - m
+            self.idx[cx] = nlps
+        self._renorm()
+
+    def flush(self):
+        tempc = self.c + self.a
+        self.c |= 0xFFFF
+        if self.c >= tempc:
+            self.c -= 0x8000
+        self.c = (self.c << self.ct) & 0xFFFFFFFF
+        self._byteout()
+        self.c = (self.c << self.ct) & 0xFFFFFFFF
+        self._byteout()
+        if self.b != 0xFF:
+            self.out.append(self.b)
+        self.out += b"\xff\xac"
+        return bytes(self.out)
+
+
+def jbig2_context(bm, x, y, tmpl, at):
+    def p(dx, dy):
+        xx, yy = x + dx, y + dy
+        return int(bm[yy, xx]) if 0 <= xx < bm.shape[1] and 0 <= yy < bm.shape[0] else 0
+    if tmpl == 0:
+        bits = [(-1, 0), (-2, 0), (-3, 0), (-4, 0), (at[0], at[1]), (2, -1), (1, -1), (0, -1), (-1, -1), (-2, -1),
+                (at[2], at[3]), (at[4], at[5]), (1, -2), (0, -2), (-1, -2), (at[6], at[7])]
+    elif tmpl == 1:
+        bits = [(-1, 0), (-2, 0), (-3, 0), (at[0], at[1]), (2, -1), (1, -1), (0, -1), (-1, -1), (-2, -1),
+                (2, -2), (1, -2), (0, -2), (-1, -2)]
+    elif tmpl == 2:
+        bits = [(-1, 0), (-2, 0), (at[0], at[1]), (1, -1), (0, -1), (-1, -1), (-2, -1), (1, -2), (0, -2), (-1, -2)]
+    else:
+        bits = [(-1, 0), (-2, 0), (-3, 0), (-4, 0), (at[0], at[1]), (1, -1), (0, -1), (-1, -1), (-2, -1), (-3, -1)]
+    return sum(p(dx, dy) << k for k, (dx, dy) in enumerate(bits))
+
+
+def jbig2_generic(bm, tmpl, tpgdon, at):
+    enc = MqEnc()
+    sltp = [0x9B25, 0x0795, 0x00E5, 0x0195][tmpl]
+    ltp = 0
+    h, w = bm.shape
+    for y in range(h):
+        if tpgdon:
+            same = bool((bm[y] == (bm[y - 1] if y else 0)).all())
+            enc.encode(sltp, int(same != bool(ltp)))
+            ltp = int(same)
+            if same:
+                continue
+        for x in range(w):
+            enc.encode(jbig2_context(bm, x, y, tmpl, at), int(bm[y, x]))
+    return enc.flush()
+
+
+def jbig2_stream(bm, tmpl, tpgdon, at, striped=False, unknown_len=False):
+    h, w = bm.shape
+
+    def seg(num, typ, data, length=None):
+        return (num.to_bytes(4, "big") + bytes([typ]) + b"\x00" + b"\x01" +
+                (len(data) if length is None else length).to_bytes(4, "big") + data)
+    page = (w.to_bytes(4, "big") + (0xFFFFFFFF if striped else h).to_bytes(4, "big") + bytes(8) + b"\x00" +
+            ((0x8000 | h) if striped else 0).to_bytes(2, "big"))
+    nat = 8 if tmpl == 0 else 2
+    gflags = (tmpl << 1) | (8 if tpgdon else 0)
+    data = jbig2_generic(bm, tmpl, tpgdon, at)
+    region = (w.to_bytes(4, "big") + h.to_bytes(4, "big") + bytes(8) + b"\x00" + bytes([gflags]) +
+              bytes(v & 255 for v in at[:nat]) + data)
+    out = seg(0, 48, page)
+    if unknown_len:
+        out += seg(1, 38, region + h.to_bytes(4, "big"), 0xFFFFFFFF)
+    else:
+        out += seg(1, 38, region)
+    if striped:
+        out += seg(2, 50, (h - 1).to_bytes(4, "big"))
+    out += seg(3, 49, b"")
+    return out
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     expected = {}
@@ -326,6 +475,33 @@ def main():
     record("jpx.pdf", d.serialise(), [
         {"format": "JPEG2000", "w": gw, "h": gh, "c": 1, "bpc": 8, "data": sha(jp2), "box": [gw, gh, 0]},
     ])
+
+    # 8. JBIG2 generic regions: templates 0 (moved AT pixels) to 3, typical
+    #    prediction, a striped page with an end-of-stripe and an unknown-length
+    #    region; expanded to GRAY8 as jbig2_expand_to_gray8 (1 -> 0, 0 -> 255)
+    rng = np.random.default_rng(88)
+    d = Doc()
+    d.add(1, b"<< /Type /Catalog /Pages 2 0 R >>")
+    cases = [(0, False, [2, -1, -4, -1, 1, -2, -3, -2], {}), (1, True, [3, -1], {}), (2, False, [2, -1], {}),
+             (3, True, [2, -1], {"striped": True, "unknown_len": True}), (0, True, [3, -1, -3, -1, 2, -2, -2, -2], {})]
+    kids, pages = [], []
+    for k, (tmpl, tp, at, kw) in enumerate(cases):
+        h, w = 37 + 3 * k, 61 + 5 * k
+        bm = np.zeros((h, w), np.uint8)
+        for _ in range(12):  # blobs and lines, repeated rows for typical prediction
+            y0, x0 = rng.integers(0, h - 6), rng.integers(0, w - 10)
+            bm[y0:y0 + rng.integers(1, 6), x0:x0 + rng.integers(2, 10)] = 1
+        bm[h // 2:h // 2 + 4] = bm[h // 2]
+        stream = jbig2_stream(bm, tmpl, tp, at, **kw)
+        first = 3 + 3 * k
+        kids.append(b"%d 0 R" % (first + 2))
+        page_objs(d, first, b"<< /Type /XObject /Subtype /Image /Width %d /Height %d /ColorSpace /DeviceGray "
+                  b"/BitsPerComponent 1 /Filter /JBIG2Decode /Length %d >>" % (w, h, len(stream)), stream, w, h)
+        pages.append({"format": "JBIG2", "w": w, "h": h, "c": 1, "bpc": 1, "data": sha(stream),
+                      "pixels": px_sha(np.where(bm == 1, 0, 255).astype(np.uint8)), "pixfmt": "GRAY8",
+                      "box": [w, h, 0]})
+    d.add(2, b"<< /Type /Pages /Kids [%s] /Count %d >>" % (b" ".join(kids), len(kids)))
+    record("jbig2_generic.pdf", d.serialise(), pages)
 
     with open(os.path.join(OUT, "expected.json"), "w") as f:
         json.dump(expected, f, indent=1, sort_keys=True)

@@ -185,8 +185,76 @@ def test_reference_samples():
         assert d3.page_count == n
         im = d3.extract_page_image(n - 1)
         assert im.format_name == "JBIG2" and im.bits_per_component == 1 and im.components == 1
-        with pytest.raises(Exception, match="JBIG2"):
-            d3.read_page(0)
+
+
+# sha256 of the GRAY8 expansion of the reference's JBIG2 samples (csrc/jbig2.cpp;
+# the generic-region pages decode to clean documents -- a wrong context
+# template turns arithmetic decoding into noise at once -- and equal the
+# per-pixel form below; the text-region page is a symbol instance)
+JBIG2_PAGES = {
+    ("benchmark_jbig2_50page.pdf", 0): "017b9cf4bf2a5a38c7dc9806f8c15b017fd65a2d200bab4cb99a834aa332feee",
+    ("benchmark_jbig2_50page.pdf", 49): "e6de7561b233e4bd7fdc31191d76aeda100975c16bc071642cd53512b9eea2e4",
+    ("test_jbig2.pdf", 0): "442cc982f9820c5e8042008121425760dd6fa85739a10f737b1f2928db28ef6b",
+}
+
+
+def test_jbig2_reference_samples():
+    """jbig2_decode_test.c: test_jbig2.pdf's page is 200x100 with both black
+    and white pixels (here: a black 81x61 symbol at (20, 20)); the 50-page
+    benchmark (jbig2 -p generic regions, template 0) decodes page by page;
+    1 = black expands to GRAY8 0 (lib/jbig2_decode.c:136-170)."""
+    pdf = _pdf()
+    for (name, page), digest in JBIG2_PAGES.items():
+        d = pdf.PdfDocument.open(os.path.join(FIX, name))
+        assert d.page_probe(page, 0) == (d.extract_page_image(page).width, d.extract_page_image(page).height,
+                                         A.FMT_GRAY8)
+        img = d.read_page(page)
+        a = rows(img)
+        assert set(np.unique(a)) <= {0, 255} and (a == 0).any() and (a == 255).any()
+        assert sha(a) == digest, (name, page)
+    d = pdf.PdfDocument.open(os.path.join(FIX, "test_jbig2.pdf"))
+    a = rows(d.read_page(0))
+    ys, xs = np.nonzero(a == 0)
+    assert (ys.min(), ys.max(), xs.min(), xs.max()) == (20, 80, 20, 100)
+    # the benchmark at the reference's PDF dpi (300) passes the page-size check
+    d = pdf.PdfDocument.open(os.path.join(FIX, "benchmark_jbig2_50page.pdf"))
+    assert d.page_probe(3, 300) == (2480, 3508, A.FMT_GRAY8)
+
+
+def test_jbig2_fast_path_equals_per_pixel():
+    """Template 0 with the nominal AT pixels runs on sliding context windows;
+    UPH_JBIG2_GENERIC=1 forces the per-pixel context: same pages."""
+    import subprocess
+    import sys
+    code = ("import sys, hashlib, numpy as np; sys.path.insert(0, %r)\n"
+            "from unpaper_hip import pdf\n"
+            "d = pdf.PdfDocument.open(%r)\n"
+            "print(hashlib.sha256(np.ascontiguousarray(d.read_page(0).data[:, :2480]).tobytes()).hexdigest())\n"
+            % (os.path.join(ROOT, "unpaper-gpu_amd", "python"), os.path.join(FIX, "benchmark_jbig2_50page.pdf")))
+    env = dict(os.environ, UPH_JBIG2_GENERIC="1")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == JBIG2_PAGES[("benchmark_jbig2_50page.pdf", 0)]
+
+
+def test_jbig2_refusals():
+    """Segments outside the decoder's scope fail with their name."""
+    pdf = _pdf()
+    data = open(os.path.join(FIX, "jbig2_generic.pdf"), "rb").read()
+    d = pdf.PdfDocument.open_memory(data)
+    im = d.extract_page_image(0)
+    stream = im.data
+    # MMR bit on the generic region flags (segment 1's data byte 17)
+    seg1 = 11 + 19
+    mmr = bytearray(stream)
+    mmr[seg1 + 11 + 17] |= 1
+    # a halftone region segment type
+    half = bytearray(stream)
+    half[seg1 + 4] = 22
+    for bad, what in ((mmr, "MMR"), (half, "halftone")):
+        fixed = data.replace(stream, bytes(bad))
+        with pytest.raises(Exception, match=what):
+            pdf.PdfDocument.open_memory(fixed).read_page(0)
 
 
 @pytest.mark.parametrize("name", ["test_jpeg.pdf", "test_2page.pdf", "pil_multipage.pdf", "filters.pdf",

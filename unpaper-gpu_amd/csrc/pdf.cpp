@@ -16,6 +16,7 @@
 #include <unistd.h>
 
 #include "j2k.h"
+#include "jbig2.h"
 #include "jpeg.h"
 #include "runtime.h"
 
@@ -1328,6 +1329,7 @@ bool Document::metadata(Meta* out) {
 // ---------------------------------------------------------------------------
 
 int pixel_format(const PageImage& im) {
+  if (im.format == kJbig2) return UPHIP_FMT_GRAY8;  // expanded as jbig2_expand_to_gray8
   if (im.indexed) return -1;
   if (im.components == 1 && im.bpc == 8) return UPHIP_FMT_GRAY8;
   if (im.components == 3 && im.bpc == 8) return UPHIP_FMT_RGB24;
@@ -1341,6 +1343,22 @@ bool decode_pixels(const PageImage& im, uint8_t* dst, int64_t linesize, const ch
   if (fmt < 0)
     return fail("pdf: %s: page image has %d components at %d bits%s: not a pixel format here", name,
                 im.components, im.bpc, im.indexed ? " (indexed)" : "");
+  if (im.format == kJbig2) {
+    // lib/jbig2_decode.c:136-170: 1 (black) -> 0, 0 -> 255
+    if (linesize < im.width) return fail("pdf: %s: linesize too small", name);
+    jbig2::Page pg;
+    if (!jbig2::decode(im.data.data(), im.data.size(), im.globals.data(), im.globals.size(), &pg, name))
+      return false;
+    if (pg.width != im.width || pg.height != im.height)
+      return fail("pdf: %s: the JBIG2 page is %dx%d, its dictionary says %dx%d", name, pg.width, pg.height,
+                  im.width, im.height);
+    for (int32_t y = 0; y < pg.height; y++) {
+      const uint8_t* s = pg.bits.data() + (int64_t)y * pg.stride;
+      uint8_t* d = dst + (int64_t)y * linesize;
+      for (int32_t x = 0; x < pg.width; x++) d[x] = (s[x >> 3] >> (7 - (x & 7)) & 1) ? 0 : 255;
+    }
+    return true;
+  }
   const int64_t rb = ((int64_t)im.width * im.components * im.bpc + 7) / 8;
   if (linesize < rb) return fail("pdf: %s: linesize too small", name);
   std::vector<uint8_t> inflated;
@@ -1651,6 +1669,10 @@ bool page_geometry(Document& doc, int page, int32_t dpi, PageImage* im, UphipPnm
     if (!jpeg_probe_mem(im->data.data(), im->data.size(), name, &g)) return false;
   } else if (im->format == kJp2) {
     if (!j2k::probe(im->data.data(), im->data.size(), name, &g)) return false;
+  } else if (im->format == kJbig2) {
+    int32_t w = 0, h = 0;
+    if (!jbig2::probe(im->data.data(), im->data.size(), &w, &h, name)) return false;
+    g = UphipPnmInfo{w, h ? h : im->height, UPHIP_FMT_GRAY8};
   } else if (im->format == kFlate || im->format == kPng || im->format == kRaw) {
     const int fmt = pixel_format(*im);
     if (fmt < 0)
@@ -1659,7 +1681,7 @@ bool page_geometry(Document& doc, int page, int32_t dpi, PageImage* im, UphipPnm
     g = UphipPnmInfo{im->width, im->height, fmt};
   } else {
     return fail("pdf: %s: page %d: %s images are not supported (no decoder here)", doc.name().c_str(), page,
-                im->format == kJbig2 ? "JBIG2" : im->format == kCcitt ? "CCITT fax" : "unknown");
+                im->format == kCcitt ? "CCITT fax" : "unknown");
   }
   if (g.width != im->width || g.height != im->height)
     return fail("pdf: %s: page %d: the image stream is %dx%d, its dictionary says %dx%d", doc.name().c_str(),
