@@ -38,6 +38,7 @@ against tests/golden/c4_hashes.json (N=1 only; `--config c4` prints it alone).
 import argparse
 import ctypes as C
 import hashlib
+import io
 import json
 import os
 import shutil
@@ -89,7 +90,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c3", choices=("c3", "c4", "jpeg", "jp2"),
+    ap.add_argument("--config", default="c3", choices=("c3", "c4", "jpeg", "jp2", "pdf"),
                     help="c3: BASELINE configs[2] (the metric); c4: configs[3], RGB24 600dpi "
                          "double-page sheets, layout double, bilinear, border wipe; jpeg: the "
                          "JPEG decode peer (SURVEY f3) feeding the runner from JPEG files")
@@ -552,6 +553,108 @@ def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid, codec="jpeg"):
             "verified": checked, "library": version, "valid": valid}
 
 
+def run_pdf(args, L, d, devices, firsts, n_gpus, version, valid):
+    """The PDF pipeline (pdf/pdf_pipeline_cpu_batch.c; SURVEY §8 f rank 4):
+    PDF in -> pages decoded (JBIG2 on the load pool, JPEG on the device) ->
+    the default pipeline -> every sheet JPEG-encoded on the device into one
+    PDF (--pdf-quality fast, 300 dpi).  Two legs:
+      * the reference's own benchmark file (tools/bench_jbig2_pdf.py):
+        tests/golden/pdf/benchmark_jbig2_50page.pdf, 50 A4 pages of JBIG2
+        generic regions;
+      * a PDF of 512 A4 JPEG pages (quality 95) written by our writer.
+    File-to-file, host-inclusive: figures of their own, never `value` of the
+    C3 line.  Two pages of each leg are checked against the oracle run on
+    the decoded page (our JBIG2 decode / PIL's JPEG decode)."""
+    from PIL import Image
+    from concurrent.futures import ThreadPoolExecutor
+    from unpaper_hip import pdf as P
+    from unpaper_hip.pipeline import sink_pdf, source_pdf, source_page_count
+    threads = host_threads_share()
+    tmpdir = tempfile.mkdtemp(prefix="uphip_pdf_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    legs = {}
+    try:
+        jb = os.path.join(ROOT, "tests", "golden", "pdf", "benchmark_jbig2_50page.pdf")
+        jpg_pdf = os.path.join(tmpdir, "jpeg512.pdf")
+        n_jpeg = args.pages or 512
+
+        def make(i):
+            g = np.empty((H, W), np.uint8)
+            L.uphip_synth_page_host(g.ctypes.data, W, W, H, firsts[0] + i)
+            b = io.BytesIO()
+            Image.fromarray(g).save(b, "JPEG", quality=95)
+            return b.getvalue()
+        with ThreadPoolExecutor(min(16, threads)) as ex:
+            uniq = list(ex.map(make, range(16)))
+        w = P.PdfWriter.create(jpg_pdf, {"title": "bench"}, 300)
+        for i in range(n_jpeg):
+            w.add_page_jpeg(uniq[i % 16], W, H)
+        w.close()
+        opts = A.Options()
+        L.uphip_options_init(C.byref(opts))
+        r = Runner(opts, 32, W, H, A.FMT_GRAY8, devices=devices[:1], streams=8, host_threads=threads)
+        try:
+            for name, path in (("jbig2_50", jb), ("jpeg_%d" % n_jpeg, jpg_pdf)):
+                src = source_pdf(path, 300)
+                n = source_page_count(src)
+                meta = P.PdfDocument.open(path).metadata()
+                out = os.path.join(tmpdir, "out_%s.pdf" % name)
+                best = None
+                for rep in range(3):  # the first pass warms the pinned buffers
+                    k = sink_pdf(out, meta, 300, 0, 0)
+                    t0 = time.perf_counter()
+                    failed, err = r.run_host(n, src, k)
+                    k.finish()
+                    t = time.perf_counter() - t0
+                    k.close()
+                    if failed:
+                        raise UnpaperHipError("pdf %s: %d failed: %s" % (name, failed, err))
+                    if rep:
+                        best = t if best is None else min(best, t)
+                st = r.stats()
+                d_out = P.PdfDocument.open(out)
+                if d_out.page_count != n:
+                    raise SystemExit("bench.py: pdf %s wrote %d pages of %d" % (name, d_out.page_count, n))
+                checked = 0
+                if not args.no_verify:
+                    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+                    from oracle_py import Oracle
+                    from unpaper_hip.hostimage import HostImage
+                    from unpaper_hip.pipeline import pnm_read
+                    oracle = Oracle()
+                    oo = oracle.default_options()
+                    d_in = P.PdfDocument.open(path)
+                    pnm = os.path.join(tmpdir, "v%02d.pgm")
+                    failed, err = r.run_host(2, src, sink_pnm(pnm))
+                    if failed:
+                        raise UnpaperHipError("pdf %s check run: %s" % (name, err))
+                    for i in range(2):
+                        im = d_in.extract_page_image(i)
+                        if im.format == P.IMAGE_JPEG:
+                            px = np.asarray(Image.open(io.BytesIO(im.data)))
+                        else:  # the host JBIG2 decode (the reference's jbig2dec step)
+                            px = d_in.read_page(i).data[:, :W].copy()
+                        sheet, fmt, _ = oracle.process_sheet(oo, [HostImage.from_array(px, A.FMT_GRAY8)])
+                        exp = oracle.convert_for_save(sheet, fmt)
+                        if not np.array_equal(pnm_read(pnm % i).payload(), exp.payload()):
+                            raise SystemExit("bench.py: pdf %s page %d differs from the oracle" % (name, i))
+                        checked += 1
+                legs[name] = {"pages": n, "pages_per_s": round(n / best, 2), "s": round(best, 3),
+                              "load_s": round(st.load_s, 3), "store_s": round(st.store_s, 3),
+                              "in_mb": round(os.path.getsize(path) / 1e6, 3),
+                              "out_mb": round(os.path.getsize(out) / 1e6, 3), "verified": checked}
+        finally:
+            r.close()
+    finally:
+        shutil.rmtree(tmpdir, ignore_errors=True)
+    return {"metric": "pages/s, A4 GRAY8 PDF -> PDF (JBIG2 or JPEG pages in, JPEG pages out)",
+            "value": legs["jbig2_50"]["pages_per_s"], "unit": "pages/s", "n_gpus": 1,
+            "higher_is_better": True, "dtype": "u8",
+            "data": "the reference's benchmark_jbig2_50page.pdf; synthetic JPEG pages (PIL quality 95)",
+            "host_threads": threads, "legs": legs,
+            "config": {"sheets_per_batch": 32, "streams": 8, "dpi": 300, "pdf_quality": "fast (JPEG 85)"},
+            "library": version, "valid": valid}
+
+
 def run_c4(args, L, d, devices, firsts, n_gpus, version, valid, nsheets=0, steps=0, warmup=-1,
            batch=0):
     """BASELINE configs[3]: RGB24 600dpi double-page sheets, layout double,
@@ -684,6 +787,10 @@ def main():
         line = run_c4(args, L, d, devices, firsts, n_gpus, version, valid)
         if d.rank == 0:
             print(json.dumps(line), flush=True)
+        return
+    if args.config == "pdf":
+        line = run_pdf(args, L, d, devices, firsts, n_gpus, version, valid)
+        print(json.dumps(line))
         return
     if args.config in ("jpeg", "jp2"):
         line = run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid, args.config)
