@@ -358,7 +358,7 @@ struct Decoder {
   // a striped page of unknown height grows as regions land
   bool ensure_rows(int64_t rows) {
     if (!striped || rows <= page.h) return true;
-    if ((int64_t)page.w * rows > kMaxPixels) return fail("jbig2: %s: page too large", name);
+    if (rows > (1 << 20) || (int64_t)page.w * rows > kMaxPixels) return fail("jbig2: %s: page too large", name);
     const int64_t old_h = page.h;
     page.h = (int32_t)rows;
     page.px.resize((size_t)(page.pitch() * (rows + Bitmap::kTop)), 0);
@@ -372,6 +372,11 @@ struct Decoder {
     const uint32_t W = be32(s.data), H = be32(s.data + 4);
     if (W > (1u << 24) || H > (1u << 24) || (int64_t)W * H > kMaxPixels)
       return fail("jbig2: %s: region %ux%u", name, W, H);
+    // a region no larger than its page (a crafted header must not size a
+    // bitmap, or a decode loop, beyond what the page can show)
+    if (!have_page) return fail("jbig2: %s: region before the page information", name);
+    if ((int64_t)W > page.w || (!striped && (int64_t)H > page.h) || H > (1u << 20))
+      return fail("jbig2: %s: region %ux%u larger than the page %dx%d", name, W, H, page.w, page.h);
     *w = (int32_t)W;
     *h = (int32_t)H;
     *x = (int32_t)be32(s.data + 8);
@@ -459,8 +464,9 @@ struct Decoder {
     std::vector<uint8_t> gb(gb_contexts(gp.tmpl), 0);
     std::vector<Bitmap> fresh;
     fresh.reserve(nnew);
-    int64_t hc = 0;
-    while (fresh.size() < nnew) {
+    int64_t hc = 0, area = 0;
+    for (uint32_t classes = 0; fresh.size() < nnew; classes++) {
+      if (classes > nnew + 16) return fail("jbig2: %s: empty height classes", name);
       int32_t dh;
       if (!iadh.decode(mq, &dh)) return fail("jbig2: %s: symbol height OOB", name);
       hc += dh;
@@ -471,7 +477,10 @@ struct Decoder {
         if (!iadw.decode(mq, &dw)) break;  // end of the height class
         if (fresh.size() >= nnew) return fail("jbig2: %s: more symbols than declared", name);
         sw += dw;
-        if (sw < 0 || sw > (1 << 24) || sw * hc > kMaxPixels) return fail("jbig2: %s: symbol width %lld", name, (long long)sw);
+        if (sw < 0 || sw > (1 << 24) || sw * hc > (1 << 24))
+          return fail("jbig2: %s: symbol %lldx%lld", name, (long long)sw, (long long)hc);
+        area += sw * hc;
+        if (area > (1 << 28)) return fail("jbig2: %s: symbol dictionary too large", name);
         Bitmap b;
         b.alloc((int32_t)sw, (int32_t)hc, 0);
         if (sw > 0 && !generic_decode(mq, gp, gb.data(), &b)) return false;
@@ -514,6 +523,7 @@ struct Decoder {
     if (s.len < i + 4) return fail("jbig2: %s: short text region", name);
     const uint32_t ninst = be32(s.data + i);
     i += 4;
+    if (ninst > (1u << 22)) return fail("jbig2: %s: %u symbol instances", name, ninst);
     std::vector<const Bitmap*> syms;
     for (uint32_t r : s.refs)
       if (const Dict* d = dict(r))

@@ -1207,7 +1207,8 @@ bool Document::extract_image(int page, PageImage* out) {
   out->object = (int32_t)best_num;
   const Obj* w = resolve(im.get("Width"));
   const Obj* h = resolve(im.get("Height"));
-  if (w->num() < 1 || h->num() < 1 || w->num() > (1 << 20) || h->num() > (1 << 20))
+  if (w->num() < 1 || h->num() < 1 || w->num() > (1 << 20) || h->num() > (1 << 20) ||
+      w->num() * h->num() > 2147483648.0)
     return fail("pdf: %s: page %d: image size %gx%g", name_.c_str(), page, w->num(), h->num());
   out->width = (int32_t)w->num();
   out->height = (int32_t)h->num();
