@@ -117,7 +117,7 @@ $(LIBM_CHECK): tests/c/libm_check.cpp $(CSRC)/libm_glibc.h
 # One compiler (ROCm clang) for every object so that one sanitizer runtime
 # serves the program; the HIP sources are compiled for the host only.
 $(SANITIZE): tests/c/sanitize_main.c oracle/oracle.c oracle/oracle.h $(CSRC)/pnm.cpp $(CSRC)/png.cpp \
-             $(CSRC)/jpeg.cpp $(CSRC)/j2k.cpp $(CSRC)/pdf.cpp $(CSRC)/jbig2.cpp tests/c/san_stubs.cpp $(CSRC)/runtime.hip $(HDRS)
+             $(CSRC)/jpeg.cpp $(CSRC)/j2k.cpp $(CSRC)/pdf.cpp $(CSRC)/jbig2.cpp $(CSRC)/ccitt.cpp tests/c/san_stubs.cpp $(CSRC)/runtime.hip $(HDRS)
 	@mkdir -p tests/c/_build/san
 	$(LLVMCC) $(SANFLAGS) -std=gnu11 -ffp-contract=off -c oracle/oracle.c -o tests/c/_build/san/oracle.o
 	$(LLVMCC) $(SANFLAGS) -std=gnu11 -Iinclude -c tests/c/sanitize_main.c -o tests/c/_build/san/main.o
@@ -133,6 +133,8 @@ $(SANITIZE): tests/c/sanitize_main.c oracle/oracle.c oracle/oracle.h $(CSRC)/pnm
 	  -Iinclude -I$(CSRC) -c $(CSRC)/pdf.cpp -o tests/c/_build/san/pdf.o
 	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
 	  -Iinclude -I$(CSRC) -c $(CSRC)/jbig2.cpp -o tests/c/_build/san/jbig2.o
+	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
+	  -Iinclude -I$(CSRC) -c $(CSRC)/ccitt.cpp -o tests/c/_build/san/ccitt.o
 	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \
 	  -Iinclude -I$(CSRC) -c tests/c/san_stubs.cpp -o tests/c/_build/san/san_stubs.o
 	$(HIPCC) --cuda-host-only -x hip $(SANFLAGS) -std=c++17 -Wno-unused-result -Wno-unused-value \

@@ -583,9 +583,10 @@ int uphip_image_read(const char *path, void *dst, int64_t linesize,
  * pdf/pdf_writer.h without MuPDF: a reader of scanned documents (one image
  * per page: classic and stream cross-reference sections, object streams,
  * incremental updates, a file scan when the xref is damaged) and an
- * image-per-page writer.  Not provided: rendering of vector / text pages
- * (pdf_render_page*), decryption (pdf_doc_authenticate), JBIG2 / CCITT
- * decoding -- pages that need them fail with an error naming the cause.
+ * image-per-page writer; JBIG2 and CCITT fax pages decode on the host.  Not
+ * provided: rendering of vector / text pages (pdf_render_page*) and
+ * decryption (pdf_doc_authenticate) -- pages that need them fail with an
+ * error naming the cause.
  * Functions returning int give 0 on success, -1 on error (uphip_last_error).
  * ------------------------------------------------------------------------- */
 typedef struct UphipPdfDocument UphipPdfDocument;
@@ -640,8 +641,9 @@ void uphip_pdf_free_metadata(UphipPdfMetadata *meta);
 const char *uphip_pdf_image_format_name(int32_t format);
 int uphip_pdf_is_pdf_file(const char *filename);  /* by extension, pdf_reader.c:60-70 */
 /* A page's pixels (pdf_pipeline_decode.c:278-320 without the render
- * fallback): JPEG / JPEG 2000 images decode on the current device, Flate and
- * raw 8-bit gray / RGB and 1-bit images on the host.  dpi > 0 applies the
+ * fallback): JPEG / JPEG 2000 images decode on the current device; Flate and
+ * raw 8-bit gray / RGB and 1-bit images, JBIG2 and CCITT fax images (both
+ * expanded to GRAY8, black 0) on the host.  dpi > 0 applies the
  * reference's size check (the image within 4 px of the page at `dpi`,
  * pdf_pipeline_decode.c:69-111; a mismatch would need rendering and fails);
  * dpi 0 takes the image as it is.  read: `expect` as uphip_image_read. */

@@ -245,7 +245,7 @@ static void pdf_case(const UphipPdfDocument *unused, const uint8_t *p, size_t n)
         UphipPdfImage im2;
         if (uphip_pdf_extract_page_image(d, i, &im2) == 0) {
           if (im2.format == UPHIP_PDF_IMAGE_FLATE || im2.format == UPHIP_PDF_IMAGE_RAW ||
-              im2.format == UPHIP_PDF_IMAGE_JBIG2)
+              im2.format == UPHIP_PDF_IMAGE_JBIG2 || im2.format == UPHIP_PDF_IMAGE_CCITT)
             uphip_pdf_read_page(d, i, 0, px, ls, &g);
           uphip_pdf_free_image(&im2);
         }
@@ -262,7 +262,7 @@ static void pdf_case(const UphipPdfDocument *unused, const uint8_t *p, size_t n)
 static void pdf(const char *dir, const char *fixtures) {
   static const char *good[] = {"xrefstream_objstm.pdf", "incremental.pdf", "damaged_xref.pdf", "filters.pdf",
                                "pil_multipage.pdf",     "jpx.pdf",         "encrypted.pdf",    "test_jbig2.pdf",
-                               "jbig2_generic.pdf"};
+                               "jbig2_generic.pdf",     "ccitt_pil.pdf",   "ccitt_g3.pdf"};
   static uint8_t raw[1 << 16], tmp[1 << 16];
   char path[512];
   unsigned seed = 777;

@@ -503,6 +503,55 @@ def main():
     d.add(2, b"<< /Type /Pages /Kids [%s] /Count %d >>" % (b" ".join(kids), len(kids)))
     record("jbig2_generic.pdf", d.serialise(), pages)
 
+    # 9. CCITT fax pages: PIL's own bilevel PDF (Group 4, /BlackIs1 true), and
+    #    libtiff's Group 3 strips (1-D, 2-D, with EOL fill bits) wrapped with
+    #    the matching /DecodeParms; one page with /BlackIs1 false and
+    #    /Decode [1 0] (the two inversions cancel).  Expected pixels: PIL's
+    #    image, white 255 / black 0.
+    from PIL import ImageDraw
+
+    def bilevel(w, h, seed):
+        r = np.random.default_rng(seed)
+        im = Image.new("1", (w, h), 1)
+        dr = ImageDraw.Draw(im)
+        for _ in range(30):
+            x0, y0 = int(r.integers(0, w)), int(r.integers(0, h))
+            dr.rectangle([x0, y0, x0 + int(r.integers(0, w // 3 + 1)), y0 + int(r.integers(0, 6))], fill=0)
+        for _ in range(12):
+            dr.text((int(r.integers(0, w)), int(r.integers(0, h))), "Scan 42", fill=0)
+        return im
+
+    def gray_of(im):
+        return np.where(np.asarray(im), 255, 0).astype(np.uint8)
+    ims = [bilevel(201, 90, 1), bilevel(2600, 40, 2)]  # the second needs the extended make-up codes
+    b = io.BytesIO()
+    ims[0].save(b, "PDF", save_all=True, append_images=ims[1:])
+    record("ccitt_pil.pdf", b.getvalue(), [
+        {"format": "CCITT", "w": im.width, "h": im.height, "c": 1, "bpc": 1, "pixels": px_sha(gray_of(im)),
+         "pixfmt": "GRAY8", "box": [im.width, im.height, 0]} for im in ims])
+    d = Doc()
+    d.add(1, b"<< /Type /Catalog /Pages 2 0 R >>")
+    kids, pages = [], []
+    for k, (opts, black1) in enumerate([(0, True), (1, True), (4, True), (5, True), (1, False)]):
+        im = bilevel(300, 60 + k, 10 + k)
+        t = io.BytesIO()
+        im.save(t, "TIFF", compression="group3", tiffinfo={278: im.height, 292: opts})
+        tg = Image.open(io.BytesIO(t.getvalue())).tag_v2
+        strip = t.getvalue()[tg[273][0]:tg[273][0] + tg[279][0]]
+        parms = b"<< /K %d /Columns %d /Rows %d /BlackIs1 %s%s >>" % (
+            opts & 1, im.width, im.height, b"true" if black1 else b"false",
+            b" /EncodedByteAlign true /EndOfLine true" if opts & 4 else b"")
+        first = 3 + 3 * k
+        kids.append(b"%d 0 R" % (first + 2))
+        page_objs(d, first, b"<< /Type /XObject /Subtype /Image /Width %d /Height %d /ColorSpace /DeviceGray "
+                  b"/BitsPerComponent 1 /Filter /CCITTFaxDecode /DecodeParms %s%s /Length %d >>"
+                  % (im.width, im.height, parms, b"" if black1 else b" /Decode [1 0]", len(strip)),
+                  strip, im.width, im.height)
+        pages.append({"format": "CCITT", "w": im.width, "h": im.height, "c": 1, "bpc": 1, "data": sha(strip),
+                      "pixels": px_sha(gray_of(im)), "pixfmt": "GRAY8", "box": [im.width, im.height, 0]})
+    d.add(2, b"<< /Type /Pages /Kids [%s] /Count %d >>" % (b" ".join(kids), len(kids)))
+    record("ccitt_g3.pdf", d.serialise(), pages)
+
     with open(os.path.join(OUT, "expected.json"), "w") as f:
         json.dump(expected, f, indent=1, sort_keys=True)
 

@@ -258,7 +258,7 @@ def test_jbig2_refusals():
 
 
 @pytest.mark.parametrize("name", ["test_jpeg.pdf", "test_2page.pdf", "pil_multipage.pdf", "filters.pdf",
-                                  "incremental.pdf", "jpx.pdf", "test_jbig2.pdf"])
+                                  "incremental.pdf", "jpx.pdf", "test_jbig2.pdf", "ccitt_pil.pdf"])
 def test_reader_matches_independent_parse(name):
     """The largest image of every page equals what PIL's parser finds: the
     raw bytes of DCT / JPX / JBIG2 / Flate streams; Flate pixels equal
@@ -275,7 +275,7 @@ def test_reader_matches_independent_parse(name):
         im = d.extract_page_image(i)
         assert (im.width, im.height) == (w, h)
         last = flt[-1] if flt else None
-        if last in (b"DCTDecode", b"JPXDecode", b"JBIG2Decode", b"FlateDecode") and len(flt) == 1:
+        if last in (b"DCTDecode", b"JPXDecode", b"JBIG2Decode", b"FlateDecode", b"CCITTFaxDecode") and len(flt) == 1:
             assert im.data == raw, (name, i)
         if last == b"FlateDecode" and len(flt) == 1 and im.bits_per_component == 8:
             px = np.frombuffer(zlib.decompress(raw), np.uint8)

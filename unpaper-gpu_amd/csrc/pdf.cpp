@@ -15,6 +15,7 @@
 
 #include <unistd.h>
 
+#include "ccitt.h"
 #include "j2k.h"
 #include "jbig2.h"
 #include "jpeg.h"
@@ -1274,6 +1275,16 @@ bool Document::extract_image(int page, PageImage* out) {
   } else if (last == "CCITTFaxDecode") {
     out->format = kCcitt;
     keep_from--;
+    const Obj* pm = fs.back().parms;
+    out->fax.k = parm_int(this, pm, "K", 0);
+    out->fax.columns = parm_int(this, pm, "Columns", 1728);
+    auto flag = [&](const char* key, bool dflt) {
+      const Obj* v = pm ? resolve(pm->get(key)) : nullptr;
+      return v && v->t == T::Bool ? v->i != 0 : dflt;
+    };
+    out->fax.byte_align = flag("EncodedByteAlign", false);
+    out->fax.eol = flag("EndOfLine", false);
+    out->fax.black_is_1 = flag("BlackIs1", false);
   } else if (last == "FlateDecode") {
     out->format = kFlate;
     keep_from--;
@@ -1330,7 +1341,7 @@ bool Document::metadata(Meta* out) {
 // ---------------------------------------------------------------------------
 
 int pixel_format(const PageImage& im) {
-  if (im.format == kJbig2) return UPHIP_FMT_GRAY8;  // expanded as jbig2_expand_to_gray8
+  if (im.format == kJbig2 || im.format == kCcitt) return UPHIP_FMT_GRAY8;  // expanded to 0 / 255
   if (im.indexed) return -1;
   if (im.components == 1 && im.bpc == 8) return UPHIP_FMT_GRAY8;
   if (im.components == 3 && im.bpc == 8) return UPHIP_FMT_RGB24;
@@ -1344,6 +1355,24 @@ bool decode_pixels(const PageImage& im, uint8_t* dst, int64_t linesize, const ch
   if (fmt < 0)
     return fail("pdf: %s: page image has %d components at %d bits%s: not a pixel format here", name,
                 im.components, im.bpc, im.indexed ? " (indexed)" : "");
+  if (im.format == kCcitt) {
+    if (linesize < im.width) return fail("pdf: %s: linesize too small", name);
+    ccitt::Image cm;
+    ccitt::Params prm = im.fax;
+    if (prm.columns != im.width)
+      return fail("pdf: %s: CCITT /Columns %d but the image is %d wide", name, prm.columns, im.width);
+    if (!ccitt::decode(im.data.data(), im.data.size(), prm, im.height, &cm, name)) return false;
+    // a black run is the sample 1 when /BlackIs1, else 0; DeviceGray 0 is
+    // black, and /Decode [1 0] swaps the two
+    const uint8_t on_black = (uint8_t)((prm.black_is_1 ^ im.inverted) ? 255 : 0);
+    for (int32_t y = 0; y < cm.height; y++) {
+      const uint8_t* s = cm.bits.data() + (int64_t)y * cm.stride;
+      uint8_t* d = dst + (int64_t)y * linesize;
+      for (int32_t x = 0; x < cm.width; x++)
+        d[x] = (s[x >> 3] >> (7 - (x & 7)) & 1) ? on_black : (uint8_t)(255 - on_black);
+    }
+    return true;
+  }
   if (im.format == kJbig2) {
     // lib/jbig2_decode.c:136-170: 1 (black) -> 0, 0 -> 255
     if (linesize < im.width) return fail("pdf: %s: linesize too small", name);
@@ -1670,6 +1699,8 @@ bool page_geometry(Document& doc, int page, int32_t dpi, PageImage* im, UphipPnm
     if (!jpeg_probe_mem(im->data.data(), im->data.size(), name, &g)) return false;
   } else if (im->format == kJp2) {
     if (!j2k::probe(im->data.data(), im->data.size(), name, &g)) return false;
+  } else if (im->format == kCcitt) {
+    g = UphipPnmInfo{im->width, im->height, UPHIP_FMT_GRAY8};
   } else if (im->format == kJbig2) {
     int32_t w = 0, h = 0;
     if (!jbig2::probe(im->data.data(), im->data.size(), &w, &h, name)) return false;
@@ -1681,8 +1712,7 @@ bool page_geometry(Document& doc, int page, int32_t dpi, PageImage* im, UphipPnm
                   page, im->components, im->bpc, im->indexed ? ", indexed colours" : "");
     g = UphipPnmInfo{im->width, im->height, fmt};
   } else {
-    return fail("pdf: %s: page %d: %s images are not supported (no decoder here)", doc.name().c_str(), page,
-                im->format == kCcitt ? "CCITT fax" : "unknown");
+    return fail("pdf: %s: page %d: images of unknown format are not supported", doc.name().c_str(), page);
   }
   if (g.width != im->width || g.height != im->height)
     return fail("pdf: %s: page %d: the image stream is %dx%d, its dictionary says %dx%d", doc.name().c_str(),

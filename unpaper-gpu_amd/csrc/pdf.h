@@ -13,8 +13,9 @@
 // (pdf_writer.c:357-433), streaming each page to disk as it arrives.
 //
 // Not here: rendering of vector / text pages (pdf_reader.c:443-775, MuPDF's
-// rasteriser), decryption (pdf_doc_authenticate), JBIG2 and CCITT image
-// decoding.  Pages that need them fail loudly.
+// rasteriser) and decryption (pdf_doc_authenticate).  Pages that need them
+// fail loudly.  JBIG2 and CCITT fax pages decode on the host (jbig2.h,
+// ccitt.h).
 #pragma once
 
 #include <cstdint>
@@ -25,6 +26,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "ccitt.h"
 #include "unpaper_hip.h"
 
 namespace uph {
@@ -69,6 +71,7 @@ struct PageImage {
   bool inverted = false;  // /Decode [1 0] on a one-component image
   bool indexed = false;   // /Indexed colour space (not supported by the pixel path)
   int32_t predictor = 1, colors = 1, pbpc = 8, columns = 1;  // Flate /DecodeParms
+  ccitt::Params fax;                                          // CCITTFaxDecode /DecodeParms
   int32_t object = 0;  // its object number (diagnostics)
 };
 
