@@ -607,3 +607,31 @@ def test_runner_pdf_source_and_sinks(hip, oracle, tmp_path):
     d = pdf.PdfDocument.open(outs[1])
     for i in range(5):
         assert (rows(d.read_page(i)) == pnm_read(str(tmp_path / ("o%02d.pgm" % i))).payload()).all()
+
+
+@pytest.mark.gpu
+def test_runner_host_decoded_pdf_pages(hip, oracle, tmp_path):
+    """JBIG2 and CCITT pages (decoded on the runner's load pool by the PDF
+    source) through the pipeline equal the oracle on the same decoded pages:
+    jobs 0..page of the document (pages of one geometry), sheets to PGM."""
+    from unpaper_hip.hostimage import HostImage
+    from unpaper_hip.pipeline import Runner, sink_pnm, source_pdf, pnm_read
+    pdf = _pdf()
+    opts = oracle.default_options()
+    for name, page in (("jbig2_generic.pdf", 0), ("ccitt_g3.pdf", 0), ("ccitt_pil.pdf", 0),
+                       ("test_jbig2.pdf", 0), ("benchmark_jbig2_50page.pdf", 3)):
+        path = os.path.join(FIX, name)
+        d = pdf.PdfDocument.open(path)
+        w, h, fmt = d.page_probe(page, 0)
+        assert fmt == A.FMT_GRAY8 and all(d.page_probe(i, 0) == (w, h, fmt) for i in range(page + 1))
+        px = rows(d.read_page(page))
+        sheet, ofmt, _ = oracle.process_sheet(opts, [HostImage.from_array(px, A.FMT_GRAY8)])
+        exp = oracle.convert_for_save(sheet, ofmt)
+        out = str(tmp_path / ("o_%s_%%02d.pgm" % name.replace(".", "_")))
+        r = Runner(opts, 2, w, h, A.FMT_GRAY8, devices=(0,), streams=2, host_threads=2)
+        try:
+            failed, err = r.run_host(page + 1, source_pdf(path, 0), sink_pnm(out))
+        finally:
+            r.close()
+        assert failed == 0, err
+        assert (pnm_read(out % page).payload() == exp.payload()).all(), (name, page)
