@@ -13,7 +13,11 @@
 #include <cstring>
 #include <set>
 
+#include <fcntl.h>
+#include <sys/uio.h>
 #include <unistd.h>
+
+#include <thread>
 
 #include "ccitt.h"
 #include "j2k.h"
@@ -1172,8 +1176,13 @@ bool Document::page_box(int page, PageBox* out) {
 }
 
 bool Document::extract_image(int page, PageImage* out) {
-  std::lock_guard<std::recursive_mutex> lk(mu_);
-  *out = PageImage();
+  std::unique_lock<std::recursive_mutex> lk(mu_);
+  {  // reset, keeping the data buffer's capacity (load tasks reuse one per thread)
+    std::vector<uint8_t> keep = std::move(out->data);
+    keep.clear();
+    *out = PageImage();
+    out->data = std::move(keep);
+  }
   if (encrypted_) return fail("pdf: %s is encrypted (decryption is not supported)", name_.c_str());
   if (page < 0 || page >= (int)pages_.size())
     return fail("pdf: %s: page %d out of range (%d pages)", name_.c_str(), page, (int)pages_.size());
@@ -1296,12 +1305,22 @@ bool Document::extract_image(int page, PageImage* out) {
   } else {
     out->format = kRaw;  // no filter, or only ones decoded here
   }
-  const size_t raw_cap = (size_t)out->width * out->height * std::max(comps, 1) * 2 + (1 << 20);
-  if (!stream_data(im, &out->data, std::max(raw_cap, im.slen * 4 + (1 << 20)), 0, 0, keep_from))
-    return false;
   if (out->format == kJbig2 && fs.back().parms) {
     const Obj* g = resolve(fs.back().parms->get("JBIG2Globals"));
     if (g && g->t == T::Stream && !stream_data(*g, &out->globals, kStreamCap)) return false;
+  }
+  if (keep_from == 0) {
+    // the stream's bytes as stored: copied outside the document lock (the
+    // file buffer never changes), so load tasks of other pages do not queue
+    // behind a multi-MB copy
+    const size_t off = im.soff, len = im.slen;
+    lk.unlock();
+    out->data.assign(p_ + off, p_ + off + len);
+  } else {
+    const size_t raw_cap = (size_t)out->width * out->height * std::max(comps, 1) * 2 + (1 << 20);
+    if (!stream_data(im, &out->data, std::max(raw_cap, im.slen * 4 + (1 << 20)), 0, 0, keep_from))
+      return false;
+    lk.unlock();
   }
   // what the codestream says when the dictionary does not
   if (out->format == kJpeg && !comps) comps = jpeg_components(out->data.data(), out->data.size());
@@ -1477,9 +1496,35 @@ std::string pdf_text(const std::string& utf8) {
 
 Writer::~Writer() { abort(); }
 
+namespace {
+
+// all of [p, p + n) at `off`
+bool pwrite_all(int fd, const struct iovec* iov, int n, int64_t off) {
+  std::vector<struct iovec> v(iov, iov + n);
+  size_t k = 0;
+  while (k < v.size()) {
+    const ssize_t w = pwritev(fd, v.data() + k, (int)(v.size() - k), (off_t)off);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    off += w;
+    size_t left = (size_t)w;
+    while (k < v.size() && left >= v[k].iov_len) left -= v[k++].iov_len;
+    if (k < v.size()) {
+      v[k].iov_base = (uint8_t*)v[k].iov_base + left;
+      v[k].iov_len -= left;
+    }
+  }
+  return true;
+}
+
+}  // namespace
+
 bool Writer::put(const void* p, size_t n) {
-  if (failed_ || !f_) return false;
-  if (fwrite(p, 1, n, f_) != n) {
+  if (failed_ || fd_ < 0) return false;
+  struct iovec v = {const_cast<void*>(p), n};
+  if (!pwrite_all(fd_, &v, 1, pos_)) {
     failed_ = true;
     return fail("pdf_writer: cannot write %s", part_.c_str());
   }
@@ -1497,10 +1542,8 @@ bool Writer::putf(const char* fmt, ...) {
   return put(buf, (size_t)n);
 }
 
-int64_t Writer::begin_obj() {
-  offsets_.push_back(pos_);
-  const int64_t num = (int64_t)offsets_.size() - 1;
-  return putf("%lld 0 obj\n", (long long)num) ? num : -1;
+void Writer::drain() {
+  while (inflight_.load(std::memory_order_acquire) > 0) std::this_thread::yield();
 }
 
 bool Writer::create(const char* path, const Meta* meta, int dpi) {
@@ -1509,8 +1552,8 @@ bool Writer::create(const char* path, const Meta* meta, int dpi) {
   path_ = path;
   part_ = path_ + ".part";
   dpi_ = dpi > 0 ? dpi : 72;  // pdf_writer.c:91-93
-  f_ = fopen(part_.c_str(), "wb");
-  if (!f_) return fail("pdf_writer: cannot create %s: %s", part_.c_str(), strerror(errno));
+  fd_ = ::open(part_.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd_ < 0) return fail("pdf_writer: cannot create %s: %s", part_.c_str(), strerror(errno));
   if (meta) {
     meta_ = *meta;
     has_meta_ = true;
@@ -1564,32 +1607,46 @@ bool Writer::add_page(int64_t index, int kind, const uint8_t* data, size_t len, 
   const char* cs = components == 1 ? "/DeviceGray" : components == 4 ? "/DeviceCMYK" : "/DeviceRGB";
   const int eff = dpi > 0 ? dpi : dpi_;
   const double pw = (double)width * 72.0 / eff, ph = (double)height * 72.0 / eff;
+  const std::string spw = real(pw), sph = real(ph);
   char content[160];
-  const int cl = snprintf(content, sizeof(content), "q %s 0 0 %s 0 0 cm /Im0 Do Q", real(pw).c_str(),
-                          real(ph).c_str());
-  std::lock_guard<std::mutex> lk(mu_);
-  if (!f_) return fail("pdf_writer: Writer has been closed or aborted");
-  if (failed_) return false;
-  const int64_t im = begin_obj();
-  bool ok = im > 0 &&
-            putf("<< /Type /XObject /Subtype /Image /Width %d /Height %d /BitsPerComponent 8 "
-                 "/ColorSpace %s /Filter /%s /Length %zu >>\nstream\n",
-                 width, height, cs, filter, blen) &&
-            put(body, blen) && putf("\nendstream\nendobj\n");
-  const int64_t ct = ok ? begin_obj() : -1;
-  ok = ok && ct > 0 && putf("<< /Length %d >>\nstream\n", cl) && put(content, (size_t)cl) &&
-       putf("\nendstream\nendobj\n");
-  const int64_t pg = ok ? begin_obj() : -1;
-  ok = ok && pg > 0 &&
-       putf("<< /Type /Page /Parent 2 0 R /MediaBox [0 0 %s %s] /Resources << /XObject << /Im0 %lld 0 R >> >> "
-            "/Contents %lld 0 R >>\nendobj\n",
-            real(pw).c_str(), real(ph).c_str(), (long long)im, (long long)ct);
-  if (!ok) {
-    failed_ = true;
-    return false;
+  const int cl = snprintf(content, sizeof(content), "q %s 0 0 %s 0 0 cm /Im0 Do Q", spw.c_str(), sph.c_str());
+  char h1[320], t1[640];
+  int64_t off;
+  int n1, n2;
+  {
+    // reserve the page's objects and bytes
+    std::lock_guard<std::mutex> lk(mu_);
+    if (fd_ < 0) return fail("pdf_writer: Writer has been closed or aborted");
+    if (failed_) return false;
+    const int64_t im = (int64_t)offsets_.size(), ct = im + 1, pg = im + 2;
+    n1 = snprintf(h1, sizeof(h1),
+                  "%lld 0 obj\n<< /Type /XObject /Subtype /Image /Width %d /Height %d /BitsPerComponent 8 "
+                  "/ColorSpace %s /Filter /%s /Length %zu >>\nstream\n",
+                  (long long)im, width, height, cs, filter, blen);
+    const int a = snprintf(t1, sizeof(t1), "\nendstream\nendobj\n%lld 0 obj\n<< /Length %d >>\nstream\n%s\nendstream\nendobj\n",
+                           (long long)ct, cl, content);
+    const int b = snprintf(t1 + a, sizeof(t1) - (size_t)a,
+                           "%lld 0 obj\n<< /Type /Page /Parent 2 0 R /MediaBox [0 0 %s %s] /Resources << /XObject "
+                           "<< /Im0 %lld 0 R >> >> /Contents %lld 0 R >>\nendobj\n",
+                           (long long)pg, spw.c_str(), sph.c_str(), (long long)im, (long long)ct);
+    n2 = a + b;
+    off = pos_;
+    // object offsets: the image at off, the content after the image's
+    // "endstream endobj" (18 bytes), the page after the content object
+    const int64_t ct_at = off + n1 + (int64_t)blen + 18;
+    const int64_t pg_at = off + n1 + (int64_t)blen + a;
+    offsets_.push_back(off);
+    offsets_.push_back(ct_at);
+    offsets_.push_back(pg_at);
+    pos_ += n1 + (int64_t)blen + n2;
+    pages_.emplace_back(index, pg);
+    inflight_.fetch_add(1, std::memory_order_acq_rel);
   }
-  pages_.emplace_back(index, pg);
-  return true;
+  struct iovec v[3] = {{h1, (size_t)n1}, {const_cast<uint8_t*>(body), blen}, {t1, (size_t)n2}};
+  const bool ok = pwrite_all(fd_, v, 3, off);
+  if (!ok) failed_ = true;
+  inflight_.fetch_sub(1, std::memory_order_acq_rel);
+  return ok || fail("pdf_writer: cannot write %s", part_.c_str());
 }
 
 bool Writer::add_page_next(int kind, const uint8_t* data, size_t len, int width, int height, int stride,
@@ -1609,7 +1666,8 @@ int Writer::page_count() {
 
 bool Writer::close() {
   std::lock_guard<std::mutex> lk(mu_);
-  if (!f_) return fail("pdf_writer: Writer has been closed or aborted");
+  if (fd_ < 0) return fail("pdf_writer: Writer has been closed or aborted");
+  drain();
   bool ok = !failed_;
   std::stable_sort(pages_.begin(), pages_.end());
   // page tree
@@ -1636,13 +1694,24 @@ bool Writer::close() {
   }
   info += " /Producer (unpaper) >>\nendobj\n";
   ok = ok && put(info.data(), info.size());
+  // the cross-reference table in one write
   const int64_t xref = pos_;
-  ok = ok && putf("xref\n0 %zu\n0000000000 65535 f\r\n", offsets_.size());
-  for (size_t k = 1; ok && k < offsets_.size(); k++) ok = putf("%010lld 00000 n\r\n", (long long)offsets_[k]);
-  ok = ok && putf("trailer\n<< /Size %zu /Root 1 0 R /Info 3 0 R >>\nstartxref\n%lld\n%%%%EOF\n",
-                  offsets_.size(), (long long)xref);
-  ok = (fclose(f_) == 0) && ok;
-  f_ = nullptr;
+  std::string x;
+  x.reserve(offsets_.size() * 20 + 128);
+  char line[64];
+  snprintf(line, sizeof(line), "xref\n0 %zu\n0000000000 65535 f\r\n", offsets_.size());
+  x += line;
+  for (size_t k = 1; k < offsets_.size(); k++) {
+    snprintf(line, sizeof(line), "%010lld 00000 n\r\n", (long long)offsets_[k]);
+    x += line;
+  }
+  snprintf(line, sizeof(line), "trailer\n<< /Size %zu /Root 1 0 R /Info 3 0 R >>\n", offsets_.size());
+  x += line;
+  snprintf(line, sizeof(line), "startxref\n%lld\n%%%%EOF\n", (long long)xref);
+  x += line;
+  ok = ok && put(x.data(), x.size());
+  ok = (::close(fd_) == 0) && ok;
+  fd_ = -1;
   if (ok && rename(part_.c_str(), path_.c_str()) != 0) ok = fail("pdf_writer: cannot rename %s", part_.c_str());
   if (!ok) {
     unlink(part_.c_str());
@@ -1653,9 +1722,10 @@ bool Writer::close() {
 
 void Writer::abort() {
   std::lock_guard<std::mutex> lk(mu_);
-  if (!f_) return;
-  fclose(f_);
-  f_ = nullptr;
+  if (fd_ < 0) return;
+  drain();
+  ::close(fd_);
+  fd_ = -1;
   unlink(part_.c_str());
 }
 

@@ -18,6 +18,7 @@
 // ccitt.h).
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <memory>
@@ -163,10 +164,12 @@ bool decode_pixels(const PageImage& im, uint8_t* dst, int64_t linesize, const ch
 bool page_geometry(Document& doc, int page, int32_t dpi, PageImage* im, UphipPnmInfo* info);
 
 // The image-per-page writer (PdfWriter, pdf_writer.h).  Pages stream to
-// "<path>.part" as they are added, in any order; close() writes the page
-// tree in page-index order, the cross-reference table and trailer, and
-// renames the file into place; abort() (or destruction without close)
-// removes it.  Thread-safe.
+// "<path>.part" as they are added, in any order: a page reserves its byte
+// range and object numbers under the lock, then writes its objects with one
+// positioned write outside it, so store tasks write concurrently.  close()
+// waits for those writes, writes the page tree in page-index order, the
+// cross-reference table and trailer, and renames the file into place;
+// abort() (or destruction without close) removes it.  Thread-safe.
 class Writer {
  public:
   ~Writer();
@@ -182,19 +185,20 @@ class Writer {
 
  private:
   std::mutex mu_;
-  FILE* f_ = nullptr;
+  int fd_ = -1;
   std::string path_, part_;
   int dpi_ = 72;
-  int64_t pos_ = 0;
+  int64_t pos_ = 0;                                   // bytes reserved so far
   std::vector<int64_t> offsets_;                      // by object number (0 unused)
   std::vector<std::pair<int64_t, int64_t>> pages_;    // (page index, page object)
   int64_t next_index_ = 0;
-  bool failed_ = false;
+  std::atomic<int> inflight_{0};                      // page writes outside the lock
+  std::atomic<bool> failed_{false};
   Meta meta_;
   bool has_meta_ = false;
-  bool put(const void* p, size_t n);
+  bool put(const void* p, size_t n);  // at pos_, under the lock
   bool putf(const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-  int64_t begin_obj();
+  void drain();
 };
 
 }  // namespace pdf
