@@ -202,13 +202,17 @@ bool generic_decode(Mq& mq, const GenericParams& gp, uint8_t* gb, Bitmap* bm) {
       uint32_t w1 = (uint32_t)r1[-3] << 6 | (uint32_t)r1[-2] << 5 | (uint32_t)r1[-1] << 4 | (uint32_t)r1[0] << 3 |
                     (uint32_t)r1[1] << 2 | (uint32_t)r1[2] << 1 | r1[3];
       uint32_t w2 = (uint32_t)r2[-2] << 4 | (uint32_t)r2[-1] << 3 | (uint32_t)r2[0] << 2 | (uint32_t)r2[1] << 1 | r2[2];
+      // the coder's registers in locals: stores through the byte pointers
+      // (contexts, pixels) may alias the struct, which would reload it
+      Mq m = mq;
       for (int32_t x = 0; x < W; x++) {
-        const uint32_t b = (uint32_t)mq.decode(&gb[w2 << 11 | w1 << 4 | w0]);
+        const uint32_t b = (uint32_t)m.decode(&gb[w2 << 11 | w1 << 4 | w0]);
         r0[x] = (uint8_t)b;
         w0 = ((w0 << 1) | b) & 0xF;
         w1 = ((w1 << 1) | r1[x + 4]) & 0x7F;
         w2 = ((w2 << 1) | r2[x + 3]) & 0x1F;
       }
+      mq = m;
       continue;
     }
     auto P = [&](int dx, int dy) -> uint32_t { return bm->row(y + dy)[dx]; };
@@ -348,6 +352,7 @@ struct Decoder {
   uint8_t page_default = 0;
   int page_op = 0;
   int32_t end_row = 0;
+  bool page_touched = false;  // a region has been placed
 
   const Dict* dict(uint32_t num) const {
     for (const auto& d : dicts)
@@ -387,6 +392,7 @@ struct Decoder {
 
   bool place(const Bitmap& region, int32_t x, int32_t y, int op) {
     if (!have_page) return fail("jbig2: %s: region before the page information", name);
+    page_touched = true;
     if (!ensure_rows((int64_t)y + region.h)) return false;
     compose(&page, region, x, y, op);
     return true;
@@ -428,11 +434,19 @@ struct Decoder {
       const uint32_t rows = be32(d + dlen - 4);
       if (rows < (uint32_t)h) h = (int32_t)rows;
     }
-    Bitmap bm;
-    if (!bm.alloc(w, h, 0)) return fail("jbig2: %s: region %dx%d too large", name, w, h);
     std::vector<uint8_t> gb(gb_contexts(gp.tmpl), 0);
     Mq mq;
     mq.init(d, dlen);
+    // the common page (jbig2 -p): one region covering a fresh all-0 page,
+    // combined by OR / XOR / REPLACE -- the result is the region itself, so
+    // it is decoded into the page's bitmap directly
+    if (!page_touched && !striped && page_default == 0 && x == 0 && y == 0 && w == page.w && h == page.h &&
+        (op == 0 || op == 2 || op == 4)) {
+      page_touched = true;
+      return generic_decode(mq, gp, gb.data(), &page);
+    }
+    Bitmap bm;
+    if (!bm.alloc(w, h, 0)) return fail("jbig2: %s: region %dx%d too large", name, w, h);
     if (!generic_decode(mq, gp, gb.data(), &bm)) return false;
     return place(bm, x, y, op);
   }
