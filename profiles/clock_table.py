@@ -35,7 +35,7 @@ launches = collections.Counter()
 if kt:
     for r in csv.DictReader(open(kt[0])):
         launches[r["Kernel_Name"][:56]] += 1
-print("%-56s %9s %9s %8s %8s" % ("kernel", "dur_ms", "GHz", "VALU%", "VALU/wave"))
+print("%-56s %9s %9s %8s %9s %9s" % ("kernel", "dur_ms", "GHz", "VALU%", "VALU/wave", "SALU/wave"))
 for k, v in sorted(agg.items(), key=lambda kv: -dur.get(kv[0], 0)):
     t = dur.get(k, 0.0)
     gui = v.get("GRBM_GUI_ACTIVE", 0.0)
@@ -44,12 +44,16 @@ for k, v in sorted(agg.items(), key=lambda kv: -dur.get(kv[0], 0)):
     valu = v.get("SQ_INSTS_VALU", 0.0)
     frac = valu * 4 / (1024 * gui) if gui > 0 else 0.0
     waves = v.get("SQ_WAVES", 0.0)
-    print("%-56s %9.3f %9.3f %8.1f %8.0f" % (k, t * 1e3, ghz, 100 * frac, valu / waves if waves else 0))
+    salu = v.get("SQ_INSTS_SALU", 0.0)
+    print("%-56s %9.3f %9.3f %8.1f %9.0f %9.0f" % (k, t * 1e3, ghz, 100 * frac, valu / waves if waves else 0,
+                                                  salu / waves if waves else 0))
     n = launches.get(k, 0)
     if len(sys.argv) > 3 and n:
         doc["kernels"][k.split("(")[0].split("::")[-1].split("<")[0] + ("<" + k.split("<")[1].split(">")[0] + ">" if "<" in k else "")] = {
             "launches": n, "ms_per_launch": round(t * 1e3 / n, 4), "clock_ghz": round(ghz, 3),
-            "valu_insts_per_sheet": int(valu / n / int(sys.argv[2])), "valu_issue_frac": round(frac, 4)}
+            "valu_insts_per_sheet": int(valu / n / int(sys.argv[2])), "valu_issue_frac": round(frac, 4),
+            "valu_insts_per_wave": round(valu / waves, 1) if waves else None,
+            "salu_insts_per_wave": round(salu / waves, 1) if waves else None}
 if len(sys.argv) > 3:
     with open(sys.argv[3], "w") as f:
         json.dump(doc, f, indent=1)
