@@ -262,7 +262,8 @@ static void pdf_case(const UphipPdfDocument *unused, const uint8_t *p, size_t n)
 static void pdf(const char *dir, const char *fixtures) {
   static const char *good[] = {"xrefstream_objstm.pdf", "incremental.pdf", "damaged_xref.pdf", "filters.pdf",
                                "pil_multipage.pdf",     "jpx.pdf",         "encrypted.pdf",    "test_jbig2.pdf",
-                               "jbig2_generic.pdf",     "ccitt_pil.pdf",   "ccitt_g3.pdf"};
+                               "jbig2_generic.pdf",     "ccitt_pil.pdf",   "ccitt_g3.pdf",
+                               "palette_pil.pdf",       "palette_4bit.pdf"};
   static uint8_t raw[1 << 16], tmp[1 << 16];
   char path[512];
   unsigned seed = 777;

@@ -418,7 +418,7 @@ def main():
     jg = jpeg_bytes(gradient(30, 20, 1))
     d = Doc()
     d.add(1, b"<< /Type /Catalog /Pages 2 0 R >>")
-    d.add(2, b"<< /Type /Pages /Kids [5 0 R 8 0 R 11 0 R 14 0 R 17 0 R] /Count 5 >>")
+    d.add(2, b"<< /Type /Pages /Kids [5 0 R 8 0 R 11 0 R 14 0 R 17 0 R 21 0 R] /Count 6 >>")
     page_objs(d, 3, b"<< /Type /XObject /Subtype /Image /Width 24 /Height 16 /ColorSpace /DeviceRGB "
               b"/BitsPerComponent 8 /Filter [/ASCII85Decode /FlateDecode] /Length %d >>" % len(a85), a85, 24, 16)
     page_objs(d, 6, b"<< /Type /XObject /Subtype /Image /Width 20 /Height 10 /ColorSpace /DeviceGray "
@@ -431,6 +431,8 @@ def main():
     page_objs(d, 15, b"<< /Type /XObject /Subtype /Image /Width 4 /Height 4 /ColorSpace [/Indexed /DeviceRGB 1 <000000FFFFFF>] "
               b"/BitsPerComponent 8 /Length 16 >>", bytes(16), 4, 4)
     d.add(18, b"<< /N 1 /Length 4 >>", b"\x00\x00\x00\x00")
+    page_objs(d, 19, b"<< /Type /XObject /Subtype /Image /Width 5 /Height 3 /ColorSpace /DeviceCMYK "
+              b"/BitsPerComponent 8 /Length 60 >>", bytes(60), 5, 3)
     record("filters.pdf", d.serialise(), [
         {"format": "FLATE", "w": 24, "h": 16, "c": 3, "bpc": 8, "data": sha(zlib.compress(rgb2.tobytes())),
          "pixels": px_sha(rgb2), "box": [24, 16, 0]},
@@ -439,8 +441,10 @@ def main():
         {"format": "RAW", "w": 16, "h": 12, "c": 1, "bpc": 1, "data": sha(packed1.tobytes()),
          "pixels": px_sha(packed1), "pixfmt": "MONOWHITE", "box": [16, 12, 0]},
         {"format": "JPEG", "w": 30, "h": 20, "c": 1, "bpc": 8, "data": sha(jg), "box": [20, 10, 0]},
-        {"format": "RAW", "w": 4, "h": 4, "c": 1, "bpc": 8, "data": sha(bytes(16)), "nopixels": True,
-         "box": [4, 4, 0]},
+        {"format": "RAW", "w": 4, "h": 4, "c": 1, "bpc": 8, "data": sha(bytes(16)),
+         "pixels": px_sha(np.zeros((4, 12), np.uint8)), "pixfmt": "RGB24", "box": [4, 4, 0]},
+        {"format": "RAW", "w": 5, "h": 3, "c": 4, "bpc": 8, "data": sha(bytes(60)), "nopixels": True,
+         "box": [5, 3, 0]},
     ])
 
     # 5. an encrypted trailer (refused: no decryption)
@@ -551,6 +555,34 @@ def main():
                       "pixels": px_sha(gray_of(im)), "pixfmt": "GRAY8", "box": [im.width, im.height, 0]})
     d.add(2, b"<< /Type /Pages /Kids [%s] /Count %d >>" % (b" ".join(kids), len(kids)))
     record("ccitt_g3.pdf", d.serialise(), pages)
+
+    # 10. palette images: PIL's own (ASCIIHex, /Indexed /DeviceRGB 255 with a
+    #     hex-string lookup) and a 4-bit index stream with a gray base and a
+    #     stream lookup; expected: PIL's RGB conversion / the lookup applied
+    r = np.random.default_rng(9)
+    a = r.integers(0, 200, (30, 41)).astype(np.uint8)
+    pim = Image.fromarray(a, "P")
+    pim.putpalette(list(r.integers(0, 256, 768).astype(np.uint8)))
+    b = io.BytesIO()
+    pim.save(b, "PDF")
+    record("palette_pil.pdf", b.getvalue(), [
+        {"format": "RAW", "w": 41, "h": 30, "c": 1, "bpc": 8, "pixels": px_sha(np.asarray(pim.convert("RGB"))),
+         "pixfmt": "RGB24", "box": [41, 30, 0]}])
+    idx = r.integers(0, 16, (7, 9)).astype(np.uint8)
+    packed4 = np.zeros((7, 5), np.uint8)
+    for x in range(9):
+        packed4[:, x // 2] |= idx[:, x] << (4 if x % 2 == 0 else 0)
+    lut = r.integers(0, 256, 16).astype(np.uint8)
+    d = Doc()
+    d.add(1, b"<< /Type /Catalog /Pages 2 0 R >>")
+    d.add(2, b"<< /Type /Pages /Kids [5 0 R] /Count 1 >>")
+    z4 = zlib.compress(packed4.tobytes())
+    page_objs(d, 3, b"<< /Type /XObject /Subtype /Image /Width 9 /Height 7 /ColorSpace [/Indexed /DeviceGray 15 6 0 R] "
+              b"/BitsPerComponent 4 /Filter /FlateDecode /Length %d >>" % len(z4), z4, 9, 7)
+    d.add(6, b"<< /Length 16 >>", lut.tobytes())
+    record("palette_4bit.pdf", d.serialise(), [
+        {"format": "FLATE", "w": 9, "h": 7, "c": 1, "bpc": 4, "data": sha(z4), "pixels": px_sha(lut[idx]),
+         "pixfmt": "GRAY8", "box": [9, 7, 0]}])
 
     with open(os.path.join(OUT, "expected.json"), "w") as f:
         json.dump(expected, f, indent=1, sort_keys=True)

@@ -319,7 +319,7 @@ def test_reader_errors():
     with pytest.raises(Exception, match="PDF"):
         pdf.PdfDocument.open_memory(b"not a pdf at all, just text" * 4)
     d = pdf.PdfDocument.open(os.path.join(FIX, "filters.pdf"))
-    for bad in (-1, 5, 1 << 20):
+    for bad in (-1, 6, 1 << 20):
         with pytest.raises(Exception, match="out of range"):
             d.extract_page_image(bad)
         with pytest.raises(Exception, match="out of range"):

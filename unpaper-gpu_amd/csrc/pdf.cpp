@@ -1244,9 +1244,43 @@ bool Document::extract_image(int page, PageImage* out) {
       const Obj* icc = resolve(&cs->a[1]);
       const Obj* N = icc && (icc->t == T::Stream || icc->t == T::Dict) ? resolve(icc->get("N")) : nullptr;
       comps = N && N->t == T::Int ? (int)N->i : 0;
-    } else if (f == "Indexed" || f == "I") {
+    } else if ((f == "Indexed" || f == "I") && cs->a.size() >= 4) {
+      // [/Indexed base hival lookup]: one index per pixel, the palette's
+      // entries of the base space (lookup a string or a stream)
       comps = 1;
       out->indexed = true;
+      const Obj* base = resolve(&cs->a[1]);
+      int bn = 0;
+      if (base && base->t == T::Name)
+        bn = (base->s == "DeviceGray" || base->s == "G" || base->s == "CalGray") ? 1
+             : (base->s == "DeviceRGB" || base->s == "RGB" || base->s == "CalRGB") ? 3 : 0;
+      else if (base && base->t == T::Arr && !base->a.empty()) {
+        const Obj* bf = resolve(&base->a[0]);
+        if (bf && bf->is_name("ICCBased") && base->a.size() > 1) {
+          const Obj* icc = resolve(&base->a[1]);
+          const Obj* N = icc && (icc->t == T::Stream || icc->t == T::Dict) ? resolve(icc->get("N")) : nullptr;
+          bn = N && N->t == T::Int && (N->i == 1 || N->i == 3) ? (int)N->i : 0;
+        } else if (bf && (bf->is_name("CalRGB") || bf->is_name("DeviceRGB"))) {
+          bn = 3;
+        } else if (bf && (bf->is_name("CalGray") || bf->is_name("DeviceGray"))) {
+          bn = 1;
+        }
+      }
+      const Obj* hv = resolve(&cs->a[2]);
+      const Obj* lk = resolve(&cs->a[3]);
+      const int hival = hv && hv->t == T::Int ? (int)hv->i : -1;
+      if (bn && hival >= 0 && hival <= 255 && lk) {
+        if (lk->t == T::Str)
+          out->palette.assign(lk->s.begin(), lk->s.end());
+        else if (lk->t == T::Stream && !stream_data(*lk, &out->palette, 1 << 16))
+          out->palette.clear();
+        if (out->palette.size() >= (size_t)(hival + 1) * bn) {
+          out->palette.resize((size_t)(hival + 1) * bn);
+          out->palette_comps = bn;
+        } else {
+          out->palette.clear();
+        }
+      }
     } else if (f == "CalGray" || f == "DeviceGray" || f == "G" || f == "Separation") {
       comps = 1;
     } else if (f == "CalRGB" || f == "Lab" || f == "DeviceRGB" || f == "RGB") {
@@ -1361,7 +1395,10 @@ bool Document::metadata(Meta* out) {
 
 int pixel_format(const PageImage& im) {
   if (im.format == kJbig2 || im.format == kCcitt) return UPHIP_FMT_GRAY8;  // expanded to 0 / 255
-  if (im.indexed) return -1;
+  if (im.indexed)  // palette images expand to their base space
+    return im.palette_comps && (im.bpc == 1 || im.bpc == 2 || im.bpc == 4 || im.bpc == 8)
+               ? (im.palette_comps == 3 ? UPHIP_FMT_RGB24 : UPHIP_FMT_GRAY8)
+               : -1;
   if (im.components == 1 && im.bpc == 8) return UPHIP_FMT_GRAY8;
   if (im.components == 3 && im.bpc == 8) return UPHIP_FMT_RGB24;
   // one bit: 0 is black under the default /Decode [0 1] (FFmpeg's monoblack)
@@ -1409,7 +1446,8 @@ bool decode_pixels(const PageImage& im, uint8_t* dst, int64_t linesize, const ch
     return true;
   }
   const int64_t rb = ((int64_t)im.width * im.components * im.bpc + 7) / 8;
-  if (linesize < rb) return fail("pdf: %s: linesize too small", name);
+  if (linesize < (im.indexed ? (int64_t)im.width * im.palette_comps : rb))
+    return fail("pdf: %s: linesize too small", name);
   std::vector<uint8_t> inflated;
   const std::vector<uint8_t>* px = &im.data;
   if (im.format == kFlate || im.format == kPng) {
@@ -1422,6 +1460,23 @@ bool decode_pixels(const PageImage& im, uint8_t* dst, int64_t linesize, const ch
   }
   if ((int64_t)px->size() < rb * im.height)
     return fail("pdf: %s: image data is short (%zu bytes for %dx%d)", name, px->size(), im.width, im.height);
+  if (im.indexed) {
+    // indices of bpc bits, MSB first; past hival they take the last entry
+    // (as MuPDF clamps)
+    const int bn = im.palette_comps, bpc = im.bpc;
+    const int last = (int)im.palette.size() / bn - 1;
+    for (int32_t y = 0; y < im.height; y++) {
+      const uint8_t* s = px->data() + (int64_t)y * rb;
+      uint8_t* d = dst + (int64_t)y * linesize;
+      for (int32_t x = 0; x < im.width; x++) {
+        const int64_t bit = (int64_t)x * bpc;
+        int idx = bpc == 8 ? s[x] : (s[bit >> 3] >> (8 - bpc - (int)(bit & 7))) & ((1 << bpc) - 1);
+        if (idx > last) idx = last;
+        for (int c = 0; c < bn; c++) d[x * bn + c] = im.palette[(size_t)(idx * bn + c)];
+      }
+    }
+    return true;
+  }
   const bool invert8 = im.inverted && fmt == UPHIP_FMT_GRAY8;
   for (int32_t y = 0; y < im.height; y++) {
     const uint8_t* s = px->data() + (int64_t)y * rb;

@@ -70,7 +70,9 @@ struct PageImage {
   int32_t format = kUnknown;
   bool mask = false;
   bool inverted = false;  // /Decode [1 0] on a one-component image
-  bool indexed = false;   // /Indexed colour space (not supported by the pixel path)
+  bool indexed = false;   // /Indexed colour space: expanded through `palette`
+  std::vector<uint8_t> palette;  // (hival + 1) entries of palette_comps bytes
+  int32_t palette_comps = 0;     // 1 (gray base) or 3 (RGB base); 0 = not expandable
   int32_t predictor = 1, colors = 1, pbpc = 8, columns = 1;  // Flate /DecodeParms
   ccitt::Params fax;                                          // CCITTFaxDecode /DecodeParms
   int32_t object = 0;  // its object number (diagnostics)
