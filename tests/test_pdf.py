@@ -338,6 +338,10 @@ def test_reader_errors():
     L.uphip_pdf_close(None)
     L.uphip_pdf_free_image(None)
     assert pdf.is_pdf_file("a.PDF") and pdf.is_pdf_file("/x/y.pdf") and not pdf.is_pdf_file("a.png")
+    # a PDF handed to the single-image readers names the document path
+    info = A.PnmInfo()
+    assert L.uphip_image_probe(os.path.join(FIX, "filters.pdf").encode(), C.byref(info)) == -1
+    assert "uphip_source_pdf" in _err()
     assert not pdf.is_pdf_file(None)
     assert [pdf.image_format_name(k) for k in range(9)] == [
         "UNKNOWN", "JPEG", "JPEG2000", "JBIG2", "CCITT", "PNG", "RAW", "FLATE", "UNKNOWN"]

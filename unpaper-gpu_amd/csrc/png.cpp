@@ -329,7 +329,8 @@ bool decode(Png& p, uint8_t* out, int64_t linesize, const char* path) {
 }
 
 // the file's signature: 1 PNG, 2 JPEG (SOI + a marker), 3 JPEG 2000 (the JP2
-// signature box or SOC + SIZ), 0 anything else (PNM)
+// signature box or SOC + SIZ), 4 PDF (whole documents: uphip_source_pdf),
+// 0 anything else (PNM)
 int sniff(FILE* f) {
   uint8_t sig[12];
   const size_t n = fread(sig, 1, 12, f);
@@ -340,6 +341,7 @@ int sniff(FILE* f) {
   if ((n == 12 && memcmp(sig, kJp2, 12) == 0) ||
       (n >= 4 && sig[0] == 0xFF && sig[1] == 0x4F && sig[2] == 0xFF && sig[3] == 0x51))
     return 3;
+  if (n >= 5 && memcmp(sig, "%PDF-", 5) == 0) return 4;
   return 0;
 }
 
@@ -403,6 +405,9 @@ int uphip_image_probe(const char* path, UphipPnmInfo* info) {
   if (!f) return fail("image: cannot open %s: %s", path, strerror(errno)), -1;
   const int kind = sniff(f);
   fclose(f);
+  if (kind == 4)
+    return fail("image: %s is a PDF document: read its pages with uphip_source_pdf / uphip_pdf_read_page", path),
+           -1;
   return kind == 1 ? uphip_png_probe(path, info)
        : kind == 2 ? uphip_jpeg_probe(path, info)
        : kind == 3 ? uphip_jp2_probe(path, info)
@@ -415,6 +420,9 @@ int uphip_image_read(const char* path, void* dst, int64_t linesize, const UphipP
   if (!f) return fail("image: cannot open %s: %s", path, strerror(errno)), -1;
   const int kind = sniff(f);
   fclose(f);
+  if (kind == 4)
+    return fail("image: %s is a PDF document: read its pages with uphip_source_pdf / uphip_pdf_read_page", path),
+           -1;
   return kind == 1 ? uphip_png_read(path, dst, linesize, expect)
        : kind == 2 ? uphip_jpeg_read(path, dst, linesize, expect)
        : kind == 3 ? uphip_jp2_read(path, dst, linesize, expect)
