@@ -56,6 +56,9 @@ CTEST      := tests/c/_build/backend_ops
 # own headers, where they lie; skipped when the tree is absent (GPU box)
 REFERENCE  ?= /root/reference
 ADAPTER    := tests/c/_build/adapter_ops
+# the reference's own PDF unit tests (tests/pdf_{reader,writer}_test.c, compiled
+# where they lie) linked against integration/pdf_hip.c instead of MuPDF
+REF_PDF_TESTS := tests/c/_build/ref_pdf_reader_test tests/c/_build/ref_pdf_writer_test
 
 LIBM_CHECK := tests/c/_build/libm_check
 SANITIZE   := tests/c/_build/sanitize
@@ -69,7 +72,7 @@ all: lib oracle ctest libm_check jdec_emul j2k_emul
 lib: $(LIB)
 oracle: $(ORACLE_LIB)
 ctest: $(CTEST)
-adapter: $(ADAPTER)
+adapter: $(ADAPTER) $(REF_PDF_TESTS)
 
 $(OBJDIR)/%.hip.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -106,6 +109,13 @@ $(ADAPTER): tests/c/adapter_main.c tests/c/pages.h integration/backend_hip.c int
 	  tests/c/adapter_main.c integration/backend_hip.c -o $@ \
 	  -L$(PKG)/lib -L oracle/_build -lunpaper_hip -loracle -lm \
 	  -Wl,-rpath,'$$ORIGIN/../../../$(PKG)/lib' -Wl,-rpath,'$$ORIGIN/../../../oracle/_build'
+
+tests/c/_build/ref_pdf_%_test: integration/pdf_hip.c include/unpaper_hip.h $(LIB)
+	@test -f $(REFERENCE)/tests/pdf_$*_test.c || { echo "ref pdf tests: no reference tree under $(REFERENCE)"; exit 1; }
+	@mkdir -p tests/c/_build
+	$(CC) -O2 -std=gnu11 -Wall -Wno-unused-variable -Wno-unused-function -I$(REFERENCE) -Iinclude \
+	  $(REFERENCE)/tests/pdf_$*_test.c integration/pdf_hip.c -o $@ \
+	  -L$(PKG)/lib -lunpaper_hip -lm -Wl,-rpath,'$$ORIGIN/../../../$(PKG)/lib'
 
 # glibc sinf/cosf/powf(x, 2) restatement (csrc/libm_glibc.h) against this
 # host's libm; plain g++, contraction off like the device build.

@@ -639,3 +639,54 @@ def test_runner_host_decoded_pdf_pages(hip, oracle, tmp_path):
             r.close()
         assert failed == 0, err
         assert (pnm_read(out % page).payload() == exp.payload()).all(), (name, page)
+
+
+# ---------------------------------------------------------------------------
+# the reference's own PDF unit tests (tests/pdf_reader_test.c,
+# tests/pdf_writer_test.c in the reference), compiled where they lie against
+# integration/pdf_hip.c -- the reference's reader / writer API on this
+# library instead of MuPDF (make adapter; built here, run here and on the box)
+# ---------------------------------------------------------------------------
+REF_PDF = {k: os.path.join(ROOT, "tests", "c", "_build", "ref_pdf_%s_test" % k) for k in ("reader", "writer")}
+
+
+def _ref_pdf_run(which, tmp_path):
+    import subprocess
+    exe = REF_PDF[which]
+    if not os.path.exists(exe):
+        if not os.path.isdir("/root/reference/tests"):
+            pytest.skip("reference tree absent and %s not prebuilt" % exe)
+        subprocess.check_call(["make", "-s", os.path.relpath(exe, ROOT)], cwd=ROOT)
+    # the tests find tests/pdf_samples beside $TEST_IMGSRC_DIR and a JPEG in it
+    (tmp_path / "source_images").mkdir()
+    os.symlink(FIX, tmp_path / "pdf_samples")
+    Image.fromarray((np.arange(120 * 90).reshape(90, 120) % 251).astype(np.uint8)).save(
+        tmp_path / "source_images" / "test_jpeg.jpg", quality=90)
+    env = dict(os.environ, TEST_IMGSRC_DIR=str(tmp_path / "source_images"))
+    return subprocess.run([exe], cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+
+
+def test_reference_pdf_writer_unit_tests(tmp_path):
+    """The reference's pdf_writer_test.c passes unchanged on integration/pdf_hip.c."""
+    r = _ref_pdf_run("writer", tmp_path)
+    assert r.returncode == 0 and "All tests passed!" in r.stdout, r.stdout + r.stderr
+    assert "FAILED" not in r.stdout and "SKIPPED" not in r.stdout
+
+
+def test_reference_pdf_reader_unit_tests_host(tmp_path):
+    """The reference's pdf_reader_test.c up to its render tests, which need
+    the device JPEG decode (the GPU test below runs them)."""
+    r = _ref_pdf_run("reader", tmp_path)
+    out = r.stdout
+    head = out.split("Test: pdf_render_page...")[0]
+    assert head.count("PASSED") == 8 and "FAILED" not in head and "SKIPPED" not in head, out
+    assert "(2480x3507, JPEG, 1444986 bytes)" in head
+
+
+@pytest.mark.gpu
+def test_reference_pdf_reader_unit_tests(hip, tmp_path):
+    """All of pdf_reader_test.c, render tests included (image pages: the
+    page's image decoded on the device, box-resampled to the page at 150 dpi)."""
+    r = _ref_pdf_run("reader", tmp_path)
+    assert r.returncode == 0 and "All tests passed!" in r.stdout, r.stdout + r.stderr
+    assert "FAILED" not in r.stdout and "SKIPPED" not in r.stdout
