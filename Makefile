@@ -58,7 +58,8 @@ REFERENCE  ?= /root/reference
 ADAPTER    := tests/c/_build/adapter_ops
 # the reference's own PDF unit tests (tests/pdf_{reader,writer}_test.c, compiled
 # where they lie) linked against integration/pdf_hip.c instead of MuPDF
-REF_PDF_TESTS := tests/c/_build/ref_pdf_reader_test tests/c/_build/ref_pdf_writer_test
+REF_PDF_TESTS := tests/c/_build/ref_pdf_reader_test tests/c/_build/ref_pdf_writer_test \
+                 tests/c/_build/ref_jbig2_decode_test
 
 LIBM_CHECK := tests/c/_build/libm_check
 SANITIZE   := tests/c/_build/sanitize
@@ -116,6 +117,13 @@ tests/c/_build/ref_pdf_%_test: integration/pdf_hip.c include/unpaper_hip.h $(LIB
 	$(CC) -O2 -std=gnu11 -Wall -Wno-unused-variable -Wno-unused-function -I$(REFERENCE) -Iinclude \
 	  $(REFERENCE)/tests/pdf_$*_test.c integration/pdf_hip.c -o $@ \
 	  -L$(PKG)/lib -lunpaper_hip -lm -Wl,-rpath,'$$ORIGIN/../../../$(PKG)/lib'
+
+tests/c/_build/ref_jbig2_decode_test: integration/jbig2_hip.c integration/pdf_hip.c include/unpaper_hip.h $(LIB)
+	@test -f $(REFERENCE)/tests/jbig2_decode_test.c || { echo "ref jbig2 test: no reference tree under $(REFERENCE)"; exit 1; }
+	@mkdir -p tests/c/_build
+	$(CC) -O2 -std=gnu11 -Wall -Wno-unused-variable -Wno-unused-function -DUNPAPER_WITH_JBIG2 -DUNPAPER_WITH_PDF \
+	  -I$(REFERENCE) -Iinclude $(REFERENCE)/tests/jbig2_decode_test.c integration/jbig2_hip.c integration/pdf_hip.c \
+	  -o $@ -L$(PKG)/lib -lunpaper_hip -lm -Wl,-rpath,'$$ORIGIN/../../../$(PKG)/lib'
 
 # glibc sinf/cosf/powf(x, 2) restatement (csrc/libm_glibc.h) against this
 # host's libm; plain g++, contraction off like the device build.

@@ -664,6 +664,18 @@ int uphip_pdf_writer_add_page_pixels(UphipPdfWriter *writer, const uint8_t *pixe
                                      int32_t width, int32_t height, int32_t stride,
                                      int32_t format, int32_t dpi);
 int uphip_pdf_writer_page_count(UphipPdfWriter *writer);
+/* lib/jbig2_decode.h:19-45 (jbig2_decode over jbig2dec): an embedded JBIG2
+ * stream (+ its globals) to a 1-bit page, MSB first, 1 = black, rows
+ * `stride` bytes; free with uphip_jbig2_free_image.  Generic regions
+ * (arithmetic, templates 0-3, TPGDON), symbol dictionaries and text
+ * regions (csrc/jbig2.h). */
+typedef struct {
+  uint8_t *data;
+  uint32_t width, height, stride;
+} UphipJbig2Image;
+int uphip_jbig2_decode(const uint8_t *data, size_t size, const uint8_t *globals,
+                       size_t globals_size, UphipJbig2Image *out);
+void uphip_jbig2_free_image(UphipJbig2Image *image);
 int uphip_pdf_writer_close(UphipPdfWriter *writer);  /* frees the writer */
 void uphip_pdf_writer_abort(UphipPdfWriter *writer); /* frees the writer */
 

@@ -648,6 +648,7 @@ def test_runner_host_decoded_pdf_pages(hip, oracle, tmp_path):
 # library instead of MuPDF (make adapter; built here, run here and on the box)
 # ---------------------------------------------------------------------------
 REF_PDF = {k: os.path.join(ROOT, "tests", "c", "_build", "ref_pdf_%s_test" % k) for k in ("reader", "writer")}
+REF_PDF["jbig2"] = os.path.join(ROOT, "tests", "c", "_build", "ref_jbig2_decode_test")
 
 
 def _ref_pdf_run(which, tmp_path):
@@ -690,3 +691,13 @@ def test_reference_pdf_reader_unit_tests(hip, tmp_path):
     r = _ref_pdf_run("reader", tmp_path)
     assert r.returncode == 0 and "All tests passed!" in r.stdout, r.stdout + r.stderr
     assert "FAILED" not in r.stdout and "SKIPPED" not in r.stdout
+
+
+def test_reference_jbig2_unit_tests(tmp_path):
+    """The reference's jbig2_decode_test.c (built with JBIG2 and PDF on)
+    passes unchanged on integration/jbig2_hip.c + pdf_hip.c: test_jbig2.pdf
+    decodes to 200x100 with both colours after the gray expansion."""
+    r = _ref_pdf_run("jbig2", tmp_path)
+    assert r.returncode == 0 and "All tests passed!" in r.stdout, r.stdout + r.stderr
+    assert r.stdout.count("PASSED") == 4 and "FAILED" not in r.stdout and "skipped" not in r.stdout
+    assert "(200x100, stride=25)" in r.stdout

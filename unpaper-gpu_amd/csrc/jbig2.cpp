@@ -6,6 +6,7 @@
 #include <cstring>
 #include <string>
 
+#include "unpaper_hip.h"
 #include "j2k_t1.h"  // the MQ coder's state table (T.88 Table E.1 = T.800 Table C.2)
 #include "runtime.h"
 
@@ -692,3 +693,32 @@ bool decode(const uint8_t* data, size_t n, const uint8_t* globals, size_t gn, Pa
 
 }  // namespace jbig2
 }  // namespace uph
+
+// ---------------------------------------------------------------------------
+// C ABI (include/unpaper_hip.h): lib/jbig2_decode.h's decode on this decoder
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int uphip_jbig2_decode(const uint8_t* data, size_t size, const uint8_t* globals, size_t globals_size,
+                       UphipJbig2Image* out) {
+  if (!out) return uph::fail("jbig2_decode: null output"), -1;
+  memset(out, 0, sizeof(*out));
+  if (!data || !size) return uph::fail("jbig2_decode: no data"), -1;
+  uph::jbig2::Page pg;
+  if (!uph::jbig2::decode(data, size, globals, globals_size, &pg, "<memory>")) return -1;
+  out->data = (uint8_t*)malloc(pg.bits.size() ? pg.bits.size() : 1);
+  if (!out->data) return uph::fail("jbig2_decode: out of memory"), -1;
+  memcpy(out->data, pg.bits.data(), pg.bits.size());
+  out->width = (uint32_t)pg.width;
+  out->height = (uint32_t)pg.height;
+  out->stride = (uint32_t)pg.stride;
+  return 0;
+}
+
+void uphip_jbig2_free_image(UphipJbig2Image* image) {
+  if (!image) return;
+  free(image->data);
+  memset(image, 0, sizeof(*image));
+}
+
+}  // extern "C"

@@ -65,6 +65,7 @@ EXPORTED = [
     "uphip_pdf_writer_add_page_jp2", "uphip_pdf_writer_add_page_pixels",
     "uphip_pdf_writer_page_count", "uphip_pdf_writer_close", "uphip_pdf_writer_abort",
     "uphip_source_pdf", "uphip_source_page_count", "uphip_sink_pdf", "uphip_sink_finish",
+    "uphip_jbig2_decode", "uphip_jbig2_free_image",
 ]
 
 
