@@ -110,6 +110,8 @@ def parse():
                     help="skip the C2 single-page latency and the C4 single-sheet runs")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the C4 object of the default line (16 RGB24 sheets, verified)")
+    ap.add_argument("--c4-streams", type=int, default=0,
+                    help="C4 batches (HIP streams) in flight (0 = --streams)")
     ap.add_argument("--host-batch", type=int, default=32, help="sheets per batch, host-fed runs")
     ap.add_argument("--host-streams", type=int, default=8, help="batches per device, host-fed")
     ap.add_argument("--valu", default=os.path.join(ROOT, "profiles", "valu.json"),
@@ -674,7 +676,12 @@ def run_c4(args, L, d, devices, firsts, n_gpus, version, valid, nsheets=0, steps
     pages = DeviceBuffer(stride * nsheets)
     if L.uphip_synth_sheets_rgb(pages.ptr, pitch, stride, C4_W, C4_H, firsts[0], nsheets) != 0:
         raise UnpaperHipError("synth_sheets_rgb failed")
-    streams = min(args.streams, max(1, (nsheets + bsz - 1) // bsz))
+    # batches in flight (--streams, as C3): more than a pass's chunks, so the
+    # next pass's chunks start while a pass's flood-heavy chunk still runs on
+    # its own batch -- a long job of C4 sheets keeps as many in flight
+    # (tools/c4_streams.sh: 4 -> 316, 8 -> 439, 12 -> 476, 16 -> 494 sheets/s,
+    # every resident sheet checked)
+    streams = args.c4_streams or args.streams
     r = Runner(opts, bsz, C4_W, C4_H, A.FMT_RGB24, devices=devices[:1], streams=streams,
                timing=True)
     shard = [(pages.ptr, pitch, stride, nsheets)]
