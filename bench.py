@@ -110,6 +110,8 @@ def parse():
                     help="skip the C2 single-page latency and the C4 single-sheet runs")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the C4 object of the default line (16 RGB24 sheets, verified)")
+    ap.add_argument("--codec-streams", type=int, default=0,
+                    help="batches in flight for --config jpeg / jp2 (0 = 8 / 16)")
     ap.add_argument("--c4-streams", type=int, default=0,
                     help="C4 batches (HIP streams) in flight (0 = --streams)")
     ap.add_argument("--host-batch", type=int, default=32, help="sheets per batch, host-fed runs")
@@ -509,7 +511,11 @@ def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid, codec="jpeg"):
         mb = sum(os.path.getsize(p) for p in uniq) / 16 / 1e6
         opts = A.Options()
         L.uphip_options_init(C.byref(opts))
-        r = Runner(opts, 32, W, H, A.FMT_GRAY8, devices=devices[:1], streams=8,
+        # batches in flight: JPEG 2000 chunks wait on their one code-block
+        # launch, so more of them in flight pay (tools/codec_streams.sh: 32 x 8
+        # 698, 32 x 16 856, 64 x 8 797, 64 x 16 821 pages/s); JPEG is host-bound
+        streams = args.codec_streams or (16 if codec == "jp2" else 8)
+        r = Runner(opts, args.host_batch, W, H, A.FMT_GRAY8, devices=devices[:1], streams=streams,
                    host_threads=threads)
         try:
             outs = os.path.join(tmpdir, "o%02d.pgm")
@@ -549,7 +555,7 @@ def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid, codec="jpeg"):
             "value": round(n / t, 2), "unit": "pages/s", "n_gpus": 1, "higher_is_better": True,
             "dtype": "u8", "data": "synthetic (%s, %.2f MB a page)" % (made, mb),
             "host_threads": threads, "load_s": round(st.load_s, 3),
-            "config": {"pages": n, "sheets_per_batch": 32, "streams": 8,
+            "config": {"pages": n, "sheets_per_batch": args.host_batch, "streams": streams,
                        "source": "%s files in tmpfs (16 distinct, round robin)" % codec.upper(),
                        "sink": "discarded"},
             "verified": checked, "library": version, "valid": valid}
