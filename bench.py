@@ -599,7 +599,9 @@ def run_pdf(args, L, d, devices, firsts, n_gpus, version, valid):
         w.close()
         opts = A.Options()
         L.uphip_options_init(C.byref(opts))
-        r = Runner(opts, 32, W, H, A.FMT_GRAY8, devices=devices[:1], streams=8, host_threads=threads)
+        pdf_streams = args.codec_streams or 8
+        r = Runner(opts, args.host_batch, W, H, A.FMT_GRAY8, devices=devices[:1], streams=pdf_streams,
+                   host_threads=threads)
         try:
             for name, path in (("jbig2_50", jb), ("jpeg_%d" % n_jpeg, jpg_pdf)):
                 src = source_pdf(path, 300)
@@ -659,7 +661,8 @@ def run_pdf(args, L, d, devices, firsts, n_gpus, version, valid):
             "higher_is_better": True, "dtype": "u8",
             "data": "the reference's benchmark_jbig2_50page.pdf; synthetic JPEG pages (PIL quality 95)",
             "host_threads": threads, "legs": legs,
-            "config": {"sheets_per_batch": 32, "streams": 8, "dpi": 300, "pdf_quality": "fast (JPEG 85)"},
+            "config": {"sheets_per_batch": args.host_batch, "streams": args.codec_streams or 8, "dpi": 300,
+                       "pdf_quality": "fast (JPEG 85)"},
             "library": version, "valid": valid}
 
 
