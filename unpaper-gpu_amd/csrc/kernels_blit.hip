@@ -1943,6 +1943,9 @@ __device__ __forceinline__ uint32_t row_off(int32_t y, int64_t pitch) {
 #ifndef UPH_ROT_FULL
 #define UPH_ROT_FULL 1  // the branch-free row loop for full tiles
 #endif
+#ifndef UPH_ROT_EARLY
+#define UPH_ROT_EARLY 1  // 0: the column-sum zero barrier in every tile (round-4 form)
+#endif
 #ifndef UPH_ROT_UNIFORM
 #define UPH_ROT_UNIFORM 0  // 1: skip wave rows of uniform 4x4 windows (A/B: see DESIGN §5)
 #endif
@@ -2020,9 +2023,14 @@ __global__ void __launch_bounds__(kRFT, UPH_ROT_MINB) k_rotate_cubic_g8f(PlaneRe
     if (!inside) __syncthreads();  // in-mask tiles: the staging barrier orders it
   }
 #else
+  // the tile's column sums zeroed; in-mask tiles need no barrier of their
+  // own here (the corners barrier below orders these writes before any
+  // wave's adds), so wave 0 starts on the corners while the block's other
+  // waves are still arriving
+  const bool outside_tile = !(cu0 <= cu1 && cv0 <= cv1);
   if (colsum) {
     if (threadIdx.x < kRFW) csum_s[threadIdx.x] = 0;
-    __syncthreads();
+    if (!UPH_ROT_EARLY || outside_tile) __syncthreads();
   }
 #endif
   if (!(cu0 <= cu1 && cv0 <= cv1)) {
