@@ -455,6 +455,9 @@ __device__ __forceinline__ void blur_rect_origin(const BlurGeom& g, int32_t r, i
   }
 }
 
+#ifndef UPH_BLUR_V16
+#define UPH_BLUR_V16 1  // 16-byte loads, 16 columns a lane (0: 4-byte loads; A/B 146.5 -> 140.6 us a launch)
+#endif
 // k_blur_counts for a gray plane: one workgroup per row of rectangles (the
 // first row at y = 0, row t at step_y + t*sh).  Lanes count dark pixels
 // (gray <= white) of aligned dwords over the strip's rows into per-column
@@ -468,10 +471,36 @@ __global__ void __launch_bounds__(256) k_blur_counts_g(PlaneRef img, BlurGeom g,
   const int32_t y0 = imax(ry, 0), y1 = imin(ry + g.sh, g.H);  // [y0, y1)
   const uint8_t* base = plane_ptr(img, s);
   extern __shared__ uint16_t ccount[];
-  const int32_t nd = (g.W + 3) >> 2;
-  // one compare per byte: the byte select of an SDWA compare and an add with
-  // carry-in make it two instructions, fewer than the 16-bit lane form
-  for (int32_t d = threadIdx.x; d < nd; d += 256) {
+#if UPH_BLUR_V16
+  // 16-byte loads (rows are 256-byte pitched, so a vector past W stays in
+  // the row): a lane counts 16 columns, 8 rows' loads in flight
+  const int32_t nv = (g.W + 15) >> 4;
+  for (int32_t vi = threadIdx.x; vi < nv; vi += 256) {
+    uint32_t c[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) c[j] = 0;
+    for (int32_t y = y0; y < y1; y += 8) {
+      uint4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        v[k] = *reinterpret_cast<const uint4*>(base + (int64_t)imin(y + k, y1 - 1) * img.P.pitch + 16 * vi);
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t keep = y + k < y1 ? 1u : 0u;
+        const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+          for (int j = 0; j < 4; j++) c[4 * q + j] += keep & (((w4[q] >> (8 * j)) & 0xFF) <= g.white ? 1u : 0u);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+      if (16 * vi + j < g.W) ccount[16 * vi + j] = (uint16_t)c[j];
+  }
+  if (false)
+#endif
+  for (int32_t d = threadIdx.x; d < ((g.W + 3) >> 2); d += 256) {
     uint32_t c[4] = {0, 0, 0, 0};
     for (int32_t y = y0; y < y1; y += 8) {
       uint32_t v[8];
