@@ -466,8 +466,11 @@ bool read_siz(Reader& r, const char* name, Siz* s) {
   s->XTO = (int32_t)r.u32();
   s->YTO = (int32_t)r.u32();
   s->C = (int)r.u16();
-  if (!r.ok || s->X <= 0 || s->Y <= 0 || s->XT <= 0 || s->YT <= 0 || s->X <= s->XO ||
-      s->Y <= s->YO || s->XTO > s->XO || s->YTO > s->YO)
+  // (offsets read as int32: a u32 above INT_MAX is negative and refused; the
+  // first tile must overlap the image area, A.5.1)
+  if (!r.ok || s->X <= 0 || s->Y <= 0 || s->XT <= 0 || s->YT <= 0 || s->XO < 0 || s->YO < 0 ||
+      s->XTO < 0 || s->YTO < 0 || s->X <= s->XO || s->Y <= s->YO || s->XTO > s->XO ||
+      s->YTO > s->YO || (int64_t)s->XTO + s->XT <= s->XO || (int64_t)s->YTO + s->YT <= s->YO)
     return jfail(name, "bad SIZ");
   if (s->C != 1 && s->C != 3) return jfail(name, "only 1- and 3-component images are supported");
   for (int c = 0; c < s->C; c++) {
@@ -609,11 +612,13 @@ bool read_stream(const uint8_t* d, size_t n, const char* name, Stream* S, bool h
 }
 
 // tile-component geometry (B.3, B.5)
+// (tile bounds in int64: XTO + (tx + 1) * XT overflows int32 for large XT;
+// clipped to the image, so the results fit again)
 void tile_geometry(const Siz& z, int tx, int ty, int ntx, const Params& P, Tile* T) {
-  T->x0 = std::max(z.XTO + tx * z.XT, z.XO);
-  T->x1 = std::min(z.XTO + (tx + 1) * z.XT, z.X);
-  T->y0 = std::max(z.YTO + ty * z.YT, z.YO);
-  T->y1 = std::min(z.YTO + (ty + 1) * z.YT, z.Y);
+  T->x0 = (int32_t)std::max<int64_t>(z.XTO + (int64_t)tx * z.XT, z.XO);
+  T->x1 = (int32_t)std::min<int64_t>(z.XTO + (int64_t)(tx + 1) * z.XT, z.X);
+  T->y0 = (int32_t)std::max<int64_t>(z.YTO + (int64_t)ty * z.YT, z.YO);
+  T->y1 = (int32_t)std::min<int64_t>(z.YTO + (int64_t)(ty + 1) * z.YT, z.Y);
   (void)ntx;
   T->mct = (z.C == 3 && P.cod[0].mct) ? 1 : 0;
   for (int c = 0; c < z.C; c++) {
@@ -783,6 +788,7 @@ bool decode_host(const uint8_t* d, size_t n, const char* name, Image* img,
       }
       Tile& T = img->tiles[(size_t)t];
       tile_geometry(z, t % ntx, t / ntx, ntx, P, &T);
+      if (T.x1 <= T.x0 || T.y1 <= T.y0) return jfail(name, "empty tile");
       for (int c = 0; c < z.C; c++) {
         T.tc[c].off = total;
         total += (int64_t)(T.tc[c].x1 - T.tc[c].x0) * (T.tc[c].y1 - T.tc[c].y0);

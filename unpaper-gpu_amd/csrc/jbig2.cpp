@@ -255,14 +255,16 @@ bool generic_decode(Mq& mq, const GenericParams& gp, uint8_t* gb, Bitmap* bm) {
 
 size_t gb_contexts(int tmpl) { return tmpl == 0 ? 65536 : tmpl == 1 ? 8192 : 1024; }
 
-// 6.3.6 combination of a bitmap onto another at (x, y)
-void compose(Bitmap* dst, const Bitmap& src, int64_t x, int64_t y, int op) {
-  for (int32_t r = 0; r < src.h; r++) {
+// 6.3.6 combination of a bitmap onto another at (x, y); only the rows and
+// columns inside dst are walked.  Returns the number of pixels combined.
+int64_t compose(Bitmap* dst, const Bitmap& src, int64_t x, int64_t y, int op) {
+  const int64_t r0 = std::max<int64_t>(0, -y), r1 = std::min<int64_t>(src.h, (int64_t)dst->h - y);
+  const int64_t x0 = std::max<int64_t>(0, -x), x1 = std::min<int64_t>(src.w, (int64_t)dst->w - x);
+  if (r1 <= r0 || x1 <= x0) return 0;
+  for (int64_t r = r0; r < r1; r++) {
     const int64_t ty = y + r;
-    if (ty < 0 || ty >= dst->h) continue;
-    const uint8_t* s = src.row(r);
+    const uint8_t* s = src.row((int32_t)r);
     uint8_t* d = dst->row((int32_t)ty);
-    const int64_t x0 = std::max<int64_t>(0, -x), x1 = std::min<int64_t>(src.w, (int64_t)dst->w - x);
     for (int64_t c = x0; c < x1; c++) {
       uint8_t& o = d[x + c];
       const uint8_t v = s[c];
@@ -275,6 +277,7 @@ void compose(Bitmap* dst, const Bitmap& src, int64_t x, int64_t y, int op) {
       }
     }
   }
+  return (r1 - r0) * (x1 - x0);
 }
 
 struct Segment {
@@ -557,6 +560,8 @@ struct Decoder {
     if (!iadt.decode(mq, &v)) return fail("jbig2: %s: bad strip", name);
     int64_t stript = -(int64_t)v * strips, firsts = 0;
     uint32_t n = 0;
+    int64_t placed = 0;
+    const int64_t place_cap = 16 * (int64_t)w * h + ((int64_t)1 << 24);
     while (n < ninst) {
       if (!iadt.decode(mq, &v)) return fail("jbig2: %s: bad strip", name);
       stript += (int64_t)v * strips;
@@ -593,7 +598,12 @@ struct Decoder {
           px = (corner == 2 || corner == 3) ? t - wi + 1 : t;
           py = (corner == 0 || corner == 2) ? si - hi + 1 : si;
         }
-        compose(&bm, ib, px, py, combop);
+        // instances are bounded by the region, not their total: a crafted
+        // stream could stack millions of region-sized symbols
+        placed += compose(&bm, ib, px, py, combop);
+        if (placed > place_cap)
+          return fail("jbig2: %s: text region places %lld pixels into %dx%d", name, (long long)placed,
+                      w, h);
         if (!transposed && (corner == 0 || corner == 1)) curs += wi - 1;
         if (transposed && (corner == 1 || corner == 3)) curs += hi - 1;
         n++;

@@ -455,13 +455,15 @@ __device__ __forceinline__ void blur_rect_origin(const BlurGeom& g, int32_t r, i
   }
 }
 
-#ifndef UPH_BLUR_V16
-#define UPH_BLUR_V16 1  // 16-byte loads, 16 columns a lane (0: 4-byte loads; A/B 146.5 -> 140.6 us a launch)
-#endif
 // k_blur_counts for a gray plane: one workgroup per row of rectangles (the
 // first row at y = 0, row t at step_y + t*sh).  Lanes count dark pixels
 // (gray <= white) of aligned dwords over the strip's rows into per-column
 // 16-bit totals in LDS, then one lane per rectangle adds its sw columns.
+// V16: 16-byte loads, 16 columns a lane (A/B 146.5 -> 140.6 us a launch
+// against 4-byte loads); the host takes it only for planes whose bases,
+// stride and pitch are 16-byte aligned with pitch >= round16(W), so the last
+// vector of a row stays inside the row.
+template <bool V16>
 __global__ void __launch_bounds__(256) k_blur_counts_g(PlaneRef img, BlurGeom g, uint8_t* scratch,
                                                        int64_t sstride, const int32_t* active) {
   const int s = blockIdx.y;
@@ -471,10 +473,8 @@ __global__ void __launch_bounds__(256) k_blur_counts_g(PlaneRef img, BlurGeom g,
   const int32_t y0 = imax(ry, 0), y1 = imin(ry + g.sh, g.H);  // [y0, y1)
   const uint8_t* base = plane_ptr(img, s);
   extern __shared__ uint16_t ccount[];
-#if UPH_BLUR_V16
-  // 16-byte loads (rows are 256-byte pitched, so a vector past W stays in
-  // the row): a lane counts 16 columns, 8 rows' loads in flight
-  const int32_t nv = (g.W + 15) >> 4;
+  // V16: a lane counts 16 columns, 8 rows' loads in flight
+  const int32_t nv = V16 ? (g.W + 15) >> 4 : 0;
   for (int32_t vi = threadIdx.x; vi < nv; vi += 256) {
     uint32_t c[16];
 #pragma unroll
@@ -498,9 +498,8 @@ __global__ void __launch_bounds__(256) k_blur_counts_g(PlaneRef img, BlurGeom g,
     for (int j = 0; j < 16; j++)
       if (16 * vi + j < g.W) ccount[16 * vi + j] = (uint16_t)c[j];
   }
-  if (false)
-#endif
-  for (int32_t d = threadIdx.x; d < ((g.W + 3) >> 2); d += 256) {
+  const int32_t nd = V16 ? 0 : (g.W + 3) >> 2;
+  for (int32_t d = threadIdx.x; d < nd; d += 256) {
     uint32_t c[4] = {0, 0, 0, 0};
     for (int32_t y = y0; y < y1; y += 8) {
       uint32_t v[8];
@@ -979,8 +978,14 @@ __global__ void __launch_bounds__(256) k_blur_wipe(PlaneRef img, BlurGeom g, uin
 template <int FMT>
 static void launch_blur_t(const PlaneRef& img, const BlurGeom& g, uint8_t* scr, int64_t ss,
                           const int32_t* active, int count, hipStream_t st) {
-  if (g.nrect > 0 && FMT == F_GRAY8 && g.sh <= 65535 && g.W <= (1 << 16))
-    UPH_LAUNCH_DIAG(64, k_blur_counts_g, dim3(1 + g.T, count), dim3(256),
+  const auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  const bool v16 = img.P.pitch % 16 == 0 && img.P.stride % 16 == 0 && img.P.pitch >= ((g.W + 15) & ~15) &&
+                   a16(img.P.base[0]) && a16(img.P.base[1]);
+  if (g.nrect > 0 && FMT == F_GRAY8 && g.sh <= 65535 && g.W <= (1 << 16) && v16)
+    UPH_LAUNCH_DIAG(64, k_blur_counts_g<true>, dim3(1 + g.T, count), dim3(256),
+                    2 * (size_t)((g.W + 3) & ~3), st, img, g, scr, ss, active);
+  else if (g.nrect > 0 && FMT == F_GRAY8 && g.sh <= 65535 && g.W <= (1 << 16))
+    UPH_LAUNCH_DIAG(64, k_blur_counts_g<false>, dim3(1 + g.T, count), dim3(256),
                     2 * (size_t)((g.W + 3) & ~3), st, img, g, scr, ss, active);
   else if (g.nrect > 0)
     hipLaunchKernelGGL(k_blur_counts<FMT>, dim3(g.nrect, count), dim3(256), 0, st, img, g, scr, ss,
@@ -2144,10 +2149,14 @@ __device__ void noise_resolve_components(const uint32_t* keys, uint32_t* aux, in
 constexpr int kCompCap = 16384;  // triggers the component replay keeps in LDS
 static_assert(kCompCap == 16384, "noise_scratch_bytes reserves 3 x 16384 words for k_noise_group");
 constexpr int kResolveThreads = 1024;
-#ifndef UPH_REPLAY_BLOCKS
-#define UPH_REPLAY_BLOCKS 4
-#endif
-constexpr int kReplayBlocks = UPH_REPLAY_BLOCKS;  // k_noise_replay blocks per sheet
+// k_noise_replay blocks per sheet: enough that a lone sheet's components
+// spread over the chip (C2/C4 latency: up to kCompCap threads a sheet), few
+// enough that a 64-sheet batch is not mostly blocks that exit (C3): about one
+// block a CU over the launch, clamped to [4, kCompCap / 256].
+static int replay_blocks(int count) {
+  const int per = (256 + count - 1) / (count > 0 ? count : 1);
+  return per < 4 ? 4 : per > kCompCap / 256 ? kCompCap / 256 : per;
+}
 
 // The component replay in two kernels for intensity N <= 4 and at most
 // kCompCap triggers: k_noise_group (a block per sheet) orders the triggers
@@ -2516,7 +2525,7 @@ static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr
   if (!(diag_skip() & 2)) {
     hipLaunchKernelGGL(k_noise_group, dim3(count), dim3(1024), kGroupLds, st, g, scr, ss, active, ctl,
                        sortbuf, sort_stride);
-    hipLaunchKernelGGL(k_noise_replay<FMT>, dim3(kReplayBlocks, count), dim3(256), 0, st, img, g,
+    hipLaunchKernelGGL(k_noise_replay<FMT>, dim3(replay_blocks(count), count), dim3(256), 0, st, img, g,
                        scr, ss, active, sortbuf, sort_stride);
     hipLaunchKernelGGL(k_noise_resolve<FMT>, dim3(count), dim3(kResolveThreads), kResolveLds, st, img,
                        gd, scr, ss, active, ctl, sortbuf, sort_stride);

@@ -1194,7 +1194,8 @@ bool Document::extract_image(int page, PageImage* out) {
                 name_.c_str(), page);
   // the largest image, first one on ties (pdf_reader.c:311-333)
   const Obj* best = nullptr;
-  int64_t best_area = 0, best_num = 0;
+  double best_area = 0;  // in double: /Width and /Height may be any number
+  int64_t best_num = 0;
   for (const auto& kv : xo->d) {
     const Obj* o = resolve(&kv.second);
     if (!o || o->t != T::Stream) continue;
@@ -1203,7 +1204,7 @@ bool Document::extract_image(int page, PageImage* out) {
     const Obj* w = resolve(o->get("Width"));
     const Obj* h = resolve(o->get("Height"));
     if (!w || !h || !w->is_num() || !h->is_num()) continue;
-    const int64_t area = (int64_t)w->num() * (int64_t)h->num();
+    const double area = std::trunc(w->num()) * std::trunc(h->num());
     if (area > best_area) {
       best = o;
       best_area = area;
