@@ -67,6 +67,7 @@ W, H = A4_W, A4_H
 HBM_PEAK_GBS = 8000.0                   # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 ALG_BYTES_PER_PAGE = 10 * W * H         # SURVEY.md §8(d) fixed credit (86 998 400 B)
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+NDISTINCT = 64                          # distinct input files of the codec / PDF legs
 
 # Algorithmic HBM bytes per page of each timed stage (DESIGN.md "Kernels"):
 # the bytes the stage must move at minimum, in units of one W*H plane.
@@ -191,6 +192,24 @@ def load_hashes(name, key):
             return json.load(f).get(key, {})
     except (OSError, ValueError):
         return {}
+
+
+def note(msg):
+    """A progress line on stderr (long legs print one a phase, so a watcher
+    sees the run alive)."""
+    print("bench.py: %s" % msg, file=sys.stderr, flush=True)
+
+
+def sha_rows(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def pmap(fn, items, threads):
+    """fn over items on a thread pool (hashlib, PIL and numpy release the GIL
+    on large buffers); results in order."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max(1, min(16, threads))) as ex:
+        return list(ex.map(fn, items))
 
 
 def verify_resident(runner, devices, firsts, npages, bsz, hashes):
@@ -338,18 +357,33 @@ def host_io(opts, dev0, host_in, npages, args, threads):
             if failed:
                 raise UnpaperHipError("host-fed run: %d failed: %s" % (failed, err))
         st = r.stats()
+        # every page of the timed pass against the oracle's hashes
         hashes = load_hashes("bench_hashes.json", "pages")
-        sample = [p for p in range(min(npages, 32)) if str(p) in hashes]
-        ok = sum(hashlib.sha256(np.ascontiguousarray(host_out[p][:, :W]).tobytes()).hexdigest()
-                 == hashes[str(p)] for p in sample)
-        if ok != len(sample):
+        sample = [p for p in range(npages) if str(p) in hashes]
+        got = pmap(lambda p: sha_rows(host_out[p][:, :W]), sample, threads)
+        bad = sum(g != hashes[str(p)] for g, p in zip(got, sample))
+        if bad:
             raise SystemExit("bench.py: host-fed outputs differ from the oracle (%d of %d)"
-                             % (len(sample) - ok, len(sample)))
+                             % (bad, len(sample)))
         out["h2d_d2h"] = {"value": round(npages / t, 2), "unit": "pages/s",
                           "load_s": round(st.load_s, 3), "store_s": round(st.store_s, 3),
                           "verified": len(sample)}
-        keep = [np.ascontiguousarray(host_out[p][:, :W]) for p in sample[:2]]
-        del host_out, snk
+        del snk
+        verified_pages = set(sample)
+
+        def per_chunk_check(snk, n, check):
+            """Re-run the first n pages in chunks of 64 (file names wrap every
+            64 pages, so after a chunk file i holds page k + i) and check
+            every file; untimed, after the timed passes."""
+            done = 0
+            for k in range(0, n, 64):
+                m = min(64, n - k)
+                src_k = source_memory(host_in[k:].ctypes.data, W, W * H, m, keep=host_in)
+                failed, err = r.run_host(m, src_k, snk)
+                if failed:
+                    raise UnpaperHipError("check run: %d failed: %s" % (failed, err))
+                done += sum(pmap(lambda i: check(k + i, i), range(m), threads))
+            return done
         tmpdir = tempfile.mkdtemp(prefix="uphip_bench_",
                                   dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
         try:
@@ -361,6 +395,7 @@ def host_io(opts, dev0, host_in, npages, args, threads):
                 if failed:
                     raise UnpaperHipError("PNM run: %d failed: %s" % (failed, err))
             st = r.stats()
+            note("host-fed: PNM written; JPEG sink")
             out["pnm_write"] = {"value": round(npages / t, 2), "unit": "pages/s",
                                 "load_s": round(st.load_s, 3), "store_s": round(st.store_s, 3),
                                 "files": "PGM (P5) into tmpfs, 64 names reused"}
@@ -374,21 +409,19 @@ def host_io(opts, dev0, host_in, npages, args, threads):
                 if failed:
                     raise UnpaperHipError("JPEG run: %d failed: %s" % (failed, err))
             st = r.stats()
-            # files equal libjpeg-turbo's (PIL) encode of the oracle-verified
-            # sheets: names wrap every 64 pages, so an untimed pass over the
-            # first 64 leaves file p holding page p
-            failed, err = r.run_host(min(npages, 64), src, snk)
-            if failed:
-                raise UnpaperHipError("JPEG check run: %d failed: %s" % (failed, err))
-            import io
+            # every page's file equals libjpeg-turbo's (PIL) encode of that
+            # page's oracle-verified sheet
             from PIL import Image
-            same = 0
-            for i, sheet in enumerate(keep):
+
+            def jpeg_same(p, i):
+                if p not in verified_pages:
+                    return 0
                 b = io.BytesIO()
-                Image.fromarray(sheet).save(b, "JPEG", quality=85)
-                with open(os.path.join(tmpdir, "out_%04d.jpg" % sample[i]), "rb") as f:
-                    same += f.read() == b.getvalue()
-            if same != len(keep):
+                Image.fromarray(np.ascontiguousarray(host_out[p][:, :W])).save(b, "JPEG", quality=85)
+                with open(os.path.join(tmpdir, "out_%04d.jpg" % i), "rb") as f:
+                    return int(f.read() == b.getvalue())
+            same = per_chunk_check(snk, npages, jpeg_same)
+            if same != len([p for p in range(npages) if p in verified_pages]):
                 raise SystemExit("bench.py: JPEG files differ from PIL's encode of the sheets")
             kb = os.path.getsize(os.path.join(tmpdir, "out_0000.jpg")) / 1e3
             out["jpeg_write"] = {"value": round(npages / t, 2), "unit": "pages/s",
@@ -400,6 +433,7 @@ def host_io(opts, dev0, host_in, npages, args, threads):
             # transforms and code-blocks on the device per output page (the
             # store tasks), packets on the host; files decode (PIL) to the
             # oracle-verified sheets
+            note("host-fed: JPEG files checked (%d); JP2 sink" % same)
             nj = min(npages, 256)
             snk = sink_jp2(os.path.join(tmpdir, "out_%04lld.jp2"), 64)
             for rep in range(2):
@@ -409,14 +443,14 @@ def host_io(opts, dev0, host_in, npages, args, threads):
                 if failed:
                     raise UnpaperHipError("JP2 run: %d failed: %s" % (failed, err))
             st = r.stats()
-            failed, err = r.run_host(min(nj, 64), src, snk)  # file p holds page p again
-            if failed:
-                raise UnpaperHipError("JP2 check run: %d failed: %s" % (failed, err))
-            same = 0
-            for i, sheet in enumerate(keep):
-                back = np.asarray(Image.open(os.path.join(tmpdir, "out_%04d.jp2" % sample[i])))
-                same += bool(np.array_equal(back, sheet))
-            if same != len(keep):
+
+            def jp2_same(p, i):  # every file decodes (OpenJPEG) to its verified sheet
+                if p not in verified_pages:
+                    return 0
+                back = np.asarray(Image.open(os.path.join(tmpdir, "out_%04d.jp2" % i)))
+                return int(np.array_equal(back, host_out[p][:, :W]))
+            same = per_chunk_check(snk, nj, jp2_same)
+            if same != len([p for p in range(nj) if p in verified_pages]):
                 raise SystemExit("bench.py: JP2 files do not decode to the sheets")
             kb = os.path.getsize(os.path.join(tmpdir, "out_0000.jp2")) / 1e3
             out["jp2_write"] = {"value": round(nj / t, 2), "unit": "pages/s",
@@ -426,6 +460,7 @@ def host_io(opts, dev0, host_in, npages, args, threads):
                                 "verified": same}
         finally:
             shutil.rmtree(tmpdir, ignore_errors=True)
+            del host_out
         out["config"] = {"sheets_per_batch": args.host_batch, "streams": args.host_streams,
                          "host_threads": threads, "staging": "pinned, per batch, in + out",
                          "source": "pages in host RAM (decoded)"}
@@ -481,8 +516,10 @@ def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid, codec="jpeg"):
     Huffman decode of every page of a chunk in one set of launches, then the
     IDCT into the batch's input slots, on the device), the default pipeline,
     sheets discarded.  PCIe- and host-inclusive: a figure of its own, never `value`
-    of the C3 line.  Two pages' outputs are checked against the oracle on
-    PIL's decode of the same files.  codec "jp2": the same pages saved
+    of the C3 line.  64 distinct input files; the sheets come back into host
+    RAM and every page is checked against the oracle's hash of its decoded
+    input (tests/golden/codec_hashes.json for JPEG, bench_hashes.json for the
+    lossless JPEG 2000 files).  codec "jp2": the same pages saved
     losslessly as JPEG 2000 (OpenJPEG's defaults), headers and packet headers
     parsed on the load pool, every code-block of a chunk decoded on the
     device in one launch, then the wavelet into the input slots."""
@@ -493,7 +530,7 @@ def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid, codec="jpeg"):
     tmpdir = tempfile.mkdtemp(prefix="uphip_jpeg_",
                               dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
     try:
-        # 16 distinct pages, reused round robin (the decode cost does not
+        # 64 distinct pages, reused round robin (the decode cost does not
         # depend on the name)
         def make(i):
             g = np.empty((H, W), np.uint8)
@@ -506,9 +543,9 @@ def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid, codec="jpeg"):
                 Image.fromarray(g).save(path, "JPEG", quality=95)
             return path
         with ThreadPoolExecutor(min(16, threads)) as ex:
-            uniq = list(ex.map(make, range(16)))
-        paths = [uniq[i % 16] for i in range(n)]
-        mb = sum(os.path.getsize(p) for p in uniq) / 16 / 1e6
+            uniq = list(ex.map(make, range(NDISTINCT)))
+        paths = [uniq[i % NDISTINCT] for i in range(n)]
+        mb = sum(os.path.getsize(p) for p in uniq) / NDISTINCT / 1e6
         opts = A.Options()
         L.uphip_options_init(C.byref(opts))
         # batches in flight: JPEG 2000 chunks wait on their one code-block
@@ -518,11 +555,15 @@ def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid, codec="jpeg"):
         r = Runner(opts, args.host_batch, W, H, A.FMT_GRAY8, devices=devices[:1], streams=streams,
                    host_threads=threads)
         try:
-            outs = os.path.join(tmpdir, "o%02d.pgm")
+            # the sheets come back into host RAM (registered, DMA'd straight
+            # into place), so every output page of the timed pass is checked
+            host_out = np.empty((n, H, r.out_linesize), np.uint8)
+            snk = sink_memory(host_out.ctypes.data, r.out_linesize, r.out_linesize * H, n,
+                              keep=host_out)
+            src = source_pnm(paths)
             for rep in range(2):  # one warm-up pass (pinned buffers grow once)
                 t0 = time.perf_counter()
-                failed, err = r.run_host(n, source_pnm(paths), sink_pnm(outs, 16) if rep == 0 else
-                                         sink_discard())
+                failed, err = r.run_host(n, src, snk)
                 t = time.perf_counter() - t0
                 if failed:
                     raise UnpaperHipError("%s run: %d failed: %s" % (codec, failed, err))
@@ -531,21 +572,23 @@ def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid, codec="jpeg"):
             r.close()
         checked = 0
         if not args.no_verify:
-            sys.path.insert(0, os.path.join(ROOT, "oracle"))
-            from oracle_py import Oracle
-            from unpaper_hip.hostimage import HostImage
-            from unpaper_hip.pipeline import pnm_read
-            oracle = Oracle()
-            oo = oracle.default_options()
-            for i in range(2):
-                px = np.asarray(Image.open(uniq[i]))
-                sheet, fmt, _ = oracle.process_sheet(oo, [HostImage.from_array(px.copy(),
-                                                                                A.FMT_GRAY8)])
-                exp = oracle.convert_for_save(sheet, fmt)
-                got = pnm_read(outs % i)
-                if not np.array_equal(got.payload(), exp.payload()):
-                    raise SystemExit("bench.py: %s page %d differs from the oracle" % (codec, i))
-                checked += 1
+            # the oracle's hashes of the decoded inputs' cleaned sheets: JPEG
+            # from tests/golden/codec_hashes.json (PIL's decode of the same
+            # files), lossless JPEG 2000 = the synthetic pages themselves
+            if codec == "jp2":
+                hs = load_hashes("bench_hashes.json", "pages")
+                exp = [hs[str(firsts[0] + i)] for i in range(NDISTINCT)]
+            else:
+                if firsts[0] != 0:
+                    raise SystemExit("bench.py: JPEG hashes exist for rank 0's pages only")
+                hs = load_hashes("codec_hashes.json", "jpeg_q95")
+                exp = [hs[str(i)] for i in range(NDISTINCT)]
+            got = pmap(lambda i: sha_rows(host_out[i][:, :W]), range(n), threads)
+            bad = [i for i in range(n) if got[i] != exp[i % NDISTINCT]]
+            if bad:
+                raise SystemExit("bench.py: %s pages %s differ from the oracle" % (codec, bad[:8]))
+            checked = n
+        del host_out, snk
     finally:
         shutil.rmtree(tmpdir, ignore_errors=True)
     what = ("JPEG 2000 files through the runner (JPEG 2000 decode peer)" if codec == "jp2" else
@@ -556,8 +599,9 @@ def run_jpeg(args, L, d, devices, firsts, n_gpus, version, valid, codec="jpeg"):
             "dtype": "u8", "data": "synthetic (%s, %.2f MB a page)" % (made, mb),
             "host_threads": threads, "load_s": round(st.load_s, 3),
             "config": {"pages": n, "sheets_per_batch": args.host_batch, "streams": streams,
-                       "source": "%s files in tmpfs (16 distinct, round robin)" % codec.upper(),
-                       "sink": "discarded"},
+                       "source": "%s files in tmpfs (%d distinct, round robin)"
+                                 % (codec.upper(), NDISTINCT),
+                       "sink": "host RAM (registered memory sink), every page hashed"},
             "verified": checked, "library": version, "valid": valid}
 
 
@@ -571,8 +615,10 @@ def run_pdf(args, L, d, devices, firsts, n_gpus, version, valid):
         generic regions;
       * a PDF of 512 A4 JPEG pages (quality 95) written by our writer.
     File-to-file, host-inclusive: figures of their own, never `value` of the
-    C3 line.  Two pages of each leg are checked against the oracle run on
-    the decoded page (our JBIG2 decode / PIL's JPEG decode)."""
+    C3 line.  Every page of each leg is checked: the sheets of an untimed
+    pass against the oracle's hashes of the decoded pages (our JBIG2 decode /
+    PIL's JPEG decode, tests/golden/codec_hashes.json), and every page of the
+    timed pass's output PDF against PIL's quality-85 encode of its sheet."""
     from PIL import Image
     from concurrent.futures import ThreadPoolExecutor
     from unpaper_hip import pdf as P
@@ -592,10 +638,10 @@ def run_pdf(args, L, d, devices, firsts, n_gpus, version, valid):
             Image.fromarray(g).save(b, "JPEG", quality=95)
             return b.getvalue()
         with ThreadPoolExecutor(min(16, threads)) as ex:
-            uniq = list(ex.map(make, range(16)))
+            uniq = list(ex.map(make, range(NDISTINCT)))
         w = P.PdfWriter.create(jpg_pdf, {"title": "bench"}, 300)
         for i in range(n_jpeg):
-            w.add_page_jpeg(uniq[i % 16], W, H)
+            w.add_page_jpeg(uniq[i % NDISTINCT], W, H)
         w.close()
         opts = A.Options()
         L.uphip_options_init(C.byref(opts))
@@ -626,28 +672,44 @@ def run_pdf(args, L, d, devices, firsts, n_gpus, version, valid):
                     raise SystemExit("bench.py: pdf %s wrote %d pages of %d" % (name, d_out.page_count, n))
                 checked = 0
                 if not args.no_verify:
-                    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-                    from oracle_py import Oracle
-                    from unpaper_hip.hostimage import HostImage
-                    from unpaper_hip.pipeline import pnm_read
-                    oracle = Oracle()
-                    oo = oracle.default_options()
-                    d_in = P.PdfDocument.open(path)
-                    pnm = os.path.join(tmpdir, "v%02d.pgm")
-                    failed, err = r.run_host(2, src, sink_pnm(pnm))
+                    # every page: (1) an untimed pass into host RAM, each sheet
+                    # against the oracle's hash of its decoded input
+                    # (tests/golden/codec_hashes.json: our JBIG2 decode /
+                    # PIL's JPEG decode); (2) every JPEG page of the timed
+                    # pass's output PDF equals PIL's (libjpeg-turbo) quality-85
+                    # encode of its verified sheet
+                    if name == "jbig2_50":
+                        hs = load_hashes("codec_hashes.json", "jbig2_50")
+                        exp = [hs[str(i)] for i in range(n)]
+                    else:
+                        hs = load_hashes("codec_hashes.json", "jpeg_q95")
+                        exp = [hs[str(i % NDISTINCT)] for i in range(n)]
+                    host_out = np.empty((n, H, r.out_linesize), np.uint8)
+                    snk = sink_memory(host_out.ctypes.data, r.out_linesize, r.out_linesize * H, n,
+                                      keep=host_out)
+                    failed, err = r.run_host(n, src, snk)
                     if failed:
                         raise UnpaperHipError("pdf %s check run: %s" % (name, err))
-                    for i in range(2):
-                        im = d_in.extract_page_image(i)
-                        if im.format == P.IMAGE_JPEG:
-                            px = np.asarray(Image.open(io.BytesIO(im.data)))
-                        else:  # the host JBIG2 decode (the reference's jbig2dec step)
-                            px = d_in.read_page(i).data[:, :W].copy()
-                        sheet, fmt, _ = oracle.process_sheet(oo, [HostImage.from_array(px, A.FMT_GRAY8)])
-                        exp = oracle.convert_for_save(sheet, fmt)
-                        if not np.array_equal(pnm_read(pnm % i).payload(), exp.payload()):
-                            raise SystemExit("bench.py: pdf %s page %d differs from the oracle" % (name, i))
-                        checked += 1
+                    got = pmap(lambda i: sha_rows(host_out[i][:, :W]), range(n), threads)
+                    bad = [i for i in range(n) if got[i] != exp[i]]
+                    if bad:
+                        raise SystemExit("bench.py: pdf %s pages %s differ from the oracle" % (name, bad[:8]))
+
+                    tls = threading.local()
+
+                    def page_same(i):
+                        b = io.BytesIO()
+                        Image.fromarray(np.ascontiguousarray(host_out[i][:, :W])).save(b, "JPEG", quality=85)
+                        if not hasattr(tls, "doc"):
+                            tls.doc = P.PdfDocument.open(out)
+                        im = tls.doc.extract_page_image(i)
+                        return int(im.format == P.IMAGE_JPEG and bytes(im.data) == b.getvalue())
+                    same = sum(pmap(page_same, range(n), threads))
+                    if same != n:
+                        raise SystemExit("bench.py: pdf %s: %d of %d output pages differ from PIL's "
+                                         "encode of the verified sheets" % (name, n - same, n))
+                    checked = n
+                    del host_out, snk
                 legs[name] = {"pages": n, "pages_per_s": round(n / best, 2), "s": round(best, 3),
                               "load_s": round(st.load_s, 3), "store_s": round(st.store_s, 3),
                               "in_mb": round(os.path.getsize(path) / 1e6, 3),
@@ -891,6 +953,7 @@ def main():
     single = d.world == 1 and len(devices) == 1
     c4 = None
     if single and not args.no_c4:
+        note("C3 done (%.0f pages/s); C4" % pages_per_s)
         # BASELINE configs[3] measured and verified in every default run: the
         # 16-sheet C4 workload, 1 warm-up + 3 timed passes
         c4 = run_c4(args, L, d, devices, [0], 1, version, valid, nsheets=16, steps=3, warmup=1,
@@ -902,19 +965,37 @@ def main():
     if single and not (args.no_host_io and args.no_cpu and args.no_latency):
         host_pages = device_pages_to_host(L, bufs[0], pitch, stride, npages, W, H)
     if single and not args.no_latency:
+        note("C2 latency")
         dev_ms, host_ms, stages = latency_c2(L, opts, host_pages[0], bufs[0].ptr, pitch, stride)
         latency = {"device_ms": dev_ms, "with_pcie_ms": host_ms,
                    "what": "one A4 GRAY8 page alone, idle GPU, median of 7 (C2)",
                    "stages_ms": stages}
     if single and not args.no_host_io:
+        note("host-fed figures")
         hio = host_io(opts, devices[0], host_pages, npages, args, threads)
     if single and not args.no_cpu:
-        n = min(args.cpu_pages or 8 * threads, npages)
+        note("CPU baseline")
+        n = min(args.cpu_pages or 4 * threads, npages)
         v = cpu_baseline(host_pages, n, threads)
+        n1 = min(3, npages)
+        v1 = cpu_baseline(host_pages, n1, 1)
+        # The reference's own --batch default is min(nproc, 64) worker
+        # threads (lib/batch.c:72-83).  The box allots this job its CPU share
+        # (OMP_NUM_THREADS), so the whole-host figure is the measured
+        # one-thread rate times that thread count, with the measured scaling
+        # of the share beside it.
+        ref_threads = min(os.cpu_count() or 1, 64)
         cpu = {"value": round(v, 3), "unit": "pages/s", "cores": threads, "kind": "port",
                "host_cpus": os.cpu_count(),
                "sample": "%d synthetic A4 GRAY8 pages (the first of the GPU workload), default "
-                         "options, oracle/oracle.c on %d host threads" % (n, threads)}
+                         "options, oracle/oracle.c on %d host threads" % (n, threads),
+               "one_thread": {"value": round(v1, 4), "cores": 1, "sample": "%d pages" % n1},
+               "share_scaling": round(v / max(v1 * threads, 1e-9), 3),
+               "whole_host": {"value": round(v1 * ref_threads, 2), "unit": "pages/s",
+                              "cores": ref_threads, "kind": "port, extrapolated",
+                              "how": "one-thread rate x min(nproc, 64) threads, the reference's "
+                                     "batch default (lib/batch.c:72-83); not run at that width "
+                                     "because the box allots this job %d CPUs" % threads}}
     for b in bufs:
         b.close()
     if d.rank == 0:

@@ -215,6 +215,27 @@ static void j2k(const char *fixtures) {
         uphip_clear_error();
       }
     }
+    /* crafted SIZ: huge tiles and offsets (XO = XTO = 10, XT = YT = INT_MAX;
+     * then XT = 0x80000000, read as a negative int32): the tile bounds must
+     * not overflow */
+    for (size_t q = 0; q + 40 < n; q++) {
+      if (raw[q] != 0xFF || raw[q + 1] != 0x51) continue;
+      static const uint32_t xt[] = {0x7FFFFFFFu, 0x80000000u, 0xFFFFFFFFu};
+      for (int v = 0; v < 3; v++) {
+        memcpy(tmp, raw, n);
+        uint8_t *z = tmp + q + 6; /* X, Y, XO, YO, XT, YT, XTO, YTO (big-endian u32) */
+        const uint32_t vals[8] = {0, 0, 10, 10, xt[v], xt[v], 10, 10};
+        for (int k = 2; k < 8; k++) {
+          z[4 * k] = (uint8_t)(vals[k] >> 24);
+          z[4 * k + 1] = (uint8_t)(vals[k] >> 16);
+          z[4 * k + 2] = (uint8_t)(vals[k] >> 8);
+          z[4 * k + 3] = (uint8_t)vals[k];
+        }
+        uphip_jp2_entropy_decode(tmp, n, NULL, 0, &info); /* fails or decodes; never UB */
+        uphip_clear_error();
+      }
+      break;
+    }
   }
 }
 

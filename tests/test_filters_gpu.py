@@ -111,6 +111,59 @@ def test_noisefilter_edge_quirk(hip, oracle):
          lambda o: oracle.noisefilter(o, 4, 229))
 
 
+def noisy_scan(w, h, page, specks, seed, quality=75, border=True, dashes=True):
+    """A synthetic page made to look like a poor scan: clustered 1-px specks
+    (sequentially resolved components), a ragged dark left border (the
+    edge zone; its interior is the no-op triggers k_noise_classify drops), a
+    dashed rule in the top zone (one row of several hundred triggers), all
+    through a JPEG round trip (compression noise)."""
+    import io
+    from PIL import Image
+    from unpaper_hip.pipeline import synth_page_host
+    g = synth_page_host(w, h, page).copy()
+    rng = np.random.default_rng(seed)
+    ys, xs = rng.integers(0, h, specks), rng.integers(0, w, specks)
+    g[ys, xs] = rng.integers(0, 120, specks)
+    if border:
+        edge = 20 + rng.integers(0, 12, h)
+        for y in range(h):
+            g[y, :edge[y]] = 30
+    if dashes:
+        g[3, 40::2] = 0
+        g[9, 100::3] = 10
+    b = io.BytesIO()
+    Image.fromarray(g).save(b, "JPEG", quality=quality)
+    return np.asarray(Image.open(io.BytesIO(b.getvalue()))).copy()
+
+
+@pytest.mark.parametrize("fmt", [A.FMT_GRAY8, A.FMT_RGB24])
+@pytest.mark.parametrize("specks,intensity", [(40000, 4), (40000, 2), (6000, 4), (6000, 3)])
+def test_noisefilter_group_caps(hip, oracle, fmt, specks, intensity):
+    # 40000 specks: more than 16384 sequential triggers (k_noise_group's
+    # global layout); 6000: within the LDS layout; both with rows of more than
+    # 256 triggers (the dashed rules: the block-wide bucket sort)
+    g = noisy_scan(1240, 1754, 3, specks, specks + intensity)
+    h = HostImage.from_array(np.repeat(g[:, :, None], 3, axis=2) if fmt == A.FMT_RGB24 else g, fmt)
+    both(hip, oracle, h, lambda d: hip.noisefilter(d, intensity, 229),
+         lambda o: oracle.noisefilter(o, intensity, 229))
+
+
+def test_noisefilter_border_quirk_strip(hip, oracle):
+    # a solid border band with thin spurs reaching into the quirk strip
+    # (x < 7, y < 6): the no-op trigger test must leave those in the sequence
+    g = np.full((300, 400), 255, np.uint8)
+    g[:, :25] = 0
+    g[:40, :] = 0
+    for y in range(45, 300, 7):
+        g[y, 25:25 + (y % 11)] = 0      # spurs off the band's edge
+        g[y + 1, 3] = 255               # notches inside the quirk strip
+    g[50:60, 0:2] = 255
+    g[2, 100:300:2] = 255
+    h = HostImage.from_array(g, A.FMT_GRAY8)
+    both(hip, oracle, h, lambda d: hip.noisefilter(d, 4, 229),
+         lambda o: oracle.noisefilter(o, 4, 229))
+
+
 # ---------------------------------------------------------------- grayfilter
 def test_grayfilter_reference_scene(hip, oracle):  # cuda_filters_test.c:296-331
     h = blank(8, 8, A.FMT_GRAY8, 50)

@@ -1717,7 +1717,15 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
         const bool trig = (trow[ry][rx >> 5] >> (rx & 31)) & 1;
         const bool zone = g.all_seq || gx < kZone || gy < kZone;
         const bool dark = (drow[ry][rx >> 5] >> (rx & 31)) & 1;
-        wave_append(cx < NTX && dark & zone & trig, gx, gy, NP.nseq, NP.seq, g.capacity);
+        // A trigger with >= 5 dark pixels in its 3x3 block, all outside the
+        // strip the quirk triggers can bite (x < 2N-1 or y < 2N-2, N <= 4),
+        // never clears: that block is connected and larger than N, so no
+        // clear ever removes a pixel of it (away from the strip a clear
+        // removes whole components of <= N pixels, see above), and its >= 4
+        // dark ring-1 pixels keep the trigger's count above N.  Such triggers
+        // are left out of the sequence (a dark border's interior).
+        const bool noop = !g.all_seq && gx >= 8 && gy >= 7 && ((l3[ry][rx >> 6] >> (rx & 63)) & 1);
+        wave_append(cx < NTX && dark & zone & trig & !noop, gx, gy, NP.nseq, NP.seq, g.capacity);
       }
     }
   }
@@ -2043,19 +2051,30 @@ __device__ __forceinline__ void replay_trigger4(int32_t x, int32_t y, int N, con
 }
 
 // Parallel union-find over the trigger indices (parents always point to a
-// smaller index, so the CAS links never form a cycle).
+// smaller index, so the CAS links never form a cycle).  GLOBAL: the parents
+// live in HBM and are read past the vector L1 (agent-scope atomic loads), so
+// a link another wave's CAS made in L2 is seen on the next read.
+template <bool GLOBAL = false>
+__device__ __forceinline__ uint32_t uf_load(const uint32_t* parent, uint32_t i) {
+  if constexpr (GLOBAL)
+    return __hip_atomic_load(parent + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    return parent[i];
+}
+template <bool GLOBAL = false>
 __device__ __forceinline__ uint32_t uf_find(const uint32_t* parent, uint32_t i) {
-  uint32_t p = parent[i];
+  uint32_t p = uf_load<GLOBAL>(parent, i);
   while (p != i) {
     i = p;
-    p = parent[i];
+    p = uf_load<GLOBAL>(parent, i);
   }
   return i;
 }
+template <bool GLOBAL = false>
 __device__ __forceinline__ void uf_union(uint32_t* parent, uint32_t a, uint32_t b) {
   for (;;) {
-    a = uf_find(parent, a);
-    b = uf_find(parent, b);
+    a = uf_find<GLOBAL>(parent, a);
+    b = uf_find<GLOBAL>(parent, b);
     if (a == b) return;
     if (a < b) {
       const uint32_t t = a;
@@ -2066,89 +2085,9 @@ __device__ __forceinline__ void uf_union(uint32_t* parent, uint32_t a, uint32_t 
   }
 }
 
-// The raster-order replay for intensity N <= 4, split by dependence: trigger
-// T reads pixels within Chebyshev N of itself and clears within N-1, so it can
-// only see the clears of triggers closer than 2N.  The triggers linked by that
-// relation form components that never touch each other's windows; each
-// component is replayed in raster order by one thread, all components at
-// once.  The result equals the single raster-order scan (filters.c:243-348).
-//   keys: the n trigger keys (y << 16 | x) sorted, p2 = pow2 >= n entries;
-//   aux:  p2 entries of scratch (parents, then (root << 16 | index) pairs).
-template <int FMT>
-__device__ void noise_resolve_components(const uint32_t* keys, uint32_t* aux, int n, int p2, int N,
-                                         const NoiseGeom& g, uint8_t* base, int64_t pitch
-#ifdef UPHIP_DIAG
-                                         , uint64_t* ph, int* maxrun
-#endif
-                                         ) {
-  const int R = 2 * N - 1;  // dependence radius
-  for (int i = threadIdx.x; i < n; i += blockDim.x) aux[i] = (uint32_t)i;
-  __syncthreads();
-  // link every trigger to the earlier ones within R: one binary search for
-  // the first trigger of row y-R in the sorted keys, then a scan of the
-  // band's earlier triggers (rows y-R .. y, raster order) for |dx| <= R
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const uint32_t key = keys[i];
-    const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
-    const uint32_t lo = (uint32_t)imax(y - R, 0) << 16;
-    int a = 0, b = i;  // first index in [0, i) with keys >= lo
-    while (a < b) {
-      const int mid = (a + b) >> 1;
-      if (keys[mid] < lo) a = mid + 1;
-      else b = mid;
-    }
-    for (int j = a; j < i; j++) {
-      const int32_t xj = (int32_t)(keys[j] & 0xFFFF);
-      if (xj >= x - R && xj <= x + R) uf_union(aux, (uint32_t)i, (uint32_t)j);
-    }
-  }
-  __syncthreads();
-#ifdef UPHIP_DIAG
-  ph[0] = wall_clock64();
-#endif
-  // flatten (a concurrent reader sees either an old parent or the root: both
-  // ancestors), then (root, index) pairs sorted so that each component's
-  // triggers are contiguous and in raster order
-  for (int i = threadIdx.x; i < n; i += blockDim.x) aux[i] = uf_find(aux, (uint32_t)i);
-  __syncthreads();
-  for (int i = threadIdx.x; i < p2; i += blockDim.x) aux[i] = i < n ? (aux[i] << 16) | (uint32_t)i : 0xFFFFFFFFu;
-  __threadfence_block();
-  __syncthreads();
-  block_sort(aux, p2);
-#ifdef UPHIP_DIAG
-  ph[1] = wall_clock64();
-  int run = 0;
-#endif
-  Mask81 rowp[5], colp[5];
-#pragma unroll
-  for (int L = 1; L <= 4; L++) {
-    rowp[L] = ring_part(L, true);
-    colp[L] = ring_part(L, false);
-  }
-  // thread t replays the components that start in its slice of the pairs
-  const int per = (n + (int)blockDim.x - 1) / (int)blockDim.x;
-  const int b0 = threadIdx.x * per, b1 = imin(b0 + per, n);
-  for (int c = b0; c < b1; c++) {
-    const uint32_t root = aux[c] >> 16;
-    if (c > 0 && (aux[c - 1] >> 16) == root) continue;  // not a component start
-    for (int m = c; m < n && (aux[m] >> 16) == root; m++) {
-      const uint32_t key = keys[aux[m] & 0xFFFFu];
-      __threadfence_block();  // this thread's earlier clears are visible to its loads
-      replay_trigger4<FMT>((int32_t)(key & 0xFFFF), (int32_t)(key >> 16), N, g, base, pitch, rowp,
-                           colp);
-#ifdef UPHIP_DIAG
-      run++;
-#endif
-    }
-  }
-#ifdef UPHIP_DIAG
-  *maxrun = run;
-#endif
-}
-
 constexpr int kCompCap = 16384;  // triggers the component replay keeps in LDS
 static_assert(kCompCap == 16384, "noise_scratch_bytes reserves 3 x 16384 words for k_noise_group");
-constexpr int kResolveThreads = 1024;
+constexpr int kGroupThreads = 1024;
 // k_noise_replay blocks per sheet: enough that a lone sheet's components
 // spread over the chip (C2/C4 latency: up to kCompCap threads a sheet), few
 // enough that a 64-sheet batch is not mostly blocks that exit (C3): about one
@@ -2158,22 +2097,38 @@ static int replay_blocks(int count) {
   return per < 4 ? 4 : per > kCompCap / 256 ? kCompCap / 256 : per;
 }
 
-// The component replay in two kernels for intensity N <= 4 and at most
-// kCompCap triggers: k_noise_group (a block per sheet) orders the triggers
-// in raster order by a counting sort over row buckets (then insertion sort
-// within a bucket), links those within 2N-1 by union-find and writes, per
-// trigger in raster order, its key, its component's root (the component's
-// first trigger) and, for a root, its component's last trigger;
-// k_noise_replay (many blocks per sheet) gives each component to one
-// thread, which replays its triggers in raster order.  The replay's
-// scattered box reads then spread over the chip instead of one CU's address
-// path.  The group kernel writes a flag (word 2 of the sheet's list header):
-// 1 when the two kernels handle the sheet, 0 when k_noise_resolve must.
+// The sequential part of the noisefilter (the triggers k_noise_classify could
+// not decide in parallel) for intensity N <= 4, in two kernels:
+// k_noise_group (a block per sheet) orders the triggers in raster order by a
+// counting sort over row buckets (then insertion sort within a bucket; a
+// bucket longer than kGroupBucketMax is bitonic-sorted by the whole block in
+// LDS), links those within 2N-1 by union-find and writes, per trigger in
+// raster order, its key, its component's root (the component's first
+// trigger) and, for a root, its component's last trigger; k_noise_replay
+// (many blocks per sheet) gives each component to one thread, which replays
+// its triggers in raster order.  The replay's scattered box reads then spread
+// over the chip instead of one CU's address path.  Where the arrays live is
+// the sheet's layout word (word 2 of its list header):
+//   kNoiseNothing  nothing left to replay (no trigger, or done in k_noise_group)
+//   kNoiseLds      n <= kCompCap: keys / roots / last at [0, C), [C, 2C),
+//                  [2C, 3C) of the sort buffer (C = kCompCap); the sort and
+//                  the links ran in LDS
+//   kNoiseBig      n > kCompCap: keys in the sort buffer, roots in the seq
+//                  list (free once its keys are scattered), last in the clear
+//                  list (free once k_noise_apply ran); the sort and the links
+//                  ran on those global arrays
+// Intensity > 4 (every trigger replayed: up to W*H of them) and a bucket of
+// more than kCompCap triggers take the literal raster scan by one wave inside
+// k_noise_group.  No separate resolver launch: a kernel asking for 128 KiB
+// of LDS waits for a nearly idle CU even when all its blocks would exit.
+constexpr uint32_t kNoiseNothing = 0, kNoiseLds = 1, kNoiseBig = 2;
 constexpr int kNoiseBuckets = 4096;
-constexpr int kGroupBucketMax = 256;  // longer buckets: k_noise_resolve's sort
-// keys, parents, bucket starts, the scan's wave sums, a flag (all dynamic:
-// allow_dynamic_lds raises the dynamic limit to the whole 160 KiB)
-constexpr size_t kGroupLds = sizeof(uint32_t) * (2 * (size_t)kCompCap + kNoiseBuckets + 1 + 16 + 1);
+constexpr int kGroupBucketMax = 256;  // longer buckets: block-wide bitonic sort
+constexpr int kLongList = 64;         // long buckets remembered by id (else: all scanned)
+// keys, parents, bucket starts, the scan's wave sums + 3 words, the long
+// bucket list (all dynamic: allow_dynamic_lds raises the limit to 160 KiB)
+constexpr size_t kGroupLds =
+    sizeof(uint32_t) * (2 * (size_t)kCompCap + kNoiseBuckets + 1 + 16 + 3 + kLongList);
 
 __device__ __forceinline__ int noise_bucket_shift(int32_t H) {
   int b = 0;
@@ -2181,221 +2136,27 @@ __device__ __forceinline__ int noise_bucket_shift(int32_t H) {
   return b;
 }
 
-__global__ void __launch_bounds__(1024) k_noise_group(NoiseGeom g, uint8_t* scratch, int64_t sstride,
-                                                      const int32_t* active, SheetCtl* ctl,
-                                                      uint32_t* sortbuf, int64_t sort_stride) {
-  const int s = blockIdx.x;
-  if (active && !active[s]) return;
-  NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
-  uint32_t* flag = NP.nclear + 2;
-  const uint32_t n = *NP.nseq;
-  const int N = g.intensity;
-  const int tid = threadIdx.x;
-  if (n == 0 || n > (uint32_t)kCompCap || N > 4) {
-    if (tid == 0) *flag = n == 0 ? 1u : 0u;
-    return;
-  }
-  uint32_t* gk = sortbuf + s * sort_stride;  // keys [0, C), roots [C, 2C), last [2C, 3C)
-  extern __shared__ uint32_t glds[];
-  uint32_t* keys = glds;
-  uint32_t* par = glds + kCompCap;
-  uint32_t* bc = glds + 2 * kCompCap;  // bucket starts (nb + 1)
-  uint32_t* wsum = bc + kNoiseBuckets + 1;
-  uint32_t& too_long = wsum[16];
-  const int b = noise_bucket_shift(g.H);
-  const int nb = ((g.H - 1) >> b) + 1;
-  const int R = 2 * N - 1;
-  if (tid == 0) too_long = 0u;
-  for (int i = tid; i <= nb; i += 1024) bc[i] = 0;
-  __syncthreads();
-  for (int i = tid; i < (int)n; i += 1024) atomicAdd(&bc[(NP.seq[i] >> 16) >> b], 1u);
-  __syncthreads();
-  // exclusive scan of the nb counts: 4 consecutive buckets a thread
-  {
-    const int b0 = 4 * tid;
-    uint32_t c[4], sum = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      c[k] = b0 + k < nb ? bc[b0 + k] : 0u;
-      sum += c[k];
-    }
-    if (c[0] > kGroupBucketMax || c[1] > kGroupBucketMax || c[2] > kGroupBucketMax ||
-        c[3] > kGroupBucketMax)
-      too_long = 1u;
-    // block exclusive scan of `sum`
-    uint32_t incl = sum;
-    const int lane = tid & 63, wv = tid >> 6;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = (uint32_t)__shfl_up((int)incl, o, 64);
-      if (lane >= o) incl += u;
-    }
-    if (lane == 63) wsum[wv] = incl;
-    __syncthreads();
-    uint32_t before = 0;
-    for (int k = 0; k < wv; k++) before += wsum[k];
-    uint32_t run = before + incl - sum;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      if (b0 + k < nb) {
-        bc[b0 + k] = run;
-        par[b0 + k] = run;  // scatter cursors
-      }
-      run += c[k];
-    }
-    if (tid == 0) bc[nb] = n;
-  }
-  __syncthreads();
-  if (too_long) {  // a dense stretch of triggers: the general resolver's sort
-    if (tid == 0) *flag = 0u;
-    return;
-  }
-  for (int i = tid; i < (int)n; i += 1024) {
-    const uint32_t key = NP.seq[i];
-    keys[atomicAdd(&par[(key >> 16) >> b], 1u)] = key;
-  }
-  __syncthreads();
-  for (int k = tid; k < nb; k += 1024) {  // raster order inside each bucket
-    const int lo = (int)bc[k], hi = (int)bc[k + 1];
-    for (int i = lo + 1; i < hi; i++) {
-      const uint32_t v = keys[i];
-      int j = i - 1;
-      while (j >= lo && keys[j] > v) {
-        keys[j + 1] = keys[j];
-        j--;
-      }
-      keys[j + 1] = v;
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < (int)n; i += 1024) par[i] = (uint32_t)i;
-  __syncthreads();
-  // link every trigger to the earlier ones within R (rows y-R .. y)
-  for (int i = tid; i < (int)n; i += 1024) {
-    const uint32_t key = keys[i];
-    const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
-    for (int j = (int)bc[imax(y - R, 0) >> b]; j < i; j++) {
-      const uint32_t kj = keys[j];
-      const int32_t xj = (int32_t)(kj & 0xFFFF), yj = (int32_t)(kj >> 16);
-      if (yj >= y - R && xj >= x - R && xj <= x + R) uf_union(par, (uint32_t)i, (uint32_t)j);
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < (int)n; i += 1024) {
-    gk[i] = keys[i];
-    gk[kCompCap + i] = uf_find(par, (uint32_t)i);
-  }
-  __syncthreads();
-  for (int i = tid; i < (int)n; i += 1024) keys[i] = 0u;
-  __syncthreads();
-  for (int i = tid; i < (int)n; i += 1024) atomicMax(&keys[gk[kCompCap + i]], (uint32_t)i);
-  __syncthreads();
-  for (int i = tid; i < (int)n; i += 1024) gk[2 * kCompCap + i] = keys[i];
-  if (tid == 0) *flag = 1u;
-}
-
+// The literal raster scan of the sorted triggers by one wave (filters.c:
+// 243-348): for intensity > 4 (every trigger queued) and for a sheet whose
+// triggers crowd one bucket beyond what the block can sort in LDS.  keys: n
+// triggers, pow2 p2 >= n slots (LDS when p2 <= kCompCap, else the sheet's
+// global sort buffer).
 template <int FMT>
-__global__ void __launch_bounds__(256) k_noise_replay(PlaneRef img, NoiseGeom g, uint8_t* scratch,
-                                                      int64_t sstride, const int32_t* active,
-                                                      const uint32_t* sortbuf, int64_t sort_stride) {
-  const int s = blockIdx.y;
-  if (active && !active[s]) return;
-  NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
-  const uint32_t n = *NP.nseq;
-  if (NP.nclear[2] != 1u || blockIdx.x * blockDim.x >= n) return;
-  const uint32_t* gk = sortbuf + s * sort_stride;
-  Mask81 rowp[5], colp[5];
-#pragma unroll
-  for (int L = 1; L <= 4; L++) {
-    rowp[L] = ring_part(L, true);
-    colp[L] = ring_part(L, false);
-  }
-  uint8_t* base = plane_ptr(img, s);
-  // a few blocks per sheet walk its triggers (sheets hold far fewer triggers
-  // than kCompCap: a grid sized for the cap was mostly blocks that exit)
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)n; i += gridDim.x * blockDim.x) {
-    if (gk[kCompCap + i] != (uint32_t)i) continue;  // not a component's first trigger
-    const int last = (int)gk[2 * kCompCap + i];
-    for (int j = i; j <= last; j++) {
-      if (gk[kCompCap + j] != (uint32_t)i) continue;
-      const uint32_t key = gk[j];
-      __threadfence_block();  // this thread's earlier clears are visible to its loads
-      replay_trigger4<FMT>((int32_t)(key & 0xFFFF), (int32_t)(key >> 16), g.intensity, g, base,
-                           img.P.pitch, rowp, colp);
-    }
-  }
-}
-
-template <int FMT>
-__global__ void __launch_bounds__(kResolveThreads) k_noise_resolve(PlaneRef img, NoiseGeom g, uint8_t* scratch,
-                                                       int64_t sstride, const int32_t* active,
-                                                       SheetCtl* ctl, uint32_t* sortbuf,
-                                                       int64_t sort_stride) {
-  const int s = blockIdx.x;
-  if (active && !active[s]) return;
-  NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
-  uint32_t n = *NP.nseq;
-#ifdef UPHIP_DIAG
-  if ((g.diag & 8) && threadIdx.x == 0) printf("uphip noise: sheet %d seq %u clear %u\n", s, n, *NP.nclear);
-#endif
-  if (n == 0 || NP.nclear[2] == 1u) return;  // done by k_noise_group + k_noise_replay
-  if (n > (uint32_t)g.capacity) {
-    if (threadIdx.x == 0 && ctl) atomicOr(&ctl[s].status, STATUS_NOISE_OVERFLOW);
-    return;
-  }
-  int p2 = 1;
-  while (p2 < (int)n) p2 <<= 1;
-  extern __shared__ uint32_t nlds[];  // keys[kCompCap], aux[kCompCap]
-  uint32_t* keys;
-  if (p2 <= kCompCap) {
-    keys = nlds;
-  } else {
-    keys = sortbuf + s * sort_stride;  // global fallback (rare: dark edge zones)
-  }
-#ifdef UPHIP_DIAG
-  const uint64_t t_start = wall_clock64();
-#endif
-  for (int i = threadIdx.x; i < p2; i += blockDim.x) keys[i] = i < (int)n ? NP.seq[i] : 0xFFFFFFFFu;
+__device__ void noise_raster_replay(uint32_t* keys, int n, int p2, const NoiseGeom& g, const NoisePtrs& NP,
+                                    uint8_t* base, int64_t pitch) {
+  for (int i = threadIdx.x; i < p2; i += blockDim.x) keys[i] = i < n ? NP.seq[i] : 0xFFFFFFFFu;
   __threadfence_block();
   __syncthreads();
   block_sort(keys, p2);
-#ifdef UPHIP_DIAG
-  const uint64_t t_sorted = wall_clock64();
-#endif
-  const int N = g.intensity;
-  uint8_t* base = plane_ptr(img, s);
-  const int64_t pitch = img.P.pitch;
-  if (N <= 4 && p2 <= kCompCap) {
-#ifdef UPHIP_DIAG
-    uint64_t ph[3];
-    int maxrun = 0;
-    noise_resolve_components<FMT>(keys, nlds + kCompCap, (int)n, p2, N, g, base, pitch, ph, &maxrun);
-    __syncthreads();
-    const uint64_t t_end = wall_clock64();
-    // the longest run of replayed triggers of one thread
-    __shared__ int mr;
-    if (threadIdx.x == 0) mr = 0;
-    __syncthreads();
-    atomicMax(&mr, maxrun);
-    __syncthreads();
-    if ((g.diag & 8) && threadIdx.x == 0)
-      printf("uphip noise: sheet %d n %u sort %llu link %llu sort2 %llu replay %llu ticks, longest run %d\n",
-             s, n, (unsigned long long)(t_sorted - t_start), (unsigned long long)(ph[0] - t_sorted),
-             (unsigned long long)(ph[1] - ph[0]), (unsigned long long)(t_end - ph[1]), mr);
-#else
-    noise_resolve_components<FMT>(keys, nlds + kCompCap, (int)n, p2, N, g, base, pitch);
-#endif
-    return;
-  }
   if (threadIdx.x >= 64) return;
-  // one wave replays the raster scan over the sorted triggers
+  const int N = g.intensity;
   const int lane = threadIdx.x;
   if (N <= 4) {
     // small intensity: the whole (2N+1)^2 box of a trigger is read in one
     // round trip (two pixels per lane) and the rings are counted from
     // registers; clears are written straight back
     const int side = 2 * N + 1, area = side * side;
-    for (uint32_t idx = 0; idx < n; idx++) {
+    for (int idx = 0; idx < n; idx++) {
       const uint32_t key = keys[idx];
       const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
       __threadfence_block();
@@ -2439,7 +2200,7 @@ __global__ void __launch_bounds__(kResolveThreads) k_noise_resolve(PlaneRef img,
     }
     return;
   }
-  for (uint32_t idx = 0; idx < n; idx++) {
+  for (int idx = 0; idx < n; idx++) {
     const uint32_t key = keys[idx];
     const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
     __threadfence_block();
@@ -2483,6 +2244,257 @@ __global__ void __launch_bounds__(kResolveThreads) k_noise_resolve(PlaneRef img,
   }
 }
 
+// UPH_NOISE_CHECK (tuning builds): index checks in k_noise_group that print
+// and skip the access instead of faulting; NCHK(...) is `true` otherwise.
+#ifdef UPH_NOISE_CHECK
+__device__ __forceinline__ bool nchk(bool ok, int tag, long long idx, unsigned n) {
+  if (!ok) printf("uphip noise check: sheet %d tag %d idx %lld n %u\n", (int)blockIdx.x, tag, idx, n);
+  return ok;
+}
+#define NCHK(ok, tag, idx) nchk((ok), (tag), (long long)(idx), n)
+#else
+#define NCHK(ok, tag, idx) true
+#endif
+// k_noise_group's ordering and linking for one sheet of n (> 0) triggers;
+// BIG (n > kCompCap): keys and parents in HBM, else in LDS.  A template
+// parameter, so that every pointer below has one address space (LDS through
+// ds_*, HBM through global_*): no flat accesses to LDS.
+template <int FMT, bool BIG>
+__device__ __forceinline__ void noise_group_sheet(const NoiseGeom& g, const NoisePtrs& NP, uint32_t* gk,
+                                                  uint32_t* glds, uint8_t* base, int64_t pitch,
+                                                  uint32_t* flag, uint32_t n) {
+  const int N = g.intensity;
+  const int tid = threadIdx.x;
+  const bool big = BIG;
+  uint32_t* keys = big ? gk : glds;         // the sorted keys
+  uint32_t* cur = glds + kCompCap;          // scatter cursors, then the long-bucket stage
+  uint32_t* bc = glds + 2 * kCompCap;       // bucket starts (nb + 1)
+  uint32_t* wsum = bc + kNoiseBuckets + 1;
+  uint32_t& nlong = wsum[16];
+  uint32_t& huge = wsum[17];
+  uint32_t* longs = wsum + 19;
+  const int b = noise_bucket_shift(g.H);
+  const int nb = ((g.H - 1) >> b) + 1;
+  const int R = 2 * N - 1;
+  if (tid == 0) {
+    nlong = 0u;
+    huge = 0u;
+  }
+  for (int i = tid; i <= nb; i += kGroupThreads) bc[i] = 0;
+  __syncthreads();
+  for (int i = tid; i < (int)n; i += kGroupThreads) {
+    if (NCHK(((NP.seq[i] >> 16) >> b) < (uint32_t)nb, 1, NP.seq[i])) atomicAdd(&bc[(NP.seq[i] >> 16) >> b], 1u);
+  }
+  __syncthreads();
+  // exclusive scan of the nb counts: 4 consecutive buckets a thread
+  {
+    const int b0 = 4 * tid;
+    uint32_t c[4], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      c[k] = b0 + k < nb ? bc[b0 + k] : 0u;
+      sum += c[k];
+      if (c[k] > (uint32_t)kCompCap) huge = 1u;
+      if (c[k] > (uint32_t)kGroupBucketMax) {
+        const uint32_t q = atomicAdd(&nlong, 1u);
+        if (q < (uint32_t)kLongList) longs[q] = (uint32_t)(b0 + k);
+      }
+    }
+    // block exclusive scan of `sum`
+    uint32_t incl = sum;
+    const int lane = tid & 63, wv = tid >> 6;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = (uint32_t)__shfl_up((int)incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (int k = 0; k < wv; k++) before += wsum[k];
+    uint32_t run = before + incl - sum;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (b0 + k < nb) {
+        bc[b0 + k] = run;
+        cur[b0 + k] = run;
+      }
+      run += c[k];
+    }
+    if (tid == 0) bc[nb] = n;
+  }
+  __syncthreads();
+  if (huge) {  // one bucket beyond the LDS sort: the literal scan (never on real pages)
+    int p2 = 1;
+    while (p2 < (int)n) p2 <<= 1;
+    if (tid == 0) *flag = kNoiseNothing;
+    noise_raster_replay<FMT>(gk, (int)n, p2, g, NP, base, pitch);
+    return;
+  }
+  for (int i = tid; i < (int)n; i += kGroupThreads) {
+    const uint32_t key = NP.seq[i];
+    const uint32_t dst = atomicAdd(&cur[(key >> 16) >> b], 1u);
+    if (NCHK(dst < n, 2, dst)) keys[dst] = key;
+  }
+  __threadfence_block();
+  __syncthreads();
+  // raster order inside each bucket: short ones by one thread each
+  for (int k = tid; k < nb; k += kGroupThreads) {
+    const int lo = (int)bc[k], hi = (int)bc[k + 1];
+    if (hi - lo > kGroupBucketMax) continue;
+    for (int i = lo + 1; i < hi; i++) {
+      const uint32_t v = keys[i];
+      int j = i - 1;
+      while (j >= lo && keys[j] > v) {
+        keys[j + 1] = keys[j];
+        j--;
+      }
+      keys[j + 1] = v;
+    }
+  }
+  // long ones by the whole block, one after another, staged in LDS
+  const int nl = (int)nlong;
+  for (int q = 0, k = 0; nl > 0 && (nl <= kLongList ? q < nl : k < nb);) {
+    const int kb = nl <= kLongList ? (int)longs[q++] : k++;  // uniform
+    const int lo = (int)bc[kb], len = (int)bc[kb + 1] - lo;
+    if (!NCHK(kb < nb && len <= kCompCap && lo + len <= (int)n, 3, kb)) continue;
+    if (len <= kGroupBucketMax) continue;
+    int p2 = 1;
+    while (p2 < len) p2 <<= 1;
+    __threadfence_block();
+    __syncthreads();
+    for (int i = tid; i < p2; i += kGroupThreads) cur[i] = i < len ? keys[lo + i] : 0xFFFFFFFFu;
+    __threadfence_block();
+    __syncthreads();
+    block_sort(cur, p2);
+    for (int i = tid; i < len; i += kGroupThreads) keys[lo + i] = cur[i];
+  }
+  __threadfence_block();
+  __syncthreads();
+  // parents: LDS, or (big) the seq list, whose keys are all scattered now
+  uint32_t* par = big ? NP.seq : cur;
+  for (int i = tid; i < (int)n; i += kGroupThreads) par[i] = (uint32_t)i;
+  __threadfence_block();
+  __syncthreads();
+  // link every trigger to the earlier ones within R (rows y-R .. y)
+  for (int i = tid; i < (int)n; i += kGroupThreads) {
+    const uint32_t key = keys[i];
+    const int32_t x = (int32_t)(key & 0xFFFF), y = (int32_t)(key >> 16);
+    if (!NCHK(y < g.H && (imax(y - R, 0) >> b) < nb, 4, key)) continue;
+    for (int j = (int)bc[imax(y - R, 0) >> b]; j < i; j++) {
+      const uint32_t kj = keys[j];
+      const int32_t xj = (int32_t)(kj & 0xFFFF), yj = (int32_t)(kj >> 16);
+      if (yj >= y - R && xj >= x - R && xj <= x + R) {
+        if (big) uf_union<true>(par, (uint32_t)i, (uint32_t)j);
+        else uf_union(par, (uint32_t)i, (uint32_t)j);
+      }
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (!big) {
+    for (int i = tid; i < (int)n; i += kGroupThreads) {
+      gk[i] = keys[i];
+      gk[kCompCap + i] = uf_find(par, (uint32_t)i);
+      (void)NCHK(gk[kCompCap + i] < n, 5, gk[kCompCap + i]);
+    }
+    __syncthreads();
+    for (int i = tid; i < (int)n; i += kGroupThreads) keys[i] = 0u;
+    __syncthreads();
+    for (int i = tid; i < (int)n; i += kGroupThreads) atomicMax(&keys[gk[kCompCap + i]], (uint32_t)i);
+    __syncthreads();
+    for (int i = tid; i < (int)n; i += kGroupThreads) gk[2 * kCompCap + i] = keys[i];
+    if (tid == 0) *flag = kNoiseLds;
+    return;
+  }
+  // big: roots flattened in place (a concurrent reader sees an old parent or
+  // the root, both ancestors), last trigger per root in the clear list
+  uint32_t* last = NP.clear;
+  for (int i = tid; i < (int)n; i += kGroupThreads) last[i] = 0u;
+  for (int i = tid; i < (int)n; i += kGroupThreads) par[i] = uf_find<true>(par, (uint32_t)i);
+  __threadfence_block();
+  __syncthreads();
+  for (int i = tid; i < (int)n; i += kGroupThreads) atomicMax(&last[par[i]], (uint32_t)i);
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) *flag = kNoiseBig;
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(kGroupThreads) k_noise_group(PlaneRef img, NoiseGeom g, uint8_t* scratch,
+                                                               int64_t sstride, const int32_t* active,
+                                                               SheetCtl* ctl, uint32_t* sortbuf,
+                                                               int64_t sort_stride) {
+  const int s = blockIdx.x;
+  if (active && !active[s]) return;
+  NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
+  uint32_t* flag = NP.nclear + 2;
+  const uint32_t n = *NP.nseq;
+  const int N = g.intensity;
+  const int tid = threadIdx.x;
+#ifdef UPHIP_DIAG
+  if ((g.diag & 8) && tid == 0) printf("uphip noise: sheet %d seq %u clear %u\n", s, n, *NP.nclear);
+#endif
+  if (n == 0 || n > (uint32_t)g.capacity) {
+    if (tid == 0) {
+      *flag = kNoiseNothing;
+      if (n != 0 && ctl) atomicOr(&ctl[s].status, STATUS_NOISE_OVERFLOW);
+    }
+    return;
+  }
+  uint32_t* gk = sortbuf + s * sort_stride;
+  extern __shared__ uint32_t glds[];
+  uint8_t* base = plane_ptr(img, s);
+  const int64_t pitch = img.P.pitch;
+  if (N > 4) {  // intensity > 4: every trigger, one wave in raster order
+    int p2 = 1;
+    while (p2 < (int)n) p2 <<= 1;
+    if (tid == 0) *flag = kNoiseNothing;
+    if (p2 <= kCompCap) noise_raster_replay<FMT>(glds, (int)n, p2, g, NP, base, pitch);
+    else noise_raster_replay<FMT>(gk, (int)n, p2, g, NP, base, pitch);
+    return;
+  }
+  if (n > (uint32_t)kCompCap)
+    noise_group_sheet<FMT, true>(g, NP, gk, glds, base, pitch, flag, n);
+  else
+    noise_group_sheet<FMT, false>(g, NP, gk, glds, base, pitch, flag, n);
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(256) k_noise_replay(PlaneRef img, NoiseGeom g, uint8_t* scratch,
+                                                      int64_t sstride, const int32_t* active,
+                                                      const uint32_t* sortbuf, int64_t sort_stride) {
+  const int s = blockIdx.y;
+  if (active && !active[s]) return;
+  NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
+  const uint32_t n = *NP.nseq;
+  const uint32_t layout = NP.nclear[2];
+  if (layout == kNoiseNothing || blockIdx.x * blockDim.x >= n) return;
+  const uint32_t* keys = sortbuf + s * sort_stride;
+  const uint32_t* root = layout == kNoiseLds ? keys + kCompCap : NP.seq;
+  const uint32_t* last = layout == kNoiseLds ? keys + 2 * kCompCap : NP.clear;
+  Mask81 rowp[5], colp[5];
+#pragma unroll
+  for (int L = 1; L <= 4; L++) {
+    rowp[L] = ring_part(L, true);
+    colp[L] = ring_part(L, false);
+  }
+  uint8_t* base = plane_ptr(img, s);
+  // a few blocks per sheet walk its triggers (sheets hold far fewer triggers
+  // than kCompCap: a grid sized for the cap was mostly blocks that exit)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)n; i += gridDim.x * blockDim.x) {
+    if (root[i] != (uint32_t)i) continue;  // not a component's first trigger
+    const int end = (int)last[i];
+    for (int j = i; j <= end; j++) {
+      if (root[j] != (uint32_t)i) continue;
+      const uint32_t key = keys[j];
+      __threadfence_block();  // this thread's earlier clears are visible to its loads
+      replay_trigger4<FMT>((int32_t)(key & 0xFFFF), (int32_t)(key >> 16), g.intensity, g, base,
+                           img.P.pitch, rowp, colp);
+    }
+  }
+}
+
 __global__ void k_noise_zero(uint8_t* scr, int64_t stride, int count) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s < count) {
@@ -2519,16 +2531,12 @@ static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr
                      bits, bstride);
   hipLaunchKernelGGL(k_noise_apply<FMT>, dim3(64, count), dim3(256), 0, st, img, g, scr, ss,
                      active, ctl);
-  constexpr size_t kResolveLds = 2 * sizeof(uint32_t) * kCompCap;  // 128 KiB
-  allow_dynamic_lds((const void*)k_noise_resolve<FMT>, kResolveLds);
-  allow_dynamic_lds((const void*)k_noise_group, kGroupLds);
+  allow_dynamic_lds((const void*)k_noise_group<FMT>, kGroupLds);
   if (!(diag_skip() & 2)) {
-    hipLaunchKernelGGL(k_noise_group, dim3(count), dim3(1024), kGroupLds, st, g, scr, ss, active, ctl,
-                       sortbuf, sort_stride);
+    hipLaunchKernelGGL(k_noise_group<FMT>, dim3(count), dim3(kGroupThreads), kGroupLds, st, img, gd, scr,
+                       ss, active, ctl, sortbuf, sort_stride);
     hipLaunchKernelGGL(k_noise_replay<FMT>, dim3(replay_blocks(count), count), dim3(256), 0, st, img, g,
                        scr, ss, active, sortbuf, sort_stride);
-    hipLaunchKernelGGL(k_noise_resolve<FMT>, dim3(count), dim3(kResolveThreads), kResolveLds, st, img,
-                       gd, scr, ss, active, ctl, sortbuf, sort_stride);
   }
 }
 
