@@ -593,6 +593,81 @@ __device__ __forceinline__ void check_cursor(const int32_t (&cs)[5], int32_t c, 
   for (int d = 0; d < 4; d++) p[d] = d == *dc ? ((c - cd) >> 1) + 1 : 1;
   *sub = (c - cd) & 1;
 }
+// Later check trips of a frame (its lines' lengths known): the 32 window
+// slots of a trip (lane = 2 * slot + side) go to the checks in order -- the
+// cursor's line from the cursor, then the following lines from their first
+// position -- as many windows as each needs, so a long line is read 2048
+// positions a trip instead of 512 (a C3 band column is 3508 long).
+struct ChkPlan {
+  int32_t start[4], cnt[4], p0[4];  // slot range and first position per line
+  int32_t cov;                      // the first check the windows do not reach
+};
+__device__ __forceinline__ ChkPlan check_plan(const Frame& f, const int32_t (&cs)[5], int dc,
+                                              int32_t pc) {
+  ChkPlan pl;
+  int32_t left = 32;
+  pl.cov = cs[4];
+  bool open = true;
+#pragma unroll
+  for (int d = 0; d < 4; d++) {
+    pl.p0[d] = d == dc ? pc : 1;
+    const int32_t rem = d < dc ? 0 : f.dist[d] - pl.p0[d] + 1;  // positions to read
+    const int32_t need = rem > 0 ? (rem + 63) >> 6 : 0;
+    pl.start[d] = 32 - left;
+    pl.cnt[d] = open ? imin(need, left) : 0;
+    if (open && need > left) {  // this line runs past the trip's windows
+      pl.cov = cs[d] + 2 * (pl.p0[d] + 64 * left - 1);
+      open = false;
+    }
+    left -= pl.cnt[d];
+  }
+  return pl;
+}
+__device__ __forceinline__ void check_issue_plan(const Sheet& S, Win& w, const Frame& f, const ChkPlan& pl,
+                                                 int* ln_out, int32_t* base_out) {
+  const int lane = lane_id(), j = lane >> 1, side = lane & 1;
+  int ln = -1;
+  int32_t base = 0;
+#pragma unroll
+  for (int d = 0; d < 4; d++)
+    if (j >= pl.start[d] && j < pl.start[d] + pl.cnt[d]) {
+      ln = d;
+      base = pl.p0[d] + 64 * (j - pl.start[d]);
+    }
+  if (ln >= 0) ray_issue(S, w, ln, f.x, f.y, side == 0 ? 1 : -1, base);
+  *ln_out = ln;
+  *base_out = base;
+}
+// The first matching check in the planned windows (INT_MAX: none, *next =
+// the plan's coverage); *resume as in check_eval.
+__device__ __forceinline__ int32_t check_eval_plan(const Sheet& S, const Win& w, const Frame& f,
+                                                   const int32_t (&cs)[5], int dc, int32_t sub,
+                                                   int32_t pc, const ChkPlan& pl, int ln, int32_t base,
+                                                   int32_t* resume, int32_t* next) {
+  const int lane = lane_id(), side = lane & 1;
+  uint64_t E = 0;
+  int32_t csd = 0;
+  if (ln >= 0) {
+    E = ray_bits(S, w, ln);
+    const int32_t lim = pick4(f.dist, ln) - base + 1;  // this window's positions on the line
+    if (lim < 64) E &= lim > 0 ? (1ull << lim) - 1 : 0;
+    if (ln == dc && side == 0 && base == pc && sub) E &= ~1ull;  // behind the cursor
+    csd = ln == 0 ? cs[0] : ln == 1 ? cs[1] : ln == 2 ? cs[2] : cs[3];
+  }
+  // check index of the lane's first match; the windows are a prefix of the
+  // checks in order, so the smallest index over the wave is the first match
+  int32_t c = E ? csd + 2 * (base + ctz64(E) - 1) + side : INT_MAX;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) c = imin(c, __shfl_xor(c, o, 64));
+  c = uni(c);
+  *next = pl.cov;
+  if (c == INT_MAX) return INT_MAX;
+  const uint64_t hasb = __ballot(E != 0);
+  const bool multi = __ballot(__popcll(E) >= 2) != 0 || __popcll(hasb) >= 2;
+  *resume = multi ? c + 1 : pl.cov;
+  return c;
+}
+
 // The first matching check of frame f at or after check c, or n (none).
 __device__ __forceinline__ int32_t check_scan(const Sheet& S, const Frame& f,
                                               const int32_t (&cs)[5], int32_t c, int32_t* resume,
@@ -603,12 +678,16 @@ __device__ __forceinline__ int32_t check_scan(const Sheet& S, const Frame& f,
     int dc;
     int32_t p[4], sub;
     check_cursor(cs, c, &dc, p, &sub);
+    const int32_t pc = pick4(p, dc);
+    const ChkPlan pl = check_plan(f, cs, dc, pc);
     Win w;
-    check_issue(S, w, f, dc, p, true);
+    int ln;
+    int32_t base;
+    check_issue_plan(S, w, f, pl, &ln, &base);
     int32_t nx;
-    const int32_t r = check_eval(S, w, f, cs, dc, sub, p, resume, &nx);
+    const int32_t r = check_eval_plan(S, w, f, cs, dc, sub, pc, pl, ln, base, resume, &nx);
     if (r != INT_MAX) return r;
-    c = nx;
+    c = uni(nx);
   }
   return cs[4];
 }
@@ -720,20 +799,30 @@ __global__ void __launch_bounds__(64) k_black_resolve(PlaneRef img, BlackGeom g,
         const Rect c = clip(bb.r, g.W, g.H);
         uint64_t sum = 0;
         if (c.x0 <= c.x1 && c.y0 <= c.y1) {
+          // pixel i of the bar (row-major) is lane i % 64's; eight of a
+          // lane's pixels are loaded before any is summed, so their loads are
+          // in flight together (a bar is ~10^4 pixels: one load round trip
+          // per pixel made each remeasure ~40 us)
           const int32_t cwid = c.x1 - c.x0 + 1;
           const int64_t npx = (int64_t)cwid * (c.y1 - c.y0 + 1);
-          const int32_t q64 = 64 / cwid, r64 = 64 % cwid;
-          int32_t y = c.y0 + lane / cwid, x = c.x0 + lane % cwid;
-          for (int64_t i = lane; i < npx; i += 64) {
-            const uint64_t pw = Sheet::pload(S.RP + (int64_t)y * S.wpr + (x >> 6));
-            const uint32_t v = dark_of(load_px_row<FMT>(base + (int64_t)y * pitch, x));
-            sum += ((pw >> (x & 63)) & 1) ? 255u : v;
-            x += r64;
-            y += q64;
-            if (x > c.x1) {
-              x -= cwid;
-              y++;
+          constexpr int kU = 8;
+          for (int64_t i0 = lane; i0 < npx; i0 += 64 * kU) {
+            uint64_t pw[kU];
+            uint32_t v[kU];
+            int32_t bit[kU];
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+              const int64_t i = i0 + 64 * u;
+              const bool ok = i < npx;
+              const int32_t y = ok ? c.y0 + (int32_t)(i / cwid) : c.y0;
+              const int32_t x = ok ? c.x0 + (int32_t)(i % cwid) : c.x0;
+              pw[u] = ok ? Sheet::pload(S.RP + (int64_t)y * S.wpr + (x >> 6)) : 0ull;
+              v[u] = ok ? dark_of(load_px_row<FMT>(base + (int64_t)y * pitch, x)) : 0u;
+              bit[u] = x & 63;
             }
+#pragma unroll
+            for (int u = 0; u < kU; u++)
+              if (i0 + 64 * u < npx) sum += ((pw[u] >> bit[u]) & 1) ? 255u : v[u];
           }
         }
         for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
