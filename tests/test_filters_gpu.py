@@ -137,10 +137,10 @@ def noisy_scan(w, h, page, specks, seed, quality=75, border=True, dashes=True):
 
 
 @pytest.mark.parametrize("fmt", [A.FMT_GRAY8, A.FMT_RGB24])
-@pytest.mark.parametrize("specks,intensity", [(40000, 4), (40000, 2), (6000, 4), (6000, 3)])
+@pytest.mark.parametrize("specks,intensity", [(40000, 4), (40000, 2), (6000, 4), (800, 3), (800, 4)])
 def test_noisefilter_group_caps(hip, oracle, fmt, specks, intensity):
-    # 40000 specks: more than 16384 sequential triggers (k_noise_group's
-    # global layout); 6000: within the LDS layout; both with rows of more than
+    # 40000 / 6000 specks: more than 4096 sequential triggers (k_noise_group's
+    # global layout); 800: within its LDS layout; all with rows of more than
     # 256 triggers (the dashed rules: the block-wide bucket sort)
     g = noisy_scan(1240, 1754, 3, specks, specks + intensity)
     h = HostImage.from_array(np.repeat(g[:, :, None], 3, axis=2) if fmt == A.FMT_RGB24 else g, fmt)

@@ -437,28 +437,32 @@ __device__ __forceinline__ void paint_cross(const Sheet& S, int32_t px, int32_t 
   const int lane = lane_id();
   const int32_t xa = px - dist[0], xb = px + dist[2], ya = py - dist[1], yb = py + dist[3];
   const int32_t nrw = (xb >> 6) - (xa >> 6) + 1, nown = nrw + (yb >> 6) - (ya >> 6) + 1;
-  const int32_t nrx = dist[0] + dist[2], ncross = nrx + dist[1] + dist[3];
+  const int32_t nrx = dist[0] + dist[2];
   uint64_t *RP = S.RP, *CP = S.CP;
   const int32_t wpr = S.wpr, W = S.W;
-  for (int32_t i0 = 0; i0 < imax(nown, ncross); i0 += 64) {
-    const int32_t i = i0 + lane;
-    if (i < nown) {
-      const bool row = i < nrw;
-      const int32_t lo = row ? xa : ya, hi = row ? xb : yb;
-      const int32_t w = (lo >> 6) + (row ? i : i - nrw);
-      const int a = imax(lo - 64 * w, 0), b = imin(hi - 64 * w, 63);
-      Sheet::por(row ? RP + (int64_t)py * wpr + w : CP + (int64_t)w * W + px,
-                 (~0ull >> (63 - b)) & (~0ull << a));
-    }
-    if (i < nrx) {
-      const int32_t x = i < dist[0] ? px - 1 - i : px + 1 + (i - dist[0]);
-      Sheet::por(CP + (int64_t)(py >> 6) * W + x, 1ull << (py & 63));
-    } else if (i < ncross) {
-      const int32_t j = i - nrx;
-      const int32_t y = j < dist[1] ? py - 1 - j : py + 1 + (j - dist[1]);
-      Sheet::por(RP + (int64_t)y * wpr + (px >> 6), 1ull << (px & 63));
-    }
+  // own planes: a word per lane
+  for (int32_t i = lane; i < nown; i += 64) {
+    const bool row = i < nrw;
+    const int32_t lo = row ? xa : ya, hi = row ? xb : yb;
+    const int32_t w = (lo >> 6) + (row ? i : i - nrw);
+    const int a = imax(lo - 64 * w, 0), b = imin(hi - 64 * w, 63);
+    Sheet::por(row ? RP + (int64_t)py * wpr + w : CP + (int64_t)w * W + px,
+               (~0ull >> (63 - b)) & (~0ull << a));
   }
+  // crossing planes, a bit per lane: the row's pixels in the column planes
+  const uint64_t bit_y = 1ull << (py & 63);
+  uint64_t* const crow = CP + (int64_t)(py >> 6) * W;
+  for (int32_t i = lane; i < nrx; i += 64)
+    Sheet::por(crow + (i < dist[0] ? px - 1 - i : px + 1 + (i - dist[0])), bit_y);
+  // ... and the column's pixels in the row planes: straight pointer walks up
+  // and down (a C3 band column is ~3500 pixels: this is most of a frame's
+  // paint)
+  const uint64_t bit_x = 1ull << (px & 63);
+  const int64_t step = (int64_t)64 * wpr;
+  uint64_t* up = RP + (int64_t)(py - 1 - lane) * wpr + (px >> 6);
+  for (int32_t j = lane; j < dist[1]; j += 64, up -= step) Sheet::por(up, bit_x);
+  uint64_t* dn = RP + (int64_t)(py + 1 + lane) * wpr + (px >> 6);
+  for (int32_t j = lane; j < dist[3]; j += 64, dn += step) Sheet::por(dn, bit_x);
 }
 
 // The four fill_lines of a frame at (px, py) (fill.c:16-43, :88-95): left,
@@ -475,7 +479,7 @@ __device__ __forceinline__ void fill_issue(const Sheet& S, Win& w, int32_t px, i
 }
 __device__ __forceinline__ void fill_cross(const Sheet& S, int32_t px, int32_t py, int32_t (&dist)[4],
                                            Win& w, BlackStats* bs) {
-  const int lane = lane_id(), ln = lane >> 4, k = lane & 15;
+  const int lane = lane_id();
   if (S.I == 0) {  // the counter is 0 after the first position, whatever it holds
 #pragma unroll
     for (int d = 0; d < 4; d++) dist[d] = 0;
@@ -495,24 +499,46 @@ __device__ __forceinline__ void fill_cross(const Sheet& S, int32_t px, int32_t p
       carry[d] = uni(carry[d]);
     }
     done = uni(done);
-    const bool run = !((done >> ln) & 1);
-    const int32_t base = pick4(pos0, ln) + 64 * k;
-    if (trip > 0 && run) ray_issue(S, w, ln, px, py, 0, base);
-    const uint64_t E = run ? ray_bits(S, w, ln) : 0;
+    // lanes of line d: [lo[d], lo[d] + cnt[d]); 16 each on the first trip
+    // (issued with the frame's check windows), afterwards the lines still
+    // open share all 64 (one open line: 4096 positions a trip, two: 2048)
+    const int nopen = __popc(~done & 15u);
+    int32_t lo[4], cnt[4];
+    {
+      const int32_t per = (trip == 0 || nopen > 2) ? 16 : 64 / nopen;
+      int32_t next = 0;
+#pragma unroll
+      for (int d = 0; d < 4; d++) {
+        const bool open = !((done >> d) & 1);
+        lo[d] = per == 16 ? 16 * d : next;
+        cnt[d] = open ? per : 0;
+        if (open) next += per;
+      }
+    }
+    int mln = -1;
+#pragma unroll
+    for (int d = 0; d < 4; d++)
+      if (lane >= lo[d] && lane < lo[d] + cnt[d]) mln = d;
+    const bool run = mln >= 0;
+    const int lnx = run ? mln : 0;
+    const int32_t kk = lane - pick4(lo, lnx);
+    const int32_t base = pick4(pos0, lnx) + 64 * kk;
+    if (trip > 0 && run) ray_issue(S, w, lnx, px, py, 0, base);
+    const uint64_t E = run ? ray_bits(S, w, lnx) : 0;
     // the last match of this line's lanes before this one, or the carry
     const int32_t lastabs = E ? base + hib64(E) : INT_MIN;
     const uint64_t hasb = __ballot(E != 0);
-    const uint64_t before = hasb & lane_range(16 * ln, k);
+    const uint64_t before = hasb & lane_range(pick4(lo, lnx), kk);
     const int32_t lsrc = __shfl(lastabs, before ? hib64(before) : lane, 64);
-    const int32_t L = before ? lsrc : pick4(carry, ln);
+    const int32_t L = before ? lsrc : pick4(carry, lnx);
     const int32_t st = run ? window_stop(E, base, L, S.I) : INT_MAX;
     const uint64_t stb = __ballot(st != INT_MAX);
 #pragma unroll
     for (int d = 0; d < 4; d++) {
       if ((done >> d) & 1) continue;
-      const uint64_t rng = lane_range(16 * d, 16);
+      const uint64_t rng = lane_range(lo[d], cnt[d]);
       int32_t sd = (stb & rng) ? __builtin_amdgcn_readlane(st, ctz64(stb & rng)) : INT_MAX;
-      const int32_t end = pos0[d] + 64 * 16;  // first position not read
+      const int32_t end = pos0[d] + 64 * cnt[d];  // first position not read
       if (sd == INT_MAX && end > edge[d]) sd = edge[d];
       if (sd != INT_MAX) {
         stop[d] = imin(sd, edge[d]);
@@ -598,6 +624,9 @@ __device__ __forceinline__ void check_cursor(const int32_t (&cs)[5], int32_t c, 
 // cursor's line from the cursor, then the following lines from their first
 // position -- as many windows as each needs, so a long line is read 2048
 // positions a trip instead of 512 (a C3 band column is 3508 long).
+#ifndef UPH_BLACK_PLAN
+#define UPH_BLACK_PLAN 1
+#endif
 struct ChkPlan {
   int32_t start[4], cnt[4], p0[4];  // slot range and first position per line
   int32_t cov;                      // the first check the windows do not reach
@@ -654,15 +683,15 @@ __device__ __forceinline__ int32_t check_eval_plan(const Sheet& S, const Win& w,
     if (ln == dc && side == 0 && base == pc && sub) E &= ~1ull;  // behind the cursor
     csd = ln == 0 ? cs[0] : ln == 1 ? cs[1] : ln == 2 ? cs[2] : cs[3];
   }
-  // check index of the lane's first match; the windows are a prefix of the
-  // checks in order, so the smallest index over the wave is the first match
-  int32_t c = E ? csd + 2 * (base + ctz64(E) - 1) + side : INT_MAX;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) c = imin(c, __shfl_xor(c, o, 64));
-  c = uni(c);
-  *next = pl.cov;
-  if (c == INT_MAX) return INT_MAX;
+  // check index of the lane's first match; slots follow the check order, so
+  // the first match is in the lowest slot with one: the smaller of its two
+  // sides' first matches
+  const int32_t cl = E ? csd + 2 * (base + ctz64(E) - 1) + side : INT_MAX;
   const uint64_t hasb = __ballot(E != 0);
+  *next = pl.cov;
+  if (!hasb) return INT_MAX;
+  const int l0 = ctz64(hasb) & ~1;
+  const int32_t c = imin(__builtin_amdgcn_readlane(cl, l0), __builtin_amdgcn_readlane(cl, l0 + 1));
   const bool multi = __ballot(__popcll(E) >= 2) != 0 || __popcll(hasb) >= 2;
   *resume = multi ? c + 1 : pl.cov;
   return c;
@@ -678,6 +707,7 @@ __device__ __forceinline__ int32_t check_scan(const Sheet& S, const Frame& f,
     int dc;
     int32_t p[4], sub;
     check_cursor(cs, c, &dc, p, &sub);
+#if UPH_BLACK_PLAN
     const int32_t pc = pick4(p, dc);
     const ChkPlan pl = check_plan(f, cs, dc, pc);
     Win w;
@@ -686,6 +716,12 @@ __device__ __forceinline__ int32_t check_scan(const Sheet& S, const Frame& f,
     check_issue_plan(S, w, f, pl, &ln, &base);
     int32_t nx;
     const int32_t r = check_eval_plan(S, w, f, cs, dc, sub, pc, pl, ln, base, resume, &nx);
+#else
+    Win w;
+    check_issue(S, w, f, dc, p, true);
+    int32_t nx;
+    const int32_t r = check_eval(S, w, f, cs, dc, sub, p, resume, &nx);
+#endif
     if (r != INT_MAX) return r;
     c = uni(nx);
   }
@@ -798,31 +834,73 @@ __global__ void __launch_bounds__(64) k_black_resolve(PlaneRef img, BlackGeom g,
         BSTAT(const uint64_t tr = wall_clock64(); bs->remeasures++;)
         const Rect c = clip(bb.r, g.W, g.H);
         uint64_t sum = 0;
-        if (c.x0 <= c.x1 && c.y0 <= c.y1) {
-          // pixel i of the bar (row-major) is lane i % 64's; eight of a
-          // lane's pixels are loaded before any is summed, so their loads are
-          // in flight together (a bar is ~10^4 pixels: one load round trip
-          // per pixel made each remeasure ~40 us)
-          const int32_t cwid = c.x1 - c.x0 + 1;
-          const int64_t npx = (int64_t)cwid * (c.y1 - c.y0 + 1);
-          constexpr int kU = 8;
-          for (int64_t i0 = lane; i0 < npx; i0 += 64 * kU) {
+        if (c.x0 <= c.x1 && c.y0 <= c.y1 && FMT == F_GRAY8 && pitch % 16 == 0 &&
+            ((uintptr_t)base & 15) == 0) {
+          // GRAY8: a lane per (row, 64-pixel word of the row plane): the P
+          // word and the segment's 64 bytes as four 16-byte loads, four
+          // segments' loads in flight at once (a bar is ~10^4 pixels: a
+          // load round trip a pixel made a remeasure ~40 us)
+          const int32_t w0 = c.x0 >> 6, nw = (c.x1 >> 6) - w0 + 1;
+          const int32_t nseg = nw * (c.y1 - c.y0 + 1);
+          constexpr int kU = 4;
+          for (int32_t i0 = lane; i0 < nseg; i0 += 64 * kU) {
             uint64_t pw[kU];
-            uint32_t v[kU];
-            int32_t bit[kU];
+            uint4 px[kU][4];
+            int32_t lo[kU], hi[kU];
 #pragma unroll
             for (int u = 0; u < kU; u++) {
-              const int64_t i = i0 + 64 * u;
-              const bool ok = i < npx;
-              const int32_t y = ok ? c.y0 + (int32_t)(i / cwid) : c.y0;
-              const int32_t x = ok ? c.x0 + (int32_t)(i % cwid) : c.x0;
-              pw[u] = ok ? Sheet::pload(S.RP + (int64_t)y * S.wpr + (x >> 6)) : 0ull;
-              v[u] = ok ? dark_of(load_px_row<FMT>(base + (int64_t)y * pitch, x)) : 0u;
-              bit[u] = x & 63;
-            }
+              const int32_t i = i0 + 64 * u;
+              const bool ok = i < nseg;
+              const int32_t y = c.y0 + (ok ? i / nw : 0), w = w0 + (ok ? i % nw : 0);
+              lo[u] = ok ? imax(c.x0 - 64 * w, 0) : 64;
+              hi[u] = ok ? imin(c.x1 - 64 * w, 63) : -1;
+              pw[u] = ok ? Sheet::pload(S.RP + (int64_t)y * S.wpr + w) : 0ull;
+              const uint4* q = reinterpret_cast<const uint4*>(base + (int64_t)y * pitch + 64 * w);
 #pragma unroll
-            for (int u = 0; u < kU; u++)
-              if (i0 + 64 * u < npx) sum += ((pw[u] >> bit[u]) & 1) ? 255u : v[u];
+              for (int k = 0; k < 4; k++) {
+                // the row's last word may reach past the pitch: only bytes
+                // at or below x1 are summed, and loads stay inside the row
+                const bool in = ok && 64 * w + 16 * k < (int32_t)pitch;
+                px[u][k] = in ? q[k] : make_uint4(0, 0, 0, 0);
+              }
+            }
+            // painted pixels count 255 (white); the others' bytes are summed
+            // four at a time (v_sad_u8 over the bytes the mask keeps)
+            uint32_t acc = 0;
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+              const uint64_t rmask =
+                  hi[u] >= lo[u] ? (~0ull >> (63 - hi[u])) & (~0ull << lo[u]) : 0ull;
+              sum += 255u * (uint32_t)__popcll(pw[u] & rmask);
+              const uint64_t keep = rmask & ~pw[u];
+#pragma unroll
+              for (int k = 0; k < 4; k++) {
+                const uint32_t d4[4] = {px[u][k].x, px[u][k].y, px[u][k].z, px[u][k].w};
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                  const uint32_t m = (uint32_t)(keep >> (16 * k + 4 * j)) & 0xFu;
+                  const uint32_t M = ((m * 0x00204081u) & 0x01010101u) * 0xFFu;
+                  acc = __builtin_amdgcn_sad_u8(d4[j] & M, 0u, acc);
+                }
+              }
+            }
+            sum += acc;
+          }
+        } else if (c.x0 <= c.x1 && c.y0 <= c.y1) {
+          const int32_t cwid = c.x1 - c.x0 + 1;
+          const int64_t npx = (int64_t)cwid * (c.y1 - c.y0 + 1);
+          const int32_t q64 = 64 / cwid, r64 = 64 % cwid;
+          int32_t y = c.y0 + lane / cwid, x = c.x0 + lane % cwid;
+          for (int64_t i = lane; i < npx; i += 64) {
+            const uint64_t pw = Sheet::pload(S.RP + (int64_t)y * S.wpr + (x >> 6));
+            const uint32_t v = dark_of(load_px_row<FMT>(base + (int64_t)y * pitch, x));
+            sum += ((pw >> (x & 63)) & 1) ? 255u : v;
+            x += r64;
+            y += q64;
+            if (x > c.x1) {
+              x -= cwid;
+              y++;
+            }
           }
         }
         for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);

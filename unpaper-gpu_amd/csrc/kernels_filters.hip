@@ -1077,9 +1077,9 @@ size_t noise_scratch_bytes(const NoiseGeom& g) {
   // lists + a global sort buffer for the rare > 8192-trigger sequential case;
   // the GRAY8 dark bit-plane shares the sort buffer's space (it is read by
   // k_noise_classify only, before k_noise_resolve may sort)
-  // (and k_noise_group's keys / roots / last, 3 x 16384 words)
+  // (and k_noise_group's keys / roots / last, 3 x 4096 words)
   size_t sort = 4 * pow2_at_least((size_t)g.capacity);
-  if (sort < 12 * 16384) sort = 12 * 16384;
+  if (sort < 12 * 4096) sort = 12 * 4096;
   const size_t bits = 4 * (size_t)noise_bit_words(g) * (size_t)g.H;
   return noise_list_bytes(g) + (sort > bits ? sort : bits);
 }
@@ -2085,16 +2085,20 @@ __device__ __forceinline__ void uf_union(uint32_t* parent, uint32_t a, uint32_t 
   }
 }
 
-constexpr int kCompCap = 16384;  // triggers the component replay keeps in LDS
-static_assert(kCompCap == 16384, "noise_scratch_bytes reserves 3 x 16384 words for k_noise_group");
-constexpr int kGroupThreads = 1024;
+constexpr int kCompCap = 4096;  // triggers k_noise_group keeps in LDS (more: in HBM)
+static_assert(kCompCap == 4096, "noise_scratch_bytes reserves 3 x 4096 words for k_noise_group");
+// k_noise_group is one 256-thread block a sheet with ~49 KiB of LDS: a block
+// that needs a whole CU's wave slots and LDS (1024 threads, 147 KiB, round
+// 5) waits for a CU to drain while other streams' kernels keep them busy
+// (84 ms a launch in the JPEG 2000 runner, behind the code-block decode).
+constexpr int kGroupThreads = 256;
 // k_noise_replay blocks per sheet: enough that a lone sheet's components
-// spread over the chip (C2/C4 latency: up to kCompCap threads a sheet), few
+// spread over the chip (C2/C4 latency: up to 16384 threads a sheet), few
 // enough that a 64-sheet batch is not mostly blocks that exit (C3): about one
-// block a CU over the launch, clamped to [4, kCompCap / 256].
+// block a CU over the launch, clamped to [4, 64].
 static int replay_blocks(int count) {
   const int per = (256 + count - 1) / (count > 0 ? count : 1);
-  return per < 4 ? 4 : per > kCompCap / 256 ? kCompCap / 256 : per;
+  return per < 4 ? 4 : per > 64 ? 64 : per;
 }
 
 // The sequential part of the noisefilter (the triggers k_noise_classify could
@@ -2286,18 +2290,23 @@ __device__ __forceinline__ void noise_group_sheet(const NoiseGeom& g, const Nois
     if (NCHK(((NP.seq[i] >> 16) >> b) < (uint32_t)nb, 1, NP.seq[i])) atomicAdd(&bc[(NP.seq[i] >> 16) >> b], 1u);
   }
   __syncthreads();
-  // exclusive scan of the nb counts: 4 consecutive buckets a thread
+  // exclusive scan of the nb counts: KB consecutive buckets a thread
   {
-    const int b0 = 4 * tid;
-    uint32_t c[4], sum = 0;
+    constexpr int KB = kNoiseBuckets / kGroupThreads;
+    const int b0 = KB * tid;
+    uint32_t c[KB], sum = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < KB; k++) {
       c[k] = b0 + k < nb ? bc[b0 + k] : 0u;
       sum += c[k];
-      if (c[k] > (uint32_t)kCompCap) huge = 1u;
       if (c[k] > (uint32_t)kGroupBucketMax) {
         const uint32_t q = atomicAdd(&nlong, 1u);
         if (q < (uint32_t)kLongList) longs[q] = (uint32_t)(b0 + k);
+        // staged in LDS, or (BIG) in the clear list: a bucket past that
+        // (pow2 slots) takes the literal scan
+        int p2 = 1;
+        while (p2 < (int)c[k]) p2 <<= 1;
+        if (p2 > (BIG ? g.capacity : kCompCap)) huge = 1u;
       }
     }
     // block exclusive scan of `sum`
@@ -2314,7 +2323,7 @@ __device__ __forceinline__ void noise_group_sheet(const NoiseGeom& g, const Nois
     uint32_t run = before + incl - sum;
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < KB; k++) {
       if (b0 + k < nb) {
         bc[b0 + k] = run;
         cur[b0 + k] = run;
@@ -2352,22 +2361,32 @@ __device__ __forceinline__ void noise_group_sheet(const NoiseGeom& g, const Nois
       keys[j + 1] = v;
     }
   }
-  // long ones by the whole block, one after another, staged in LDS
+  // long ones by the whole block, one after another, staged in LDS (BIG: in
+  // the clear list when longer than the LDS stage)
   const int nl = (int)nlong;
   for (int q = 0, k = 0; nl > 0 && (nl <= kLongList ? q < nl : k < nb);) {
     const int kb = nl <= kLongList ? (int)longs[q++] : k++;  // uniform
     const int lo = (int)bc[kb], len = (int)bc[kb + 1] - lo;
-    if (!NCHK(kb < nb && len <= kCompCap && lo + len <= (int)n, 3, kb)) continue;
+    if (!NCHK(kb < nb && lo + len <= (int)n, 3, kb)) continue;
     if (len <= kGroupBucketMax) continue;
     int p2 = 1;
     while (p2 < len) p2 <<= 1;
     __threadfence_block();
     __syncthreads();
-    for (int i = tid; i < p2; i += kGroupThreads) cur[i] = i < len ? keys[lo + i] : 0xFFFFFFFFu;
-    __threadfence_block();
-    __syncthreads();
-    block_sort(cur, p2);
-    for (int i = tid; i < len; i += kGroupThreads) keys[lo + i] = cur[i];
+    if (!BIG || p2 <= kCompCap) {
+      for (int i = tid; i < p2; i += kGroupThreads) cur[i] = i < len ? keys[lo + i] : 0xFFFFFFFFu;
+      __threadfence_block();
+      __syncthreads();
+      block_sort(cur, p2);
+      for (int i = tid; i < len; i += kGroupThreads) keys[lo + i] = cur[i];
+    } else {
+      uint32_t* stage = NP.clear;
+      for (int i = tid; i < p2; i += kGroupThreads) stage[i] = i < len ? keys[lo + i] : 0xFFFFFFFFu;
+      __threadfence_block();
+      __syncthreads();
+      block_sort(stage, p2);
+      for (int i = tid; i < len; i += kGroupThreads) keys[lo + i] = stage[i];
+    }
   }
   __threadfence_block();
   __syncthreads();
