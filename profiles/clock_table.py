@@ -35,25 +35,40 @@ launches = collections.Counter()
 if kt:
     for r in csv.DictReader(open(kt[0])):
         launches[r["Kernel_Name"][:56]] += 1
+# GRBM_GUI_ACTIVE / 8 / wall time is the effective clock only for dispatches
+# of about 0.3 ms or more (MI355X_MICROARCH.md, DVFS give-back: it reads high
+# on shorter ones).  Shorter kernels get the median clock of the long ones in
+# the same run ("assumed" in the table), so no clock above the chip's 2.4 GHz
+# is reported and their VALU fraction is not understated.
+LONG_MS = 0.3
+clk = {}
+for k, v in agg.items():
+    t = dur.get(k, 0.0)
+    n = launches.get(k, 0) or 1
+    if t > 0 and t * 1e3 / n >= LONG_MS:
+        clk[k] = v.get("GRBM_GUI_ACTIVE", 0.0) / 8 / t / 1e9
+long_ghz = sorted(clk.values())[len(clk) // 2] if clk else 2.4
 print("%-56s %9s %9s %8s %9s %9s" % ("kernel", "dur_ms", "GHz", "VALU%", "VALU/wave", "SALU/wave"))
 for k, v in sorted(agg.items(), key=lambda kv: -dur.get(kv[0], 0)):
     t = dur.get(k, 0.0)
-    gui = v.get("GRBM_GUI_ACTIVE", 0.0)
-    gui /= 8  # GRBM_GUI_ACTIVE is summed over the 8 XCDs
-    ghz = gui / t / 1e9 if t > 0 else 0.0
+    ghz = clk.get(k, long_ghz)
+    gui = ghz * 1e9 * t  # active cycles of the kernel
     valu = v.get("SQ_INSTS_VALU", 0.0)
     frac = valu * 4 / (1024 * gui) if gui > 0 else 0.0
     waves = v.get("SQ_WAVES", 0.0)
     salu = v.get("SQ_INSTS_SALU", 0.0)
-    print("%-56s %9.3f %9.3f %8.1f %9.0f %9.0f" % (k, t * 1e3, ghz, 100 * frac, valu / waves if waves else 0,
-                                                  salu / waves if waves else 0))
+    print("%-56s %9.3f %9s %8.1f %9.0f %9.0f" % (k, t * 1e3, ("%.3f" % ghz) + ("" if k in clk else "*"),
+                                                100 * frac, valu / waves if waves else 0,
+                                                salu / waves if waves else 0))
     n = launches.get(k, 0)
     if len(sys.argv) > 3 and n:
         doc["kernels"][k.split("(")[0].split("::")[-1].split("<")[0] + ("<" + k.split("<")[1].split(">")[0] + ">" if "<" in k else "")] = {
             "launches": n, "ms_per_launch": round(t * 1e3 / n, 4), "clock_ghz": round(ghz, 3),
+            "clock_from": "GRBM_GUI_ACTIVE" if k in clk else "median of the run's >= 0.3 ms kernels",
             "valu_insts_per_sheet": int(valu / n / int(sys.argv[2])), "valu_issue_frac": round(frac, 4),
             "valu_insts_per_wave": round(valu / waves, 1) if waves else None,
             "salu_insts_per_wave": round(salu / waves, 1) if waves else None}
+print("* clock assumed: the median (%.3f GHz) of the kernels of >= %.1f ms a launch" % (long_ghz, LONG_MS))
 if len(sys.argv) > 3:
     with open(sys.argv[3], "w") as f:
         json.dump(doc, f, indent=1)

@@ -59,6 +59,8 @@ def merge_c4(path, out):
             doc = json.load(f)
     except (OSError, ValueError):
         doc = {}
+    if os.environ.get("TRAFFIC_COMMIT"):
+        c4["library_commit"] = os.environ["TRAFFIC_COMMIT"]
     doc["c4"] = c4
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)
@@ -111,6 +113,13 @@ def main():
             doc.setdefault(k, v)
     except (OSError, ValueError):
         pass
+    # the library the passes measured (the GPU box gets no .git: the caller
+    # passes the commit) and the script that ran them
+    for key, env in (("library_commit", "TRAFFIC_COMMIT"), ("script", "TRAFFIC_SCRIPT")):
+        if os.environ.get(env):
+            doc[key] = os.environ[env]
+    if os.environ.get("TRAFFIC_SCRIPT"):
+        doc["source"] = doc["source"].replace("tools/pmc_passes.sh", os.environ["TRAFFIC_SCRIPT"])
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)
     print("%s: fetch %.1f MB (x2 %.1f) + write %.1f MB = %.1f MB/launch vs alg %.1f MB (%.3fx)" %

@@ -627,6 +627,13 @@ __device__ __forceinline__ void check_cursor(const int32_t (&cs)[5], int32_t c, 
 #ifndef UPH_BLACK_PLAN
 #define UPH_BLACK_PLAN 1
 #endif
+// positions a lane reads on one side of a line per scan trip: UPH_BLACK_SPAN
+// windows of 64 (32 lanes a side: 4096 positions a trip at 2)
+#ifndef UPH_BLACK_SPAN
+#define UPH_BLACK_SPAN 2
+#endif
+constexpr int kSpan = UPH_BLACK_SPAN;
+constexpr int kSpanPos = 64 * kSpan;
 struct ChkPlan {
   int32_t start[4], cnt[4], p0[4];  // slot range and first position per line
   int32_t cov;                      // the first check the windows do not reach
@@ -641,19 +648,19 @@ __device__ __forceinline__ ChkPlan check_plan(const Frame& f, const int32_t (&cs
   for (int d = 0; d < 4; d++) {
     pl.p0[d] = d == dc ? pc : 1;
     const int32_t rem = d < dc ? 0 : f.dist[d] - pl.p0[d] + 1;  // positions to read
-    const int32_t need = rem > 0 ? (rem + 63) >> 6 : 0;
+    const int32_t need = rem > 0 ? (rem + kSpanPos - 1) / kSpanPos : 0;
     pl.start[d] = 32 - left;
     pl.cnt[d] = open ? imin(need, left) : 0;
     if (open && need > left) {  // this line runs past the trip's windows
-      pl.cov = cs[d] + 2 * (pl.p0[d] + 64 * left - 1);
+      pl.cov = cs[d] + 2 * (pl.p0[d] + kSpanPos * left - 1);
       open = false;
     }
     left -= pl.cnt[d];
   }
   return pl;
 }
-__device__ __forceinline__ void check_issue_plan(const Sheet& S, Win& w, const Frame& f, const ChkPlan& pl,
-                                                 int* ln_out, int32_t* base_out) {
+__device__ __forceinline__ void check_issue_plan(const Sheet& S, Win (&w)[kSpan], const Frame& f,
+                                                 const ChkPlan& pl, int* ln_out, int32_t* base_out) {
   const int lane = lane_id(), j = lane >> 1, side = lane & 1;
   int ln = -1;
   int32_t base = 0;
@@ -661,38 +668,51 @@ __device__ __forceinline__ void check_issue_plan(const Sheet& S, Win& w, const F
   for (int d = 0; d < 4; d++)
     if (j >= pl.start[d] && j < pl.start[d] + pl.cnt[d]) {
       ln = d;
-      base = pl.p0[d] + 64 * (j - pl.start[d]);
+      base = pl.p0[d] + kSpanPos * (j - pl.start[d]);
     }
-  if (ln >= 0) ray_issue(S, w, ln, f.x, f.y, side == 0 ? 1 : -1, base);
+  if (ln >= 0) {
+#pragma unroll
+    for (int h = 0; h < kSpan; h++) ray_issue(S, w[h], ln, f.x, f.y, side == 0 ? 1 : -1, base + 64 * h);
+  }
   *ln_out = ln;
   *base_out = base;
 }
 // The first matching check in the planned windows (INT_MAX: none, *next =
 // the plan's coverage); *resume as in check_eval.
-__device__ __forceinline__ int32_t check_eval_plan(const Sheet& S, const Win& w, const Frame& f,
+__device__ __forceinline__ int32_t check_eval_plan(const Sheet& S, const Win (&w)[kSpan], const Frame& f,
                                                    const int32_t (&cs)[5], int dc, int32_t sub,
                                                    int32_t pc, const ChkPlan& pl, int ln, int32_t base,
                                                    int32_t* resume, int32_t* next) {
   const int lane = lane_id(), side = lane & 1;
-  uint64_t E = 0;
+  int32_t fpos = INT_MAX;  // the lane's first matching position
+  int nm = 0;              // its matches (0, 1, or 2 = more than one)
   int32_t csd = 0;
   if (ln >= 0) {
-    E = ray_bits(S, w, ln);
-    const int32_t lim = pick4(f.dist, ln) - base + 1;  // this window's positions on the line
-    if (lim < 64) E &= lim > 0 ? (1ull << lim) - 1 : 0;
-    if (ln == dc && side == 0 && base == pc && sub) E &= ~1ull;  // behind the cursor
+    const int32_t dl = pick4(f.dist, ln);
+#pragma unroll
+    for (int h = kSpan - 1; h >= 0; h--) {
+      uint64_t E = ray_bits(S, w[h], ln);
+      const int32_t bh = base + 64 * h;
+      const int32_t lim = dl - bh + 1;  // this window's positions on the line
+      if (lim < 64) E &= lim > 0 ? (1ull << lim) - 1 : 0;
+      if (h == 0 && ln == dc && side == 0 && base == pc && sub) E &= ~1ull;  // behind the cursor
+      if (E) {
+        fpos = bh + ctz64(E);
+        nm += __popcll(E);
+      }
+    }
     csd = ln == 0 ? cs[0] : ln == 1 ? cs[1] : ln == 2 ? cs[2] : cs[3];
   }
   // check index of the lane's first match; slots follow the check order, so
   // the first match is in the lowest slot with one: the smaller of its two
   // sides' first matches
-  const int32_t cl = E ? csd + 2 * (base + ctz64(E) - 1) + side : INT_MAX;
-  const uint64_t hasb = __ballot(E != 0);
+  const int32_t cl = fpos != INT_MAX ? csd + 2 * (fpos - 1) + side : INT_MAX;
+  const uint64_t hasb = __ballot(fpos != INT_MAX);
   *next = pl.cov;
   if (!hasb) return INT_MAX;
   const int l0 = ctz64(hasb) & ~1;
   const int32_t c = imin(__builtin_amdgcn_readlane(cl, l0), __builtin_amdgcn_readlane(cl, l0 + 1));
-  const bool multi = __ballot(__popcll(E) >= 2) != 0 || __popcll(hasb) >= 2;
+  const bool multi = __ballot(nm >= 2) != 0 || __popcll(hasb) >= 2;
   *resume = multi ? c + 1 : pl.cov;
   return c;
 }
@@ -710,7 +730,7 @@ __device__ __forceinline__ int32_t check_scan(const Sheet& S, const Frame& f,
 #if UPH_BLACK_PLAN
     const int32_t pc = pick4(p, dc);
     const ChkPlan pl = check_plan(f, cs, dc, pc);
-    Win w;
+    Win w[kSpan];
     int ln;
     int32_t base;
     check_issue_plan(S, w, f, pl, &ln, &base);
