@@ -432,6 +432,7 @@ __device__ __forceinline__ int32_t window_stop(uint64_t E, int32_t base, int32_t
 // four lines.  In the own planes (row py: [px - dist0, px + dist2], column
 // px: [py - dist1, py + dist3]) a word per lane; in the crossing planes a bit
 // per lane (column words of the row's pixels, row words of the column's).
+template <bool LONG>
 __device__ __forceinline__ void paint_cross(const Sheet& S, int32_t px, int32_t py,
                                             const int32_t (&dist)[4]) {
   const int lane = lane_id();
@@ -440,6 +441,50 @@ __device__ __forceinline__ void paint_cross(const Sheet& S, int32_t px, int32_t 
   const int32_t nrx = dist[0] + dist[2];
   uint64_t *RP = S.RP, *CP = S.CP;
   const int32_t wpr = S.wpr, W = S.W;
+  const int32_t ncross = nrx + dist[1] + dist[3];
+  if (!LONG) {  // the one lane loop over everything (round 5)
+    for (int32_t i0 = 0; i0 < imax(nown, ncross); i0 += 64) {
+      const int32_t i = i0 + lane;
+      if (i < nown) {
+        const bool row = i < nrw;
+        const int32_t lo = row ? xa : ya, hi = row ? xb : yb;
+        const int32_t w = (lo >> 6) + (row ? i : i - nrw);
+        const int a = imax(lo - 64 * w, 0), b = imin(hi - 64 * w, 63);
+        Sheet::por(row ? RP + (int64_t)py * wpr + w : CP + (int64_t)w * W + px,
+                   (~0ull >> (63 - b)) & (~0ull << a));
+      }
+      if (i < nrx) {
+        const int32_t x = i < dist[0] ? px - 1 - i : px + 1 + (i - dist[0]);
+        Sheet::por(CP + (int64_t)(py >> 6) * W + x, 1ull << (py & 63));
+      } else if (i < ncross) {
+        const int32_t j = i - nrx;
+        const int32_t y = j < dist[1] ? py - 1 - j : py + 1 + (j - dist[1]);
+        Sheet::por(RP + (int64_t)y * wpr + (px >> 6), 1ull << (px & 63));
+      }
+    }
+    return;
+  }
+  if (nown <= 64 && ncross <= 64) {
+    // a short cross (the common frame): one lane step does everything
+    const int32_t i = lane;
+    if (i < nown) {
+      const bool row = i < nrw;
+      const int32_t lo = row ? xa : ya, hi = row ? xb : yb;
+      const int32_t w = (lo >> 6) + (row ? i : i - nrw);
+      const int a = imax(lo - 64 * w, 0), b = imin(hi - 64 * w, 63);
+      Sheet::por(row ? RP + (int64_t)py * wpr + w : CP + (int64_t)w * W + px,
+                 (~0ull >> (63 - b)) & (~0ull << a));
+    }
+    if (i < nrx) {
+      const int32_t x = i < dist[0] ? px - 1 - i : px + 1 + (i - dist[0]);
+      Sheet::por(CP + (int64_t)(py >> 6) * W + x, 1ull << (py & 63));
+    } else if (i < ncross) {
+      const int32_t j = i - nrx;
+      const int32_t y = j < dist[1] ? py - 1 - j : py + 1 + (j - dist[1]);
+      Sheet::por(RP + (int64_t)y * wpr + (px >> 6), 1ull << (px & 63));
+    }
+    return;
+  }
   // own planes: a word per lane
   for (int32_t i = lane; i < nown; i += 64) {
     const bool row = i < nrw;
@@ -477,6 +522,7 @@ __device__ __forceinline__ void fill_issue(const Sheet& S, Win& w, int32_t px, i
   const int lane = lane_id();
   ray_issue(S, w, lane >> 4, px, py, 0, 1 + 64 * (lane & 15));
 }
+template <bool LONG>
 __device__ __forceinline__ void fill_cross(const Sheet& S, int32_t px, int32_t py, int32_t (&dist)[4],
                                            Win& w, BlackStats* bs) {
   const int lane = lane_id();
@@ -491,7 +537,38 @@ __device__ __forceinline__ void fill_cross(const Sheet& S, int32_t px, int32_t p
 #pragma unroll
   for (int d = 0; d < 4; d++) carry[d] = 1 - S.I;
   uint32_t done = 0;
-  for (int trip = 0; done != 15; trip++) {
+  {
+    // trip 0: 16 lanes a line, the windows issued with the frame's first
+    // check windows (a short cross ends here)
+    BSTAT(bs->fill_trips++;)
+    const int ln = lane >> 4, k = lane & 15;
+    const int32_t base = 1 + 64 * k;
+    const uint64_t E = ray_bits(S, w, ln);
+    const int32_t lastabs = E ? base + hib64(E) : INT_MIN;
+    const uint64_t hasb = __ballot(E != 0);
+    const uint64_t before = hasb & lane_range(16 * ln, k);
+    const int32_t lsrc = __shfl(lastabs, before ? hib64(before) : lane, 64);
+    const int32_t L = before ? lsrc : 1 - S.I;
+    const int32_t st = window_stop(E, base, L, S.I);
+    const uint64_t stb = __ballot(st != INT_MAX);
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      const uint64_t rng = lane_range(16 * d, 16);
+      int32_t sd = (stb & rng) ? __builtin_amdgcn_readlane(st, ctz64(stb & rng)) : INT_MAX;
+      const int32_t end = 1 + 64 * 16;  // first position not read
+      if (sd == INT_MAX && end > edge[d]) sd = edge[d];
+      if (sd != INT_MAX) {
+        stop[d] = imin(sd, edge[d]);
+        done |= 1u << d;
+      } else {
+        if (hasb & rng) carry[d] = __builtin_amdgcn_readlane(lastabs, hib64(hasb & rng));
+        pos0[d] = end;
+      }
+    }
+  }
+  // later trips: the lines still open share all 64 lanes (one open line:
+  // 4096 positions a trip, two: 2048; three or four: 16 lanes each)
+  while (uni(done) != 15) {
     BSTAT(bs->fill_trips++;)
 #pragma unroll
     for (int d = 0; d < 4; d++) {
@@ -499,21 +576,16 @@ __device__ __forceinline__ void fill_cross(const Sheet& S, int32_t px, int32_t p
       carry[d] = uni(carry[d]);
     }
     done = uni(done);
-    // lanes of line d: [lo[d], lo[d] + cnt[d]); 16 each on the first trip
-    // (issued with the frame's check windows), afterwards the lines still
-    // open share all 64 (one open line: 4096 positions a trip, two: 2048)
     const int nopen = __popc(~done & 15u);
+    const int32_t per = (!LONG || nopen > 2) ? 16 : 64 / nopen;
     int32_t lo[4], cnt[4];
-    {
-      const int32_t per = (trip == 0 || nopen > 2) ? 16 : 64 / nopen;
-      int32_t next = 0;
+    int32_t next = 0;
 #pragma unroll
-      for (int d = 0; d < 4; d++) {
-        const bool open = !((done >> d) & 1);
-        lo[d] = per == 16 ? 16 * d : next;
-        cnt[d] = open ? per : 0;
-        if (open) next += per;
-      }
+    for (int d = 0; d < 4; d++) {
+      const bool open = !((done >> d) & 1);
+      lo[d] = per == 16 ? 16 * d : next;
+      cnt[d] = open ? per : 0;
+      if (open) next += per;
     }
     int mln = -1;
 #pragma unroll
@@ -521,14 +593,14 @@ __device__ __forceinline__ void fill_cross(const Sheet& S, int32_t px, int32_t p
       if (lane >= lo[d] && lane < lo[d] + cnt[d]) mln = d;
     const bool run = mln >= 0;
     const int lnx = run ? mln : 0;
-    const int32_t kk = lane - pick4(lo, lnx);
+    const int32_t lol = pick4(lo, lnx), kk = lane - lol;
     const int32_t base = pick4(pos0, lnx) + 64 * kk;
-    if (trip > 0 && run) ray_issue(S, w, lnx, px, py, 0, base);
+    if (run) ray_issue(S, w, lnx, px, py, 0, base);
     const uint64_t E = run ? ray_bits(S, w, lnx) : 0;
     // the last match of this line's lanes before this one, or the carry
     const int32_t lastabs = E ? base + hib64(E) : INT_MIN;
     const uint64_t hasb = __ballot(E != 0);
-    const uint64_t before = hasb & lane_range(pick4(lo, lnx), kk);
+    const uint64_t before = hasb & lane_range(lol, kk);
     const int32_t lsrc = __shfl(lastabs, before ? hib64(before) : lane, 64);
     const int32_t L = before ? lsrc : pick4(carry, lnx);
     const int32_t st = run ? window_stop(E, base, L, S.I) : INT_MAX;
@@ -717,7 +789,28 @@ __device__ __forceinline__ int32_t check_eval_plan(const Sheet& S, const Win (&w
   return c;
 }
 
+// One planned scan trip, out of line: it is taken for long lines only, and
+// inlined it costs every frame of the replay SGPR spills.
+#ifndef UPH_BLACK_PLAN_NOINLINE
+#define UPH_BLACK_PLAN_NOINLINE 0
+#endif
+#if UPH_BLACK_PLAN_NOINLINE
+__device__ __attribute__((noinline))
+#else
+__device__ __forceinline__
+#endif
+int32_t check_trip_plan(const Sheet& S, const Frame& f, const int32_t (&cs)[5], int dc, int32_t sub,
+                        int32_t pc, int32_t* resume, int32_t* next) {
+  const ChkPlan pl = check_plan(f, cs, dc, pc);
+  Win w[kSpan];
+  int ln;
+  int32_t base;
+  check_issue_plan(S, w, f, pl, &ln, &base);
+  return check_eval_plan(S, w, f, cs, dc, sub, pc, pl, ln, base, resume, next);
+}
+
 // The first matching check of frame f at or after check c, or n (none).
+template <bool LONG>
 __device__ __forceinline__ int32_t check_scan(const Sheet& S, const Frame& f,
                                               const int32_t (&cs)[5], int32_t c, int32_t* resume,
                                               BlackStats* bs) {
@@ -727,21 +820,20 @@ __device__ __forceinline__ int32_t check_scan(const Sheet& S, const Frame& f,
     int dc;
     int32_t p[4], sub;
     check_cursor(cs, c, &dc, p, &sub);
-#if UPH_BLACK_PLAN
     const int32_t pc = pick4(p, dc);
-    const ChkPlan pl = check_plan(f, cs, dc, pc);
-    Win w[kSpan];
-    int ln;
-    int32_t base;
-    check_issue_plan(S, w, f, pl, &ln, &base);
-    int32_t nx;
-    const int32_t r = check_eval_plan(S, w, f, cs, dc, sub, pc, pl, ln, base, resume, &nx);
-#else
-    Win w;
-    check_issue(S, w, f, dc, p, true);
-    int32_t nx;
-    const int32_t r = check_eval(S, w, f, cs, dc, sub, p, resume, &nx);
-#endif
+    int32_t nx, r;
+    // a line the fixed layout (8 windows a side of every line from the
+    // cursor's) cannot finish in this trip: planned slots instead
+    bool longl = pick4(f.dist, dc) - pc + 1 > 64 * kChkWin;
+#pragma unroll
+    for (int d = 0; d < 4; d++) longl |= d > dc && f.dist[d] > 64 * kChkWin;
+    if (LONG && UPH_BLACK_PLAN && longl) {
+      r = check_trip_plan(S, f, cs, dc, sub, pc, resume, &nx);
+    } else {
+      Win w;
+      check_issue(S, w, f, dc, p, true);
+      r = check_eval(S, w, f, cs, dc, sub, p, resume, &nx);
+    }
     if (r != INT_MAX) return r;
     c = uni(nx);
   }
@@ -751,6 +843,7 @@ __device__ __forceinline__ int32_t check_scan(const Sheet& S, const Frame& f,
 // flood_fill (fill.c:81-107) + flood_fill_around_line (fill.c:54-74), depth
 // first with an explicit stack.  The caller has just read (sx, sy) as
 // matching.  Returns false on a stack overflow.
+template <bool LONG>
 __device__ __forceinline__ bool flood(const Sheet& S, int32_t sx, int32_t sy, Frame* stack,
                                       int32_t capacity, BlackStats* bs) {
   Frame top;
@@ -775,7 +868,7 @@ __device__ __forceinline__ bool flood(const Sheet& S, int32_t sx, int32_t sy, Fr
       const int32_t p1[4] = {1, 1, 1, 1};
       check_issue(S, wc, top, 0, p1, false);
       BSTAT(const uint64_t t0 = wall_clock64();)
-      fill_cross(S, nx, ny, top.dist, wf, bs);
+      fill_cross<LONG>(S, nx, ny, top.dist, wf, bs);
       BSTAT(bs->t_fill += wall_clock64() - t0; bs->frames++;)
       cs[0] = 0;
 #pragma unroll
@@ -787,9 +880,9 @@ __device__ __forceinline__ bool flood(const Sheet& S, int32_t sx, int32_t sy, Fr
       // the cross's paints touch none of its checks: issued now, before any
       // later load (this wave's memory operations stay in order)
       BSTAT(const uint64_t tp = wall_clock64();)
-      paint_cross(S, nx, ny, top.dist);
+      paint_cross<LONG>(S, nx, ny, top.dist);
       BSTAT(bs->t_paint += wall_clock64() - tp;)
-      if (c == INT_MAX) c = uni(check_scan(S, top, cs, nxt, &resume, bs));
+      if (c == INT_MAX) c = uni(check_scan<LONG>(S, top, cs, nxt, &resume, bs));
       BSTAT(bs->t_check += wall_clock64() - t1;)
       sp++;
       start = false;
@@ -798,7 +891,7 @@ __device__ __forceinline__ bool flood(const Sheet& S, int32_t sx, int32_t sy, Fr
 #pragma unroll
       for (int d = 0; d < 4; d++) cs[d + 1] = cs[d] + 2 * top.dist[d];
       BSTAT(const uint64_t t1 = wall_clock64();)
-      c = uni(check_scan(S, top, cs, top.cursor, &resume, bs));
+      c = uni(check_scan<LONG>(S, top, cs, top.cursor, &resume, bs));
       BSTAT(bs->t_check += wall_clock64() - t1;)
     }
     if (c >= cs[4]) {
@@ -822,7 +915,7 @@ __device__ __forceinline__ bool flood(const Sheet& S, int32_t sx, int32_t sy, Fr
   }
 }
 
-template <int FMT>
+template <int FMT, bool LONG>
 __global__ void __launch_bounds__(64) k_black_resolve(PlaneRef img, BlackGeom g,
                                                       const BlackBar* bars, uint8_t* scratch,
                                                       int64_t sstride, const int32_t* active,
@@ -963,7 +1056,7 @@ __global__ void __launch_bounds__(64) k_black_resolve(PlaneRef img, BlackGeom g,
         const int hl = ctz64(hit);
         const int32_t fx = __builtin_amdgcn_readlane(sx + (e ? ctz64(e) : 0), hl);
         const int32_t fy = __builtin_amdgcn_readlane(ry, hl);
-        if (!flood(S, fx, fy, stack, g.stack_capacity, bs)) {
+        if (!flood<LONG>(S, fx, fy, stack, g.stack_capacity, bs)) {
           if (lane == 0 && ctl) atomicOr(&ctl[s].status, STATUS_FLOOD_OVERFLOW);
           return;
         }
@@ -1005,10 +1098,24 @@ static void launch_black_t(const PlaneRef& img, const BlackGeom& g, const BlackB
                      dim3(256), 0, st, img, g, scr, ss, active);
   BlackGeom gd = g;
   gd.diag = diag_noise();
-  allow_dynamic_lds((const void*)k_black_resolve<FMT>, kStackLdsBytes);
-  if (!(diag_skip() & 1))
-    hipLaunchKernelGGL(k_black_resolve<FMT>, dim3(count), dim3(64), kStackLdsBytes, st, img, gd,
-                       bars, scr, ss, active, ctl);
+  // LONG: the long-line machinery (open fill lines sharing the wave, planned
+  // two-window scan trips, pointer-walk paints).  Exact either way; chosen by
+  // sheet size as measured: A4 pages (a solid band: ~40 frames of 3508-long
+  // columns) 877 -> ~540 us a 64-sheet launch, while on C4's 70-Mpixel sheets
+  // (floods percolating through specks: ~17k short crosses) its register
+  // pressure made every frame slower (heaviest sheet 75 -> 88 ms).
+  const bool longl = (int64_t)g.W * g.H <= (16 << 20);
+  if (!(diag_skip() & 1)) {
+    if (longl) {
+      allow_dynamic_lds((const void*)k_black_resolve<FMT, true>, kStackLdsBytes);
+      hipLaunchKernelGGL((k_black_resolve<FMT, true>), dim3(count), dim3(64), kStackLdsBytes, st, img, gd,
+                         bars, scr, ss, active, ctl);
+    } else {
+      allow_dynamic_lds((const void*)k_black_resolve<FMT, false>, kStackLdsBytes);
+      hipLaunchKernelGGL((k_black_resolve<FMT, false>), dim3(count), dim3(64), kStackLdsBytes, st, img, gd,
+                         bars, scr, ss, active, ctl);
+    }
+  }
   hipLaunchKernelGGL(k_black_paint<FMT>, dim3((black_wpr(g) + 63) / 64, (g.H + 3) / 4, count),
                      dim3(256), 0, st, img, g, scr, ss, active, FMT == F_GRAY8 ? nbits : nullptr,
                      nbits_stride);

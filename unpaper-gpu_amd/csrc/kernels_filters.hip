@@ -1073,13 +1073,20 @@ static size_t pow2_at_least(size_t n) {
 // 32-pixel words per row of the GRAY8 dark bit-plane
 static int32_t noise_bit_words(const NoiseGeom& g) { return noise_bit_words(g.W); }
 
+// k_noise_group keeps up to 16 triggers a thread in LDS (more: in HBM)
+constexpr int kCapPerThread = 16;
+// Large sheets (C4's 9920 x 7016 double pages: several thousand triggers a
+// sheet, never next to the code-block decode) keep 1024 threads and 16384
+// triggers in LDS.
+static int group_threads(int32_t W, int32_t H) { return (int64_t)W * H > (16 << 20) ? 1024 : 256; }
 size_t noise_scratch_bytes(const NoiseGeom& g) {
   // lists + a global sort buffer for the rare > 8192-trigger sequential case;
   // the GRAY8 dark bit-plane shares the sort buffer's space (it is read by
   // k_noise_classify only, before k_noise_resolve may sort)
-  // (and k_noise_group's keys / roots / last, 3 x 4096 words)
+  // (and k_noise_group's keys / roots / last, 3 x its LDS cap words)
   size_t sort = 4 * pow2_at_least((size_t)g.capacity);
-  if (sort < 12 * 4096) sort = 12 * 4096;
+  const size_t cap3 = 12 * (size_t)kCapPerThread * (size_t)group_threads(g.W, g.H);
+  if (sort < cap3) sort = cap3;
   const size_t bits = 4 * (size_t)noise_bit_words(g) * (size_t)g.H;
   return noise_list_bytes(g) + (sort > bits ? sort : bits);
 }
@@ -2085,13 +2092,10 @@ __device__ __forceinline__ void uf_union(uint32_t* parent, uint32_t a, uint32_t 
   }
 }
 
-constexpr int kCompCap = 4096;  // triggers k_noise_group keeps in LDS (more: in HBM)
-static_assert(kCompCap == 4096, "noise_scratch_bytes reserves 3 x 4096 words for k_noise_group");
 // k_noise_group is one 256-thread block a sheet with ~49 KiB of LDS: a block
 // that needs a whole CU's wave slots and LDS (1024 threads, 147 KiB, round
 // 5) waits for a CU to drain while other streams' kernels keep them busy
 // (84 ms a launch in the JPEG 2000 runner, behind the code-block decode).
-constexpr int kGroupThreads = 256;
 // k_noise_replay blocks per sheet: enough that a lone sheet's components
 // spread over the chip (C2/C4 latency: up to 16384 threads a sheet), few
 // enough that a 64-sheet batch is not mostly blocks that exit (C3): about one
@@ -2131,8 +2135,9 @@ constexpr int kGroupBucketMax = 256;  // longer buckets: block-wide bitonic sort
 constexpr int kLongList = 64;         // long buckets remembered by id (else: all scanned)
 // keys, parents, bucket starts, the scan's wave sums + 3 words, the long
 // bucket list (all dynamic: allow_dynamic_lds raises the limit to 160 KiB)
-constexpr size_t kGroupLds =
-    sizeof(uint32_t) * (2 * (size_t)kCompCap + kNoiseBuckets + 1 + 16 + 3 + kLongList);
+constexpr size_t group_lds(int threads) {
+  return sizeof(uint32_t) * (2 * (size_t)(kCapPerThread * threads) + kNoiseBuckets + 1 + 16 + 3 + kLongList);
+}
 
 __device__ __forceinline__ int noise_bucket_shift(int32_t H) {
   int b = 0;
@@ -2263,13 +2268,15 @@ __device__ __forceinline__ bool nchk(bool ok, int tag, long long idx, unsigned n
 // BIG (n > kCompCap): keys and parents in HBM, else in LDS.  A template
 // parameter, so that every pointer below has one address space (LDS through
 // ds_*, HBM through global_*): no flat accesses to LDS.
-template <int FMT, bool BIG>
+template <int FMT, int T, bool BIG>
 __device__ __forceinline__ void noise_group_sheet(const NoiseGeom& g, const NoisePtrs& NP, uint32_t* gk,
                                                   uint32_t* glds, uint8_t* base, int64_t pitch,
                                                   uint32_t* flag, uint32_t n) {
   const int N = g.intensity;
   const int tid = threadIdx.x;
   const bool big = BIG;
+  constexpr int kCompCap = kCapPerThread * T;
+  constexpr int kGroupThreads = T;
   uint32_t* keys = big ? gk : glds;         // the sorted keys
   uint32_t* cur = glds + kCompCap;          // scatter cursors, then the long-bucket stage
   uint32_t* bc = glds + 2 * kCompCap;       // bucket starts (nb + 1)
@@ -2439,11 +2446,12 @@ __device__ __forceinline__ void noise_group_sheet(const NoiseGeom& g, const Nois
   if (tid == 0) *flag = kNoiseBig;
 }
 
-template <int FMT>
-__global__ void __launch_bounds__(kGroupThreads) k_noise_group(PlaneRef img, NoiseGeom g, uint8_t* scratch,
+template <int FMT, int T>
+__global__ void __launch_bounds__(T) k_noise_group(PlaneRef img, NoiseGeom g, uint8_t* scratch,
                                                                int64_t sstride, const int32_t* active,
                                                                SheetCtl* ctl, uint32_t* sortbuf,
                                                                int64_t sort_stride) {
+  constexpr int kCompCap = kCapPerThread * T;
   const int s = blockIdx.x;
   if (active && !active[s]) return;
   NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
@@ -2474,15 +2482,16 @@ __global__ void __launch_bounds__(kGroupThreads) k_noise_group(PlaneRef img, Noi
     return;
   }
   if (n > (uint32_t)kCompCap)
-    noise_group_sheet<FMT, true>(g, NP, gk, glds, base, pitch, flag, n);
+    noise_group_sheet<FMT, T, true>(g, NP, gk, glds, base, pitch, flag, n);
   else
-    noise_group_sheet<FMT, false>(g, NP, gk, glds, base, pitch, flag, n);
+    noise_group_sheet<FMT, T, false>(g, NP, gk, glds, base, pitch, flag, n);
 }
 
 template <int FMT>
 __global__ void __launch_bounds__(256) k_noise_replay(PlaneRef img, NoiseGeom g, uint8_t* scratch,
                                                       int64_t sstride, const int32_t* active,
-                                                      const uint32_t* sortbuf, int64_t sort_stride) {
+                                                      const uint32_t* sortbuf, int64_t sort_stride,
+                                                      int kCompCap) {
   const int s = blockIdx.y;
   if (active && !active[s]) return;
   NoisePtrs NP = noise_ptrs(g, scratch + s * sstride);
@@ -2550,12 +2559,19 @@ static void launch_noise_t(const PlaneRef& img, const NoiseGeom& g, uint8_t* scr
                      bits, bstride);
   hipLaunchKernelGGL(k_noise_apply<FMT>, dim3(64, count), dim3(256), 0, st, img, g, scr, ss,
                      active, ctl);
-  allow_dynamic_lds((const void*)k_noise_group<FMT>, kGroupLds);
+  const int gt = group_threads(g.W, g.H);
   if (!(diag_skip() & 2)) {
-    hipLaunchKernelGGL(k_noise_group<FMT>, dim3(count), dim3(kGroupThreads), kGroupLds, st, img, gd, scr,
-                       ss, active, ctl, sortbuf, sort_stride);
+    if (gt == 1024) {
+      allow_dynamic_lds((const void*)k_noise_group<FMT, 1024>, group_lds(1024));
+      hipLaunchKernelGGL((k_noise_group<FMT, 1024>), dim3(count), dim3(1024), group_lds(1024), st, img, gd,
+                         scr, ss, active, ctl, sortbuf, sort_stride);
+    } else {
+      allow_dynamic_lds((const void*)k_noise_group<FMT, 256>, group_lds(256));
+      hipLaunchKernelGGL((k_noise_group<FMT, 256>), dim3(count), dim3(256), group_lds(256), st, img, gd,
+                         scr, ss, active, ctl, sortbuf, sort_stride);
+    }
     hipLaunchKernelGGL(k_noise_replay<FMT>, dim3(replay_blocks(count), count), dim3(256), 0, st, img, g,
-                       scr, ss, active, sortbuf, sort_stride);
+                       scr, ss, active, sortbuf, sort_stride, kCapPerThread * gt);
   }
 }
 
