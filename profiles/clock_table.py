@@ -35,19 +35,23 @@ launches = collections.Counter()
 if kt:
     for r in csv.DictReader(open(kt[0])):
         launches[r["Kernel_Name"][:56]] += 1
-# GRBM_GUI_ACTIVE / 8 / wall time is the effective clock only for dispatches
-# of about 0.3 ms or more (MI355X_MICROARCH.md, DVFS give-back: it reads high
-# on shorter ones).  Shorter kernels get the median clock of the long ones in
-# the same run ("assumed" in the table), so no clock above the chip's 2.4 GHz
-# is reported and their VALU fraction is not understated.
-LONG_MS = 0.3
+# GRBM_GUI_ACTIVE / 8 / wall time is the effective clock only for long
+# dispatches (MI355X_MICROARCH.md, DVFS give-back: it reads high below about
+# 0.3 ms and is within 3 % from 10 ms up); a kernel of a few waves keeps the
+# GUI busy as long as it runs and reads high too.  A kernel's own figure is
+# used only from dispatches of >= 0.5 ms that come out at or below the chip's
+# 2.4 GHz; every other kernel gets the median of those ("*" in the table), so
+# no clock above 2.4 GHz is reported and no VALU fraction is understated.
+LONG_MS, MAX_GHZ = 0.5, 2.4
 clk = {}
 for k, v in agg.items():
     t = dur.get(k, 0.0)
     n = launches.get(k, 0) or 1
     if t > 0 and t * 1e3 / n >= LONG_MS:
-        clk[k] = v.get("GRBM_GUI_ACTIVE", 0.0) / 8 / t / 1e9
-long_ghz = sorted(clk.values())[len(clk) // 2] if clk else 2.4
+        ghz = v.get("GRBM_GUI_ACTIVE", 0.0) / 8 / t / 1e9
+        if 0 < ghz <= MAX_GHZ:
+            clk[k] = ghz
+long_ghz = min(sorted(clk.values())[len(clk) // 2], MAX_GHZ) if clk else MAX_GHZ
 print("%-56s %9s %9s %8s %9s %9s" % ("kernel", "dur_ms", "GHz", "VALU%", "VALU/wave", "SALU/wave"))
 for k, v in sorted(agg.items(), key=lambda kv: -dur.get(kv[0], 0)):
     t = dur.get(k, 0.0)
@@ -64,11 +68,12 @@ for k, v in sorted(agg.items(), key=lambda kv: -dur.get(kv[0], 0)):
     if len(sys.argv) > 3 and n:
         doc["kernels"][k.split("(")[0].split("::")[-1].split("<")[0] + ("<" + k.split("<")[1].split(">")[0] + ">" if "<" in k else "")] = {
             "launches": n, "ms_per_launch": round(t * 1e3 / n, 4), "clock_ghz": round(ghz, 3),
-            "clock_from": "GRBM_GUI_ACTIVE" if k in clk else "median of the run's >= 0.3 ms kernels",
+            "clock_from": "GRBM_GUI_ACTIVE" if k in clk else "assumed: median of the run's measured kernels",
             "valu_insts_per_sheet": int(valu / n / int(sys.argv[2])), "valu_issue_frac": round(frac, 4),
             "valu_insts_per_wave": round(valu / waves, 1) if waves else None,
             "salu_insts_per_wave": round(salu / waves, 1) if waves else None}
-print("* clock assumed: the median (%.3f GHz) of the kernels of >= %.1f ms a launch" % (long_ghz, LONG_MS))
+print("* clock assumed: the median (%.3f GHz) of the kernels measured at >= %.1f ms a launch and <= %.1f GHz"
+      % (long_ghz, LONG_MS, MAX_GHZ))
 if len(sys.argv) > 3:
     with open(sys.argv[3], "w") as f:
         json.dump(doc, f, indent=1)
