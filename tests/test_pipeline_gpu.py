@@ -303,6 +303,38 @@ def test_filter_parameters(hip, oracle):
     check(oracle, opts, [[synth(*SMALL, 3)], [synth(*SMALL, 4)]], "filters")
 
 
+def speckled(w, h, page, per_rect, seed):
+    """Synthetic page `page` over its top half; below, blank paper holding
+    isolated black specks (the noisefilter clears them) and specks at the
+    white threshold 229 (dark for the blurfilter only) at `per_rect` per
+    100x100 blurfilter block, near the default wipe threshold of 100, plus a
+    solid bar on the left edge (the blackfilter paints it): the blurfilter's
+    block counts hold only if its bit-plane lost what the other two cleared."""
+    g = synth_page_host(w, h, page).copy()
+    rng = np.random.default_rng(seed)
+    y0 = h // 2
+    g[y0:] = 255
+    area = (h - y0) * w // 10000
+    for val, n in ((0, 150 * area), (229, per_rect * area)):
+        ys, xs = rng.integers(y0, h, n), rng.integers(0, w, n)
+        g[ys, xs] = val
+    g[y0:, 0:60] = 0
+    return HostImage.from_array(g, A.FMT_GRAY8, abs_black_threshold=170)
+
+
+@pytest.mark.parametrize("white", [229, 255])
+def test_blur_counts_after_noise_and_black_clears(hip, oracle, white):
+    # the fused GRAY8 decode's blurfilter bit-plane (pixel <= white), kept by
+    # the blackfilter's paint and the noisefilter's clears (off at white 255:
+    # a cleared pixel would still count); the grayfilter, which would wipe
+    # the blocks anyway, is off
+    opts = oracle.default_options()
+    opts.abs_white_threshold = white
+    opts.disable |= A.NO_GRAYFILTER
+    sheets = [[speckled(*SMALL, p, k, 10 * p + k)] for p, k in ((3, 40), (0, 70), (3, 90), (5, 110))]
+    check(oracle, opts, sheets, "blur bits")
+
+
 def test_noisefilter_sequential_intensity(hip, oracle):
     opts = oracle.default_options()
     opts.noisefilter_intensity = 6

@@ -42,8 +42,13 @@ struct BlurGeom {
 bool blur_geometry(int32_t W, int32_t H, const UphipBlurfilterParameters& p, uint8_t white,
                    BlurGeom* g);
 size_t blur_scratch_bytes(const BlurGeom& g);
+// bbits (optional): the GRAY8 bit-plane of pixels <= white of the image as it
+// stands (k_decode_gray made it, the blackfilter and noisefilter kept it
+// current), bb_stride words per sheet: the block counts then read it instead
+// of the plane (1/8 of the bytes).
 void launch_blurfilter(const PlaneRef& img, const BlurGeom& g, void* scratch,
-                       int64_t scratch_stride, const int32_t* active, int count, hipStream_t st);
+                       int64_t scratch_stride, const int32_t* active, int count, hipStream_t st,
+                       const uint32_t* bbits = nullptr, int64_t bb_stride = 0);
 
 // ---- noisefilter (filters.c:238-338) ------------------------------------
 struct NoiseGeom {
@@ -53,6 +58,10 @@ struct NoiseGeom {
   int32_t capacity;    // entries per list per sheet
   int32_t all_seq;
   int32_t diag;        // TEMP timing diagnostics
+  // optional: the blurfilter's GRAY8 bit-plane (pixel <= white, k_decode_gray),
+  // bb_stride words per sheet; every clear of the filter clears its bit too
+  uint32_t* bbits;
+  int64_t bb_stride;
 };
 bool noise_geometry(int32_t W, int32_t H, uint64_t intensity, uint8_t white, NoiseGeom* g);
 size_t noise_scratch_bytes(const NoiseGeom& g);
@@ -124,13 +133,16 @@ void launch_blackfilter_impl(const PlaneRef& img, const BlackGeom& g, const Blac
                              void* scratch, int64_t ss, const int32_t* active, SheetCtl* ctl,
                              int count, hipStream_t st, const AxisArgs* hargs,
                              const AxisArgs* vargs, bool vsum_ready = false,
-                             uint32_t* nbits = nullptr, int64_t nbits_stride = 0);
+                             uint32_t* nbits = nullptr, int64_t nbits_stride = 0,
+                             uint32_t* bbits = nullptr, int64_t bb_stride = 0);
 // GRAY8 page -> sheet plane (same size), plus on the way: the noisefilter's
 // dark bit-plane (pixel < white) and the blackfilter's v-stripe row sums over
 // columns [vx0, vx1] (vsum: H entries per sheet after W, vx0 > vx1 = none).
 // Pages 16-byte aligned with a 16-multiple pitch.
+// bbits (optional): also the blurfilter's plane of pixels <= white, same layout
 void launch_decode_gray(const uint8_t* src, int64_t spitch, int64_t sstride, const PlaneRef& dst,
                         uint8_t white, uint32_t* bits, int64_t bits_stride, uint32_t* vsum,
-                        int64_t vsum_stride, int32_t vx0, int32_t vx1, int count, hipStream_t st);
+                        int64_t vsum_stride, int32_t vx0, int32_t vx1, int count, hipStream_t st,
+                        uint32_t* bbits = nullptr);
 
 }  // namespace uph

@@ -209,7 +209,8 @@ __global__ void __launch_bounds__(256) k_black_planes(PlaneRef img, BlackGeom g,
 template <int FMT>
 __global__ void __launch_bounds__(256) k_black_paint(PlaneRef img, BlackGeom g, uint8_t* scratch,
                                                      int64_t sstride, const int32_t* active,
-                                                     uint32_t* nbits, int64_t nbits_stride) {
+                                                     uint32_t* nbits, int64_t nbits_stride,
+                                                     uint32_t* bbits, int64_t bb_stride) {
   const int s = blockIdx.z;
   if (active && !active[s]) return;
   uint8_t* scr = scratch + s * sstride;
@@ -243,6 +244,12 @@ __global__ void __launch_bounds__(256) k_black_paint(PlaneRef img, BlackGeom g, 
     uint32_t* nb = nbits + s * nbits_stride + (int64_t)y * nwr + 2 * xw;
     nb[0] &= ~(uint32_t)p;
     if (2 * xw + 1 < nwr) nb[1] &= ~(uint32_t)(p >> 32);
+  }
+  if (FMT == F_GRAY8 && bbits) {  // the blurfilter's plane (pixel <= white < 255)
+    const int32_t nwr = (g.W + 31) >> 5;
+    uint32_t* bb = bbits + s * bb_stride + (int64_t)y * nwr + 2 * xw;
+    bb[0] &= ~(uint32_t)p;
+    if (2 * xw + 1 < nwr) bb[1] &= ~(uint32_t)(p >> 32);
   }
 }
 
@@ -1086,7 +1093,7 @@ static void launch_black_t(const PlaneRef& img, const BlackGeom& g, const BlackB
                            uint8_t* scr, int64_t ss, const int32_t* active, SheetCtl* ctl,
                            int count, hipStream_t st, const AxisArgs* hargs,
                            const AxisArgs* vargs, bool vsum_ready, uint32_t* nbits,
-                           int64_t nbits_stride) {
+                           int64_t nbits_stride, uint32_t* bbits, int64_t bb_stride) {
   // column sums of max(rgb) over the h-stripe rows, row sums over the v-stripe cols
   if (g.hregion.x1 >= g.hregion.x0 && g.hregion.y1 >= g.hregion.y0)
     launch_axis_reduce(img, hargs, 0, M_DARKINV_SUM, g.W, g.H, (uint32_t*)scr, ss / 4, count, st);
@@ -1118,7 +1125,7 @@ static void launch_black_t(const PlaneRef& img, const BlackGeom& g, const BlackB
   }
   hipLaunchKernelGGL(k_black_paint<FMT>, dim3((black_wpr(g) + 63) / 64, (g.H + 3) / 4, count),
                      dim3(256), 0, st, img, g, scr, ss, active, FMT == F_GRAY8 ? nbits : nullptr,
-                     nbits_stride);
+                     nbits_stride, FMT == F_GRAY8 ? bbits : nullptr, bb_stride);
 }
 
 __global__ void k_black_prep(uint8_t* scr, int64_t ss, int32_t words, int count) {
@@ -1133,21 +1140,21 @@ void launch_blackfilter_impl(const PlaneRef& img, const BlackGeom& g, const Blac
                              void* scratch, int64_t ss, const int32_t* active, SheetCtl* ctl,
                              int count, hipStream_t st, const AxisArgs* hargs,
                              const AxisArgs* vargs, bool vsum_ready, uint32_t* nbits,
-                             int64_t nbits_stride) {
+                             int64_t nbits_stride, uint32_t* bbits, int64_t bb_stride) {
   uint8_t* scr = (uint8_t*)scratch;
   hipLaunchKernelGGL(k_black_prep, dim3(8, count), dim3(256), 0, st, scr, ss, g.W, count);
   switch (img.P.fmt) {
     case F_GRAY8:
       launch_black_t<F_GRAY8>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs,
-                              vsum_ready, nbits, nbits_stride);
+                              vsum_ready, nbits, nbits_stride, bbits, bb_stride);
       break;
     case F_Y400A:
       launch_black_t<F_Y400A>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs,
-                              vsum_ready, nbits, nbits_stride);
+                              vsum_ready, nbits, nbits_stride, bbits, bb_stride);
       break;
     default:
       launch_black_t<F_RGB24>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs,
-                              vsum_ready, nbits, nbits_stride);
+                              vsum_ready, nbits, nbits_stride, bbits, bb_stride);
       break;
   }
 }

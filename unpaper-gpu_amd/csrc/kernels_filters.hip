@@ -529,6 +529,61 @@ __global__ void __launch_bounds__(256) k_blur_counts_g(PlaneRef img, BlurGeom g,
   }
 }
 
+// k_blur_counts_g from the bit-plane of pixels <= white (1/8 of the plane's
+// bytes; NoiseGeom::bbits, kept current by the black- and noisefilter's
+// clears).  Rectangles at least 32 wide, so a 32-pixel word meets at most two
+// of them: a lane per (word column, row phase) keeps two popcount sums over
+// its rows of the strip, then adds them into per-rectangle LDS counters.
+__global__ void __launch_bounds__(256) k_blur_counts_bits(BlurGeom g, const uint32_t* bbits,
+                                                          int64_t bb_stride, uint8_t* scratch,
+                                                          int64_t sstride, const int32_t* active) {
+  const int s = blockIdx.y;
+  if (active && !active[s]) return;
+  const int32_t row = blockIdx.x;
+  const int32_t ry = row == 0 ? 0 : (row - 1) * g.sh + g.step_y;
+  const int32_t y0 = imax(ry, 0), y1 = imin(ry + g.sh, g.H);
+  const int32_t nr = row == 0 ? g.bpr : g.bpr + 1;
+  const int32_t nwr = (g.W + 31) >> 5;
+  extern __shared__ uint32_t rcount[];
+  for (int32_t j = threadIdx.x; j < nr + 1; j += 256) rcount[j] = 0;
+  __syncthreads();
+  const uint32_t* plane = bbits + s * bb_stride;
+  const int32_t nph = nwr >= 256 ? 1 : 256 / nwr;  // row phases
+  const int32_t lanes = nph * nwr;
+  for (int32_t t = threadIdx.x; t < (nwr >= 256 ? nwr : lanes); t += 256) {
+    const int32_t wi = nwr >= 256 ? t : t % nwr, ph = nwr >= 256 ? 0 : t / nwr;
+    const int32_t x0 = 32 * wi;
+    const int32_t j0 = x0 / g.sw;
+    // bits [0, cut) of a word belong to rectangle j0, [cut, 32) to j0 + 1
+    const int32_t cut = imin((j0 + 1) * g.sw - x0, 32);
+    const uint32_t m0 = cut >= 32 ? ~0u : (1u << cut) - 1u;
+    uint32_t a0 = 0, a1 = 0;
+    const uint32_t* col = plane + wi;
+    int32_t y = y0 + ph;
+    for (; y + 3 * nph < y1; y += 4 * nph) {
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) v[k] = col[(int64_t)(y + k * nph) * nwr];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        a0 += __popc(v[k] & m0);
+        a1 += __popc(v[k] & ~m0);
+      }
+    }
+    for (; y < y1; y += nph) {
+      const uint32_t v = col[(int64_t)y * nwr];
+      a0 += __popc(v & m0);
+      a1 += __popc(v & ~m0);
+    }
+    if (a0 && j0 < nr) atomicAdd(&rcount[j0], a0);
+    if (a1 && j0 + 1 < nr) atomicAdd(&rcount[j0 + 1], a1);
+  }
+  __syncthreads();
+  uint32_t* counts = (uint32_t*)(scratch + s * sstride);
+  for (int32_t j = threadIdx.x; j < nr; j += 256)
+    counts[row == 0 ? j : g.bpr + (row - 1) * (g.bpr + 1) + j] = rcount[j];
+}
+
 template <int FMT>
 __global__ void __launch_bounds__(256) k_blur_counts(PlaneRef img, BlurGeom g, uint8_t* scratch,
                                                      int64_t sstride, const int32_t* active) {
@@ -977,11 +1032,15 @@ __global__ void __launch_bounds__(256) k_blur_wipe(PlaneRef img, BlurGeom g, uin
 
 template <int FMT>
 static void launch_blur_t(const PlaneRef& img, const BlurGeom& g, uint8_t* scr, int64_t ss,
-                          const int32_t* active, int count, hipStream_t st) {
+                          const int32_t* active, int count, hipStream_t st, const uint32_t* bbits,
+                          int64_t bb_stride) {
   const auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   const bool v16 = img.P.pitch % 16 == 0 && img.P.stride % 16 == 0 && img.P.pitch >= ((g.W + 15) & ~15) &&
                    a16(img.P.base[0]) && a16(img.P.base[1]);
-  if (g.nrect > 0 && FMT == F_GRAY8 && g.sh <= 65535 && g.W <= (1 << 16) && v16)
+  if (g.nrect > 0 && FMT == F_GRAY8 && bbits && g.sw >= 32 && g.W <= (1 << 16))
+    UPH_LAUNCH_DIAG(64, k_blur_counts_bits, dim3(1 + g.T, count), dim3(256),
+                    4 * (size_t)(g.bpr + 2), st, g, bbits, bb_stride, scr, ss, active);
+  else if (g.nrect > 0 && FMT == F_GRAY8 && g.sh <= 65535 && g.W <= (1 << 16) && v16)
     UPH_LAUNCH_DIAG(64, k_blur_counts_g<true>, dim3(1 + g.T, count), dim3(256),
                     2 * (size_t)((g.W + 3) & ~3), st, img, g, scr, ss, active);
   else if (g.nrect > 0 && FMT == F_GRAY8 && g.sh <= 65535 && g.W <= (1 << 16))
@@ -1006,12 +1065,17 @@ static void launch_blur_t(const PlaneRef& img, const BlurGeom& g, uint8_t* scr, 
 }
 
 void launch_blurfilter(const PlaneRef& img, const BlurGeom& g, void* scratch,
-                       int64_t scratch_stride, const int32_t* active, int count, hipStream_t st) {
+                       int64_t scratch_stride, const int32_t* active, int count, hipStream_t st,
+                       const uint32_t* bbits, int64_t bb_stride) {
   uint8_t* scr = (uint8_t*)scratch;
   switch (img.P.fmt) {
-    case F_GRAY8: launch_blur_t<F_GRAY8>(img, g, scr, scratch_stride, active, count, st); break;
-    case F_Y400A: launch_blur_t<F_Y400A>(img, g, scr, scratch_stride, active, count, st); break;
-    default: launch_blur_t<F_RGB24>(img, g, scr, scratch_stride, active, count, st); break;
+    case F_GRAY8:
+      launch_blur_t<F_GRAY8>(img, g, scr, scratch_stride, active, count, st, bbits, bb_stride);
+      break;
+    case F_Y400A:
+      launch_blur_t<F_Y400A>(img, g, scr, scratch_stride, active, count, st, nullptr, 0);
+      break;
+    default: launch_blur_t<F_RGB24>(img, g, scr, scratch_stride, active, count, st, nullptr, 0); break;
   }
 }
 
@@ -1055,6 +1119,8 @@ bool noise_geometry(int32_t W, int32_t H, uint64_t intensity, uint8_t white, Noi
   int64_t cap = g->all_seq ? (int64_t)W * H + 64 : ((int64_t)W * H) / 4 + 1024;
   if (cap > (1 << 27)) cap = 1 << 27;
   g->capacity = (int32_t)cap;
+  g->bbits = nullptr;
+  g->bb_stride = 0;
   return true;
 }
 
@@ -1239,7 +1305,7 @@ __global__ void __launch_bounds__(256) k_noise_bits(PlaneRef img, NoiseGeom g, u
 __global__ void __launch_bounds__(256) k_decode_gray(const uint8_t* src, int64_t spitch,
                                                      int64_t sstride, PlaneRef dst, uint8_t white,
                                                      uint32_t* bits, int64_t bstride, int32_t nwr,
-                                                     float rnwr) {
+                                                     float rnwr, uint32_t* bbits) {
   const int s = blockIdx.y;
   const Planes& P = dst.P;
   const int32_t t = blockIdx.x * 256 + threadIdx.x;
@@ -1256,6 +1322,8 @@ __global__ void __launch_bounds__(256) k_decode_gray(const uint8_t* src, int64_t
   const uint4 b = x0 + 16 < P.W ? *reinterpret_cast<const uint4*>(srow + x0 + 16)
                                 : make_uint4(~0u, ~0u, ~0u, ~0u);
   uint32_t m = dark_bits32({a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}, white);
+  // the blurfilter's bits: pixel <= white (byte < white + 1)
+  uint32_t mb = bbits ? dark_bits32({a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}, (uint32_t)white + 1u) : 0u;
   if (x0 + 32 <= P.W) {
     *reinterpret_cast<uint4*>(d) = a;
     *reinterpret_cast<uint4*>(d + 16) = b;
@@ -1264,6 +1332,7 @@ __global__ void __launch_bounds__(256) k_decode_gray(const uint8_t* src, int64_t
     // dwords and the last dword's bytes
     const int32_t n = P.W - x0;
     m &= (1u << n) - 1u;
+    mb &= (1u << n) - 1u;
     uint4 q = a;
     int32_t j = 0;
     if (n >= 16) {
@@ -1279,6 +1348,7 @@ __global__ void __launch_bounds__(256) k_decode_gray(const uint8_t* src, int64_t
     for (int32_t i = j + (r & ~3); i < n; i++, last >>= 8) d[i] = (uint8_t)last;
   }
   if (bits) bits[s * bstride + t] = m;
+  if (bbits) bbits[s * bstride + t] = mb;
 }
 
 // The blackfilter's v-stripe row sums (darkness_rect's sums over the stripe's
@@ -1333,11 +1403,13 @@ __global__ void __launch_bounds__(256) k_stripe_sums(const uint8_t* src, int64_t
 
 void launch_decode_gray(const uint8_t* src, int64_t spitch, int64_t sstride, const PlaneRef& dst,
                         uint8_t white, uint32_t* bits, int64_t bits_stride, uint32_t* vsum,
-                        int64_t vsum_stride, int32_t vx0, int32_t vx1, int count, hipStream_t st) {
+                        int64_t vsum_stride, int32_t vx0, int32_t vx1, int count, hipStream_t st,
+                        uint32_t* bbits) {
   const int32_t nwr = (dst.P.W + 31) >> 5;
   const int64_t words = (int64_t)nwr * dst.P.H;
   UPH_LAUNCH_DIAG(262144, k_decode_gray, dim3((unsigned)((words + 255) / 256), count), dim3(256), 0, st,
-                     src, spitch, sstride, dst, white, bits, bits_stride, nwr, 1.0f / (float)nwr);
+                     src, spitch, sstride, dst, white, bits, bits_stride, nwr, 1.0f / (float)nwr,
+                     bbits);
   if (vsum && vx0 <= vx1)
     hipLaunchKernelGGL(k_stripe_sums,
                        dim3((unsigned)((dst.P.H + 4 * kStripeRowsPerWave - 1) / (4 * kStripeRowsPerWave)),
@@ -1827,6 +1899,14 @@ __global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGe
 }
 
 template <int FMT>
+__device__ __forceinline__ uint32_t* sheet_bb(const NoiseGeom& g, int s) {
+  return FMT == F_GRAY8 && g.bbits ? g.bbits + s * g.bb_stride : nullptr;
+}
+__device__ __forceinline__ void bb_clear(uint32_t* bb, int32_t W, int32_t x, int32_t y) {
+  if (bb) atomicAnd(bb + (int64_t)y * ((W + 31) >> 5) + (x >> 5), ~(1u << (x & 31)));
+}
+
+template <int FMT>
 __global__ void __launch_bounds__(256) k_noise_apply(PlaneRef img, NoiseGeom g, uint8_t* scratch,
                                                      int64_t sstride, const int32_t* active,
                                                      SheetCtl* ctl) {
@@ -1839,9 +1919,11 @@ __global__ void __launch_bounds__(256) k_noise_apply(PlaneRef img, NoiseGeom g, 
     return;
   }
   uint8_t* base = plane_ptr(img, s);
+  uint32_t* bb = sheet_bb<FMT>(g, s);
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const uint32_t k = NP.clear[i];
     white_px<FMT>(base + (int64_t)(k >> 16) * img.P.pitch, (int32_t)(k & 0xFFFF));
+    bb_clear(bb, g.W, (int32_t)(k & 0xFFFF), (int32_t)(k >> 16));
   }
 }
 
@@ -1932,6 +2014,8 @@ __device__ __forceinline__ Mask81 ring_part(int L, bool rows) {
   return m;
 }
 
+// The blurfilter's GRAY8 bit-plane (pixel <= white, NoiseGeom::bbits) follows
+// a clear: the sheet's plane `bb` (null: none), bit x of row y.
 // One trigger of the raster replay for intensity N <= 4 (filters.c:309-338):
 // the 9x9 window read from the frame (dark = lightness < white), rings with
 // the reference loops' unsigned comparisons -- rows of ring L counted iff
@@ -1939,7 +2023,8 @@ __device__ __forceinline__ Mask81 ring_part(int L, bool rows) {
 template <int FMT>
 __device__ __forceinline__ void replay_trigger4(int32_t x, int32_t y, int N, const NoiseGeom& g,
                                                 uint8_t* base, int64_t pitch,
-                                                const Mask81 (&rowp)[5], const Mask81 (&colp)[5]) {
+                                                const Mask81 (&rowp)[5], const Mask81 (&colp)[5],
+                                                uint32_t* bb) {
   uint64_t dlo = 0;
   uint32_t dhi = 0;
   bool ctr = false;
@@ -2039,6 +2124,7 @@ __device__ __forceinline__ void replay_trigger4(int32_t x, int32_t y, int N, con
   if (count > N) return;
   // the centre and rings 1..k-1 are cleared
   white_px<FMT>(base + (int64_t)y * pitch, x);
+  bb_clear(bb, g.W, x, y);
 #pragma unroll
   for (int Lc = 1; Lc <= 3; Lc++) {
     if (Lc >= k) continue;
@@ -2048,11 +2134,13 @@ __device__ __forceinline__ void replay_trigger4(int32_t x, int32_t y, int N, con
       const int p = __ffsll((long long)clo) - 1;
       clo &= clo - 1;
       white_px<FMT>(base + (int64_t)(y + p / 9 - 4) * pitch, x + p % 9 - 4);
+      bb_clear(bb, g.W, x + p % 9 - 4, y + p / 9 - 4);
     }
     while (chi) {
       const int p = 64 + __ffs(chi) - 1;
       chi &= chi - 1;
       white_px<FMT>(base + (int64_t)(y + p / 9 - 4) * pitch, x + p % 9 - 4);
+      bb_clear(bb, g.W, x + p % 9 - 4, y + p / 9 - 4);
     }
   }
 }
@@ -2152,7 +2240,7 @@ __device__ __forceinline__ int noise_bucket_shift(int32_t H) {
 // global sort buffer).
 template <int FMT>
 __device__ void noise_raster_replay(uint32_t* keys, int n, int p2, const NoiseGeom& g, const NoisePtrs& NP,
-                                    uint8_t* base, int64_t pitch) {
+                                    uint8_t* base, int64_t pitch, uint32_t* bb) {
   for (int i = threadIdx.x; i < p2; i += blockDim.x) keys[i] = i < n ? NP.seq[i] : 0xFFFFFFFFu;
   __threadfence_block();
   __syncthreads();
@@ -2205,6 +2293,7 @@ __device__ void noise_raster_replay(uint32_t* keys, int n, int p2, const NoiseGe
         if (pos >= area || Lv[h] >= k || (Lv[h] > 0 && !dk[h])) continue;
         const int32_t qx = x + pos % side - N, qy = y + pos / side - N;
         white_px<FMT>(base + (int64_t)qy * pitch, qx);
+        bb_clear(bb, g.W, qx, qy);
       }
     }
     return;
@@ -2238,7 +2327,10 @@ __device__ void noise_raster_replay(uint32_t* keys, int n, int p2, const NoiseGe
     if (count > N) continue;
     // centre + rings 1..k-1 (the loop stopped at the first empty ring k)
     const int k = level - 1;
-    if (lane == 0) white_px<FMT>(base + (int64_t)y * pitch, x);
+    if (lane == 0) {
+      white_px<FMT>(base + (int64_t)y * pitch, x);
+      bb_clear(bb, g.W, x, y);
+    }
     for (int L = 1; L < k; L++) {
       for (int b = 0; b < 8 * L; b += 64) {
         int dx, dy;
@@ -2246,7 +2338,10 @@ __device__ void noise_raster_replay(uint32_t* keys, int n, int p2, const NoiseGe
         const int32_t qx = x + dx, qy = y + dy;
         if (qx < 0 || qy < 0 || qx >= g.W || qy >= g.H) continue;
         uint8_t* row = base + (int64_t)qy * pitch;
-        if (light_of(load_px_row<FMT>(row, qx)) < g.white) white_px<FMT>(row, qx);
+        if (light_of(load_px_row<FMT>(row, qx)) < g.white) {
+          white_px<FMT>(row, qx);
+          bb_clear(bb, g.W, qx, qy);
+        }
       }
     }
     __threadfence_block();
@@ -2271,7 +2366,7 @@ __device__ __forceinline__ bool nchk(bool ok, int tag, long long idx, unsigned n
 template <int FMT, int T, bool BIG>
 __device__ __forceinline__ void noise_group_sheet(const NoiseGeom& g, const NoisePtrs& NP, uint32_t* gk,
                                                   uint32_t* glds, uint8_t* base, int64_t pitch,
-                                                  uint32_t* flag, uint32_t n) {
+                                                  uint32_t* flag, uint32_t n, uint32_t* bb) {
   const int N = g.intensity;
   const int tid = threadIdx.x;
   const bool big = BIG;
@@ -2344,7 +2439,7 @@ __device__ __forceinline__ void noise_group_sheet(const NoiseGeom& g, const Nois
     int p2 = 1;
     while (p2 < (int)n) p2 <<= 1;
     if (tid == 0) *flag = kNoiseNothing;
-    noise_raster_replay<FMT>(gk, (int)n, p2, g, NP, base, pitch);
+    noise_raster_replay<FMT>(gk, (int)n, p2, g, NP, base, pitch, bb);
     return;
   }
   for (int i = tid; i < (int)n; i += kGroupThreads) {
@@ -2473,18 +2568,19 @@ __global__ void __launch_bounds__(T) k_noise_group(PlaneRef img, NoiseGeom g, ui
   extern __shared__ uint32_t glds[];
   uint8_t* base = plane_ptr(img, s);
   const int64_t pitch = img.P.pitch;
+  uint32_t* bb = sheet_bb<FMT>(g, s);
   if (N > 4) {  // intensity > 4: every trigger, one wave in raster order
     int p2 = 1;
     while (p2 < (int)n) p2 <<= 1;
     if (tid == 0) *flag = kNoiseNothing;
-    if (p2 <= kCompCap) noise_raster_replay<FMT>(glds, (int)n, p2, g, NP, base, pitch);
-    else noise_raster_replay<FMT>(gk, (int)n, p2, g, NP, base, pitch);
+    if (p2 <= kCompCap) noise_raster_replay<FMT>(glds, (int)n, p2, g, NP, base, pitch, bb);
+    else noise_raster_replay<FMT>(gk, (int)n, p2, g, NP, base, pitch, bb);
     return;
   }
   if (n > (uint32_t)kCompCap)
-    noise_group_sheet<FMT, T, true>(g, NP, gk, glds, base, pitch, flag, n);
+    noise_group_sheet<FMT, T, true>(g, NP, gk, glds, base, pitch, flag, n, bb);
   else
-    noise_group_sheet<FMT, T, false>(g, NP, gk, glds, base, pitch, flag, n);
+    noise_group_sheet<FMT, T, false>(g, NP, gk, glds, base, pitch, flag, n, bb);
 }
 
 template <int FMT>
@@ -2508,6 +2604,7 @@ __global__ void __launch_bounds__(256) k_noise_replay(PlaneRef img, NoiseGeom g,
     colp[L] = ring_part(L, false);
   }
   uint8_t* base = plane_ptr(img, s);
+  uint32_t* bb = sheet_bb<FMT>(g, s);
   // a few blocks per sheet walk its triggers (sheets hold far fewer triggers
   // than kCompCap: a grid sized for the cap was mostly blocks that exit)
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)n; i += gridDim.x * blockDim.x) {
@@ -2518,7 +2615,7 @@ __global__ void __launch_bounds__(256) k_noise_replay(PlaneRef img, NoiseGeom g,
       const uint32_t key = keys[j];
       __threadfence_block();  // this thread's earlier clears are visible to its loads
       replay_trigger4<FMT>((int32_t)(key & 0xFFFF), (int32_t)(key >> 16), g.intensity, g, base,
-                           img.P.pitch, rowp, colp);
+                           img.P.pitch, rowp, colp, bb);
     }
   }
 }

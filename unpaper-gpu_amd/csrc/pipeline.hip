@@ -464,7 +464,8 @@ struct UphipBatch {
   int32_t* rot_indep = nullptr;        // two-mask launch: mask 1 independent of deskew 0
   int32_t* rot_dep = nullptr;          // ... or redone after it
   uint32_t* nbits = nullptr;           // GRAY8 noisefilter dark bit-plane (k_decode_gray)
-  int64_t nbits_stride = 0;            // words per sheet
+  int64_t nbits_stride = 0;            // words per sheet (also bbits')
+  uint32_t* bbits = nullptr;           // GRAY8 blurfilter bit-plane, pixel <= white (k_decode_gray)
   MoveArgs* move_args = nullptr;      // cap * MAX_PAGES
   int32_t* border_need = nullptr;     // cap: the chained border scan needs the middle rows
   MaskArgs* border_mask_args = nullptr;
@@ -765,6 +766,13 @@ static bool allocate(UphipBatch* b) {
     if (!blur_geometry(W, H, o.blurfilter_parameters, o.abs_white_threshold, &b->blgeo))
       return fail("batch: invalid blurfilter parameters");
     need = std::max(need, blur_scratch_bytes(b->blgeo));
+    // the bit-plane stays exact only while every clear makes a pixel > white
+    if (b->work_fmt == F_GRAY8 && o.abs_white_threshold < 255 && b->blgeo.nrect > 0 &&
+        b->blgeo.sw >= 32) {
+      b->nbits_stride = ((int64_t)noise_bit_words(W) * H + 63) & ~(int64_t)63;
+      b->bbits = dalloc<uint32_t>(b, (size_t)b->nbits_stride * cap);
+      if (!b->bbits) return false;
+    }
   }
   if (!(o.disable & UPHIP_NO_GRAYFILTER)) {
     if (!gray_geometry(W, H, o.grayfilter_parameters, o.abs_black_threshold, &b->ggeo))
@@ -1239,10 +1247,17 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
   const bool black_on = !(dis & UPHIP_NO_BLACKFILTER) && b->bgeo.nbars > 0;
   const bool vsum_ready = fused && black_on && b->bgeo.vregion.x1 >= b->bgeo.vregion.x0;
   uint32_t* bits_ready = fused && !(dis & UPHIP_NO_NOISEFILTER) ? b->nbits : nullptr;
+  // the blurfilter's plane: made by the decode, kept by the black/noise clears
+#ifndef UPH_NO_BLUR_BITS
+  uint32_t* bb_ready = fused && !(dis & UPHIP_NO_BLURFILTER) ? b->bbits : nullptr;
+#else  // tuning A/B: the blur counts read the plane
+  uint32_t* bb_ready = nullptr;
+#endif
   if (fused) {
     launch_decode_gray(src, spitch, sstride, cur_ref(S0, b->ctl), o.abs_white_threshold, bits_ready,
                        b->nbits_stride, vsum_ready ? (uint32_t*)b->scr + b->bgeo.W : nullptr,
-                       b->scr_stride / 4, b->bgeo.vregion.x0, b->bgeo.vregion.x1, count, b->st);
+                       b->scr_stride / 4, b->bgeo.vregion.x0, b->bgeo.vregion.x1, count, b->st,
+                       bb_ready);
   }
   if (!covered) fill_uniform(b, S0, 0, Rect{0, 0, w - 1, h - 1}, o.sheet_background, count);
   for (int j = 0; j < n && !fused; j++) {
@@ -1325,16 +1340,20 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
   if (!(dis & UPHIP_NO_BLACKFILTER) && b->bgeo.nbars > 0) {
     launch_blackfilter_impl(cur_ref(P, b->ctl), b->bgeo, b->dbars, b->scr, b->scr_stride, nullptr,
                             b->ctl, count, b->st, b->black_h, b->black_v, vsum_ready, bits_ready,
-                            b->nbits_stride);
+                            b->nbits_stride, bb_ready, b->nbits_stride);
     mark(b, "blackfilter");
   }
   if (!(dis & UPHIP_NO_NOISEFILTER)) {
-    launch_noisefilter(cur_ref(P, b->ctl), b->ngeo, b->scr, b->scr_stride, nullptr, b->ctl, count,
+    NoiseGeom ng = b->ngeo;
+    ng.bbits = bb_ready;
+    ng.bb_stride = b->nbits_stride;
+    launch_noisefilter(cur_ref(P, b->ctl), ng, b->scr, b->scr_stride, nullptr, b->ctl, count,
                        b->st, bits_ready, b->nbits_stride);
     mark(b, "noisefilter");
   }
   if (!(dis & UPHIP_NO_BLURFILTER)) {
-    launch_blurfilter(cur_ref(P, b->ctl), b->blgeo, b->scr, b->scr_stride, nullptr, count, b->st);
+    launch_blurfilter(cur_ref(P, b->ctl), b->blgeo, b->scr, b->scr_stride, nullptr, count, b->st,
+                      bb_ready, b->nbits_stride);
     mark(b, "blurfilter");
   }
   bool mask_sums_ready = false;
