@@ -1582,10 +1582,20 @@ __device__ __forceinline__ f2 splat2(float v) { return f2{v, v}; }
 // (the result is an integer-valued float).  The integer-valued terms are
 // formed from the differences ba = b-a, ca = c-a, da = d-a:
 //   2a-5b+4c-d = -5ba + 4ca - da,   3(b-c)+d-a = 3(ba-ca) + da
+// The integer coefficients of cubic_scale (interpolate.c:24-31) for taps
+// a..d, exact in fp32 (|values| <= 1530), in six packed operations:
+//   ca = c - a,  s2 = 3(b - c) + (d - a),  s1 = 2a - 5b + 4c - d
+//                                         = -5(b - c) - ((d - a) + (c - a))
+__device__ __forceinline__ void cubic_terms(f2 a, f2 b, f2 c, f2 d, f2& ca, f2& s1, f2& s2) {
+  const f2 e = d - a, g = b - c;
+  ca = c - a;
+  s2 = fma2(splat2(3.0f), g, e);
+  s1 = fma2(splat2(-5.0f), g, -(e + ca));
+}
+
 __device__ __forceinline__ f2 cubic2(f2 f, f2 h, f2 a, f2 b, f2 c, f2 d) {
-  const f2 ba = b - a, ca = c - a, da = d - a;                                   // exact
-  const f2 s1 = fma2(splat2(-5.0f), ba, fma2(splat2(4.0f), ca, -da));            // exact
-  const f2 s2 = fma2(splat2(3.0f), ba - ca, da);                                 // exact
+  f2 ca, s1, s2;
+  cubic_terms(a, b, c, d, ca, s1, s2);  // exact
   const f2 u = s1 + f * s2;
   const f2 v = ca + f * u;
   const f2 r = b + h * v;
@@ -1863,11 +1873,8 @@ __device__ __forceinline__ void lds_wait_pair_after(f2 (&t)[4], f2& prev) {
 
 // one packed row cubic (rows 2q, 2q+1 of one pixel), clamped like cubic_scale
 __device__ __forceinline__ f2 cubic2_row(f2 f, f2 h, const f2 (&t)[4]) {
-  const f2 ba = t[1] - t[0], ca = t[2] - t[0], da = t[3] - t[0];
-  f2 s1 = fma2(splat2(4.0f), ca, -da);  // exact
-  f2 s2 = ba - ca;
-  s1 = fma2(splat2(-5.0f), ba, s1);     // exact
-  s2 = fma2(splat2(3.0f), s2, da);      // exact
+  f2 ca, s1, s2;
+  cubic_terms(t[0], t[1], t[2], t[3], ca, s1, s2);  // exact
   f2 u = f * s2;
   u = s1 + u;
   u = f * u;
@@ -1883,21 +1890,9 @@ __device__ __forceinline__ f2 cubic2_row(f2 f, f2 h, const f2 (&t)[4]) {
 __device__ __forceinline__ void cubic2x2(f2 f, f2 h, const f2 (&t0)[4], const f2 (&t1)[4],
                                          f2& out0, f2& out1) {
   const f2* t[2] = {t0, t1};
-  f2 ba[2], ca[2], da[2], s1[2], s2[2], u[2];
+  f2 ca[2], s1[2], s2[2], u[2];
 #pragma unroll
-  for (int i = 0; i < 2; i++) {
-    ba[i] = t[i][1] - t[i][0];
-    ca[i] = t[i][2] - t[i][0];
-    da[i] = t[i][3] - t[i][0];
-  }
-#pragma unroll
-  for (int i = 0; i < 2; i++) s1[i] = fma2(splat2(4.0f), ca[i], -da[i]);                // exact
-#pragma unroll
-  for (int i = 0; i < 2; i++) s2[i] = ba[i] - ca[i];
-#pragma unroll
-  for (int i = 0; i < 2; i++) s1[i] = fma2(splat2(-5.0f), ba[i], s1[i]);                // exact
-#pragma unroll
-  for (int i = 0; i < 2; i++) s2[i] = fma2(splat2(3.0f), s2[i], da[i]);                 // exact
+  for (int i = 0; i < 2; i++) cubic_terms(t[i][0], t[i][1], t[i][2], t[i][3], ca[i], s1[i], s2[i]);  // exact
 #pragma unroll
   for (int i = 0; i < 2; i++) u[i] = f * s2[i];
 #pragma unroll
