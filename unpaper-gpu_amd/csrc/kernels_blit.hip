@@ -1872,7 +1872,7 @@ __device__ __forceinline__ void lds_wait_pair_after(f2 (&t)[4], f2& prev) {
 }
 
 // one packed row cubic (rows 2q, 2q+1 of one pixel), clamped like cubic_scale
-__device__ __forceinline__ f2 cubic2_row(f2 f, f2 h, const f2 (&t)[4]) {
+__device__ __forceinline__ f2 cubic2_row_u(f2 f, f2 h, const f2 (&t)[4]) {
   f2 ca, s1, s2;
   cubic_terms(t[0], t[1], t[2], t[3], ca, s1, s2);  // exact
   f2 u = f * s2;
@@ -1880,35 +1880,11 @@ __device__ __forceinline__ f2 cubic2_row(f2 f, f2 h, const f2 (&t)[4]) {
   u = f * u;
   u = ca + u;
   u = h * u;
-  u = t[1] + u;
-  return f2{__builtin_amdgcn_fmed3f(__builtin_truncf(u.x), 0.0f, 255.0f),
-            __builtin_amdgcn_fmed3f(__builtin_truncf(u.y), 0.0f, 255.0f)};
+  return t[1] + u;
 }
-
-// cubic2 on two independent pairs, step by step, so the dependent packed
-// operations of one chain interleave with the other's.
-__device__ __forceinline__ void cubic2x2(f2 f, f2 h, const f2 (&t0)[4], const f2 (&t1)[4],
-                                         f2& out0, f2& out1) {
-  const f2* t[2] = {t0, t1};
-  f2 ca[2], s1[2], s2[2], u[2];
-#pragma unroll
-  for (int i = 0; i < 2; i++) cubic_terms(t[i][0], t[i][1], t[i][2], t[i][3], ca[i], s1[i], s2[i]);  // exact
-#pragma unroll
-  for (int i = 0; i < 2; i++) u[i] = f * s2[i];
-#pragma unroll
-  for (int i = 0; i < 2; i++) u[i] = s1[i] + u[i];
-#pragma unroll
-  for (int i = 0; i < 2; i++) u[i] = f * u[i];
-#pragma unroll
-  for (int i = 0; i < 2; i++) u[i] = ca[i] + u[i];
-#pragma unroll
-  for (int i = 0; i < 2; i++) u[i] = h * u[i];
-#pragma unroll
-  for (int i = 0; i < 2; i++) u[i] = t[i][1] + u[i];
-  out0 = f2{__builtin_amdgcn_fmed3f(__builtin_truncf(u[0].x), 0.0f, 255.0f),
-            __builtin_amdgcn_fmed3f(__builtin_truncf(u[0].y), 0.0f, 255.0f)};
-  out1 = f2{__builtin_amdgcn_fmed3f(__builtin_truncf(u[1].x), 0.0f, 255.0f),
-            __builtin_amdgcn_fmed3f(__builtin_truncf(u[1].y), 0.0f, 255.0f)};
+// cubic_scale's truncation and clamp of one result
+__device__ __forceinline__ float clamp_t255(float u) {
+  return __builtin_amdgcn_fmed3f(__builtin_truncf(u), 0.0f, 255.0f);
 }
 
 // v from the lane given by the quad permutation CTRL (DPP quad_perm)
@@ -2338,18 +2314,21 @@ __global__ void __launch_bounds__(kRFT, UPH_ROT_MINB) k_rotate_cubic_g8f(PlaneRe
       // rows (0,1) and (2,3) of A once its eight tap pairs are in, then of B
       const f2 FA = splat2(fxA), HA = splat2(0.5f * fxA);
       const f2 FB = splat2(fxB), HB = splat2(0.5f * fxB);
-      f2 c[4];
+      f2 c[4];  // unclamped row results; clamped straight into the column pairs
       lds_wait_pair<12>(t[0]);
-      c[0] = cubic2_row(FA, HA, t[0]);
+      c[0] = cubic2_row_u(FA, HA, t[0]);
       lds_wait_pair_after<8>(t[1], c[0]);
-      c[1] = cubic2_row(FA, HA, t[1]);
+      c[1] = cubic2_row_u(FA, HA, t[1]);
       lds_wait_pair_after<4>(t[2], c[1]);
-      c[2] = cubic2_row(FB, HB, t[2]);
+      c[2] = cubic2_row_u(FB, HB, t[2]);
       lds_wait_pair_after<0>(t[3], c[2]);
-      c[3] = cubic2_row(FB, HB, t[3]);
+      c[3] = cubic2_row_u(FB, HB, t[3]);
       // the column cubic of A and B as one pair
-      const f2 o = cubic2(f2{fyA, fyB}, f2{0.5f * fyA, 0.5f * fyB}, f2{c[0].x, c[2].x},
-                          f2{c[0].y, c[2].y}, f2{c[1].x, c[3].x}, f2{c[1].y, c[3].y});
+      const f2 o = cubic2(f2{fyA, fyB}, f2{0.5f * fyA, 0.5f * fyB},
+                          f2{clamp_t255(c[0].x), clamp_t255(c[2].x)},
+                          f2{clamp_t255(c[0].y), clamp_t255(c[2].y)},
+                          f2{clamp_t255(c[1].x), clamp_t255(c[3].x)},
+                          f2{clamp_t255(c[1].y), clamp_t255(c[3].y)});
       oA = (uint32_t)o.x;  // integer-valued in [0, 255]
       oB = (uint32_t)o.y;
       }
