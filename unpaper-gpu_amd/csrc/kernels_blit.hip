@@ -1882,6 +1882,25 @@ __device__ __forceinline__ f2 cubic2_row_u(f2 f, f2 h, const f2 (&t)[4]) {
   u = h * u;
   return t[1] + u;
 }
+// cubic2_row_u on two independent pairs step by step, so the dependent
+// packed operations of one chain fill the other's wait states
+__device__ __forceinline__ void cubic2_row_u2(f2 f0, f2 h0, const f2 (&t0)[4], f2 f1, f2 h1,
+                                              const f2 (&t1)[4], f2& o0, f2& o1) {
+  f2 ca0, s10, s20, ca1, s11, s21;
+  cubic_terms(t0[0], t0[1], t0[2], t0[3], ca0, s10, s20);
+  cubic_terms(t1[0], t1[1], t1[2], t1[3], ca1, s11, s21);
+  f2 u0 = f0 * s20, u1 = f1 * s21;
+  u0 = s10 + u0;
+  u1 = s11 + u1;
+  u0 = f0 * u0;
+  u1 = f1 * u1;
+  u0 = ca0 + u0;
+  u1 = ca1 + u1;
+  u0 = h0 * u0;
+  u1 = h1 * u1;
+  o0 = t0[1] + u0;
+  o1 = t1[1] + u1;
+}
 // cubic_scale's truncation and clamp of one result
 __device__ __forceinline__ float clamp_t255(float u) {
   return __builtin_amdgcn_fmed3f(__builtin_truncf(u), 0.0f, 255.0f);
@@ -1916,6 +1935,11 @@ __device__ __forceinline__ uint32_t row_off(int32_t y, int64_t pitch) {
 #endif
 #ifndef UPH_ROT_EARLY
 #define UPH_ROT_EARLY 1  // 0: the column-sum zero barrier in every tile (round-4 form)
+#endif
+#ifndef UPH_ROT_PAIRS
+// 1: a pixel's two row pairs interleaved after one wait (fewer wait states,
+// less overlap with the tap reads: A/B 0.99 vs 0.975 ms a launch, kept off)
+#define UPH_ROT_PAIRS 0
 #endif
 #ifndef UPH_ROT_UNIFORM
 #define UPH_ROT_UNIFORM 0  // 1: skip wave rows of uniform 4x4 windows (A/B: see DESIGN §5)
@@ -2315,6 +2339,13 @@ __global__ void __launch_bounds__(kRFT, UPH_ROT_MINB) k_rotate_cubic_g8f(PlaneRe
       const f2 FA = splat2(fxA), HA = splat2(0.5f * fxA);
       const f2 FB = splat2(fxB), HB = splat2(0.5f * fxB);
       f2 c[4];  // unclamped row results; clamped straight into the column pairs
+#if UPH_ROT_PAIRS
+      // A's two row pairs interleaved once its eight tap pairs are in, then B's
+      lds_wait_pairs<8>(t[0], t[1]);
+      cubic2_row_u2(FA, HA, t[0], FA, HA, t[1], c[0], c[1]);
+      lds_wait_pairs<0>(t[2], t[3]);
+      cubic2_row_u2(FB, HB, t[2], FB, HB, t[3], c[2], c[3]);
+#else
       lds_wait_pair<12>(t[0]);
       c[0] = cubic2_row_u(FA, HA, t[0]);
       lds_wait_pair_after<8>(t[1], c[0]);
@@ -2323,6 +2354,7 @@ __global__ void __launch_bounds__(kRFT, UPH_ROT_MINB) k_rotate_cubic_g8f(PlaneRe
       c[2] = cubic2_row_u(FB, HB, t[2]);
       lds_wait_pair_after<0>(t[3], c[2]);
       c[3] = cubic2_row_u(FB, HB, t[3]);
+#endif
       // the column cubic of A and B as one pair
       const f2 o = cubic2(f2{fyA, fyB}, f2{0.5f * fyA, 0.5f * fyB},
                           f2{clamp_t255(c[0].x), clamp_t255(c[2].x)},
