@@ -974,6 +974,9 @@ constexpr int kChainBp = 17;  // 7 of the align move and mask + 2 x 5 of the cen
 #ifndef UPH_CHAIN_WAVES
 #define UPH_CHAIN_WAVES 4
 #endif
+#ifndef UPH_CHAIN_OCC
+#define UPH_CHAIN_OCC 1  // waves per SIMD the register budget must allow
+#endif
 constexpr int kChainThreads = 64 * UPH_CHAIN_WAVES;
 constexpr int kChainRows = kMoveRows * UPH_CHAIN_WAVES;  // rows per block (kMoveRows a wave)
 static_assert(kChainThreads >= kChainBp, "a thread per breakpoint");
@@ -996,7 +999,7 @@ __device__ __forceinline__ int2 chain_cell(const ChainSheet& c, int32_t W, int32
   return make_int2(-1, (int32_t)((int64_t)(sy - y) * pitch + (sx - x)));
 }
 
-__global__ void __launch_bounds__(kChainThreads) k_move_chain_g16(PlaneRef src, PlaneRef dst,
+__global__ void __launch_bounds__(kChainThreads, UPH_CHAIN_OCC) k_move_chain_g16(PlaneRef src, PlaneRef dst,
                                                              const MoveArgs* center,
                                                              const MaskArgs* masks,
                                                              const MoveArgs* align) {
@@ -1022,10 +1025,10 @@ __global__ void __launch_bounds__(kChainThreads) k_move_chain_g16(PlaneRef src, 
   __shared__ int32_t dv[kChainBp + 1];  // vectors holding a breakpoint (+ the row's partial one)
   __shared__ uint8_t live[kChainBp], imap[kChainBp + 1];
   __shared__ int2 cell[kChainRows][kChainBp + 1];
+  __shared__ int32_t b[kChainBp];  // thread 0's candidate list (LDS, not scratch)
   if (threadIdx.x == 0) {
     // the columns where some stage's class can change (first column of the
     // new interval), sorted, unique, inside (0, W)
-    int32_t b[kChainBp];
     int n = 0;
     auto add = [&](int32_t v) {
       if (v > 0 && v < W) b[n++] = v;
@@ -1109,7 +1112,7 @@ __global__ void __launch_bounds__(kChainThreads) k_move_chain_g16(PlaneRef src, 
   nbp = nbp_s;
   int32_t bpr[kChainBp];  // the breakpoints in registers (INT_MAX past nbp)
 #pragma unroll
-  for (int k = 0; k < kChainBp; k++) bpr[k] = bp[k];
+  for (int k = 0; k < kChainBp; k++) bpr[k] = __builtin_amdgcn_readfirstlane(bp[k]);  // uniform: SGPRs
   auto interval = [&](int32_t x) {
     int i = 0;
 #pragma unroll
@@ -1120,7 +1123,10 @@ __global__ void __launch_bounds__(kChainThreads) k_move_chain_g16(PlaneRef src, 
   const int32_t nv = (W + 15) >> 4;
   const int r0 = (threadIdx.x >> 6) * kMoveRows;  // the wave's rows of the block
   // uniform vectors: lanes along the row, the wave's kMoveRows rows
-  constexpr int kG = 4;  // rows whose loads are in flight together
+#ifndef UPH_CHAIN_KG
+#define UPH_CHAIN_KG 4
+#endif
+  constexpr int kG = UPH_CHAIN_KG;  // rows whose loads are in flight together
   for (int32_t vi = lane; vi < nv; vi += 64) {
     const int32_t x0 = 16 * vi;
     const int il = interval(x0);

@@ -1537,8 +1537,11 @@ __device__ __forceinline__ SmallVerdict small_verdict(const uint32_t (*drow)[4],
 
 constexpr int kListCap = 1024;  // LDS work list of one tile (else: row loops)
 
+#ifndef UPH_CLASSIFY_OCC
+#define UPH_CLASSIFY_OCC 8
+#endif
 template <int FMT>
-__global__ void __launch_bounds__(256, 8) k_noise_classify(PlaneRef img, NoiseGeom g, uint8_t* scratch,
+__global__ void __launch_bounds__(256, UPH_CLASSIFY_OCC) k_noise_classify(PlaneRef img, NoiseGeom g, uint8_t* scratch,
                                                         int64_t sstride, const int32_t* active,
                                                         SheetCtl* ctl, const uint32_t* bits,
                                                         int64_t bstride) {
