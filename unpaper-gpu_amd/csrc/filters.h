@@ -134,15 +134,24 @@ void launch_blackfilter_impl(const PlaneRef& img, const BlackGeom& g, const Blac
                              int count, hipStream_t st, const AxisArgs* hargs,
                              const AxisArgs* vargs, bool vsum_ready = false,
                              uint32_t* nbits = nullptr, int64_t nbits_stride = 0,
-                             uint32_t* bbits = nullptr, int64_t bb_stride = 0);
+                             uint32_t* bbits = nullptr, int64_t bb_stride = 0,
+                             bool rm_ready = false);
+// The blackfilter's row-major match plane (RM: bit x of row y = gray <=
+// mask_max, 64-bit words, black_wpr words a row) of sheet 0 inside its
+// scratch; sheet s at + s * scratch_stride bytes.  k_decode_gray can write it
+// (launch_blackfilter_impl's rm_ready).
+uint32_t* black_rm_plane(const BlackGeom& g, void* scratch);
 // GRAY8 page -> sheet plane (same size), plus on the way: the noisefilter's
 // dark bit-plane (pixel < white) and the blackfilter's v-stripe row sums over
 // columns [vx0, vx1] (vsum: H entries per sheet after W, vx0 > vx1 = none).
 // Pages 16-byte aligned with a 16-multiple pitch.
 // bbits (optional): also the blurfilter's plane of pixels <= white, same layout
+// rm (optional): also the blackfilter's RM plane (pixel <= rm_max; rows of
+// 2 * ceil(W / 64) words, rm_stride words a sheet, black_rm_plane)
 void launch_decode_gray(const uint8_t* src, int64_t spitch, int64_t sstride, const PlaneRef& dst,
                         uint8_t white, uint32_t* bits, int64_t bits_stride, uint32_t* vsum,
                         int64_t vsum_stride, int32_t vx0, int32_t vx1, int count, hipStream_t st,
-                        uint32_t* bbits = nullptr);
+                        uint32_t* bbits = nullptr, uint32_t* rm = nullptr, int64_t rm_stride = 0,
+                        uint8_t rm_max = 0);
 
 }  // namespace uph

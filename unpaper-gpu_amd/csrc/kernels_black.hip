@@ -156,7 +156,9 @@ __device__ __forceinline__ bool sheet_has_candidate(const BlackGeom& g, const ui
 // makes row word t & 3 of row t >> 2 (M from the image, P clear; a row's
 // four words from 256 contiguous bytes), then the column word of column t
 // from the 64 row words in LDS.  Both planes are written in whole lines.
-template <int FMT>
+// RM_READY: the decode wrote RM (GRAY8 page = sheet, nothing between): the
+// row words are read from it instead of from the image.
+template <int FMT, bool RM_READY>
 __global__ void __launch_bounds__(256) k_black_planes(PlaneRef img, BlackGeom g, uint8_t* scratch,
                                                       int64_t sstride, const int32_t* active) {
   const int s = blockIdx.z;
@@ -168,7 +170,13 @@ __global__ void __launch_bounds__(256) k_black_planes(PlaneRef img, BlackGeom g,
   const int t = threadIdx.x, r = t >> 2, q = t & 3;
   const int32_t xw = 4 * blockIdx.x + q, y = 64 * blockIdx.y + r, x0 = 64 * xw;
   uint64_t m = 0;
-  if (y < g.H && xw < wpr) {
+  if (RM_READY) {
+    if (y < g.H && xw < wpr) {
+      const int64_t i = (int64_t)y * wpr + xw;
+      m = ((const uint64_t*)(scr + black_rm_off(g)))[i];
+      ((uint64_t*)(scr + black_rp_off(g)))[i] = 0;
+    }
+  } else if (y < g.H && xw < wpr) {
     const uint8_t* row = plane_ptr(img, s) + (int64_t)y * img.P.pitch;
     if (FMT == F_GRAY8 && x0 + 64 <= g.W && ((uintptr_t)(row + x0) & 15) == 0) {
 #pragma unroll
@@ -1093,7 +1101,8 @@ static void launch_black_t(const PlaneRef& img, const BlackGeom& g, const BlackB
                            uint8_t* scr, int64_t ss, const int32_t* active, SheetCtl* ctl,
                            int count, hipStream_t st, const AxisArgs* hargs,
                            const AxisArgs* vargs, bool vsum_ready, uint32_t* nbits,
-                           int64_t nbits_stride, uint32_t* bbits, int64_t bb_stride) {
+                           int64_t nbits_stride, uint32_t* bbits, int64_t bb_stride,
+                           bool rm_ready) {
   // column sums of max(rgb) over the h-stripe rows, row sums over the v-stripe cols
   if (g.hregion.x1 >= g.hregion.x0 && g.hregion.y1 >= g.hregion.y0)
     launch_axis_reduce(img, hargs, 0, M_DARKINV_SUM, g.W, g.H, (uint32_t*)scr, ss / 4, count, st);
@@ -1101,8 +1110,12 @@ static void launch_black_t(const PlaneRef& img, const BlackGeom& g, const BlackB
     launch_axis_reduce(img, vargs, 1, M_DARKINV_SUM, g.vregion.x1 - g.vregion.x0 + 1, g.H,
                        (uint32_t*)scr + g.W, ss / 4, count, st);
   hipLaunchKernelGGL(k_black_cand, dim3(count), dim3(kCandThreads), 0, st, g, bars, scr, ss, active);
-  hipLaunchKernelGGL(k_black_planes<FMT>, dim3((black_wpr(g) + 3) / 4, black_hpc(g), count),
-                     dim3(256), 0, st, img, g, scr, ss, active);
+  if (FMT == F_GRAY8 && rm_ready)
+    hipLaunchKernelGGL((k_black_planes<FMT, true>), dim3((black_wpr(g) + 3) / 4, black_hpc(g), count),
+                       dim3(256), 0, st, img, g, scr, ss, active);
+  else
+    hipLaunchKernelGGL((k_black_planes<FMT, false>), dim3((black_wpr(g) + 3) / 4, black_hpc(g), count),
+                       dim3(256), 0, st, img, g, scr, ss, active);
   BlackGeom gd = g;
   gd.diag = diag_noise();
   // LONG: the long-line machinery (open fill lines sharing the wave, planned
@@ -1128,6 +1141,10 @@ static void launch_black_t(const PlaneRef& img, const BlackGeom& g, const BlackB
                      nbits_stride, FMT == F_GRAY8 ? bbits : nullptr, bb_stride);
 }
 
+uint32_t* black_rm_plane(const BlackGeom& g, void* scratch) {
+  return (uint32_t*)((uint8_t*)scratch + black_rm_off(g));
+}
+
 __global__ void k_black_prep(uint8_t* scr, int64_t ss, int32_t words, int count) {
   // zero the column sums (atomic accumulation) of every sheet
   const int s = blockIdx.y;
@@ -1140,21 +1157,22 @@ void launch_blackfilter_impl(const PlaneRef& img, const BlackGeom& g, const Blac
                              void* scratch, int64_t ss, const int32_t* active, SheetCtl* ctl,
                              int count, hipStream_t st, const AxisArgs* hargs,
                              const AxisArgs* vargs, bool vsum_ready, uint32_t* nbits,
-                             int64_t nbits_stride, uint32_t* bbits, int64_t bb_stride) {
+                             int64_t nbits_stride, uint32_t* bbits, int64_t bb_stride,
+                             bool rm_ready) {
   uint8_t* scr = (uint8_t*)scratch;
   hipLaunchKernelGGL(k_black_prep, dim3(8, count), dim3(256), 0, st, scr, ss, g.W, count);
   switch (img.P.fmt) {
     case F_GRAY8:
       launch_black_t<F_GRAY8>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs,
-                              vsum_ready, nbits, nbits_stride, bbits, bb_stride);
+                              vsum_ready, nbits, nbits_stride, bbits, bb_stride, rm_ready);
       break;
     case F_Y400A:
       launch_black_t<F_Y400A>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs,
-                              vsum_ready, nbits, nbits_stride, bbits, bb_stride);
+                              vsum_ready, nbits, nbits_stride, bbits, bb_stride, rm_ready);
       break;
     default:
       launch_black_t<F_RGB24>(img, g, bars, scr, ss, active, ctl, count, st, hargs, vargs,
-                              vsum_ready, nbits, nbits_stride, bbits, bb_stride);
+                              vsum_ready, nbits, nbits_stride, bbits, bb_stride, rm_ready);
       break;
   }
 }

@@ -1305,7 +1305,8 @@ __global__ void __launch_bounds__(256) k_noise_bits(PlaneRef img, NoiseGeom g, u
 __global__ void __launch_bounds__(256) k_decode_gray(const uint8_t* src, int64_t spitch,
                                                      int64_t sstride, PlaneRef dst, uint8_t white,
                                                      uint32_t* bits, int64_t bstride, int32_t nwr,
-                                                     float rnwr, uint32_t* bbits) {
+                                                     float rnwr, uint32_t* bbits, uint32_t* rm,
+                                                     int64_t rm_stride, uint32_t rm_max) {
   const int s = blockIdx.y;
   const Planes& P = dst.P;
   const int32_t t = blockIdx.x * 256 + threadIdx.x;
@@ -1324,6 +1325,8 @@ __global__ void __launch_bounds__(256) k_decode_gray(const uint8_t* src, int64_t
   uint32_t m = dark_bits32({a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}, white);
   // the blurfilter's bits: pixel <= white (byte < white + 1)
   uint32_t mb = bbits ? dark_bits32({a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}, (uint32_t)white + 1u) : 0u;
+  // the blackfilter's match plane: pixel <= mask_max
+  uint32_t mr = rm ? dark_bits32({a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}, rm_max + 1u) : 0u;
   if (x0 + 32 <= P.W) {
     *reinterpret_cast<uint4*>(d) = a;
     *reinterpret_cast<uint4*>(d + 16) = b;
@@ -1333,6 +1336,7 @@ __global__ void __launch_bounds__(256) k_decode_gray(const uint8_t* src, int64_t
     const int32_t n = P.W - x0;
     m &= (1u << n) - 1u;
     mb &= (1u << n) - 1u;
+    mr &= (1u << n) - 1u;
     uint4 q = a;
     int32_t j = 0;
     if (n >= 16) {
@@ -1349,6 +1353,12 @@ __global__ void __launch_bounds__(256) k_decode_gray(const uint8_t* src, int64_t
   }
   if (bits) bits[s * bstride + t] = m;
   if (bbits) bbits[s * bstride + t] = mb;
+  if (rm) {  // rows of (nwr + 1) & ~1 words: an odd row's pad word is 0
+    const int32_t rw = (nwr + 1) & ~1;
+    uint32_t* r = rm + s * rm_stride + (int64_t)y * rw + wi;
+    if (wi + 1 == nwr && (nwr & 1)) *reinterpret_cast<uint2*>(r) = make_uint2(mr, 0u);
+    else *r = mr;
+  }
 }
 
 // The blackfilter's v-stripe row sums (darkness_rect's sums over the stripe's
@@ -1404,12 +1414,12 @@ __global__ void __launch_bounds__(256) k_stripe_sums(const uint8_t* src, int64_t
 void launch_decode_gray(const uint8_t* src, int64_t spitch, int64_t sstride, const PlaneRef& dst,
                         uint8_t white, uint32_t* bits, int64_t bits_stride, uint32_t* vsum,
                         int64_t vsum_stride, int32_t vx0, int32_t vx1, int count, hipStream_t st,
-                        uint32_t* bbits) {
+                        uint32_t* bbits, uint32_t* rm, int64_t rm_stride, uint8_t rm_max) {
   const int32_t nwr = (dst.P.W + 31) >> 5;
   const int64_t words = (int64_t)nwr * dst.P.H;
   UPH_LAUNCH_DIAG(262144, k_decode_gray, dim3((unsigned)((words + 255) / 256), count), dim3(256), 0, st,
                      src, spitch, sstride, dst, white, bits, bits_stride, nwr, 1.0f / (float)nwr,
-                     bbits);
+                     bbits, rm, rm_stride, (uint32_t)rm_max);
   if (vsum && vx0 <= vx1)
     hipLaunchKernelGGL(k_stripe_sums,
                        dim3((unsigned)((dst.P.H + 4 * kStripeRowsPerWave - 1) / (4 * kStripeRowsPerWave)),

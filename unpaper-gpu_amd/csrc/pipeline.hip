@@ -1246,6 +1246,11 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
   // what the fused decode hands on
   const bool black_on = !(dis & UPHIP_NO_BLACKFILTER) && b->bgeo.nbars > 0;
   const bool vsum_ready = fused && black_on && b->bgeo.vregion.x1 >= b->bgeo.vregion.x0;
+#ifndef UPH_NO_DECODE_RM
+  const bool rm_ready = fused && black_on;  // the blackfilter's match plane from the decode
+#else
+  const bool rm_ready = false;
+#endif
   uint32_t* bits_ready = fused && !(dis & UPHIP_NO_NOISEFILTER) ? b->nbits : nullptr;
   // the blurfilter's plane: made by the decode, kept by the black/noise clears
 #ifndef UPH_NO_BLUR_BITS
@@ -1257,7 +1262,8 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
     launch_decode_gray(src, spitch, sstride, cur_ref(S0, b->ctl), o.abs_white_threshold, bits_ready,
                        b->nbits_stride, vsum_ready ? (uint32_t*)b->scr + b->bgeo.W : nullptr,
                        b->scr_stride / 4, b->bgeo.vregion.x0, b->bgeo.vregion.x1, count, b->st,
-                       bb_ready);
+                       bb_ready, rm_ready ? black_rm_plane(b->bgeo, b->scr) : nullptr,
+                       b->scr_stride / 4, b->bgeo.mask_max);
   }
   if (!covered) fill_uniform(b, S0, 0, Rect{0, 0, w - 1, h - 1}, o.sheet_background, count);
   for (int j = 0; j < n && !fused; j++) {
@@ -1340,7 +1346,7 @@ static bool run_batch(UphipBatch* b, int count, const uint8_t* src, int64_t spit
   if (!(dis & UPHIP_NO_BLACKFILTER) && b->bgeo.nbars > 0) {
     launch_blackfilter_impl(cur_ref(P, b->ctl), b->bgeo, b->dbars, b->scr, b->scr_stride, nullptr,
                             b->ctl, count, b->st, b->black_h, b->black_v, vsum_ready, bits_ready,
-                            b->nbits_stride, bb_ready, b->nbits_stride);
+                            b->nbits_stride, bb_ready, b->nbits_stride, rm_ready);
     mark(b, "blackfilter");
   }
   if (!(dis & UPHIP_NO_NOISEFILTER)) {
