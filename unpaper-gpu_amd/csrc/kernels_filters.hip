@@ -349,10 +349,11 @@ __global__ void __launch_bounds__(256) k_gray_wipe(PlaneRef img, GrayGeom g, uin
   const int32_t cx = blockIdx.x * 256 + threadIdx.x, cy = blockIdx.y;
   if (cx >= g.ncx) return;
   GrayPtrs P = gray_ptrs(g, scratch + s * sstride);
-  if (!gray_cell_wiped(g, P.tile, cx, cy)) return;
   // a cell whose lightness sum is all white is white already (Y400A wipes
-  // also set alpha, so its cells are always written)
+  // also set alpha, so its cells are always written): one load decides the
+  // blank paper before the covering tiles' states are read
   if (FMT != F_Y400A && P.light[(size_t)cy * g.ncx + cx] == 255u * cell_pixels(g, cx, cy)) return;
+  if (!gray_cell_wiped(g, P.tile, cx, cy)) return;
   uint8_t* base = plane_ptr(img, s);
   const int32_t x0 = cx * g.cw, x1 = imin(x0 + g.cw, g.W);
   const int32_t y0 = cy * g.ch, y1 = imin(y0 + g.ch, g.H);
