@@ -129,6 +129,9 @@ __global__ void __launch_bounds__(256) k_gray_cells(PlaneRef img, GrayGeom g, ui
 // the image the grayfilter leaves; k_gray_wipe adds what its wipes change), so
 // that scan needs no pass of its own.  kGrayStrips strips per block keep the
 // atomics at W per kGrayStrips * ch rows.
+#ifndef UPH_GRAY_ROWS
+#define UPH_GRAY_ROWS 1  // k_gray_tiles_rows (0: a thread per tile reading its cells)
+#endif
 constexpr int kGrayStripMaxW = 16384;
 constexpr int kGrayStrips = 8;
 constexpr int kGrayMaxCh = 255;
@@ -222,6 +225,28 @@ __device__ __forceinline__ uint32_t cell_pixels(const GrayGeom& g, int32_t cx, i
   return (w > 0 && h > 0) ? (uint32_t)(w * h) : 0u;
 }
 
+// inverse_lightness_rect of tile (tx,ty) on the original image, the cells'
+// lightness sums from light(cx, cy)
+template <class Light>
+__device__ __forceinline__ uint8_t gray_tile_inv0(const GrayGeom& g, int32_t tx, int32_t ty,
+                                                  Light light) {
+  const Rect r = clip(rect_from_size(tx * g.step_x, ty * g.step_y, g.scan_w, g.scan_h), g.W, g.H);
+  const uint64_t count = count_pixels(r);
+  uint64_t sum = 0;
+  const int32_t cx0 = tx * g.tsx, cy0 = ty * g.tsy;
+  for (int32_t j = 0; j < g.th; j++) {
+    const int32_t cy = cy0 + j;
+    if (cy >= g.ncy) break;
+    for (int32_t i = 0; i < g.tw; i++) {
+      const int32_t cx = cx0 + i;
+      if (cx >= g.ncx) break;
+      sum += light(cx, cy);
+    }
+  }
+  if (r.x1 < r.x0 || r.y1 < r.y0) sum = 0;  // loop body never runs
+  return (uint8_t)(0xFFull - sum / count);
+}
+
 // inverse_lightness_rect of tile (tx,ty) with wiped cells reading 255.
 // mode 0: original image; mode 1: cells covered by an EARLIER wiped tile are white.
 __device__ uint8_t gray_tile_inv(const GrayGeom& g, const GrayPtrs& P, int32_t tx, int32_t ty,
@@ -309,6 +334,52 @@ __global__ void __launch_bounds__(256) k_gray_tiles(GrayGeom g, uint8_t* scratch
   if (M && (threadIdx.x & 63) == __ffsll((long long)M) - 1) atomicAdd(P.nund, (uint32_t)__popcll(M));
 }
 
+// k_gray_tiles with a workgroup per tile row: the th cell rows it covers
+// (dark counts and lightness sums) staged in LDS once instead of every tile
+// reading its tw x th cells from the scratch (the host takes it when those
+// rows fit kGrayRowLds).
+constexpr int kGrayRowLds = 32 * 1024;
+__global__ void __launch_bounds__(256) k_gray_tiles_rows(GrayGeom g, uint8_t* scratch, int64_t sstride,
+                                                         const int32_t* active) {
+  const int s = blockIdx.y;
+  if (active && !active[s]) return;
+  GrayPtrs P = gray_ptrs(g, scratch + s * sstride);
+  const int32_t ty = blockIdx.x, cy0 = ty * g.tsy;
+  const int32_t nr = imax(0, imin(g.th, g.ncy - cy0));  // cell rows inside the image
+  extern __shared__ uint32_t gcl[];
+  uint32_t* sd = gcl;                 // [nr][ncx] dark
+  uint32_t* sl = gcl + nr * g.ncx;    // [nr][ncx] light
+  for (int32_t i = threadIdx.x; i < nr * g.ncx; i += 256) {
+    const size_t c = (size_t)cy0 * g.ncx + i;  // rows cy0.. are consecutive
+    sd[i] = P.dark[c];
+    sl[i] = P.light[c];
+  }
+  __syncthreads();
+  bool und_any = false;
+  for (int32_t tx = threadIdx.x; tx - (int32_t)threadIdx.x < g.ntx; tx += 256) {
+    bool und = false;
+    if (tx < g.ntx) {
+      const int32_t cx0 = tx * g.tsx;
+      uint32_t dark = 0;
+      for (int32_t j = 0; j < nr; j++)
+        for (int32_t i = 0; i < g.tw && cx0 + i < g.ncx; i++) dark += sd[j * g.ncx + cx0 + i];
+      uint8_t st = 0;
+      if (dark == 0) {
+        const uint8_t inv = gray_tile_inv0(g, tx, ty, [&](int32_t cx, int32_t cy) {
+          return sl[(cy - cy0) * g.ncx + cx];
+        });
+        st = inv < g.abs_thr ? 2 : 1;
+        und = st == 1;
+      }
+      P.tile[(size_t)ty * g.ntx + tx] = st;
+    }
+    const unsigned long long M = __ballot(und);
+    if (M && (threadIdx.x & 63) == __ffsll((long long)M) - 1) atomicAdd(P.nund, (uint32_t)__popcll(M));
+    und_any |= und;
+  }
+  (void)und_any;
+}
+
 // The wipe feedback: Jacobi sweeps over the undecided tiles until nothing
 // changes (one block per sheet; returns at once when none is undecided).
 __global__ void __launch_bounds__(1024) k_gray_decide(GrayGeom g, uint8_t* scratch, int64_t sstride,
@@ -391,8 +462,12 @@ static bool launch_gray_t(const PlaneRef& img, const GrayGeom& g, uint8_t* scr, 
     hipLaunchKernelGGL(k_gray_cells<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active);
   }
   const int32_t ntiles = g.ntx * g.nty;
-  hipLaunchKernelGGL(k_gray_tiles, dim3((ntiles + 255) / 256, count), dim3(256), 0, st, g, scr, ss,
-                     active);
+  const size_t rows_lds = 2 * sizeof(uint32_t) * (size_t)g.th * g.ncx;
+  if (UPH_GRAY_ROWS && rows_lds <= (size_t)kGrayRowLds)
+    hipLaunchKernelGGL(k_gray_tiles_rows, dim3(g.nty, count), dim3(256), rows_lds, st, g, scr, ss, active);
+  else
+    hipLaunchKernelGGL(k_gray_tiles, dim3((ntiles + 255) / 256, count), dim3(256), 0, st, g, scr, ss,
+                       active);
   if (!(diag_skip() & 4)) hipLaunchKernelGGL(k_gray_decide, dim3(count), dim3(1024), 0, st, g, scr, ss, active);
   hipLaunchKernelGGL(k_gray_wipe<FMT>, grid, dim3(256), 0, st, img, g, scr, ss, active, colsum, cs);
   return colsum != nullptr;
