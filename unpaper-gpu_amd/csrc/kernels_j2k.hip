@@ -327,11 +327,34 @@ __device__ __attribute__((noinline)) int32_t t1_encode_ring(T1EncLane<64>& L, bo
   return active ? L.flush() : 0;
 }
 
+// Register budgets (waves a SIMD; 0: the compiler's choice, 98-105 VGPRs =
+// 4 waves): several code-block launches share the SIMDs, and each lane's
+// flag and context traffic is latency, so more resident waves pay even with
+// a few spilled registers (JP2 runner A/B: 4 -> 6 waves 847 -> 965-975
+// pages/s; 5 and 7 waves 927, 8 waves spill 124 bytes a lane: 772).  The
+// encoder at 6 waves measured no different (jp2_write 133 vs 134 pages/s).
+#ifndef UPH_T1_WAVES
+#define UPH_T1_WAVES 6
+#endif
+#ifndef UPH_T1ENC_WAVES
+#define UPH_T1ENC_WAVES 0
+#endif
+#if UPH_T1_WAVES > 0
+#define UPH_T1_ATTR __attribute__((amdgpu_waves_per_eu(UPH_T1_WAVES)))
+#else
+#define UPH_T1_ATTR
+#endif
+#if UPH_T1ENC_WAVES > 0
+#define UPH_T1ENC_ATTR __attribute__((amdgpu_waves_per_eu(UPH_T1ENC_WAVES)))
+#else
+#define UPH_T1ENC_ATTR
+#endif
+
 // EBCOT code-block encode, a lane per block: the block's magnitudes and
 // preset signs into the slot (lane-minor), its plane count, then every pass
 // (flags through the LDS ring when the group is at most 64 wide); the
 // codeword into the job's output region.
-__global__ void __launch_bounds__(64) k_j2k_t1enc(const T1EncJob* jobs, int njobs,
+__global__ void __launch_bounds__(64) UPH_T1ENC_ATTR k_j2k_t1enc(const T1EncJob* jobs, int njobs,
                                                   const uint32_t* coef, uint8_t* dout,
                                                   uint32_t* dlen, uint8_t* dnb, uint8_t* scr,
                                                   int64_t slot_bytes, int64_t mg_off) {
@@ -464,7 +487,7 @@ __global__ void __launch_bounds__(256) k_j2k_gather(const T1EncJob* jobs, int nj
 // and the context bytes in LDS, flags in the block's scratch slot laid out
 // lane-minor (coalesced; through the LDS ring for groups up to 64 wide),
 // magnitude bits there too, the decoded block into the coefficients.
-__global__ void __launch_bounds__(64) k_j2k_t1(const T1Job* jobs, int njobs, const uint8_t* data,
+__global__ void __launch_bounds__(64) UPH_T1_ATTR k_j2k_t1(const T1Job* jobs, int njobs, const uint8_t* data,
                                                uint32_t* coef, uint8_t* scr, int64_t slot_bytes,
                                                int64_t val_off) {
   __shared__ MqState qe[47];

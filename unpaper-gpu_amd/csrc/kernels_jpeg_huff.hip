@@ -96,7 +96,17 @@ __global__ void k_jdec_init(const JdecJob* jobs) {
 }
 
 // Sync pass `pass` (0: from the macro starts).  Grid: (macros / 256, images).
-__global__ void __launch_bounds__(256) k_jdec_sync(const JdecJob* jobs, int pass) {
+#ifndef UPH_JDEC_WAVES
+// > 0: k_jdec_sync's register budget in waves a SIMD (JPEG runner A/B: 6
+// waves 3,404 vs 3,399 pages/s, 8 waves 3,326: kept at the compiler's 5)
+#define UPH_JDEC_WAVES 0
+#endif
+#if UPH_JDEC_WAVES > 0
+#define UPH_JDEC_ATTR __attribute__((amdgpu_waves_per_eu(UPH_JDEC_WAVES)))
+#else
+#define UPH_JDEC_ATTR
+#endif
+__global__ void __launch_bounds__(256) UPH_JDEC_ATTR k_jdec_sync(const JdecJob* jobs, int pass) {
   const JdecJob J = jobs[blockIdx.y];
   const JdecHeader& H = *(const JdecHeader*)J.stream;
   if ((int64_t)blockIdx.x * blockDim.x >= H.nmac) return;
