@@ -2672,8 +2672,16 @@ __global__ void __launch_bounds__(T) k_noise_group(PlaneRef img, NoiseGeom g, ui
     noise_group_sheet<FMT, T, false>(g, NP, gk, glds, base, pitch, flag, n, bb);
 }
 
+#ifndef UPH_REPLAY_WAVES
+#define UPH_REPLAY_WAVES 0  // > 0: k_noise_replay's register budget in waves a SIMD
+#endif
+#if UPH_REPLAY_WAVES > 0
+#define UPH_REPLAY_ATTR __attribute__((amdgpu_waves_per_eu(UPH_REPLAY_WAVES)))
+#else
+#define UPH_REPLAY_ATTR
+#endif
 template <int FMT>
-__global__ void __launch_bounds__(256) k_noise_replay(PlaneRef img, NoiseGeom g, uint8_t* scratch,
+__global__ void __launch_bounds__(256) UPH_REPLAY_ATTR k_noise_replay(PlaneRef img, NoiseGeom g, uint8_t* scratch,
                                                       int64_t sstride, const int32_t* active,
                                                       const uint32_t* sortbuf, int64_t sort_stride,
                                                       int kCompCap) {
