@@ -2673,7 +2673,9 @@ __global__ void __launch_bounds__(T) k_noise_group(PlaneRef img, NoiseGeom g, ui
 }
 
 #ifndef UPH_REPLAY_WAVES
-#define UPH_REPLAY_WAVES 0  // > 0: k_noise_replay's register budget in waves a SIMD
+// > 0: k_noise_replay's register budget in waves a SIMD (A/B: 6 waves 131 ->
+// 144 us a C3 launch, C4 noisefilter 0.82 -> 0.88 ms; 8 waves worse: off)
+#define UPH_REPLAY_WAVES 0
 #endif
 #if UPH_REPLAY_WAVES > 0
 #define UPH_REPLAY_ATTR __attribute__((amdgpu_waves_per_eu(UPH_REPLAY_WAVES)))
